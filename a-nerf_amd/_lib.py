@@ -1,0 +1,118 @@
+"""ctypes binding of libanerf_hip.so (the C ABI declared in include/anerf.h).
+
+The library is built in-tree (see build.py).  Importing torch first makes the library's
+libamdhip64.so.7 dependency resolve to the HIP runtime torch already loaded, so device
+pointers and streams are shared with PyTorch.  There is no fallback: if the library is
+missing this module raises.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must be loaded before the HIP library, see module docstring)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libanerf_hip.so")
+
+MAXL = 16
+c_f = ctypes.POINTER(ctypes.c_float)
+c_i32p = ctypes.POINTER(ctypes.c_int32)
+c_i64p = ctypes.POINTER(ctypes.c_int64)
+
+ANERF_PREC_FP32 = 0
+
+
+class ModelDesc(ctypes.Structure):
+    _fields_ = [("n_joints", ctypes.c_int32), ("net_depth", ctypes.c_int32), ("net_width", ctypes.c_int32),
+                ("skip", ctypes.c_int32), ("multires", ctypes.c_int32), ("multires_views", ctypes.c_int32),
+                ("use_cutoff", ctypes.c_int32), ("cutoff_inputs", ctypes.c_int32),
+                ("cutoff_viewdir", ctypes.c_int32), ("framecode_ch", ctypes.c_int32),
+                ("n_framecodes", ctypes.c_int32), ("density_softplus", ctypes.c_int32),
+                ("softplus_shift", ctypes.c_float), ("density_scale", ctypes.c_float),
+                ("has_fine", ctypes.c_int32)]
+
+
+class NetWeights(ctypes.Structure):
+    _fields_ = [("pts_w", c_f * MAXL), ("pts_b", c_f * MAXL), ("alpha_w", c_f), ("alpha_b", c_f),
+                ("feature_w", c_f), ("feature_b", c_f), ("views_w", c_f), ("views_b", c_f),
+                ("rgb_w", c_f), ("rgb_b", c_f), ("codes", c_f)]
+
+
+class EmbedParams(ctypes.Structure):
+    _fields_ = [("cutoff_dist", c_f), ("tau", ctypes.c_float), ("cutoff_dist_v", c_f), ("tau_v", ctypes.c_float)]
+
+
+class Debug(ctypes.Structure):
+    _fields_ = [("near", c_f), ("far", c_f), ("z_coarse", c_f), ("raw_coarse", c_f), ("weights0", c_f),
+                ("z_fine", c_f), ("raw_fine", c_f)]
+
+
+# name -> (restype, argtypes); must cover every entry point of include/anerf.h
+SIGNATURES = {
+    "anerf_abi_version": (ctypes.c_int, []),
+    "anerf_last_error": (ctypes.c_char_p, []),
+    "anerf_model_create": (ctypes.c_int, [ctypes.POINTER(ModelDesc), ctypes.POINTER(NetWeights),
+                                          ctypes.POINTER(NetWeights), ctypes.POINTER(EmbedParams), ctypes.c_int,
+                                          ctypes.POINTER(ctypes.c_void_p)]),
+    "anerf_model_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "anerf_model_bytes": (ctypes.c_size_t, [ctypes.c_void_p]),
+    "anerf_workspace_size": (ctypes.c_size_t, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]),
+    "anerf_render_rays": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64,
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                         ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.POINTER(Debug), ctypes.c_void_p, ctypes.c_size_t,
+                                         ctypes.c_void_p]),
+    "anerf_gen_rays": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_float,
+                                      ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_int32,
+                                      ctypes.c_void_p, ctypes.c_int64, ctypes.c_float, ctypes.c_float,
+                                      ctypes.c_void_p, ctypes.c_void_p]),
+    "anerf_near_far": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "anerf_encode_points": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
+    "anerf_compose": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64,
+                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+}
+
+_lib = None
+
+
+class AnerfError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libanerf_hip.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise AnerfError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                         "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = load().anerf_last_error().decode(errors="replace")
+        raise AnerfError(f"{what} failed ({rc}): {msg}")
+
+
+def ptr(t):
+    """Device (or host) pointer of a tensor / None."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream_handle(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)

@@ -1,0 +1,124 @@
+"""Render-path configuration: the subset of run_nerf.py's flags that shape the kernel.
+
+Mirrors the arguments `create_raycaster` reads (`core/raycasters.py:17-184`) and the
+flags listed in SURVEY.md §8b.  Flags whose code paths are not implemented raise
+`NotImplementedError` up front (the reference raises `NotImplementedError` for unknown
+encoder types too, `core/raycasters.py:238,247,267,283,302`) — never a silent fallback.
+"""
+from dataclasses import dataclass, field
+
+
+@dataclass
+class RenderConfig:
+    n_joints: int = 24
+    netdepth: int = 8
+    netwidth: int = 256
+    skips: tuple = (4,)
+    multires: int = 7
+    multires_views: int = 4
+    multires_bones: int = 0
+    use_cutoff: bool = True
+    cutoff_inputs: bool = True
+    cutoff_viewdir: bool = True
+    use_viewdirs: bool = True
+    opt_framecode: bool = False
+    framecode_size: int = 16
+    n_framecodes: int = 0
+    density_type: str = "relu"
+    softplus_shift: float = 1.0
+    density_scale: float = 1.0
+    N_samples: int = 64
+    N_importance: int = 0
+    single_net: bool = False
+    chunk: int = 4096
+    ext_scale: float = 0.001
+    extra: dict = field(default_factory=dict)
+
+    def validate(self):
+        if not self.use_viewdirs:
+            raise NotImplementedError("use_viewdirs=False (output_linear head) is not implemented")
+        if self.multires_bones != 0:
+            raise NotImplementedError("multires_bones > 0 is not implemented (configs use 0)")
+        if self.single_net:
+            raise NotImplementedError("single_net is not implemented yet")
+        if len(self.skips) != 1 or self.skips[0] < 0:
+            # a skip index >= netdepth-1 is never reached (D=4 configs): no skip layer
+            raise NotImplementedError(f"skips={self.skips}: exactly one skip index is supported")
+        if self.netwidth % 64 != 0 or self.netwidth > 256:
+            raise NotImplementedError(f"netwidth={self.netwidth}: multiples of 64 up to 256 are supported")
+        if self.netdepth < 2 or self.netdepth > 16:
+            raise NotImplementedError(f"netdepth={self.netdepth} outside [2, 16]")
+        if self.multires < 1 or self.multires > 10 or self.multires_views < 1 or self.multires_views > 10:
+            raise NotImplementedError("multires / multires_views must be in [1, 10]")
+        if self.density_type not in ("relu", "softplus"):
+            raise NotImplementedError(f"density activation {self.density_type} is undefined")
+        if self.opt_framecode and self.n_framecodes <= 0:
+            raise ValueError("opt_framecode needs n_framecodes > 0")
+        if self.n_joints < 1 or self.n_joints > 128:
+            raise NotImplementedError(f"n_joints={self.n_joints} outside [1, 128]")
+        for k in ("normalize_cutoff", "cut_to_dist", "cutoff_shift", "freq_schedule", "cutoff_bones"):
+            if self.extra.get(k):
+                raise NotImplementedError(f"--{k} is not implemented")
+        for k, allowed in (("kp_dist_type", "reldist"), ("bone_type", "reldir"), ("view_type", "relray"),
+                           ("pts_tr_type", "local")):
+            v = self.extra.get(k, allowed)
+            if v != allowed:
+                raise NotImplementedError(f"--{k}={v}: only {allowed} is implemented")
+        return self
+
+    @property
+    def framecode_ch(self):
+        return self.framecode_size if self.opt_framecode else 0
+
+    @property
+    def input_ch(self):
+        return self.n_joints * (1 + 2 * self.multires)
+
+    @property
+    def input_ch_bones(self):
+        return 3 * self.n_joints
+
+    @property
+    def input_ch_views(self):
+        return 3 * self.n_joints * (1 + 2 * self.multires_views)
+
+    @property
+    def feature_dim(self):
+        return self.input_ch + self.input_ch_bones + self.input_ch_views
+
+    @classmethod
+    def from_args(cls, args, n_joints):
+        """Build from a run_nerf.config_parser() namespace (or anything with those attributes)."""
+        g = lambda k, d=None: getattr(args, k, d)  # noqa: E731
+        extra = {k: g(k) for k in ("normalize_cutoff", "cut_to_dist", "cutoff_shift", "freq_schedule",
+                                   "cutoff_bones", "kp_dist_type", "bone_type", "view_type", "pts_tr_type")
+                 if g(k) is not None}
+        cfg = cls(n_joints=n_joints, netdepth=g("netdepth", 8), netwidth=g("netwidth", 256),
+                  multires=g("multires", 7), multires_views=g("multires_views", 4),
+                  multires_bones=g("multires_bones", 0), use_cutoff=bool(g("use_cutoff", True)),
+                  cutoff_inputs=bool(g("cutoff_inputs", True)), cutoff_viewdir=bool(g("cutoff_viewdir", True)),
+                  use_viewdirs=bool(g("use_viewdirs", True)), opt_framecode=bool(g("opt_framecode", False)),
+                  framecode_size=g("framecode_size", 16), n_framecodes=g("n_framecodes", 0) or 0,
+                  density_type=g("density_type", "relu"), softplus_shift=g("softplus_shift", 1.0),
+                  density_scale=g("density_scale", 1.0), N_samples=g("N_samples", 64),
+                  N_importance=g("N_importance", 0), single_net=bool(g("single_net", False)),
+                  chunk=g("chunk", 4096), ext_scale=g("ext_scale", 0.001), extra=extra)
+        return cfg.validate()
+
+
+def flops_per_sample(cfg):
+    """Reference MLP FLOPs per sample point (2 x MACs of core/networks/nerf.py:133-148)."""
+    W, D = cfg.netwidth, cfg.netdepth
+    dnet = cfg.input_ch + cfg.input_ch_bones
+    macs = dnet * W
+    for i in range(D - 1):
+        macs += (W + dnet if i in cfg.skips else W) * W
+    macs += W * 1 + W * W + (W + cfg.input_ch_views + cfg.framecode_ch) * (W // 2) + (W // 2) * 3
+    return 2 * macs
+
+
+def samples_per_ray(cfg):
+    """MLP evaluations per ray: coarse S plus, with importance sampling, all S+I merged samples
+    through the fine net (core/raycasters.py:456-461)."""
+    S, I = cfg.N_samples, cfg.N_importance
+    return S + (S + I if I > 0 else 0)

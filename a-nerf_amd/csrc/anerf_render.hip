@@ -1,0 +1,1264 @@
+// anerf_render.hip — MI355X (gfx950) render path of A-NeRF behind the C ABI in include/anerf.h.
+//
+// One fused kernel renders a group of R rays per 256-thread workgroup (4 waves, one per SIMD):
+//   coarse z (linspace) -> per-sample skeleton-relative encoding generated IN REGISTERS as the
+//   MFMA B operand -> 8x256 MLP on v_mfma_f32_32x32x2_f32 with activations resident in the
+//   accumulator/VGPR file across layers (the transposed product out^T = W^T in^T keeps each
+//   layer's accumulator layout directly usable as the next layer's B operand; weights are
+//   packed on the host in that permuted k order) -> alpha / rgb heads on the VALU ->
+//   compositing + sample_pdf + merge-sort per ray in LDS -> fine pass over all S+I samples.
+// The view layer is factorised: its per-sample direction input dv = T_k(e_jc) * w'_j is
+// split into a per-ray matrix G[j][n] (computed once per ray in LDS) and the per-sample cutoff
+// weights w'_j, so the per-sample K of the view layer is W + NJ + 1 instead of W + 27 NJ.
+//
+// Reference behaviour restated (paths relative to danielajisafe/A-NeRF):
+//   core/raycasters.py:361-474 render_rays, 476-555 encode_inputs, 557-577 run_network
+//   core/encoders.py:8-37, 101-122, 172-193; core/cutoff_embedder.py:111-174
+//   core/networks/nerf.py:90-205; core/utils/ray_utils.py:6-28, 157-251, 255-344
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/anerf.h"
+#include "anerf_device.hpp"
+
+using namespace anerf;
+
+#define MAXL 16
+
+// ======================================================================= device model
+struct NetDev {
+    const float* wl[MAXL];   // packed layer weights; [0] feature schedule, [i>0] activation (regs) part
+    const float* bl[MAXL];   // packed biases [RB][2][16]
+    const float* wskipx;     // skip layer, x part (feature schedule) or null
+    const float* walpha;     // [2][RB][16]
+    const float* wfeat;      // packed regs W->W
+    const float* bfeat;      // packed bias
+    const float* wview;      // packed regs W->W/2 (feature part of views_linears.0)
+    const float* wvdir;      // [NJ][NK][3][W/2] direction part, transposed
+    const float* wvcode;     // [cfc][W/2] code part, transposed
+    const float* bview;      // [W/2]
+    const float* wrgb;       // [3][2][RBV][16]
+    const float* brgb;       // [3]
+    const float* codes;      // [n_codes + 1][cfc]: last row = eval-mode mean code
+    float balpha;
+};
+
+struct ModelDev {
+    int nj, njh, ngh, D, skip, mr, mrv, use_cutoff, cutoff_inputs, cutoff_viewdir, cfc, n_codes, softplus;
+    float shift, B, tau, tau_v;
+    const float* cutoff;
+    const float* cutoff_v;
+    NetDev net[2];
+};
+
+struct RenderArgs {
+    const float* rb;
+    int64_t n;
+    int stride, S, I, R;
+    const float* skts;
+    const int32_t* ray_pose;
+    const float* cams;
+    const float* near;
+    const float* far;
+    float *rgb, *disp, *acc, *rgb0, *disp0, *acc0, *alpha, *alpha0;
+    float *dbg_z0, *dbg_raw0, *dbg_w0, *dbg_z1, *dbg_raw1;
+};
+
+// ======================================================================= LDS plan
+struct LdsPlan {
+    int ray, sk, zc, zf, raw, g, scr;  // float offsets
+    int total;                          // floats
+    int sk_stride, z_stride, raw_stride, g_stride, scr_stride;
+};
+
+__host__ __device__ inline int pad32(int x) { return (x + 31) & ~31; }
+
+__host__ __device__ inline LdsPlan make_plan(int R, int nj, int W, int S, int T, int mrv, int ngh) {
+    LdsPlan p;
+    const int wh = W / 2;
+    const int nk = 1 + 2 * mrv;
+    p.sk_stride = nj * 12;
+    p.z_stride = pad32(T > S ? T : S);
+    p.raw_stride = p.z_stride * 4;
+    p.g_stride = 2 * ngh * wh;
+    int scr_a = 8 * p.z_stride;          // composite / importance scratch
+    int scr_b = nk * 3 * nj;             // trig table for G
+    p.scr_stride = (scr_a > scr_b ? scr_a : scr_b);
+    int o = 0;
+    p.ray = o; o += 16 * R;
+    p.sk = o; o += p.sk_stride * R;
+    p.zc = o; o += p.z_stride * R;
+    p.zf = o; o += p.z_stride * R;
+    p.raw = o; o += p.raw_stride * R;
+    p.g = o; o += p.g_stride * R;
+    p.scr = o; o += p.scr_stride * R;
+    p.total = (o + 3) & ~3;
+    return p;
+}
+
+// ======================================================================= MLP building blocks
+// Weight streams are read with buffer loads: one SGPR descriptor per array plus a single 32-bit
+// lane offset, so the unrolled K loops carry no per-load 64-bit address registers.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* p) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ f32x2 bload2(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+    return __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0));
+}
+__device__ __forceinline__ f32x4 bload4(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
+}
+
+template <int RB>
+__device__ __forceinline__ void load_bias(f32x16 (&acc)[RB], const float* __restrict__ bp, int hh) {
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(bp);
+    const int voff = hh * 64;
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+        f32x4 v0 = bload4(rs, voff, rb * 128 + 0), v1 = bload4(rs, voff, rb * 128 + 16);
+        f32x4 v2 = bload4(rs, voff, rb * 128 + 32), v3 = bload4(rs, voff, rb * 128 + 48);
+        acc[rb] = f32x16{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3],
+                         v2[0], v2[1], v2[2], v2[3], v3[0], v3[1], v3[2], v3[3]};
+    }
+}
+
+// acc[RBO] += W^T * h  over the RBI*32 activations held in h (k-steps in accumulator order).
+// Weights packed [group = q/2][RBO][64 lanes][2]; 3-slot register ring, prefetch distance 2.
+template <int RBO, int RBI>
+__device__ __forceinline__ void regs_layer(f32x16 (&acc)[RBO], const f32x16 (&h)[RBI], const float* __restrict__ wp,
+                                           int lane) {
+    constexpr int NG = 8 * RBI;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(wp);
+    const int voff = lane * 8;
+    f32x2 ring[3][RBO];
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+        for (int rb = 0; rb < RBO; ++rb) ring[g][rb] = bload2(rs, voff, (g * RBO + rb) * 512);
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+        // keep the ring three groups deep: no load crosses a group boundary
+        __builtin_amdgcn_sched_barrier(0);
+        if (g + 2 < NG) {
+#pragma unroll
+            for (int rb = 0; rb < RBO; ++rb) ring[(g + 2) % 3][rb] = bload2(rs, voff, ((g + 2) * RBO + rb) * 512);
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int q = 2 * g + t;
+            const float b = h[q >> 4][q & 15];
+#pragma unroll
+            for (int rb = 0; rb < RBO; ++rb) acc[rb] = mfma_f32_32x32x2(ring[g % 3][rb][t], b, acc[rb]);
+        }
+    }
+}
+
+// Features of one (sample, joint): [dist*w, sin(2^f dist)*w, cos(2^f dist)*w (f < MR), u0, u1, u2]
+template <int MR>
+__device__ __forceinline__ void joint_features(const ModelDev& M, const float* __restrict__ S, int j, bool valid,
+                                               float px, float py, float pz, float (&f)[2 * MR + 4]) {
+    float qx = 0.f, qy = 0.f, qz = 0.f;
+    if (valid) joint_local(S, px, py, pz, qx, qy, qz);
+    const float dist = norm3(qx, qy, qz);
+    const float dn = fmaxf(dist, 1e-12f);
+    float w = 1.0f;
+    if (M.use_cutoff) w = valid ? cutoff_w(M.tau, dist, M.cutoff[j]) : 0.0f;
+    f[0] = (M.use_cutoff && M.cutoff_inputs) ? dist * w : dist;
+#pragma unroll
+    for (int fi = 0; fi < MR; ++fi) {
+        float s, c;
+        sincosf(dist * (float)(1 << fi), &s, &c);
+        f[1 + 2 * fi] = s * w;
+        f[2 + 2 * fi] = c * w;
+    }
+    f[2 * MR + 1] = qx / dn;
+    f[2 * MR + 2] = qy / dn;
+    f[2 * MR + 3] = qz / dn;
+}
+
+// acc[RB] += W_x^T * x where x (the 15NJ + 3NJ input features) is generated on the fly:
+// lane half hh encodes joint p + hh*NJh for joint pair p; k-step = p*FPJ + feature index.
+template <int RB, int MR>
+__device__ __forceinline__ void feature_layer(f32x16 (&acc)[RB], const ModelDev& M, const float* __restrict__ wp,
+                                              const float* __restrict__ sk, float px, float py, float pz, int lane) {
+    constexpr int FPJ = 2 * MR + 4;
+    constexpr int NG = FPJ / 2;
+    static_assert(NG % 3 == 0, "feature groups per joint must be a multiple of the ring depth");
+    const int hh = lane >> 5;
+    const int total_groups = M.njh * NG;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(wp);
+    const int voff = lane * 8;
+    f32x2 ring[3][RB];
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) ring[g][rb] = bload2(rs, voff, (g * RB + rb) * 512);
+    for (int p = 0; p < M.njh; ++p) {
+        const int j = p + hh * M.njh;
+        const bool valid = j < M.nj;
+        float f[FPJ];
+        joint_features<MR>(M, sk + 12 * (valid ? j : 0), j, valid, px, py, pz, f);
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            __builtin_amdgcn_sched_barrier(0);
+            const int gn = p * NG + g + 2;
+            if (gn < total_groups) {
+#pragma unroll
+                for (int rb = 0; rb < RB; ++rb) ring[(g + 2) % 3][rb] = bload2(rs, voff, (gn * RB + rb) * 512);
+            }
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const float b = f[2 * g + t];
+#pragma unroll
+                for (int rb = 0; rb < RB; ++rb) acc[rb] = mfma_f32_32x32x2(ring[g % 3][rb][t], b, acc[rb]);
+            }
+        }
+    }
+}
+
+// View layer, per-ray direction part: acc[RBV] += G^T * [w'_0 .. w'_{NJ-1}, 1]  (G in LDS)
+template <int RBV>
+__device__ __forceinline__ void view_dir_part(f32x16 (&acc)[RBV], const ModelDev& M, const float* __restrict__ G,
+                                              const float* __restrict__ sk, float px, float py, float pz, int lane) {
+    constexpr int WH = RBV * 32;
+    const int hh = lane >> 5, sl = lane & 31;
+    for (int q = 0; q < M.ngh; ++q) {
+        const int c = q + hh * M.ngh;
+        float b = 0.0f;
+        if (c < M.nj) {
+            if (M.cutoff_viewdir) {
+                float qx, qy, qz;
+                joint_local(sk + 12 * c, px, py, pz, qx, qy, qz);
+                b = cutoff_w(M.tau_v, norm3(qx, qy, qz), M.cutoff_v[c]);
+            }
+        } else if (c == M.nj) {
+            b = 1.0f;
+        }
+        const float* gc = G + c * WH + sl;
+#pragma unroll
+        for (int rb = 0; rb < RBV; ++rb) acc[rb] = mfma_f32_32x32x2(gc[32 * rb], b, acc[rb]);
+    }
+}
+
+// One 32-sample block of one ray through a whole NeRF: raw (rgb, sigma) into LDS.
+template <int W, int MR>
+__device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __restrict__ ray,
+                          const float* __restrict__ sk, const float* __restrict__ z, int n, int s0,
+                          const float* __restrict__ G, float* __restrict__ raw_out, int lane) {
+    constexpr int RB = W / 32;
+    constexpr int RBV = (W / 2) / 32;
+    const int sl = lane & 31, hh = lane >> 5;
+    int s = s0 + sl;
+    if (s >= n) s = n - 1;
+    const float zs = z[s];
+    // pts = rays_o + rays_d * z (raycasters.py:658), separately rounded
+    const float px = ray[0] + ray[3] * zs;
+    const float py = ray[1] + ray[4] * zs;
+    const float pz = ray[2] + ray[5] * zs;
+
+    f32x16 acc[RB], h[RB];
+    load_bias<RB>(acc, net.bl[0], hh);
+    feature_layer<RB, MR>(acc, M, net.wl[0], sk, px, py, pz, lane);
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) h[rb][i] = relu(acc[rb][i]);
+    for (int L = 1; L < M.D; ++L) {
+        load_bias<RB>(acc, net.bl[L], hh);
+        if (L == M.skip + 1) feature_layer<RB, MR>(acc, M, net.wskipx, sk, px, py, pz, lane);
+        regs_layer<RB, RB>(acc, h, net.wl[L], lane);
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) h[rb][i] = relu(acc[rb][i]);
+    }
+    // alpha head (VALU): this lane holds half of the W activations of sample sl
+    float sig = 0.0f;
+    {
+        const float* wa = net.walpha + hh * RB * 16;
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) sig += wa[rb * 16 + i] * h[rb][i];
+        sig += __shfl_xor(sig, 32);
+        sig += net.balpha;
+    }
+    // feature_linear (no activation)
+    load_bias<RB>(acc, net.bfeat, hh);
+    regs_layer<RB, RB>(acc, h, net.wfeat, lane);
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) h[rb] = acc[rb];
+    // views_linears.0: feature part + factorised direction/code/bias part, then relu
+    f32x16 av[RBV];
+#pragma unroll
+    for (int rb = 0; rb < RBV; ++rb) av[rb] = f32x16{0};
+    regs_layer<RBV, RB>(av, h, net.wview, lane);
+    view_dir_part<RBV>(av, M, G, sk, px, py, pz, lane);
+    float rgb[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const float* wr = net.wrgb + (c * 2 + hh) * RBV * 16;
+        float a = 0.0f;
+#pragma unroll
+        for (int rb = 0; rb < RBV; ++rb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) a += wr[rb * 16 + i] * relu(av[rb][i]);
+        a += __shfl_xor(a, 32);
+        rgb[c] = a + net.brgb[c];
+    }
+    if (hh == 0 && s0 + sl < n) {
+        float* o = raw_out + 4 * (s0 + sl);
+        o[0] = rgb[0];
+        o[1] = rgb[1];
+        o[2] = rgb[2];
+        o[3] = sig;
+    }
+}
+
+// ======================================================================= per-ray stages
+// Per-ray view factor G[c][n] for every ray of the group (all threads). Needs Tt scratch.
+__device__ void compute_view_factor(const ModelDev& M, const NetDev& net, float* lds, const LdsPlan& P, int nr,
+                                    int WH, int tid) {
+    const int nj = M.nj, nk = 1 + 2 * M.mrv;
+    // trig table Tt[k][3j+c] of the normalised joint-frame ray directions
+    for (int idx = tid; idx < nr * nj; idx += blockDim.x) {
+        const int r = idx / nj, j = idx % nj;
+        const float* ray = lds + P.ray + 16 * r;
+        const float* S = lds + P.sk + P.sk_stride * r + 12 * j;
+        float ex, ey, ez;
+        joint_rot(S, ray[3], ray[4], ray[5], ex, ey, ez);
+        const float en = fmaxf(norm3(ex, ey, ez), 1e-12f);
+        const float e[3] = {ex / en, ey / en, ez / en};
+        float* Tt = lds + P.scr + P.scr_stride * r;
+        for (int c = 0; c < 3; ++c) {
+            Tt[3 * j + c] = e[c];
+            for (int f = 0; f < M.mrv; ++f) {
+                float s, co;
+                sincosf(e[c] * (float)(1 << f), &s, &co);
+                Tt[(1 + 2 * f) * 3 * nj + 3 * j + c] = s;
+                Tt[(2 + 2 * f) * 3 * nj + 3 * j + c] = co;
+            }
+        }
+    }
+    __syncthreads();
+    const int ncol = 2 * M.ngh;
+    const int k_first_w = M.cutoff_inputs ? 0 : 1;  // k terms multiplied by w'
+    for (int idx = tid; idx < nr * ncol * WH; idx += blockDim.x) {
+        const int r = idx / (ncol * WH);
+        const int c = (idx / WH) % ncol;
+        const int nn = idx % WH;
+        const float* Tt = lds + P.scr + P.scr_stride * r;
+        const float* ray = lds + P.ray + 16 * r;
+        float v = 0.0f;
+        if (c < nj) {
+            if (M.cutoff_viewdir) {
+                for (int k = k_first_w; k < nk; ++k)
+                    for (int cc = 0; cc < 3; ++cc)
+                        v += net.wvdir[((c * nk + k) * 3 + cc) * WH + nn] * Tt[k * 3 * nj + 3 * c + cc];
+            }
+        } else if (c == nj) {
+            v = net.bview[nn];
+            if (M.cfc) {
+                const float cam = ray[6];
+                const int64_t row = cam < 0.0f ? (int64_t)M.n_codes : (int64_t)cam;
+                for (int m = 0; m < M.cfc; ++m) v += net.wvcode[m * WH + nn] * net.codes[row * M.cfc + m];
+            }
+            // terms that the cutoff does not weight
+            const int kend = M.cutoff_viewdir ? k_first_w : nk;
+            for (int j = 0; j < nj; ++j)
+                for (int k = 0; k < kend; ++k)
+                    for (int cc = 0; cc < 3; ++cc)
+                        v += net.wvdir[((j * nk + k) * 3 + cc) * WH + nn] * Tt[k * 3 * nj + 3 * j + cc];
+        }
+        lds[P.g + P.g_stride * r + c * WH + nn] = v;
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ float density_act(const ModelDev& M, float x) {
+    if (!M.softplus) return relu(x);
+    const float y = x - M.shift;  // F.softplus(beta=1, threshold=20)
+    return y > 20.0f ? y : log1pf(expf(y));
+}
+
+// raw2outputs (nerf.py:150-205) of ray slot r over n samples; wave-cooperative, all waves call it.
+// scr layout: w[zs], wz[zs], wc[3 zs], fac[zs], al[zs]
+// Results (rgb[3], disp, acc) are left in res[0..4] (LDS) for the caller to store.
+__device__ void composite(const ModelDev& M, const float* ray, const float* z, const float* raw, int n, float* scr,
+                          int zs, bool active, int lane, float* o_alpha, float* res) {
+    float* w = scr;
+    float* wz = scr + zs;
+    float* wc = scr + 2 * zs;
+    float* fac = scr + 5 * zs;
+    float* al = scr + 6 * zs;
+    if (active) {
+        const float dn = ray[9];  // |d| cached in slot 9
+        for (int i = lane; i < n; i += 64) {
+            float dist = (i + 1 < n) ? (z[i + 1] - z[i]) : 1e10f;
+            dist = dist * dn;
+            const float a = 1.0f - expf(-density_act(M, raw[4 * i + 3] / M.B) * dist);
+            al[i] = a;
+            fac[i] = (1.0f - a) + 1e-10f;
+            if (o_alpha) o_alpha[i] = a;
+        }
+    }
+    __syncthreads();
+    if (active && lane == 0) {
+        double T = 1.0;  // torch CPU cumprod accumulates in double
+        for (int i = 0; i < n; ++i) {
+            w[i] = (float)T;
+            T *= (double)fac[i];
+        }
+    }
+    __syncthreads();
+    if (active) {
+        for (int i = lane; i < n; i += 64) {
+            const float wi = al[i] * w[i];
+            w[i] = wi;
+            wz[i] = wi * z[i];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) wc[3 * i + c] = wi * (sigmoid(raw[4 * i + c]) * 1.002f - 0.001f);
+        }
+    }
+    __syncthreads();
+    if (active && lane < 5) {
+        float v;
+        if (lane < 2) v = torch_sum(lane == 0 ? w : wz, n);
+        else v = torch_sum_strided(wc + (lane - 2), 3, n);
+        fac[lane] = v;  // fac[] no longer needed
+    }
+    __syncthreads();
+    if (active && lane == 0) {
+        const float accf = fac[0], depth = fac[1];
+        const float ratio = depth / (accf + 1e-10f);
+        float dsp = 1.0f / fmaxf(ratio, 1e-10f);
+        if (ratio != ratio) dsp = ratio;  // torch.max propagates NaN
+        if (fabsf(accf) <= 1e-8f) dsp = 0.0f;
+        res[0] = fac[2];
+        res[1] = fac[3];
+        res[2] = fac[4];
+        res[3] = dsp;
+        res[4] = accf < 1.0f ? accf : 1.0f;
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ bool z_less(float a, float b) { return a < b || (b != b && a == a); }
+__device__ __forceinline__ bool z_eq(float a, float b) { return a == b || (a != a && b != b); }
+
+// isample_from_lineseg + sample_pdf(det) + sort (ray_utils.py:157-201, 255-289) for ray slot r.
+// weights w (S) in scr; writes sorted z_all (S+I) to zf.
+__device__ void importance(const float* zc, const float* w, int S, int I, float* zf, float* scr2, bool active,
+                           int lane) {
+    const int nb = S - 1;  // bins = mids
+    float* mids = scr2;
+    float* wp = scr2 + nb;
+    float* cdf = scr2 + 2 * nb;
+    float* zall = scr2 + 3 * nb + 1;  // S + I unsorted
+    if (active) {
+        for (int i = lane; i < nb; i += 64) mids[i] = 0.5f * (zc[i + 1] + zc[i]);
+        for (int i = lane; i < nb - 1; i += 64) wp[i] = w[i + 1] + 1e-5f;
+    }
+    __syncthreads();
+    if (active && lane == 0) {
+        const float sum = torch_sum(wp, nb - 1);
+        double c = 0.0;  // torch CPU cumsum accumulates in double
+        cdf[0] = 0.0f;
+        for (int i = 0; i < nb - 1; ++i) {
+            c += (double)(wp[i] / sum);
+            cdf[i + 1] = (float)c;
+        }
+    }
+    __syncthreads();
+    if (active) {
+        for (int k = lane; k < I; k += 64) {
+            const float u = torch_linspace01(k, I);
+            int lo = 0, hi = nb;  // searchsorted(right=True) over nb cdf entries
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (cdf[mid] <= u) lo = mid + 1; else hi = mid;
+            }
+            const int below = max(lo - 1, 0), above = min(lo, nb - 1);
+            const float cb = cdf[below], ca = cdf[above];
+            const float bb = mids[below], ba = mids[above];
+            float denom = ca - cb;
+            if (denom < 1e-5f) denom = 1.0f;
+            const float t = (u - cb) / denom;
+            zall[S + k] = bb + t * (ba - bb);
+        }
+        for (int i = lane; i < S; i += 64) zall[i] = zc[i];
+    }
+    __syncthreads();
+    const int T = S + I;
+    if (active) {
+        for (int e = lane; e < T; e += 64) {  // stable rank sort (values identical to torch.sort)
+            const float v = zall[e];
+            int rank = 0;
+            for (int f = 0; f < T; ++f) {
+                const float x = zall[f];
+                rank += z_less(x, v) || (z_eq(x, v) && f < e);
+            }
+            zf[rank] = v;
+        }
+    }
+    __syncthreads();
+}
+
+// ======================================================================= fused render kernel
+template <int W, int MR>
+__global__ __launch_bounds__(256, 1) void render_kernel(ModelDev M, RenderArgs A, LdsPlan P) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    constexpr int WH = W / 2;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int R = A.R, S = A.S, I = A.I, T = S + I;
+    const int64_t ray0 = (int64_t)blockIdx.x * R;
+    const int nr = (int)min((int64_t)R, A.n - ray0);
+
+    // ---- rays, poses, skeleton transforms into LDS
+    for (int r = tid; r < nr; r += blockDim.x) {
+        const int64_t i = ray0 + r;
+        const float* src = A.rb + i * A.stride;
+        float* d = lds + P.ray + 16 * r;
+        for (int c = 0; c < 6; ++c) d[c] = src[c];
+        d[6] = A.cams ? A.cams[i] : -1.0f;
+        d[7] = A.near[i];
+        d[8] = A.far[i];
+        d[9] = norm3(src[3], src[4], src[5]);
+        d[10] = __int_as_float(A.ray_pose ? A.ray_pose[i] : 0);
+    }
+    __syncthreads();
+    for (int idx = tid; idx < nr * M.nj * 12; idx += blockDim.x) {
+        const int r = idx / (M.nj * 12), e = idx % (M.nj * 12);
+        const int j = e / 12, c = e % 12;
+        const int pose = __float_as_int(lds[P.ray + 16 * r + 10]);
+        lds[P.sk + P.sk_stride * r + e] = A.skts[((int64_t)pose * M.nj + j) * 16 + c];
+    }
+    // coarse samples (sample_from_lineseg, ray_utils.py:218-224)
+    for (int idx = tid; idx < nr * S; idx += blockDim.x) {
+        const int r = idx / S, s = idx % S;
+        const float t = torch_linspace01(s, S);
+        const float nearv = lds[P.ray + 16 * r + 7], farv = lds[P.ray + 16 * r + 8];
+        lds[P.zc + P.z_stride * r + s] = nearv * (1.0f - t) + farv * t;
+    }
+    __syncthreads();
+
+    const int n_pass = I > 0 ? 2 : 1;
+    for (int pass = 0; pass < n_pass; ++pass) {
+        const NetDev& net = M.net[pass];
+        const int n = pass == 0 ? S : T;
+        const int zoff = pass == 0 ? P.zc : P.zf;
+        compute_view_factor(M, net, lds, P, nr, WH, tid);
+        // ---- MLP over 32-sample blocks, round-robin over the 4 waves
+        const int nb = (n + 31) / 32;
+        for (int b = wave; b < nr * nb; b += 4) {
+            const int r = b / nb, s0 = (b % nb) * 32;
+            mlp_block<W, MR>(M, net, lds + P.ray + 16 * r, lds + P.sk + P.sk_stride * r,
+                             lds + zoff + P.z_stride * r, n, s0, lds + P.g + P.g_stride * r,
+                             lds + P.raw + P.raw_stride * r, lane);
+        }
+        __syncthreads();
+        // ---- composite (+ importance sampling after the coarse pass); one wave per ray
+        for (int r0 = 0; r0 < R; r0 += 4) {
+            const int r = r0 + wave;
+            const bool active = r < nr;
+            const int64_t i = ray0 + r;
+            const float* ray = lds + P.ray + 16 * min(r, R - 1);
+            const float* z = lds + zoff + P.z_stride * min(r, R - 1);
+            const float* raw = lds + P.raw + P.raw_stride * min(r, R - 1);
+            float* scr = lds + P.scr + P.scr_stride * min(r, R - 1);
+            const bool final_pass = pass == n_pass - 1;
+            float* o_rgb = final_pass ? A.rgb : A.rgb0;
+            float* o_disp = final_pass ? A.disp : A.disp0;
+            float* o_acc = final_pass ? A.acc : A.acc0;
+            float* o_alpha = final_pass ? A.alpha : A.alpha0;
+            float* pal = (active && o_alpha) ? o_alpha + i * n : nullptr;
+            if (active) {
+                float* dz = pass == 0 ? A.dbg_z0 : A.dbg_z1;
+                float* draw = pass == 0 ? A.dbg_raw0 : A.dbg_raw1;
+                for (int s = lane; s < n; s += 64) {
+                    if (dz) dz[i * n + s] = z[s];
+                    if (draw)
+                        for (int c = 0; c < 4; ++c) draw[(i * n + s) * 4 + c] = raw[4 * s + c];
+                }
+            }
+            float* res = scr + 7 * P.z_stride;
+            composite(M, ray, z, raw, n, scr, P.z_stride, active, lane, pal, res);
+            if (active && lane < 5) {
+                const float v = res[lane];
+                if (lane < 3) {
+                    if (o_rgb) o_rgb[3 * i + lane] = v;
+                } else if (lane == 3) {
+                    if (o_disp) o_disp[i] = v;
+                } else if (o_acc) {
+                    o_acc[i] = v;
+                }
+            }
+            if (pass == 0 && I > 0) {
+                if (active && A.dbg_w0)
+                    for (int s = lane; s < S; s += 64) A.dbg_w0[i * S + s] = scr[s];
+                importance(z, scr, S, I, lds + P.zf + P.z_stride * min(r, R - 1), scr + P.z_stride, active, lane);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ======================================================================= small kernels
+__global__ void near_far_kernel(const float* __restrict__ rb, int stride, int64_t n, const float* __restrict__ cyls,
+                                const int32_t* __restrict__ ray_pose, float* __restrict__ near_out,
+                                float* __restrict__ far_out, uint8_t* __restrict__ qnan) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float* r = rb + i * stride;
+    const float* cy = cyls + 5 * (ray_pose ? ray_pose[i] : 0);
+    const float nearv = r[6], farv = r[7];
+    // g_axes = [0, -1]: the x-z ground plane (ray_utils.py:292-327)
+    const float rn0 = r[0] + r[3] * nearv, rn1 = r[2] + r[5] * nearv;
+    const float rf0 = r[0] + r[3] * farv, rf1 = r[2] + r[5] * farv;
+    const float nc0 = cy[0] - rn0, nc1 = cy[1] - rn1;
+    const float nf0 = rf0 - rn0, nf1 = rf1 - rn1;
+    const float nfn = norm2(nf0, nf1);
+    const float scale = norm2(r[3], r[5]);
+    const float cross = nc0 * nf1 - nc1 * nf0;
+    const float dist = fabsf(cross) / nfn;
+    const float rad = cy[2];
+    const float Q = sqrtf(rad * rad - dist * dist);
+    const float K = (nc0 * nf0 + nc1 * nf1) / nfn;
+    const float mask = (Q < K) ? 1.0f : 0.0f;
+    near_out[i] = nearv + (mask * (K - Q)) / scale;
+    far_out[i] = nearv + (K + Q) / scale;
+    qnan[i] = (Q != Q) ? 1 : 0;
+}
+
+// one workgroup per chunk: NaN rows <- np.nanmean of the chunk (ray_utils.py:328-342)
+__global__ void nan_fill_kernel(const float* __restrict__ rb, int stride, int64_t n, int chunk,
+                                float* __restrict__ near_io, float* __restrict__ far_io,
+                                const uint8_t* __restrict__ qnan, float* __restrict__ scratch) {
+    const int64_t c0 = (int64_t)blockIdx.x * chunk;
+    const int64_t c1 = min(c0 + chunk, n);
+    __shared__ int any;
+    __shared__ float means[2];
+    if (threadIdx.x == 0) any = 0;
+    __syncthreads();
+    for (int64_t i = c0 + threadIdx.x; i < c1; i += blockDim.x)
+        if (near_io[i] != near_io[i]) any = 1;
+    __syncthreads();
+    if (!any) return;
+    float* buf = scratch + c0;  // NaN -> 0 copies, one vector at a time
+    for (int v = 0; v < 2; ++v) {
+        const float* src = v == 0 ? near_io : far_io;
+        for (int64_t i = c0 + threadIdx.x; i < c1; i += blockDim.x) buf[i - c0] = (src[i] != src[i]) ? 0.0f : src[i];
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int64_t cnt = 0;
+            for (int64_t i = c0; i < c1; ++i) cnt += (src[i] == src[i]);
+            means[v] = cnt ? (float)((double)np_pairwise_sum(buf, c1 - c0) / (double)cnt) : __int_as_float(0x7fc00000);
+        }
+        __syncthreads();
+    }
+    for (int64_t i = c0 + threadIdx.x; i < c1; i += blockDim.x) {
+        if (qnan[i]) {
+            const float* r = rb + i * stride;
+            near_io[i] = (means[0] != means[0]) ? r[6] : means[0];
+            far_io[i] = (means[1] != means[1]) ? r[7] : means[1];
+        }
+    }
+}
+
+__global__ void gen_rays_kernel(const float* __restrict__ c2w, int H, int W, float fx, float fy, float cx, float cy,
+                                const int64_t* __restrict__ idx, int64_t n, float nearv, float farv,
+                                float* __restrict__ out) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const int64_t p = idx[t];
+    const float x = (float)(p % W), y = (float)(p / W);
+    // dirs = ((i - cx)/fx, -(j - cy)/fy, -1); rays_d = sum(dirs * c2w[:3,:3], -1) (ray_utils.py:22-25)
+    const float d0 = (x - cx) / fx;
+    const float d1 = -(y - cy) / fy;
+    const float d2 = -1.0f;
+    float* o = out + t * 11;
+    float dd[3];
+    for (int r = 0; r < 3; ++r) {
+        dd[r] = (d0 * c2w[4 * r + 0] + d1 * c2w[4 * r + 1]) + d2 * c2w[4 * r + 2];
+        o[r] = c2w[4 * r + 3];
+        o[3 + r] = dd[r];
+    }
+    o[6] = nearv;
+    o[7] = farv;
+    const float nn = norm3(dd[0], dd[1], dd[2]);  // viewdirs = d / |d| (core/trainer.py:123)
+    o[8] = dd[0] / nn;
+    o[9] = dd[1] / nn;
+    o[10] = dd[2] / nn;
+}
+
+__global__ void compose_fill_kernel(const float* __restrict__ bg, int white, int64_t hw, float* __restrict__ out_rgb,
+                                    float* __restrict__ out_disp, float* __restrict__ out_acc) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= hw) return;
+    for (int c = 0; c < 3; ++c) out_rgb[3 * p + c] = bg ? bg[3 * p + c] : (white ? 1.0f : 0.0f);
+    out_disp[p] = 0.0f;
+    if (out_acc) out_acc[p] = 0.0f;
+}
+
+__global__ void compose_scatter_kernel(const float* __restrict__ rgb, const float* __restrict__ disp,
+                                       const float* __restrict__ acc, const int64_t* __restrict__ idx, int64_t n,
+                                       float* __restrict__ out_rgb, float* __restrict__ out_disp,
+                                       float* __restrict__ out_acc) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t p = idx[i];
+    const float a = acc[i];
+    for (int c = 0; c < 3; ++c) out_rgb[3 * p + c] = rgb[3 * i + c] + (1.0f - a) * out_rgb[3 * p + c];
+    const float d = disp[i];
+    out_disp[p] = (d != d) ? 0.0f : d;  // disps[isnan] = 0 (run_nerf.py:140-141)
+    if (out_acc) out_acc[p] = a;
+}
+
+// full torch-order feature vectors (encode_inputs + embedders), one thread per point
+__global__ void encode_points_kernel(ModelDev M, const float* __restrict__ skts, const float* __restrict__ pts,
+                                     const float* __restrict__ dirs, int64_t n, float* __restrict__ feat) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int nj = M.nj, nv = 1 + 2 * M.mr, nk = 1 + 2 * M.mrv;
+    const int cx = nj * nv + 3 * nj;
+    const int F = cx + 3 * nj * nk;
+    float* f = feat + i * F;
+    const float px = pts[3 * i], py = pts[3 * i + 1], pz = pts[3 * i + 2];
+    const float dx = dirs[3 * i], dy = dirs[3 * i + 1], dz = dirs[3 * i + 2];
+    for (int j = 0; j < nj; ++j) {
+        float S[12];
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 4; ++c) S[4 * r + c] = skts[j * 16 + 4 * r + c];
+        float qx, qy, qz;
+        joint_local(S, px, py, pz, qx, qy, qz);
+        const float dist = norm3(qx, qy, qz);
+        const float dn = fmaxf(dist, 1e-12f);
+        const float w = M.use_cutoff ? cutoff_w(M.tau, dist, M.cutoff[j]) : 1.0f;
+        f[j] = (M.use_cutoff && M.cutoff_inputs) ? dist * w : dist;
+        for (int fi = 0; fi < M.mr; ++fi) {
+            float s, c;
+            sincosf(dist * (float)(1 << fi), &s, &c);
+            f[(1 + 2 * fi) * nj + j] = s * w;
+            f[(2 + 2 * fi) * nj + j] = c * w;
+        }
+        f[nj * nv + 3 * j + 0] = qx / dn;
+        f[nj * nv + 3 * j + 1] = qy / dn;
+        f[nj * nv + 3 * j + 2] = qz / dn;
+        float ex, ey, ez;
+        joint_rot(S, dx, dy, dz, ex, ey, ez);
+        const float en = fmaxf(norm3(ex, ey, ez), 1e-12f);
+        const float e[3] = {ex / en, ey / en, ez / en};
+        const float wv = M.cutoff_viewdir ? cutoff_w(M.tau_v, dist, M.cutoff_v[j]) : 1.0f;
+        for (int c = 0; c < 3; ++c) {
+            f[cx + 3 * j + c] = (M.cutoff_viewdir && M.cutoff_inputs) ? e[c] * wv : e[c];
+            for (int fi = 0; fi < M.mrv; ++fi) {
+                float s, co;
+                sincosf(e[c] * (float)(1 << fi), &s, &co);
+                f[cx + (1 + 2 * fi) * 3 * nj + 3 * j + c] = s * wv;
+                f[cx + (2 + 2 * fi) * 3 * nj + 3 * j + c] = co * wv;
+            }
+        }
+    }
+}
+
+// ======================================================================= host side
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(x)                                                                              \
+    do {                                                                                        \
+        hipError_t e_ = (x);                                                                    \
+        if (e_ != hipSuccess) return fail(ANERF_EHIP, std::string(#x ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+// ---- packing (host): k-source maps into the MFMA operand order
+struct Packer {
+    std::vector<float> buf;
+    size_t add(const std::vector<float>& v) {
+        size_t off = buf.size();
+        buf.insert(buf.end(), v.begin(), v.end());
+        while (buf.size() % 64) buf.push_back(0.0f);  // 256-byte alignment of every array
+        return off;
+    }
+};
+
+// W torch [n_out][ld]; kmap(q, h) -> input column or -1; nq k-steps (even); out [nq/2][RB][64][2]
+template <class F>
+std::vector<float> pack_kmajor(const float* Wt, int n_out, int ld, int nq, F kmap) {
+    const int RB = n_out / 32;
+    std::vector<float> out((size_t)(nq / 2) * RB * 128, 0.0f);
+    for (int g = 0; g < nq / 2; ++g)
+        for (int rb = 0; rb < RB; ++rb)
+            for (int l = 0; l < 64; ++l)
+                for (int t = 0; t < 2; ++t) {
+                    const int q = 2 * g + t;
+                    const int col = kmap(q, l >> 5);
+                    const int row = 32 * rb + (l & 31);
+                    out[(((size_t)g * RB + rb) * 64 + l) * 2 + t] = col >= 0 ? Wt[(size_t)row * ld + col] : 0.0f;
+                }
+    return out;
+}
+
+std::vector<float> pack_regs(const float* Wt, int n_out, int ld, int col_off, int n_in) {
+    return pack_kmajor(Wt, n_out, ld, n_in / 2, [&](int q, int h) {
+        return col_off + 32 * (q >> 4) + acc_row(q & 15, h);
+    });
+}
+
+std::vector<float> pack_features(const float* Wt, int n_out, int ld, int nj, int njh, int mr) {
+    const int nv = 1 + 2 * mr, fpj = nv + 3;
+    return pack_kmajor(Wt, n_out, ld, njh * fpj, [&](int q, int h) {
+        const int p = q / fpj, t = q % fpj;
+        const int j = p + h * njh;
+        if (j >= nj) return -1;
+        return t < nv ? t * nj + j : nv * nj + 3 * j + (t - nv);
+    });
+}
+
+// per-lane-half vectors [rb][h][16] of a length-n vector in accumulator row order
+std::vector<float> pack_rowvec(const float* v, int n, bool half_major) {
+    const int RB = n / 32;
+    std::vector<float> out((size_t)RB * 32, 0.0f);
+    for (int rb = 0; rb < RB; ++rb)
+        for (int h = 0; h < 2; ++h)
+            for (int i = 0; i < 16; ++i) {
+                const size_t idx = half_major ? ((size_t)h * RB + rb) * 16 + i : ((size_t)rb * 2 + h) * 16 + i;
+                out[idx] = v[32 * rb + acc_row(i, h)];
+            }
+    return out;
+}
+
+}  // namespace
+
+struct anerf_model {
+    anerf_model_desc desc;
+    int device;
+    int njh, ngh;
+    float* dev_buf;
+    size_t dev_bytes;
+    ModelDev md;
+};
+
+template <int WIDTH>
+static void host_row_sum(const float* x, int64_t xs, int64_t n, float* out) {
+    // host twin of torch_row_sum (used for the eval-mode mean framecode)
+    const int64_t size = n / 4;
+    int lp = 0;
+    while (((int64_t)1 << lp) < size) ++lp;
+    lp /= 4;
+    if (lp < 4) lp = 4;
+    const int64_t step = (int64_t)1 << lp, mask = step - 1;
+    float acc[4][4][WIDTH] = {};
+    int64_t i = 0;
+    while (i + step <= size) {
+        for (int64_t jj = 0; jj < step; ++jj, ++i)
+            for (int k = 0; k < 4; ++k)
+                for (int l = 0; l < WIDTH; ++l) acc[0][k][l] += x[((4 * i + k) * WIDTH + l) * xs];
+        for (int j = 1; j < 4; ++j) {
+            for (int k = 0; k < 4; ++k)
+                for (int l = 0; l < WIDTH; ++l) {
+                    acc[j][k][l] += acc[j - 1][k][l];
+                    acc[j - 1][k][l] = 0.0f;
+                }
+            if ((i & (mask << (j * lp))) != 0) break;
+        }
+    }
+    for (; i < size; ++i)
+        for (int k = 0; k < 4; ++k)
+            for (int l = 0; l < WIDTH; ++l) acc[0][k][l] += x[((4 * i + k) * WIDTH + l) * xs];
+    for (int j = 1; j < 4; ++j)
+        for (int k = 0; k < 4; ++k)
+            for (int l = 0; l < WIDTH; ++l) acc[0][k][l] += acc[j][k][l];
+    for (int64_t e = size * 4; e < n; ++e)
+        for (int l = 0; l < WIDTH; ++l) acc[0][0][l] += x[(e * WIDTH + l) * xs];
+    for (int k = 1; k < 4; ++k)
+        for (int l = 0; l < WIDTH; ++l) acc[0][0][l] += acc[0][k][l];
+    for (int l = 0; l < WIDTH; ++l) out[l] = acc[0][0][l];
+}
+
+static int validate_desc(const anerf_model_desc* d) {
+    if (!d) return fail(ANERF_EINVAL, "desc is NULL");
+    if (d->net_width != 64 && d->net_width != 128 && d->net_width != 256)
+        return fail(ANERF_EINVAL, "net_width must be 64, 128 or 256");
+    if (d->net_depth < 2 || d->net_depth > MAXL) return fail(ANERF_EINVAL, "net_depth outside [2, 16]");
+    if (d->multires != 7 && d->multires != 10) return fail(ANERF_EINVAL, "multires must be 7 or 10");
+    if (d->multires_views < 1 || d->multires_views > 10) return fail(ANERF_EINVAL, "multires_views outside [1, 10]");
+    if (d->n_joints < 1 || d->n_joints > 128) return fail(ANERF_EINVAL, "n_joints outside [1, 128]");
+    if (d->skip < 0) return fail(ANERF_EINVAL, "skip must be >= 0");
+    if (d->framecode_ch < 0 || d->framecode_ch > 64) return fail(ANERF_EINVAL, "framecode_ch outside [0, 64]");
+    if (d->framecode_ch > 0 && d->n_framecodes <= 0) return fail(ANERF_EINVAL, "n_framecodes must be > 0");
+    if (d->density_scale == 0.0f) return fail(ANERF_EINVAL, "density_scale must be non-zero");
+    return ANERF_OK;
+}
+
+static int pack_net(const anerf_model_desc* d, int njh, const anerf_net_weights* w, Packer& pk,
+                    std::vector<size_t>& offs) {
+    const int W = d->net_width, WH = W / 2, nj = d->n_joints, mr = d->multires, mrv = d->multires_views;
+    const int cin = nj * (1 + 2 * mr) + 3 * nj;
+    const int nk = 1 + 2 * mrv;
+    const int cv = 3 * nj * nk, cfc = d->framecode_ch;
+    const int ldv = W + cv + cfc;
+    for (int i = 0; i < d->net_depth; ++i)
+        if (!w->pts_w[i] || !w->pts_b[i]) return fail(ANERF_EINVAL, "missing pts_linears weight");
+    if (!w->alpha_w || !w->alpha_b || !w->feature_w || !w->feature_b || !w->views_w || !w->views_b || !w->rgb_w ||
+        !w->rgb_b)
+        return fail(ANERF_EINVAL, "missing head weight");
+    if (cfc && !w->codes) return fail(ANERF_EINVAL, "framecode weights missing");
+    offs.clear();
+    // [0] layer 0 (features), [1..D-1] activation parts, [D] skip x part, [D+1..2D] biases
+    offs.push_back(pk.add(pack_features(w->pts_w[0], W, cin, nj, njh, mr)));
+    for (int i = 1; i < d->net_depth; ++i) {
+        const bool sk = (i == d->skip + 1);
+        offs.push_back(pk.add(pack_regs(w->pts_w[i], W, sk ? cin + W : W, sk ? cin : 0, W)));
+    }
+    const int skl = d->skip + 1;
+    if (skl < d->net_depth) offs.push_back(pk.add(pack_features(w->pts_w[skl], W, cin + W, nj, njh, mr)));
+    else offs.push_back((size_t)-1);
+    for (int i = 0; i < d->net_depth; ++i) offs.push_back(pk.add(pack_rowvec(w->pts_b[i], W, false)));
+    offs.push_back(pk.add(pack_rowvec(w->alpha_w, W, true)));                         // walpha
+    offs.push_back(pk.add(pack_regs(w->feature_w, W, W, 0, W)));                      // wfeat
+    offs.push_back(pk.add(pack_rowvec(w->feature_b, W, false)));                      // bfeat
+    offs.push_back(pk.add(pack_regs(w->views_w, WH, ldv, 0, W)));                     // wview
+    {
+        std::vector<float> t((size_t)nj * nk * 3 * WH);
+        for (int j = 0; j < nj; ++j)
+            for (int k = 0; k < nk; ++k)
+                for (int c = 0; c < 3; ++c)
+                    for (int n = 0; n < WH; ++n)
+                        t[(((size_t)j * nk + k) * 3 + c) * WH + n] = w->views_w[(size_t)n * ldv + W + k * 3 * nj + 3 * j + c];
+        offs.push_back(pk.add(t));                                                    // wvdir
+    }
+    {
+        std::vector<float> t((size_t)std::max(cfc, 1) * WH, 0.0f);
+        for (int m = 0; m < cfc; ++m)
+            for (int n = 0; n < WH; ++n) t[(size_t)m * WH + n] = w->views_w[(size_t)n * ldv + W + cv + m];
+        offs.push_back(pk.add(t));                                                    // wvcode
+    }
+    offs.push_back(pk.add(std::vector<float>(w->views_b, w->views_b + WH)));          // bview
+    {
+        std::vector<float> t;
+        for (int c = 0; c < 3; ++c) {
+            // [c][h][rb][16]
+            std::vector<float> v = pack_rowvec(w->rgb_w + (size_t)c * WH, WH, true);
+            t.insert(t.end(), v.begin(), v.end());
+        }
+        offs.push_back(pk.add(t));                                                    // wrgb
+    }
+    offs.push_back(pk.add(std::vector<float>(w->rgb_b, w->rgb_b + 3)));               // brgb
+    {
+        std::vector<float> t((size_t)(std::max(d->n_framecodes, 0) + 1) * std::max(cfc, 1), 0.0f);
+        if (cfc) {
+            std::memcpy(t.data(), w->codes, sizeof(float) * (size_t)d->n_framecodes * cfc);
+            for (int m = 0; m < cfc; ++m) {  // codes.weight.mean(0) = torch sum over dim 0 / n
+                float s;
+                host_row_sum<1>(w->codes + m, cfc, d->n_framecodes, &s);
+                t[(size_t)d->n_framecodes * cfc + m] = s / (float)d->n_framecodes;
+            }
+        }
+        offs.push_back(pk.add(t));                                                    // codes
+    }
+    return ANERF_OK;
+}
+
+static void bind_net(const anerf_model_desc* d, const float* base, const std::vector<size_t>& o, float balpha,
+                     NetDev& nd) {
+    std::memset(&nd, 0, sizeof(nd));
+    const int D = d->net_depth;
+    size_t k = 0;
+    nd.wl[0] = base + o[k++];
+    for (int i = 1; i < D; ++i) nd.wl[i] = base + o[k++];
+    nd.wskipx = o[k] == (size_t)-1 ? nullptr : base + o[k];
+    ++k;
+    for (int i = 0; i < D; ++i) nd.bl[i] = base + o[k++];
+    nd.walpha = base + o[k++];
+    nd.wfeat = base + o[k++];
+    nd.bfeat = base + o[k++];
+    nd.wview = base + o[k++];
+    nd.wvdir = base + o[k++];
+    nd.wvcode = base + o[k++];
+    nd.bview = base + o[k++];
+    nd.wrgb = base + o[k++];
+    nd.brgb = base + o[k++];
+    nd.codes = base + o[k++];
+    nd.balpha = balpha;
+}
+
+extern "C" {
+
+int anerf_abi_version(void) { return ANERF_ABI_VERSION; }
+
+const char* anerf_last_error(void) { return g_err.c_str(); }
+
+int anerf_model_create(const anerf_model_desc* desc, const anerf_net_weights* coarse, const anerf_net_weights* fine,
+                       const anerf_embed_params* embed, int device, anerf_model** out) {
+    if (!out) return fail(ANERF_EINVAL, "out is NULL");
+    *out = nullptr;
+    int rc = validate_desc(desc);
+    if (rc) return rc;
+    if (!coarse || !embed) return fail(ANERF_EINVAL, "coarse weights / embed params are NULL");
+    if (desc->has_fine && !fine) return fail(ANERF_EINVAL, "has_fine but fine weights are NULL");
+    if (!embed->cutoff_dist || !embed->cutoff_dist_v) return fail(ANERF_EINVAL, "cutoff_dist is NULL");
+    const int nj = desc->n_joints;
+    const int njh = (nj + 1) / 2;
+    const int ngh = (nj + 2) / 2;  // NJ + 1 columns split over two lane halves
+    Packer pk;
+    std::vector<size_t> oc, of;
+    rc = pack_net(desc, njh, coarse, pk, oc);
+    if (rc) return rc;
+    if (desc->has_fine) {
+        rc = pack_net(desc, njh, fine, pk, of);
+        if (rc) return rc;
+    }
+    const size_t off_cut = pk.add(std::vector<float>(embed->cutoff_dist, embed->cutoff_dist + nj));
+    const size_t off_cutv = pk.add(std::vector<float>(embed->cutoff_dist_v, embed->cutoff_dist_v + nj));
+
+    int prev = 0;
+    HIP_TRY(hipGetDevice(&prev));
+    HIP_TRY(hipSetDevice(device));
+    float* dbuf = nullptr;
+    const size_t bytes = pk.buf.size() * sizeof(float);
+    hipError_t e = hipMalloc(&dbuf, bytes);
+    if (e == hipSuccess) e = hipMemcpy(dbuf, pk.buf.data(), bytes, hipMemcpyHostToDevice);
+    hipSetDevice(prev);
+    if (e != hipSuccess) {
+        if (dbuf) hipFree(dbuf);
+        return fail(ANERF_EHIP, std::string("weight upload: ") + hipGetErrorString(e));
+    }
+    anerf_model* m = new anerf_model();
+    m->desc = *desc;
+    m->device = device;
+    m->njh = njh;
+    m->ngh = ngh;
+    m->dev_buf = dbuf;
+    m->dev_bytes = bytes;
+    ModelDev& md = m->md;
+    std::memset(&md, 0, sizeof(md));
+    md.nj = nj;
+    md.njh = njh;
+    md.ngh = ngh;
+    md.D = desc->net_depth;
+    md.skip = desc->skip;
+    md.mr = desc->multires;
+    md.mrv = desc->multires_views;
+    md.use_cutoff = desc->use_cutoff;
+    md.cutoff_inputs = desc->cutoff_inputs;
+    md.cutoff_viewdir = desc->cutoff_viewdir;
+    md.cfc = desc->framecode_ch;
+    md.n_codes = desc->n_framecodes;
+    md.softplus = desc->density_softplus;
+    md.shift = desc->softplus_shift;
+    md.B = desc->density_scale;
+    md.tau = embed->tau;
+    md.tau_v = embed->tau_v;
+    md.cutoff = dbuf + off_cut;
+    md.cutoff_v = dbuf + off_cutv;
+    bind_net(desc, dbuf, oc, coarse->alpha_b[0], md.net[0]);
+    if (desc->has_fine) bind_net(desc, dbuf, of, fine->alpha_b[0], md.net[1]);
+    else md.net[1] = md.net[0];
+    *out = m;
+    return ANERF_OK;
+}
+
+int anerf_model_destroy(anerf_model* m) {
+    if (!m) return ANERF_OK;
+    if (m->dev_buf) hipFree(m->dev_buf);
+    delete m;
+    return ANERF_OK;
+}
+
+size_t anerf_model_bytes(const anerf_model* m) { return m ? m->dev_bytes : 0; }
+
+static size_t ws_near_far_bytes(int64_t n) {
+    // near, far, fill scratch (floats) + qnan flags, each 256-byte aligned
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    return 3 * al(sizeof(float) * (size_t)n) + al((size_t)n);
+}
+
+size_t anerf_workspace_size(const anerf_model* m, int64_t n_rays, int32_t n_samples, int32_t n_importance) {
+    (void)m; (void)n_samples; (void)n_importance;
+    return ws_near_far_bytes(n_rays > 0 ? n_rays : 1);
+}
+
+static int launch_near_far(const float* rb, int stride, int64_t n, const float* cyls, const int32_t* ray_pose,
+                           int chunk, char* ws, float** near_o, float** far_o, hipStream_t st) {
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    float* nearp = reinterpret_cast<float*>(ws);
+    float* farp = reinterpret_cast<float*>(ws + al(sizeof(float) * n));
+    float* scratch = reinterpret_cast<float*>(ws + 2 * al(sizeof(float) * n));
+    uint8_t* qnan = reinterpret_cast<uint8_t*>(ws + 3 * al(sizeof(float) * n));
+    const int bs = 256;
+    hipLaunchKernelGGL(near_far_kernel, dim3((unsigned)((n + bs - 1) / bs)), dim3(bs), 0, st, rb, stride, n, cyls,
+                       ray_pose, nearp, farp, qnan);
+    const int64_t nchunks = (n + chunk - 1) / chunk;
+    hipLaunchKernelGGL(nan_fill_kernel, dim3((unsigned)nchunks), dim3(256), 0, st, rb, stride, n, chunk, nearp, farp,
+                       qnan, scratch);
+    HIP_TRY(hipGetLastError());
+    *near_o = nearp;
+    *far_o = farp;
+    return ANERF_OK;
+}
+
+int anerf_near_far(const float* ray_batch, int32_t ray_stride, int64_t n_rays, const float* cyls,
+                   const int32_t* ray_pose, int32_t chunk, float* near_out, float* far_out, void* workspace,
+                   size_t workspace_bytes, void* stream) {
+    if (n_rays <= 0) return ANERF_OK;
+    if (!ray_batch || !cyls || !near_out || !far_out || ray_stride < 8 || chunk <= 0)
+        return fail(ANERF_EINVAL, "anerf_near_far: bad arguments");
+    if (!workspace || workspace_bytes < ws_near_far_bytes(n_rays)) return fail(ANERF_EWORKSPACE, "workspace too small");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    float *np_, *fp_;
+    int rc = launch_near_far(ray_batch, ray_stride, n_rays, cyls, ray_pose, chunk, (char*)workspace, &np_, &fp_, st);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(near_out, np_, sizeof(float) * n_rays, hipMemcpyDeviceToDevice, st));
+    HIP_TRY(hipMemcpyAsync(far_out, fp_, sizeof(float) * n_rays, hipMemcpyDeviceToDevice, st));
+    return ANERF_OK;
+}
+
+int anerf_render_rays(const anerf_model* m, const float* ray_batch, int32_t ray_stride, int64_t n_rays,
+                      const float* skts, const float* cyls, int32_t n_poses, const int32_t* ray_pose,
+                      const float* cams, int32_t n_samples, int32_t n_importance, int32_t chunk, int32_t precision,
+                      float* rgb, float* disp, float* acc, float* rgb0, float* disp0, float* acc0, float* alpha,
+                      float* alpha0, const anerf_debug* debug, void* workspace, size_t workspace_bytes,
+                      void* stream) {
+    if (!m) return fail(ANERF_EINVAL, "model is NULL");
+    if (n_rays < 0) return fail(ANERF_EINVAL, "n_rays < 0");
+    if (n_rays == 0) return ANERF_OK;
+    if (precision != ANERF_PREC_FP32) return fail(ANERF_EINVAL, "unsupported precision");
+    if (!ray_batch || ray_stride < 8 || !skts || !cyls || n_poses < 1 || !rgb || !disp || !acc)
+        return fail(ANERF_EINVAL, "anerf_render_rays: bad arguments");
+    if (n_samples < 2 || n_samples > 1024 || n_importance < 0 || n_importance > 2048)
+        return fail(ANERF_EINVAL, "n_samples must be in [2, 1024], n_importance in [0, 2048]");
+    if (n_importance > 0 && !m->desc.has_fine) return fail(ANERF_EINVAL, "n_importance > 0 needs a fine network");
+    if (n_importance > 0 && n_samples < 3) return fail(ANERF_EINVAL, "importance sampling needs n_samples >= 3");
+    if (m->desc.framecode_ch > 0 && !cams) return fail(ANERF_EINVAL, "model uses framecodes: cams required");
+    if (chunk <= 0) return fail(ANERF_EINVAL, "chunk must be > 0");
+    if (!workspace || workspace_bytes < anerf_workspace_size(m, n_rays, n_samples, n_importance))
+        return fail(ANERF_EWORKSPACE, "workspace too small");
+    int dev = -1;
+    HIP_TRY(hipGetDevice(&dev));
+    if (dev != m->device) return fail(ANERF_EINVAL, "current device differs from the model's device");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+
+    float *nearp, *farp;
+    int rc = launch_near_far(ray_batch, ray_stride, n_rays, cyls, ray_pose, chunk, (char*)workspace, &nearp, &farp, st);
+    if (rc) return rc;
+    if (debug && debug->near) HIP_TRY(hipMemcpyAsync(debug->near, nearp, 4 * n_rays, hipMemcpyDeviceToDevice, st));
+    if (debug && debug->far) HIP_TRY(hipMemcpyAsync(debug->far, farp, 4 * n_rays, hipMemcpyDeviceToDevice, st));
+
+    const int S = n_samples, I = n_importance, T = S + I;
+    const int nbc = (S + 31) / 32;
+    int R = 4;
+    for (int g = 4; g > 1; g /= 2)
+        if (nbc % g == 0) { R = 4 / g; break; }
+    if (nbc % 4 == 0) R = 1;
+    const int W = m->desc.net_width;
+    LdsPlan P = make_plan(R, m->desc.n_joints, W, S, T, m->desc.multires_views, m->ngh);
+    while (R > 1 && P.total * 4 > 160 * 1024) {
+        R /= 2;
+        P = make_plan(R, m->desc.n_joints, W, S, T, m->desc.multires_views, m->ngh);
+    }
+    if (P.total * 4 > 160 * 1024) return fail(ANERF_EINVAL, "configuration exceeds the 160 KiB LDS budget");
+
+    RenderArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.rb = ray_batch;
+    a.n = n_rays;
+    a.stride = ray_stride;
+    a.S = S;
+    a.I = I;
+    a.R = R;
+    a.skts = skts;
+    a.ray_pose = ray_pose;
+    a.cams = cams;
+    a.near = nearp;
+    a.far = farp;
+    a.rgb = rgb;
+    a.disp = disp;
+    a.acc = acc;
+    a.rgb0 = rgb0;
+    a.disp0 = disp0;
+    a.acc0 = acc0;
+    a.alpha = alpha;
+    a.alpha0 = alpha0;
+    if (debug) {
+        a.dbg_z0 = debug->z_coarse;
+        a.dbg_raw0 = debug->raw_coarse;
+        a.dbg_w0 = debug->weights0;
+        a.dbg_z1 = debug->z_fine;
+        a.dbg_raw1 = debug->raw_fine;
+    }
+    const unsigned grid = (unsigned)((n_rays + R - 1) / R);
+    const size_t lds_bytes = (size_t)P.total * 4;
+    const int mr = m->desc.multires;
+#define ANERF_LAUNCH(WW, MM)                                                                         \
+    do {                                                                                            \
+        auto kfn = render_kernel<WW, MM>;                                                           \
+        HIP_TRY(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,  \
+                                    (int)lds_bytes));                                               \
+        hipLaunchKernelGGL(kfn, dim3(grid), dim3(256), lds_bytes, st, m->md, a, P);                \
+    } while (0)
+    if (W == 256 && mr == 7) ANERF_LAUNCH(256, 7);
+    else if (W == 128 && mr == 7) ANERF_LAUNCH(128, 7);
+    else if (W == 64 && mr == 7) ANERF_LAUNCH(64, 7);
+    else if (W == 256 && mr == 10) ANERF_LAUNCH(256, 10);
+    else if (W == 128 && mr == 10) ANERF_LAUNCH(128, 10);
+    else if (W == 64 && mr == 10) ANERF_LAUNCH(64, 10);
+    else return fail(ANERF_EINVAL, "no kernel instance for this width / multires");
+#undef ANERF_LAUNCH
+    HIP_TRY(hipGetLastError());
+    return ANERF_OK;
+}
+
+int anerf_gen_rays(const float* c2w, int32_t H, int32_t W, float focal_x, float focal_y, float center_x,
+                   float center_y, int32_t has_center, const int64_t* idx, int64_t n, float nearv, float farv,
+                   float* ray_batch_out, void* stream) {
+    if (n == 0) return ANERF_OK;
+    if (!c2w || !idx || !ray_batch_out || H <= 0 || W <= 0 || n < 0) return fail(ANERF_EINVAL, "anerf_gen_rays: bad arguments");
+    const float cx = has_center ? center_x : (float)(W * 0.5);
+    const float cy = has_center ? center_y : (float)(H * 0.5);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(gen_rays_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, c2w, H, W, focal_x,
+                       focal_y, cx, cy, idx, n, nearv, farv, ray_batch_out);
+    HIP_TRY(hipGetLastError());
+    return ANERF_OK;
+}
+
+int anerf_compose(const float* rgb, const float* disp, const float* acc, const int64_t* idx, int64_t n,
+                  const float* bg, int32_t white_bkgd, int64_t hw, float* out_rgb, float* out_disp, float* out_acc,
+                  void* stream) {
+    if (hw <= 0 || !out_rgb || !out_disp || n < 0 || (n > 0 && (!rgb || !disp || !acc || !idx)))
+        return fail(ANERF_EINVAL, "anerf_compose: bad arguments");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(compose_fill_kernel, dim3((unsigned)((hw + 255) / 256)), dim3(256), 0, st, bg, white_bkgd, hw,
+                       out_rgb, out_disp, out_acc);
+    if (n > 0)
+        hipLaunchKernelGGL(compose_scatter_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, rgb, disp, acc,
+                           idx, n, out_rgb, out_disp, out_acc);
+    HIP_TRY(hipGetLastError());
+    return ANERF_OK;
+}
+
+int anerf_encode_points(const anerf_model* m, const float* skts, const float* pts, const float* dirs, int64_t n_points,
+                        float* feat_out, void* stream) {
+    if (!m || !skts || !pts || !dirs || !feat_out || n_points < 0) return fail(ANERF_EINVAL, "anerf_encode_points: bad arguments");
+    if (n_points == 0) return ANERF_OK;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(encode_points_kernel, dim3((unsigned)((n_points + 127) / 128)), dim3(128), 0, st, m->md, skts,
+                       pts, dirs, n_points, feat_out);
+    HIP_TRY(hipGetLastError());
+    return ANERF_OK;
+}
+
+}  // extern "C"

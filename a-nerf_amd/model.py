@@ -1,0 +1,99 @@
+"""Device model: the reference checkpoint's weights packed once into HBM.
+
+Replaces the weight side of `create_raycaster` / `RayCaster.load_state_dict`
+(`core/raycasters.py:17-184, 768-788`): it takes the same state-dict keys
+(`network_fn_state_dict`, `network_fine_state_dict`, `embed_state_dict`,
+`embeddirs_state_dict`, `core/raycasters.py:752-766`) and hands host copies to
+`anerf_model_create`, which permutes them into the MFMA operand order and uploads them
+once (the reference's DataParallel re-broadcasts every weight on every forward).
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+
+
+def _np(x):
+    if isinstance(x, torch.Tensor):
+        x = x.detach().cpu().numpy()
+    return np.ascontiguousarray(np.asarray(x, dtype=np.float32))
+
+
+class DeviceModel:
+    """Owns one `anerf_model*` on one GPU."""
+
+    def __init__(self, cfg, ckpt, device=None):
+        cfg.validate()
+        self.cfg = cfg
+        lib = _lib.load()
+        if device is None:
+            device = torch.cuda.current_device()
+        self.device = int(device)
+        self._keep = []
+        d = _lib.ModelDesc()
+        d.n_joints, d.net_depth, d.net_width = cfg.n_joints, cfg.netdepth, cfg.netwidth
+        d.skip = cfg.skips[0]
+        d.multires, d.multires_views = cfg.multires, cfg.multires_views
+        d.use_cutoff, d.cutoff_inputs, d.cutoff_viewdir = int(cfg.use_cutoff), int(cfg.cutoff_inputs), int(
+            cfg.cutoff_viewdir)
+        d.framecode_ch = cfg.framecode_ch
+        d.n_framecodes = cfg.n_framecodes if cfg.opt_framecode else 0
+        d.density_softplus = int(cfg.density_type == "softplus")
+        d.softplus_shift, d.density_scale = cfg.softplus_shift, cfg.density_scale
+        fine_sd = ckpt.get("network_fine_state_dict")
+        d.has_fine = int(fine_sd is not None and cfg.N_importance > 0)
+        coarse = self._net(ckpt["network_fn_state_dict"])
+        fine = self._net(fine_sd) if d.has_fine else None
+        e, ev = ckpt["embed_state_dict"], ckpt["embeddirs_state_dict"]
+        emb = _lib.EmbedParams()
+        emb.cutoff_dist, emb.tau = self._p(e["cutoff_dist"]), float(_np(e["tau"]).reshape(-1)[0])
+        emb.cutoff_dist_v, emb.tau_v = self._p(ev["cutoff_dist"]), float(_np(ev["tau"]).reshape(-1)[0])
+        h = ctypes.c_void_p()
+        rc = lib.anerf_model_create(ctypes.byref(d), ctypes.byref(coarse), ctypes.byref(fine) if fine else None,
+                                    ctypes.byref(emb), self.device, ctypes.byref(h))
+        _lib.check(rc, "anerf_model_create")
+        self.handle = h
+        self._keep = []  # host copies are no longer needed once packed
+        self._ws = None
+
+    def _p(self, a):
+        a = _np(a)
+        self._keep.append(a)
+        return a.ctypes.data_as(_lib.c_f)
+
+    def _net(self, sd):
+        cfg = self.cfg
+        w = _lib.NetWeights()
+        for i in range(cfg.netdepth):
+            w.pts_w[i] = self._p(sd[f"pts_linears.{i}.weight"])
+            w.pts_b[i] = self._p(sd[f"pts_linears.{i}.bias"])
+        w.alpha_w, w.alpha_b = self._p(sd["alpha_linear.weight"]), self._p(sd["alpha_linear.bias"])
+        w.feature_w, w.feature_b = self._p(sd["feature_linear.weight"]), self._p(sd["feature_linear.bias"])
+        w.views_w, w.views_b = self._p(sd["views_linears.0.weight"]), self._p(sd["views_linears.0.bias"])
+        w.rgb_w, w.rgb_b = self._p(sd["rgb_linear.weight"]), self._p(sd["rgb_linear.bias"])
+        w.codes = self._p(sd["framecodes.codes.weight"]) if cfg.opt_framecode else None
+        return w
+
+    @property
+    def nbytes(self):
+        return int(_lib.load().anerf_model_bytes(self.handle))
+
+    def workspace(self, n_rays, S, I):
+        """Cached device workspace, grown on demand (allocation happens outside any launch)."""
+        need = int(_lib.load().anerf_workspace_size(self.handle, int(n_rays), int(S), int(I)))
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = torch.empty(max(need, 256), dtype=torch.uint8, device=f"cuda:{self.device}")
+        return self._ws, need
+
+    def close(self):
+        if getattr(self, "handle", None):
+            _lib.load().anerf_model_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,182 @@
+"""Drop-in `RayCaster` for the eval render path, backed by the HIP kernels.
+
+Mirrors `core/raycasters.py:326-474` (`RayCaster.forward` / `render_rays` and the output
+dict of `_collect_outputs`, :711-724) and the model factory `create_raycaster`
+(:17-184).  `render_rays` keeps the reference signature; what the reference does in a
+dozen ATen ops per stage happens in one fused launch (`anerf_render_rays`).
+
+Supported: eval-mode rendering (`perturb=0`, `raw_noise_std=0`, `ray_noise_std=0`,
+`lindisp=False`), any per-ray poses (`skts`/`cyls` may be expanded views of one pose —
+detected without copying — or genuinely per-ray), framecodes via `cams`.  Anything else
+raises `NotImplementedError`; nothing silently falls back to the CPU.
+"""
+import ctypes
+import glob
+import os
+
+import numpy as np
+import torch
+
+from . import _lib
+from .config import RenderConfig
+from .model import DeviceModel
+
+
+def _pose_table(x, n, per_ray_shape):
+    """(table, ray_pose) from a per-ray tensor that is often an expand() of one pose."""
+    x = x.to(dtype=torch.float32)
+    if x.dim() == len(per_ray_shape):
+        x = x.unsqueeze(0)
+    if x.shape[0] == 1 or x.stride(0) == 0:
+        return x[:1].contiguous(), None
+    if x.shape[0] != n:
+        raise ValueError(f"per-ray tensor has {x.shape[0]} rows for {n} rays")
+    flat = x.reshape(n, -1)
+    table, inverse = torch.unique(flat, dim=0, return_inverse=True)
+    return table.reshape(-1, *per_ray_shape).contiguous(), inverse.to(torch.int32).contiguous()
+
+
+class RayCaster:
+    """Eval-mode RayCaster over a DeviceModel (the reference class is an nn.Module; this one holds
+    no torch parameters: its weights live packed in HBM)."""
+
+    def __init__(self, cfg, ckpt, device=None):
+        self.cfg = cfg.validate()
+        self.model = DeviceModel(cfg, ckpt, device=device)
+        self.training = False
+        self.last_debug = None
+
+    # nn.Module-like surface used by the reference's callers
+    def eval(self):
+        self.training = False
+        return self
+
+    def train(self, mode=True):
+        if mode:
+            raise NotImplementedError("training (backward) is not implemented; use eval()")
+        return self
+
+    def load_state_dict(self, ckpt, strict=True):
+        self.model.close()
+        self.model = DeviceModel(self.cfg, ckpt, device=self.model.device)
+
+    def __call__(self, *args, fwd_type="", **kwargs):
+        return self.forward(*args, fwd_type=fwd_type, **kwargs)
+
+    def forward(self, *args, fwd_type="", **kwargs):
+        if fwd_type:
+            raise NotImplementedError(f"fwd_type={fwd_type!r} (density / mesh queries) is not implemented yet")
+        return self.render_rays(*args, **kwargs)
+
+    def render_rays(self, ray_batch, N_samples, kp_batch=None, skts=None, cyls=None, bones=None, cams=None,
+                    subject_idxs=None, retraw=False, lindisp=False, perturb=0., N_importance=0, network_fine=None,
+                    raw_noise_std=0., ray_noise_std=0., verbose=False, ext_scale=0.001, pytest=False,
+                    preproc_kwargs=None, nerf_type="nerf", chunk=None, debug=False, ret_alpha=True):
+        """Same arguments and output dict as core/raycasters.py:361-474.
+
+        `chunk` (extension): NaN-fill granularity; the reference fills per render_rays call,
+        i.e. per batchify chunk, so the default is the whole batch."""
+        if perturb or raw_noise_std or ray_noise_std:
+            raise NotImplementedError("stochastic sampling / noise (training mode) is not implemented")
+        if lindisp:
+            raise NotImplementedError("lindisp sampling is not implemented")
+        if subject_idxs is not None:
+            raise NotImplementedError("multi-subject rendering (subject_idxs) is not implemented")
+        if preproc_kwargs:
+            B = preproc_kwargs.get("density_scale", self.cfg.density_scale)
+            if B != self.cfg.density_scale:
+                raise ValueError("density_scale differs from the model's configuration")
+        if skts is None or cyls is None:
+            raise ValueError("skts and cyls are required")
+        dev = torch.device(f"cuda:{self.model.device}")
+        rb = ray_batch.to(dev, torch.float32)
+        if rb.stride(-1) != 1 or rb.stride(0) != rb.shape[1]:
+            rb = rb.contiguous()
+        n = rb.shape[0]
+        S, I = int(N_samples), int(N_importance)
+        T = S + I
+        nj = self.cfg.n_joints
+        skt_tab, pose = _pose_table(skts.to(dev), n, (nj, 4, 4))
+        cyl_tab, cpose = _pose_table(cyls.to(dev), n, (5,))
+        if (pose is None) != (cpose is None) or (pose is not None and not torch.equal(pose, cpose)):
+            if pose is None:
+                skt_tab = skt_tab.expand(n, nj, 4, 4).contiguous()
+            if cpose is None:
+                cyl_tab = cyl_tab.expand(n, 5).contiguous()
+            if pose is not None:
+                skt_tab = skt_tab[pose.long()].contiguous()
+            if cpose is not None:
+                cyl_tab = cyl_tab[cpose.long()].contiguous()
+            pose = torch.arange(n, device=dev, dtype=torch.int32)
+        cam_t = None
+        if self.cfg.opt_framecode:
+            if cams is None:
+                raise ValueError("this model uses framecodes: cams are required")
+            cam_t = cams.to(dev, torch.float32).reshape(n).contiguous()
+        f32 = dict(device=dev, dtype=torch.float32)
+        out = {"rgb_map": torch.empty(n, 3, **f32), "disp_map": torch.empty(n, **f32),
+               "acc_map": torch.empty(n, **f32)}
+        out["alpha"] = torch.empty(n, T if I > 0 else S, **f32) if ret_alpha else None
+        if I > 0:
+            out.update(rgb0=torch.empty(n, 3, **f32), disp0=torch.empty(n, **f32), acc0=torch.empty(n, **f32),
+                       alpha0=torch.empty(n, S, **f32) if ret_alpha else None)
+        dbg = None
+        if debug:
+            dd = {"near": torch.empty(n, **f32), "far": torch.empty(n, **f32), "z_coarse": torch.empty(n, S, **f32),
+                  "raw_coarse": torch.empty(n, S, 4, **f32)}
+            if I > 0:
+                dd.update(weights0=torch.empty(n, S, **f32), z_fine=torch.empty(n, T, **f32),
+                          raw_fine=torch.empty(n, T, 4, **f32))
+            dbg = _lib.Debug()
+            for k, v in dd.items():
+                setattr(dbg, k, ctypes.cast(v.data_ptr(), _lib.c_f))
+            self.last_debug = dd
+        ws, need = self.model.workspace(n, S, I)
+        rc = _lib.load().anerf_render_rays(
+            self.model.handle, _lib.ptr(rb), rb.shape[1], n, _lib.ptr(skt_tab), _lib.ptr(cyl_tab),
+            skt_tab.shape[0], _lib.ptr(pose), _lib.ptr(cam_t), S, I, int(chunk or max(n, 1)), _lib.ANERF_PREC_FP32,
+            _lib.ptr(out["rgb_map"]), _lib.ptr(out["disp_map"]), _lib.ptr(out["acc_map"]),
+            _lib.ptr(out.get("rgb0")), _lib.ptr(out.get("disp0")), _lib.ptr(out.get("acc0")),
+            _lib.ptr(out["alpha"]), _lib.ptr(out.get("alpha0")), ctypes.byref(dbg) if dbg else None,
+            _lib.ptr(ws), need, _lib.stream_handle(dev))
+        _lib.check(rc, "anerf_render_rays")
+        if not ret_alpha:
+            out.pop("alpha")
+            out.pop("alpha0", None)
+        return out
+
+
+def load_checkpoint(path):
+    """torch.load with weights_only=True (never unpickles code) -> dict of state dicts."""
+    ck = torch.load(path, map_location="cpu", weights_only=True)
+    return ck
+
+
+def create_raycaster(args, data_attrs, device=None, ckpt=None):
+    """Mirror of core/raycasters.py:17-184 for rendering.
+
+    Returns (render_kwargs_train, render_kwargs_test, start, grad_vars, optimizer, ckpt) like the
+    reference; training objects are None (training is not implemented)."""
+    skel = data_attrs["skel_type"]
+    nj = len(skel.joint_names) if hasattr(skel, "joint_names") else int(skel)
+    cfg = RenderConfig.from_args(args, nj)
+    start = 0
+    if ckpt is None:
+        ft = getattr(args, "ft_path", None)
+        if ft is not None and ft != "None":
+            paths = [ft]
+        else:
+            paths = sorted(p for p in glob.glob(os.path.join(args.basedir, args.expname, "*")) if "tar" in
+                           os.path.basename(p) and "pose" not in os.path.basename(p))
+        if not paths or getattr(args, "no_reload", False):
+            raise ValueError("no checkpoint to render (the reference would render random weights)")
+        ckpt = load_checkpoint(paths[-1])
+        start = int(ckpt.get("global_step", 0))
+    rc = RayCaster(cfg, ckpt, device=device)
+    render_kwargs_test = {
+        "ray_caster": rc, "perturb": False, "N_importance": cfg.N_importance, "N_samples": cfg.N_samples,
+        "use_viewdirs": cfg.use_viewdirs, "raw_noise_std": 0., "ray_noise_std": 0., "ext_scale": cfg.ext_scale,
+        "preproc_kwargs": {"density_scale": cfg.density_scale}, "lindisp": False,
+        "nerf_type": getattr(args, "nerf_type", "nerf"),
+    }
+    return None, render_kwargs_test, start, [], None, ckpt

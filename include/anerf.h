@@ -1,0 +1,159 @@
+/*
+ * anerf.h — C ABI of the MI355X-native A-NeRF render path (libanerf_hip.so).
+ *
+ * Plain pointers and sizes only: every float/int pointer passed to a render or stage entry is
+ * a DEVICE pointer (HBM) on the model's device; model creation takes HOST pointers to the
+ * reference's weights in their torch layout.  Every entry returns 0 on success or a negative
+ * ANERF_E* code; anerf_last_error() returns a thread-local message.  Launch entries never
+ * allocate, never synchronise and are safe to capture in a hipGraph; their scratch is the
+ * caller's workspace (size from anerf_workspace_size).
+ *
+ * Reference interfaces replaced (paths relative to danielajisafe/A-NeRF):
+ *   anerf_model_create      create_raycaster + RayCaster.load_state_dict      core/raycasters.py:17-184, 768-788
+ *   anerf_render_rays       RayCaster.render_rays (eval, perturb=0, no noise)   core/raycasters.py:361-474
+ *                           incl. get_near_far_in_cylinder + chunk NaN fill     core/utils/ray_utils.py:292-344
+ *                           batchify_rays chunking (NaN-fill granularity)       core/trainer.py:64-79
+ *   anerf_gen_rays          get_rays gathered at kp_to_valid_rays' pixel list  core/utils/ray_utils.py:6-28, 127-132
+ *   anerf_encode_points     encode_inputs + embedders (stage / debug)          core/raycasters.py:476-555
+ *   anerf_near_far          get_near_far_in_cylinder (stage)                   core/utils/ray_utils.py:292-344
+ *   anerf_compose           render_path's image composition + NaN disp -> 0    run_nerf.py:100-141
+ */
+#ifndef ANERF_H
+#define ANERF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ANERF_ABI_VERSION 1
+
+enum {
+    ANERF_OK = 0,
+    ANERF_EINVAL = -1,      /* bad argument / unsupported configuration */
+    ANERF_EHIP = -2,        /* HIP runtime error */
+    ANERF_EWORKSPACE = -3,  /* workspace too small */
+    ANERF_ENOMEM = -4
+};
+
+/* arithmetic used for the MLP contractions */
+enum { ANERF_PREC_FP32 = 0 };
+
+typedef struct anerf_model anerf_model;
+
+/* Shape of the path: the subset of run_nerf.py flags that shapes the kernel. */
+typedef struct {
+    int32_t n_joints;        /* NJ (24 SMPL, 65 Mixamo-like) */
+    int32_t net_depth;       /* netdepth D */
+    int32_t net_width;       /* netwidth W: 64, 128 or 256 */
+    int32_t skip;            /* skips=[skip]; layer skip+1 consumes [x, h]; >= D-1 means none */
+    int32_t multires;        /* kp positional-encoding frequencies (7) */
+    int32_t multires_views;  /* view-direction frequencies (4) */
+    int32_t use_cutoff;      /* --use_cutoff */
+    int32_t cutoff_inputs;   /* --cutoff_inputs */
+    int32_t cutoff_viewdir;  /* --cutoff_viewdir */
+    int32_t framecode_ch;    /* 0, or --framecode_size when --opt_framecode */
+    int32_t n_framecodes;
+    int32_t density_softplus;/* 0: relu, 1: softplus(x - softplus_shift) */
+    float softplus_shift;
+    float density_scale;     /* B in raw2outputs */
+    int32_t has_fine;        /* a separate network_fine exists (N_importance > 0, !single_net) */
+} anerf_model_desc;
+
+/* HOST pointers to one NeRF's weights, torch nn.Linear layout [out][in] (core/networks/nerf.py:57-88). */
+typedef struct {
+    const float* pts_w[16];  /* pts_linears[i].weight, i < net_depth */
+    const float* pts_b[16];
+    const float* alpha_w;    /* alpha_linear  [1][W]   */
+    const float* alpha_b;    /* [1] */
+    const float* feature_w;  /* feature_linear [W][W] */
+    const float* feature_b;
+    const float* views_w;    /* views_linears.0 [W/2][W + 3NJ(1+2*multires_views) + framecode_ch] */
+    const float* views_b;
+    const float* rgb_w;      /* rgb_linear [3][W/2] */
+    const float* rgb_b;
+    const float* codes;      /* framecodes.codes.weight [n_framecodes][framecode_ch] or NULL */
+} anerf_net_weights;
+
+/* HOST pointers to the embedders' state (core/cutoff_embedder.py:91-95). */
+typedef struct {
+    const float* cutoff_dist;    /* embed_fn.cutoff_dist [NJ]     */
+    float tau;                   /* embed_fn.tau                  */
+    const float* cutoff_dist_v;  /* embeddirs_fn.cutoff_dist [NJ] */
+    float tau_v;                 /* embeddirs_fn.tau              */
+} anerf_embed_params;
+
+/* Optional per-stage outputs of anerf_render_rays (any member may be NULL). */
+typedef struct {
+    float* near;      /* [N]   after the chunk NaN fill */
+    float* far;       /* [N]   */
+    float* z_coarse;  /* [N][S] */
+    float* raw_coarse;/* [N][S][4] (rgb, sigma) */
+    float* weights0;  /* [N][S] */
+    float* z_fine;    /* [N][S+I] sorted merged samples */
+    float* raw_fine;  /* [N][S+I][4] */
+} anerf_debug;
+
+int anerf_abi_version(void);
+const char* anerf_last_error(void);
+
+/* Pack (on the host) and upload one model to `device`. fine may be NULL when !has_fine. */
+int anerf_model_create(const anerf_model_desc* desc, const anerf_net_weights* coarse,
+                       const anerf_net_weights* fine, const anerf_embed_params* embed, int device,
+                       anerf_model** out);
+int anerf_model_destroy(anerf_model* m);
+/* bytes of packed device weights held by the model */
+size_t anerf_model_bytes(const anerf_model* m);
+
+/* Scratch bytes anerf_render_rays needs for n_rays rays. */
+size_t anerf_workspace_size(const anerf_model* m, int64_t n_rays, int32_t n_samples, int32_t n_importance);
+
+/*
+ * Render n_rays rays (RayCaster.render_rays in eval mode).
+ *   ray_batch  [n_rays][ray_stride] float: o(3), d(3), near, far (, viewdirs...) — ray_stride >= 8
+ *   skts       [n_poses][NJ][4][4]  world->joint transforms
+ *   cyls       [n_poses][5]         bounding cylinder (cx, cz, r, top, bot)
+ *   ray_pose   [n_rays] int32 pose index per ray, or NULL (all rays use pose 0)
+ *   cams       [n_rays] float framecode index per ray (float, truncated like .long()), or NULL;
+ *              a negative index selects the eval-mode mean code (core/networks/embedding.py:23-24)
+ *   chunk      NaN-fill granularity in rays (the caller's batchify chunk, 4096 in the configs)
+ *   outputs: rgb [n][3], disp [n], acc [n]; rgb0/disp0/acc0 (coarse, only when n_importance>0),
+ *            alpha [n][S+I or S], alpha0 [n][S] — any optional output may be NULL
+ */
+int anerf_render_rays(const anerf_model* m, const float* ray_batch, int32_t ray_stride, int64_t n_rays,
+                      const float* skts, const float* cyls, int32_t n_poses, const int32_t* ray_pose,
+                      const float* cams, int32_t n_samples, int32_t n_importance, int32_t chunk,
+                      int32_t precision, float* rgb, float* disp, float* acc, float* rgb0, float* disp0,
+                      float* acc0, float* alpha, float* alpha0, const anerf_debug* debug, void* workspace,
+                      size_t workspace_bytes, void* stream);
+
+/* Ray batch [n][11] (o, d, near, far, viewdir) for pixel indices idx (y*W + x) of one camera
+ * (get_rays at ray_utils.py:6-28 + the gather at :132 + render's batch at core/trainer.py:116-135). */
+int anerf_gen_rays(const float* c2w /*3x4 row-major, device*/, int32_t H, int32_t W, float focal_x,
+                   float focal_y, float center_x, float center_y, int32_t has_center, const int64_t* idx,
+                   int64_t n, float near, float far, float* ray_batch_out, void* stream);
+
+/* Frame compose of render_path (run_nerf.py:100-141): pixels outside idx get the background
+ * (bg [hw][3] if given, else 1 when white_bkgd, else 0), disp 0, acc 0; pixels idx[i] get
+ * rgb + (1 - acc) * background, disp (NaN -> 0) and acc.  out_acc may be NULL. */
+int anerf_compose(const float* rgb, const float* disp, const float* acc, const int64_t* idx, int64_t n,
+                  const float* bg, int32_t white_bkgd, int64_t hw, float* out_rgb, float* out_disp, float* out_acc,
+                  void* stream);
+
+/* Stage: near/far of get_near_far_in_cylinder with the per-chunk NaN fill. */
+int anerf_near_far(const float* ray_batch, int32_t ray_stride, int64_t n_rays, const float* cyls,
+                   const int32_t* ray_pose, int32_t chunk, float* near_out, float* far_out, void* workspace,
+                   size_t workspace_bytes, void* stream);
+
+/* Stage: MLP input features [M][F] of points pts [M][3] on rays with directions dirs [M][3],
+ * joint transforms skts [NJ][4][4]; F = NJ(1+2 multires) + 3NJ + 3NJ(1+2 multires_views). */
+int anerf_encode_points(const anerf_model* m, const float* skts, const float* pts, const float* dirs,
+                        int64_t n_points, float* feat_out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ANERF_H */

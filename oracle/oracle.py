@@ -1,0 +1,190 @@
+"""ctypes front-end of the C oracle (oracle/anerf_oracle.c).  TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+MAXL = 16
+
+_f = ctypes.POINTER(ctypes.c_float)
+_i32 = ctypes.POINTER(ctypes.c_int32)
+
+
+class _Net(ctypes.Structure):
+    _fields_ = [("w", _f * MAXL), ("b", _f * MAXL), ("wa", _f), ("ba", _f), ("wf", _f), ("bf", _f),
+                ("wv", _f), ("bv", _f), ("wrgb", _f), ("brgb", _f), ("codes", _f)]
+
+
+class _Model(ctypes.Structure):
+    _fields_ = [("nj", ctypes.c_int), ("D", ctypes.c_int), ("W", ctypes.c_int), ("skip", ctypes.c_int),
+                ("multires", ctypes.c_int), ("multires_views", ctypes.c_int),
+                ("use_cutoff", ctypes.c_int), ("cutoff_inputs", ctypes.c_int), ("cutoff_viewdir", ctypes.c_int),
+                ("framecode_ch", ctypes.c_int), ("n_framecodes", ctypes.c_int),
+                ("density_softplus", ctypes.c_int), ("softplus_shift", ctypes.c_float),
+                ("density_scale", ctypes.c_float), ("tau", ctypes.c_float), ("tau_v", ctypes.c_float),
+                ("cutoff", _f), ("cutoff_v", _f), ("has_fine", ctypes.c_int), ("coarse", _Net), ("fine", _Net)]
+
+
+def build():
+    subprocess.run(["make", "-C", HERE, "-s"], check=True)
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        L.oracle_render_rays.restype = ctypes.c_int
+        L.oracle_near_far.restype = ctypes.c_int64
+        L.oracle_feature_dim.restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(_f) if a is not None else None
+
+
+def _f32(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float32))
+
+
+class OracleModel:
+    """Holds contiguous (transposed where the C side wants [in][out]) weight copies."""
+
+    def __init__(self, cfg, ckpt):
+        self.cfg = cfg
+        self._keep = []
+        m = _Model()
+        m.nj, m.D, m.W, m.skip = cfg.n_joints, cfg.netdepth, cfg.netwidth, cfg.skips[0]
+        m.multires, m.multires_views = cfg.multires, cfg.multires_views
+        m.use_cutoff, m.cutoff_inputs, m.cutoff_viewdir = int(cfg.use_cutoff), int(cfg.cutoff_inputs), int(
+            cfg.cutoff_viewdir)
+        m.framecode_ch, m.n_framecodes = cfg.framecode_ch, (cfg.n_framecodes if cfg.opt_framecode else 0)
+        m.density_softplus = int(cfg.density_type == "softplus")
+        m.softplus_shift, m.density_scale = cfg.softplus_shift, cfg.density_scale
+        e, ev = ckpt["embed_state_dict"], ckpt["embeddirs_state_dict"]
+        m.tau, m.tau_v = float(np.asarray(e["tau"])), float(np.asarray(ev["tau"]))
+        m.cutoff, m.cutoff_v = self._k(e["cutoff_dist"]), self._k(ev["cutoff_dist"])
+        self._net(m.coarse, ckpt["network_fn_state_dict"])
+        fine = ckpt.get("network_fine_state_dict")
+        m.has_fine = int(fine is not None)
+        if fine is not None:
+            self._net(m.fine, fine)
+        self.m = m
+
+    def _k(self, a, transpose=False):
+        a = _f32(a)
+        if transpose:
+            a = np.ascontiguousarray(a.T)
+        self._keep.append(a)
+        return _p(a)
+
+    def _net(self, net, sd):
+        for i in range(self.cfg.netdepth):
+            net.w[i] = self._k(sd[f"pts_linears.{i}.weight"], transpose=True)
+            net.b[i] = self._k(sd[f"pts_linears.{i}.bias"])
+        net.wa, net.ba = self._k(sd["alpha_linear.weight"]), self._k(sd["alpha_linear.bias"])
+        net.wf, net.bf = self._k(sd["feature_linear.weight"], True), self._k(sd["feature_linear.bias"])
+        net.wv, net.bv = self._k(sd["views_linears.0.weight"], True), self._k(sd["views_linears.0.bias"])
+        net.wrgb, net.brgb = self._k(sd["rgb_linear.weight"]), self._k(sd["rgb_linear.bias"])
+        net.codes = self._k(sd["framecodes.codes.weight"]) if self.cfg.opt_framecode else None
+
+    @property
+    def ref(self):
+        return ctypes.byref(self.m)
+
+    # ------------------------------------------------------------------ stages
+    def feature_dim(self):
+        return lib().oracle_feature_dim(self.ref)
+
+    def near_far(self, ray_batch, cyls, ray_pose=None, chunk=4096):
+        rb = _f32(ray_batch)
+        n, stride = rb.shape
+        near = np.empty(n, np.float32)
+        far = np.empty(n, np.float32)
+        q = np.empty(n, np.float32)
+        cy = _f32(cyls)
+        rp = None if ray_pose is None else np.ascontiguousarray(ray_pose, dtype=np.int32)
+        filled = lib().oracle_near_far(_p(rb), stride, ctypes.c_int64(n), _p(cy),
+                                       rp.ctypes.data_as(_i32) if rp is not None else None, chunk,
+                                       _p(near), _p(far), _p(q))
+        return near, far, q, int(filled)
+
+    def encode(self, skts, pts, dirs):
+        pts, dirs, sk = _f32(pts), _f32(dirs), _f32(skts)
+        M = pts.shape[0]
+        out = np.empty((M, self.feature_dim()), np.float32)
+        lib().oracle_encode(self.ref, _p(sk), _p(pts), _p(dirs), ctypes.c_int64(M), _p(out))
+        return out
+
+    def network(self, feat, fine=False, code=None):
+        feat = _f32(feat)
+        M = feat.shape[0]
+        raw = np.empty((M, 4), np.float32)
+        c = None if code is None else _f32(code)
+        lib().oracle_network(self.ref, int(fine), _p(feat), ctypes.c_int64(M), _p(c), _p(raw))
+        return raw
+
+    def raw2outputs(self, raw, z, dirs):
+        raw, z, dirs = _f32(raw), _f32(z), _f32(dirs)
+        n, ns = z.shape
+        rgb = np.empty((n, 3), np.float32)
+        disp, acc = np.empty(n, np.float32), np.empty(n, np.float32)
+        w, a = np.empty((n, ns), np.float32), np.empty((n, ns), np.float32)
+        lib().oracle_raw2outputs(self.ref, _p(raw), _p(z), _p(dirs), ctypes.c_int64(n), ns, _p(rgb), _p(disp),
+                                 _p(acc), _p(w), _p(a))
+        return dict(rgb_map=rgb, disp_map=disp, acc_map=acc, weights=w, alpha=a)
+
+    def sample_pdf(self, bins, weights, n_samples):
+        bins, weights = _f32(bins), _f32(weights)
+        n, nb = bins.shape
+        out = np.empty((n, n_samples), np.float32)
+        lib().oracle_sample_pdf(_p(bins), _p(weights), ctypes.c_int64(n), nb, n_samples, _p(out))
+        return out
+
+    def render_rays(self, ray_batch, skts, cyls, ray_pose=None, cams=None, N_samples=None, N_importance=None,
+                    chunk=4096, nthreads=0, with_z=False):
+        """render_rays over a whole ray list (chunked NaN fill), returns the reference's output dict."""
+        cfg = self.cfg
+        S = cfg.N_samples if N_samples is None else N_samples
+        I = cfg.N_importance if N_importance is None else N_importance
+        rb = _f32(ray_batch)
+        n, stride = rb.shape
+        T = S + I
+        rgb, disp, acc = np.empty((n, 3), np.float32), np.empty(n, np.float32), np.empty(n, np.float32)
+        alpha = np.empty((n, T if I > 0 else S), np.float32)
+        out = dict(rgb_map=rgb, disp_map=disp, acc_map=acc, alpha=alpha)
+        extra = [None] * 4
+        if I > 0:
+            out.update(rgb0=np.empty((n, 3), np.float32), disp0=np.empty(n, np.float32),
+                       acc0=np.empty(n, np.float32), alpha0=np.empty((n, S), np.float32))
+            extra = [out["rgb0"], out["disp0"], out["acc0"], out["alpha0"]]
+        z = np.empty((n, T if I > 0 else S), np.float32) if with_z else None
+        rp = None if ray_pose is None else np.ascontiguousarray(ray_pose, dtype=np.int32)
+        cm = None if cams is None else _f32(cams)
+        rc = lib().oracle_render_rays(self.ref, _p(rb), stride, ctypes.c_int64(n), _p(_f32(skts)), _p(_f32(cyls)),
+                                      rp.ctypes.data_as(_i32) if rp is not None else None, _p(cm), S, I, chunk,
+                                      nthreads, _p(rgb), _p(disp), _p(acc), _p(extra[0]), _p(extra[1]),
+                                      _p(extra[2]), _p(alpha), _p(extra[3]), _p(z))
+        if rc != 0:
+            raise RuntimeError(f"oracle_render_rays failed ({rc})")
+        if with_z:
+            out["z"] = z
+        return out
+
+
+def linspace(n):
+    out = np.empty(n, np.float32)
+    lib().oracle_linspace(n, _p(out))
+    return out

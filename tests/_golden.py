@@ -1,0 +1,45 @@
+"""Loading helpers for the committed golden fixtures (tests/golden/*.npz)."""
+import ast
+import importlib
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLDEN = os.path.join(HERE, "golden")
+
+anerf = importlib.import_module("a-nerf_amd")
+syn = importlib.import_module("a-nerf_amd.synthetic")
+config = importlib.import_module("a-nerf_amd.config")
+
+NAMES = ["c1_64_s32_d4w128", "c2_256_s64_d8w256", "c3_512_s64i128_d8w256", "c4_512_s64i128_j65",
+         "h1_nanfill_s32i16_d4w128", "fc_64_s32i32_d4w128"]
+
+
+class Golden:
+    def __init__(self, name):
+        self.name = name
+        z = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+        self.d = {k: z[k] for k in z.files}
+        self.meta = ast.literal_eval(str(self.d["meta"]))
+        m = self.meta
+        fc = bool(m.get("framecode", 0))
+        self.cfg = config.RenderConfig(n_joints=m["NJ"], netdepth=m["D"], netwidth=m["W"], N_samples=m["S"],
+                                       N_importance=m["I"], opt_framecode=fc, n_framecodes=5 if fc else 0,
+                                       chunk=m["chunk"], ext_scale=m["ext_scale"]).validate()
+        self.ckpt = syn.make_checkpoint(m["seed"], n_joints=m["NJ"], D=m["D"], W=m["W"], fine=m["I"] > 0,
+                                        tau=m["tau"], use_framecode=fc, n_framecodes=5)
+        assert syn.checkpoint_sha256(self.ckpt) == m["sha256"], "synthetic weights drifted from the fixture"
+
+    def __getitem__(self, k):
+        return self.d[k]
+
+    def has(self, k):
+        return k in self.d
+
+    def ray_batch(self):
+        o, d = self.d["rays_o"], self.d["rays_d"]
+        n = o.shape[0]
+        vd = d / np.linalg.norm(d, axis=-1, keepdims=True)
+        return np.concatenate([o, d, np.zeros((n, 1), np.float32), np.ones((n, 1), np.float32), vd],
+                              axis=-1).astype(np.float32)

@@ -1,0 +1,288 @@
+"""Generate the golden fixtures under tests/golden/ by running the REFERENCE render path.
+
+Runs ONLY in the survey/build container, where /root/reference exists; it is never
+needed on the GPU box (the fixtures it writes are committed).  It imports the
+reference's own Python modules (run_nerf.render_path, core.trainer.render,
+core.raycasters.create_raycaster / RayCaster stages) with empty stubs for the
+third-party modules that never touch the render arithmetic (SURVEY.md §8c,
+Appendix B), feeds them our deterministic synthetic scenes and seeded weights
+(a-nerf_amd/synthetic.py), and stores inputs + outputs as small .npz files.
+
+Weights are not stored: the fixture records (seed, sha256) and the tests
+regenerate them with a-nerf_amd/synthetic.py and check the hash.
+
+Usage:  python tests/golden/make_golden.py  [--only NAME]
+"""
+import argparse
+import importlib
+import importlib.abc
+import importlib.machinery
+import os
+import sys
+import tempfile
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+
+sys.path.insert(0, REPO)
+anerf_syn = importlib.import_module("a-nerf_amd.synthetic")
+
+_STUBS = ["cv2", "pytorch3d", "imageio", "deepdish", "h5py", "smplx", "pytorch_msssim",
+          "tensorboard", "mcubes", "trimesh", "plotly", "skimage", "lpips"]
+
+
+class _StubFinder(importlib.abc.MetaPathFinder, importlib.abc.Loader):
+    """Empty modules for imports the render arithmetic never uses."""
+
+    def find_spec(self, name, path, target=None):
+        if name.split(".")[0] in _STUBS or name.startswith("torch.utils.tensorboard"):
+            return importlib.machinery.ModuleSpec(name, self, is_package=True)
+        return None
+
+    def create_module(self, spec):
+        m = types.ModuleType(spec.name)
+        m.__path__ = []
+        def _attr(attr):
+            if attr.startswith("__"):
+                raise AttributeError(attr)
+            if attr[:1].isupper():
+                return type(attr, (), {"__init__": lambda self, *a, **k: None})
+            return lambda *a, **k: None
+        m.__getattr__ = _attr
+        return m
+
+    def exec_module(self, module):
+        pass
+
+
+def import_reference():
+    sys.dont_write_bytecode = True
+    sys.meta_path.insert(0, _StubFinder())
+    cap = types.ModuleType("configargparse")
+
+    class _AP(argparse.ArgumentParser):
+        def add_argument(self, *a, **k):
+            k.pop("is_config_file", None)
+            return super().add_argument(*a, **k)
+
+    cap.ArgumentParser = _AP
+    sys.modules["configargparse"] = cap
+    sys.path.insert(0, REF)
+    import torch  # noqa: F401
+    run_nerf = importlib.import_module("run_nerf")
+    trainer = importlib.import_module("core.trainer")
+    raycasters = importlib.import_module("core.raycasters")
+    ray_utils = importlib.import_module("core.utils.ray_utils")
+    sk = importlib.import_module("core.utils.skeleton_utils")
+    return run_nerf, trainer, raycasters, ray_utils, sk
+
+
+# name -> config (BASELINE.json configs 1-4, plus small edge cases)
+CONFIGS = {
+    "c1_64_s32_d4w128": dict(H=64, NJ=24, S=32, I=0, D=4, W=128, tau=20.0, kind="frame", seed=11),
+    "c2_256_s64_d8w256": dict(H=256, NJ=24, S=64, I=0, D=8, W=256, tau=20.0, kind="rays", n_rays=512, seed=12),
+    "c3_512_s64i128_d8w256": dict(H=512, NJ=24, S=64, I=128, D=8, W=256, tau=79.6, kind="rays", n_rays=256, seed=13),
+    "c4_512_s64i128_j65": dict(H=512, NJ=65, S=64, I=128, D=8, W=256, tau=20.0, kind="rays", n_rays=128, seed=14),
+    # chunk-coupled NaN fill of near/far (hazard H1): a chunk that contains rays missing the cylinder
+    "h1_nanfill_s32i16_d4w128": dict(H=128, NJ=24, S=32, I=16, D=4, W=128, tau=20.0, kind="nanfill", seed=15),
+    # per-frame code (opt_framecode, mixamo configs) with cam index >= 0 and the eval-mode mean code (< 0)
+    "fc_64_s32i32_d4w128": dict(H=64, NJ=24, S=32, I=32, D=4, W=128, tau=20.0, kind="framecode", n_rays=192, seed=16),
+}
+
+
+def build_reference(mods, cfg, tmp):
+    run_nerf, trainer, raycasters, ray_utils, sk = mods
+    import torch
+    NJ = cfg["NJ"]
+    use_fc = cfg["kind"] == "framecode"
+    argv = ["--N_samples", str(cfg["S"]), "--N_importance", str(cfg["I"]),
+            "--netdepth", str(cfg["D"]), "--netwidth", str(cfg["W"]),
+            "--multires", "7", "--multires_views", "4",
+            "--use_cutoff", "--cutoff_viewdir", "--cutoff_inputs", "--use_viewdirs",
+            "--ext_scale", "0.001", "--chunk", "4096", "--no_reload",
+            "--basedir", tmp, "--expname", "x"]
+    if use_fc:
+        argv += ["--opt_framecode", "--n_framecodes", "5"]
+    args = run_nerf.config_parser().parse_args(argv)
+    os.makedirs(os.path.join(tmp, "x"), exist_ok=True)
+    parents, rest = anerf_syn.skeleton(NJ)
+    if NJ == 24:
+        skel = sk.SMPLSkeleton
+    else:
+        skel = sk.Skeleton(joint_names=[f"j{i}" for i in range(NJ)], joint_trees=parents, root_id=0,
+                           nonroot_id=list(range(1, NJ)), cutoffs={}, end_effectors=[])
+    data_attrs = {"skel_type": skel, "near": 0.0, "far": 1.0, "n_views": 5,
+                  "joint_coords": np.zeros((NJ, 3, 3), np.float32)}
+    _, render_kwargs, _, _, _, _ = raycasters.create_raycaster(args, data_attrs)
+    ck = anerf_syn.make_checkpoint(cfg["seed"], n_joints=NJ, D=cfg["D"], W=cfg["W"], fine=cfg["I"] > 0,
+                                   tau=cfg["tau"], use_framecode=use_fc, n_framecodes=5)
+    ck_t = {k: {n: torch.from_numpy(np.array(v)) for n, v in d.items()} for k, d in ck.items()}
+    rc = render_kwargs["ray_caster"]
+    rc.load_state_dict(ck_t, strict=True)
+    rc.eval()
+    return args, render_kwargs, ck
+
+
+def scene_for(cfg):
+    sc = anerf_syn.make_scene(n_joints=cfg["NJ"], H=cfg["H"], W=cfg["H"], seed=cfg["seed"])
+    return sc
+
+
+def rays_for(mods, sc):
+    """reference kp_to_valid_rays on frame 0."""
+    import torch
+    _, _, _, ray_utils, _ = mods
+    c2w = torch.from_numpy(sc["c2ws"])
+    kp = torch.from_numpy(sc["kps"])
+    rays, valid_idxs, cyls, bboxes = ray_utils.kp_to_valid_rays(c2w, sc["H"], sc["W"], sc["focal"], kps=kp,
+                                                                ext_scale=0.001)
+    return rays[0], valid_idxs[0].numpy(), cyls.numpy(), bboxes[0]
+
+
+def render_subset(mods, render_kwargs, o, d, sc, cams=None):
+    import torch
+    _, trainer, _, _, _ = mods
+    n = o.shape[0]
+    kp = torch.from_numpy(sc["kps"][0:1]).expand(n, -1, -1)
+    skts = torch.from_numpy(sc["skts"][0:1]).expand(n, -1, -1, -1)
+    bones = torch.from_numpy(sc["bones"][0:1]).expand(n, -1, -1)
+    cyl = torch.from_numpy(sc["cyls"][0:1]).expand(n, -1)
+    cam_t = None if cams is None else torch.from_numpy(cams)
+    with torch.no_grad():
+        ret = trainer.render(sc["H"], sc["W"], sc["focal"], chunk=4096, rays=(o, d),
+                             c2w=torch.from_numpy(sc["c2ws"][0][:3, :4]),
+                             kp_batch=kp, skts=skts, cyls=cyl, bones=bones, cams=cam_t, subject_idxs=None,
+                             **render_kwargs)
+    return {k: v.numpy() for k, v in ret.items()}
+
+
+def stage_dump(mods, render_kwargs, o, d, sc, n_stage, cams=None):
+    """Per-stage tensors of render_rays (core/raycasters.py:411-474) for a few rays."""
+    import torch
+    _, _, raycasters, ray_utils, _ = mods
+    rc = render_kwargs["ray_caster"]
+    pk = render_kwargs["preproc_kwargs"]
+    S, I = render_kwargs["N_samples"], render_kwargs["N_importance"]
+    o, d = o[:n_stage], d[:n_stage]
+    n = o.shape[0]
+    kp = torch.from_numpy(sc["kps"][0:1]).expand(n, -1, -1)
+    skts = torch.from_numpy(sc["skts"][0:1]).expand(n, -1, -1, -1)
+    bones = torch.from_numpy(sc["bones"][0:1]).expand(n, -1, -1)
+    cyl = torch.from_numpy(sc["cyls"][0:1]).expand(n, -1)
+    cam_t = None if cams is None else torch.from_numpy(cams[:n_stage])
+    out = {}
+    with torch.no_grad():
+        near, far = ray_utils.get_near_far_in_cylinder(o, d, cyl, near=torch.zeros(n, 1), far=torch.ones(n, 1))
+        pts, z = rc.sample_pts(o, d, near, far, n, S, 0.0, False)
+        jc = rc.get_subject_joint_coords(None, pts.device)
+        enc = rc.encode_inputs(pts, [o[:, None, :], d[:, None, :]], kp, skts, bones, cam_idxs=cam_t,
+                               subject_idxs=None, joint_coords=jc, network=rc.network, **pk)
+        feat = torch.cat([enc["v"], enc["r"], enc["d"]], dim=-1)  # (+ cam column when cams given)
+        raw = rc.run_network(enc, rc.network)
+        ret = rc.network.raw2outputs(raw, z, d, 0.0, encoded=enc, B=pk["density_scale"], act_fn=pk["density_fn"])
+        out.update(near=near.numpy(), far=far.numpy(), z=z.numpy(), feat=feat[:, :4].numpy(),
+                   raw=raw.numpy(), weights=ret["weights"].numpy())
+        if I > 0:
+            pts_is, z_all, z_is, sidx = rc.sample_pts_is(o, d, z, ret["weights"], I, det=True, is_only=False)
+            enc_is = rc.encode_inputs(pts_is, [o[:, None, :], d[:, None, :]], kp, skts, bones, cam_idxs=cam_t,
+                                      subject_idxs=None, joint_coords=jc, network=rc.network_fine, **pk)
+            merged = rc._merge_encodings(enc, enc_is, sidx, n, S + I)
+            raw_f = rc.run_network(merged, rc.network_fine)
+            out.update(z_is=z_is.numpy(), z_all=z_all.numpy(), raw_f=raw_f.numpy())
+    return {"stage_" + k: v for k, v in out.items()}
+
+
+def make(name, cfg, mods, tmp):
+    import torch
+    run_nerf = mods[0]
+    args, render_kwargs, ck = build_reference(mods, cfg, os.path.join(tmp, name))
+    sc = scene_for(cfg)
+    sha = anerf_syn.checkpoint_sha256(ck)
+    meta = dict(seed=cfg["seed"], sha256=sha, NJ=cfg["NJ"], S=cfg["S"], I=cfg["I"], D=cfg["D"], W=cfg["W"],
+                tau=cfg["tau"], H=sc["H"], focal=sc["focal"], ext_scale=0.001, chunk=4096,
+                framecode=int(cfg["kind"] == "framecode"))
+    data = {"c2ws": sc["c2ws"], "kps": sc["kps"], "skts": sc["skts"], "bones": sc["bones"]}
+    (o, d), vidx, cyls, (tl, br) = rays_for(mods, sc)
+    sc["cyls"] = cyls
+    data.update(cyls=cyls, valid_idx=vidx, tl=np.asarray(tl), br=np.asarray(br))
+    if cfg["kind"] == "frame":
+        with torch.no_grad():
+            rgbs, disps, accs, vids, bbs = run_nerf.render_path(
+                torch.from_numpy(sc["c2ws"]), (sc["H"], sc["W"], sc["focal"]), 4096, render_kwargs,
+                kp=torch.from_numpy(sc["kps"]), skts=torch.from_numpy(sc["skts"]),
+                bones=torch.from_numpy(sc["bones"]), ret_acc=True, ext_scale=0.001)
+        data.update(frame_rgb=rgbs, frame_disp=disps, frame_acc=accs)
+        sel = np.arange(min(64, len(vidx)))
+    elif cfg["kind"] == "nanfill":
+        # contiguous 4096-ray chunk starting at the top of the box: its corner rays miss the cylinder
+        sel = np.arange(0, min(4096, len(vidx)))
+    else:
+        # a contiguous run from the middle of the box (one NaN-fill chunk)
+        start = len(vidx) // 2 - cfg["n_rays"] // 2
+        sel = np.arange(start, start + cfg["n_rays"])
+    o_s, d_s = o[sel], d[sel]
+    cams = None
+    if cfg["kind"] == "framecode":
+        cams = np.where(np.arange(len(sel)) % 3 == 0, 2.0, 4.0).astype(np.float32)
+    ret = render_subset(mods, render_kwargs, o_s, d_s, sc, cams=cams)
+    data.update(sel=sel, rays_o=o_s.numpy(), rays_d=d_s.numpy(),
+                **{"out_" + k: v for k, v in ret.items()})
+    if cams is not None:
+        data["cams"] = cams
+        # eval-mode mean code: every cam index < 0 (core/networks/embedding.py:23-24)
+        cams_neg = np.full(len(sel), -1.0, np.float32)
+        ret_neg = render_subset(mods, render_kwargs, o_s, d_s, sc, cams=cams_neg)
+        data["cams_neg"] = cams_neg
+        data.update(**{"outneg_" + k: v for k, v in ret_neg.items()})
+    if cfg["kind"] in ("rays", "framecode"):
+        data.update(stage_dump(mods, render_kwargs, o_s, d_s, sc, n_stage=4, cams=cams))
+    path = os.path.join(HERE, name + ".npz")
+    np.savez_compressed(path, meta=np.array(repr(meta)), **data)
+    print(f"wrote {path}  rays={len(sel)}  ({os.path.getsize(path) / 1024:.0f} KiB)")
+
+
+def bbox_table(mods):
+    """Integer boxes / pixel counts of the full-size frames of every config (hazard H2)."""
+    import torch
+    _, _, _, ray_utils, _ = mods
+    rows = {}
+    for name, (H, NJ, seed) in {"c2": (256, 24, 12), "c3": (512, 24, 13), "c4": (512, 65, 14),
+                                "c5": (1024, 24, 13), "c3_f3": (512, 24, 40)}.items():
+        sc = anerf_syn.make_scene(n_joints=NJ, H=H, W=H, seed=seed, n_frames=3, yaw_step=0.4)
+        rays, vids, cyls, bbs = ray_utils.kp_to_valid_rays(torch.from_numpy(sc["c2ws"]), H, H, sc["focal"],
+                                                           kps=torch.from_numpy(sc["kps"]), ext_scale=0.001)
+        rows[name + "_tl"] = np.stack([np.asarray(b[0]) for b in bbs])
+        rows[name + "_br"] = np.stack([np.asarray(b[1]) for b in bbs])
+        rows[name + "_n"] = np.array([len(v) for v in vids])
+        rows[name + "_cyls"] = cyls.numpy()
+        rows[name + "_rays_d_first"] = np.stack([r[1][:8].numpy() for r in rays])
+        rows[name + "_rays_d_last"] = np.stack([r[1][-8:].numpy() for r in rays])
+        rows[name + "_rays_o"] = np.stack([r[0][0].numpy() for r in rays])
+        rows[name + "_meta"] = np.array([H, NJ, seed])
+    path = os.path.join(HERE, "bboxes.npz")
+    np.savez_compressed(path, **rows)
+    print(f"wrote {path}")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default=None)
+    a = ap.parse_args()
+    import torch
+    torch.set_num_threads(8)
+    mods = import_reference()
+    with tempfile.TemporaryDirectory() as tmp:
+        for name, cfg in CONFIGS.items():
+            if a.only and a.only != name:
+                continue
+            make(name, cfg, mods, tmp)
+    if not a.only or a.only == "bboxes":
+        bbox_table(mods)
+
+
+if __name__ == "__main__":
+    main()
