@@ -1,0 +1,180 @@
+"""Benchmark: rays/s of the A-NeRF render path at BASELINE.json config 3.
+
+A "step" renders one synthetic 512x512 frame (64 coarse + 128 importance samples, 24-joint
+skeleton, 8x256 MLP): ray generation from the frame's bounding-cylinder pixel list, the fused
+render kernel, and frame composition — all on the GPU with inputs resident in HBM (the
+pixel lists are computed on the host before the timed region, like kp_to_valid_rays).
+
+Multi-GPU (launched by torch.distributed.run): each rank renders its own frame (a different
+pose) per step — frames are independent, so there is no collective in the data path and
+scaling is weak; rank 0 reports total rays / max-over-ranks time.
+
+Extra JSON fields:
+  roofline      dominant kernel (render_kernel) vs the FP32 MFMA peak, per-launch duration
+                from HIP events on the launch stream; algorithmic FLOPs = SURVEY §8(d)
+                per-sample MLP FLOPs x MLP samples per ray x rays per launch
+  cpu_baseline  the C oracle (oracle/anerf_oracle.c, OpenMP) on a bounded sample of the same
+                frame's rays, rank 0 at N=1 only
+"""
+import argparse
+import glob
+import importlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+BASELINE = json.load(open(os.path.join(REPO, "BASELINE.json")))
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md, FP32 matrix
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--res", type=int, default=512)
+    ap.add_argument("--joints", type=int, default=24)
+    ap.add_argument("--samples", type=int, default=64)
+    ap.add_argument("--importance", type=int, default=128)
+    ap.add_argument("--cpu-rays", type=int, default=768, help="rays in the CPU-baseline sample")
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def traffic_from_profiles():
+    """Per-launch HBM bytes of render_kernel from the committed rocprofv3 --pmc summary, if any."""
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")))
+    if not files:
+        return None
+    try:
+        d = json.load(open(files[-1]))
+        return d.get("render_kernel_hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl")
+    dev = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(dev)
+
+    anerf = importlib.import_module("a-nerf_amd")
+    syn = importlib.import_module("a-nerf_amd.synthetic")
+    _lib = importlib.import_module("a-nerf_amd._lib")
+    lib = _lib.load()
+
+    H = W = a.res
+    S, I = a.samples, a.importance
+    cfg = anerf.RenderConfig(n_joints=a.joints, N_samples=S, N_importance=I).validate()
+    ck = syn.make_checkpoint(13, n_joints=a.joints, D=8, W=256, fine=I > 0, tau=79.6)
+    sc = syn.make_scene(n_joints=a.joints, H=H, W=W, seed=13 + rank)
+    rc = anerf.RayCaster(cfg, ck, device=local)
+    idxs, cyls, _ = anerf.rays.valid_pixels(sc["c2ws"], H, W, sc["focal"], kps=sc["kps"], ext_scale=0.001)
+    idx = torch.from_numpy(idxs[0]).to(dev)
+    n = int(idx.shape[0])
+    c2w = torch.from_numpy(np.ascontiguousarray(sc["c2ws"][0][:3, :4])).to(dev)
+    skts = torch.from_numpy(sc["skts"][0:1]).to(dev)
+    cyl = torch.from_numpy(cyls[0:1]).to(dev)
+    rb = torch.empty(n, 11, device=dev)
+    img = torch.empty(H * W, 3, device=dev)
+    dimg = torch.empty(H * W, device=dev)
+    aimg = torch.empty(H * W, device=dev)
+    st = _lib.stream_handle(dev)
+    ev = []
+
+    def step(record):
+        _lib.check(lib.anerf_gen_rays(_lib.ptr(c2w), H, W, sc["focal"], sc["focal"], 0.0, 0.0, 0, _lib.ptr(idx), n,
+                                      0.0, 1.0, _lib.ptr(rb), st), "gen_rays")
+        if record:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+        out = rc.render_rays(rb, S, skts=skts.expand(n, -1, -1, -1), cyls=cyl.expand(n, -1), N_importance=I,
+                             chunk=4096, ret_alpha=False)
+        if record:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            ev.append((e0, e1))
+        _lib.check(lib.anerf_compose(_lib.ptr(out["rgb_map"]), _lib.ptr(out["disp_map"]), _lib.ptr(out["acc_map"]),
+                                     _lib.ptr(idx), n, None, 0, H * W, _lib.ptr(img), _lib.ptr(dimg), _lib.ptr(aimg),
+                                     st), "compose")
+
+    for _ in range(a.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in ev]))
+    rays_job = n * a.steps
+    if dist:
+        t = torch.tensor([elapsed, float(rays_job)], device=dev, dtype=torch.float64)
+        tmax = t[:1].clone()
+        tdist.all_reduce(tmax, op=tdist.ReduceOp.MAX)
+        tdist.all_reduce(t[1:], op=tdist.ReduceOp.SUM)
+        elapsed, rays_job = float(tmax.item()), float(t[1].item())
+
+    flop_ray = anerf.flops_per_sample(cfg) * anerf.samples_per_ray(cfg)
+    achieved_tf = flop_ray * n / (kern_ms * 1e-3) / 1e12
+    traffic = traffic_from_profiles()
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle
+        cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+        om = oracle.OracleModel(cfg, ck)
+        rb_h = rb.cpu().numpy()
+        sel = np.linspace(0, n - 1, min(a.cpu_rays, n)).astype(np.int64)
+        t1 = time.perf_counter()
+        om.render_rays(rb_h[sel], sc["skts"][0], cyls[0:1], chunk=4096, nthreads=cores)
+        dt = time.perf_counter() - t1
+        cpu = {"value": round(len(sel) / dt, 2), "unit": "rays/s", "cores": cores, "kind": "port",
+               "sample": f"{len(sel)} rays evenly spaced over the frame's {n} bbox rays, C oracle "
+                         f"(oracle/anerf_oracle.c, OpenMP {cores} threads), {dt:.1f} s wall"}
+
+    if rank == 0:
+        value = rays_job / elapsed
+        line = {
+            "metric": BASELINE["metric"], "value": round(value, 1), "unit": "rays/s", "n_gpus": world,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(1e3 * elapsed / a.steps, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic (seeded SMPL-24 pose + seeded 8x256 weights; no dataset/checkpoint offline)",
+            "config": {"workload": f"config3: {H}x{W} frame, {S}+{I} samples, {a.joints}-joint, 8x256 MLP, "
+                                   f"one frame per GPU per step", "rays_per_frame": n,
+                       "parallelism": f"frame-per-rank x{world}"},
+            "roofline": {"bound": "mfma", "achieved": round(achieved_tf, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_MFMA_PEAK_TFLOPS, 4),
+                         "traffic": traffic, "kernel_ms": round(kern_ms, 3),
+                         "flop_per_ray": flop_ray},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist:
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
