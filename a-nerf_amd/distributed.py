@@ -1,0 +1,76 @@
+"""Multi-GPU rendering: one process per GPU (torch.distributed; backend "nccl" = RCCL over xGMI).
+
+The reference's only parallelism is nn.DataParallel (core/raycasters.py:157, run_render.py:111):
+every forward re-broadcasts the weights, scatters a 4096-ray chunk over the GPUs and gathers
+the outputs on GPU 0 — and its chunk-coupled NaN fill then depends on the GPU count.  Here:
+
+* weights are uploaded once per rank (anerf_model_create), never re-broadcast;
+* `frames` mode (throughput; what bench.py measures): frames are independent, rank r renders
+  frames r, r+N, ... with no collective in the data path; `gather_frames` optionally
+  all-gathers finished frames afterwards;
+* `pixels` mode (one frame's latency): the frame's bounding-box ray list is cut into
+  contiguous ranges of whole `chunk`-ray chunks (so the per-chunk NaN fill is exactly the
+  single-GPU one), each rank renders its range, and one all-gather of (rgb, disp, acc)
+  assembles the ray outputs on every rank before composition.  Results are bit-identical to
+  the single-GPU render.
+The render function is injectable (default: the HIP RayCaster) so the sharding and collective
+logic is tested with gloo on CPU.
+"""
+import torch
+import torch.distributed as dist
+
+
+def chunk_ranges(n_rays, chunk, world):
+    """Contiguous [start, stop) ray ranges made of whole chunks, balanced by chunk count."""
+    n_chunks = (n_rays + chunk - 1) // chunk
+    out = []
+    for r in range(world):
+        c0 = (r * n_chunks) // world
+        c1 = ((r + 1) * n_chunks) // world
+        out.append((min(c0 * chunk, n_rays), min(c1 * chunk, n_rays)))
+    return out
+
+
+def frame_ids(n_frames, rank, world):
+    return list(range(rank, n_frames, world))
+
+
+def all_gather_rows(t, group=None):
+    """all_gather of a [n_local, ...] tensor with ragged n_local: pad to the max, gather, trim."""
+    world = dist.get_world_size(group)
+    n = torch.tensor([t.shape[0]], device=t.device, dtype=torch.int64)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n, group=group)
+    sizes = [int(s.item()) for s in sizes]
+    m = max(sizes)
+    pad = torch.zeros((m,) + tuple(t.shape[1:]), device=t.device, dtype=t.dtype)
+    pad[: t.shape[0]] = t
+    bufs = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(bufs, pad, group=group)
+    return torch.cat([b[:s] for b, s in zip(bufs, sizes)], 0)
+
+
+def render_rays_sharded(render_fn, ray_batch, chunk, group=None):
+    """Pixel sharding of one ray list: rank r renders its whole-chunk range, then one all-gather
+    of [rgb(3), disp, acc] per ray.  render_fn(ray_slice) -> dict(rgb_map, disp_map, acc_map)."""
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    n = ray_batch.shape[0]
+    s0, s1 = chunk_ranges(n, chunk, world)[rank]
+    if s1 > s0:
+        out = render_fn(ray_batch[s0:s1])
+        local = torch.cat([out["rgb_map"].reshape(-1, 3), out["disp_map"].reshape(-1, 1),
+                           out["acc_map"].reshape(-1, 1)], -1).contiguous()
+    else:
+        local = torch.zeros(0, 5, device=ray_batch.device, dtype=torch.float32)
+    full = all_gather_rows(local, group)
+    return {"rgb_map": full[:, 0:3], "disp_map": full[:, 3], "acc_map": full[:, 4]}
+
+
+def gather_frames(local_frames, n_frames, group=None):
+    """All-gather per-rank frames ([F_local, H, W, C] tensors) back into frame order."""
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    g = all_gather_rows(local_frames, group)
+    order = [f for r in range(world) for f in frame_ids(n_frames, r, world)]
+    out = torch.empty_like(g)
+    out[torch.tensor(order, device=g.device)] = g
+    return out

@@ -647,3 +647,25 @@ void oracle_raw2outputs(const oracle_model* m, const float* raw, const float* z,
                     weights + i * ns, alpha + i * ns, scratch);
     free(scratch);
 }
+
+/* Stage entry: get_rays (ray_utils.py:6-28) gathered at pixel indices, as render() packs them
+ * (core/trainer.py:116-135): out [n][11] = o, d, near, far, d/|d|. */
+void oracle_gen_rays(const float* c2w /*3x4*/, int H, int W, float fx, float fy, float cx, float cy,
+                     const int64_t* idx, int64_t n, float nearv, float farv, float* out) {
+    (void)H;
+    for (int64_t t = 0; t < n; ++t) {
+        const float x = (float)(idx[t] % W), y = (float)(idx[t] / W);
+        const float d0 = (x - cx) / fx, d1 = -(y - cy) / fy, d2 = -1.0f;
+        float* o = out + t * 11;
+        for (int r = 0; r < 3; ++r) {
+            o[r] = c2w[4 * r + 3];
+            o[3 + r] = (d0 * c2w[4 * r + 0] + d1 * c2w[4 * r + 1]) + d2 * c2w[4 * r + 2];
+        }
+        o[6] = nearv;
+        o[7] = farv;
+        const float nn = norm3_(o[3], o[4], o[5]);
+        o[8] = o[3] / nn;
+        o[9] = o[4] / nn;
+        o[10] = o[5] / nn;
+    }
+}

@@ -47,6 +47,8 @@ def lib():
         L.oracle_render_rays.restype = ctypes.c_int
         L.oracle_near_far.restype = ctypes.c_int64
         L.oracle_feature_dim.restype = ctypes.c_int
+        L.oracle_torch_sum.restype = ctypes.c_float
+        L.oracle_torch_sum_strided.restype = ctypes.c_float
         _lib = L
     return _lib
 
@@ -182,6 +184,21 @@ class OracleModel:
         if with_z:
             out["z"] = z
         return out
+
+
+def gen_rays(c2w, H, W, focal, idx, center=None, near=0.0, far=1.0):
+    """Ray batch [n][11] for pixel indices (oracle_gen_rays)."""
+    c2w = _f32(np.asarray(c2w)[:3, :4])
+    idx = np.ascontiguousarray(idx, dtype=np.int64)
+    out = np.empty((idx.shape[0], 11), np.float32)
+    fa = np.asarray(focal, dtype=np.float64).reshape(-1)
+    fx = float(fa[0])
+    fy = float(fa[1]) if fa.size > 1 else fx
+    cx, cy = (float(W * 0.5), float(H * 0.5)) if center is None else (float(center[0]), float(center[1]))
+    lib().oracle_gen_rays(_p(c2w), H, W, ctypes.c_float(fx), ctypes.c_float(fy), ctypes.c_float(cx),
+                          ctypes.c_float(cy), idx.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                          ctypes.c_int64(idx.shape[0]), ctypes.c_float(near), ctypes.c_float(far), _p(out))
+    return out
 
 
 def linspace(n):

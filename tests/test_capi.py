@@ -1,0 +1,58 @@
+"""CPU: the C-ABI library loads and exports every entry point include/anerf.h declares.
+
+No compute calls are made (no GPU here); argument validation paths that return before any
+HIP call are exercised.
+"""
+import ctypes
+import importlib
+import os
+import re
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+HEADER = os.path.join(os.path.dirname(HERE), "include", "anerf.h")
+_lib = importlib.import_module("a-nerf_amd._lib")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[\w]+\s*\**\s*(anerf_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_header_declares_expected_entry_points():
+    fns = header_functions()
+    for f in ("anerf_model_create", "anerf_render_rays", "anerf_gen_rays", "anerf_near_far", "anerf_compose",
+              "anerf_encode_points", "anerf_workspace_size", "anerf_last_error", "anerf_abi_version"):
+        assert f in fns
+
+
+def test_library_exports_every_header_symbol():
+    lib = _lib.load()
+    for f in header_functions():
+        assert hasattr(lib, f), f"libanerf_hip.so does not export {f}"
+    assert set(header_functions()) == set(_lib.SIGNATURES), "ctypes signatures out of sync with anerf.h"
+
+
+def test_abi_version():
+    src = open(HEADER).read()
+    ver = int(re.search(r"#define ANERF_ABI_VERSION (\d+)", src).group(1))
+    assert _lib.load().anerf_abi_version() == ver
+
+
+def test_invalid_model_desc_is_rejected_with_message():
+    lib = _lib.load()
+    d = _lib.ModelDesc()
+    d.n_joints, d.net_depth, d.net_width, d.multires, d.multires_views = 24, 8, 100, 7, 4
+    h = ctypes.c_void_p()
+    rc = lib.anerf_model_create(ctypes.byref(d), None, None, None, 0, ctypes.byref(h))
+    assert rc == -1
+    assert b"net_width" in lib.anerf_last_error()
+    assert not h.value
+
+
+def test_null_model_render_is_rejected():
+    lib = _lib.load()
+    rc = lib.anerf_render_rays(None, None, 11, 1, None, None, 1, None, None, 64, 0, 4096, 0, None, None, None,
+                               None, None, None, None, None, None, None, 0, None)
+    assert rc == -1
+    assert b"model" in lib.anerf_last_error()

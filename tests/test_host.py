@@ -1,0 +1,89 @@
+"""CPU: host-side logic of the drop-in (integer pixel sets, configuration, synthetic inputs)."""
+import importlib
+import os
+import types
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+rays = importlib.import_module("a-nerf_amd.rays")
+config = importlib.import_module("a-nerf_amd.config")
+syn = importlib.import_module("a-nerf_amd.synthetic")
+
+
+BOXES = np.load(os.path.join(HERE, "golden", "bboxes.npz"))
+
+
+@pytest.mark.parametrize("name", ["c2", "c3", "c4", "c5", "c3_f3"])
+def test_bounding_boxes_bit_exact_vs_reference(name):
+    """kp_to_valid_rays' integer boxes at every config's full size (hazard H2), 3 camera yaws."""
+    H, NJ, seed = (int(x) for x in BOXES[name + "_meta"])
+    sc = syn.make_scene(n_joints=NJ, H=H, W=H, seed=seed, n_frames=3, yaw_step=0.4)
+    idxs, cyls, boxes = rays.valid_pixels(sc["c2ws"], H, H, sc["focal"], kps=sc["kps"], ext_scale=0.001)
+    np.testing.assert_array_equal(cyls, BOXES[name + "_cyls"])
+    np.testing.assert_array_equal(np.stack([b[0] for b in boxes]), BOXES[name + "_tl"])
+    np.testing.assert_array_equal(np.stack([b[1] for b in boxes]), BOXES[name + "_br"])
+    np.testing.assert_array_equal([len(i) for i in idxs], BOXES[name + "_n"])
+    for i, (tl, br) in enumerate(boxes):
+        # exclusive upper bound, clipped to W-1/H-1: the last row/column is never traced
+        assert idxs[i].max() < (H - 1) * H + (H - 1)
+        assert np.all(np.diff(idxs[i]) > 0)
+
+
+def test_box_pixels_row_major_exclusive():
+    idx = rays.box_pixels(np.array([2, 1]), np.array([4, 3]), W=10)
+    np.testing.assert_array_equal(idx, [12, 13, 22, 23])
+    assert rays.box_pixels(np.array([3, 3]), np.array([3, 5]), W=10).size == 0
+
+
+def test_config_rejects_unsupported_flags():
+    cfg = config.RenderConfig
+    with pytest.raises(NotImplementedError):
+        cfg(use_viewdirs=False).validate()
+    with pytest.raises(NotImplementedError):
+        cfg(multires_bones=2).validate()
+    with pytest.raises(NotImplementedError):
+        cfg(extra={"freq_schedule": True}).validate()
+    with pytest.raises(NotImplementedError):
+        cfg(extra={"kp_dist_type": "relpos"}).validate()
+    with pytest.raises(NotImplementedError):
+        cfg(density_type="exp").validate()
+    cfg().validate()
+
+
+def test_config_from_args_matches_surreal_config():
+    args = types.SimpleNamespace(netdepth=8, netwidth=256, multires=7, multires_views=4, use_cutoff=True,
+                                 cutoff_inputs=True, cutoff_viewdir=True, use_viewdirs=True, N_samples=64,
+                                 N_importance=16, chunk=4096, ext_scale=0.001, kp_dist_type="reldist",
+                                 bone_type="reldir", view_type="relray", pts_tr_type="local", density_type="relu",
+                                 opt_framecode=False, framecode_size=16, n_framecodes=None, single_net=False)
+    cfg = config.RenderConfig.from_args(args, 24)
+    assert cfg.feature_dim == 360 + 72 + 648
+    assert config.flops_per_sample(cfg) == 1_723_648
+    cfg.N_importance = 128
+    assert config.flops_per_sample(cfg) * config.samples_per_ray(cfg) == 441_253_888
+
+
+def test_flops_match_survey_table():
+    assert config.flops_per_sample(config.RenderConfig(netdepth=4, netwidth=128)) == 341_632
+    assert config.flops_per_sample(config.RenderConfig(n_joints=65)) == 2_762_752
+
+
+def test_synthetic_weights_are_reproducible():
+    a = syn.make_checkpoint(5, n_joints=24, D=4, W=128)
+    b = syn.make_checkpoint(5, n_joints=24, D=4, W=128)
+    assert syn.checkpoint_sha256(a) == syn.checkpoint_sha256(b)
+    assert a["network_fn_state_dict"]["pts_linears.0.weight"].shape == (128, 432)
+    assert a["network_fn_state_dict"]["views_linears.0.weight"].shape == (64, 128 + 648)
+
+
+def test_synthetic_skeleton_chain_is_rigid():
+    sc = syn.make_scene(n_joints=24, H=64, W=64, seed=3)
+    l2w = np.linalg.inv(sc["skts"][0].astype(np.float64))
+    np.testing.assert_allclose(l2w[:, :3, 3], sc["kps"][0], atol=1e-5)
+    for j in range(1, 24):  # bone lengths preserved
+        p = syn.SMPL_PARENTS[j]
+        a = np.linalg.norm(sc["kps"][0][j] - sc["kps"][0][p])
+        b = np.linalg.norm(syn.REST_POSE_24[j] - syn.REST_POSE_24[p])
+        assert abs(a - b) < 1e-5

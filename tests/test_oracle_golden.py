@@ -1,0 +1,165 @@
+"""CPU: the oracle (oracle/anerf_oracle.c) pinned against the reference's golden outputs.
+
+The fixtures come from running the reference's own Python render path (tests/golden/make_golden.py).
+Stage by stage:
+  ray generation, near/far (incl. the chunk NaN fill), coarse z  -> bit-exact
+  encodings                                                       -> bit-exact (same fma chains as torch)
+  MLP raw outputs                                                 -> 1e-5 relative (MKL sgemm order differs)
+  compositing weights; sample_pdf on the reference's own weights  -> bit-exact / 1e-6
+  final rgb / disp / acc                                          -> 1e-4 absolute
+"""
+import ctypes
+import importlib
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "oracle"))
+
+import oracle  # noqa: E402
+from _golden import Golden, NAMES  # noqa: E402
+
+STAGED = [n for n in NAMES if n.startswith(("c2", "c3", "c4", "fc"))]
+
+
+def _om(g):
+    return oracle.OracleModel(g.cfg, g.ckpt)
+
+
+def test_linspace_matches_torch():
+    for n in list(range(1, 300)) + [512, 1000]:
+        np.testing.assert_array_equal(oracle.linspace(n), torch.linspace(0., 1., n).numpy())
+
+
+def test_torch_sum_emulation_is_bit_exact():
+    L = oracle.lib()
+    rng = np.random.default_rng(7)
+    for n in list(range(1, 260)) + [1000, 4096]:
+        x = (rng.random(n) ** 2 * 10 ** rng.uniform(-5, 2, size=n)).astype(np.float32)
+        got = np.float32(L.oracle_torch_sum(x.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), ctypes.c_int64(n)))
+        assert got == np.float32(torch.from_numpy(x).sum().item()), n
+        X = np.ascontiguousarray(rng.random((1, n, 3)).astype(np.float32))
+        t = torch.from_numpy(X).sum(-2).numpy()[0]
+        for c in range(3):
+            p = ctypes.cast(X.ctypes.data + 4 * c, ctypes.POINTER(ctypes.c_float))
+            assert np.float32(L.oracle_torch_sum_strided(p, ctypes.c_int64(3), ctypes.c_int64(n))) == t[c]
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_ray_generation_matches_reference(name):
+    g = Golden(name)
+    idx = g["valid_idx"][g["sel"]]
+    rb = oracle.gen_rays(g["c2ws"][0], g.meta["H"], g.meta["H"], g.meta["focal"], idx)
+    np.testing.assert_array_equal(rb[:, 0:3], g["rays_o"])
+    np.testing.assert_array_equal(rb[:, 3:6], g["rays_d"])
+
+
+@pytest.mark.parametrize("name", STAGED)
+def test_near_far_and_z_bit_exact(name):
+    g = Golden(name)
+    om = _om(g)
+    rb = g.ray_batch()[:4]
+    near, far, _, _ = om.near_far(rb, g["cyls"][0:1], chunk=4096)
+    np.testing.assert_array_equal(near, g["stage_near"][:, 0])
+    np.testing.assert_array_equal(far, g["stage_far"][:, 0])
+    out = om.render_rays(rb, g["skts"][0], g["cyls"][0:1], cams=g["cams"][:4] if g.has("cams") else None,
+                         N_importance=0, with_z=True)
+    np.testing.assert_array_equal(out["z"], g["stage_z"])
+
+
+def test_nan_fill_chunk_is_exercised():
+    """hazard H1: the h1 fixture's chunk holds rays that miss the cylinder."""
+    g = Golden("h1_nanfill_s32i16_d4w128")
+    near, far, q, filled = _om(g).near_far(g.ray_batch(), g["cyls"][0:1], chunk=4096)
+    assert filled > 0 and filled == int(np.isnan(q).sum())
+    assert not np.isnan(near).any() and not np.isnan(far).any()
+
+
+@pytest.mark.parametrize("name", STAGED)
+def test_encoding_matches_reference(name):
+    g = Golden(name)
+    om = _om(g)
+    rb = g.ray_batch()[:4]
+    z = g["stage_z"][:, :4]
+    pts = (rb[:, None, 0:3] + rb[:, None, 3:6] * z[..., None]).reshape(-1, 3).astype(np.float32)
+    dirs = np.repeat(rb[:, 3:6], 4, axis=0)
+    ref = g["stage_feat"].reshape(16, -1)
+    F = om.feature_dim()
+    got = om.encode(g["skts"][0], pts, dirs)
+    np.testing.assert_allclose(got, ref[:, :F], rtol=0, atol=1e-6)
+
+
+@pytest.mark.parametrize("name", STAGED)
+def test_network_matches_reference(name):
+    g = Golden(name)
+    om = _om(g)
+    rb = g.ray_batch()[:4]
+    z = g["stage_z"]
+    S = z.shape[1]
+    pts = (rb[:, None, 0:3] + rb[:, None, 3:6] * z[..., None]).reshape(-1, 3).astype(np.float32)
+    dirs = np.repeat(rb[:, 3:6], S, axis=0)
+    feat = om.encode(g["skts"][0], pts, dirs)
+    code = None
+    if g.cfg.opt_framecode:
+        codes = g.ckpt["network_fn_state_dict"]["framecodes.codes.weight"]
+        code = np.repeat(codes[g["cams"][:4].astype(np.int64)], S, axis=0)
+    raw = om.network(feat, code=code).reshape(4, S, 4)
+    ref = g["stage_raw"]
+    np.testing.assert_allclose(raw, ref, rtol=0, atol=1e-5 * max(1.0, float(np.abs(ref).max())))
+
+
+@pytest.mark.parametrize("name", STAGED)
+def test_compositing_and_sample_pdf_match_reference(name):
+    g = Golden(name)
+    om = _om(g)
+    rb = g.ray_batch()[:4]
+    r = om.raw2outputs(g["stage_raw"], g["stage_z"], rb[:, 3:6])
+    np.testing.assert_allclose(r["weights"], g["stage_weights"], rtol=0, atol=1e-7)
+    if g.cfg.N_importance > 0:
+        z = g["stage_z"]
+        mids = 0.5 * (z[:, 1:] + z[:, :-1])
+        zis = om.sample_pdf(mids.astype(np.float32), g["stage_weights"][:, 1:-1], g.cfg.N_importance)
+        np.testing.assert_array_equal(zis, g["stage_z_is"])  # same inputs -> same branch -> bit-exact
+        np.testing.assert_array_equal(np.sort(np.concatenate([z, zis], -1), -1), g["stage_z_all"])
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_render_rays_matches_reference(name):
+    g = Golden(name)
+    om = _om(g)
+    out = om.render_rays(g.ray_batch(), g["skts"][0], g["cyls"][0:1], cams=g["cams"] if g.has("cams") else None,
+                         chunk=4096)
+    for k in ("rgb_map", "disp_map", "acc_map", "rgb0", "disp0", "acc0"):
+        if g.has("out_" + k):
+            np.testing.assert_allclose(out[k], g["out_" + k], rtol=0, atol=1e-4, err_msg=k)
+    for k in ("alpha", "alpha0"):
+        if g.has("out_" + k):
+            np.testing.assert_allclose(out[k], g["out_" + k], rtol=0, atol=2e-3, err_msg=k)
+    if g.has("cams_neg"):
+        neg = om.render_rays(g.ray_batch(), g["skts"][0], g["cyls"][0:1], cams=g["cams_neg"], chunk=4096)
+        np.testing.assert_allclose(neg["rgb_map"], g["outneg_rgb_map"], rtol=0, atol=1e-4)
+
+
+def test_render_path_frame_matches_reference():
+    """Config 1 end to end on CPU: host pixel set + oracle rays + render + compose == reference frame."""
+    rays = importlib.import_module("a-nerf_amd.rays")
+    g = Golden("c1_64_s32_d4w128")
+    H, f = g.meta["H"], g.meta["focal"]
+    idxs, cyls, boxes = rays.valid_pixels(g["c2ws"], H, H, f, kps=g["kps"], ext_scale=0.001)
+    np.testing.assert_array_equal(idxs[0], g["valid_idx"])
+    np.testing.assert_array_equal(cyls, g["cyls"])
+    rb = oracle.gen_rays(g["c2ws"][0], H, H, f, idxs[0])
+    out = _om(g).render_rays(rb, g["skts"][0], cyls[0:1], chunk=4096)
+    img = np.zeros((H * H, 3), np.float32)
+    disp = np.zeros(H * H, np.float32)
+    acc = np.zeros(H * H, np.float32)
+    img[idxs[0]] = out["rgb_map"] + (1.0 - out["acc_map"][:, None]) * img[idxs[0]]
+    disp[idxs[0]] = out["disp_map"]
+    acc[idxs[0]] = out["acc_map"]
+    np.testing.assert_allclose(img.reshape(H, H, 3), g["frame_rgb"][0], rtol=0, atol=1e-4)
+    np.testing.assert_allclose(disp.reshape(H, H, 1), g["frame_disp"][0], rtol=0, atol=1e-4)
+    np.testing.assert_allclose(acc.reshape(H, H, 1), g["frame_acc"][0], rtol=0, atol=1e-4)
