@@ -43,7 +43,7 @@ class EmbedParams(ctypes.Structure):
 
 class Debug(ctypes.Structure):
     _fields_ = [("near", c_f), ("far", c_f), ("z_coarse", c_f), ("raw_coarse", c_f), ("weights0", c_f),
-                ("z_fine", c_f), ("raw_fine", c_f)]
+                ("z_fine", c_f), ("raw_fine", c_f), ("mfma_count", ctypes.POINTER(ctypes.c_uint64))]
 
 
 # name -> (restype, argtypes); must cover every entry point of include/anerf.h

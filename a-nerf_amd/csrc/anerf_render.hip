@@ -33,9 +33,11 @@ using namespace anerf;
 
 // ======================================================================= device model
 struct NetDev {
-    const float* wl[MAXL];   // packed layer weights; [0] feature schedule, [i>0] activation (regs) part
+    const float* wl[MAXL];   // packed layer weights; [0] bone-direction part of x, [i>0] activation (regs) part
+    const float* wl0v;       // layer 0, per-joint windowed part of x (dist, sin, cos)
     const float* bl[MAXL];   // packed biases [RB][2][16]
-    const float* wskipx;     // skip layer, x part (feature schedule) or null
+    const float* wskipu;     // skip layer, bone-direction part of x, or null
+    const float* wskipv;     // skip layer, per-joint windowed part of x
     const float* walpha;     // [2][RB][16]
     const float* wfeat;      // packed regs W->W
     const float* bfeat;      // packed bias
@@ -50,7 +52,8 @@ struct NetDev {
 };
 
 struct ModelDev {
-    int nj, njh, ngh, D, skip, mr, mrv, use_cutoff, cutoff_inputs, cutoff_viewdir, cfc, n_codes, softplus;
+    int nj, njh2, ngh, D, skip, mr, mrv, use_cutoff, cutoff_inputs, cutoff_viewdir, cfc, n_codes, softplus;
+    int sparse;  // windowed features are exactly 0 where w == 0 (use_cutoff && cutoff_inputs)
     float shift, B, tau, tau_v;
     const float* cutoff;
     const float* cutoff_v;
@@ -68,6 +71,7 @@ struct RenderArgs {
     const float* far;
     float *rgb, *disp, *acc, *rgb0, *disp0, *acc0, *alpha, *alpha0;
     float *dbg_z0, *dbg_raw0, *dbg_w0, *dbg_z1, *dbg_raw1;
+    unsigned long long* mfma_count;
 };
 
 // ======================================================================= LDS plan
@@ -159,39 +163,38 @@ __device__ __forceinline__ void regs_layer(f32x16 (&acc)[RBO], const f32x16 (&h)
     }
 }
 
-// Features of one (sample, joint): [dist*w, sin(2^f dist)*w, cos(2^f dist)*w (f < MR), u0, u1, u2]
-template <int MR>
-__device__ __forceinline__ void joint_features(const ModelDev& M, const float* __restrict__ S, int j, bool valid,
-                                               float px, float py, float pz, float (&f)[2 * MR + 4]) {
-    float qx = 0.f, qy = 0.f, qz = 0.f;
-    if (valid) joint_local(S, px, py, pz, qx, qy, qz);
-    const float dist = norm3(qx, qy, qz);
-    const float dn = fmaxf(dist, 1e-12f);
-    float w = 1.0f;
-    if (M.use_cutoff) w = valid ? cutoff_w(M.tau, dist, M.cutoff[j]) : 0.0f;
-    f[0] = (M.use_cutoff && M.cutoff_inputs) ? dist * w : dist;
-#pragma unroll
-    for (int fi = 0; fi < MR; ++fi) {
-        float s, c;
-        sincosf(dist * (float)(1 << fi), &s, &c);
-        f[1 + 2 * fi] = s * w;
-        f[2 + 2 * fi] = c * w;
+// The MLP input x = [v (k*NJ + j), r (NJ*NV + 3j + c)] is split into two k-streams:
+//  * the bone-direction part u_j = q_j/|q_j| (never windowed): k-step 3p+c pairs joint p (lane
+//    half 0) with joint p + NJH2 (half 1); this pass also ballots the cutoff window per joint;
+//  * the windowed part of joint j: k-step t pairs sin_t (half 0) with cos_t (half 1), then
+//    (dist, 0); executed only for joints whose window w_j is non-zero for some sample of the
+//    block.  w_j rounds to exactly 0 far from a joint, making those 2*MR+1 inputs exact zeros
+//    whose MFMAs add nothing: skipping them is bit-exact.
+struct JointMask {
+    uint64_t m0, m1;
+};
+
+__device__ __forceinline__ int mask_pop(uint64_t& a0, uint64_t& a1) {
+    if (a0) {
+        const int j = __builtin_ctzll(a0);
+        a0 &= a0 - 1;
+        return j;
     }
-    f[2 * MR + 1] = qx / dn;
-    f[2 * MR + 2] = qy / dn;
-    f[2 * MR + 3] = qz / dn;
+    if (a1) {
+        const int j = 64 + __builtin_ctzll(a1);
+        a1 &= a1 - 1;
+        return j;
+    }
+    return -1;
 }
 
-// acc[RB] += W_x^T * x where x (the 15NJ + 3NJ input features) is generated on the fly:
-// lane half hh encodes joint p + hh*NJh for joint pair p; k-step = p*FPJ + feature index.
-template <int RB, int MR>
-__device__ __forceinline__ void feature_layer(f32x16 (&acc)[RB], const ModelDev& M, const float* __restrict__ wp,
-                                              const float* __restrict__ sk, float px, float py, float pz, int lane) {
-    constexpr int FPJ = 2 * MR + 4;
-    constexpr int NG = FPJ / 2;
-    static_assert(NG % 3 == 0, "feature groups per joint must be a multiple of the ring depth");
+template <int RB>
+__device__ __forceinline__ void u_part(f32x16 (&acc)[RB], const ModelDev& M, const float* __restrict__ wp,
+                                       const float* __restrict__ sk, float px, float py, float pz, int lane,
+                                       JointMask* mask) {
     const int hh = lane >> 5;
-    const int total_groups = M.njh * NG;
+    const int njh2 = M.njh2;
+    const int total_groups = 3 * njh2 / 2;
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(wp);
     const int voff = lane * 8;
     f32x2 ring[3][RB];
@@ -199,15 +202,38 @@ __device__ __forceinline__ void feature_layer(f32x16 (&acc)[RB], const ModelDev&
     for (int g = 0; g < 2; ++g)
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb) ring[g][rb] = bload2(rs, voff, (g * RB + rb) * 512);
-    for (int p = 0; p < M.njh; ++p) {
-        const int j = p + hh * M.njh;
-        const bool valid = j < M.nj;
-        float f[FPJ];
-        joint_features<MR>(M, sk + 12 * (valid ? j : 0), j, valid, px, py, pz, f);
+    uint64_t m0 = 0, m1 = 0;
+    for (int pp = 0; pp < njh2 / 2; ++pp) {
+        float f[6];
 #pragma unroll
-        for (int g = 0; g < NG; ++g) {
+        for (int k = 0; k < 2; ++k) {
+            const int jl = 2 * pp + k;  // joint pair index
+            const int j = jl + hh * njh2;
+            const bool valid = j < M.nj;
+            float qx = 0.f, qy = 0.f, qz = 0.f;
+            if (valid) joint_local(sk + 12 * j, px, py, pz, qx, qy, qz);
+            const float dist = norm3(qx, qy, qz);
+            const float dn = fmaxf(dist, 1e-12f);
+            f[3 * k + 0] = qx / dn;
+            f[3 * k + 1] = qy / dn;
+            f[3 * k + 2] = qz / dn;
+            if (mask) {
+                bool live = valid;
+                if (valid && M.sparse) live = cutoff_w(M.tau, dist, M.cutoff[j]) != 0.0f;
+                const uint64_t b = __ballot(live);
+                const int jb = jl + njh2;
+                if (b & 0xffffffffull) {
+                    if (jl < 64) m0 |= 1ull << jl; else m1 |= 1ull << (jl - 64);
+                }
+                if (b >> 32) {
+                    if (jb < 64) m0 |= 1ull << jb; else m1 |= 1ull << (jb - 64);
+                }
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
             __builtin_amdgcn_sched_barrier(0);
-            const int gn = p * NG + g + 2;
+            const int gn = pp * 3 + g + 2;
             if (gn < total_groups) {
 #pragma unroll
                 for (int rb = 0; rb < RB; ++rb) ring[(g + 2) % 3][rb] = bload2(rs, voff, (gn * RB + rb) * 512);
@@ -219,6 +245,74 @@ __device__ __forceinline__ void feature_layer(f32x16 (&acc)[RB], const ModelDev&
                 for (int rb = 0; rb < RB; ++rb) acc[rb] = mfma_f32_32x32x2(ring[g % 3][rb][t], b, acc[rb]);
             }
         }
+    }
+    if (mask) {
+        mask->m0 = m0;
+        mask->m1 = m1;
+    }
+}
+
+template <int MR>
+struct VPart {
+    static constexpr int KB = ((MR + 1) + 1) & ~1;  // k-steps per joint (even)
+    static constexpr int GB = KB / 2;               // float2 groups per joint
+};
+
+template <int RB, int MR>
+__device__ __forceinline__ void v_part(f32x16 (&acc)[RB], const ModelDev& M, const float* __restrict__ wp,
+                                       const float* __restrict__ sk, float px, float py, float pz, int lane,
+                                       JointMask mask) {
+    constexpr int GB = VPart<MR>::GB;
+    constexpr int KB = VPart<MR>::KB;
+    const int hh = lane >> 5;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(wp);
+    const int voff = lane * 8;
+    uint64_t r0 = mask.m0, r1 = mask.m1;
+    int j = mask_pop(r0, r1);
+    if (j < 0) return;
+    int jn = mask_pop(r0, r1);
+    f32x2 ring[GB][RB];
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) ring[g][rb] = bload2(rs, voff, ((j * GB + g) * RB + rb) * 512);
+    while (j >= 0) {
+        float qx, qy, qz;
+        joint_local(sk + 12 * j, px, py, pz, qx, qy, qz);
+        const float dist = norm3(qx, qy, qz);
+        const float w = M.use_cutoff ? cutoff_w(M.tau, dist, M.cutoff[j]) : 1.0f;
+        float f[KB];
+#pragma unroll
+        for (int t = 0; t < MR; ++t) {
+            float sn, cs;
+            sincosf(dist * (float)(1 << t), &sn, &cs);
+            f[t] = (hh ? cs : sn) * w;
+        }
+        f[MR] = hh ? 0.0f : ((M.use_cutoff && M.cutoff_inputs) ? dist * w : dist);
+#pragma unroll
+        for (int t = MR + 1; t < KB; ++t) f[t] = 0.0f;
+#pragma unroll
+        for (int g = 0; g < GB; ++g) {
+            __builtin_amdgcn_sched_barrier(0);
+            constexpr int PD = 2;
+            if (g + PD < GB) {
+#pragma unroll
+                for (int rb = 0; rb < RB; ++rb)
+                    ring[(g + PD) % GB][rb] = bload2(rs, voff, ((j * GB + g + PD) * RB + rb) * 512);
+            } else if (jn >= 0) {
+#pragma unroll
+                for (int rb = 0; rb < RB; ++rb)
+                    ring[(g + PD) % GB][rb] = bload2(rs, voff, ((jn * GB + g + PD - GB) * RB + rb) * 512);
+            }
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const float b = f[2 * g + t];
+#pragma unroll
+                for (int rb = 0; rb < RB; ++rb) acc[rb] = mfma_f32_32x32x2(ring[g][rb][t], b, acc[rb]);
+            }
+        }
+        j = jn;
+        jn = mask_pop(r0, r1);
     }
 }
 
@@ -250,7 +344,8 @@ __device__ __forceinline__ void view_dir_part(f32x16 (&acc)[RBV], const ModelDev
 template <int W, int MR>
 __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __restrict__ ray,
                           const float* __restrict__ sk, const float* __restrict__ z, int n, int s0,
-                          const float* __restrict__ G, float* __restrict__ raw_out, int lane) {
+                          const float* __restrict__ G, float* __restrict__ raw_out, int lane,
+                          unsigned long long* mfma_count) {
     constexpr int RB = W / 32;
     constexpr int RBV = (W / 2) / 32;
     const int sl = lane & 31, hh = lane >> 5;
@@ -263,16 +358,21 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
     const float pz = ray[2] + ray[5] * zs;
 
     f32x16 acc[RB], h[RB];
+    JointMask mask;
     load_bias<RB>(acc, net.bl[0], hh);
-    feature_layer<RB, MR>(acc, M, net.wl[0], sk, px, py, pz, lane);
+    u_part<RB>(acc, M, net.wl[0], sk, px, py, pz, lane, &mask);
+    v_part<RB, MR>(acc, M, net.wl0v, sk, px, py, pz, lane, mask);
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
         for (int i = 0; i < 16; ++i) h[rb][i] = relu(acc[rb][i]);
     for (int L = 1; L < M.D; ++L) {
         load_bias<RB>(acc, net.bl[L], hh);
-        if (L == M.skip + 1) feature_layer<RB, MR>(acc, M, net.wskipx, sk, px, py, pz, lane);
         regs_layer<RB, RB>(acc, h, net.wl[L], lane);
+        if (L == M.skip + 1) {  // x part after the h part: h is dead, its registers hold the ring
+            u_part<RB>(acc, M, net.wskipu, sk, px, py, pz, lane, nullptr);
+            v_part<RB, MR>(acc, M, net.wskipv, sk, px, py, pz, lane, mask);
+        }
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
@@ -312,6 +412,14 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
         a += __shfl_xor(a, 32);
         rgb[c] = a + net.brgb[c];
     }
+    if (mfma_count && lane == 0) {  // exact MFMA work of this block (wave-uniform quantities)
+        const int act = __builtin_popcountll(mask.m0) + __builtin_popcountll(mask.m1);
+        const int xk = 3 * M.njh2 + act * VPart<MR>::KB;  // k-steps of one x part
+        long long k = (long long)xk * RB + (long long)(M.D - 1) * (W / 2) * RB + (long long)(W / 2) * RB +
+                      (long long)(W / 2) * RBV + (long long)M.ngh * RBV;
+        if (M.skip + 1 < M.D) k += (long long)xk * RB;
+        atomicAdd(mfma_count, (unsigned long long)k);
+    }
     if (hh == 0 && s0 + sl < n) {
         float* o = raw_out + 4 * (s0 + sl);
         o[0] = rgb[0];
@@ -349,34 +457,36 @@ __device__ void compute_view_factor(const ModelDev& M, const NetDev& net, float*
     __syncthreads();
     const int ncol = 2 * M.ngh;
     const int k_first_w = M.cutoff_inputs ? 0 : 1;  // k terms multiplied by w'
-    for (int idx = tid; idx < nr * ncol * WH; idx += blockDim.x) {
-        const int r = idx / (ncol * WH);
-        const int c = (idx / WH) % ncol;
-        const int nn = idx % WH;
+    const int kend = M.cutoff_viewdir ? k_first_w : nk;  // k terms the cutoff does not weight
+    // one thread per (ray, output row n): coalesced reads of the transposed weights
+    for (int idx = tid; idx < nr * WH; idx += blockDim.x) {
+        const int r = idx / WH, nn = idx % WH;
         const float* Tt = lds + P.scr + P.scr_stride * r;
         const float* ray = lds + P.ray + 16 * r;
-        float v = 0.0f;
-        if (c < nj) {
-            if (M.cutoff_viewdir) {
-                for (int k = k_first_w; k < nk; ++k)
-                    for (int cc = 0; cc < 3; ++cc)
-                        v += net.wvdir[((c * nk + k) * 3 + cc) * WH + nn] * Tt[k * 3 * nj + 3 * c + cc];
-            }
-        } else if (c == nj) {
-            v = net.bview[nn];
-            if (M.cfc) {
-                const float cam = ray[6];
-                const int64_t row = cam < 0.0f ? (int64_t)M.n_codes : (int64_t)cam;
-                for (int m = 0; m < M.cfc; ++m) v += net.wvcode[m * WH + nn] * net.codes[row * M.cfc + m];
-            }
-            // terms that the cutoff does not weight
-            const int kend = M.cutoff_viewdir ? k_first_w : nk;
-            for (int j = 0; j < nj; ++j)
-                for (int k = 0; k < kend; ++k)
-                    for (int cc = 0; cc < 3; ++cc)
-                        v += net.wvdir[((j * nk + k) * 3 + cc) * WH + nn] * Tt[k * 3 * nj + 3 * j + cc];
+        float* G = lds + P.g + P.g_stride * r;
+        float bias = net.bview[nn];
+        if (M.cfc) {
+            const float cam = ray[6];
+            const int64_t row = cam < 0.0f ? (int64_t)M.n_codes : (int64_t)cam;
+            for (int m = 0; m < M.cfc; ++m) bias += net.wvcode[m * WH + nn] * net.codes[row * M.cfc + m];
         }
-        lds[P.g + P.g_stride * r + c * WH + nn] = v;
+        for (int c = 0; c < nj; ++c) {
+            const float* wv = net.wvdir + (size_t)c * nk * 3 * WH + nn;
+            const float* tc = Tt + 3 * c;
+            float v = 0.0f;
+            if (M.cutoff_viewdir) {
+                for (int k = k_first_w; k < nk; ++k) {
+                    v += wv[(k * 3 + 0) * WH] * tc[k * 3 * nj + 0];
+                    v += wv[(k * 3 + 1) * WH] * tc[k * 3 * nj + 1];
+                    v += wv[(k * 3 + 2) * WH] * tc[k * 3 * nj + 2];
+                }
+            }
+            for (int k = 0; k < kend; ++k)
+                for (int cc = 0; cc < 3; ++cc) bias += wv[(k * 3 + cc) * WH] * tc[k * 3 * nj + cc];
+            G[c * WH + nn] = v;
+        }
+        G[nj * WH + nn] = bias;
+        for (int c = nj + 1; c < ncol; ++c) G[c * WH + nn] = 0.0f;
     }
     __syncthreads();
 }
@@ -497,14 +607,40 @@ __device__ void importance(const float* zc, const float* w, int S, int I, float*
     __syncthreads();
     const int T = S + I;
     if (active) {
-        for (int e = lane; e < T; e += 64) {  // stable rank sort (values identical to torch.sort)
+        // both lists are normally sorted (z monotone in t, samples monotone in u): merge by binary
+        // search; otherwise a stable O(T^2) rank sort.  Both equal torch.sort's values.
+        bool ok = true;
+        for (int e = lane; e < T; e += 64) {
             const float v = zall[e];
-            int rank = 0;
-            for (int f = 0; f < T; ++f) {
-                const float x = zall[f];
-                rank += z_less(x, v) || (z_eq(x, v) && f < e);
+            if (v != v) ok = false;
+            if (e != 0 && e != S && !(zall[e - 1] <= v)) ok = false;
+        }
+        if (__all(ok)) {
+            const float* zs = zall + S;
+            for (int e = lane; e < T; e += 64) {
+                const float v = zall[e];
+                int lo, hi, rank;
+                if (e < S) {  // coarse sample: after fine samples strictly below it
+                    lo = 0; hi = I;
+                    while (lo < hi) { const int mid = (lo + hi) >> 1; if (zs[mid] < v) lo = mid + 1; else hi = mid; }
+                    rank = e + lo;
+                } else {      // fine sample: after coarse samples <= it
+                    lo = 0; hi = S;
+                    while (lo < hi) { const int mid = (lo + hi) >> 1; if (zall[mid] <= v) lo = mid + 1; else hi = mid; }
+                    rank = (e - S) + lo;
+                }
+                zf[rank] = v;
             }
-            zf[rank] = v;
+        } else {
+            for (int e = lane; e < T; e += 64) {
+                const float v = zall[e];
+                int rank = 0;
+                for (int f = 0; f < T; ++f) {
+                    const float x = zall[f];
+                    rank += z_less(x, v) || (z_eq(x, v) && f < e);
+                }
+                zf[rank] = v;
+            }
         }
     }
     __syncthreads();
@@ -560,7 +696,7 @@ __global__ __launch_bounds__(256, 1) void render_kernel(ModelDev M, RenderArgs A
             const int r = b / nb, s0 = (b % nb) * 32;
             mlp_block<W, MR>(M, net, lds + P.ray + 16 * r, lds + P.sk + P.sk_stride * r,
                              lds + zoff + P.z_stride * r, n, s0, lds + P.g + P.g_stride * r,
-                             lds + P.raw + P.raw_stride * r, lane);
+                             lds + P.raw + P.raw_stride * r, lane, A.mfma_count);
         }
         __syncthreads();
         // ---- composite (+ importance sampling after the coarse pass); one wave per ray
@@ -817,14 +953,30 @@ std::vector<float> pack_regs(const float* Wt, int n_out, int ld, int col_off, in
     });
 }
 
-std::vector<float> pack_features(const float* Wt, int n_out, int ld, int nj, int njh, int mr) {
-    const int nv = 1 + 2 * mr, fpj = nv + 3;
-    return pack_kmajor(Wt, n_out, ld, njh * fpj, [&](int q, int h) {
-        const int p = q / fpj, t = q % fpj;
-        const int j = p + h * njh;
-        if (j >= nj) return -1;
-        return t < nv ? t * nj + j : nv * nj + 3 * j + (t - nv);
+// bone-direction part: k-step q = 3p + c, half h -> joint p + h*njh2, column nv*nj + 3j + c
+std::vector<float> pack_upart(const float* Wt, int n_out, int ld, int nj, int njh2, int mr) {
+    const int nv = 1 + 2 * mr;
+    return pack_kmajor(Wt, n_out, ld, 3 * njh2, [&](int q, int h) {
+        const int p = q / 3, c = q % 3;
+        const int j = p + h * njh2;
+        return j < nj ? nv * nj + 3 * j + c : -1;
     });
+}
+
+// windowed part, per joint j: k-step t < mr -> (sin_t, cos_t) = columns ((1+2t)NJ + j, (2+2t)NJ + j);
+// t == mr -> (dist, pad); padded to an even count.  Layout [joint][group][RB][64][2].
+std::vector<float> pack_vpart(const float* Wt, int n_out, int ld, int nj, int mr) {
+    const int kb = ((mr + 1) + 1) & ~1;
+    std::vector<float> out;
+    for (int j = 0; j < nj; ++j) {
+        std::vector<float> pj = pack_kmajor(Wt, n_out, ld, kb, [&](int t, int h) {
+            if (t < mr) return (1 + 2 * t + h) * nj + j;
+            if (t == mr && h == 0) return j;
+            return -1;
+        });
+        out.insert(out.end(), pj.begin(), pj.end());
+    }
+    return out;
 }
 
 // per-lane-half vectors [rb][h][16] of a length-n vector in accumulator row order
@@ -845,7 +997,7 @@ std::vector<float> pack_rowvec(const float* v, int n, bool half_major) {
 struct anerf_model {
     anerf_model_desc desc;
     int device;
-    int njh, ngh;
+    int njh2, ngh;
     float* dev_buf;
     size_t dev_bytes;
     ModelDev md;
@@ -903,7 +1055,7 @@ static int validate_desc(const anerf_model_desc* d) {
     return ANERF_OK;
 }
 
-static int pack_net(const anerf_model_desc* d, int njh, const anerf_net_weights* w, Packer& pk,
+static int pack_net(const anerf_model_desc* d, int njh2, const anerf_net_weights* w, Packer& pk,
                     std::vector<size_t>& offs) {
     const int W = d->net_width, WH = W / 2, nj = d->n_joints, mr = d->multires, mrv = d->multires_views;
     const int cin = nj * (1 + 2 * mr) + 3 * nj;
@@ -917,15 +1069,22 @@ static int pack_net(const anerf_model_desc* d, int njh, const anerf_net_weights*
         return fail(ANERF_EINVAL, "missing head weight");
     if (cfc && !w->codes) return fail(ANERF_EINVAL, "framecode weights missing");
     offs.clear();
-    // [0] layer 0 (features), [1..D-1] activation parts, [D] skip x part, [D+1..2D] biases
-    offs.push_back(pk.add(pack_features(w->pts_w[0], W, cin, nj, njh, mr)));
+    // [0] layer 0 u part, [1..D-1] activation parts, [D] layer 0 v part, [D+1, D+2] skip u / v parts,
+    // [D+3 ..] biases
+    offs.push_back(pk.add(pack_upart(w->pts_w[0], W, cin, nj, njh2, mr)));
     for (int i = 1; i < d->net_depth; ++i) {
         const bool sk = (i == d->skip + 1);
         offs.push_back(pk.add(pack_regs(w->pts_w[i], W, sk ? cin + W : W, sk ? cin : 0, W)));
     }
+    offs.push_back(pk.add(pack_vpart(w->pts_w[0], W, cin, nj, mr)));
     const int skl = d->skip + 1;
-    if (skl < d->net_depth) offs.push_back(pk.add(pack_features(w->pts_w[skl], W, cin + W, nj, njh, mr)));
-    else offs.push_back((size_t)-1);
+    if (skl < d->net_depth) {
+        offs.push_back(pk.add(pack_upart(w->pts_w[skl], W, cin + W, nj, njh2, mr)));
+        offs.push_back(pk.add(pack_vpart(w->pts_w[skl], W, cin + W, nj, mr)));
+    } else {
+        offs.push_back((size_t)-1);
+        offs.push_back((size_t)-1);
+    }
     for (int i = 0; i < d->net_depth; ++i) offs.push_back(pk.add(pack_rowvec(w->pts_b[i], W, false)));
     offs.push_back(pk.add(pack_rowvec(w->alpha_w, W, true)));                         // walpha
     offs.push_back(pk.add(pack_regs(w->feature_w, W, W, 0, W)));                      // wfeat
@@ -979,7 +1138,10 @@ static void bind_net(const anerf_model_desc* d, const float* base, const std::ve
     size_t k = 0;
     nd.wl[0] = base + o[k++];
     for (int i = 1; i < D; ++i) nd.wl[i] = base + o[k++];
-    nd.wskipx = o[k] == (size_t)-1 ? nullptr : base + o[k];
+    nd.wl0v = base + o[k++];
+    nd.wskipu = o[k] == (size_t)-1 ? nullptr : base + o[k];
+    ++k;
+    nd.wskipv = o[k] == (size_t)-1 ? nullptr : base + o[k];
     ++k;
     for (int i = 0; i < D; ++i) nd.bl[i] = base + o[k++];
     nd.walpha = base + o[k++];
@@ -1011,14 +1173,14 @@ int anerf_model_create(const anerf_model_desc* desc, const anerf_net_weights* co
     if (desc->has_fine && !fine) return fail(ANERF_EINVAL, "has_fine but fine weights are NULL");
     if (!embed->cutoff_dist || !embed->cutoff_dist_v) return fail(ANERF_EINVAL, "cutoff_dist is NULL");
     const int nj = desc->n_joints;
-    const int njh = (nj + 1) / 2;
-    const int ngh = (nj + 2) / 2;  // NJ + 1 columns split over two lane halves
+    const int njh2 = (((nj + 1) / 2) + 1) & ~1;  // joint pairs of the u part, even
+    const int ngh = (nj + 2) / 2;                   // NJ + 1 view columns split over two lane halves
     Packer pk;
     std::vector<size_t> oc, of;
-    rc = pack_net(desc, njh, coarse, pk, oc);
+    rc = pack_net(desc, njh2, coarse, pk, oc);
     if (rc) return rc;
     if (desc->has_fine) {
-        rc = pack_net(desc, njh, fine, pk, of);
+        rc = pack_net(desc, njh2, fine, pk, of);
         if (rc) return rc;
     }
     const size_t off_cut = pk.add(std::vector<float>(embed->cutoff_dist, embed->cutoff_dist + nj));
@@ -1039,14 +1201,15 @@ int anerf_model_create(const anerf_model_desc* desc, const anerf_net_weights* co
     anerf_model* m = new anerf_model();
     m->desc = *desc;
     m->device = device;
-    m->njh = njh;
+    m->njh2 = njh2;
     m->ngh = ngh;
     m->dev_buf = dbuf;
     m->dev_bytes = bytes;
     ModelDev& md = m->md;
     std::memset(&md, 0, sizeof(md));
     md.nj = nj;
-    md.njh = njh;
+    md.njh2 = njh2;
+    md.sparse = desc->use_cutoff && desc->cutoff_inputs;
     md.ngh = ngh;
     md.D = desc->net_depth;
     md.skip = desc->skip;
@@ -1198,6 +1361,7 @@ int anerf_render_rays(const anerf_model* m, const float* ray_batch, int32_t ray_
         a.dbg_w0 = debug->weights0;
         a.dbg_z1 = debug->z_fine;
         a.dbg_raw1 = debug->raw_fine;
+        a.mfma_count = debug->mfma_count;
     }
     const unsigned grid = (unsigned)((n_rays + R - 1) / R);
     const size_t lds_bytes = (size_t)P.total * 4;

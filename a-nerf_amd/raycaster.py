@@ -71,7 +71,8 @@ class RayCaster:
     def render_rays(self, ray_batch, N_samples, kp_batch=None, skts=None, cyls=None, bones=None, cams=None,
                     subject_idxs=None, retraw=False, lindisp=False, perturb=0., N_importance=0, network_fine=None,
                     raw_noise_std=0., ray_noise_std=0., verbose=False, ext_scale=0.001, pytest=False,
-                    preproc_kwargs=None, nerf_type="nerf", chunk=None, debug=False, ret_alpha=True):
+                    preproc_kwargs=None, nerf_type="nerf", chunk=None, debug=False, ret_alpha=True,
+                    count_mfma=False):
         """Same arguments and output dict as core/raycasters.py:361-474.
 
         `chunk` (extension): NaN-fill granularity; the reference fills per render_rays call,
@@ -121,13 +122,17 @@ class RayCaster:
             out.update(rgb0=torch.empty(n, 3, **f32), disp0=torch.empty(n, **f32), acc0=torch.empty(n, **f32),
                        alpha0=torch.empty(n, S, **f32) if ret_alpha else None)
         dbg = None
+        if debug or count_mfma:
+            dbg = _lib.Debug()
+        if count_mfma:
+            self.last_mfma = torch.zeros(1, device=dev, dtype=torch.int64)
+            dbg.mfma_count = ctypes.cast(self.last_mfma.data_ptr(), ctypes.POINTER(ctypes.c_uint64))
         if debug:
             dd = {"near": torch.empty(n, **f32), "far": torch.empty(n, **f32), "z_coarse": torch.empty(n, S, **f32),
                   "raw_coarse": torch.empty(n, S, 4, **f32)}
             if I > 0:
                 dd.update(weights0=torch.empty(n, S, **f32), z_fine=torch.empty(n, T, **f32),
                           raw_fine=torch.empty(n, T, 4, **f32))
-            dbg = _lib.Debug()
             for k, v in dd.items():
                 setattr(dbg, k, ctypes.cast(v.data_ptr(), _lib.c_f))
             self.last_debug = dd

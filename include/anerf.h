@@ -94,6 +94,7 @@ typedef struct {
     float* weights0;  /* [N][S] */
     float* z_fine;    /* [N][S+I] sorted merged samples */
     float* raw_fine;  /* [N][S+I][4] */
+    unsigned long long* mfma_count; /* [1] += v_mfma_f32_32x32x2_f32 instructions issued (work counter) */
 } anerf_debug;
 
 int anerf_abi_version(void);
