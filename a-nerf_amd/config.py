@@ -48,8 +48,8 @@ class RenderConfig:
             raise NotImplementedError(f"netwidth={self.netwidth}: multiples of 64 up to 256 are supported")
         if self.netdepth < 2 or self.netdepth > 16:
             raise NotImplementedError(f"netdepth={self.netdepth} outside [2, 16]")
-        if self.multires < 1 or self.multires > 10 or self.multires_views < 1 or self.multires_views > 10:
-            raise NotImplementedError("multires / multires_views must be in [1, 10]")
+        if self.multires not in (7, 10) or self.multires_views != 4:
+            raise NotImplementedError("kernel instances exist for multires in {7, 10} and multires_views == 4")
         if self.density_type not in ("relu", "softplus"):
             raise NotImplementedError(f"density activation {self.density_type} is undefined")
         if self.opt_framecode and self.n_framecodes <= 0:

@@ -29,6 +29,38 @@
 
 using namespace anerf;
 
+// Diagnostic build only (-DANERF_STAMPS): per-phase shader-cycle totals, summed over waves into
+// RenderArgs::stamps[16]; read only by tools/stamps.py, never part of an output.
+struct Stamps {
+#ifdef ANERF_STAMPS
+    unsigned long long last, acc[16];
+#endif
+};
+#ifdef ANERF_STAMPS
+#define STAMP_INIT(st)                                      \
+    do {                                                    \
+        (st).last = __builtin_amdgcn_s_memtime();           \
+        for (int i_ = 0; i_ < 16; ++i_) (st).acc[i_] = 0;   \
+    } while (0)
+#define STAMP(st, i)                                                      \
+    do {                                                                  \
+        __builtin_amdgcn_sched_barrier(0);                                \
+        const unsigned long long now_ = __builtin_amdgcn_s_memtime();     \
+        (st).acc[i] += now_ - (st).last;                                  \
+        (st).last = now_;                                                 \
+        __builtin_amdgcn_sched_barrier(0);                                \
+    } while (0)
+#define STAMP_FLUSH(st, ptr)                                              \
+    do {                                                                  \
+        if ((threadIdx.x & 63) == 0 && (ptr))                             \
+            for (int i_ = 0; i_ < 16; ++i_) atomicAdd((ptr) + i_, (st).acc[i_]); \
+    } while (0)
+#else
+#define STAMP_INIT(st) do { } while (0)
+#define STAMP(st, i) do { } while (0)
+#define STAMP_FLUSH(st, ptr) do { } while (0)
+#endif
+
 #define MAXL 16
 
 // ======================================================================= device model
@@ -72,18 +104,19 @@ struct RenderArgs {
     float *rgb, *disp, *acc, *rgb0, *disp0, *acc0, *alpha, *alpha0;
     float *dbg_z0, *dbg_raw0, *dbg_w0, *dbg_z1, *dbg_raw1;
     unsigned long long* mfma_count;
+    unsigned long long* stamps;
 };
 
 // ======================================================================= LDS plan
 struct LdsPlan {
-    int ray, sk, zc, zf, raw, g, scr;  // float offsets
+    int ray, sk, zc, zf, raw, g, scr, bias;  // float offsets
     int total;                          // floats
     int sk_stride, z_stride, raw_stride, g_stride, scr_stride;
 };
 
 __host__ __device__ inline int pad32(int x) { return (x + 31) & ~31; }
 
-__host__ __device__ inline LdsPlan make_plan(int R, int nj, int W, int S, int T, int mrv, int ngh) {
+__host__ __device__ inline LdsPlan make_plan(int R, int nj, int W, int S, int T, int mrv, int ngh, int D) {
     LdsPlan p;
     const int wh = W / 2;
     const int nk = 1 + 2 * mrv;
@@ -92,7 +125,7 @@ __host__ __device__ inline LdsPlan make_plan(int R, int nj, int W, int S, int T,
     p.raw_stride = p.z_stride * 4;
     p.g_stride = 2 * ngh * wh;
     int scr_a = 8 * p.z_stride;          // composite / importance scratch
-    int scr_b = nk * 3 * nj;             // trig table for G
+    int scr_b = nk * 3 * nj + 256;  // trig table for G + per-part bias partials (256 / WH parts x WH)
     p.scr_stride = (scr_a > scr_b ? scr_a : scr_b);
     int o = 0;
     p.ray = o; o += 16 * R;
@@ -102,6 +135,8 @@ __host__ __device__ inline LdsPlan make_plan(int R, int nj, int W, int S, int T,
     p.raw = o; o += p.raw_stride * R;
     p.g = o; o += p.g_stride * R;
     p.scr = o; o += p.scr_stride * R;
+    o = (o + 3) & ~3;
+    p.bias = o; o += (D + 1) * W;  // the current net's hidden + feature biases, accumulator order
     p.total = (o + 3) & ~3;
     return p;
 }
@@ -120,45 +155,61 @@ __device__ __forceinline__ f32x4 bload4(__amdgpu_buffer_rsrc_t rs, int voff, int
 }
 
 template <int RB>
-__device__ __forceinline__ void load_bias(f32x16 (&acc)[RB], const float* __restrict__ bp, int hh) {
-    const __amdgpu_buffer_rsrc_t rs = make_rsrc(bp);
-    const int voff = hh * 64;
+__device__ __forceinline__ void load_bias(f32x16 (&acc)[RB], const float* __restrict__ bp_lds, int hh) {
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) {
-        f32x4 v0 = bload4(rs, voff, rb * 128 + 0), v1 = bload4(rs, voff, rb * 128 + 16);
-        f32x4 v2 = bload4(rs, voff, rb * 128 + 32), v3 = bload4(rs, voff, rb * 128 + 48);
+        const f32x4* p = reinterpret_cast<const f32x4*>(bp_lds + (rb * 2 + hh) * 16);
+        f32x4 v0 = p[0], v1 = p[1], v2 = p[2], v3 = p[3];
         acc[rb] = f32x16{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3],
                          v2[0], v2[1], v2[2], v2[3], v3[0], v3[1], v3[2], v3[3]};
     }
 }
 
 // acc[RBO] += W^T * h  over the RBI*32 activations held in h (k-steps in accumulator order).
-// Weights packed [group = q/2][RBO][64 lanes][2]; 3-slot register ring, prefetch distance 2.
-template <int RBO, int RBI>
-__device__ __forceinline__ void regs_layer(f32x16 (&acc)[RBO], const f32x16 (&h)[RBI], const float* __restrict__ wp,
-                                           int lane) {
-    constexpr int NG = 8 * RBI;
+// Weights packed [group = q/2][RBO][64 lanes][2].  The 4-slot register ring is shared by
+// consecutive activation layers: group g lives in slot g % 4 (NG is a multiple of 4), the
+// prefetch distance is 2 groups, and the last two groups of a layer prefetch groups 0 and 1 of
+// `next` (RBN row blocks) so the next layer starts without a load bubble.
+template <int RB>
+struct Ring {
+    f32x2 s[4][RB];
+};
+
+template <int RBO, int RB>
+__device__ __forceinline__ void ring_preload(Ring<RB>& ring, const float* __restrict__ wp, int lane) {
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(wp);
-    const int voff = lane * 8;
-    f32x2 ring[3][RBO];
 #pragma unroll
     for (int g = 0; g < 2; ++g)
 #pragma unroll
-        for (int rb = 0; rb < RBO; ++rb) ring[g][rb] = bload2(rs, voff, (g * RBO + rb) * 512);
+        for (int rb = 0; rb < RBO; ++rb) ring.s[g][rb] = bload2(rs, lane * 8, (g * RBO + rb) * 512);
+}
+
+template <int RBO, int RBI, int RBN, int RB>
+__device__ __forceinline__ void regs_layer(f32x16 (&acc)[RBO], const f32x16 (&h)[RBI], const float* __restrict__ wp,
+                                           int lane, Ring<RB>& ring, const float* __restrict__ next) {
+    constexpr int NG = 8 * RBI;
+    static_assert(NG % 4 == 0, "ring slot alignment");
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(wp);
+    const __amdgpu_buffer_rsrc_t rn = make_rsrc(next);
+    const int voff = lane * 8;
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
-        // keep the ring three groups deep: no load crosses a group boundary
+        // keep the ring four groups deep: no load crosses a group boundary
         __builtin_amdgcn_sched_barrier(0);
         if (g + 2 < NG) {
 #pragma unroll
-            for (int rb = 0; rb < RBO; ++rb) ring[(g + 2) % 3][rb] = bload2(rs, voff, ((g + 2) * RBO + rb) * 512);
+            for (int rb = 0; rb < RBO; ++rb) ring.s[(g + 2) % 4][rb] = bload2(rs, voff, ((g + 2) * RBO + rb) * 512);
+        } else if (next) {
+#pragma unroll
+            for (int rb = 0; rb < RBN; ++rb)
+                ring.s[(g + 2) % 4][rb] = bload2(rn, voff, ((g + 2 - NG) * RBN + rb) * 512);
         }
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
             const int q = 2 * g + t;
             const float b = h[q >> 4][q & 15];
 #pragma unroll
-            for (int rb = 0; rb < RBO; ++rb) acc[rb] = mfma_f32_32x32x2(ring[g % 3][rb][t], b, acc[rb]);
+            for (int rb = 0; rb < RBO; ++rb) acc[rb] = mfma_f32_32x32x2(ring.s[g % 4][rb][t], b, acc[rb]);
         }
     }
 }
@@ -188,13 +239,31 @@ __device__ __forceinline__ int mask_pop(uint64_t& a0, uint64_t& a1) {
     return -1;
 }
 
+// bone direction u_j of this lane's sample, and whether its cutoff window is non-zero
+__device__ __forceinline__ void u_joint(const ModelDev& M, const float* __restrict__ sk, int j, float px, float py,
+                                        float pz, float& u0, float& u1, float& u2, bool& live) {
+    const bool valid = j < M.nj;
+    float qx = 0.f, qy = 0.f, qz = 0.f;
+    if (valid) joint_local(sk + 12 * j, px, py, pz, qx, qy, qz);
+    const float dist = norm3(qx, qy, qz);
+    const float dn = fmaxf(dist, 1e-12f);
+    u0 = qx / dn;
+    u1 = qy / dn;
+    u2 = qz / dn;
+    live = valid;
+    if (valid && M.sparse) live = cutoff_w(M.tau, dist, M.cutoff[j]) != 0.0f;
+}
+
+// The geometry of pair-of-pairs pp+1 is computed under the MFMAs of pp (software pipeline:
+// between two sched_barriers the scheduler interleaves the VALU with the async MFMAs).
 template <int RB>
 __device__ __forceinline__ void u_part(f32x16 (&acc)[RB], const ModelDev& M, const float* __restrict__ wp,
                                        const float* __restrict__ sk, float px, float py, float pz, int lane,
                                        JointMask* mask) {
     const int hh = lane >> 5;
     const int njh2 = M.njh2;
-    const int total_groups = 3 * njh2 / 2;
+    const int npp = njh2 / 2;
+    const int total_groups = 3 * npp;
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(wp);
     const int voff = lane * 8;
     f32x2 ring[3][RB];
@@ -203,33 +272,26 @@ __device__ __forceinline__ void u_part(f32x16 (&acc)[RB], const ModelDev& M, con
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb) ring[g][rb] = bload2(rs, voff, (g * RB + rb) * 512);
     uint64_t m0 = 0, m1 = 0;
-    for (int pp = 0; pp < njh2 / 2; ++pp) {
-        float f[6];
+    float f[6];
+    bool lv0, lv1;
+    u_joint(M, sk, 0 + hh * njh2, px, py, pz, f[0], f[1], f[2], lv0);
+    u_joint(M, sk, 1 + hh * njh2, px, py, pz, f[3], f[4], f[5], lv1);
+    for (int pp = 0; pp < npp; ++pp) {
+        if (mask) {
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const int jl = 2 * pp + k;  // joint pair index
-            const int j = jl + hh * njh2;
-            const bool valid = j < M.nj;
-            float qx = 0.f, qy = 0.f, qz = 0.f;
-            if (valid) joint_local(sk + 12 * j, px, py, pz, qx, qy, qz);
-            const float dist = norm3(qx, qy, qz);
-            const float dn = fmaxf(dist, 1e-12f);
-            f[3 * k + 0] = qx / dn;
-            f[3 * k + 1] = qy / dn;
-            f[3 * k + 2] = qz / dn;
-            if (mask) {
-                bool live = valid;
-                if (valid && M.sparse) live = cutoff_w(M.tau, dist, M.cutoff[j]) != 0.0f;
-                const uint64_t b = __ballot(live);
-                const int jb = jl + njh2;
+            for (int k = 0; k < 2; ++k) {
+                const uint64_t b = __ballot(k == 0 ? lv0 : lv1);
+                const int ja = 2 * pp + k, jb = ja + njh2;
                 if (b & 0xffffffffull) {
-                    if (jl < 64) m0 |= 1ull << jl; else m1 |= 1ull << (jl - 64);
+                    if (ja < 64) m0 |= 1ull << ja; else m1 |= 1ull << (ja - 64);
                 }
                 if (b >> 32) {
                     if (jb < 64) m0 |= 1ull << jb; else m1 |= 1ull << (jb - 64);
                 }
             }
         }
+        float fn[6];
+        bool ln0 = false, ln1 = false;
 #pragma unroll
         for (int g = 0; g < 3; ++g) {
             __builtin_amdgcn_sched_barrier(0);
@@ -244,7 +306,13 @@ __device__ __forceinline__ void u_part(f32x16 (&acc)[RB], const ModelDev& M, con
 #pragma unroll
                 for (int rb = 0; rb < RB; ++rb) acc[rb] = mfma_f32_32x32x2(ring[g % 3][rb][t], b, acc[rb]);
             }
+            if (g == 0) u_joint(M, sk, 2 * pp + 2 + hh * njh2, px, py, pz, fn[0], fn[1], fn[2], ln0);
+            if (g == 1) u_joint(M, sk, 2 * pp + 3 + hh * njh2, px, py, pz, fn[3], fn[4], fn[5], ln1);
         }
+#pragma unroll
+        for (int i = 0; i < 6; ++i) f[i] = fn[i];
+        lv0 = ln0;
+        lv1 = ln1;
     }
     if (mask) {
         mask->m0 = m0;
@@ -258,15 +326,25 @@ struct VPart {
     static constexpr int GB = KB / 2;               // float2 groups per joint
 };
 
+__device__ __forceinline__ void v_geom(const ModelDev& M, const float* __restrict__ sk, int j, float px, float py,
+                                       float pz, float& dist, float& w) {
+    float qx, qy, qz;
+    joint_local(sk + 12 * j, px, py, pz, qx, qy, qz);
+    dist = norm3(qx, qy, qz);
+    w = M.use_cutoff ? cutoff_w(M.tau, dist, M.cutoff[j]) : 1.0f;
+}
+
 template <int RB, int MR>
 __device__ __forceinline__ void v_part(f32x16 (&acc)[RB], const ModelDev& M, const float* __restrict__ wp,
                                        const float* __restrict__ sk, float px, float py, float pz, int lane,
                                        JointMask mask) {
     constexpr int GB = VPart<MR>::GB;
     constexpr int KB = VPart<MR>::KB;
+    constexpr int PER = (MR + GB - 2) / (GB - 1);  // sin/cos terms of the next joint per group 1..GB-1
     const int hh = lane >> 5;
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(wp);
     const int voff = lane * 8;
+    const bool dist_in = M.use_cutoff && M.cutoff_inputs;
     uint64_t r0 = mask.m0, r1 = mask.m1;
     int j = mask_pop(r0, r1);
     if (j < 0) return;
@@ -276,21 +354,24 @@ __device__ __forceinline__ void v_part(f32x16 (&acc)[RB], const ModelDev& M, con
     for (int g = 0; g < 2; ++g)
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb) ring[g][rb] = bload2(rs, voff, ((j * GB + g) * RB + rb) * 512);
-    while (j >= 0) {
-        float qx, qy, qz;
-        joint_local(sk + 12 * j, px, py, pz, qx, qy, qz);
-        const float dist = norm3(qx, qy, qz);
-        const float w = M.use_cutoff ? cutoff_w(M.tau, dist, M.cutoff[j]) : 1.0f;
-        float f[KB];
+    float f[KB];
+    {
+        float dist, w;
+        v_geom(M, sk, j, px, py, pz, dist, w);
 #pragma unroll
         for (int t = 0; t < MR; ++t) {
             float sn, cs;
             sincosf(dist * (float)(1 << t), &sn, &cs);
             f[t] = (hh ? cs : sn) * w;
         }
-        f[MR] = hh ? 0.0f : ((M.use_cutoff && M.cutoff_inputs) ? dist * w : dist);
+        f[MR] = hh ? 0.0f : (dist_in ? dist * w : dist);
 #pragma unroll
         for (int t = MR + 1; t < KB; ++t) f[t] = 0.0f;
+    }
+    while (j >= 0) {
+        float fn[KB];
+        float dn = 0.0f, wn = 0.0f;
+        const int jg = jn >= 0 ? jn : j;  // geometry of the next joint (harmless redo at the end)
 #pragma unroll
         for (int g = 0; g < GB; ++g) {
             __builtin_amdgcn_sched_barrier(0);
@@ -310,7 +391,23 @@ __device__ __forceinline__ void v_part(f32x16 (&acc)[RB], const ModelDev& M, con
 #pragma unroll
                 for (int rb = 0; rb < RB; ++rb) acc[rb] = mfma_f32_32x32x2(ring[g][rb][t], b, acc[rb]);
             }
+            // next joint's features under these MFMAs
+            if (g == 0) {
+                v_geom(M, sk, jg, px, py, pz, dn, wn);
+            } else {
+#pragma unroll
+                for (int t = (g - 1) * PER; t < g * PER && t < MR; ++t) {
+                    float sn, cs;
+                    sincosf(dn * (float)(1 << t), &sn, &cs);
+                    fn[t] = (hh ? cs : sn) * wn;
+                }
+            }
         }
+        fn[MR] = hh ? 0.0f : (dist_in ? dn * wn : dn);
+#pragma unroll
+        for (int t = MR + 1; t < KB; ++t) fn[t] = 0.0f;
+#pragma unroll
+        for (int t = 0; t < KB; ++t) f[t] = fn[t];
         j = jn;
         jn = mask_pop(r0, r1);
     }
@@ -345,7 +442,7 @@ template <int W, int MR>
 __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __restrict__ ray,
                           const float* __restrict__ sk, const float* __restrict__ z, int n, int s0,
                           const float* __restrict__ G, float* __restrict__ raw_out, int lane,
-                          unsigned long long* mfma_count) {
+                          unsigned long long* mfma_count, const float* __restrict__ bias, Stamps& st) {
     constexpr int RB = W / 32;
     constexpr int RBV = (W / 2) / 32;
     const int sl = lane & 31, hh = lane >> 5;
@@ -359,25 +456,34 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
 
     f32x16 acc[RB], h[RB];
     JointMask mask;
-    load_bias<RB>(acc, net.bl[0], hh);
+    Ring<RB> ring;
+    if (M.D > 1) ring_preload<RB, RB>(ring, net.wl[1], lane);  // layer 1's first groups, early
+    load_bias<RB>(acc, bias, hh);
+    STAMP(st, 10);
     u_part<RB>(acc, M, net.wl[0], sk, px, py, pz, lane, &mask);
+    STAMP(st, 8);
     v_part<RB, MR>(acc, M, net.wl0v, sk, px, py, pz, lane, mask);
+    STAMP(st, 9);
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
         for (int i = 0; i < 16; ++i) h[rb][i] = relu(acc[rb][i]);
     for (int L = 1; L < M.D; ++L) {
-        load_bias<RB>(acc, net.bl[L], hh);
-        regs_layer<RB, RB>(acc, h, net.wl[L], lane);
+        load_bias<RB>(acc, bias + L * W, hh);
+        STAMP(st, 10);
+        regs_layer<RB, RB, RB>(acc, h, net.wl[L], lane, ring, L + 1 < M.D ? net.wl[L + 1] : net.wfeat);
+        STAMP(st, 11);
         if (L == M.skip + 1) {  // x part after the h part: h is dead, its registers hold the ring
             u_part<RB>(acc, M, net.wskipu, sk, px, py, pz, lane, nullptr);
             v_part<RB, MR>(acc, M, net.wskipv, sk, px, py, pz, lane, mask);
+            STAMP(st, 12);
         }
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
             for (int i = 0; i < 16; ++i) h[rb][i] = relu(acc[rb][i]);
     }
+    STAMP(st, 10);
     // alpha head (VALU): this lane holds half of the W activations of sample sl
     float sig = 0.0f;
     {
@@ -390,15 +496,15 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
         sig += net.balpha;
     }
     // feature_linear (no activation)
-    load_bias<RB>(acc, net.bfeat, hh);
-    regs_layer<RB, RB>(acc, h, net.wfeat, lane);
+    load_bias<RB>(acc, bias + M.D * W, hh);
+    regs_layer<RB, RB, RBV>(acc, h, net.wfeat, lane, ring, net.wview);
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) h[rb] = acc[rb];
     // views_linears.0: feature part + factorised direction/code/bias part, then relu
     f32x16 av[RBV];
 #pragma unroll
     for (int rb = 0; rb < RBV; ++rb) av[rb] = f32x16{0};
-    regs_layer<RBV, RB>(av, h, net.wview, lane);
+    regs_layer<RBV, RB, RBV>(av, h, net.wview, lane, ring, nullptr);
     view_dir_part<RBV>(av, M, G, sk, px, py, pz, lane);
     float rgb[3];
 #pragma unroll
@@ -412,6 +518,7 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
         a += __shfl_xor(a, 32);
         rgb[c] = a + net.brgb[c];
     }
+    STAMP(st, 13);
     if (mfma_count && lane == 0) {  // exact MFMA work of this block (wave-uniform quantities)
         const int act = __builtin_popcountll(mask.m0) + __builtin_popcountll(mask.m1);
         const int xk = 3 * M.njh2 + act * VPart<MR>::KB;  // k-steps of one x part
@@ -431,9 +538,16 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
 
 // ======================================================================= per-ray stages
 // Per-ray view factor G[c][n] for every ray of the group (all threads). Needs Tt scratch.
+// Thread t owns output row n = t % WH and the joint columns c = t / WH (mod 256 / WH) for ALL rays
+// of the group, so every weight it loads is used once per ray; the 3 * NK weights of the next
+// column are loaded while the current column is reduced (double buffer).
+template <int WH, int MRV>
 __device__ void compute_view_factor(const ModelDev& M, const NetDev& net, float* lds, const LdsPlan& P, int nr,
-                                    int WH, int tid) {
-    const int nj = M.nj, nk = 1 + 2 * M.mrv;
+                                    int tid) {
+    constexpr int NK = 1 + 2 * MRV;
+    constexpr int KC = 3 * NK;
+    constexpr int NPART = 256 / WH;
+    const int nj = M.nj;
     // trig table Tt[k][3j+c] of the normalised joint-frame ray directions
     for (int idx = tid; idx < nr * nj; idx += blockDim.x) {
         const int r = idx / nj, j = idx % nj;
@@ -444,9 +558,11 @@ __device__ void compute_view_factor(const ModelDev& M, const NetDev& net, float*
         const float en = fmaxf(norm3(ex, ey, ez), 1e-12f);
         const float e[3] = {ex / en, ey / en, ez / en};
         float* Tt = lds + P.scr + P.scr_stride * r;
+#pragma unroll
         for (int c = 0; c < 3; ++c) {
             Tt[3 * j + c] = e[c];
-            for (int f = 0; f < M.mrv; ++f) {
+#pragma unroll
+            for (int f = 0; f < MRV; ++f) {
                 float s, co;
                 sincosf(e[c] * (float)(1 << f), &s, &co);
                 Tt[(1 + 2 * f) * 3 * nj + 3 * j + c] = s;
@@ -456,37 +572,60 @@ __device__ void compute_view_factor(const ModelDev& M, const NetDev& net, float*
     }
     __syncthreads();
     const int ncol = 2 * M.ngh;
-    const int k_first_w = M.cutoff_inputs ? 0 : 1;  // k terms multiplied by w'
-    const int kend = M.cutoff_viewdir ? k_first_w : nk;  // k terms the cutoff does not weight
-    // one thread per (ray, output row n): coalesced reads of the transposed weights
+    const int kfw = M.cutoff_inputs ? 0 : 1;             // first k term multiplied by w'
+    const int kend = M.cutoff_viewdir ? kfw : NK;         // k terms the cutoff does not weight
+    const int nn = tid % WH, part = tid / WH;
+    if (part < NPART) {
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(net.wvdir);
+        if (kend > 0)  // this thread's partial of the unweighted terms, per ray, in scratch
+            for (int r = 0; r < nr; ++r) lds[P.scr + P.scr_stride * r + KC * nj + part * WH + nn] = 0.0f;
+        float wc[KC], wn[KC];
+        int c = part;
+        if (c < nj) {
+#pragma unroll
+            for (int kc = 0; kc < KC; ++kc)
+                wc[kc] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, ((c * KC + kc) * WH + nn) * 4, 0, 0));
+        }
+        for (; c < nj; c += NPART) {
+            const int cn = c + NPART;
+            if (cn < nj) {
+#pragma unroll
+                for (int kc = 0; kc < KC; ++kc)
+                    wn[kc] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, ((cn * KC + kc) * WH + nn) * 4, 0, 0));
+            }
+            for (int r = 0; r < nr; ++r) {
+                const float* tc = lds + P.scr + P.scr_stride * r + 3 * c;
+                float v = 0.0f, u = 0.0f;
+#pragma unroll
+                for (int k = 0; k < NK; ++k)
+#pragma unroll
+                    for (int cc = 0; cc < 3; ++cc) {
+                        const float term = wc[k * 3 + cc] * tc[k * 3 * nj + cc];
+                        if (M.cutoff_viewdir && k >= kfw) v += term;
+                        if (k < kend) u += term;
+                    }
+                lds[P.g + P.g_stride * r + c * WH + nn] = v;
+                if (kend > 0) lds[P.scr + P.scr_stride * r + KC * nj + part * WH + nn] += u;
+            }
+#pragma unroll
+            for (int kc = 0; kc < KC; ++kc) wc[kc] = wn[kc];
+        }
+    }
+    __syncthreads();
     for (int idx = tid; idx < nr * WH; idx += blockDim.x) {
-        const int r = idx / WH, nn = idx % WH;
-        const float* Tt = lds + P.scr + P.scr_stride * r;
+        const int r = idx / WH, n2 = idx % WH;
         const float* ray = lds + P.ray + 16 * r;
         float* G = lds + P.g + P.g_stride * r;
-        float bias = net.bview[nn];
+        float b = net.bview[n2];
         if (M.cfc) {
             const float cam = ray[6];
             const int64_t row = cam < 0.0f ? (int64_t)M.n_codes : (int64_t)cam;
-            for (int m = 0; m < M.cfc; ++m) bias += net.wvcode[m * WH + nn] * net.codes[row * M.cfc + m];
+            for (int m = 0; m < M.cfc; ++m) b += net.wvcode[m * WH + n2] * net.codes[row * M.cfc + m];
         }
-        for (int c = 0; c < nj; ++c) {
-            const float* wv = net.wvdir + (size_t)c * nk * 3 * WH + nn;
-            const float* tc = Tt + 3 * c;
-            float v = 0.0f;
-            if (M.cutoff_viewdir) {
-                for (int k = k_first_w; k < nk; ++k) {
-                    v += wv[(k * 3 + 0) * WH] * tc[k * 3 * nj + 0];
-                    v += wv[(k * 3 + 1) * WH] * tc[k * 3 * nj + 1];
-                    v += wv[(k * 3 + 2) * WH] * tc[k * 3 * nj + 2];
-                }
-            }
-            for (int k = 0; k < kend; ++k)
-                for (int cc = 0; cc < 3; ++cc) bias += wv[(k * 3 + cc) * WH] * tc[k * 3 * nj + cc];
-            G[c * WH + nn] = v;
-        }
-        G[nj * WH + nn] = bias;
-        for (int c = nj + 1; c < ncol; ++c) G[c * WH + nn] = 0.0f;
+        if (kend > 0)
+            for (int pp = 0; pp < NPART; ++pp) b += lds[P.scr + P.scr_stride * r + KC * nj + pp * WH + n2];
+        G[nj * WH + n2] = b;
+        for (int c = nj + 1; c < ncol; ++c) G[c * WH + n2] = 0.0f;
     }
     __syncthreads();
 }
@@ -684,21 +823,31 @@ __global__ __launch_bounds__(256, 1) void render_kernel(ModelDev M, RenderArgs A
     }
     __syncthreads();
 
+    Stamps st;
+    STAMP_INIT(st);
+    STAMP(st, 0);
     const int n_pass = I > 0 ? 2 : 1;
     for (int pass = 0; pass < n_pass; ++pass) {
         const NetDev& net = M.net[pass];
         const int n = pass == 0 ? S : T;
         const int zoff = pass == 0 ? P.zc : P.zf;
-        compute_view_factor(M, net, lds, P, nr, WH, tid);
+        for (int idx = tid; idx < (M.D + 1) * W; idx += blockDim.x) {  // biases -> LDS (synced below)
+            const int L = idx / W, e = idx % W;
+            lds[P.bias + idx] = L < M.D ? net.bl[L][e] : net.bfeat[e];
+        }
+        compute_view_factor<WH, 4>(M, net, lds, P, nr, tid);
+        STAMP(st, 1);
         // ---- MLP over 32-sample blocks, round-robin over the 4 waves
         const int nb = (n + 31) / 32;
         for (int b = wave; b < nr * nb; b += 4) {
             const int r = b / nb, s0 = (b % nb) * 32;
             mlp_block<W, MR>(M, net, lds + P.ray + 16 * r, lds + P.sk + P.sk_stride * r,
                              lds + zoff + P.z_stride * r, n, s0, lds + P.g + P.g_stride * r,
-                             lds + P.raw + P.raw_stride * r, lane, A.mfma_count);
+                             lds + P.raw + P.raw_stride * r, lane, A.mfma_count, lds + P.bias, st);
         }
+        STAMP(st, 2 + 2 * pass);
         __syncthreads();
+        STAMP(st, 6);
         // ---- composite (+ importance sampling after the coarse pass); one wave per ray
         for (int r0 = 0; r0 < R; r0 += 4) {
             const int r = r0 + wave;
@@ -742,7 +891,9 @@ __global__ __launch_bounds__(256, 1) void render_kernel(ModelDev M, RenderArgs A
             }
         }
         __syncthreads();
+        STAMP(st, 3 + 2 * pass);
     }
+    STAMP_FLUSH(st, A.stamps);
 }
 
 // ======================================================================= small kernels
@@ -1046,7 +1197,7 @@ static int validate_desc(const anerf_model_desc* d) {
         return fail(ANERF_EINVAL, "net_width must be 64, 128 or 256");
     if (d->net_depth < 2 || d->net_depth > MAXL) return fail(ANERF_EINVAL, "net_depth outside [2, 16]");
     if (d->multires != 7 && d->multires != 10) return fail(ANERF_EINVAL, "multires must be 7 or 10");
-    if (d->multires_views < 1 || d->multires_views > 10) return fail(ANERF_EINVAL, "multires_views outside [1, 10]");
+    if (d->multires_views != 4) return fail(ANERF_EINVAL, "multires_views must be 4 (the reference default)");
     if (d->n_joints < 1 || d->n_joints > 128) return fail(ANERF_EINVAL, "n_joints outside [1, 128]");
     if (d->skip < 0) return fail(ANERF_EINVAL, "skip must be >= 0");
     if (d->framecode_ch < 0 || d->framecode_ch > 64) return fail(ANERF_EINVAL, "framecode_ch outside [0, 64]");
@@ -1156,6 +1307,11 @@ static void bind_net(const anerf_model_desc* d, const float* base, const std::ve
     nd.codes = base + o[k++];
     nd.balpha = balpha;
 }
+
+#ifdef ANERF_STAMPS
+static unsigned long long* g_stamps = nullptr;
+extern "C" void anerf_diag_set_stamps(unsigned long long* p) { g_stamps = p; }  // diagnostic build only
+#endif
 
 extern "C" {
 
@@ -1321,16 +1477,16 @@ int anerf_render_rays(const anerf_model* m, const float* ray_batch, int32_t ray_
     if (debug && debug->far) HIP_TRY(hipMemcpyAsync(debug->far, farp, 4 * n_rays, hipMemcpyDeviceToDevice, st));
 
     const int S = n_samples, I = n_importance, T = S + I;
+    // rays per workgroup: >= 8 coarse 32-sample blocks (2 per wave) and >= 4 rays, so the per-ray
+    // stages (view factor, compositing: one wave per ray) use all 4 waves
     const int nbc = (S + 31) / 32;
-    int R = 4;
-    for (int g = 4; g > 1; g /= 2)
-        if (nbc % g == 0) { R = 4 / g; break; }
-    if (nbc % 4 == 0) R = 1;
+    int R = std::max(4, 8 / nbc);
+    R = std::min(R, 8);
     const int W = m->desc.net_width;
-    LdsPlan P = make_plan(R, m->desc.n_joints, W, S, T, m->desc.multires_views, m->ngh);
+    LdsPlan P = make_plan(R, m->desc.n_joints, W, S, T, m->desc.multires_views, m->ngh, m->desc.net_depth);
     while (R > 1 && P.total * 4 > 160 * 1024) {
         R /= 2;
-        P = make_plan(R, m->desc.n_joints, W, S, T, m->desc.multires_views, m->ngh);
+        P = make_plan(R, m->desc.n_joints, W, S, T, m->desc.multires_views, m->ngh, m->desc.net_depth);
     }
     if (P.total * 4 > 160 * 1024) return fail(ANERF_EINVAL, "configuration exceeds the 160 KiB LDS budget");
 
@@ -1363,6 +1519,9 @@ int anerf_render_rays(const anerf_model* m, const float* ray_batch, int32_t ray_
         a.dbg_raw1 = debug->raw_fine;
         a.mfma_count = debug->mfma_count;
     }
+#ifdef ANERF_STAMPS
+    a.stamps = g_stamps;
+#endif
     const unsigned grid = (unsigned)((n_rays + R - 1) / R);
     const size_t lds_bytes = (size_t)P.total * 4;
     const int mr = m->desc.multires;
