@@ -36,6 +36,29 @@ __device__ __forceinline__ float torch_linspace01(int i, int n) {
 
 __device__ __forceinline__ float norm3(float a, float b, float c) { return sqrtf(fmaf(c, c, fmaf(b, b, a * a))); }
 __device__ __forceinline__ float norm2(float a, float b) { return sqrtf(fmaf(b, b, a * a)); }
+// Branch-free sin/cos (ocml's sincosf branches to a Payne-Hanek path for large arguments, which
+// splits the MFMA scheduling regions the encoding is interleaved into).  Cody-Waite reduction by
+// pi/2 in three fma steps (exact for |x| < 2^14 * pi/2; the encoder's arguments are distances to
+// joints times 2^t, t < 10) and minimax polynomials on [-pi/4, pi/4]: within 2 ulp of sinf/cosf.
+__device__ __forceinline__ void sincos_rr(float x, float& s, float& c) {
+    const float k = __builtin_rintf(x * 0.636619772f);
+    float r = fmaf(-k, 1.57079637e+00f, x);
+    r = fmaf(-k, -4.37113883e-08f, r);
+    r = fmaf(-k, -1.71512451e-15f, r);
+    const float r2 = r * r;
+    float ps = fmaf(r2, -1.95152959e-4f, 8.33216087e-3f);
+    ps = fmaf(r2, ps, -1.66666546e-1f);
+    ps = fmaf(r2 * r, ps, r);
+    float pc = fmaf(r2, 2.44331571e-5f, -1.38873163e-3f);
+    pc = fmaf(r2, pc, 4.16666457e-2f);
+    pc = fmaf(r2 * r2, pc, fmaf(-0.5f, r2, 1.0f));
+    const int q = (int)k;
+    const float a = (q & 1) ? pc : ps;
+    const float b = (q & 1) ? ps : pc;
+    s = (q & 2) ? -a : a;
+    c = ((q + 1) & 2) ? -b : b;
+}
+
 __device__ __forceinline__ float sigmoid(float x) { return 1.0f / (1.0f + expf(-x)); }
 // torch.relu keeps NaN
 __device__ __forceinline__ float relu(float x) { return x < 0.0f ? 0.0f : x; }

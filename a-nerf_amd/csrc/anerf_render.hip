@@ -109,14 +109,15 @@ struct RenderArgs {
 
 // ======================================================================= LDS plan
 struct LdsPlan {
-    int ray, sk, zc, zf, raw, g, scr, bias;  // float offsets
+    int ray, sk, zc, zf, raw, g, scr, bias, cut, uf;  // float offsets (uf < 0: no u-feature store)
     int total;                          // floats
-    int sk_stride, z_stride, raw_stride, g_stride, scr_stride;
+    int sk_stride, z_stride, raw_stride, g_stride, scr_stride, uf_stride;
 };
 
 __host__ __device__ inline int pad32(int x) { return (x + 31) & ~31; }
 
-__host__ __device__ inline LdsPlan make_plan(int R, int nj, int W, int S, int T, int mrv, int ngh, int D) {
+__host__ __device__ inline LdsPlan make_plan(int R, int nj, int W, int S, int T, int mrv, int ngh, int D, int njh2,
+                                             bool with_uf) {
     LdsPlan p;
     const int wh = W / 2;
     const int nk = 1 + 2 * mrv;
@@ -137,6 +138,11 @@ __host__ __device__ inline LdsPlan make_plan(int R, int nj, int W, int S, int T,
     p.scr = o; o += p.scr_stride * R;
     o = (o + 3) & ~3;
     p.bias = o; o += (D + 1) * W;  // the current net's hidden + feature biases, accumulator order
+    p.cut = o; o += 2 * nj;        // cutoff distances of the window (points, view directions)
+    o = (o + 3) & ~3;
+    p.uf_stride = 64 * 3 * njh2;   // per wave: the L0 bone directions, re-read by the skip layer
+    p.uf = with_uf ? o : -1;
+    if (with_uf) o += 4 * p.uf_stride;
     p.total = (o + 3) & ~3;
     return p;
 }
@@ -239,43 +245,88 @@ __device__ __forceinline__ int mask_pop(uint64_t& a0, uint64_t& a1) {
     return -1;
 }
 
-// bone direction u_j of this lane's sample, and whether its cutoff window is non-zero
-__device__ __forceinline__ void u_joint(const ModelDev& M, const float* __restrict__ sk, int j, float px, float py,
-                                        float pz, float& u0, float& u1, float& u2, bool& live) {
-    const bool valid = j < M.nj;
-    float qx = 0.f, qy = 0.f, qz = 0.f;
-    if (valid) joint_local(sk + 12 * j, px, py, pz, qx, qy, qz);
+// Pin a value's computation before this point: IR passes otherwise sink the software-pipelined
+// encoding math out of the MFMA region it was written in (sched_barrier only binds the
+// machine scheduler).
+__device__ __forceinline__ void pin(float x) { asm volatile("" ::"v"(x)); }
+__device__ __forceinline__ void pin(bool x) { asm volatile("" ::"v"((int)x)); }
+
+// Compile-time interleave of one scheduling region: NM MFMAs, each followed by up to NV VALU
+// instructions (one wave per SIMD: without it the scheduler issues the MFMAs back to back and
+// leaves the encoding VALU exposed after them).
+template <int NM, int NV>
+__device__ __forceinline__ void interleave_mfma_valu() {
+#pragma unroll
+    for (int i = 0; i < NM; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);
+    }
+}
+
+// One joint's skeleton row (3x4 of the world->joint transform) and window distance, loaded from
+// LDS into registers two MFMA groups before use, so the encoder math never waits on LDS.
+struct JRow {
+    f32x4 a, b, c;
+    float cut;
+};
+
+__device__ __forceinline__ JRow load_row(const float* __restrict__ sk, const float* __restrict__ cut, int j, int nj) {
+    const int jc = j < nj ? j : 0;
+    const f32x4* p = reinterpret_cast<const f32x4*>(sk + 12 * jc);
+    return JRow{p[0], p[1], p[2], cut[jc]};
+}
+
+// bone direction u_j of this lane's sample, and whether its cutoff window is non-zero.
+// dist is the correctly rounded norm (as in the oracle); the normalisation multiplies by the
+// hardware reciprocal (<= 1.5 ulp from q / max(dist, 1e-12)), and the window test is exact:
+// cutoff_w = 1 - 1/(1 + e) is 0 iff 1 + e rounds to 1 (e = expf(-tau (dist - c))).
+// Branch-free (per-lane selects) so that it stays in the MFMA region it is scheduled into.
+__device__ __forceinline__ void u_joint(const ModelDev& M, const JRow& r, bool valid, float px, float py, float pz,
+                                        float& u0, float& u1, float& u2, bool& live) {
+#ifdef ANERF_EXP_UFAST  // timing experiment only (stamps build): encoder VALU removed
+    u0 = px * r.a[0]; u1 = py; u2 = pz; live = false; return;
+#endif
+    float qx = fmaf(r.a[3], 1.0f, fmaf(r.a[2], pz, fmaf(r.a[1], py, r.a[0] * px)));
+    float qy = fmaf(r.b[3], 1.0f, fmaf(r.b[2], pz, fmaf(r.b[1], py, r.b[0] * px)));
+    float qz = fmaf(r.c[3], 1.0f, fmaf(r.c[2], pz, fmaf(r.c[1], py, r.c[0] * px)));
+    qx = valid ? qx : 0.0f;
+    qy = valid ? qy : 0.0f;
+    qz = valid ? qz : 0.0f;
     const float dist = norm3(qx, qy, qz);
-    const float dn = fmaxf(dist, 1e-12f);
-    u0 = qx / dn;
-    u1 = qy / dn;
-    u2 = qz / dn;
-    live = valid;
-    if (valid && M.sparse) live = cutoff_w(M.tau, dist, M.cutoff[j]) != 0.0f;
+    const float inv = __builtin_amdgcn_rcpf(fmaxf(dist, 1e-12f));
+    u0 = qx * inv;
+    u1 = qy * inv;
+    u2 = qz * inv;
+    const float e = expf(-(M.tau * (dist - r.cut)));
+    live = valid & (!M.sparse | ((1.0f + e) != 1.0f));  // (no short-circuit: no branch)
 }
 
 // The geometry of pair-of-pairs pp+1 is computed under the MFMAs of pp (software pipeline:
 // between two sched_barriers the scheduler interleaves the VALU with the async MFMAs).
 template <int RB>
 __device__ __forceinline__ void u_part(f32x16 (&acc)[RB], const ModelDev& M, const float* __restrict__ wp,
-                                       const float* __restrict__ sk, float px, float py, float pz, int lane,
-                                       JointMask* mask) {
+                                       const float* __restrict__ sk, const float* __restrict__ cut, float px,
+                                       float py, float pz, int lane, JointMask* mask, float* __restrict__ uf,
+                                       Ring<RB>& sh, const float* __restrict__ next, Stamps& st) {
     const int hh = lane >> 5;
     const int njh2 = M.njh2;
     const int npp = njh2 / 2;
     const int total_groups = 3 * npp;
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(wp);
     const int voff = lane * 8;
-    f32x2 ring[3][RB];
+    f32x2 ring[3][RB];  // groups 0 and 1 were prefetched into the shared ring by the caller
 #pragma unroll
-    for (int g = 0; g < 2; ++g)
-#pragma unroll
-        for (int rb = 0; rb < RB; ++rb) ring[g][rb] = bload2(rs, voff, (g * RB + rb) * 512);
+    for (int rb = 0; rb < RB; ++rb) ring[0][rb] = sh.s[0][rb], ring[1][rb] = sh.s[1][rb];
     uint64_t m0 = 0, m1 = 0;
     float f[6];
     bool lv0, lv1;
-    u_joint(M, sk, 0 + hh * njh2, px, py, pz, f[0], f[1], f[2], lv0);
-    u_joint(M, sk, 1 + hh * njh2, px, py, pz, f[3], f[4], f[5], lv1);
+    const int nj = M.nj, j0 = hh * njh2;
+    JRow ra = load_row(sk, cut, j0, nj), rb2 = load_row(sk, cut, j0 + 1, nj);
+    u_joint(M, ra, j0 < nj, px, py, pz, f[0], f[1], f[2], lv0);
+    u_joint(M, rb2, j0 + 1 < nj, px, py, pz, f[3], f[4], f[5], lv1);
+    ra = load_row(sk, cut, j0 + 2, nj);
+    rb2 = load_row(sk, cut, j0 + 3, nj);
+    STAMP(st, 14);
     for (int pp = 0; pp < npp; ++pp) {
         if (mask) {
 #pragma unroll
@@ -290,24 +341,36 @@ __device__ __forceinline__ void u_part(f32x16 (&acc)[RB], const ModelDev& M, con
                 }
             }
         }
+        if (uf) {  // keep this block's bone directions for the skip layer: [group][lane][2]
+#pragma unroll
+            for (int g = 0; g < 3; ++g)
+                *reinterpret_cast<f32x2*>(uf + ((pp * 3 + g) * 64 + lane) * 2) = f32x2{f[2 * g], f[2 * g + 1]};
+        }
         float fn[6];
         bool ln0 = false, ln1 = false;
 #pragma unroll
         for (int g = 0; g < 3; ++g) {
             __builtin_amdgcn_sched_barrier(0);
-            const int gn = pp * 3 + g + 2;
-            if (gn < total_groups) {
+            const int gn = min(pp * 3 + g + 2, total_groups - 1);  // (a harmless reload at the end)
 #pragma unroll
-                for (int rb = 0; rb < RB; ++rb) ring[(g + 2) % 3][rb] = bload2(rs, voff, (gn * RB + rb) * 512);
-            }
+            for (int rb = 0; rb < RB; ++rb) ring[(g + 2) % 3][rb] = bload2(rs, voff, (gn * RB + rb) * 512);
 #pragma unroll
             for (int t = 0; t < 2; ++t) {
                 const float b = f[2 * g + t];
 #pragma unroll
                 for (int rb = 0; rb < RB; ++rb) acc[rb] = mfma_f32_32x32x2(ring[g % 3][rb][t], b, acc[rb]);
             }
-            if (g == 0) u_joint(M, sk, 2 * pp + 2 + hh * njh2, px, py, pz, fn[0], fn[1], fn[2], ln0);
-            if (g == 1) u_joint(M, sk, 2 * pp + 3 + hh * njh2, px, py, pz, fn[3], fn[4], fn[5], ln1);
+            if (g == 0) {  // joint 2pp+2 from its prefetched row; then prefetch joint 2pp+4
+                u_joint(M, ra, j0 + 2 * pp + 2 < nj, px, py, pz, fn[0], fn[1], fn[2], ln0);
+                pin(fn[0]), pin(fn[1]), pin(fn[2]), pin(ln0);
+                ra = load_row(sk, cut, j0 + 2 * pp + 4, nj);
+            }
+            if (g == 1) {
+                u_joint(M, rb2, j0 + 2 * pp + 3 < nj, px, py, pz, fn[3], fn[4], fn[5], ln1);
+                pin(fn[3]), pin(fn[4]), pin(fn[5]), pin(ln1);
+                rb2 = load_row(sk, cut, j0 + 2 * pp + 5, nj);
+            }
+            interleave_mfma_valu<2 * RB, 8>();
         }
 #pragma unroll
         for (int i = 0; i < 6; ++i) f[i] = fn[i];
@@ -318,6 +381,40 @@ __device__ __forceinline__ void u_part(f32x16 (&acc)[RB], const ModelDev& M, con
         mask->m0 = m0;
         mask->m1 = m1;
     }
+    if (next) ring_preload<RB, RB>(sh, next, lane);
+}
+
+// The skip layer's bone-direction part from the features u_part stored in LDS: a pure MFMA
+// stream (B operands read one group ahead) with the weight ring two groups ahead.
+template <int RB>
+__device__ __forceinline__ void u_part_lds(f32x16 (&acc)[RB], const ModelDev& M, const float* __restrict__ wp,
+                                           const float* __restrict__ uf, int lane, Ring<RB>& sh,
+                                           const float* __restrict__ next) {
+    const int total_groups = 3 * (M.njh2 / 2);
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(wp);
+    const int voff = lane * 8;
+    const f32x2* ub = reinterpret_cast<const f32x2*>(uf) + lane;
+    f32x2 ring[3][RB];
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) ring[0][rb] = sh.s[0][rb], ring[1][rb] = sh.s[1][rb];
+    f32x2 bc = ub[0];
+    for (int g0 = 0; g0 < total_groups; g0 += 3) {
+#pragma unroll
+        for (int gg = 0; gg < 3; ++gg) {
+            __builtin_amdgcn_sched_barrier(0);
+            const int g = g0 + gg;
+            const int gn = min(g + 2, total_groups - 1);
+#pragma unroll
+            for (int rb = 0; rb < RB; ++rb) ring[(gg + 2) % 3][rb] = bload2(rs, voff, (gn * RB + rb) * 512);
+            const f32x2 bn = ub[min(g + 1, total_groups - 1) * 64];
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int rb = 0; rb < RB; ++rb) acc[rb] = mfma_f32_32x32x2(ring[gg][rb][t], bc[t], acc[rb]);
+            bc = bn;
+        }
+    }
+    if (next) ring_preload<RB, RB>(sh, next, lane);
 }
 
 template <int MR>
@@ -326,18 +423,19 @@ struct VPart {
     static constexpr int GB = KB / 2;               // float2 groups per joint
 };
 
-__device__ __forceinline__ void v_geom(const ModelDev& M, const float* __restrict__ sk, int j, float px, float py,
-                                       float pz, float& dist, float& w) {
+__device__ __forceinline__ void v_geom(const ModelDev& M, const float* __restrict__ sk, const float* __restrict__ cut,
+                                       int j, float px, float py, float pz, float& dist, float& w) {
     float qx, qy, qz;
     joint_local(sk + 12 * j, px, py, pz, qx, qy, qz);
     dist = norm3(qx, qy, qz);
-    w = M.use_cutoff ? cutoff_w(M.tau, dist, M.cutoff[j]) : 1.0f;
+    const float wc = cutoff_w(M.tau, dist, cut[j]);
+    w = M.use_cutoff ? wc : 1.0f;
 }
 
 template <int RB, int MR>
 __device__ __forceinline__ void v_part(f32x16 (&acc)[RB], const ModelDev& M, const float* __restrict__ wp,
-                                       const float* __restrict__ sk, float px, float py, float pz, int lane,
-                                       JointMask mask) {
+                                       const float* __restrict__ sk, const float* __restrict__ cut, float px,
+                                       float py, float pz, int lane, JointMask mask, Stamps& st) {
     constexpr int GB = VPart<MR>::GB;
     constexpr int KB = VPart<MR>::KB;
     constexpr int PER = (MR + GB - 2) / (GB - 1);  // sin/cos terms of the next joint per group 1..GB-1
@@ -357,17 +455,18 @@ __device__ __forceinline__ void v_part(f32x16 (&acc)[RB], const ModelDev& M, con
     float f[KB];
     {
         float dist, w;
-        v_geom(M, sk, j, px, py, pz, dist, w);
+        v_geom(M, sk, cut, j, px, py, pz, dist, w);
 #pragma unroll
         for (int t = 0; t < MR; ++t) {
             float sn, cs;
-            sincosf(dist * (float)(1 << t), &sn, &cs);
+            sincos_rr(dist * (float)(1 << t), sn, cs);
             f[t] = (hh ? cs : sn) * w;
         }
         f[MR] = hh ? 0.0f : (dist_in ? dist * w : dist);
 #pragma unroll
         for (int t = MR + 1; t < KB; ++t) f[t] = 0.0f;
     }
+    STAMP(st, 15);
     while (j >= 0) {
         float fn[KB];
         float dn = 0.0f, wn = 0.0f;
@@ -380,10 +479,10 @@ __device__ __forceinline__ void v_part(f32x16 (&acc)[RB], const ModelDev& M, con
 #pragma unroll
                 for (int rb = 0; rb < RB; ++rb)
                     ring[(g + PD) % GB][rb] = bload2(rs, voff, ((j * GB + g + PD) * RB + rb) * 512);
-            } else if (jn >= 0) {
+            } else {  // the next joint's first groups (this joint's again after the last: harmless)
 #pragma unroll
                 for (int rb = 0; rb < RB; ++rb)
-                    ring[(g + PD) % GB][rb] = bload2(rs, voff, ((jn * GB + g + PD - GB) * RB + rb) * 512);
+                    ring[(g + PD) % GB][rb] = bload2(rs, voff, ((jg * GB + g + PD - GB) * RB + rb) * 512);
             }
 #pragma unroll
             for (int t = 0; t < 2; ++t) {
@@ -393,15 +492,18 @@ __device__ __forceinline__ void v_part(f32x16 (&acc)[RB], const ModelDev& M, con
             }
             // next joint's features under these MFMAs
             if (g == 0) {
-                v_geom(M, sk, jg, px, py, pz, dn, wn);
+                v_geom(M, sk, cut, jg, px, py, pz, dn, wn);
+                pin(dn), pin(wn);
             } else {
 #pragma unroll
                 for (int t = (g - 1) * PER; t < g * PER && t < MR; ++t) {
                     float sn, cs;
-                    sincosf(dn * (float)(1 << t), &sn, &cs);
+                    sincos_rr(dn * (float)(1 << t), sn, cs);
                     fn[t] = (hh ? cs : sn) * wn;
+                    pin(fn[t]);
                 }
             }
+            interleave_mfma_valu<2 * RB, 8>();
         }
         fn[MR] = hh ? 0.0f : (dist_in ? dn * wn : dn);
 #pragma unroll
@@ -413,36 +515,44 @@ __device__ __forceinline__ void v_part(f32x16 (&acc)[RB], const ModelDev& M, con
     }
 }
 
-// View layer, per-ray direction part: acc[RBV] += G^T * [w'_0 .. w'_{NJ-1}, 1]  (G in LDS)
+// View layer, per-ray direction part: acc[RBV] += G^T * [w'_0 .. w'_{NJ-1}, 1]  (G in LDS).
+// Column q+1's window weight is computed under column q's MFMAs.
+__device__ __forceinline__ float view_weight(const ModelDev& M, const float* __restrict__ sk,
+                                             const float* __restrict__ cut, int c, float px, float py, float pz) {
+    const int cc = c < M.nj ? c : 0;
+    float qx, qy, qz;
+    joint_local(sk + 12 * cc, px, py, pz, qx, qy, qz);
+    const float w = cutoff_w(M.tau_v, norm3(qx, qy, qz), cut[M.nj + cc]);
+    return c < M.nj ? (M.cutoff_viewdir ? w : 0.0f) : (c == M.nj ? 1.0f : 0.0f);
+}
+
 template <int RBV>
 __device__ __forceinline__ void view_dir_part(f32x16 (&acc)[RBV], const ModelDev& M, const float* __restrict__ G,
-                                              const float* __restrict__ sk, float px, float py, float pz, int lane) {
+                                              const float* __restrict__ sk, const float* __restrict__ cut, float px,
+                                              float py, float pz, int lane) {
     constexpr int WH = RBV * 32;
     const int hh = lane >> 5, sl = lane & 31;
+    float b = view_weight(M, sk, cut, hh * M.ngh, px, py, pz);
     for (int q = 0; q < M.ngh; ++q) {
+        __builtin_amdgcn_sched_barrier(0);
         const int c = q + hh * M.ngh;
-        float b = 0.0f;
-        if (c < M.nj) {
-            if (M.cutoff_viewdir) {
-                float qx, qy, qz;
-                joint_local(sk + 12 * c, px, py, pz, qx, qy, qz);
-                b = cutoff_w(M.tau_v, norm3(qx, qy, qz), M.cutoff_v[c]);
-            }
-        } else if (c == M.nj) {
-            b = 1.0f;
-        }
         const float* gc = G + c * WH + sl;
 #pragma unroll
         for (int rb = 0; rb < RBV; ++rb) acc[rb] = mfma_f32_32x32x2(gc[32 * rb], b, acc[rb]);
+        b = view_weight(M, sk, cut, c + 1, px, py, pz);  // (q+1 == ngh: not used)
+        pin(b);
+        interleave_mfma_valu<RBV, 14>();
     }
 }
 
 // One 32-sample block of one ray through a whole NeRF: raw (rgb, sigma) into LDS.
 template <int W, int MR>
 __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __restrict__ ray,
-                          const float* __restrict__ sk, const float* __restrict__ z, int n, int s0,
+                          const float* __restrict__ sk, const float* __restrict__ cut, const float* __restrict__ z,
+                          int n, int s0,
                           const float* __restrict__ G, float* __restrict__ raw_out, int lane,
-                          unsigned long long* mfma_count, const float* __restrict__ bias, Stamps& st) {
+                          unsigned long long* mfma_count, const float* __restrict__ bias, float* __restrict__ uf,
+                          Stamps& st) {
     constexpr int RB = W / 32;
     constexpr int RBV = (W / 2) / 32;
     const int sl = lane & 31, hh = lane >> 5;
@@ -457,12 +567,12 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
     f32x16 acc[RB], h[RB];
     JointMask mask;
     Ring<RB> ring;
-    if (M.D > 1) ring_preload<RB, RB>(ring, net.wl[1], lane);  // layer 1's first groups, early
+    ring_preload<RB, RB>(ring, net.wl[0], lane);  // the u part's first groups, early
     load_bias<RB>(acc, bias, hh);
     STAMP(st, 10);
-    u_part<RB>(acc, M, net.wl[0], sk, px, py, pz, lane, &mask);
+    u_part<RB>(acc, M, net.wl[0], sk, cut, px, py, pz, lane, &mask, uf, ring, M.D > 1 ? net.wl[1] : net.wfeat, st);
     STAMP(st, 8);
-    v_part<RB, MR>(acc, M, net.wl0v, sk, px, py, pz, lane, mask);
+    v_part<RB, MR>(acc, M, net.wl0v, sk, cut, px, py, pz, lane, mask, st);
     STAMP(st, 9);
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb)
@@ -471,11 +581,15 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
     for (int L = 1; L < M.D; ++L) {
         load_bias<RB>(acc, bias + L * W, hh);
         STAMP(st, 10);
-        regs_layer<RB, RB, RB>(acc, h, net.wl[L], lane, ring, L + 1 < M.D ? net.wl[L + 1] : net.wfeat);
+        const float* after = L + 1 < M.D ? net.wl[L + 1] : net.wfeat;
+        regs_layer<RB, RB, RB>(acc, h, net.wl[L], lane, ring, L == M.skip + 1 ? net.wskipu : after);
         STAMP(st, 11);
         if (L == M.skip + 1) {  // x part after the h part: h is dead, its registers hold the ring
-            u_part<RB>(acc, M, net.wskipu, sk, px, py, pz, lane, nullptr);
-            v_part<RB, MR>(acc, M, net.wskipv, sk, px, py, pz, lane, mask);
+            if (uf)
+                u_part_lds<RB>(acc, M, net.wskipu, uf, lane, ring, after);
+            else
+                u_part<RB>(acc, M, net.wskipu, sk, cut, px, py, pz, lane, nullptr, nullptr, ring, after, st);
+            v_part<RB, MR>(acc, M, net.wskipv, sk, cut, px, py, pz, lane, mask, st);
             STAMP(st, 12);
         }
 #pragma unroll
@@ -505,7 +619,7 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
 #pragma unroll
     for (int rb = 0; rb < RBV; ++rb) av[rb] = f32x16{0};
     regs_layer<RBV, RB, RBV>(av, h, net.wview, lane, ring, nullptr);
-    view_dir_part<RBV>(av, M, G, sk, px, py, pz, lane);
+    view_dir_part<RBV>(av, M, G, sk, cut, px, py, pz, lane);
     float rgb[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
@@ -814,6 +928,7 @@ __global__ __launch_bounds__(256, 1) void render_kernel(ModelDev M, RenderArgs A
         const int pose = __float_as_int(lds[P.ray + 16 * r + 10]);
         lds[P.sk + P.sk_stride * r + e] = A.skts[((int64_t)pose * M.nj + j) * 16 + c];
     }
+    for (int j = tid; j < 2 * M.nj; j += blockDim.x) lds[P.cut + j] = j < M.nj ? M.cutoff[j] : M.cutoff_v[j - M.nj];
     // coarse samples (sample_from_lineseg, ray_utils.py:218-224)
     for (int idx = tid; idx < nr * S; idx += blockDim.x) {
         const int r = idx / S, s = idx % S;
@@ -841,9 +956,10 @@ __global__ __launch_bounds__(256, 1) void render_kernel(ModelDev M, RenderArgs A
         const int nb = (n + 31) / 32;
         for (int b = wave; b < nr * nb; b += 4) {
             const int r = b / nb, s0 = (b % nb) * 32;
-            mlp_block<W, MR>(M, net, lds + P.ray + 16 * r, lds + P.sk + P.sk_stride * r,
+            mlp_block<W, MR>(M, net, lds + P.ray + 16 * r, lds + P.sk + P.sk_stride * r, lds + P.cut,
                              lds + zoff + P.z_stride * r, n, s0, lds + P.g + P.g_stride * r,
-                             lds + P.raw + P.raw_stride * r, lane, A.mfma_count, lds + P.bias, st);
+                             lds + P.raw + P.raw_stride * r, lane, A.mfma_count, lds + P.bias,
+                             (P.uf >= 0 && M.skip + 1 < M.D) ? lds + P.uf + wave * P.uf_stride : nullptr, st);
         }
         STAMP(st, 2 + 2 * pass);
         __syncthreads();
@@ -1483,10 +1599,12 @@ int anerf_render_rays(const anerf_model* m, const float* ray_batch, int32_t ray_
     int R = std::max(4, 8 / nbc);
     R = std::min(R, 8);
     const int W = m->desc.net_width;
-    LdsPlan P = make_plan(R, m->desc.n_joints, W, S, T, m->desc.multires_views, m->ngh, m->desc.net_depth);
+    const int nj = m->desc.n_joints, mrv = m->desc.multires_views, D = m->desc.net_depth;
+    LdsPlan P = make_plan(R, nj, W, S, T, mrv, m->ngh, D, m->njh2, true);
+    if (P.total * 4 > 160 * 1024) P = make_plan(R, nj, W, S, T, mrv, m->ngh, D, m->njh2, false);
     while (R > 1 && P.total * 4 > 160 * 1024) {
         R /= 2;
-        P = make_plan(R, m->desc.n_joints, W, S, T, m->desc.multires_views, m->ngh, m->desc.net_depth);
+        P = make_plan(R, nj, W, S, T, mrv, m->ngh, D, m->njh2, false);
     }
     if (P.total * 4 > 160 * 1024) return fail(ANERF_EINVAL, "configuration exceeds the 160 KiB LDS budget");
 

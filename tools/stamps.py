@@ -12,12 +12,13 @@ import torch
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 _lib = importlib.import_module("a-nerf_amd._lib")
-_lib.LIB_PATH = os.path.join(REPO, "tools", "libanerf_hip_stamps.so")
+_lib.LIB_PATH = os.path.join(REPO, "tools", os.environ.get("ANERF_STAMPS_LIB", "libanerf_hip_stamps.so"))
 anerf = importlib.import_module("a-nerf_amd")
 syn = importlib.import_module("a-nerf_amd.synthetic")
 NAMES = {0: "prologue", 1: "view factor G", 2: "MLP coarse", 3: "composite+importance", 4: "MLP fine",
          5: "composite fine", 6: "barrier wait after MLP", 8: "  L0 u-part", 9: "  L0 v-part",
-         10: "  bias/relu boundaries", 11: "  hidden h-parts", 12: "  skip u+v", 13: "  heads (alpha/feat/view/rgb)"}
+         10: "  bias/relu boundaries", 11: "  hidden h-parts", 12: "  skip u+v", 13: "  heads (alpha/feat/view/rgb)",
+         14: "  L0 u-part prologue", 15: "  v-part prologues (L0 + skip)"}
 
 
 def main():
@@ -39,7 +40,7 @@ def main():
                         skts=torch.from_numpy(sc["skts"]), ext_scale=0.001, to_host=False)
     torch.cuda.synchronize()
     v = st.cpu().numpy().astype(np.float64)
-    tot = v[0:14].sum()  # top-level phases + the MLP sub-phases (stamped separately)
+    tot = v[0:16].sum()  # top-level phases + the MLP sub-phases (stamped separately)
     print(f"tau={tau}: total wave-cycles {tot:.3e}")
     for i, nm in NAMES.items():
         print(f"{nm:34s} {100 * v[i] / tot:6.2f} %")
