@@ -62,6 +62,12 @@ __device__ __forceinline__ void sincos_rr(float x, float& s, float& c) {
 __device__ __forceinline__ float sigmoid(float x) { return 1.0f / (1.0f + expf(-x)); }
 // torch.relu keeps NaN
 __device__ __forceinline__ float relu(float x) { return x < 0.0f ? 0.0f : x; }
+// MLP activation relu in one VALU op: signed-integer max of the bit pattern maps every float with
+// the sign bit set to +0 and keeps the rest (incl. +NaN, which is what the GPU generates and what
+// the host NaN fill produces).  Differs from relu only in -0 -> +0 and -NaN -> 0.
+__device__ __forceinline__ float relu_act(float x) {
+    return __builtin_bit_cast(float, max(__builtin_bit_cast(int, x), 0));
+}
 
 // numpy pairwise float32 sum (np.nanmean of get_near_far_in_cylinder, ray_utils.py:332)
 __device__ inline float np_leaf_sum(const float* a, int64_t n) {

@@ -137,7 +137,7 @@ __host__ __device__ inline LdsPlan make_plan(int R, int nj, int W, int S, int T,
     p.g = o; o += p.g_stride * R;
     p.scr = o; o += p.scr_stride * R;
     o = (o + 3) & ~3;
-    p.bias = o; o += (D + 1) * W;  // the current net's hidden + feature biases, accumulator order
+    p.bias = o; o += (D + 2) * W;  // the current net's hidden + feature biases, accumulator order; w_alpha
     p.cut = o; o += 2 * nj;        // cutoff distances of the window (points, view directions)
     o = (o + 3) & ~3;
     p.uf_stride = 64 * 3 * njh2;   // per wave: the L0 bone directions, re-read by the skip layer
@@ -171,51 +171,108 @@ __device__ __forceinline__ void load_bias(f32x16 (&acc)[RB], const float* __rest
     }
 }
 
-// acc[RBO] += W^T * h  over the RBI*32 activations held in h (k-steps in accumulator order).
-// Weights packed [group = q/2][RBO][64 lanes][2].  The 4-slot register ring is shared by
-// consecutive activation layers: group g lives in slot g % 4 (NG is a multiple of 4), the
-// prefetch distance is 2 groups, and the last two groups of a layer prefetch groups 0 and 1 of
-// `next` (RBN row blocks) so the next layer starts without a load bubble.
-template <int RB>
+// Weight streams are cut into groups of F floats per lane (one MFMA A operand each), stored
+// [group][F/4][64 lanes][4] so that every b128 load reads 1 KiB contiguous.  A 4-slot register
+// ring is shared by consecutive phases: group g of a layer lives in slot g % 4, the prefetch
+// distance is 2 groups, and the last two groups of a layer prefetch groups 0 and 1 of the next
+// phase so it starts without a load bubble.
 struct Ring {
-    f32x2 s[4][RB];
+    float v[4][16];
 };
 
-template <int RBO, int RB>
-__device__ __forceinline__ void ring_preload(Ring<RB>& ring, const float* __restrict__ wp, int lane) {
-    const __amdgpu_buffer_rsrc_t rs = make_rsrc(wp);
+template <int F>
+__device__ __forceinline__ void load_group(float (&slot)[16], __amdgpu_buffer_rsrc_t rs, int lane, int g) {
 #pragma unroll
-    for (int g = 0; g < 2; ++g)
-#pragma unroll
-        for (int rb = 0; rb < RBO; ++rb) ring.s[g][rb] = bload2(rs, lane * 8, (g * RBO + rb) * 512);
+    for (int i = 0; i < F / 4; ++i) {
+        const f32x4 x = bload4(rs, lane * 16 + i * 1024, g * F * 256);  // (i * 1024 -> immediate offset)
+        slot[4 * i] = x[0], slot[4 * i + 1] = x[1], slot[4 * i + 2] = x[2], slot[4 * i + 3] = x[3];
+    }
 }
 
-template <int RBO, int RBI, int RBN, int RB>
-__device__ __forceinline__ void regs_layer(f32x16 (&acc)[RBO], const f32x16 (&h)[RBI], const float* __restrict__ wp,
-                                           int lane, Ring<RB>& ring, const float* __restrict__ next) {
-    constexpr int NG = 8 * RBI;
-    static_assert(NG % 4 == 0, "ring slot alignment");
+template <int F>
+__device__ __forceinline__ void ring_preload(Ring& ring, const float* __restrict__ wp, int lane) {
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(wp);
+    load_group<F>(ring.v[0], rs, lane, 0);
+    load_group<F>(ring.v[1], rs, lane, 1);
+}
+
+// One dense layer, out[RBO] (+)= W^T act(in) over 32*RBI inputs, with the layer boundary fused in:
+// the previous layer's accumulators ain[rb] are turned into B operands h[rb] (relu, or used as
+// they are for the feature -> view edge) and the output blocks are initialised with their bias
+// *inside* the first groups, under the MFMAs.  To make that possible the first RBO groups are
+// "lead" groups: group rb < RBO runs k-steps 0..15 (input block 0) of output block rb only, so
+// block rb+1 is converted while block rb accumulates; the remaining groups are k-major
+// (KG = 16/RBO k-steps x RBO blocks = 16 MFMAs each).  ALPHA folds the alpha head
+// (sig += w_alpha . h in k-step order) into the groups as VALU filler.
+template <int RBO, int RBI, bool RELU_IN, bool OUT_SAME, bool ALPHA>
+__device__ __forceinline__ void mlp_layer(f32x16 (&out)[RBO], f32x16 (&ain)[RBI], f32x16 (&h)[RBI],
+                                          const float* __restrict__ bias, const float* __restrict__ wp, int lane,
+                                          Ring& ring, const float* __restrict__ next, const float* __restrict__ wa,
+                                          float& sig) {
+    constexpr int KG = 16 / RBO;
+    constexpr int NQ = 16 * RBI;
+    constexpr int NG = RBO + (NQ - 16) / KG;
+    static_assert(RBO * KG == 16 && (NQ - 16) % KG == 0, "group shape");
+    const int hh = lane >> 5;
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(wp);
     const __amdgpu_buffer_rsrc_t rn = make_rsrc(next);
-    const int voff = lane * 8;
+    auto init_out = [&](int rb) {  // bias (OUT_SAME layers) or zero
+        if constexpr (OUT_SAME) {
+            const f32x4* p = reinterpret_cast<const f32x4*>(bias + (rb * 2 + hh) * 16);
+            const f32x4 v0 = p[0], v1 = p[1], v2 = p[2], v3 = p[3];
+            out[rb] = f32x16{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3],
+                             v2[0], v2[1], v2[2], v2[3], v3[0], v3[1], v3[2], v3[3]};
+        } else {
+            out[rb] = f32x16{0};
+        }
+    };
+    auto convert = [&](int rb) {
+        if constexpr (RELU_IN) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) h[rb][i] = relu_act(ain[rb][i]);
+        }
+        if constexpr (OUT_SAME) {
+            if (rb < RBO) init_out(rb);
+        }
+    };
+    auto B = [&](int q) -> float { return RELU_IN ? h[q >> 4][q & 15] : ain[q >> 4][q & 15]; };
+    if constexpr (!OUT_SAME) {
+#pragma unroll
+        for (int rb = 0; rb < RBO; ++rb) init_out(rb);
+    }
+    convert(0);
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
-        // keep the ring four groups deep: no load crosses a group boundary
         __builtin_amdgcn_sched_barrier(0);
-        if (g + 2 < NG) {
+        if (g + 2 < NG)
+            load_group<16>(ring.v[(g + 2) % 4], rs, lane, g + 2);
+        else if (NG % 4 == 0 && next)
+            load_group<16>(ring.v[(g + 2) % 4], rn, lane, g + 2 - NG);
+        if (g < RBO) {
 #pragma unroll
-            for (int rb = 0; rb < RBO; ++rb) ring.s[(g + 2) % 4][rb] = bload2(rs, voff, ((g + 2) * RBO + rb) * 512);
-        } else if (next) {
+            for (int t = 15; t >= 0; --t)  // (last-loaded float first: one vmcnt wait per group)
+                out[g] = mfma_f32_32x32x2(ring.v[g % 4][t], B(t), out[g]);
+            if (ALPHA && g == 0) {
+                const f32x4* w4 = reinterpret_cast<const f32x4*>(wa + hh * 16 * RBI);
 #pragma unroll
-            for (int rb = 0; rb < RBN; ++rb)
-                ring.s[(g + 2) % 4][rb] = bload2(rn, voff, ((g + 2 - NG) * RBN + rb) * 512);
-        }
+                for (int t = 0; t < 16; ++t) sig = fmaf(w4[t >> 2][t & 3], B(t), sig);
+            }
+            if (g + 1 < RBO) {
+                convert(g + 1);
+            } else {
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            const int q = 2 * g + t;
-            const float b = h[q >> 4][q & 15];
+                for (int rb = RBO; rb < RBI; ++rb) convert(rb);
+            }
+        } else {
+            const int q0 = 16 + (g - RBO) * KG;
 #pragma unroll
-            for (int rb = 0; rb < RBO; ++rb) acc[rb] = mfma_f32_32x32x2(ring.s[g % 4][rb][t], b, acc[rb]);
+            for (int t = 0; t < KG; ++t) {
+                const float b = B(q0 + t);
+#pragma unroll
+                for (int rb = RBO - 1; rb >= 0; --rb)
+                    out[rb] = mfma_f32_32x32x2(ring.v[g % 4][rb * KG + t], b, out[rb]);
+                if (ALPHA) sig = fmaf(wa[hh * 16 * RBI + q0 + t], b, sig);
+            }
         }
     }
 }
@@ -263,6 +320,22 @@ __device__ __forceinline__ void interleave_mfma_valu() {
     }
 }
 
+// u-part weight groups: 2 k-steps x RB row blocks = 2*RB floats per lane (slot float 2*rb + t)
+template <int RB>
+__device__ __forceinline__ void load_u_group(f32x2 (&slot)[RB], __amdgpu_buffer_rsrc_t rs, int lane, int g) {
+#pragma unroll
+    for (int i = 0; i < RB / 2; ++i) {
+        const f32x4 x = bload4(rs, lane * 16 + i * 1024, g * 2 * RB * 256);
+        slot[2 * i] = f32x2{x[0], x[1]};
+        slot[2 * i + 1] = f32x2{x[2], x[3]};
+    }
+}
+template <int RB>
+__device__ __forceinline__ void ring_take(f32x2 (&slot)[RB], const float (&v)[16]) {
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) slot[rb] = f32x2{v[2 * rb], v[2 * rb + 1]};
+}
+
 // One joint's skeleton row (3x4 of the world->joint transform) and window distance, loaded from
 // LDS into registers two MFMA groups before use, so the encoder math never waits on LDS.
 struct JRow {
@@ -307,16 +380,15 @@ template <int RB>
 __device__ __forceinline__ void u_part(f32x16 (&acc)[RB], const ModelDev& M, const float* __restrict__ wp,
                                        const float* __restrict__ sk, const float* __restrict__ cut, float px,
                                        float py, float pz, int lane, JointMask* mask, float* __restrict__ uf,
-                                       Ring<RB>& sh, const float* __restrict__ next, Stamps& st) {
+                                       Ring& sh, const float* __restrict__ next, Stamps& st) {
     const int hh = lane >> 5;
     const int njh2 = M.njh2;
     const int npp = njh2 / 2;
     const int total_groups = 3 * npp;
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(wp);
-    const int voff = lane * 8;
     f32x2 ring[3][RB];  // groups 0 and 1 were prefetched into the shared ring by the caller
-#pragma unroll
-    for (int rb = 0; rb < RB; ++rb) ring[0][rb] = sh.s[0][rb], ring[1][rb] = sh.s[1][rb];
+    ring_take<RB>(ring[0], sh.v[0]);
+    ring_take<RB>(ring[1], sh.v[1]);
     uint64_t m0 = 0, m1 = 0;
     float f[6];
     bool lv0, lv1;
@@ -352,8 +424,7 @@ __device__ __forceinline__ void u_part(f32x16 (&acc)[RB], const ModelDev& M, con
         for (int g = 0; g < 3; ++g) {
             __builtin_amdgcn_sched_barrier(0);
             const int gn = min(pp * 3 + g + 2, total_groups - 1);  // (a harmless reload at the end)
-#pragma unroll
-            for (int rb = 0; rb < RB; ++rb) ring[(g + 2) % 3][rb] = bload2(rs, voff, (gn * RB + rb) * 512);
+            load_u_group<RB>(ring[(g + 2) % 3], rs, lane, gn);
 #pragma unroll
             for (int t = 0; t < 2; ++t) {
                 const float b = f[2 * g + t];
@@ -381,22 +452,21 @@ __device__ __forceinline__ void u_part(f32x16 (&acc)[RB], const ModelDev& M, con
         mask->m0 = m0;
         mask->m1 = m1;
     }
-    if (next) ring_preload<RB, RB>(sh, next, lane);
+    if (next) ring_preload<16>(sh, next, lane);
 }
 
 // The skip layer's bone-direction part from the features u_part stored in LDS: a pure MFMA
 // stream (B operands read one group ahead) with the weight ring two groups ahead.
 template <int RB>
 __device__ __forceinline__ void u_part_lds(f32x16 (&acc)[RB], const ModelDev& M, const float* __restrict__ wp,
-                                           const float* __restrict__ uf, int lane, Ring<RB>& sh,
+                                           const float* __restrict__ uf, int lane, Ring& sh,
                                            const float* __restrict__ next) {
     const int total_groups = 3 * (M.njh2 / 2);
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(wp);
-    const int voff = lane * 8;
     const f32x2* ub = reinterpret_cast<const f32x2*>(uf) + lane;
     f32x2 ring[3][RB];
-#pragma unroll
-    for (int rb = 0; rb < RB; ++rb) ring[0][rb] = sh.s[0][rb], ring[1][rb] = sh.s[1][rb];
+    ring_take<RB>(ring[0], sh.v[0]);
+    ring_take<RB>(ring[1], sh.v[1]);
     f32x2 bc = ub[0];
     for (int g0 = 0; g0 < total_groups; g0 += 3) {
 #pragma unroll
@@ -404,8 +474,7 @@ __device__ __forceinline__ void u_part_lds(f32x16 (&acc)[RB], const ModelDev& M,
             __builtin_amdgcn_sched_barrier(0);
             const int g = g0 + gg;
             const int gn = min(g + 2, total_groups - 1);
-#pragma unroll
-            for (int rb = 0; rb < RB; ++rb) ring[(gg + 2) % 3][rb] = bload2(rs, voff, (gn * RB + rb) * 512);
+            load_u_group<RB>(ring[(gg + 2) % 3], rs, lane, gn);
             const f32x2 bn = ub[min(g + 1, total_groups - 1) * 64];
 #pragma unroll
             for (int t = 0; t < 2; ++t)
@@ -414,7 +483,7 @@ __device__ __forceinline__ void u_part_lds(f32x16 (&acc)[RB], const ModelDev& M,
             bc = bn;
         }
     }
-    if (next) ring_preload<RB, RB>(sh, next, lane);
+    if (next) ring_preload<16>(sh, next, lane);
 }
 
 template <int MR>
@@ -566,25 +635,24 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
 
     f32x16 acc[RB], h[RB];
     JointMask mask;
-    Ring<RB> ring;
-    ring_preload<RB, RB>(ring, net.wl[0], lane);  // the u part's first groups, early
+    Ring ring;
+    constexpr bool HANDOFF = (2 * RB == 16);  // u-part groups have the regs layers' group size
+    ring_preload<2 * RB>(ring, net.wl[0], lane);  // the u part's first groups, early
     load_bias<RB>(acc, bias, hh);
     STAMP(st, 10);
     u_part<RB>(acc, M, net.wl[0], sk, cut, px, py, pz, lane, &mask, uf, ring, M.D > 1 ? net.wl[1] : net.wfeat, st);
     STAMP(st, 8);
     v_part<RB, MR>(acc, M, net.wl0v, sk, cut, px, py, pz, lane, mask, st);
     STAMP(st, 9);
-#pragma unroll
-    for (int rb = 0; rb < RB; ++rb)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) h[rb][i] = relu(acc[rb][i]);
+    float sig = 0.0f;
     for (int L = 1; L < M.D; ++L) {
-        load_bias<RB>(acc, bias + L * W, hh);
-        STAMP(st, 10);
         const float* after = L + 1 < M.D ? net.wl[L + 1] : net.wfeat;
-        regs_layer<RB, RB, RB>(acc, h, net.wl[L], lane, ring, L == M.skip + 1 ? net.wskipu : after);
+        const bool skl = (L == M.skip + 1);
+        mlp_layer<RB, RB, true, true, false>(acc, acc, h, bias + L * W, net.wl[L], lane, ring,
+                                             skl ? (HANDOFF ? net.wskipu : nullptr) : after, nullptr, sig);
         STAMP(st, 11);
-        if (L == M.skip + 1) {  // x part after the h part: h is dead, its registers hold the ring
+        if (skl) {  // x part after the h part
+            if (!HANDOFF) ring_preload<2 * RB>(ring, net.wskipu, lane);
             if (uf)
                 u_part_lds<RB>(acc, M, net.wskipu, uf, lane, ring, after);
             else
@@ -592,33 +660,16 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
             v_part<RB, MR>(acc, M, net.wskipv, sk, cut, px, py, pz, lane, mask, st);
             STAMP(st, 12);
         }
-#pragma unroll
-        for (int rb = 0; rb < RB; ++rb)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) h[rb][i] = relu(acc[rb][i]);
     }
-    STAMP(st, 10);
-    // alpha head (VALU): this lane holds half of the W activations of sample sl
-    float sig = 0.0f;
-    {
-        const float* wa = net.walpha + hh * RB * 16;
-#pragma unroll
-        for (int rb = 0; rb < RB; ++rb)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) sig += wa[rb * 16 + i] * h[rb][i];
-        sig += __shfl_xor(sig, 32);
-        sig += net.balpha;
-    }
-    // feature_linear (no activation)
-    load_bias<RB>(acc, bias + M.D * W, hh);
-    regs_layer<RB, RB, RBV>(acc, h, net.wfeat, lane, ring, net.wview);
-#pragma unroll
-    for (int rb = 0; rb < RB; ++rb) h[rb] = acc[rb];
-    // views_linears.0: feature part + factorised direction/code/bias part, then relu
+    // feature_linear (no activation) with the alpha head folded in (both read relu(h_last))
+    mlp_layer<RB, RB, true, true, true>(acc, acc, h, bias + M.D * W, net.wfeat, lane, ring, net.wview,
+                                        bias + (M.D + 1) * W, sig);
+    sig += __shfl_xor(sig, 32);
+    sig += net.balpha;
+    // views_linears.0: feature part (B operands straight from the feature accumulators) +
+    // factorised direction/code/bias part, then relu
     f32x16 av[RBV];
-#pragma unroll
-    for (int rb = 0; rb < RBV; ++rb) av[rb] = f32x16{0};
-    regs_layer<RBV, RB, RBV>(av, h, net.wview, lane, ring, nullptr);
+    mlp_layer<RBV, RB, false, false, false>(av, acc, h, nullptr, net.wview, lane, ring, nullptr, nullptr, sig);
     view_dir_part<RBV>(av, M, G, sk, cut, px, py, pz, lane);
     float rgb[3];
 #pragma unroll
@@ -628,7 +679,7 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
 #pragma unroll
         for (int rb = 0; rb < RBV; ++rb)
 #pragma unroll
-            for (int i = 0; i < 16; ++i) a += wr[rb * 16 + i] * relu(av[rb][i]);
+            for (int i = 0; i < 16; ++i) a += wr[rb * 16 + i] * relu_act(av[rb][i]);
         a += __shfl_xor(a, 32);
         rgb[c] = a + net.brgb[c];
     }
@@ -946,9 +997,9 @@ __global__ __launch_bounds__(256, 1) void render_kernel(ModelDev M, RenderArgs A
         const NetDev& net = M.net[pass];
         const int n = pass == 0 ? S : T;
         const int zoff = pass == 0 ? P.zc : P.zf;
-        for (int idx = tid; idx < (M.D + 1) * W; idx += blockDim.x) {  // biases -> LDS (synced below)
+        for (int idx = tid; idx < (M.D + 2) * W; idx += blockDim.x) {  // biases, w_alpha -> LDS (synced below)
             const int L = idx / W, e = idx % W;
-            lds[P.bias + idx] = L < M.D ? net.bl[L][e] : net.bfeat[e];
+            lds[P.bias + idx] = L < M.D ? net.bl[L][e] : (L == M.D ? net.bfeat[e] : net.walpha[e]);
         }
         compute_view_factor<WH, 4>(M, net, lds, P, nr, tid);
         STAMP(st, 1);
@@ -1214,19 +1265,45 @@ std::vector<float> pack_kmajor(const float* Wt, int n_out, int ld, int nq, F kma
     return out;
 }
 
-std::vector<float> pack_regs(const float* Wt, int n_out, int ld, int col_off, int n_in) {
-    return pack_kmajor(Wt, n_out, ld, n_in / 2, [&](int q, int h) {
-        return col_off + 32 * (q >> 4) + acc_row(q & 15, h);
+// ng groups of F floats per lane, stored [group][F/4][64 lanes][4] (one 1 KiB b128 load per F/4);
+// fn(g, s, lane) = value of slot float s of lane `lane` in group g
+template <class Fn>
+std::vector<float> pack_groups(int ng, int F, Fn fn) {
+    std::vector<float> out((size_t)ng * F * 64, 0.0f);
+    for (int g = 0; g < ng; ++g)
+        for (int i = 0; i < F / 4; ++i)
+            for (int l = 0; l < 64; ++l)
+                for (int e = 0; e < 4; ++e) out[(((size_t)g * (F / 4) + i) * 64 + l) * 4 + e] = fn(g, 4 * i + e, l);
+    return out;
+}
+
+// dense layer for mlp_layer: RBO lead groups (block rb, k-steps 0..15) then k-major groups of
+// KG = 16/RBO k-steps x RBO blocks (slot float rb*KG + t); k-step q, half h -> input column
+// col_off + 32 (q >> 4) + acc_row(q & 15, h)
+std::vector<float> pack_layer(const float* Wt, int n_out, int ld, int col_off, int n_in) {
+    const int RBO = n_out / 32, RBI = n_in / 32, KG = 16 / RBO;
+    const int ng = RBO + (16 * RBI - 16) / KG;
+    return pack_groups(ng, 16, [&](int g, int sl, int l) {
+        int rb, q;
+        if (g < RBO) {
+            rb = g, q = sl;
+        } else {
+            rb = sl / KG, q = 16 + (g - RBO) * KG + sl % KG;
+        }
+        const int col = col_off + 32 * (q >> 4) + acc_row(q & 15, l >> 5);
+        return Wt[(size_t)(32 * rb + (l & 31)) * ld + col];
     });
 }
 
-// bone-direction part: k-step q = 3p + c, half h -> joint p + h*njh2, column nv*nj + 3j + c
+// bone-direction part: k-step q = 3p + c, half h -> joint p + h*njh2, column nv*nj + 3j + c;
+// groups of 2 k-steps x RB blocks (slot float 2 rb + t)
 std::vector<float> pack_upart(const float* Wt, int n_out, int ld, int nj, int njh2, int mr) {
-    const int nv = 1 + 2 * mr;
-    return pack_kmajor(Wt, n_out, ld, 3 * njh2, [&](int q, int h) {
+    const int nv = 1 + 2 * mr, RB = n_out / 32;
+    return pack_groups(3 * njh2 / 2, 2 * RB, [&](int g, int sl, int l) {
+        const int rb = sl / 2, q = 2 * g + sl % 2;
         const int p = q / 3, c = q % 3;
-        const int j = p + h * njh2;
-        return j < nj ? nv * nj + 3 * j + c : -1;
+        const int j = p + (l >> 5) * njh2;
+        return j < nj ? Wt[(size_t)(32 * rb + (l & 31)) * ld + nv * nj + 3 * j + c] : 0.0f;
     });
 }
 
@@ -1341,7 +1418,7 @@ static int pack_net(const anerf_model_desc* d, int njh2, const anerf_net_weights
     offs.push_back(pk.add(pack_upart(w->pts_w[0], W, cin, nj, njh2, mr)));
     for (int i = 1; i < d->net_depth; ++i) {
         const bool sk = (i == d->skip + 1);
-        offs.push_back(pk.add(pack_regs(w->pts_w[i], W, sk ? cin + W : W, sk ? cin : 0, W)));
+        offs.push_back(pk.add(pack_layer(w->pts_w[i], W, sk ? cin + W : W, sk ? cin : 0, W)));
     }
     offs.push_back(pk.add(pack_vpart(w->pts_w[0], W, cin, nj, mr)));
     const int skl = d->skip + 1;
@@ -1354,9 +1431,9 @@ static int pack_net(const anerf_model_desc* d, int njh2, const anerf_net_weights
     }
     for (int i = 0; i < d->net_depth; ++i) offs.push_back(pk.add(pack_rowvec(w->pts_b[i], W, false)));
     offs.push_back(pk.add(pack_rowvec(w->alpha_w, W, true)));                         // walpha
-    offs.push_back(pk.add(pack_regs(w->feature_w, W, W, 0, W)));                      // wfeat
+    offs.push_back(pk.add(pack_layer(w->feature_w, W, W, 0, W)));                     // wfeat
     offs.push_back(pk.add(pack_rowvec(w->feature_b, W, false)));                      // bfeat
-    offs.push_back(pk.add(pack_regs(w->views_w, WH, ldv, 0, W)));                     // wview
+    offs.push_back(pk.add(pack_layer(w->views_w, WH, ldv, 0, W)));                    // wview
     {
         std::vector<float> t((size_t)nj * nk * 3 * WH);
         for (int j = 0; j < nj; ++j)
