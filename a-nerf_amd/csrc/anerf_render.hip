@@ -614,6 +614,44 @@ __device__ __forceinline__ void view_dir_part(f32x16 (&acc)[RBV], const ModelDev
     }
 }
 
+// Encoder + density trunk of one 32-sample block: L0 (u and v parts), the hidden layers with the
+// skip; acc ends as the pre-activation of the last hidden layer.  `after_last` is the weight stream
+// that follows (the feature layer, or nothing for density-only queries).
+template <int W, int MR>
+__device__ __forceinline__ void mlp_trunk(const ModelDev& M, const NetDev& net, const float* __restrict__ sk,
+                                          const float* __restrict__ cut, float px, float py, float pz, int lane,
+                                          const float* __restrict__ bias, float* __restrict__ uf,
+                                          f32x16 (&acc)[W / 32], f32x16 (&h)[W / 32], Ring& ring, JointMask& mask,
+                                          const float* __restrict__ after_last, Stamps& st) {
+    constexpr int RB = W / 32;
+    const int hh = lane >> 5;
+    float nosig = 0.0f;
+    constexpr bool HANDOFF = (2 * RB == 16);  // u-part groups have the regs layers' group size
+    ring_preload<2 * RB>(ring, net.wl[0], lane);  // the u part's first groups, early
+    load_bias<RB>(acc, bias, hh);
+    STAMP(st, 10);
+    u_part<RB>(acc, M, net.wl[0], sk, cut, px, py, pz, lane, &mask, uf, ring, M.D > 1 ? net.wl[1] : after_last, st);
+    STAMP(st, 8);
+    v_part<RB, MR>(acc, M, net.wl0v, sk, cut, px, py, pz, lane, mask, st);
+    STAMP(st, 9);
+    for (int L = 1; L < M.D; ++L) {
+        const float* after = L + 1 < M.D ? net.wl[L + 1] : after_last;
+        const bool skl = (L == M.skip + 1);
+        mlp_layer<RB, RB, true, true, false>(acc, acc, h, bias + L * W, net.wl[L], lane, ring,
+                                             skl ? (HANDOFF ? net.wskipu : nullptr) : after, nullptr, nosig);
+        STAMP(st, 11);
+        if (skl) {  // x part after the h part
+            if (!HANDOFF) ring_preload<2 * RB>(ring, net.wskipu, lane);
+            if (uf)
+                u_part_lds<RB>(acc, M, net.wskipu, uf, lane, ring, after);
+            else
+                u_part<RB>(acc, M, net.wskipu, sk, cut, px, py, pz, lane, nullptr, nullptr, ring, after, st);
+            v_part<RB, MR>(acc, M, net.wskipv, sk, cut, px, py, pz, lane, mask, st);
+            STAMP(st, 12);
+        }
+    }
+}
+
 // One 32-sample block of one ray through a whole NeRF: raw (rgb, sigma) into LDS.
 template <int W, int MR>
 __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __restrict__ ray,
@@ -636,31 +674,8 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
     f32x16 acc[RB], h[RB];
     JointMask mask;
     Ring ring;
-    constexpr bool HANDOFF = (2 * RB == 16);  // u-part groups have the regs layers' group size
-    ring_preload<2 * RB>(ring, net.wl[0], lane);  // the u part's first groups, early
-    load_bias<RB>(acc, bias, hh);
-    STAMP(st, 10);
-    u_part<RB>(acc, M, net.wl[0], sk, cut, px, py, pz, lane, &mask, uf, ring, M.D > 1 ? net.wl[1] : net.wfeat, st);
-    STAMP(st, 8);
-    v_part<RB, MR>(acc, M, net.wl0v, sk, cut, px, py, pz, lane, mask, st);
-    STAMP(st, 9);
+    mlp_trunk<W, MR>(M, net, sk, cut, px, py, pz, lane, bias, uf, acc, h, ring, mask, net.wfeat, st);
     float sig = 0.0f;
-    for (int L = 1; L < M.D; ++L) {
-        const float* after = L + 1 < M.D ? net.wl[L + 1] : net.wfeat;
-        const bool skl = (L == M.skip + 1);
-        mlp_layer<RB, RB, true, true, false>(acc, acc, h, bias + L * W, net.wl[L], lane, ring,
-                                             skl ? (HANDOFF ? net.wskipu : nullptr) : after, nullptr, sig);
-        STAMP(st, 11);
-        if (skl) {  // x part after the h part
-            if (!HANDOFF) ring_preload<2 * RB>(ring, net.wskipu, lane);
-            if (uf)
-                u_part_lds<RB>(acc, M, net.wskipu, uf, lane, ring, after);
-            else
-                u_part<RB>(acc, M, net.wskipu, sk, cut, px, py, pz, lane, nullptr, nullptr, ring, after, st);
-            v_part<RB, MR>(acc, M, net.wskipv, sk, cut, px, py, pz, lane, mask, st);
-            STAMP(st, 12);
-        }
-    }
     // feature_linear (no activation) with the alpha head folded in (both read relu(h_last))
     mlp_layer<RB, RB, true, true, true>(acc, acc, h, bias + M.D * W, net.wfeat, lane, ring, net.wview,
                                         bias + (M.D + 1) * W, sig);
@@ -1061,6 +1076,79 @@ __global__ __launch_bounds__(256, 1) void render_kernel(ModelDev M, RenderArgs A
         STAMP(st, 3 + 2 * pass);
     }
     STAMP_FLUSH(st, A.stamps);
+}
+
+// ======================================================================= density-only queries
+// RayCaster.render_pts_density / render_mesh_density (core/raycasters.py:579-648): the trunk of
+// one network and alpha_linear at arbitrary points (or at the (res+1)^3 mesh grid, generated here:
+// point (a, b, c) = (t[b], t[a], t[c]) + kp0, the 'xy' meshgrid order of the reference).
+struct DensityArgs {
+    const float* pts;  // N x 3, or NULL for the grid
+    const float* t;    // grid axis, res1 floats
+    const float* kp0;  // 3
+    int64_t res1;
+    int64_t n;
+    const float* skts;  // NJ x 16, one pose
+    int net;
+    float* out;  // N raw densities
+};
+
+__host__ __device__ inline LdsPlan make_density_plan(int nj, int W, int D, int njh2) {
+    LdsPlan p;
+    std::memset(&p, 0, sizeof(p));
+    int o = 0;
+    p.sk = o; o += 12 * nj;
+    p.cut = o; o += 2 * nj;
+    o = (o + 3) & ~3;
+    p.bias = o; o += (D + 2) * W;
+    p.uf_stride = 64 * 3 * njh2;
+    p.uf = o; o += 4 * p.uf_stride;
+    p.total = (o + 3) & ~3;
+    return p;
+}
+
+template <int W, int MR>
+__global__ __launch_bounds__(256, 1) void density_kernel(ModelDev M, DensityArgs A, LdsPlan P) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    constexpr int RB = W / 32;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hh = lane >> 5;
+    const NetDev& net = M.net[A.net];
+    for (int idx = tid; idx < M.nj * 12; idx += blockDim.x) lds[P.sk + idx] = A.skts[(idx / 12) * 16 + idx % 12];
+    for (int j = tid; j < 2 * M.nj; j += blockDim.x) lds[P.cut + j] = j < M.nj ? M.cutoff[j] : M.cutoff_v[j - M.nj];
+    for (int idx = tid; idx < (M.D + 2) * W; idx += blockDim.x) {
+        const int L = idx / W, e = idx % W;
+        lds[P.bias + idx] = L < M.D ? net.bl[L][e] : (L == M.D ? net.bfeat[e] : net.walpha[e]);
+    }
+    __syncthreads();
+    Stamps st;
+    float* uf = (M.skip + 1 < M.D) ? lds + P.uf + wave * P.uf_stride : nullptr;
+    const float* wa = lds + P.bias + (M.D + 1) * W + hh * (W / 2);
+    const int64_t nb = (A.n + 31) / 32;
+    for (int64_t b = (int64_t)blockIdx.x * 4 + wave; b < nb; b += (int64_t)gridDim.x * 4) {
+        const int64_t s_out = b * 32 + (lane & 31);
+        const int64_t s = s_out < A.n ? s_out : A.n - 1;
+        float px, py, pz;
+        if (A.pts) {
+            px = A.pts[3 * s], py = A.pts[3 * s + 1], pz = A.pts[3 * s + 2];
+        } else {
+            const int64_t a = s / (A.res1 * A.res1), r = s % (A.res1 * A.res1);
+            px = A.t[r / A.res1] + A.kp0[0];
+            py = A.t[a] + A.kp0[1];
+            pz = A.t[r % A.res1] + A.kp0[2];
+        }
+        f32x16 acc[RB], h[RB];
+        JointMask mask;
+        Ring ring;
+        mlp_trunk<W, MR>(M, net, lds + P.sk, lds + P.cut, px, py, pz, lane, lds + P.bias, uf, acc, h, ring, mask,
+                         nullptr, st);
+        // alpha_linear on relu(h_last), in the k-step order of the render path's fused alpha head
+        float sig = 0.0f;
+#pragma unroll
+        for (int q = 0; q < W / 2; ++q) sig = fmaf(wa[q], relu_act(acc[q >> 4][q & 15]), sig);
+        sig += __shfl_xor(sig, 32);
+        sig += net.balpha;
+        if (hh == 0 && s_out < A.n) A.out[s_out] = sig;
+    }
 }
 
 // ======================================================================= small kernels
@@ -1777,6 +1865,69 @@ int anerf_encode_points(const anerf_model* m, const float* skts, const float* pt
                        pts, dirs, n_points, feat_out);
     HIP_TRY(hipGetLastError());
     return ANERF_OK;
+}
+
+static int launch_density(const anerf_model* m, DensityArgs a, void* stream) {
+    if (a.n == 0) return ANERF_OK;
+    int dev = -1;
+    HIP_TRY(hipGetDevice(&dev));
+    if (dev != m->device) return fail(ANERF_EINVAL, "current device differs from the model's device");
+    if (a.net < 0) a.net = m->desc.has_fine ? 1 : 0;  // the reference's default network (raycasters.py:616-620)
+    if (a.net > 1 || (a.net == 1 && !m->desc.has_fine)) return fail(ANERF_EINVAL, "no such network");
+    const int W = m->desc.net_width, mr = m->desc.multires;
+    const LdsPlan P = make_density_plan(m->desc.n_joints, W, m->desc.net_depth, m->njh2);
+    if (P.total * 4 > 160 * 1024) return fail(ANERF_EINVAL, "configuration exceeds the 160 KiB LDS budget");
+    const int64_t nb = (a.n + 31) / 32;
+    const unsigned grid = (unsigned)std::min<int64_t>((nb + 3) / 4, 256 * 32);
+    const size_t lds_bytes = (size_t)P.total * 4;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+#define ANERF_LAUNCH(WW, MM)                                                                         \
+    do {                                                                                            \
+        auto kfn = density_kernel<WW, MM>;                                                          \
+        HIP_TRY(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,  \
+                                    (int)lds_bytes));                                               \
+        hipLaunchKernelGGL(kfn, dim3(grid), dim3(256), lds_bytes, st, m->md, a, P);                \
+    } while (0)
+    if (W == 256 && mr == 7) ANERF_LAUNCH(256, 7);
+    else if (W == 128 && mr == 7) ANERF_LAUNCH(128, 7);
+    else if (W == 64 && mr == 7) ANERF_LAUNCH(64, 7);
+    else if (W == 256 && mr == 10) ANERF_LAUNCH(256, 10);
+    else if (W == 128 && mr == 10) ANERF_LAUNCH(128, 10);
+    else if (W == 64 && mr == 10) ANERF_LAUNCH(64, 10);
+    else return fail(ANERF_EINVAL, "no kernel instance for this width / multires");
+#undef ANERF_LAUNCH
+    HIP_TRY(hipGetLastError());
+    return ANERF_OK;
+}
+
+int anerf_density_points(const anerf_model* m, const float* pts, int64_t n_points, const float* skts, int32_t net,
+                         float* raw_out, void* stream) {
+    if (!m || n_points < 0) return fail(ANERF_EINVAL, "anerf_density_points: bad arguments");
+    if (n_points == 0) return ANERF_OK;
+    if (!pts || !skts || !raw_out) return fail(ANERF_EINVAL, "anerf_density_points: bad arguments");
+    DensityArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.pts = pts;
+    a.n = n_points;
+    a.skts = skts;
+    a.net = net;
+    a.out = raw_out;
+    return launch_density(m, a, stream);
+}
+
+int anerf_density_grid(const anerf_model* m, const float* axis, int32_t res1, const float* kp0, const float* skts,
+                       int32_t net, float* raw_out, void* stream) {
+    if (!m || !axis || !kp0 || !skts || !raw_out || res1 < 1) return fail(ANERF_EINVAL, "anerf_density_grid: bad arguments");
+    DensityArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.t = axis;
+    a.kp0 = kp0;
+    a.res1 = res1;
+    a.n = (int64_t)res1 * res1 * res1;
+    a.skts = skts;
+    a.net = net;
+    a.out = raw_out;
+    return launch_density(m, a, stream);
 }
 
 }  // extern "C"

@@ -44,6 +44,7 @@ class DeviceModel:
         d.softplus_shift, d.density_scale = cfg.softplus_shift, cfg.density_scale
         fine_sd = ckpt.get("network_fine_state_dict")
         d.has_fine = int(fine_sd is not None and cfg.N_importance > 0)
+        self.has_fine = bool(d.has_fine)
         coarse = self._net(ckpt["network_fn_state_dict"])
         fine = self._net(fine_sd) if d.has_fine else None
         e, ev = ckpt["embed_state_dict"], ckpt["embeddirs_state_dict"]

@@ -7,8 +7,9 @@ dozen ATen ops per stage happens in one fused launch (`anerf_render_rays`).
 
 Supported: eval-mode rendering (`perturb=0`, `raw_noise_std=0`, `ray_noise_std=0`,
 `lindisp=False`), any per-ray poses (`skts`/`cyls` may be expanded views of one pose —
-detected without copying — or genuinely per-ray), framecodes via `cams`.  Anything else
-raises `NotImplementedError`; nothing silently falls back to the CPU.
+detected without copying — or genuinely per-ray), framecodes via `cams`; density-only
+queries `fwd_type='density'` / `'mesh'` (`render_pts_density` / `render_mesh_density`,
+:579-648).  Anything else raises `NotImplementedError`; nothing silently falls back to the CPU.
 """
 import ctypes
 import glob
@@ -64,9 +65,74 @@ class RayCaster:
         return self.forward(*args, fwd_type=fwd_type, **kwargs)
 
     def forward(self, *args, fwd_type="", **kwargs):
+        """core/raycasters.py:349-359."""
+        if fwd_type == "density":
+            return self.render_pts_density(*args, **kwargs)
+        if fwd_type == "mesh":
+            return self.render_mesh_density(*args, **kwargs)
+        if fwd_type == "density_color":
+            raise NotImplementedError("fwd_type='density_color' needs texture layers the NeRF model does not have")
         if fwd_type:
-            raise NotImplementedError(f"fwd_type={fwd_type!r} (density / mesh queries) is not implemented yet")
+            raise ValueError(f"unknown fwd_type {fwd_type!r}")
         return self.render_rays(*args, **kwargs)
+
+    # ------------------------------------------------------------------ density-only queries
+    def _net_index(self, network):
+        if network is None or network == -1:
+            return -1  # fine if the model has one (raycasters.py:616-620)
+        if network in ("coarse", 0):
+            return 0
+        if network in ("fine", 1):
+            if not self.model.has_fine:
+                raise ValueError("this model has no fine network")
+            return 1
+        raise ValueError(f"network must be None, 'coarse' or 'fine', got {network!r}")
+
+    def _one_pose(self, skts, dev):
+        sk = torch.as_tensor(skts).to(dev, torch.float32)
+        nj = self.cfg.n_joints
+        sk = sk.reshape(-1, nj, 4, 4)
+        if sk.shape[0] != 1 and not (sk.stride(0) == 0):
+            raise NotImplementedError("density queries take one pose (skts of shape (1, NJ, 4, 4))")
+        return sk[:1].contiguous()
+
+    @torch.no_grad()
+    def render_pts_density(self, pts, kps, skts, bones, render_kwargs=None, subject_idxs=None, netchunk=1024 * 64,
+                           network=None, color=False, v=None):
+        """Raw density (alpha_linear, before the density activation) at points, shape
+        pts.shape[:-1] + (1,)  (core/raycasters.py:597-648; `netchunk` is only a batching hint there)."""
+        if color:
+            raise NotImplementedError("color=True needs texture layers the NeRF model does not have")
+        if subject_idxs is not None or v is not None:
+            raise NotImplementedError("subject_idxs / precomputed kp inputs are not supported")
+        dev = torch.device(f"cuda:{self.model.device}")
+        p = torch.as_tensor(pts).to(dev, torch.float32)
+        shape = p.shape[:-1]
+        p = p.reshape(-1, 3).contiguous()
+        sk = self._one_pose(skts, dev)
+        out = torch.empty(p.shape[0], device=dev, dtype=torch.float32)
+        _lib.check(_lib.load().anerf_density_points(self.model.handle, _lib.ptr(p), p.shape[0], _lib.ptr(sk),
+                                                    self._net_index(network), _lib.ptr(out),
+                                                    _lib.stream_handle(dev)), "anerf_density_points")
+        return out.reshape(*shape, 1)
+
+    @torch.no_grad()
+    def render_mesh_density(self, kps, skts, bones, subject_idxs=None, radius=1.0, res=64, render_kwargs=None,
+                            netchunk=1024 * 64, v=None, network=None):
+        """Raw density on the (res+1)^3 grid around kps[0, 0] (core/raycasters.py:579-595), generated
+        on the device; same grid and element order as the reference's meshgrid."""
+        if subject_idxs is not None or v is not None:
+            raise NotImplementedError("subject_idxs / precomputed kp inputs are not supported")
+        dev = torch.device(f"cuda:{self.model.device}")
+        res1 = int(res) + 1
+        axis = torch.from_numpy(np.linspace(-radius, radius, res1).astype(np.float32)).to(dev)
+        kp0 = torch.as_tensor(kps).to(dev, torch.float32).reshape(-1, 3)[0].contiguous()
+        sk = self._one_pose(skts, dev)
+        out = torch.empty((res1, res1, res1), device=dev, dtype=torch.float32)
+        _lib.check(_lib.load().anerf_density_grid(self.model.handle, _lib.ptr(axis), res1, _lib.ptr(kp0),
+                                                  _lib.ptr(sk), self._net_index(network), _lib.ptr(out),
+                                                  _lib.stream_handle(dev)), "anerf_density_grid")
+        return out
 
     def render_rays(self, ray_batch, N_samples, kp_batch=None, skts=None, cyls=None, bones=None, cams=None,
                     subject_idxs=None, retraw=False, lindisp=False, perturb=0., N_importance=0, network_fine=None,

@@ -17,6 +17,9 @@
  *   anerf_encode_points     encode_inputs + embedders (stage / debug)          core/raycasters.py:476-555
  *   anerf_near_far          get_near_far_in_cylinder (stage)                   core/utils/ray_utils.py:292-344
  *   anerf_compose           render_path's image composition + NaN disp -> 0    run_nerf.py:100-141
+ *   anerf_density_points    RayCaster.render_pts_density (fwd_type='density')  core/raycasters.py:597-648
+ *   anerf_density_grid      RayCaster.render_mesh_density (fwd_type='mesh')    core/raycasters.py:579-595
+ *                           (called by run_render.render_mesh)                 run_render.py:970-986
  */
 #ifndef ANERF_H
 #define ANERF_H
@@ -152,6 +155,18 @@ int anerf_near_far(const float* ray_batch, int32_t ray_stride, int64_t n_rays, c
  * joint transforms skts [NJ][4][4]; F = NJ(1+2 multires) + 3NJ + 3NJ(1+2 multires_views). */
 int anerf_encode_points(const anerf_model* m, const float* skts, const float* pts, const float* dirs,
                         int64_t n_points, float* feat_out, void* stream);
+
+/* Raw density (alpha_linear output, before the density activation) of the trunk of one network at
+ * points pts [n][3] in world space, one pose skts [NJ][4][4]: _get_density_fwd_fn's fwd_fn.
+ * net: 0 coarse, 1 fine, -1 the reference's default (fine if the model has one). */
+int anerf_density_points(const anerf_model* m, const float* pts, int64_t n_points, const float* skts, int32_t net,
+                         float* raw_out, void* stream);
+
+/* The same on render_mesh_density's grid, generated on the device: raw_out [res1][res1][res1],
+ * element (a, b, c) at (axis[b], axis[a], axis[c]) + kp0 (numpy 'xy' meshgrid order), where
+ * axis [res1] = float32(linspace(-radius, radius, res1)) and kp0 [3] = kps[0, 0]. */
+int anerf_density_grid(const anerf_model* m, const float* axis, int32_t res1, const float* kp0, const float* skts,
+                       int32_t net, float* raw_out, void* stream);
 
 #ifdef __cplusplus
 }

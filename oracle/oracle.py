@@ -130,6 +130,14 @@ class OracleModel:
         lib().oracle_encode(self.ref, _p(sk), _p(pts), _p(dirs), ctypes.c_int64(M), _p(out))
         return out
 
+    def density(self, skts, pts, fine=False):
+        """Raw density (alpha_linear output) of the density trunk at points (N, 3): the path of
+        RayCaster.render_pts_density / _get_density_fwd_fn (core/raycasters.py:597-648) -- the
+        trunk reads only the point part of the encoding, so the view directions are arbitrary."""
+        pts = _f32(pts).reshape(-1, 3)
+        feat = self.encode(skts, pts, np.ones_like(pts))
+        return self.network(feat, fine=fine)[:, 3].copy()
+
     def network(self, feat, fine=False, code=None):
         feat = _f32(feat)
         M = feat.shape[0]
@@ -199,6 +207,14 @@ def gen_rays(c2w, H, W, focal, idx, center=None, near=0.0, far=1.0):
                           ctypes.c_float(cy), idx.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
                           ctypes.c_int64(idx.shape[0]), ctypes.c_float(near), ctypes.c_float(far), _p(out))
     return out
+
+
+def mesh_grid_points(radius, res, kp0):
+    """Grid of render_mesh_density (core/raycasters.py:583-588): float64 linspace, 'xy' meshgrid,
+    cast to float32, then + kps[0, 0] in float32.  Returns ((res+1)^3, 3)."""
+    t = np.linspace(-radius, radius, res + 1)
+    g = np.stack(np.meshgrid(t, t, t), axis=-1).astype(np.float32).reshape(-1, 3)
+    return (g + np.asarray(kp0, np.float32)).astype(np.float32)
 
 
 def linspace(n):

@@ -91,6 +91,12 @@ CONFIGS = {
     "h1_nanfill_s32i16_d4w128": dict(H=128, NJ=24, S=32, I=16, D=4, W=128, tau=20.0, kind="nanfill", seed=15),
     # per-frame code (opt_framecode, mixamo configs) with cam index >= 0 and the eval-mode mean code (< 0)
     "fc_64_s32i32_d4w128": dict(H=64, NJ=24, S=32, I=32, D=4, W=128, tau=20.0, kind="framecode", n_rays=192, seed=16),
+    # density-only queries (RayCaster.forward fwd_type='mesh' / 'density', core/raycasters.py:579-648):
+    # the fine net of the config-3 model, and the coarse-only D=4 model
+    "dm_fine_d8w256": dict(H=64, NJ=24, S=64, I=128, D=8, W=256, tau=79.6, kind="density", seed=13, res=16,
+                           radius=1.8, n_pts=1000),
+    "dm_coarse_d4w128": dict(H=64, NJ=24, S=32, I=0, D=4, W=128, tau=20.0, kind="density", seed=11, res=12,
+                             radius=1.8, n_pts=600),
 }
 
 
@@ -196,8 +202,38 @@ def stage_dump(mods, render_kwargs, o, d, sc, n_stage, cams=None):
     return {"stage_" + k: v for k, v in out.items()}
 
 
+def make_density(name, cfg, mods, tmp):
+    """fwd_type='mesh' on a small grid and fwd_type='density' on scattered points (frame 0 pose)."""
+    import torch
+    args, render_kwargs, ck = build_reference(mods, cfg, os.path.join(tmp, name))
+    sc = scene_for(cfg)
+    rc = render_kwargs["ray_caster"]
+    pk = render_kwargs["preproc_kwargs"]
+    kps = torch.from_numpy(sc["kps"][0:1])
+    skts = torch.from_numpy(sc["skts"][0:1])
+    bones = torch.from_numpy(sc["bones"][0:1])
+    rng = np.random.default_rng(cfg["seed"] + 100)
+    pts = (sc["kps"][0][rng.integers(0, cfg["NJ"], cfg["n_pts"])] +
+           rng.normal(0.0, 0.15, (cfg["n_pts"], 3))).astype(np.float32)
+    with torch.no_grad():
+        grid = rc(kps=kps, skts=skts, bones=bones, radius=cfg["radius"], render_kwargs=pk, res=cfg["res"],
+                  netchunk=1024, fwd_type="mesh")
+        dens = rc(torch.from_numpy(pts).reshape(-1, 1, 3), kps, skts, bones, render_kwargs=pk, netchunk=1024,
+                  fwd_type="density")
+    meta = dict(seed=cfg["seed"], sha256=anerf_syn.checkpoint_sha256(ck), NJ=cfg["NJ"], S=cfg["S"], I=cfg["I"],
+                D=cfg["D"], W=cfg["W"], tau=cfg["tau"], H=sc["H"], focal=sc["focal"], ext_scale=0.001, chunk=4096,
+                framecode=0, res=cfg["res"], radius=cfg["radius"])
+    data = {"kps": sc["kps"][0:1], "skts": sc["skts"][0:1], "bones": sc["bones"][0:1], "pts": pts,
+            "grid_density": grid.numpy(), "pts_density": dens.numpy()}
+    path = os.path.join(HERE, name + ".npz")
+    np.savez_compressed(path, meta=np.array(repr(meta)), **data)
+    print(f"wrote {path}  grid={grid.shape}  pts={dens.shape}  ({os.path.getsize(path) / 1024:.0f} KiB)")
+
+
 def make(name, cfg, mods, tmp):
     import torch
+    if cfg["kind"] == "density":
+        return make_density(name, cfg, mods, tmp)
     run_nerf = mods[0]
     args, render_kwargs, ck = build_reference(mods, cfg, os.path.join(tmp, name))
     sc = scene_for(cfg)

@@ -213,3 +213,70 @@ def test_full_size_frame_properties():
                                         kp=torch.from_numpy(sc["kps"]), skts=torch.from_numpy(sc["skts"]),
                                         ext_scale=0.001, to_host=False)
     assert torch.equal(frames2[0][0], rgb) and torch.equal(frames2[0][1], disp)
+
+
+# ---------------------------------------------------------------- density-only queries (§8f row 1)
+DENSITY = ["dm_fine_d8w256", "dm_coarse_d4w128"]
+TOL_DENSITY = 1e-4  # raw alpha_linear output, |x| <= ~3 on these fixtures (MFMA vs MKL summation order)
+
+
+@pytest.mark.parametrize("name", DENSITY)
+def test_mesh_density_grid_matches_reference(name):
+    """fwd_type='mesh': the (res+1)^3 grid generated on the device, element order and values."""
+    g = Golden(name)
+    rc = _caster(g)
+    out = rc(kps=torch.from_numpy(g["kps"]), skts=torch.from_numpy(g["skts"]), bones=torch.from_numpy(g["bones"]),
+             radius=g.meta["radius"], res=g.meta["res"], render_kwargs={}, netchunk=1024, fwd_type="mesh")
+    torch.cuda.synchronize()
+    ref = g["grid_density"]
+    assert tuple(out.shape) == ref.shape
+    assert _maxdiff(out.cpu().numpy(), ref) <= TOL_DENSITY
+
+
+@pytest.mark.parametrize("name", DENSITY)
+def test_pts_density_matches_reference(name):
+    g = Golden(name)
+    rc = _caster(g)
+    pts = torch.from_numpy(g["pts"]).reshape(-1, 1, 3)
+    out = rc(pts, torch.from_numpy(g["kps"]), torch.from_numpy(g["skts"]), torch.from_numpy(g["bones"]),
+             render_kwargs={}, fwd_type="density")
+    torch.cuda.synchronize()
+    ref = g["pts_density"]
+    assert tuple(out.shape) == ref.shape
+    assert _maxdiff(out.cpu().numpy(), ref) <= TOL_DENSITY
+
+
+def test_density_matches_oracle_both_nets_and_ragged():
+    """Config-3 model, coarse and fine trunks, 5000 scattered points (ragged last block) vs the oracle;
+    the density of a point equals the raw sigma the render path computes for the same sample."""
+    orc = _oracle()
+    g = Golden("dm_fine_d8w256")
+    om = orc.OracleModel(g.cfg, g.ckpt)
+    rc = _caster(g)
+    rng = np.random.default_rng(3)
+    pts = (g["kps"][0][rng.integers(0, 24, 5003)] + rng.normal(0, 0.2, (5003, 3))).astype(np.float32)
+    for net, fine in (("coarse", False), ("fine", True)):
+        ref = om.density(g["skts"][0], pts, fine=fine)
+        out = rc.render_pts_density(torch.from_numpy(pts), None, torch.from_numpy(g["skts"]), None, network=net)
+        torch.cuda.synchronize()
+        assert out.shape == (5003, 1)
+        assert _maxdiff(out.cpu().numpy()[:, 0], ref) <= TOL_DENSITY * max(1.0, float(np.abs(ref).max())), net
+    one = rc.render_pts_density(torch.from_numpy(pts[7:8]), None, torch.from_numpy(g["skts"]), None)
+    full = rc.render_pts_density(torch.from_numpy(pts), None, torch.from_numpy(g["skts"]), None)
+    np.testing.assert_array_equal(one.cpu().numpy()[0], full.cpu().numpy()[7])  # points are independent
+    empty = rc.render_pts_density(torch.from_numpy(pts[:0]), None, torch.from_numpy(g["skts"]), None)
+    assert empty.shape == (0, 1)
+
+
+def test_density_grid_equals_points_path():
+    """The device-generated grid is the reference's numpy grid: grid and explicit points agree bit-exactly."""
+    orc = _oracle()
+    g = Golden("dm_coarse_d4w128")
+    rc = _caster(g)
+    res, radius = 9, 1.3
+    grid = rc.render_mesh_density(torch.from_numpy(g["kps"]), torch.from_numpy(g["skts"]), None, radius=radius,
+                                  res=res)
+    pts = orc.mesh_grid_points(radius, res, g["kps"][0, 0])
+    flat = rc.render_pts_density(torch.from_numpy(pts), None, torch.from_numpy(g["skts"]), None)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(grid.cpu().numpy().reshape(-1), flat.cpu().numpy()[:, 0])

@@ -163,3 +163,19 @@ def test_render_path_frame_matches_reference():
     np.testing.assert_allclose(img.reshape(H, H, 3), g["frame_rgb"][0], rtol=0, atol=1e-4)
     np.testing.assert_allclose(disp.reshape(H, H, 1), g["frame_disp"][0], rtol=0, atol=1e-4)
     np.testing.assert_allclose(acc.reshape(H, H, 1), g["frame_acc"][0], rtol=0, atol=1e-4)
+
+
+@pytest.mark.parametrize("name", ["dm_fine_d8w256", "dm_coarse_d4w128"])
+def test_density_matches_reference(name):
+    """fwd_type='density' / 'mesh' (core/raycasters.py:579-648): the oracle's trunk + alpha_linear on
+    the reference's scattered points and on its mesh grid (rebuilt with the reference's meshgrid)."""
+    g = Golden(name)
+    om = _om(g)
+    fine = g.cfg.N_importance > 0
+    ref = g["pts_density"].reshape(-1)
+    got = om.density(g["skts"][0], g["pts"], fine=fine)
+    assert np.abs(got - ref).max() <= 1e-5 * max(1.0, np.abs(ref).max())
+    gp = oracle.mesh_grid_points(g.meta["radius"], g.meta["res"], g["kps"][0, 0])
+    refg = g["grid_density"].reshape(-1)
+    assert gp.shape[0] == refg.shape[0]
+    assert np.abs(om.density(g["skts"][0], gp, fine=fine) - refg).max() <= 1e-5 * max(1.0, np.abs(refg).max())
