@@ -679,6 +679,7 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
     // feature_linear (no activation) with the alpha head folded in (both read relu(h_last))
     mlp_layer<RB, RB, true, true, true>(acc, acc, h, bias + M.D * W, net.wfeat, lane, ring, net.wview,
                                         bias + (M.D + 1) * W, sig);
+    pin(sig);  // keep the alpha FMAs in the feature layer: sunk into the view layer they keep h alive
     sig += __shfl_xor(sig, 32);
     sig += net.balpha;
     // views_linears.0: feature part (B operands straight from the feature accumulators) +

@@ -1,0 +1,57 @@
+"""Summarise the rocprofv3 --pmc passes of tools/gpu_pmc.sh for render_kernel into one JSON
+(profiles/<round>_pmc.json).  HBM bytes follow MI355X_MICROARCH.md's rocprofv3 section:
+FETCH_SIZE is in KiB and counts half of the bytes of wide streaming reads on gfx950 (x2),
+WRITE_SIZE is exact (KiB).  Usage: python tools/pmc_summary.py gpurun_out OUT.json [label]"""
+import csv
+import json
+import os
+import sys
+
+
+def rows(path, kernel="render_kernel"):
+    out = {}
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if kernel in r["Kernel_Name"]:
+                d = out.setdefault(r["Dispatch_Id"], {"ns": int(r["End_Timestamp"]) - int(r["Start_Timestamp"])})
+                d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    return out
+
+
+def main():
+    base, out_path = sys.argv[1], sys.argv[2]
+    label = sys.argv[3] if len(sys.argv) > 3 else ""
+    fetch = rows(os.path.join(base, "pmc_fetch", "run_counter_collection.csv"))
+    write = rows(os.path.join(base, "pmc_write", "run_counter_collection.csv"))
+    sq = rows(os.path.join(base, "pmc_sq", "run_counter_collection.csv"))
+    f = next(iter(fetch.values()))
+    w = next(iter(write.values()))
+    s = next(iter(sq.values()))
+    hbm = 2 * f["FETCH_SIZE"] * 1024 + w["WRITE_SIZE"] * 1024
+    clock = s["GRBM_GUI_ACTIVE"] / 8 / (s["ns"] * 1e-9) / 1e9
+    busy = s["SQ_INSTS_MFMA"] / 1024 * 64 / (s["ns"] * 1e-9 * clock * 1e9)
+    res = {
+        "kernel": "render_kernel<256,7> " + label,
+        "source": "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE | SQ_INSTS_VALU SQ_INSTS_MFMA SQ_WAVES SQ_BUSY_CYCLES "
+                  "GRBM_GUI_ACTIVE (separate passes) --kernel-trace -- python3 bench.py --steps 1 --warmup 0 --no-cpu",
+        "dispatches": len(fetch),
+        "FETCH_SIZE_KB_per_launch": f["FETCH_SIZE"],
+        "WRITE_SIZE_KB_per_launch": w["WRITE_SIZE"],
+        "render_kernel_hbm_bytes_per_launch": int(hbm),
+        "hbm_bytes_note": "2 x FETCH_SIZE x 1024 (gfx950 half-count correction) + WRITE_SIZE x 1024",
+        "SQ_INSTS_MFMA": s["SQ_INSTS_MFMA"],
+        "SQ_INSTS_VALU": s["SQ_INSTS_VALU"],
+        "SQ_WAVES": s["SQ_WAVES"],
+        "GRBM_GUI_ACTIVE": s["GRBM_GUI_ACTIVE"],
+        "kernel_ns": s["ns"],
+        "effective_clock_GHz": round(clock, 4),
+        "mfma_pipe_busy_frac": round(busy, 4),
+        "mfma_busy_note": "SQ_INSTS_MFMA / 1024 SIMDs x 64 cycles (v_mfma_f32_32x32x2_f32) / (kernel time x clock)",
+        "valu_per_mfma": round(s["SQ_INSTS_VALU"] / s["SQ_INSTS_MFMA"], 3),
+    }
+    json.dump(res, open(out_path, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
