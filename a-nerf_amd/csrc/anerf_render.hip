@@ -138,7 +138,7 @@ __host__ __device__ inline LdsPlan make_plan(int R, int nj, int W, int S, int T,
     p.scr = o; o += p.scr_stride * R;
     o = (o + 3) & ~3;
     p.bias = o; o += (D + 2) * W;  // the current net's hidden + feature biases, accumulator order; w_alpha
-    p.cut = o; o += 2 * nj;        // cutoff distances of the window (points, view directions)
+    p.cut = o; o += 3 * nj;        // window: cutoff distances (points, view directions), live thresholds
     o = (o + 3) & ~3;
     p.uf_stride = 64 * 3 * njh2;   // per wave: the L0 bone directions, re-read by the skip layer
     p.uf = with_uf ? o : -1;
@@ -336,24 +336,42 @@ __device__ __forceinline__ void ring_take(f32x2 (&slot)[RB], const float (&v)[16
     for (int rb = 0; rb < RB; ++rb) slot[rb] = f32x2{v[2 * rb], v[2 * rb + 1]};
 }
 
-// One joint's skeleton row (3x4 of the world->joint transform) and window distance, loaded from
+// Window tables in LDS: cut[j] = c_j, cut[NJ + j] = c'_j (view directions), cut[2NJ + j] = thr2_j,
+// a conservative squared-distance bound of the window's support: w_j = 1 - 1/(1 + e),
+// e = expf(-tau (d - c_j)), is exactly 0 iff 1 + e rounds to 1, i.e. e <= 2^-24, i.e.
+// tau (d - c_j) >= 24 ln 2 = 16.6355 (up to expf's rounding).  With a 0.05 margin on that
+// argument (and 1e-5 on the square), d^2 >= thr2 implies w_j == 0 exactly; joints that are
+// "live" by this test but have w_j == 0 just add exact zeros.
+__device__ __forceinline__ float live_thr2(float tau, float c) {
+    if (!(tau > 0.0f)) return __builtin_inff();
+    const float d0 = c + 16.69f / tau;
+    return d0 <= 0.0f ? -1.0f : d0 * d0 * 1.00001f;
+}
+
+__device__ __forceinline__ void stage_cut(const ModelDev& M, float* __restrict__ cut, int tid) {
+    for (int j = tid; j < 3 * M.nj; j += blockDim.x) {
+        const int k = j % M.nj;
+        cut[j] = j < M.nj ? M.cutoff[k] : (j < 2 * M.nj ? M.cutoff_v[k] : live_thr2(M.tau, M.cutoff[k]));
+    }
+}
+
+// One joint's skeleton row (3x4 of the world->joint transform) and live threshold, loaded from
 // LDS into registers two MFMA groups before use, so the encoder math never waits on LDS.
 struct JRow {
     f32x4 a, b, c;
-    float cut;
+    float thr2;
 };
 
 __device__ __forceinline__ JRow load_row(const float* __restrict__ sk, const float* __restrict__ cut, int j, int nj) {
     const int jc = j < nj ? j : 0;
     const f32x4* p = reinterpret_cast<const f32x4*>(sk + 12 * jc);
-    return JRow{p[0], p[1], p[2], cut[jc]};
+    return JRow{p[0], p[1], p[2], cut[2 * nj + jc]};
 }
 
-// bone direction u_j of this lane's sample, and whether its cutoff window is non-zero.
-// dist is the correctly rounded norm (as in the oracle); the normalisation multiplies by the
-// hardware reciprocal (<= 1.5 ulp from q / max(dist, 1e-12)), and the window test is exact:
-// cutoff_w = 1 - 1/(1 + e) is 0 iff 1 + e rounds to 1 (e = expf(-tau (dist - c))).
-// Branch-free (per-lane selects) so that it stays in the MFMA region it is scheduled into.
+// bone direction u_j = q / max(|q|, 1e-12) of this lane's sample (q * rsq(max(|q|^2, 1e-24)),
+// within 2 ulp) and whether the joint's window may be non-zero (d^2 < thr2, conservative, see
+// live_thr2).  Branch-free (per-lane selects) so that it stays in the MFMA region it is
+// scheduled into.
 __device__ __forceinline__ void u_joint(const ModelDev& M, const JRow& r, bool valid, float px, float py, float pz,
                                         float& u0, float& u1, float& u2, bool& live) {
 #ifdef ANERF_EXP_UFAST  // timing experiment only (stamps build): encoder VALU removed
@@ -365,13 +383,12 @@ __device__ __forceinline__ void u_joint(const ModelDev& M, const JRow& r, bool v
     qx = valid ? qx : 0.0f;
     qy = valid ? qy : 0.0f;
     qz = valid ? qz : 0.0f;
-    const float dist = norm3(qx, qy, qz);
-    const float inv = __builtin_amdgcn_rcpf(fmaxf(dist, 1e-12f));
+    const float d2 = fmaf(qz, qz, fmaf(qy, qy, qx * qx));
+    const float inv = __builtin_amdgcn_rsqf(fmaxf(d2, 1e-24f));
     u0 = qx * inv;
     u1 = qy * inv;
     u2 = qz * inv;
-    const float e = expf(-(M.tau * (dist - r.cut)));
-    live = valid & (!M.sparse | ((1.0f + e) != 1.0f));  // (no short-circuit: no branch)
+    live = valid & (!M.sparse | !(d2 >= r.thr2));  // (no short-circuit: no branch; NaN -> live)
 }
 
 // The geometry of pair-of-pairs pp+1 is computed under the MFMAs of pp (software pipeline:
@@ -591,7 +608,11 @@ __device__ __forceinline__ float view_weight(const ModelDev& M, const float* __r
     const int cc = c < M.nj ? c : 0;
     float qx, qy, qz;
     joint_local(sk + 12 * cc, px, py, pz, qx, qy, qz);
-    const float w = cutoff_w(M.tau_v, norm3(qx, qy, qz), cut[M.nj + cc]);
+    // w' = 1 - sigmoid(tau' (|q| - c')) with hardware sqrt / exp2 / rcp (a few ulp; w' only scales
+    // the per-ray factor G)
+    const float d = __builtin_amdgcn_sqrtf(fmaf(qz, qz, fmaf(qy, qy, qx * qx)));
+    const float e = __builtin_amdgcn_exp2f(-(M.tau_v * (d - cut[M.nj + cc])) * 1.44269504f);
+    const float w = 1.0f - __builtin_amdgcn_rcpf(1.0f + e);
     return c < M.nj ? (M.cutoff_viewdir ? w : 0.0f) : (c == M.nj ? 1.0f : 0.0f);
 }
 
@@ -820,11 +841,26 @@ __device__ __forceinline__ float density_act(const ModelDev& M, float x) {
 // raw2outputs (nerf.py:150-205) of ray slot r over n samples; wave-cooperative, all waves call it.
 // scr layout: w[zs], wz[zs], wc[3 zs], fac[zs], al[zs]
 // Results (rgb[3], disp, acc) are left in res[0..4] (LDS) for the caller to store.
+// Per-ray stages run one wave per ray on the ray's own LDS scratch: a wave-level fence orders the
+// LDS hand-offs between lanes (a wave's LDS operations complete in order), no workgroup barrier.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+// raw2outputs (nerf.py:150-205) for one ray: alpha, transmittance (torch's CPU cumprod: a
+// sequential double product, run by lane 0 four samples per LDS access), weights (left in scr
+// for importance sampling), and rgb / depth / acc as wave reductions.  Results in res[0..4].
 __device__ void composite(const ModelDev& M, const float* ray, const float* z, const float* raw, int n, float* scr,
                           int zs, bool active, int lane, float* o_alpha, float* res) {
     float* w = scr;
-    float* wz = scr + zs;
-    float* wc = scr + 2 * zs;
     float* fac = scr + 5 * zs;
     float* al = scr + 6 * zs;
     if (active) {
@@ -838,45 +874,50 @@ __device__ void composite(const ModelDev& M, const float* ray, const float* z, c
             if (o_alpha) o_alpha[i] = a;
         }
     }
-    __syncthreads();
+    wave_sync();
     if (active && lane == 0) {
-        double T = 1.0;  // torch CPU cumprod accumulates in double
-        for (int i = 0; i < n; ++i) {
+        double T = 1.0;
+        int i = 0;
+        for (; i + 4 <= n; i += 4) {
+            const f32x4 f = *reinterpret_cast<const f32x4*>(fac + i);
+            f32x4 o;
+            o[0] = (float)T; T *= (double)f[0];
+            o[1] = (float)T; T *= (double)f[1];
+            o[2] = (float)T; T *= (double)f[2];
+            o[3] = (float)T; T *= (double)f[3];
+            *reinterpret_cast<f32x4*>(w + i) = o;
+        }
+        for (; i < n; ++i) {
             w[i] = (float)T;
             T *= (double)fac[i];
         }
     }
-    __syncthreads();
+    wave_sync();
+    float sa = 0.0f, sd = 0.0f, sr = 0.0f, sg = 0.0f, sb = 0.0f;
     if (active) {
         for (int i = lane; i < n; i += 64) {
             const float wi = al[i] * w[i];
             w[i] = wi;
-            wz[i] = wi * z[i];
-#pragma unroll
-            for (int c = 0; c < 3; ++c) wc[3 * i + c] = wi * (sigmoid(raw[4 * i + c]) * 1.002f - 0.001f);
+            sa += wi;
+            sd += wi * z[i];
+            sr += wi * (sigmoid(raw[4 * i + 0]) * 1.002f - 0.001f);
+            sg += wi * (sigmoid(raw[4 * i + 1]) * 1.002f - 0.001f);
+            sb += wi * (sigmoid(raw[4 * i + 2]) * 1.002f - 0.001f);
         }
     }
-    __syncthreads();
-    if (active && lane < 5) {
-        float v;
-        if (lane < 2) v = torch_sum(lane == 0 ? w : wz, n);
-        else v = torch_sum_strided(wc + (lane - 2), 3, n);
-        fac[lane] = v;  // fac[] no longer needed
-    }
-    __syncthreads();
+    sa = wave_sum(sa), sd = wave_sum(sd), sr = wave_sum(sr), sg = wave_sum(sg), sb = wave_sum(sb);
     if (active && lane == 0) {
-        const float accf = fac[0], depth = fac[1];
-        const float ratio = depth / (accf + 1e-10f);
+        const float ratio = sd / (sa + 1e-10f);
         float dsp = 1.0f / fmaxf(ratio, 1e-10f);
         if (ratio != ratio) dsp = ratio;  // torch.max propagates NaN
-        if (fabsf(accf) <= 1e-8f) dsp = 0.0f;
-        res[0] = fac[2];
-        res[1] = fac[3];
-        res[2] = fac[4];
+        if (fabsf(sa) <= 1e-8f) dsp = 0.0f;
+        res[0] = sr;
+        res[1] = sg;
+        res[2] = sb;
         res[3] = dsp;
-        res[4] = accf < 1.0f ? accf : 1.0f;
+        res[4] = sa < 1.0f ? sa : 1.0f;
     }
-    __syncthreads();
+    wave_sync();
 }
 
 __device__ __forceinline__ bool z_less(float a, float b) { return a < b || (b != b && a == a); }
@@ -895,17 +936,34 @@ __device__ void importance(const float* zc, const float* w, int S, int I, float*
         for (int i = lane; i < nb; i += 64) mids[i] = 0.5f * (zc[i + 1] + zc[i]);
         for (int i = lane; i < nb - 1; i += 64) wp[i] = w[i + 1] + 1e-5f;
     }
-    __syncthreads();
-    if (active && lane == 0) {
+    wave_sync();
+    if (active) {
+        // pdf = wp / torch.sum(wp) (every lane computes the same cascade sum), in parallel; then
+        // torch's CPU cumsum, a sequential double sum, by lane 0 four values per LDS access
         const float sum = torch_sum(wp, nb - 1);
-        double c = 0.0;  // torch CPU cumsum accumulates in double
+        for (int i = lane; i < nb - 1; i += 64) wp[i] = wp[i] / sum;
+    }
+    wave_sync();
+    if (active && lane == 0) {
+        double c = 0.0;
         cdf[0] = 0.0f;
-        for (int i = 0; i < nb - 1; ++i) {
-            c += (double)(wp[i] / sum);
+        int i = 0;
+        for (; i + 4 <= nb - 1; i += 4) {
+            float q[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) q[k] = wp[i + k];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                c += (double)q[k];
+                cdf[i + k + 1] = (float)c;
+            }
+        }
+        for (; i < nb - 1; ++i) {
+            c += (double)wp[i];
             cdf[i + 1] = (float)c;
         }
     }
-    __syncthreads();
+    wave_sync();
     if (active) {
         for (int k = lane; k < I; k += 64) {
             const float u = torch_linspace01(k, I);
@@ -924,7 +982,7 @@ __device__ void importance(const float* zc, const float* w, int S, int I, float*
         }
         for (int i = lane; i < S; i += 64) zall[i] = zc[i];
     }
-    __syncthreads();
+    wave_sync();
     const int T = S + I;
     if (active) {
         // both lists are normally sorted (z monotone in t, samples monotone in u): merge by binary
@@ -963,7 +1021,7 @@ __device__ void importance(const float* zc, const float* w, int S, int I, float*
             }
         }
     }
-    __syncthreads();
+    wave_sync();
 }
 
 // ======================================================================= fused render kernel
@@ -995,7 +1053,7 @@ __global__ __launch_bounds__(256, 1) void render_kernel(ModelDev M, RenderArgs A
         const int pose = __float_as_int(lds[P.ray + 16 * r + 10]);
         lds[P.sk + P.sk_stride * r + e] = A.skts[((int64_t)pose * M.nj + j) * 16 + c];
     }
-    for (int j = tid; j < 2 * M.nj; j += blockDim.x) lds[P.cut + j] = j < M.nj ? M.cutoff[j] : M.cutoff_v[j - M.nj];
+    stage_cut(M, lds + P.cut, tid);
     // coarse samples (sample_from_lineseg, ray_utils.py:218-224)
     for (int idx = tid; idx < nr * S; idx += blockDim.x) {
         const int r = idx / S, s = idx % S;
@@ -1099,7 +1157,7 @@ __host__ __device__ inline LdsPlan make_density_plan(int nj, int W, int D, int n
     std::memset(&p, 0, sizeof(p));
     int o = 0;
     p.sk = o; o += 12 * nj;
-    p.cut = o; o += 2 * nj;
+    p.cut = o; o += 3 * nj;
     o = (o + 3) & ~3;
     p.bias = o; o += (D + 2) * W;
     p.uf_stride = 64 * 3 * njh2;
@@ -1115,7 +1173,7 @@ __global__ __launch_bounds__(256, 1) void density_kernel(ModelDev M, DensityArgs
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hh = lane >> 5;
     const NetDev& net = M.net[A.net];
     for (int idx = tid; idx < M.nj * 12; idx += blockDim.x) lds[P.sk + idx] = A.skts[(idx / 12) * 16 + idx % 12];
-    for (int j = tid; j < 2 * M.nj; j += blockDim.x) lds[P.cut + j] = j < M.nj ? M.cutoff[j] : M.cutoff_v[j - M.nj];
+    stage_cut(M, lds + P.cut, tid);
     for (int idx = tid; idx < (M.D + 2) * W; idx += blockDim.x) {
         const int L = idx / W, e = idx % W;
         lds[P.bias + idx] = L < M.D ? net.bl[L][e] : (L == M.D ? net.bfeat[e] : net.walpha[e]);
