@@ -126,7 +126,7 @@ __host__ __device__ inline LdsPlan make_plan(int R, int nj, int W, int S, int T,
     p.raw_stride = p.z_stride * 4;
     p.g_stride = 2 * ngh * wh;
     int scr_a = 8 * p.z_stride;          // composite / importance scratch
-    int scr_b = nk * 3 * nj + 256;  // trig table for G + per-part bias partials (256 / WH parts x WH)
+    int scr_b = ((3 * nk + 3) & ~3) * nj + 256;  // trig table for G + per-part bias partials (256 / WH parts x WH)
     p.scr_stride = (scr_a > scr_b ? scr_a : scr_b);
     int o = 0;
     p.ray = o; o += 16 * R;
@@ -750,37 +750,40 @@ __device__ void compute_view_factor(const ModelDev& M, const NetDev& net, float*
     constexpr int KC = 3 * NK;
     constexpr int NPART = 256 / WH;
     const int nj = M.nj;
-    // trig table Tt[k][3j+c] of the normalised joint-frame ray directions
-    for (int idx = tid; idx < nr * nj; idx += blockDim.x) {
-        const int r = idx / nj, j = idx % nj;
+    // trig table Tt[j][k*3 + c] (27 values, padded to 28) of the normalised joint-frame ray
+    // directions, one (ray, joint, coordinate) per thread
+    constexpr int TP = (KC + 3) & ~3;
+    for (int idx = tid; idx < nr * nj * 3; idx += blockDim.x) {
+        const int r = idx / (nj * 3), j = (idx / 3) % nj, c = idx % 3;
         const float* ray = lds + P.ray + 16 * r;
         const float* S = lds + P.sk + P.sk_stride * r + 12 * j;
         float ex, ey, ez;
         joint_rot(S, ray[3], ray[4], ray[5], ex, ey, ez);
         const float en = fmaxf(norm3(ex, ey, ez), 1e-12f);
-        const float e[3] = {ex / en, ey / en, ez / en};
-        float* Tt = lds + P.scr + P.scr_stride * r;
+        const float e = (c == 0 ? ex : (c == 1 ? ey : ez)) / en;
+        float* Tt = lds + P.scr + P.scr_stride * r + TP * j;
+        Tt[c] = e;
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            Tt[3 * j + c] = e[c];
-#pragma unroll
-            for (int f = 0; f < MRV; ++f) {
-                float s, co;
-                sincosf(e[c] * (float)(1 << f), &s, &co);
-                Tt[(1 + 2 * f) * 3 * nj + 3 * j + c] = s;
-                Tt[(2 + 2 * f) * 3 * nj + 3 * j + c] = co;
-            }
+        for (int f = 0; f < MRV; ++f) {
+            float sn, cs;
+            sincos_rr(e * (float)(1 << f), sn, cs);
+            Tt[(1 + 2 * f) * 3 + c] = sn;
+            Tt[(2 + 2 * f) * 3 + c] = cs;
         }
+        if (c == 0)
+            for (int k = KC; k < TP; ++k) Tt[k] = 0.0f;
     }
     __syncthreads();
     const int ncol = 2 * M.ngh;
     const int kfw = M.cutoff_inputs ? 0 : 1;             // first k term multiplied by w'
     const int kend = M.cutoff_viewdir ? kfw : NK;         // k terms the cutoff does not weight
     const int nn = tid % WH, part = tid / WH;
+    // G[c][n] = sum_k Wvdir[c][k][n] T_k(e_c), 4 rays at a time (independent FMA chains), the
+    // column's 27 weights in registers (next column's loaded under the current one)
     if (part < NPART) {
         const __amdgpu_buffer_rsrc_t rs = make_rsrc(net.wvdir);
         if (kend > 0)  // this thread's partial of the unweighted terms, per ray, in scratch
-            for (int r = 0; r < nr; ++r) lds[P.scr + P.scr_stride * r + KC * nj + part * WH + nn] = 0.0f;
+            for (int r = 0; r < nr; ++r) lds[P.scr + P.scr_stride * r + TP * nj + part * WH + nn] = 0.0f;
         float wc[KC], wn[KC];
         int c = part;
         if (c < nj) {
@@ -795,19 +798,43 @@ __device__ void compute_view_factor(const ModelDev& M, const NetDev& net, float*
                 for (int kc = 0; kc < KC; ++kc)
                     wn[kc] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, ((cn * KC + kc) * WH + nn) * 4, 0, 0));
             }
-            for (int r = 0; r < nr; ++r) {
-                const float* tc = lds + P.scr + P.scr_stride * r + 3 * c;
-                float v = 0.0f, u = 0.0f;
+            for (int r0 = 0; r0 < nr; r0 += 4) {
+                float v[4] = {0.0f, 0.0f, 0.0f, 0.0f}, u[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+                if (kend == 0 && kfw == 0 && M.cutoff_viewdir) {  // every term is windowed (the usual flags)
 #pragma unroll
-                for (int k = 0; k < NK; ++k)
+                    for (int q = 0; q < TP / 4; ++q) {
 #pragma unroll
-                    for (int cc = 0; cc < 3; ++cc) {
-                        const float term = wc[k * 3 + cc] * tc[k * 3 * nj + cc];
-                        if (M.cutoff_viewdir && k >= kfw) v += term;
-                        if (k < kend) u += term;
+                        for (int rr = 0; rr < 4; ++rr) {
+                            const int r = min(r0 + rr, nr - 1);
+                            const f32x4 t = *reinterpret_cast<const f32x4*>(lds + P.scr + P.scr_stride * r + TP * c + 4 * q);
+#pragma unroll
+                            for (int e = 0; e < 4; ++e)
+                                if (4 * q + e < KC) v[rr] = fmaf(wc[4 * q + e], t[e], v[rr]);
+                        }
                     }
-                lds[P.g + P.g_stride * r + c * WH + nn] = v;
-                if (kend > 0) lds[P.scr + P.scr_stride * r + KC * nj + part * WH + nn] += u;
+                } else {
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) {
+                        const int r = min(r0 + rr, nr - 1);
+                        const float* tc = lds + P.scr + P.scr_stride * r + TP * c;
+#pragma unroll
+                        for (int k = 0; k < NK; ++k)
+#pragma unroll
+                            for (int cc = 0; cc < 3; ++cc) {
+                                const float term = wc[k * 3 + cc] * tc[k * 3 + cc];
+                                if (M.cutoff_viewdir && k >= kfw) v[rr] += term;
+                                if (k < kend) u[rr] += term;
+                            }
+                    }
+                }
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) {
+                    const int r = r0 + rr;
+                    if (r < nr) {
+                        lds[P.g + P.g_stride * r + c * WH + nn] = v[rr];
+                        if (kend > 0) lds[P.scr + P.scr_stride * r + TP * nj + part * WH + nn] += u[rr];
+                    }
+                }
             }
 #pragma unroll
             for (int kc = 0; kc < KC; ++kc) wc[kc] = wn[kc];
@@ -825,7 +852,7 @@ __device__ void compute_view_factor(const ModelDev& M, const NetDev& net, float*
             for (int m = 0; m < M.cfc; ++m) b += net.wvcode[m * WH + n2] * net.codes[row * M.cfc + m];
         }
         if (kend > 0)
-            for (int pp = 0; pp < NPART; ++pp) b += lds[P.scr + P.scr_stride * r + KC * nj + pp * WH + n2];
+            for (int pp = 0; pp < NPART; ++pp) b += lds[P.scr + P.scr_stride * r + ((KC + 3) & ~3) * nj + pp * WH + n2];
         G[nj * WH + n2] = b;
         for (int c = nj + 1; c < ncol; ++c) G[c * WH + n2] = 0.0f;
     }
