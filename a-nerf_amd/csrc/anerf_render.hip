@@ -74,7 +74,7 @@ struct NetDev {
     const float* wfeat;      // packed regs W->W
     const float* bfeat;      // packed bias
     const float* wview;      // packed regs W->W/2 (feature part of views_linears.0)
-    const float* wvdir;      // [NJ][NK][3][W/2] direction part, transposed
+    const float* wvdir;      // [NJ][W/2][28] direction part (k*3 + c, padded), transposed
     const float* wvcode;     // [cfc][W/2] code part, transposed
     const float* bview;      // [W/2]
     const float* wrgb;       // [3][2][RBV][16]
@@ -745,7 +745,7 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
 // column are loaded while the current column is reduced (double buffer).
 template <int WH, int MRV>
 __device__ void compute_view_factor(const ModelDev& M, const NetDev& net, float* lds, const LdsPlan& P, int nr,
-                                    int tid) {
+                                    int tid, Stamps& st) {
     constexpr int NK = 1 + 2 * MRV;
     constexpr int KC = 3 * NK;
     constexpr int NPART = 256 / WH;
@@ -774,6 +774,7 @@ __device__ void compute_view_factor(const ModelDev& M, const NetDev& net, float*
             for (int k = KC; k < TP; ++k) Tt[k] = 0.0f;
     }
     __syncthreads();
+    STAMP(st, 7);
     const int ncol = 2 * M.ngh;
     const int kfw = M.cutoff_inputs ? 0 : 1;             // first k term multiplied by w'
     const int kend = M.cutoff_viewdir ? kfw : NK;         // k terms the cutoff does not weight
@@ -784,20 +785,19 @@ __device__ void compute_view_factor(const ModelDev& M, const NetDev& net, float*
         const __amdgpu_buffer_rsrc_t rs = make_rsrc(net.wvdir);
         if (kend > 0)  // this thread's partial of the unweighted terms, per ray, in scratch
             for (int r = 0; r < nr; ++r) lds[P.scr + P.scr_stride * r + TP * nj + part * WH + nn] = 0.0f;
-        float wc[KC], wn[KC];
-        int c = part;
-        if (c < nj) {
+        float wc[TP], wn[TP];
+        auto load_col = [&](float (&dst)[TP], int col) {
 #pragma unroll
-            for (int kc = 0; kc < KC; ++kc)
-                wc[kc] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, ((c * KC + kc) * WH + nn) * 4, 0, 0));
-        }
+            for (int q = 0; q < TP / 4; ++q) {
+                const f32x4 x = bload4(rs, (col * WH + nn) * TP * 4 + q * 16, 0);
+                dst[4 * q] = x[0], dst[4 * q + 1] = x[1], dst[4 * q + 2] = x[2], dst[4 * q + 3] = x[3];
+            }
+        };
+        int c = part;
+        if (c < nj) load_col(wc, c);
         for (; c < nj; c += NPART) {
             const int cn = c + NPART;
-            if (cn < nj) {
-#pragma unroll
-                for (int kc = 0; kc < KC; ++kc)
-                    wn[kc] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, ((cn * KC + kc) * WH + nn) * 4, 0, 0));
-            }
+            if (cn < nj) load_col(wn, cn);
             for (int r0 = 0; r0 < nr; r0 += 4) {
                 float v[4] = {0.0f, 0.0f, 0.0f, 0.0f}, u[4] = {0.0f, 0.0f, 0.0f, 0.0f};
                 if (kend == 0 && kfw == 0 && M.cutoff_viewdir) {  // every term is windowed (the usual flags)
@@ -837,7 +837,7 @@ __device__ void compute_view_factor(const ModelDev& M, const NetDev& net, float*
                 }
             }
 #pragma unroll
-            for (int kc = 0; kc < KC; ++kc) wc[kc] = wn[kc];
+            for (int kc = 0; kc < TP; ++kc) wc[kc] = wn[kc];
         }
     }
     __syncthreads();
@@ -1051,6 +1051,21 @@ __device__ void importance(const float* zc, const float* w, int S, int I, float*
     wave_sync();
 }
 
+// The current net's hidden biases, feature bias and alpha_linear row into LDS ([D + 2][W]): all
+// global loads issued before the first LDS store (one memory latency instead of D + 2).
+template <int W>
+__device__ __forceinline__ void stage_bias(const ModelDev& M, const NetDev& net, float* __restrict__ dst, int tid) {
+    static_assert(W <= 256, "one element per thread and row");
+    if (tid >= W) return;
+    float v[MAXL + 2];
+#pragma unroll
+    for (int L = 0; L < MAXL + 2; ++L)
+        if (L < M.D + 2) v[L] = L < M.D ? net.bl[L][tid] : (L == M.D ? net.bfeat[tid] : net.walpha[tid]);
+#pragma unroll
+    for (int L = 0; L < MAXL + 2; ++L)
+        if (L < M.D + 2) dst[L * W + tid] = v[L];
+}
+
 // ======================================================================= fused render kernel
 template <int W, int MR>
 __global__ __launch_bounds__(256, 1) void render_kernel(ModelDev M, RenderArgs A, LdsPlan P) {
@@ -1098,11 +1113,8 @@ __global__ __launch_bounds__(256, 1) void render_kernel(ModelDev M, RenderArgs A
         const NetDev& net = M.net[pass];
         const int n = pass == 0 ? S : T;
         const int zoff = pass == 0 ? P.zc : P.zf;
-        for (int idx = tid; idx < (M.D + 2) * W; idx += blockDim.x) {  // biases, w_alpha -> LDS (synced below)
-            const int L = idx / W, e = idx % W;
-            lds[P.bias + idx] = L < M.D ? net.bl[L][e] : (L == M.D ? net.bfeat[e] : net.walpha[e]);
-        }
-        compute_view_factor<WH, 4>(M, net, lds, P, nr, tid);
+        stage_bias<W>(M, net, lds + P.bias, tid);  // (synced below)
+        compute_view_factor<WH, 4>(M, net, lds, P, nr, tid, st);
         STAMP(st, 1);
         // ---- MLP over 32-sample blocks, round-robin over the 4 waves
         const int nb = (n + 31) / 32;
@@ -1201,10 +1213,7 @@ __global__ __launch_bounds__(256, 1) void density_kernel(ModelDev M, DensityArgs
     const NetDev& net = M.net[A.net];
     for (int idx = tid; idx < M.nj * 12; idx += blockDim.x) lds[P.sk + idx] = A.skts[(idx / 12) * 16 + idx % 12];
     stage_cut(M, lds + P.cut, tid);
-    for (int idx = tid; idx < (M.D + 2) * W; idx += blockDim.x) {
-        const int L = idx / W, e = idx % W;
-        lds[P.bias + idx] = L < M.D ? net.bl[L][e] : (L == M.D ? net.bfeat[e] : net.walpha[e]);
-    }
+    stage_bias<W>(M, net, lds + P.bias, tid);
     __syncthreads();
     Stamps st;
     float* uf = (M.skip + 1 < M.D) ? lds + P.uf + wave * P.uf_stride : nullptr;
@@ -1609,12 +1618,13 @@ static int pack_net(const anerf_model_desc* d, int njh2, const anerf_net_weights
     offs.push_back(pk.add(pack_rowvec(w->feature_b, W, false)));                      // bfeat
     offs.push_back(pk.add(pack_layer(w->views_w, WH, ldv, 0, W)));                    // wview
     {
-        std::vector<float> t((size_t)nj * nk * 3 * WH);
+        const int tp = (3 * nk + 3) & ~3;
+        std::vector<float> t((size_t)nj * WH * tp, 0.0f);
         for (int j = 0; j < nj; ++j)
             for (int k = 0; k < nk; ++k)
                 for (int c = 0; c < 3; ++c)
                     for (int n = 0; n < WH; ++n)
-                        t[(((size_t)j * nk + k) * 3 + c) * WH + n] = w->views_w[(size_t)n * ldv + W + k * 3 * nj + 3 * j + c];
+                        t[((size_t)j * WH + n) * tp + k * 3 + c] = w->views_w[(size_t)n * ldv + W + k * 3 * nj + 3 * j + c];
         offs.push_back(pk.add(t));                                                    // wvdir
     }
     {

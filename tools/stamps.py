@@ -15,7 +15,7 @@ _lib = importlib.import_module("a-nerf_amd._lib")
 _lib.LIB_PATH = os.path.join(REPO, "tools", os.environ.get("ANERF_STAMPS_LIB", "libanerf_hip_stamps.so"))
 anerf = importlib.import_module("a-nerf_amd")
 syn = importlib.import_module("a-nerf_amd.synthetic")
-NAMES = {0: "prologue", 1: "view factor G", 2: "MLP coarse", 3: "composite+importance", 4: "MLP fine",
+NAMES = {0: "prologue", 1: "view factor G (G + bias column)", 7: "  view factor: bias staging + trig table", 2: "MLP coarse", 3: "composite+importance", 4: "MLP fine",
          5: "composite fine", 6: "barrier wait after MLP", 8: "  L0 u-part", 9: "  L0 v-part",
          10: "  bias/relu boundaries", 11: "  hidden h-parts", 12: "  skip u+v", 13: "  heads (alpha/feat/view/rgb)",
          14: "  L0 u-part prologue", 15: "  v-part prologues (L0 + skip)"}
