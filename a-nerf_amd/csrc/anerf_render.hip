@@ -695,18 +695,16 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
     f32x16 acc[RB], h[RB];
     JointMask mask;
     Ring ring;
-    mlp_trunk<W, MR>(M, net, sk, cut, px, py, pz, lane, bias, uf, acc, h, ring, mask, net.wfeat, st);
+    mlp_trunk<W, MR>(M, net, sk, cut, px, py, pz, lane, bias, uf, acc, h, ring, mask, net.wview, st);
+    // views_linears.0 with feature_linear fused in (W' = Wv_f Wf, see pack_net) on relu(h_last),
+    // alpha_linear folded into its groups (same relu'd B operands), + the factorised
+    // direction / code / bias part from G, then relu
     float sig = 0.0f;
-    // feature_linear (no activation) with the alpha head folded in (both read relu(h_last))
-    mlp_layer<RB, RB, true, true, true>(acc, acc, h, bias + M.D * W, net.wfeat, lane, ring, net.wview,
-                                        bias + (M.D + 1) * W, sig);
-    pin(sig);  // keep the alpha FMAs in the feature layer: sunk into the view layer they keep h alive
+    f32x16 av[RBV];
+    mlp_layer<RBV, RB, true, false, true>(av, acc, h, nullptr, net.wview, lane, ring, nullptr, bias + (M.D + 1) * W,
+                                          sig);
     sig += __shfl_xor(sig, 32);
     sig += net.balpha;
-    // views_linears.0: feature part (B operands straight from the feature accumulators) +
-    // factorised direction/code/bias part, then relu
-    f32x16 av[RBV];
-    mlp_layer<RBV, RB, false, false, false>(av, acc, h, nullptr, net.wview, lane, ring, nullptr, nullptr, sig);
     view_dir_part<RBV>(av, M, G, sk, cut, px, py, pz, lane);
     float rgb[3];
 #pragma unroll
@@ -724,8 +722,8 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
     if (mfma_count && lane == 0) {  // exact MFMA work of this block (wave-uniform quantities)
         const int act = __builtin_popcountll(mask.m0) + __builtin_popcountll(mask.m1);
         const int xk = 3 * M.njh2 + act * VPart<MR>::KB;  // k-steps of one x part
-        long long k = (long long)xk * RB + (long long)(M.D - 1) * (W / 2) * RB + (long long)(W / 2) * RB +
-                      (long long)(W / 2) * RBV + (long long)M.ngh * RBV;
+        long long k = (long long)xk * RB + (long long)(M.D - 1) * (W / 2) * RB + (long long)(W / 2) * RBV +
+                      (long long)M.ngh * RBV;
         if (M.skip + 1 < M.D) k += (long long)xk * RB;
         atomicAdd(mfma_count, (unsigned long long)k);
     }
@@ -1614,9 +1612,25 @@ static int pack_net(const anerf_model_desc* d, int njh2, const anerf_net_weights
     }
     for (int i = 0; i < d->net_depth; ++i) offs.push_back(pk.add(pack_rowvec(w->pts_b[i], W, false)));
     offs.push_back(pk.add(pack_rowvec(w->alpha_w, W, true)));                         // walpha
-    offs.push_back(pk.add(pack_layer(w->feature_w, W, W, 0, W)));                     // wfeat
-    offs.push_back(pk.add(pack_rowvec(w->feature_b, W, false)));                      // bfeat
-    offs.push_back(pk.add(pack_layer(w->views_w, WH, ldv, 0, W)));                    // wview
+    // feature_linear has no activation, so views_linears.0's feature block and feature_linear fuse
+    // into one layer on the last hidden state (nerf.py:110-112): W' = Wv_f Wf (WH x W) and
+    // b' = Wv_f bf + bv, formed in double and rounded once.  The feature layer disappears.
+    std::vector<float> wfused((size_t)WH * W), bfused(WH);
+    for (int n = 0; n < WH; ++n) {
+        std::vector<double> row(W, 0.0);
+        double bacc = (double)w->views_b[n];
+        for (int m = 0; m < W; ++m) {
+            const double v = (double)w->views_w[(size_t)n * ldv + m];
+            const float* wf = w->feature_w + (size_t)m * W;
+            for (int k = 0; k < W; ++k) row[k] += v * (double)wf[k];
+            bacc += v * (double)w->feature_b[m];
+        }
+        for (int k = 0; k < W; ++k) wfused[(size_t)n * W + k] = (float)row[k];
+        bfused[n] = (float)bacc;
+    }
+    offs.push_back(pk.add(std::vector<float>()));                                     // wfeat (fused away)
+    offs.push_back(pk.add(pack_rowvec(w->feature_b, W, false)));                      // bfeat (unused)
+    offs.push_back(pk.add(pack_layer(wfused.data(), WH, W, 0, W)));                   // wview = Wv_f Wf
     {
         const int tp = (3 * nk + 3) & ~3;
         std::vector<float> t((size_t)nj * WH * tp, 0.0f);
@@ -1633,7 +1647,7 @@ static int pack_net(const anerf_model_desc* d, int njh2, const anerf_net_weights
             for (int n = 0; n < WH; ++n) t[(size_t)m * WH + n] = w->views_w[(size_t)n * ldv + W + cv + m];
         offs.push_back(pk.add(t));                                                    // wvcode
     }
-    offs.push_back(pk.add(std::vector<float>(w->views_b, w->views_b + WH)));          // bview
+    offs.push_back(pk.add(bfused));                                                   // bview = Wv_f bf + bv
     {
         std::vector<float> t;
         for (int c = 0; c < 3; ++c) {
