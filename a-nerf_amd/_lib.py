@@ -72,6 +72,14 @@ SIGNATURES = {
                                       ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
     "anerf_encode_points": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                            ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
+    "anerf_gen_rays_box": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_float,
+                                          ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_int32,
+                                          ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                          ctypes.c_float, ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p]),
+    "anerf_compose_box": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32,
+                                         ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                                         ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "anerf_density_points": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
                                              ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]),
     "anerf_density_grid": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,

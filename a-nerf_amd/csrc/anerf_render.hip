@@ -1306,12 +1306,21 @@ __global__ void nan_fill_kernel(const float* __restrict__ rb, int stride, int64_
     }
 }
 
+// A frame's traced pixels: an explicit index list, or (idx == NULL) the row-major half-open box
+// [x0, x0 + bw) x [y0, ...) of kp_to_valid_rays (ray_utils.py:127-130) generated on the fly.
+struct PixelSet {
+    const int64_t* idx;
+    int64_t x0, y0, bw;
+    __device__ __forceinline__ int64_t pixel(int64_t t, int W) const {
+        return idx ? idx[t] : (y0 + t / bw) * W + x0 + t % bw;
+    }
+};
+
 __global__ void gen_rays_kernel(const float* __restrict__ c2w, int H, int W, float fx, float fy, float cx, float cy,
-                                const int64_t* __restrict__ idx, int64_t n, float nearv, float farv,
-                                float* __restrict__ out) {
+                                PixelSet px, int64_t n, float nearv, float farv, float* __restrict__ out) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
-    const int64_t p = idx[t];
+    const int64_t p = px.pixel(t, W);
     const float x = (float)(p % W), y = (float)(p / W);
     // dirs = ((i - cx)/fx, -(j - cy)/fy, -1); rays_d = sum(dirs * c2w[:3,:3], -1) (ray_utils.py:22-25)
     const float d0 = (x - cx) / fx;
@@ -1342,12 +1351,12 @@ __global__ void compose_fill_kernel(const float* __restrict__ bg, int white, int
 }
 
 __global__ void compose_scatter_kernel(const float* __restrict__ rgb, const float* __restrict__ disp,
-                                       const float* __restrict__ acc, const int64_t* __restrict__ idx, int64_t n,
+                                       const float* __restrict__ acc, PixelSet px, int W, int64_t n,
                                        float* __restrict__ out_rgb, float* __restrict__ out_disp,
                                        float* __restrict__ out_acc) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const int64_t p = idx[i];
+    const int64_t p = px.pixel(i, W);
     const float a = acc[i];
     for (int c = 0; c < 3; ++c) out_rgb[3 * p + c] = rgb[3 * i + c] + (1.0f - a) * out_rgb[3 * p + c];
     const float d = disp[i];
@@ -1946,7 +1955,23 @@ int anerf_gen_rays(const float* c2w, int32_t H, int32_t W, float focal_x, float 
     const float cy = has_center ? center_y : (float)(H * 0.5);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(gen_rays_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, c2w, H, W, focal_x,
-                       focal_y, cx, cy, idx, n, nearv, farv, ray_batch_out);
+                       focal_y, cx, cy, PixelSet{idx, 0, 0, 1}, n, nearv, farv, ray_batch_out);
+    HIP_TRY(hipGetLastError());
+    return ANERF_OK;
+}
+
+int anerf_gen_rays_box(const float* c2w, int32_t H, int32_t W, float focal_x, float focal_y, float center_x,
+                       float center_y, int32_t has_center, int32_t x0, int32_t y0, int32_t x1, int32_t y1, float nearv,
+                       float farv, float* ray_batch_out, void* stream) {
+    if (!c2w || !ray_batch_out || H <= 0 || W <= 0 || x0 < 0 || y0 < 0 || x1 > W || y1 > H)
+        return fail(ANERF_EINVAL, "anerf_gen_rays_box: bad arguments");
+    if (x1 <= x0 || y1 <= y0) return ANERF_OK;
+    const int64_t n = (int64_t)(x1 - x0) * (y1 - y0);
+    const float cx = has_center ? center_x : (float)(W * 0.5);
+    const float cy = has_center ? center_y : (float)(H * 0.5);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(gen_rays_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, c2w, H, W, focal_x,
+                       focal_y, cx, cy, PixelSet{nullptr, x0, y0, x1 - x0}, n, nearv, farv, ray_batch_out);
     HIP_TRY(hipGetLastError());
     return ANERF_OK;
 }
@@ -1961,7 +1986,27 @@ int anerf_compose(const float* rgb, const float* disp, const float* acc, const i
                        out_rgb, out_disp, out_acc);
     if (n > 0)
         hipLaunchKernelGGL(compose_scatter_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, rgb, disp, acc,
-                           idx, n, out_rgb, out_disp, out_acc);
+                           PixelSet{idx, 0, 0, 1}, 1, n, out_rgb, out_disp, out_acc);
+    HIP_TRY(hipGetLastError());
+    return ANERF_OK;
+}
+
+int anerf_compose_box(const float* rgb, const float* disp, const float* acc, int32_t x0, int32_t y0, int32_t x1,
+                      int32_t y1, const float* bg, int32_t white_bkgd, int32_t H, int32_t W, float* out_rgb,
+                      float* out_disp, float* out_acc, void* stream) {
+    const bool empty = x1 <= x0 || y1 <= y0;
+    if (H <= 0 || W <= 0 || !out_rgb || !out_disp || x0 < 0 || y0 < 0 || x1 > W || y1 > H ||
+        (!empty && (!rgb || !disp || !acc)))
+        return fail(ANERF_EINVAL, "anerf_compose_box: bad arguments");
+    const int64_t hw = (int64_t)H * W;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(compose_fill_kernel, dim3((unsigned)((hw + 255) / 256)), dim3(256), 0, st, bg, white_bkgd, hw,
+                       out_rgb, out_disp, out_acc);
+    if (!empty) {
+        const int64_t n = (int64_t)(x1 - x0) * (y1 - y0);
+        hipLaunchKernelGGL(compose_scatter_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, rgb, disp, acc,
+                           PixelSet{nullptr, x0, y0, x1 - x0}, W, n, out_rgb, out_disp, out_acc);
+    }
     HIP_TRY(hipGetLastError());
     return ANERF_OK;
 }

@@ -110,14 +110,17 @@ def render_frames(render_poses, hwf, chunk, render_kwargs, centers=None, kp=None
         fa = np.asarray(focal if isinstance(focal, float) else focal[i], dtype=np.float64).reshape(-1)
         fx = float(fa[0])
         fy = float(fa[1]) if fa.size >= 2 else fx
-        idx = torch.from_numpy(valid_idxs[i]).to(dev)
-        n = idx.shape[0]
+        # the pixel set is the box [tl, br) (valid_idxs[i] is its row-major enumeration): rays are
+        # generated on the device from the box, nothing per pixel crosses PCIe
+        (x0, y0), (x1, y1) = (int(v) for v in bboxes[i][0]), (int(v) for v in bboxes[i][1])
+        n = max(x1 - x0, 0) * max(y1 - y0, 0)
+        assert n == len(valid_idxs[i])
         c2w = torch.from_numpy(np.ascontiguousarray(poses_np[i][:3, :4])).to(dev)
         rb = torch.empty(n, 11, device=dev, dtype=torch.float32)
         has_c = centers is not None
         cx, cy = (float(centers[i][0]), float(centers[i][1])) if has_c else (0.0, 0.0)
-        _lib.check(lib.anerf_gen_rays(_lib.ptr(c2w), h, w, fx, fy, cx, cy, int(has_c), _lib.ptr(idx), n, 0.0, 1.0,
-                                      _lib.ptr(rb), st), "anerf_gen_rays")
+        _lib.check(lib.anerf_gen_rays_box(_lib.ptr(c2w), h, w, fx, fy, cx, cy, int(has_c), x0, y0, x1, y1, 0.0, 1.0,
+                                          _lib.ptr(rb), st), "anerf_gen_rays_box")
         if n > 0:
             cam_i = _frame_rows(cams, i)
             ret = rc.render_rays(rb, kw.get("N_samples"), kp_batch=None, skts=_frame_rows(skts, i).to(dev),
@@ -139,9 +142,9 @@ def render_frames(render_poses, hwf, chunk, render_kwargs, centers=None, kp=None
         img = torch.empty(h * w, 3, device=dev)
         dimg = torch.empty(h * w, device=dev)
         aimg = torch.empty(h * w, device=dev)
-        _lib.check(lib.anerf_compose(_lib.ptr(rgb), _lib.ptr(disp), _lib.ptr(acc), _lib.ptr(idx), n, _lib.ptr(bg),
-                                     int(bool(white_bkgd)), h * w, _lib.ptr(img), _lib.ptr(dimg), _lib.ptr(aimg), st),
-                   "anerf_compose")
+        _lib.check(lib.anerf_compose_box(_lib.ptr(rgb), _lib.ptr(disp), _lib.ptr(acc), x0, y0, x1, y1, _lib.ptr(bg),
+                                         int(bool(white_bkgd)), h, w, _lib.ptr(img), _lib.ptr(dimg), _lib.ptr(aimg),
+                                         st), "anerf_compose_box")
         fr = (img.view(h, w, 3), dimg.view(h, w, 1), aimg.view(h, w, 1))
         if to_host:
             fr = tuple(t.cpu().numpy() for t in fr)

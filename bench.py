@@ -3,7 +3,8 @@
 A "step" renders one synthetic 512x512 frame (64 coarse + 128 importance samples, 24-joint
 skeleton, 8x256 MLP): ray generation from the frame's bounding-cylinder pixel list, the fused
 render kernel, and frame composition — all on the GPU with inputs resident in HBM (the
-pixel lists are computed on the host before the timed region, like kp_to_valid_rays).
+box of kp_to_valid_rays is computed on the host before the timed region; the pixels are
+enumerated on the device).
 
 Multi-GPU (launched by torch.distributed.run): each rank renders its own frame (a different
 pose) per step — frames are independent, so there is no collective in the data path and
@@ -87,9 +88,9 @@ def main():
     ck = syn.make_checkpoint(13, n_joints=a.joints, D=8, W=256, fine=I > 0, tau=79.6)
     sc = syn.make_scene(n_joints=a.joints, H=H, W=W, seed=13 + rank)
     rc = anerf.RayCaster(cfg, ck, device=local)
-    idxs, cyls, _ = anerf.rays.valid_pixels(sc["c2ws"], H, W, sc["focal"], kps=sc["kps"], ext_scale=0.001)
-    idx = torch.from_numpy(idxs[0]).to(dev)
-    n = int(idx.shape[0])
+    idxs, cyls, boxes = anerf.rays.valid_pixels(sc["c2ws"], H, W, sc["focal"], kps=sc["kps"], ext_scale=0.001)
+    (x0, y0), (x1, y1) = (int(v) for v in boxes[0][0]), (int(v) for v in boxes[0][1])
+    n = (x1 - x0) * (y1 - y0)
     c2w = torch.from_numpy(np.ascontiguousarray(sc["c2ws"][0][:3, :4])).to(dev)
     skts = torch.from_numpy(sc["skts"][0:1]).to(dev)
     cyl = torch.from_numpy(cyls[0:1]).to(dev)
@@ -101,8 +102,8 @@ def main():
     ev = []
 
     def step(record):
-        _lib.check(lib.anerf_gen_rays(_lib.ptr(c2w), H, W, sc["focal"], sc["focal"], 0.0, 0.0, 0, _lib.ptr(idx), n,
-                                      0.0, 1.0, _lib.ptr(rb), st), "gen_rays")
+        _lib.check(lib.anerf_gen_rays_box(_lib.ptr(c2w), H, W, sc["focal"], sc["focal"], 0.0, 0.0, 0, x0, y0, x1, y1,
+                                          0.0, 1.0, _lib.ptr(rb), st), "gen_rays_box")
         if record:
             e0 = torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -112,9 +113,9 @@ def main():
             e1 = torch.cuda.Event(enable_timing=True)
             e1.record()
             ev.append((e0, e1))
-        _lib.check(lib.anerf_compose(_lib.ptr(out["rgb_map"]), _lib.ptr(out["disp_map"]), _lib.ptr(out["acc_map"]),
-                                     _lib.ptr(idx), n, None, 0, H * W, _lib.ptr(img), _lib.ptr(dimg), _lib.ptr(aimg),
-                                     st), "compose")
+        _lib.check(lib.anerf_compose_box(_lib.ptr(out["rgb_map"]), _lib.ptr(out["disp_map"]),
+                                         _lib.ptr(out["acc_map"]), x0, y0, x1, y1, None, 0, H, W, _lib.ptr(img),
+                                         _lib.ptr(dimg), _lib.ptr(aimg), st), "compose_box")
 
     for _ in range(a.warmup):
         step(False)

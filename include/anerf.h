@@ -17,6 +17,8 @@
  *   anerf_encode_points     encode_inputs + embedders (stage / debug)          core/raycasters.py:476-555
  *   anerf_near_far          get_near_far_in_cylinder (stage)                   core/utils/ray_utils.py:292-344
  *   anerf_compose           render_path's image composition + NaN disp -> 0    run_nerf.py:100-141
+ *   anerf_gen_rays_box,     the same over kp_to_valid_rays' box, the pixel     core/utils/ray_utils.py:127-132
+ *   anerf_compose_box       list generated on the device (no index upload)
  *   anerf_density_points    RayCaster.render_pts_density (fwd_type='density')  core/raycasters.py:597-648
  *   anerf_density_grid      RayCaster.render_mesh_density (fwd_type='mesh')    core/raycasters.py:579-595
  *                           (called by run_render.render_mesh)                 run_render.py:970-986
@@ -145,6 +147,17 @@ int anerf_gen_rays(const float* c2w /*3x4 row-major, device*/, int32_t H, int32_
 int anerf_compose(const float* rgb, const float* disp, const float* acc, const int64_t* idx, int64_t n,
                   const float* bg, int32_t white_bkgd, int64_t hw, float* out_rgb, float* out_disp, float* out_acc,
                   void* stream);
+
+/* anerf_gen_rays over the pixels of kp_to_valid_rays' box, y in [y0, y1), x in [x0, x1), row-major
+ * (the valid_idx order; ray_utils.py:127-130): n = (x1 - x0)(y1 - y0) rays, no index list. */
+int anerf_gen_rays_box(const float* c2w, int32_t H, int32_t W, float focal_x, float focal_y, float center_x,
+                       float center_y, int32_t has_center, int32_t x0, int32_t y0, int32_t x1, int32_t y1, float near,
+                       float far, float* ray_batch_out, void* stream);
+
+/* anerf_compose for rays produced by anerf_gen_rays_box (same box, same order). */
+int anerf_compose_box(const float* rgb, const float* disp, const float* acc, int32_t x0, int32_t y0, int32_t x1,
+                      int32_t y1, const float* bg, int32_t white_bkgd, int32_t H, int32_t W, float* out_rgb,
+                      float* out_disp, float* out_acc, void* stream);
 
 /* Stage: near/far of get_near_far_in_cylinder with the per-chunk NaN fill. */
 int anerf_near_far(const float* ray_batch, int32_t ray_stride, int64_t n_rays, const float* cyls,

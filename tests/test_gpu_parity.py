@@ -280,3 +280,41 @@ def test_density_grid_equals_points_path():
     flat = rc.render_pts_density(torch.from_numpy(pts), None, torch.from_numpy(g["skts"]), None)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(grid.cpu().numpy().reshape(-1), flat.cpu().numpy()[:, 0])
+
+
+def test_box_ray_generation_and_composition_match_index_path():
+    """anerf_gen_rays_box / anerf_compose_box (pixels enumerated on the device) == the index-list path."""
+    g = Golden("c1_64_s32_d4w128")
+    lib = _lib.load()
+    H = g.meta["H"]
+    tl, br = g["tl"], g["br"]
+    idx = torch.from_numpy(g["valid_idx"]).cuda()
+    n = idx.shape[0]
+    c2w = torch.from_numpy(np.ascontiguousarray(g["c2ws"][0][:3, :4])).cuda()
+    a = torch.empty(n, 11, device="cuda")
+    b = torch.empty(n, 11, device="cuda")
+    f = float(g.meta["focal"])
+    _lib.check(lib.anerf_gen_rays(_lib.ptr(c2w), H, H, f, f, 0.0, 0.0, 0, _lib.ptr(idx), n, 0.0, 1.0, _lib.ptr(a),
+                                  _lib.stream_handle()), "gen")
+    _lib.check(lib.anerf_gen_rays_box(_lib.ptr(c2w), H, H, f, f, 0.0, 0.0, 0, int(tl[0]), int(tl[1]), int(br[0]),
+                                      int(br[1]), 0.0, 1.0, _lib.ptr(b), _lib.stream_handle()), "gen_box")
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    rgb, disp, acc = torch.rand(n, 3, device="cuda"), torch.rand(n, device="cuda"), torch.rand(n, device="cuda")
+    disp[::7] = float("nan")
+    outs = []
+    for box in (False, True):
+        img, dimg, aimg = torch.empty(H * H, 3, device="cuda"), torch.empty(H * H, device="cuda"), torch.empty(
+            H * H, device="cuda")
+        if box:
+            rc = lib.anerf_compose_box(_lib.ptr(rgb), _lib.ptr(disp), _lib.ptr(acc), int(tl[0]), int(tl[1]), int(br[0]),
+                                       int(br[1]), None, 1, H, H, _lib.ptr(img), _lib.ptr(dimg), _lib.ptr(aimg),
+                                       _lib.stream_handle())
+        else:
+            rc = lib.anerf_compose(_lib.ptr(rgb), _lib.ptr(disp), _lib.ptr(acc), _lib.ptr(idx), n, None, 1, H * H,
+                                   _lib.ptr(img), _lib.ptr(dimg), _lib.ptr(aimg), _lib.stream_handle())
+        _lib.check(rc, "compose")
+        torch.cuda.synchronize()
+        outs.append((img.clone(), dimg.clone(), aimg.clone()))
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)
