@@ -33,14 +33,14 @@ using namespace anerf;
 // RenderArgs::stamps[16]; read only by tools/stamps.py, never part of an output.
 struct Stamps {
 #ifdef ANERF_STAMPS
-    unsigned long long last, acc[16];
+    unsigned long long last, acc[24];
 #endif
 };
 #ifdef ANERF_STAMPS
 #define STAMP_INIT(st)                                      \
     do {                                                    \
         (st).last = __builtin_amdgcn_s_memtime();           \
-        for (int i_ = 0; i_ < 16; ++i_) (st).acc[i_] = 0;   \
+        for (int i_ = 0; i_ < 24; ++i_) (st).acc[i_] = 0;   \
     } while (0)
 #define STAMP(st, i)                                                      \
     do {                                                                  \
@@ -53,7 +53,7 @@ struct Stamps {
 #define STAMP_FLUSH(st, ptr)                                              \
     do {                                                                  \
         if ((threadIdx.x & 63) == 0 && (ptr))                             \
-            for (int i_ = 0; i_ < 16; ++i_) atomicAdd((ptr) + i_, (st).acc[i_]); \
+            for (int i_ = 0; i_ < 24; ++i_) atomicAdd((ptr) + i_, (st).acc[i_]); \
     } while (0)
 #else
 #define STAMP_INIT(st) do { } while (0)
@@ -109,9 +109,9 @@ struct RenderArgs {
 
 // ======================================================================= LDS plan
 struct LdsPlan {
-    int ray, sk, zc, zf, raw, g, scr, bias, cut, uf;  // float offsets (uf < 0: no u-feature store)
+    int ray, sk, zc, zf, raw, g, scr, bias, cut, uf, wv;  // float offsets (uf < 0: no u-feature store)
     int total;                          // floats
-    int sk_stride, z_stride, raw_stride, g_stride, scr_stride, uf_stride;
+    int sk_stride, z_stride, raw_stride, g_stride, scr_stride, uf_stride, wv_stride;
 };
 
 __host__ __device__ inline int pad32(int x) { return (x + 31) & ~31; }
@@ -143,6 +143,8 @@ __host__ __device__ inline LdsPlan make_plan(int R, int nj, int W, int S, int T,
     p.uf_stride = 64 * 3 * njh2;   // per wave: the L0 bone directions, re-read by the skip layer
     p.uf = with_uf ? o : -1;
     if (with_uf) o += 4 * p.uf_stride;
+    p.wv_stride = 64 * njh2;       // per wave: view-direction window weights w'_j of the current block
+    p.wv = o; o += 4 * p.wv_stride;
     p.total = (o + 3) & ~3;
     return p;
 }
@@ -359,23 +361,26 @@ __device__ __forceinline__ void stage_cut(const ModelDev& M, float* __restrict__
 // LDS into registers two MFMA groups before use, so the encoder math never waits on LDS.
 struct JRow {
     f32x4 a, b, c;
-    float thr2;
+    float thr2, cv;
 };
 
 __device__ __forceinline__ JRow load_row(const float* __restrict__ sk, const float* __restrict__ cut, int j, int nj) {
     const int jc = j < nj ? j : 0;
     const f32x4* p = reinterpret_cast<const f32x4*>(sk + 12 * jc);
-    return JRow{p[0], p[1], p[2], cut[2 * nj + jc]};
+    return JRow{p[0], p[1], p[2], cut[2 * nj + jc], cut[nj + jc]};
 }
 
 // bone direction u_j = q / max(|q|, 1e-12) of this lane's sample (q * rsq(max(|q|^2, 1e-24)),
 // within 2 ulp) and whether the joint's window may be non-zero (d^2 < thr2, conservative, see
 // live_thr2).  Branch-free (per-lane selects) so that it stays in the MFMA region it is
 // scheduled into.
+// With WV, also the joint's view-direction window w'_j = 1 - sigmoid(tau' (|q| - c'_j)) (hardware
+// sqrt/exp2/rcp, a few ulp; 0 for padding joints or without cutoff_viewdir) for the view layer.
+template <bool WV>
 __device__ __forceinline__ void u_joint(const ModelDev& M, const JRow& r, bool valid, float px, float py, float pz,
-                                        float& u0, float& u1, float& u2, bool& live) {
+                                        float& u0, float& u1, float& u2, bool& live, float& wv) {
 #ifdef ANERF_EXP_UFAST  // timing experiment only (stamps build): encoder VALU removed
-    u0 = px * r.a[0]; u1 = py; u2 = pz; live = false; return;
+    u0 = px * r.a[0]; u1 = py; u2 = pz; live = false; wv = 0.0f; return;
 #endif
     float qx = fmaf(r.a[3], 1.0f, fmaf(r.a[2], pz, fmaf(r.a[1], py, r.a[0] * px)));
     float qy = fmaf(r.b[3], 1.0f, fmaf(r.b[2], pz, fmaf(r.b[1], py, r.b[0] * px)));
@@ -389,6 +394,12 @@ __device__ __forceinline__ void u_joint(const ModelDev& M, const JRow& r, bool v
     u1 = qy * inv;
     u2 = qz * inv;
     live = valid & (!M.sparse | !(d2 >= r.thr2));  // (no short-circuit: no branch; NaN -> live)
+    if constexpr (WV) {
+        const float d = __builtin_amdgcn_sqrtf(d2);
+        const float e = __builtin_amdgcn_exp2f(-(M.tau_v * (d - r.cv)) * 1.44269504f);
+        const float w = 1.0f - __builtin_amdgcn_rcpf(1.0f + e);
+        wv = (valid && M.cutoff_viewdir) ? w : 0.0f;
+    }
 }
 
 // The geometry of pair-of-pairs pp+1 is computed under the MFMAs of pp (software pipeline:
@@ -397,7 +408,8 @@ template <int RB>
 __device__ __forceinline__ void u_part(f32x16 (&acc)[RB], const ModelDev& M, const float* __restrict__ wp,
                                        const float* __restrict__ sk, const float* __restrict__ cut, float px,
                                        float py, float pz, int lane, JointMask* mask, float* __restrict__ uf,
-                                       Ring& sh, const float* __restrict__ next, Stamps& st) {
+                                       float* __restrict__ wvo, Ring& sh, const float* __restrict__ next,
+                                       Stamps& st) {
     const int hh = lane >> 5;
     const int njh2 = M.njh2;
     const int npp = njh2 / 2;
@@ -411,8 +423,13 @@ __device__ __forceinline__ void u_part(f32x16 (&acc)[RB], const ModelDev& M, con
     bool lv0, lv1;
     const int nj = M.nj, j0 = hh * njh2;
     JRow ra = load_row(sk, cut, j0, nj), rb2 = load_row(sk, cut, j0 + 1, nj);
-    u_joint(M, ra, j0 < nj, px, py, pz, f[0], f[1], f[2], lv0);
-    u_joint(M, rb2, j0 + 1 < nj, px, py, pz, f[3], f[4], f[5], lv1);
+    float wv0, wv1;
+    u_joint<true>(M, ra, j0 < nj, px, py, pz, f[0], f[1], f[2], lv0, wv0);
+    u_joint<true>(M, rb2, j0 + 1 < nj, px, py, pz, f[3], f[4], f[5], lv1, wv1);
+    if (wvo) {  // w'_j of k-step p of the view layer's direction part (joint p + h NJH2)
+        wvo[lane] = wv0;
+        wvo[64 + lane] = wv1;
+    }
     ra = load_row(sk, cut, j0 + 2, nj);
     rb2 = load_row(sk, cut, j0 + 3, nj);
     STAMP(st, 14);
@@ -449,13 +466,17 @@ __device__ __forceinline__ void u_part(f32x16 (&acc)[RB], const ModelDev& M, con
                 for (int rb = 0; rb < RB; ++rb) acc[rb] = mfma_f32_32x32x2(ring[g % 3][rb][t], b, acc[rb]);
             }
             if (g == 0) {  // joint 2pp+2 from its prefetched row; then prefetch joint 2pp+4
-                u_joint(M, ra, j0 + 2 * pp + 2 < nj, px, py, pz, fn[0], fn[1], fn[2], ln0);
+                float wv;
+                u_joint<true>(M, ra, j0 + 2 * pp + 2 < nj, px, py, pz, fn[0], fn[1], fn[2], ln0, wv);
                 pin(fn[0]), pin(fn[1]), pin(fn[2]), pin(ln0);
+                if (wvo && 2 * pp + 2 < njh2) wvo[(2 * pp + 2) * 64 + lane] = wv;
                 ra = load_row(sk, cut, j0 + 2 * pp + 4, nj);
             }
             if (g == 1) {
-                u_joint(M, rb2, j0 + 2 * pp + 3 < nj, px, py, pz, fn[3], fn[4], fn[5], ln1);
+                float wv;
+                u_joint<true>(M, rb2, j0 + 2 * pp + 3 < nj, px, py, pz, fn[3], fn[4], fn[5], ln1, wv);
                 pin(fn[3]), pin(fn[4]), pin(fn[5]), pin(ln1);
+                if (wvo && 2 * pp + 3 < njh2) wvo[(2 * pp + 3) * 64 + lane] = wv;
                 rb2 = load_row(sk, cut, j0 + 2 * pp + 5, nj);
             }
             interleave_mfma_valu<2 * RB, 8>();
@@ -601,37 +622,33 @@ __device__ __forceinline__ void v_part(f32x16 (&acc)[RB], const ModelDev& M, con
     }
 }
 
-// View layer, per-ray direction part: acc[RBV] += G^T * [w'_0 .. w'_{NJ-1}, 1]  (G in LDS).
-// Column q+1's window weight is computed under column q's MFMAs.
-__device__ __forceinline__ float view_weight(const ModelDev& M, const float* __restrict__ sk,
-                                             const float* __restrict__ cut, int c, float px, float py, float pz) {
-    const int cc = c < M.nj ? c : 0;
-    float qx, qy, qz;
-    joint_local(sk + 12 * cc, px, py, pz, qx, qy, qz);
-    // w' = 1 - sigmoid(tau' (|q| - c')) with hardware sqrt / exp2 / rcp (a few ulp; w' only scales
-    // the per-ray factor G)
-    const float d = __builtin_amdgcn_sqrtf(fmaf(qz, qz, fmaf(qy, qy, qx * qx)));
-    const float e = __builtin_amdgcn_exp2f(-(M.tau_v * (d - cut[M.nj + cc])) * 1.44269504f);
-    const float w = 1.0f - __builtin_amdgcn_rcpf(1.0f + e);
-    return c < M.nj ? (M.cutoff_viewdir ? w : 0.0f) : (c == M.nj ? 1.0f : 0.0f);
-}
-
+// View layer, per-ray direction part: acc[RBV] += G^T * [w'_j, 1]  (G in LDS).  k-step p pairs
+// joint p (lane half 0) with joint p + NJH2 (half 1), exactly the u part's pairing, so w'_j comes
+// from the u part (wvp, stored per lane); k-step NJH2 adds the bias / framecode column NJ.  The G
+// values of the next k-step are read under the current k-step's MFMAs.
 template <int RBV>
 __device__ __forceinline__ void view_dir_part(f32x16 (&acc)[RBV], const ModelDev& M, const float* __restrict__ G,
-                                              const float* __restrict__ sk, const float* __restrict__ cut, float px,
-                                              float py, float pz, int lane) {
+                                              const float* __restrict__ wvp, int lane) {
     constexpr int WH = RBV * 32;
     const int hh = lane >> 5, sl = lane & 31;
-    float b = view_weight(M, sk, cut, hh * M.ngh, px, py, pz);
-    for (int q = 0; q < M.ngh; ++q) {
-        __builtin_amdgcn_sched_barrier(0);
-        const int c = q + hh * M.ngh;
-        const float* gc = G + c * WH + sl;
+    const int njh2 = M.njh2;
+    auto col = [&](int p) { return p < njh2 ? p + hh * njh2 : M.nj + hh; };
+    float gv[RBV];
 #pragma unroll
-        for (int rb = 0; rb < RBV; ++rb) acc[rb] = mfma_f32_32x32x2(gc[32 * rb], b, acc[rb]);
-        b = view_weight(M, sk, cut, c + 1, px, py, pz);  // (q+1 == ngh: not used)
-        pin(b);
-        interleave_mfma_valu<RBV, 14>();
+    for (int rb = 0; rb < RBV; ++rb) gv[rb] = G[col(0) * WH + sl + 32 * rb];
+    float b = wvp[lane];
+    for (int p = 0; p <= njh2; ++p) {
+        __builtin_amdgcn_sched_barrier(0);
+        const int pn = min(p + 1, njh2);
+        float gn[RBV];
+#pragma unroll
+        for (int rb = 0; rb < RBV; ++rb) gn[rb] = G[col(pn) * WH + sl + 32 * rb];
+        const float bn = pn < njh2 ? wvp[pn * 64 + lane] : (hh ? 0.0f : 1.0f);
+#pragma unroll
+        for (int rb = 0; rb < RBV; ++rb) acc[rb] = mfma_f32_32x32x2(gv[rb], b, acc[rb]);
+#pragma unroll
+        for (int rb = 0; rb < RBV; ++rb) gv[rb] = gn[rb];
+        b = bn;
     }
 }
 
@@ -642,8 +659,9 @@ template <int W, int MR>
 __device__ __forceinline__ void mlp_trunk(const ModelDev& M, const NetDev& net, const float* __restrict__ sk,
                                           const float* __restrict__ cut, float px, float py, float pz, int lane,
                                           const float* __restrict__ bias, float* __restrict__ uf,
-                                          f32x16 (&acc)[W / 32], f32x16 (&h)[W / 32], Ring& ring, JointMask& mask,
-                                          const float* __restrict__ after_last, Stamps& st) {
+                                          float* __restrict__ wvo, f32x16 (&acc)[W / 32], f32x16 (&h)[W / 32],
+                                          Ring& ring, JointMask& mask, const float* __restrict__ after_last,
+                                          Stamps& st) {
     constexpr int RB = W / 32;
     const int hh = lane >> 5;
     float nosig = 0.0f;
@@ -651,7 +669,8 @@ __device__ __forceinline__ void mlp_trunk(const ModelDev& M, const NetDev& net, 
     ring_preload<2 * RB>(ring, net.wl[0], lane);  // the u part's first groups, early
     load_bias<RB>(acc, bias, hh);
     STAMP(st, 10);
-    u_part<RB>(acc, M, net.wl[0], sk, cut, px, py, pz, lane, &mask, uf, ring, M.D > 1 ? net.wl[1] : after_last, st);
+    u_part<RB>(acc, M, net.wl[0], sk, cut, px, py, pz, lane, &mask, uf, wvo, ring, M.D > 1 ? net.wl[1] : after_last,
+               st);
     STAMP(st, 8);
     v_part<RB, MR>(acc, M, net.wl0v, sk, cut, px, py, pz, lane, mask, st);
     STAMP(st, 9);
@@ -666,7 +685,7 @@ __device__ __forceinline__ void mlp_trunk(const ModelDev& M, const NetDev& net, 
             if (uf)
                 u_part_lds<RB>(acc, M, net.wskipu, uf, lane, ring, after);
             else
-                u_part<RB>(acc, M, net.wskipu, sk, cut, px, py, pz, lane, nullptr, nullptr, ring, after, st);
+                u_part<RB>(acc, M, net.wskipu, sk, cut, px, py, pz, lane, nullptr, nullptr, nullptr, ring, after, st);
             v_part<RB, MR>(acc, M, net.wskipv, sk, cut, px, py, pz, lane, mask, st);
             STAMP(st, 12);
         }
@@ -680,7 +699,7 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
                           int n, int s0,
                           const float* __restrict__ G, float* __restrict__ raw_out, int lane,
                           unsigned long long* mfma_count, const float* __restrict__ bias, float* __restrict__ uf,
-                          Stamps& st) {
+                          float* __restrict__ wvp, Stamps& st) {
     constexpr int RB = W / 32;
     constexpr int RBV = (W / 2) / 32;
     const int sl = lane & 31, hh = lane >> 5;
@@ -695,7 +714,7 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
     f32x16 acc[RB], h[RB];
     JointMask mask;
     Ring ring;
-    mlp_trunk<W, MR>(M, net, sk, cut, px, py, pz, lane, bias, uf, acc, h, ring, mask, net.wview, st);
+    mlp_trunk<W, MR>(M, net, sk, cut, px, py, pz, lane, bias, uf, wvp, acc, h, ring, mask, net.wview, st);
     // views_linears.0 with feature_linear fused in (W' = Wv_f Wf, see pack_net) on relu(h_last),
     // alpha_linear folded into its groups (same relu'd B operands), + the factorised
     // direction / code / bias part from G, then relu
@@ -703,9 +722,11 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
     f32x16 av[RBV];
     mlp_layer<RBV, RB, true, false, true>(av, acc, h, nullptr, net.wview, lane, ring, nullptr, bias + (M.D + 1) * W,
                                           sig);
+    STAMP(st, 16);
     sig += __shfl_xor(sig, 32);
     sig += net.balpha;
-    view_dir_part<RBV>(av, M, G, sk, cut, px, py, pz, lane);
+    view_dir_part<RBV>(av, M, G, wvp, lane);
+    STAMP(st, 17);
     float rgb[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
@@ -723,7 +744,7 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
         const int act = __builtin_popcountll(mask.m0) + __builtin_popcountll(mask.m1);
         const int xk = 3 * M.njh2 + act * VPart<MR>::KB;  // k-steps of one x part
         long long k = (long long)xk * RB + (long long)(M.D - 1) * (W / 2) * RB + (long long)(W / 2) * RBV +
-                      (long long)M.ngh * RBV;
+                      (long long)(M.njh2 + 1) * RBV;
         if (M.skip + 1 < M.D) k += (long long)xk * RB;
         atomicAdd(mfma_count, (unsigned long long)k);
     }
@@ -1121,7 +1142,8 @@ __global__ __launch_bounds__(256, 1) void render_kernel(ModelDev M, RenderArgs A
             mlp_block<W, MR>(M, net, lds + P.ray + 16 * r, lds + P.sk + P.sk_stride * r, lds + P.cut,
                              lds + zoff + P.z_stride * r, n, s0, lds + P.g + P.g_stride * r,
                              lds + P.raw + P.raw_stride * r, lane, A.mfma_count, lds + P.bias,
-                             (P.uf >= 0 && M.skip + 1 < M.D) ? lds + P.uf + wave * P.uf_stride : nullptr, st);
+                             (P.uf >= 0 && M.skip + 1 < M.D) ? lds + P.uf + wave * P.uf_stride : nullptr,
+                             lds + P.wv + wave * P.wv_stride, st);
         }
         STAMP(st, 2 + 2 * pass);
         __syncthreads();
@@ -1232,8 +1254,8 @@ __global__ __launch_bounds__(256, 1) void density_kernel(ModelDev M, DensityArgs
         f32x16 acc[RB], h[RB];
         JointMask mask;
         Ring ring;
-        mlp_trunk<W, MR>(M, net, lds + P.sk, lds + P.cut, px, py, pz, lane, lds + P.bias, uf, acc, h, ring, mask,
-                         nullptr, st);
+        mlp_trunk<W, MR>(M, net, lds + P.sk, lds + P.cut, px, py, pz, lane, lds + P.bias, uf, nullptr, acc, h, ring,
+                         mask, nullptr, st);
         // alpha_linear on relu(h_last), in the k-step order of the render path's fused alpha head
         float sig = 0.0f;
 #pragma unroll
@@ -1730,7 +1752,7 @@ int anerf_model_create(const anerf_model_desc* desc, const anerf_net_weights* co
     if (!embed->cutoff_dist || !embed->cutoff_dist_v) return fail(ANERF_EINVAL, "cutoff_dist is NULL");
     const int nj = desc->n_joints;
     const int njh2 = (((nj + 1) / 2) + 1) & ~1;  // joint pairs of the u part, even
-    const int ngh = (nj + 2) / 2;                   // NJ + 1 view columns split over two lane halves
+    const int ngh = std::max(2 * njh2, nj + 2) / 2;  // G columns / 2: joint p + h*NJH2 at k-step p, bias at NJ
     Packer pk;
     std::vector<size_t> oc, of;
     rc = pack_net(desc, njh2, coarse, pk, oc);

@@ -18,7 +18,8 @@ syn = importlib.import_module("a-nerf_amd.synthetic")
 NAMES = {0: "prologue", 1: "view factor G (G + bias column)", 7: "  view factor: bias staging + trig table", 2: "MLP coarse", 3: "composite+importance", 4: "MLP fine",
          5: "composite fine", 6: "barrier wait after MLP", 8: "  L0 u-part", 9: "  L0 v-part",
          10: "  bias/relu boundaries", 11: "  hidden h-parts", 12: "  skip u+v", 13: "  heads (alpha/feat/view/rgb)",
-         14: "  L0 u-part prologue", 15: "  v-part prologues (L0 + skip)"}
+         14: "  L0 u-part prologue", 15: "  v-part prologues (L0 + skip)",
+         16: "  heads: view layer (+ alpha)", 17: "  heads: view-direction part", 13: "  heads: rgb head + stores"}
 
 
 def main():
@@ -32,7 +33,7 @@ def main():
     rc = anerf.RayCaster(cfg, ck)
     kw = {"ray_caster": rc, "N_samples": 64, "N_importance": 128, "use_viewdirs": True,
           "preproc_kwargs": {"density_scale": 1.0}}
-    st = torch.zeros(16, dtype=torch.int64, device="cuda")
+    st = torch.zeros(24, dtype=torch.int64, device="cuda")
     anerf.render_frames(torch.from_numpy(sc["c2ws"]), (H, H, sc["focal"]), 4096, kw, kp=torch.from_numpy(sc["kps"]),
                         skts=torch.from_numpy(sc["skts"]), ext_scale=0.001, to_host=False)
     lib.anerf_diag_set_stamps(ctypes.c_void_p(st.data_ptr()))
@@ -40,7 +41,7 @@ def main():
                         skts=torch.from_numpy(sc["skts"]), ext_scale=0.001, to_host=False)
     torch.cuda.synchronize()
     v = st.cpu().numpy().astype(np.float64)
-    tot = v[0:16].sum()  # top-level phases + the MLP sub-phases (stamped separately)
+    tot = v[0:24].sum()  # top-level phases + the MLP sub-phases (stamped separately)
     print(f"tau={tau}: total wave-cycles {tot:.3e}")
     for i, nm in NAMES.items():
         print(f"{nm:34s} {100 * v[i] / tot:6.2f} %")
