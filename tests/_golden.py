@@ -13,7 +13,10 @@ syn = importlib.import_module("a-nerf_amd.synthetic")
 config = importlib.import_module("a-nerf_amd.config")
 
 NAMES = ["c1_64_s32_d4w128", "c2_256_s64_d8w256", "c3_512_s64i128_d8w256", "c4_512_s64i128_j65",
-         "h1_nanfill_s32i16_d4w128", "fc_64_s32i32_d4w128"]
+         "h1_nanfill_s32i16_d4w128", "fc_64_s32i32_d4w128",
+         # flag variants: multires 10 + width 64; softplus density without view cutoff; unwindowed
+         # distance input; no cutoff window at all
+         "v1_mr10_w64_d4", "v2_softplus_nocutview", "v3_nocutinputs", "v4_nocutoff"]
 
 
 class Golden:
@@ -24,11 +27,20 @@ class Golden:
         self.meta = ast.literal_eval(str(self.d["meta"]))
         m = self.meta
         fc = bool(m.get("framecode", 0))
+        drop, flags = m.get("drop", []), m.get("flags", [])
+        kw = {}
+        if "--density_type" in flags:
+            kw["density_type"] = flags[flags.index("--density_type") + 1]
+        if "--softplus_shift" in flags:
+            kw["softplus_shift"] = float(flags[flags.index("--softplus_shift") + 1])
         self.cfg = config.RenderConfig(n_joints=m["NJ"], netdepth=m["D"], netwidth=m["W"], N_samples=m["S"],
                                        N_importance=m["I"], opt_framecode=fc, n_framecodes=5 if fc else 0,
-                                       chunk=m["chunk"], ext_scale=m["ext_scale"]).validate()
+                                       chunk=m["chunk"], ext_scale=m["ext_scale"], multires=m.get("mr", 7),
+                                       use_cutoff="--use_cutoff" not in drop,
+                                       cutoff_inputs="--cutoff_inputs" not in drop,
+                                       cutoff_viewdir="--cutoff_viewdir" not in drop, **kw).validate()
         self.ckpt = syn.make_checkpoint(m["seed"], n_joints=m["NJ"], D=m["D"], W=m["W"], fine=m["I"] > 0,
-                                        tau=m["tau"], use_framecode=fc, n_framecodes=5)
+                                        tau=m["tau"], use_framecode=fc, n_framecodes=5, multires=m.get("mr", 7))
         assert syn.checkpoint_sha256(self.ckpt) == m["sha256"], "synthetic weights drifted from the fixture"
 
     def __getitem__(self, k):

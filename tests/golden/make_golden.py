@@ -97,6 +97,15 @@ CONFIGS = {
                            radius=1.8, n_pts=1000),
     "dm_coarse_d4w128": dict(H=64, NJ=24, S=32, I=0, D=4, W=128, tau=20.0, kind="density", seed=11, res=12,
                              radius=1.8, n_pts=600),
+    # flag variants of the render path (kernel template / branch coverage)
+    "v1_mr10_w64_d4": dict(H=128, NJ=24, S=32, I=16, D=4, W=64, tau=20.0, kind="rays", n_rays=128, seed=21, mr=10),
+    "v2_softplus_nocutview": dict(H=128, NJ=24, S=32, I=16, D=4, W=128, tau=20.0, kind="rays", n_rays=128, seed=22,
+                                  flags=["--density_type", "softplus", "--softplus_shift", "1.0"],
+                                  drop=["--cutoff_viewdir"]),
+    "v3_nocutinputs": dict(H=128, NJ=24, S=32, I=16, D=4, W=128, tau=20.0, kind="rays", n_rays=128, seed=23,
+                           drop=["--cutoff_inputs"]),
+    "v4_nocutoff": dict(H=128, NJ=24, S=32, I=16, D=4, W=128, tau=20.0, kind="rays", n_rays=128, seed=24,
+                        drop=["--use_cutoff", "--cutoff_inputs", "--cutoff_viewdir"]),
 }
 
 
@@ -107,10 +116,11 @@ def build_reference(mods, cfg, tmp):
     use_fc = cfg["kind"] == "framecode"
     argv = ["--N_samples", str(cfg["S"]), "--N_importance", str(cfg["I"]),
             "--netdepth", str(cfg["D"]), "--netwidth", str(cfg["W"]),
-            "--multires", "7", "--multires_views", "4",
+            "--multires", str(cfg.get("mr", 7)), "--multires_views", "4",
             "--use_cutoff", "--cutoff_viewdir", "--cutoff_inputs", "--use_viewdirs",
             "--ext_scale", "0.001", "--chunk", "4096", "--no_reload",
             "--basedir", tmp, "--expname", "x"]
+    argv = [a for a in argv if a not in cfg.get("drop", [])] + cfg.get("flags", [])
     if use_fc:
         argv += ["--opt_framecode", "--n_framecodes", "5"]
     args = run_nerf.config_parser().parse_args(argv)
@@ -125,7 +135,7 @@ def build_reference(mods, cfg, tmp):
                   "joint_coords": np.zeros((NJ, 3, 3), np.float32)}
     _, render_kwargs, _, _, _, _ = raycasters.create_raycaster(args, data_attrs)
     ck = anerf_syn.make_checkpoint(cfg["seed"], n_joints=NJ, D=cfg["D"], W=cfg["W"], fine=cfg["I"] > 0,
-                                   tau=cfg["tau"], use_framecode=use_fc, n_framecodes=5)
+                                   tau=cfg["tau"], use_framecode=use_fc, n_framecodes=5, multires=cfg.get("mr", 7))
     ck_t = {k: {n: torch.from_numpy(np.array(v)) for n, v in d.items()} for k, d in ck.items()}
     rc = render_kwargs["ray_caster"]
     rc.load_state_dict(ck_t, strict=True)
@@ -240,7 +250,8 @@ def make(name, cfg, mods, tmp):
     sha = anerf_syn.checkpoint_sha256(ck)
     meta = dict(seed=cfg["seed"], sha256=sha, NJ=cfg["NJ"], S=cfg["S"], I=cfg["I"], D=cfg["D"], W=cfg["W"],
                 tau=cfg["tau"], H=sc["H"], focal=sc["focal"], ext_scale=0.001, chunk=4096,
-                framecode=int(cfg["kind"] == "framecode"))
+                framecode=int(cfg["kind"] == "framecode"), mr=cfg.get("mr", 7), flags=cfg.get("flags", []),
+                drop=cfg.get("drop", []))
     data = {"c2ws": sc["c2ws"], "kps": sc["kps"], "skts": sc["skts"], "bones": sc["bones"]}
     (o, d), vidx, cyls, (tl, br) = rays_for(mods, sc)
     sc["cyls"] = cyls

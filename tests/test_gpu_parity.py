@@ -87,7 +87,7 @@ def test_framecode_mean_code_matches_golden():
         assert _maxdiff(out[k], g["outneg_" + k]) <= TOL
 
 
-@pytest.mark.parametrize("name", [n for n in NAMES if n.startswith(("c2", "c3", "c4", "fc"))])
+@pytest.mark.parametrize("name", [n for n in NAMES if n.startswith(("c2", "c3", "c4", "fc", "v"))])
 def test_stages_match_reference(name):
     """near/far and coarse z bit-exact; raw / weights / fine z against the reference's stage dumps."""
     g = Golden(name)
