@@ -1,0 +1,352 @@
+// anerf_kernels.hpp — __global__ kernels: fused render kernel, density-only kernel, near/far + NaN fill, ray generation, composition, encoding stage.
+// Part of the single translation unit anerf_render.hip (included there, in order).
+#pragma once
+
+// ======================================================================= fused render kernel
+template <int W, int MR>
+__global__ __launch_bounds__(256, 1) void render_kernel(ModelDev M, RenderArgs A, LdsPlan P) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    constexpr int WH = W / 2;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int R = A.R, S = A.S, I = A.I, T = S + I;
+    const int64_t ray0 = (int64_t)blockIdx.x * R;
+    const int nr = (int)min((int64_t)R, A.n - ray0);
+
+    // ---- rays, poses, skeleton transforms into LDS
+    for (int r = tid; r < nr; r += blockDim.x) {
+        const int64_t i = ray0 + r;
+        const float* src = A.rb + i * A.stride;
+        float* d = lds + P.ray + 16 * r;
+        for (int c = 0; c < 6; ++c) d[c] = src[c];
+        d[6] = A.cams ? A.cams[i] : -1.0f;
+        d[7] = A.near[i];
+        d[8] = A.far[i];
+        d[9] = norm3(src[3], src[4], src[5]);
+        d[10] = __int_as_float(A.ray_pose ? A.ray_pose[i] : 0);
+    }
+    __syncthreads();
+    for (int idx = tid; idx < nr * M.nj * 12; idx += blockDim.x) {
+        const int r = idx / (M.nj * 12), e = idx % (M.nj * 12);
+        const int j = e / 12, c = e % 12;
+        const int pose = __float_as_int(lds[P.ray + 16 * r + 10]);
+        lds[P.sk + P.sk_stride * r + e] = A.skts[((int64_t)pose * M.nj + j) * 16 + c];
+    }
+    stage_cut(M, lds + P.cut, tid);
+    // coarse samples (sample_from_lineseg, ray_utils.py:218-224)
+    for (int idx = tid; idx < nr * S; idx += blockDim.x) {
+        const int r = idx / S, s = idx % S;
+        const float t = torch_linspace01(s, S);
+        const float nearv = lds[P.ray + 16 * r + 7], farv = lds[P.ray + 16 * r + 8];
+        lds[P.zc + P.z_stride * r + s] = nearv * (1.0f - t) + farv * t;
+    }
+    __syncthreads();
+
+    Stamps st;
+    STAMP_INIT(st);
+    STAMP(st, 0);
+    const int n_pass = I > 0 ? 2 : 1;
+    for (int pass = 0; pass < n_pass; ++pass) {
+        const NetDev& net = M.net[pass];
+        const int n = pass == 0 ? S : T;
+        const int zoff = pass == 0 ? P.zc : P.zf;
+        stage_bias<W>(M, net, lds + P.bias, tid);  // (synced below)
+        compute_view_factor<WH, 4>(M, net, lds, P, nr, tid, st);
+        STAMP(st, 1);
+        // ---- MLP over 32-sample blocks, round-robin over the 4 waves
+        const int nb = (n + 31) / 32;
+        for (int b = wave; b < nr * nb; b += 4) {
+            const int r = b / nb, s0 = (b % nb) * 32;
+            mlp_block<W, MR>(M, net, lds + P.ray + 16 * r, lds + P.sk + P.sk_stride * r, lds + P.cut,
+                             lds + zoff + P.z_stride * r, n, s0, lds + P.g + P.g_stride * r,
+                             lds + P.raw + P.raw_stride * r, lane, A.mfma_count, lds + P.bias,
+                             (P.uf >= 0 && M.skip + 1 < M.D) ? lds + P.uf + wave * P.uf_stride : nullptr,
+                             lds + P.wv + wave * P.wv_stride, st);
+        }
+        STAMP(st, 2 + 2 * pass);
+        __syncthreads();
+        STAMP(st, 6);
+        // ---- composite (+ importance sampling after the coarse pass); one wave per ray
+        for (int r0 = 0; r0 < R; r0 += 4) {
+            const int r = r0 + wave;
+            const bool active = r < nr;
+            const int64_t i = ray0 + r;
+            const float* ray = lds + P.ray + 16 * min(r, R - 1);
+            const float* z = lds + zoff + P.z_stride * min(r, R - 1);
+            const float* raw = lds + P.raw + P.raw_stride * min(r, R - 1);
+            float* scr = lds + P.scr + P.scr_stride * min(r, R - 1);
+            const bool final_pass = pass == n_pass - 1;
+            float* o_rgb = final_pass ? A.rgb : A.rgb0;
+            float* o_disp = final_pass ? A.disp : A.disp0;
+            float* o_acc = final_pass ? A.acc : A.acc0;
+            float* o_alpha = final_pass ? A.alpha : A.alpha0;
+            float* pal = (active && o_alpha) ? o_alpha + i * n : nullptr;
+            if (active) {
+                float* dz = pass == 0 ? A.dbg_z0 : A.dbg_z1;
+                float* draw = pass == 0 ? A.dbg_raw0 : A.dbg_raw1;
+                for (int s = lane; s < n; s += 64) {
+                    if (dz) dz[i * n + s] = z[s];
+                    if (draw)
+                        for (int c = 0; c < 4; ++c) draw[(i * n + s) * 4 + c] = raw[4 * s + c];
+                }
+            }
+            float* res = scr + 7 * P.z_stride;
+            composite(M, ray, z, raw, n, scr, P.z_stride, active, lane, pal, res);
+            if (active && lane < 5) {
+                const float v = res[lane];
+                if (lane < 3) {
+                    if (o_rgb) o_rgb[3 * i + lane] = v;
+                } else if (lane == 3) {
+                    if (o_disp) o_disp[i] = v;
+                } else if (o_acc) {
+                    o_acc[i] = v;
+                }
+            }
+            if (pass == 0 && I > 0) {
+                if (active && A.dbg_w0)
+                    for (int s = lane; s < S; s += 64) A.dbg_w0[i * S + s] = scr[s];
+                importance(z, scr, S, I, lds + P.zf + P.z_stride * min(r, R - 1), scr + P.z_stride, active, lane);
+            }
+        }
+        __syncthreads();
+        STAMP(st, 3 + 2 * pass);
+    }
+    STAMP_FLUSH(st, A.stamps);
+}
+
+// ======================================================================= density-only queries
+// RayCaster.render_pts_density / render_mesh_density (core/raycasters.py:579-648): the trunk of
+// one network and alpha_linear at arbitrary points (or at the (res+1)^3 mesh grid, generated here:
+// point (a, b, c) = (t[b], t[a], t[c]) + kp0, the 'xy' meshgrid order of the reference).
+struct DensityArgs {
+    const float* pts;  // N x 3, or NULL for the grid
+    const float* t;    // grid axis, res1 floats
+    const float* kp0;  // 3
+    int64_t res1;
+    int64_t n;
+    const float* skts;  // NJ x 16, one pose
+    int net;
+    float* out;  // N raw densities
+};
+
+__host__ __device__ inline LdsPlan make_density_plan(int nj, int W, int D, int njh2) {
+    LdsPlan p;
+    std::memset(&p, 0, sizeof(p));
+    int o = 0;
+    p.sk = o; o += 12 * nj;
+    p.cut = o; o += 3 * nj;
+    o = (o + 3) & ~3;
+    p.bias = o; o += (D + 2) * W;
+    p.uf_stride = 64 * 3 * njh2;
+    p.uf = o; o += 4 * p.uf_stride;
+    p.total = (o + 3) & ~3;
+    return p;
+}
+
+template <int W, int MR>
+__global__ __launch_bounds__(256, 1) void density_kernel(ModelDev M, DensityArgs A, LdsPlan P) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    constexpr int RB = W / 32;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hh = lane >> 5;
+    const NetDev& net = M.net[A.net];
+    for (int idx = tid; idx < M.nj * 12; idx += blockDim.x) lds[P.sk + idx] = A.skts[(idx / 12) * 16 + idx % 12];
+    stage_cut(M, lds + P.cut, tid);
+    stage_bias<W>(M, net, lds + P.bias, tid);
+    __syncthreads();
+    Stamps st;
+    float* uf = (M.skip + 1 < M.D) ? lds + P.uf + wave * P.uf_stride : nullptr;
+    const float* wa = lds + P.bias + (M.D + 1) * W + hh * (W / 2);
+    const int64_t nb = (A.n + 31) / 32;
+    for (int64_t b = (int64_t)blockIdx.x * 4 + wave; b < nb; b += (int64_t)gridDim.x * 4) {
+        const int64_t s_out = b * 32 + (lane & 31);
+        const int64_t s = s_out < A.n ? s_out : A.n - 1;
+        float px, py, pz;
+        if (A.pts) {
+            px = A.pts[3 * s], py = A.pts[3 * s + 1], pz = A.pts[3 * s + 2];
+        } else {
+            const int64_t a = s / (A.res1 * A.res1), r = s % (A.res1 * A.res1);
+            px = A.t[r / A.res1] + A.kp0[0];
+            py = A.t[a] + A.kp0[1];
+            pz = A.t[r % A.res1] + A.kp0[2];
+        }
+        f32x16 acc[RB], h[RB];
+        JointMask mask;
+        Ring ring;
+        mlp_trunk<W, MR>(M, net, lds + P.sk, lds + P.cut, px, py, pz, lane, lds + P.bias, uf, nullptr, acc, h, ring,
+                         mask, nullptr, st);
+        // alpha_linear on relu(h_last), in the k-step order of the render path's fused alpha head
+        float sig = 0.0f;
+#pragma unroll
+        for (int q = 0; q < W / 2; ++q) sig = fmaf(wa[q], relu_act(acc[q >> 4][q & 15]), sig);
+        sig += __shfl_xor(sig, 32);
+        sig += net.balpha;
+        if (hh == 0 && s_out < A.n) A.out[s_out] = sig;
+    }
+}
+
+// ======================================================================= small kernels
+__global__ void near_far_kernel(const float* __restrict__ rb, int stride, int64_t n, const float* __restrict__ cyls,
+                                const int32_t* __restrict__ ray_pose, float* __restrict__ near_out,
+                                float* __restrict__ far_out, uint8_t* __restrict__ qnan) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float* r = rb + i * stride;
+    const float* cy = cyls + 5 * (ray_pose ? ray_pose[i] : 0);
+    const float nearv = r[6], farv = r[7];
+    // g_axes = [0, -1]: the x-z ground plane (ray_utils.py:292-327)
+    const float rn0 = r[0] + r[3] * nearv, rn1 = r[2] + r[5] * nearv;
+    const float rf0 = r[0] + r[3] * farv, rf1 = r[2] + r[5] * farv;
+    const float nc0 = cy[0] - rn0, nc1 = cy[1] - rn1;
+    const float nf0 = rf0 - rn0, nf1 = rf1 - rn1;
+    const float nfn = norm2(nf0, nf1);
+    const float scale = norm2(r[3], r[5]);
+    const float cross = nc0 * nf1 - nc1 * nf0;
+    const float dist = fabsf(cross) / nfn;
+    const float rad = cy[2];
+    const float Q = sqrtf(rad * rad - dist * dist);
+    const float K = (nc0 * nf0 + nc1 * nf1) / nfn;
+    const float mask = (Q < K) ? 1.0f : 0.0f;
+    near_out[i] = nearv + (mask * (K - Q)) / scale;
+    far_out[i] = nearv + (K + Q) / scale;
+    qnan[i] = (Q != Q) ? 1 : 0;
+}
+
+// one workgroup per chunk: NaN rows <- np.nanmean of the chunk (ray_utils.py:328-342)
+__global__ void nan_fill_kernel(const float* __restrict__ rb, int stride, int64_t n, int chunk,
+                                float* __restrict__ near_io, float* __restrict__ far_io,
+                                const uint8_t* __restrict__ qnan, float* __restrict__ scratch) {
+    const int64_t c0 = (int64_t)blockIdx.x * chunk;
+    const int64_t c1 = min(c0 + chunk, n);
+    __shared__ int any;
+    __shared__ float means[2];
+    if (threadIdx.x == 0) any = 0;
+    __syncthreads();
+    for (int64_t i = c0 + threadIdx.x; i < c1; i += blockDim.x)
+        if (near_io[i] != near_io[i]) any = 1;
+    __syncthreads();
+    if (!any) return;
+    float* buf = scratch + c0;  // NaN -> 0 copies, one vector at a time
+    for (int v = 0; v < 2; ++v) {
+        const float* src = v == 0 ? near_io : far_io;
+        for (int64_t i = c0 + threadIdx.x; i < c1; i += blockDim.x) buf[i - c0] = (src[i] != src[i]) ? 0.0f : src[i];
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int64_t cnt = 0;
+            for (int64_t i = c0; i < c1; ++i) cnt += (src[i] == src[i]);
+            means[v] = cnt ? (float)((double)np_pairwise_sum(buf, c1 - c0) / (double)cnt) : __int_as_float(0x7fc00000);
+        }
+        __syncthreads();
+    }
+    for (int64_t i = c0 + threadIdx.x; i < c1; i += blockDim.x) {
+        if (qnan[i]) {
+            const float* r = rb + i * stride;
+            near_io[i] = (means[0] != means[0]) ? r[6] : means[0];
+            far_io[i] = (means[1] != means[1]) ? r[7] : means[1];
+        }
+    }
+}
+
+// A frame's traced pixels: an explicit index list, or (idx == NULL) the row-major half-open box
+// [x0, x0 + bw) x [y0, ...) of kp_to_valid_rays (ray_utils.py:127-130) generated on the fly.
+struct PixelSet {
+    const int64_t* idx;
+    int64_t x0, y0, bw;
+    __device__ __forceinline__ int64_t pixel(int64_t t, int W) const {
+        return idx ? idx[t] : (y0 + t / bw) * W + x0 + t % bw;
+    }
+};
+
+__global__ void gen_rays_kernel(const float* __restrict__ c2w, int H, int W, float fx, float fy, float cx, float cy,
+                                PixelSet px, int64_t n, float nearv, float farv, float* __restrict__ out) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const int64_t p = px.pixel(t, W);
+    const float x = (float)(p % W), y = (float)(p / W);
+    // dirs = ((i - cx)/fx, -(j - cy)/fy, -1); rays_d = sum(dirs * c2w[:3,:3], -1) (ray_utils.py:22-25)
+    const float d0 = (x - cx) / fx;
+    const float d1 = -(y - cy) / fy;
+    const float d2 = -1.0f;
+    float* o = out + t * 11;
+    float dd[3];
+    for (int r = 0; r < 3; ++r) {
+        dd[r] = (d0 * c2w[4 * r + 0] + d1 * c2w[4 * r + 1]) + d2 * c2w[4 * r + 2];
+        o[r] = c2w[4 * r + 3];
+        o[3 + r] = dd[r];
+    }
+    o[6] = nearv;
+    o[7] = farv;
+    const float nn = norm3(dd[0], dd[1], dd[2]);  // viewdirs = d / |d| (core/trainer.py:123)
+    o[8] = dd[0] / nn;
+    o[9] = dd[1] / nn;
+    o[10] = dd[2] / nn;
+}
+
+__global__ void compose_fill_kernel(const float* __restrict__ bg, int white, int64_t hw, float* __restrict__ out_rgb,
+                                    float* __restrict__ out_disp, float* __restrict__ out_acc) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= hw) return;
+    for (int c = 0; c < 3; ++c) out_rgb[3 * p + c] = bg ? bg[3 * p + c] : (white ? 1.0f : 0.0f);
+    out_disp[p] = 0.0f;
+    if (out_acc) out_acc[p] = 0.0f;
+}
+
+__global__ void compose_scatter_kernel(const float* __restrict__ rgb, const float* __restrict__ disp,
+                                       const float* __restrict__ acc, PixelSet px, int W, int64_t n,
+                                       float* __restrict__ out_rgb, float* __restrict__ out_disp,
+                                       float* __restrict__ out_acc) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t p = px.pixel(i, W);
+    const float a = acc[i];
+    for (int c = 0; c < 3; ++c) out_rgb[3 * p + c] = rgb[3 * i + c] + (1.0f - a) * out_rgb[3 * p + c];
+    const float d = disp[i];
+    out_disp[p] = (d != d) ? 0.0f : d;  // disps[isnan] = 0 (run_nerf.py:140-141)
+    if (out_acc) out_acc[p] = a;
+}
+
+// full torch-order feature vectors (encode_inputs + embedders), one thread per point
+__global__ void encode_points_kernel(ModelDev M, const float* __restrict__ skts, const float* __restrict__ pts,
+                                     const float* __restrict__ dirs, int64_t n, float* __restrict__ feat) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int nj = M.nj, nv = 1 + 2 * M.mr, nk = 1 + 2 * M.mrv;
+    const int cx = nj * nv + 3 * nj;
+    const int F = cx + 3 * nj * nk;
+    float* f = feat + i * F;
+    const float px = pts[3 * i], py = pts[3 * i + 1], pz = pts[3 * i + 2];
+    const float dx = dirs[3 * i], dy = dirs[3 * i + 1], dz = dirs[3 * i + 2];
+    for (int j = 0; j < nj; ++j) {
+        float S[12];
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 4; ++c) S[4 * r + c] = skts[j * 16 + 4 * r + c];
+        float qx, qy, qz;
+        joint_local(S, px, py, pz, qx, qy, qz);
+        const float dist = norm3(qx, qy, qz);
+        const float dn = fmaxf(dist, 1e-12f);
+        const float w = M.use_cutoff ? cutoff_w(M.tau, dist, M.cutoff[j]) : 1.0f;
+        f[j] = (M.use_cutoff && M.cutoff_inputs) ? dist * w : dist;
+        for (int fi = 0; fi < M.mr; ++fi) {
+            float s, c;
+            sincosf(dist * (float)(1 << fi), &s, &c);
+            f[(1 + 2 * fi) * nj + j] = s * w;
+            f[(2 + 2 * fi) * nj + j] = c * w;
+        }
+        f[nj * nv + 3 * j + 0] = qx / dn;
+        f[nj * nv + 3 * j + 1] = qy / dn;
+        f[nj * nv + 3 * j + 2] = qz / dn;
+        float ex, ey, ez;
+        joint_rot(S, dx, dy, dz, ex, ey, ez);
+        const float en = fmaxf(norm3(ex, ey, ez), 1e-12f);
+        const float e[3] = {ex / en, ey / en, ez / en};
+        const float wv = M.cutoff_viewdir ? cutoff_w(M.tau_v, dist, M.cutoff_v[j]) : 1.0f;
+        for (int c = 0; c < 3; ++c) {
+            f[cx + 3 * j + c] = (M.cutoff_viewdir && M.cutoff_inputs) ? e[c] * wv : e[c];
+            for (int fi = 0; fi < M.mrv; ++fi) {
+                float s, co;
+                sincosf(e[c] * (float)(1 << fi), &s, &co);
+                f[cx + (1 + 2 * fi) * 3 * nj + 3 * j + c] = s * wv;
+                f[cx + (2 + 2 * fi) * 3 * nj + 3 * j + c] = co * wv;
+            }
+        }
+    }
+}
+

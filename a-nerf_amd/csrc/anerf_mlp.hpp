@@ -1,0 +1,612 @@
+// anerf_mlp.hpp — MFMA building blocks of the fused MLP: weight ring, dense layer with fused boundary, encoder k-streams (bone directions, windowed joints), view-direction part, trunk and one 32-sample block.
+// Part of the single translation unit anerf_render.hip (included there, in order).
+#pragma once
+
+// ======================================================================= MLP building blocks
+// Weight streams are read with buffer loads: one SGPR descriptor per array plus a single 32-bit
+// lane offset, so the unrolled K loops carry no per-load 64-bit address registers.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* p) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ f32x2 bload2(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+    return __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0));
+}
+__device__ __forceinline__ f32x4 bload4(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
+}
+
+template <int RB>
+__device__ __forceinline__ void load_bias(f32x16 (&acc)[RB], const float* __restrict__ bp_lds, int hh) {
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+        const f32x4* p = reinterpret_cast<const f32x4*>(bp_lds + (rb * 2 + hh) * 16);
+        f32x4 v0 = p[0], v1 = p[1], v2 = p[2], v3 = p[3];
+        acc[rb] = f32x16{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3],
+                         v2[0], v2[1], v2[2], v2[3], v3[0], v3[1], v3[2], v3[3]};
+    }
+}
+
+// Weight streams are cut into groups of F floats per lane (one MFMA A operand each), stored
+// [group][F/4][64 lanes][4] so that every b128 load reads 1 KiB contiguous.  A 4-slot register
+// ring is shared by consecutive phases: group g of a layer lives in slot g % 4, the prefetch
+// distance is 2 groups, and the last two groups of a layer prefetch groups 0 and 1 of the next
+// phase so it starts without a load bubble.
+struct Ring {
+    float v[4][16];
+};
+
+template <int F>
+__device__ __forceinline__ void load_group(float (&slot)[16], __amdgpu_buffer_rsrc_t rs, int lane, int g) {
+#pragma unroll
+    for (int i = 0; i < F / 4; ++i) {
+        const f32x4 x = bload4(rs, lane * 16 + i * 1024, g * F * 256);  // (i * 1024 -> immediate offset)
+        slot[4 * i] = x[0], slot[4 * i + 1] = x[1], slot[4 * i + 2] = x[2], slot[4 * i + 3] = x[3];
+    }
+}
+
+template <int F>
+__device__ __forceinline__ void ring_preload(Ring& ring, const float* __restrict__ wp, int lane) {
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(wp);
+    load_group<F>(ring.v[0], rs, lane, 0);
+    load_group<F>(ring.v[1], rs, lane, 1);
+}
+
+// One dense layer, out[RBO] (+)= W^T act(in) over 32*RBI inputs, with the layer boundary fused in:
+// the previous layer's accumulators ain[rb] are turned into B operands h[rb] (relu, or used as
+// they are for the feature -> view edge) and the output blocks are initialised with their bias
+// *inside* the first groups, under the MFMAs.  To make that possible the first RBO groups are
+// "lead" groups: group rb < RBO runs k-steps 0..15 (input block 0) of output block rb only, so
+// block rb+1 is converted while block rb accumulates; the remaining groups are k-major
+// (KG = 16/RBO k-steps x RBO blocks = 16 MFMAs each).  ALPHA folds the alpha head
+// (sig += w_alpha . h in k-step order) into the groups as VALU filler.
+template <int RBO, int RBI, bool RELU_IN, bool OUT_SAME, bool ALPHA>
+__device__ __forceinline__ void mlp_layer(f32x16 (&out)[RBO], f32x16 (&ain)[RBI], f32x16 (&h)[RBI],
+                                          const float* __restrict__ bias, const float* __restrict__ wp, int lane,
+                                          Ring& ring, const float* __restrict__ next, const float* __restrict__ wa,
+                                          float& sig) {
+    constexpr int KG = 16 / RBO;
+    constexpr int NQ = 16 * RBI;
+    constexpr int NG = RBO + (NQ - 16) / KG;
+    static_assert(RBO * KG == 16 && (NQ - 16) % KG == 0, "group shape");
+    const int hh = lane >> 5;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(wp);
+    const __amdgpu_buffer_rsrc_t rn = make_rsrc(next);
+    auto init_out = [&](int rb) {  // bias (OUT_SAME layers) or zero
+        if constexpr (OUT_SAME) {
+            const f32x4* p = reinterpret_cast<const f32x4*>(bias + (rb * 2 + hh) * 16);
+            const f32x4 v0 = p[0], v1 = p[1], v2 = p[2], v3 = p[3];
+            out[rb] = f32x16{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3],
+                             v2[0], v2[1], v2[2], v2[3], v3[0], v3[1], v3[2], v3[3]};
+        } else {
+            out[rb] = f32x16{0};
+        }
+    };
+    auto convert = [&](int rb) {
+        if constexpr (RELU_IN) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) h[rb][i] = relu_act(ain[rb][i]);
+        }
+        if constexpr (OUT_SAME) {
+            if (rb < RBO) init_out(rb);
+        }
+    };
+    auto B = [&](int q) -> float { return RELU_IN ? h[q >> 4][q & 15] : ain[q >> 4][q & 15]; };
+    if constexpr (!OUT_SAME) {
+#pragma unroll
+        for (int rb = 0; rb < RBO; ++rb) init_out(rb);
+    }
+    convert(0);
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (g + 2 < NG)
+            load_group<16>(ring.v[(g + 2) % 4], rs, lane, g + 2);
+        else if (NG % 4 == 0 && next)
+            load_group<16>(ring.v[(g + 2) % 4], rn, lane, g + 2 - NG);
+        if (g < RBO) {
+#pragma unroll
+            for (int t = 15; t >= 0; --t)  // (last-loaded float first: one vmcnt wait per group)
+                out[g] = mfma_f32_32x32x2(ring.v[g % 4][t], B(t), out[g]);
+            if (ALPHA && g == 0) {
+                const f32x4* w4 = reinterpret_cast<const f32x4*>(wa + hh * 16 * RBI);
+#pragma unroll
+                for (int t = 0; t < 16; ++t) sig = fmaf(w4[t >> 2][t & 3], B(t), sig);
+            }
+            if (g + 1 < RBO) {
+                convert(g + 1);
+            } else {
+#pragma unroll
+                for (int rb = RBO; rb < RBI; ++rb) convert(rb);
+            }
+        } else {
+            const int q0 = 16 + (g - RBO) * KG;
+#pragma unroll
+            for (int t = 0; t < KG; ++t) {
+                const float b = B(q0 + t);
+#pragma unroll
+                for (int rb = RBO - 1; rb >= 0; --rb)
+                    out[rb] = mfma_f32_32x32x2(ring.v[g % 4][rb * KG + t], b, out[rb]);
+                if (ALPHA) sig = fmaf(wa[hh * 16 * RBI + q0 + t], b, sig);
+            }
+        }
+    }
+}
+
+// The MLP input x = [v (k*NJ + j), r (NJ*NV + 3j + c)] is split into two k-streams:
+//  * the bone-direction part u_j = q_j/|q_j| (never windowed): k-step 3p+c pairs joint p (lane
+//    half 0) with joint p + NJH2 (half 1); this pass also ballots the cutoff window per joint;
+//  * the windowed part of joint j: k-step t pairs sin_t (half 0) with cos_t (half 1), then
+//    (dist, 0); executed only for joints whose window w_j is non-zero for some sample of the
+//    block.  w_j rounds to exactly 0 far from a joint, making those 2*MR+1 inputs exact zeros
+//    whose MFMAs add nothing: skipping them is bit-exact.
+struct JointMask {
+    uint64_t m0, m1;
+};
+
+__device__ __forceinline__ int mask_pop(uint64_t& a0, uint64_t& a1) {
+    if (a0) {
+        const int j = __builtin_ctzll(a0);
+        a0 &= a0 - 1;
+        return j;
+    }
+    if (a1) {
+        const int j = 64 + __builtin_ctzll(a1);
+        a1 &= a1 - 1;
+        return j;
+    }
+    return -1;
+}
+
+// Pin a value's computation before this point: IR passes otherwise sink the software-pipelined
+// encoding math out of the MFMA region it was written in (sched_barrier only binds the
+// machine scheduler).
+__device__ __forceinline__ void pin(float x) { asm volatile("" ::"v"(x)); }
+__device__ __forceinline__ void pin(bool x) { asm volatile("" ::"v"((int)x)); }
+
+// Compile-time interleave of one scheduling region: NM MFMAs, each followed by up to NV VALU
+// instructions (one wave per SIMD: without it the scheduler issues the MFMAs back to back and
+// leaves the encoding VALU exposed after them).
+template <int NM, int NV>
+__device__ __forceinline__ void interleave_mfma_valu() {
+#pragma unroll
+    for (int i = 0; i < NM; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);
+    }
+}
+
+// u-part weight groups: 2 k-steps x RB row blocks = 2*RB floats per lane (slot float 2*rb + t)
+template <int RB>
+__device__ __forceinline__ void load_u_group(f32x2 (&slot)[RB], __amdgpu_buffer_rsrc_t rs, int lane, int g) {
+#pragma unroll
+    for (int i = 0; i < RB / 2; ++i) {
+        const f32x4 x = bload4(rs, lane * 16 + i * 1024, g * 2 * RB * 256);
+        slot[2 * i] = f32x2{x[0], x[1]};
+        slot[2 * i + 1] = f32x2{x[2], x[3]};
+    }
+}
+template <int RB>
+__device__ __forceinline__ void ring_take(f32x2 (&slot)[RB], const float (&v)[16]) {
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) slot[rb] = f32x2{v[2 * rb], v[2 * rb + 1]};
+}
+
+// Window tables in LDS: cut[j] = c_j, cut[NJ + j] = c'_j (view directions), cut[2NJ + j] = thr2_j,
+// a conservative squared-distance bound of the window's support: w_j = 1 - 1/(1 + e),
+// e = expf(-tau (d - c_j)), is exactly 0 iff 1 + e rounds to 1, i.e. e <= 2^-24, i.e.
+// tau (d - c_j) >= 24 ln 2 = 16.6355 (up to expf's rounding).  With a 0.05 margin on that
+// argument (and 1e-5 on the square), d^2 >= thr2 implies w_j == 0 exactly; joints that are
+// "live" by this test but have w_j == 0 just add exact zeros.
+__device__ __forceinline__ float live_thr2(float tau, float c) {
+    if (!(tau > 0.0f)) return __builtin_inff();
+    const float d0 = c + 16.69f / tau;
+    return d0 <= 0.0f ? -1.0f : d0 * d0 * 1.00001f;
+}
+
+__device__ __forceinline__ void stage_cut(const ModelDev& M, float* __restrict__ cut, int tid) {
+    for (int j = tid; j < 3 * M.nj; j += blockDim.x) {
+        const int k = j % M.nj;
+        cut[j] = j < M.nj ? M.cutoff[k] : (j < 2 * M.nj ? M.cutoff_v[k] : live_thr2(M.tau, M.cutoff[k]));
+    }
+}
+
+// One joint's skeleton row (3x4 of the world->joint transform) and live threshold, loaded from
+// LDS into registers two MFMA groups before use, so the encoder math never waits on LDS.
+struct JRow {
+    f32x4 a, b, c;
+    float thr2, cv;
+};
+
+__device__ __forceinline__ JRow load_row(const float* __restrict__ sk, const float* __restrict__ cut, int j, int nj) {
+    const int jc = j < nj ? j : 0;
+    const f32x4* p = reinterpret_cast<const f32x4*>(sk + 12 * jc);
+    return JRow{p[0], p[1], p[2], cut[2 * nj + jc], cut[nj + jc]};
+}
+
+// bone direction u_j = q / max(|q|, 1e-12) of this lane's sample (q * rsq(max(|q|^2, 1e-24)),
+// within 2 ulp) and whether the joint's window may be non-zero (d^2 < thr2, conservative, see
+// live_thr2).  Branch-free (per-lane selects) so that it stays in the MFMA region it is
+// scheduled into.
+// With WV, also the joint's view-direction window w'_j = 1 - sigmoid(tau' (|q| - c'_j)) (hardware
+// sqrt/exp2/rcp, a few ulp; 0 for padding joints or without cutoff_viewdir) for the view layer.
+template <bool WV>
+__device__ __forceinline__ void u_joint(const ModelDev& M, const JRow& r, bool valid, float px, float py, float pz,
+                                        float& u0, float& u1, float& u2, bool& live, float& wv) {
+#ifdef ANERF_EXP_UFAST  // timing experiment only (stamps build): encoder VALU removed
+    u0 = px * r.a[0]; u1 = py; u2 = pz; live = false; wv = 0.0f; return;
+#endif
+    float qx = fmaf(r.a[3], 1.0f, fmaf(r.a[2], pz, fmaf(r.a[1], py, r.a[0] * px)));
+    float qy = fmaf(r.b[3], 1.0f, fmaf(r.b[2], pz, fmaf(r.b[1], py, r.b[0] * px)));
+    float qz = fmaf(r.c[3], 1.0f, fmaf(r.c[2], pz, fmaf(r.c[1], py, r.c[0] * px)));
+    qx = valid ? qx : 0.0f;
+    qy = valid ? qy : 0.0f;
+    qz = valid ? qz : 0.0f;
+    const float d2 = fmaf(qz, qz, fmaf(qy, qy, qx * qx));
+    const float inv = __builtin_amdgcn_rsqf(fmaxf(d2, 1e-24f));
+    u0 = qx * inv;
+    u1 = qy * inv;
+    u2 = qz * inv;
+    live = valid & (!M.sparse | !(d2 >= r.thr2));  // (no short-circuit: no branch; NaN -> live)
+    if constexpr (WV) {
+        const float d = __builtin_amdgcn_sqrtf(d2);
+        const float e = __builtin_amdgcn_exp2f(-(M.tau_v * (d - r.cv)) * 1.44269504f);
+        const float w = 1.0f - __builtin_amdgcn_rcpf(1.0f + e);
+        wv = (valid && M.cutoff_viewdir) ? w : 0.0f;
+    }
+}
+
+// The geometry of pair-of-pairs pp+1 is computed under the MFMAs of pp (software pipeline:
+// between two sched_barriers the scheduler interleaves the VALU with the async MFMAs).
+template <int RB>
+__device__ __forceinline__ void u_part(f32x16 (&acc)[RB], const ModelDev& M, const float* __restrict__ wp,
+                                       const float* __restrict__ sk, const float* __restrict__ cut, float px,
+                                       float py, float pz, int lane, JointMask* mask, float* __restrict__ uf,
+                                       float* __restrict__ wvo, Ring& sh, const float* __restrict__ next,
+                                       Stamps& st) {
+    const int hh = lane >> 5;
+    const int njh2 = M.njh2;
+    const int npp = njh2 / 2;
+    const int total_groups = 3 * npp;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(wp);
+    f32x2 ring[3][RB];  // groups 0 and 1 were prefetched into the shared ring by the caller
+    ring_take<RB>(ring[0], sh.v[0]);
+    ring_take<RB>(ring[1], sh.v[1]);
+    uint64_t m0 = 0, m1 = 0;
+    float f[6];
+    bool lv0, lv1;
+    const int nj = M.nj, j0 = hh * njh2;
+    JRow ra = load_row(sk, cut, j0, nj), rb2 = load_row(sk, cut, j0 + 1, nj);
+    float wv0, wv1;
+    u_joint<true>(M, ra, j0 < nj, px, py, pz, f[0], f[1], f[2], lv0, wv0);
+    u_joint<true>(M, rb2, j0 + 1 < nj, px, py, pz, f[3], f[4], f[5], lv1, wv1);
+    if (wvo) {  // w'_j of k-step p of the view layer's direction part (joint p + h NJH2)
+        wvo[lane] = wv0;
+        wvo[64 + lane] = wv1;
+    }
+    ra = load_row(sk, cut, j0 + 2, nj);
+    rb2 = load_row(sk, cut, j0 + 3, nj);
+    STAMP(st, 14);
+    for (int pp = 0; pp < npp; ++pp) {
+        if (mask) {
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const uint64_t b = __ballot(k == 0 ? lv0 : lv1);
+                const int ja = 2 * pp + k, jb = ja + njh2;
+                if (b & 0xffffffffull) {
+                    if (ja < 64) m0 |= 1ull << ja; else m1 |= 1ull << (ja - 64);
+                }
+                if (b >> 32) {
+                    if (jb < 64) m0 |= 1ull << jb; else m1 |= 1ull << (jb - 64);
+                }
+            }
+        }
+        if (uf) {  // keep this block's bone directions for the skip layer: [group][lane][2]
+#pragma unroll
+            for (int g = 0; g < 3; ++g)
+                *reinterpret_cast<f32x2*>(uf + ((pp * 3 + g) * 64 + lane) * 2) = f32x2{f[2 * g], f[2 * g + 1]};
+        }
+        float fn[6];
+        bool ln0 = false, ln1 = false;
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+            __builtin_amdgcn_sched_barrier(0);
+            const int gn = min(pp * 3 + g + 2, total_groups - 1);  // (a harmless reload at the end)
+            load_u_group<RB>(ring[(g + 2) % 3], rs, lane, gn);
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const float b = f[2 * g + t];
+#pragma unroll
+                for (int rb = 0; rb < RB; ++rb) acc[rb] = mfma_f32_32x32x2(ring[g % 3][rb][t], b, acc[rb]);
+            }
+            if (g == 0) {  // joint 2pp+2 from its prefetched row; then prefetch joint 2pp+4
+                float wv;
+                u_joint<true>(M, ra, j0 + 2 * pp + 2 < nj, px, py, pz, fn[0], fn[1], fn[2], ln0, wv);
+                pin(fn[0]), pin(fn[1]), pin(fn[2]), pin(ln0);
+                if (wvo && 2 * pp + 2 < njh2) wvo[(2 * pp + 2) * 64 + lane] = wv;
+                ra = load_row(sk, cut, j0 + 2 * pp + 4, nj);
+            }
+            if (g == 1) {
+                float wv;
+                u_joint<true>(M, rb2, j0 + 2 * pp + 3 < nj, px, py, pz, fn[3], fn[4], fn[5], ln1, wv);
+                pin(fn[3]), pin(fn[4]), pin(fn[5]), pin(ln1);
+                if (wvo && 2 * pp + 3 < njh2) wvo[(2 * pp + 3) * 64 + lane] = wv;
+                rb2 = load_row(sk, cut, j0 + 2 * pp + 5, nj);
+            }
+            interleave_mfma_valu<2 * RB, 8>();
+        }
+#pragma unroll
+        for (int i = 0; i < 6; ++i) f[i] = fn[i];
+        lv0 = ln0;
+        lv1 = ln1;
+    }
+    if (mask) {
+        mask->m0 = m0;
+        mask->m1 = m1;
+    }
+    if (next) ring_preload<16>(sh, next, lane);
+}
+
+// The skip layer's bone-direction part from the features u_part stored in LDS: a pure MFMA
+// stream (B operands read one group ahead) with the weight ring two groups ahead.
+template <int RB>
+__device__ __forceinline__ void u_part_lds(f32x16 (&acc)[RB], const ModelDev& M, const float* __restrict__ wp,
+                                           const float* __restrict__ uf, int lane, Ring& sh,
+                                           const float* __restrict__ next) {
+    const int total_groups = 3 * (M.njh2 / 2);
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(wp);
+    const f32x2* ub = reinterpret_cast<const f32x2*>(uf) + lane;
+    f32x2 ring[3][RB];
+    ring_take<RB>(ring[0], sh.v[0]);
+    ring_take<RB>(ring[1], sh.v[1]);
+    f32x2 bc = ub[0];
+    for (int g0 = 0; g0 < total_groups; g0 += 3) {
+#pragma unroll
+        for (int gg = 0; gg < 3; ++gg) {
+            __builtin_amdgcn_sched_barrier(0);
+            const int g = g0 + gg;
+            const int gn = min(g + 2, total_groups - 1);
+            load_u_group<RB>(ring[(gg + 2) % 3], rs, lane, gn);
+            const f32x2 bn = ub[min(g + 1, total_groups - 1) * 64];
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int rb = 0; rb < RB; ++rb) acc[rb] = mfma_f32_32x32x2(ring[gg][rb][t], bc[t], acc[rb]);
+            bc = bn;
+        }
+    }
+    if (next) ring_preload<16>(sh, next, lane);
+}
+
+template <int MR>
+struct VPart {
+    static constexpr int KB = ((MR + 1) + 1) & ~1;  // k-steps per joint (even)
+    static constexpr int GB = KB / 2;               // float2 groups per joint
+};
+
+__device__ __forceinline__ void v_geom(const ModelDev& M, const float* __restrict__ sk, const float* __restrict__ cut,
+                                       int j, float px, float py, float pz, float& dist, float& w) {
+    float qx, qy, qz;
+    joint_local(sk + 12 * j, px, py, pz, qx, qy, qz);
+    dist = norm3(qx, qy, qz);
+    const float wc = cutoff_w(M.tau, dist, cut[j]);
+    w = M.use_cutoff ? wc : 1.0f;
+}
+
+template <int RB, int MR>
+__device__ __forceinline__ void v_part(f32x16 (&acc)[RB], const ModelDev& M, const float* __restrict__ wp,
+                                       const float* __restrict__ sk, const float* __restrict__ cut, float px,
+                                       float py, float pz, int lane, JointMask mask, Stamps& st) {
+    constexpr int GB = VPart<MR>::GB;
+    constexpr int KB = VPart<MR>::KB;
+    constexpr int PER = (MR + GB - 2) / (GB - 1);  // sin/cos terms of the next joint per group 1..GB-1
+    const int hh = lane >> 5;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(wp);
+    const int voff = lane * 8;
+    const bool dist_in = M.use_cutoff && M.cutoff_inputs;
+    uint64_t r0 = mask.m0, r1 = mask.m1;
+    int j = mask_pop(r0, r1);
+    if (j < 0) return;
+    int jn = mask_pop(r0, r1);
+    f32x2 ring[GB][RB];
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) ring[g][rb] = bload2(rs, voff, ((j * GB + g) * RB + rb) * 512);
+    float f[KB];
+    {
+        float dist, w;
+        v_geom(M, sk, cut, j, px, py, pz, dist, w);
+#pragma unroll
+        for (int t = 0; t < MR; ++t) {
+            float sn, cs;
+            sincos_rr(dist * (float)(1 << t), sn, cs);
+            f[t] = (hh ? cs : sn) * w;
+        }
+        f[MR] = hh ? 0.0f : (dist_in ? dist * w : dist);
+#pragma unroll
+        for (int t = MR + 1; t < KB; ++t) f[t] = 0.0f;
+    }
+    STAMP(st, 15);
+    while (j >= 0) {
+        float fn[KB];
+        float dn = 0.0f, wn = 0.0f;
+        const int jg = jn >= 0 ? jn : j;  // geometry of the next joint (harmless redo at the end)
+#pragma unroll
+        for (int g = 0; g < GB; ++g) {
+            __builtin_amdgcn_sched_barrier(0);
+            constexpr int PD = 2;
+            if (g + PD < GB) {
+#pragma unroll
+                for (int rb = 0; rb < RB; ++rb)
+                    ring[(g + PD) % GB][rb] = bload2(rs, voff, ((j * GB + g + PD) * RB + rb) * 512);
+            } else {  // the next joint's first groups (this joint's again after the last: harmless)
+#pragma unroll
+                for (int rb = 0; rb < RB; ++rb)
+                    ring[(g + PD) % GB][rb] = bload2(rs, voff, ((jg * GB + g + PD - GB) * RB + rb) * 512);
+            }
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const float b = f[2 * g + t];
+#pragma unroll
+                for (int rb = 0; rb < RB; ++rb) acc[rb] = mfma_f32_32x32x2(ring[g][rb][t], b, acc[rb]);
+            }
+            // next joint's features under these MFMAs
+            if (g == 0) {
+                v_geom(M, sk, cut, jg, px, py, pz, dn, wn);
+                pin(dn), pin(wn);
+            } else {
+#pragma unroll
+                for (int t = (g - 1) * PER; t < g * PER && t < MR; ++t) {
+                    float sn, cs;
+                    sincos_rr(dn * (float)(1 << t), sn, cs);
+                    fn[t] = (hh ? cs : sn) * wn;
+                    pin(fn[t]);
+                }
+            }
+            interleave_mfma_valu<2 * RB, 8>();
+        }
+        fn[MR] = hh ? 0.0f : (dist_in ? dn * wn : dn);
+#pragma unroll
+        for (int t = MR + 1; t < KB; ++t) fn[t] = 0.0f;
+#pragma unroll
+        for (int t = 0; t < KB; ++t) f[t] = fn[t];
+        j = jn;
+        jn = mask_pop(r0, r1);
+    }
+}
+
+// View layer, per-ray direction part: acc[RBV] += G^T * [w'_j, 1]  (G in LDS).  k-step p pairs
+// joint p (lane half 0) with joint p + NJH2 (half 1), exactly the u part's pairing, so w'_j comes
+// from the u part (wvp, stored per lane); k-step NJH2 adds the bias / framecode column NJ.  The G
+// values of the next k-step are read under the current k-step's MFMAs.
+template <int RBV>
+__device__ __forceinline__ void view_dir_part(f32x16 (&acc)[RBV], const ModelDev& M, const float* __restrict__ G,
+                                              const float* __restrict__ wvp, int lane) {
+    constexpr int WH = RBV * 32;
+    const int hh = lane >> 5, sl = lane & 31;
+    const int njh2 = M.njh2;
+    auto col = [&](int p) { return p < njh2 ? p + hh * njh2 : M.nj + hh; };
+    float gv[RBV];
+#pragma unroll
+    for (int rb = 0; rb < RBV; ++rb) gv[rb] = G[col(0) * WH + sl + 32 * rb];
+    float b = wvp[lane];
+    for (int p = 0; p <= njh2; ++p) {
+        __builtin_amdgcn_sched_barrier(0);
+        const int pn = min(p + 1, njh2);
+        float gn[RBV];
+#pragma unroll
+        for (int rb = 0; rb < RBV; ++rb) gn[rb] = G[col(pn) * WH + sl + 32 * rb];
+        const float bn = pn < njh2 ? wvp[pn * 64 + lane] : (hh ? 0.0f : 1.0f);
+#pragma unroll
+        for (int rb = 0; rb < RBV; ++rb) acc[rb] = mfma_f32_32x32x2(gv[rb], b, acc[rb]);
+#pragma unroll
+        for (int rb = 0; rb < RBV; ++rb) gv[rb] = gn[rb];
+        b = bn;
+    }
+}
+
+// Encoder + density trunk of one 32-sample block: L0 (u and v parts), the hidden layers with the
+// skip; acc ends as the pre-activation of the last hidden layer.  `after_last` is the weight stream
+// that follows (the feature layer, or nothing for density-only queries).
+template <int W, int MR>
+__device__ __forceinline__ void mlp_trunk(const ModelDev& M, const NetDev& net, const float* __restrict__ sk,
+                                          const float* __restrict__ cut, float px, float py, float pz, int lane,
+                                          const float* __restrict__ bias, float* __restrict__ uf,
+                                          float* __restrict__ wvo, f32x16 (&acc)[W / 32], f32x16 (&h)[W / 32],
+                                          Ring& ring, JointMask& mask, const float* __restrict__ after_last,
+                                          Stamps& st) {
+    constexpr int RB = W / 32;
+    const int hh = lane >> 5;
+    float nosig = 0.0f;
+    constexpr bool HANDOFF = (2 * RB == 16);  // u-part groups have the regs layers' group size
+    ring_preload<2 * RB>(ring, net.wl[0], lane);  // the u part's first groups, early
+    load_bias<RB>(acc, bias, hh);
+    STAMP(st, 10);
+    u_part<RB>(acc, M, net.wl[0], sk, cut, px, py, pz, lane, &mask, uf, wvo, ring, M.D > 1 ? net.wl[1] : after_last,
+               st);
+    STAMP(st, 8);
+    v_part<RB, MR>(acc, M, net.wl0v, sk, cut, px, py, pz, lane, mask, st);
+    STAMP(st, 9);
+    for (int L = 1; L < M.D; ++L) {
+        const float* after = L + 1 < M.D ? net.wl[L + 1] : after_last;
+        const bool skl = (L == M.skip + 1);
+        mlp_layer<RB, RB, true, true, false>(acc, acc, h, bias + L * W, net.wl[L], lane, ring,
+                                             skl ? (HANDOFF ? net.wskipu : nullptr) : after, nullptr, nosig);
+        STAMP(st, 11);
+        if (skl) {  // x part after the h part
+            if (!HANDOFF) ring_preload<2 * RB>(ring, net.wskipu, lane);
+            if (uf)
+                u_part_lds<RB>(acc, M, net.wskipu, uf, lane, ring, after);
+            else
+                u_part<RB>(acc, M, net.wskipu, sk, cut, px, py, pz, lane, nullptr, nullptr, nullptr, ring, after, st);
+            v_part<RB, MR>(acc, M, net.wskipv, sk, cut, px, py, pz, lane, mask, st);
+            STAMP(st, 12);
+        }
+    }
+}
+
+// One 32-sample block of one ray through a whole NeRF: raw (rgb, sigma) into LDS.
+template <int W, int MR>
+__device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __restrict__ ray,
+                          const float* __restrict__ sk, const float* __restrict__ cut, const float* __restrict__ z,
+                          int n, int s0,
+                          const float* __restrict__ G, float* __restrict__ raw_out, int lane,
+                          unsigned long long* mfma_count, const float* __restrict__ bias, float* __restrict__ uf,
+                          float* __restrict__ wvp, Stamps& st) {
+    constexpr int RB = W / 32;
+    constexpr int RBV = (W / 2) / 32;
+    const int sl = lane & 31, hh = lane >> 5;
+    int s = s0 + sl;
+    if (s >= n) s = n - 1;
+    const float zs = z[s];
+    // pts = rays_o + rays_d * z (raycasters.py:658), separately rounded
+    const float px = ray[0] + ray[3] * zs;
+    const float py = ray[1] + ray[4] * zs;
+    const float pz = ray[2] + ray[5] * zs;
+
+    f32x16 acc[RB], h[RB];
+    JointMask mask;
+    Ring ring;
+    mlp_trunk<W, MR>(M, net, sk, cut, px, py, pz, lane, bias, uf, wvp, acc, h, ring, mask, net.wview, st);
+    // views_linears.0 with feature_linear fused in (W' = Wv_f Wf, see pack_net) on relu(h_last),
+    // alpha_linear folded into its groups (same relu'd B operands), + the factorised
+    // direction / code / bias part from G, then relu
+    float sig = 0.0f;
+    f32x16 av[RBV];
+    mlp_layer<RBV, RB, true, false, true>(av, acc, h, nullptr, net.wview, lane, ring, nullptr, bias + (M.D + 1) * W,
+                                          sig);
+    STAMP(st, 16);
+    sig += __shfl_xor(sig, 32);
+    sig += net.balpha;
+    view_dir_part<RBV>(av, M, G, wvp, lane);
+    STAMP(st, 17);
+    float rgb[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const float* wr = net.wrgb + (c * 2 + hh) * RBV * 16;
+        float a = 0.0f;
+#pragma unroll
+        for (int rb = 0; rb < RBV; ++rb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) a += wr[rb * 16 + i] * relu_act(av[rb][i]);
+        a += __shfl_xor(a, 32);
+        rgb[c] = a + net.brgb[c];
+    }
+    STAMP(st, 13);
+    if (mfma_count && lane == 0) {  // exact MFMA work of this block (wave-uniform quantities)
+        const int act = __builtin_popcountll(mask.m0) + __builtin_popcountll(mask.m1);
+        const int xk = 3 * M.njh2 + act * VPart<MR>::KB;  // k-steps of one x part
+        long long k = (long long)xk * RB + (long long)(M.D - 1) * (W / 2) * RB + (long long)(W / 2) * RBV +
+                      (long long)(M.njh2 + 1) * RBV;
+        if (M.skip + 1 < M.D) k += (long long)xk * RB;
+        atomicAdd(mfma_count, (unsigned long long)k);
+    }
+    if (hh == 0 && s0 + sl < n) {
+        float* o = raw_out + 4 * (s0 + sl);
+        o[0] = rgb[0];
+        o[1] = rgb[1];
+        o[2] = rgb[2];
+        o[3] = sig;
+    }
+}
+

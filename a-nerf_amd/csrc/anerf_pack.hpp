@@ -1,0 +1,301 @@
+// anerf_pack.hpp — host side: weight packing into the MFMA operand streams, descriptor validation, model binding.
+// Part of the single translation unit anerf_render.hip (included there, in order).
+#pragma once
+
+// ======================================================================= host side
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(x)                                                                              \
+    do {                                                                                        \
+        hipError_t e_ = (x);                                                                    \
+        if (e_ != hipSuccess) return fail(ANERF_EHIP, std::string(#x ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+// ---- packing (host): k-source maps into the MFMA operand order
+struct Packer {
+    std::vector<float> buf;
+    size_t add(const std::vector<float>& v) {
+        size_t off = buf.size();
+        buf.insert(buf.end(), v.begin(), v.end());
+        while (buf.size() % 64) buf.push_back(0.0f);  // 256-byte alignment of every array
+        return off;
+    }
+};
+
+// W torch [n_out][ld]; kmap(q, h) -> input column or -1; nq k-steps (even); out [nq/2][RB][64][2]
+template <class F>
+std::vector<float> pack_kmajor(const float* Wt, int n_out, int ld, int nq, F kmap) {
+    const int RB = n_out / 32;
+    std::vector<float> out((size_t)(nq / 2) * RB * 128, 0.0f);
+    for (int g = 0; g < nq / 2; ++g)
+        for (int rb = 0; rb < RB; ++rb)
+            for (int l = 0; l < 64; ++l)
+                for (int t = 0; t < 2; ++t) {
+                    const int q = 2 * g + t;
+                    const int col = kmap(q, l >> 5);
+                    const int row = 32 * rb + (l & 31);
+                    out[(((size_t)g * RB + rb) * 64 + l) * 2 + t] = col >= 0 ? Wt[(size_t)row * ld + col] : 0.0f;
+                }
+    return out;
+}
+
+// ng groups of F floats per lane, stored [group][F/4][64 lanes][4] (one 1 KiB b128 load per F/4);
+// fn(g, s, lane) = value of slot float s of lane `lane` in group g
+template <class Fn>
+std::vector<float> pack_groups(int ng, int F, Fn fn) {
+    std::vector<float> out((size_t)ng * F * 64, 0.0f);
+    for (int g = 0; g < ng; ++g)
+        for (int i = 0; i < F / 4; ++i)
+            for (int l = 0; l < 64; ++l)
+                for (int e = 0; e < 4; ++e) out[(((size_t)g * (F / 4) + i) * 64 + l) * 4 + e] = fn(g, 4 * i + e, l);
+    return out;
+}
+
+// dense layer for mlp_layer: RBO lead groups (block rb, k-steps 0..15) then k-major groups of
+// KG = 16/RBO k-steps x RBO blocks (slot float rb*KG + t); k-step q, half h -> input column
+// col_off + 32 (q >> 4) + acc_row(q & 15, h)
+std::vector<float> pack_layer(const float* Wt, int n_out, int ld, int col_off, int n_in) {
+    const int RBO = n_out / 32, RBI = n_in / 32, KG = 16 / RBO;
+    const int ng = RBO + (16 * RBI - 16) / KG;
+    return pack_groups(ng, 16, [&](int g, int sl, int l) {
+        int rb, q;
+        if (g < RBO) {
+            rb = g, q = sl;
+        } else {
+            rb = sl / KG, q = 16 + (g - RBO) * KG + sl % KG;
+        }
+        const int col = col_off + 32 * (q >> 4) + acc_row(q & 15, l >> 5);
+        return Wt[(size_t)(32 * rb + (l & 31)) * ld + col];
+    });
+}
+
+// bone-direction part: k-step q = 3p + c, half h -> joint p + h*njh2, column nv*nj + 3j + c;
+// groups of 2 k-steps x RB blocks (slot float 2 rb + t)
+std::vector<float> pack_upart(const float* Wt, int n_out, int ld, int nj, int njh2, int mr) {
+    const int nv = 1 + 2 * mr, RB = n_out / 32;
+    return pack_groups(3 * njh2 / 2, 2 * RB, [&](int g, int sl, int l) {
+        const int rb = sl / 2, q = 2 * g + sl % 2;
+        const int p = q / 3, c = q % 3;
+        const int j = p + (l >> 5) * njh2;
+        return j < nj ? Wt[(size_t)(32 * rb + (l & 31)) * ld + nv * nj + 3 * j + c] : 0.0f;
+    });
+}
+
+// windowed part, per joint j: k-step t < mr -> (sin_t, cos_t) = columns ((1+2t)NJ + j, (2+2t)NJ + j);
+// t == mr -> (dist, pad); padded to an even count.  Layout [joint][group][RB][64][2].
+std::vector<float> pack_vpart(const float* Wt, int n_out, int ld, int nj, int mr) {
+    const int kb = ((mr + 1) + 1) & ~1;
+    std::vector<float> out;
+    for (int j = 0; j < nj; ++j) {
+        std::vector<float> pj = pack_kmajor(Wt, n_out, ld, kb, [&](int t, int h) {
+            if (t < mr) return (1 + 2 * t + h) * nj + j;
+            if (t == mr && h == 0) return j;
+            return -1;
+        });
+        out.insert(out.end(), pj.begin(), pj.end());
+    }
+    return out;
+}
+
+// per-lane-half vectors [rb][h][16] of a length-n vector in accumulator row order
+std::vector<float> pack_rowvec(const float* v, int n, bool half_major) {
+    const int RB = n / 32;
+    std::vector<float> out((size_t)RB * 32, 0.0f);
+    for (int rb = 0; rb < RB; ++rb)
+        for (int h = 0; h < 2; ++h)
+            for (int i = 0; i < 16; ++i) {
+                const size_t idx = half_major ? ((size_t)h * RB + rb) * 16 + i : ((size_t)rb * 2 + h) * 16 + i;
+                out[idx] = v[32 * rb + acc_row(i, h)];
+            }
+    return out;
+}
+
+}  // namespace
+
+struct anerf_model {
+    anerf_model_desc desc;
+    int device;
+    int njh2, ngh;
+    float* dev_buf;
+    size_t dev_bytes;
+    ModelDev md;
+};
+
+template <int WIDTH>
+static void host_row_sum(const float* x, int64_t xs, int64_t n, float* out) {
+    // host twin of torch_row_sum (used for the eval-mode mean framecode)
+    const int64_t size = n / 4;
+    int lp = 0;
+    while (((int64_t)1 << lp) < size) ++lp;
+    lp /= 4;
+    if (lp < 4) lp = 4;
+    const int64_t step = (int64_t)1 << lp, mask = step - 1;
+    float acc[4][4][WIDTH] = {};
+    int64_t i = 0;
+    while (i + step <= size) {
+        for (int64_t jj = 0; jj < step; ++jj, ++i)
+            for (int k = 0; k < 4; ++k)
+                for (int l = 0; l < WIDTH; ++l) acc[0][k][l] += x[((4 * i + k) * WIDTH + l) * xs];
+        for (int j = 1; j < 4; ++j) {
+            for (int k = 0; k < 4; ++k)
+                for (int l = 0; l < WIDTH; ++l) {
+                    acc[j][k][l] += acc[j - 1][k][l];
+                    acc[j - 1][k][l] = 0.0f;
+                }
+            if ((i & (mask << (j * lp))) != 0) break;
+        }
+    }
+    for (; i < size; ++i)
+        for (int k = 0; k < 4; ++k)
+            for (int l = 0; l < WIDTH; ++l) acc[0][k][l] += x[((4 * i + k) * WIDTH + l) * xs];
+    for (int j = 1; j < 4; ++j)
+        for (int k = 0; k < 4; ++k)
+            for (int l = 0; l < WIDTH; ++l) acc[0][k][l] += acc[j][k][l];
+    for (int64_t e = size * 4; e < n; ++e)
+        for (int l = 0; l < WIDTH; ++l) acc[0][0][l] += x[(e * WIDTH + l) * xs];
+    for (int k = 1; k < 4; ++k)
+        for (int l = 0; l < WIDTH; ++l) acc[0][0][l] += acc[0][k][l];
+    for (int l = 0; l < WIDTH; ++l) out[l] = acc[0][0][l];
+}
+
+static int validate_desc(const anerf_model_desc* d) {
+    if (!d) return fail(ANERF_EINVAL, "desc is NULL");
+    if (d->net_width != 64 && d->net_width != 128 && d->net_width != 256)
+        return fail(ANERF_EINVAL, "net_width must be 64, 128 or 256");
+    if (d->net_depth < 2 || d->net_depth > MAXL) return fail(ANERF_EINVAL, "net_depth outside [2, 16]");
+    if (d->multires != 7 && d->multires != 10) return fail(ANERF_EINVAL, "multires must be 7 or 10");
+    if (d->multires_views != 4) return fail(ANERF_EINVAL, "multires_views must be 4 (the reference default)");
+    if (d->n_joints < 1 || d->n_joints > 128) return fail(ANERF_EINVAL, "n_joints outside [1, 128]");
+    if (d->skip < 0) return fail(ANERF_EINVAL, "skip must be >= 0");
+    if (d->framecode_ch < 0 || d->framecode_ch > 64) return fail(ANERF_EINVAL, "framecode_ch outside [0, 64]");
+    if (d->framecode_ch > 0 && d->n_framecodes <= 0) return fail(ANERF_EINVAL, "n_framecodes must be > 0");
+    if (d->density_scale == 0.0f) return fail(ANERF_EINVAL, "density_scale must be non-zero");
+    return ANERF_OK;
+}
+
+static int pack_net(const anerf_model_desc* d, int njh2, const anerf_net_weights* w, Packer& pk,
+                    std::vector<size_t>& offs) {
+    const int W = d->net_width, WH = W / 2, nj = d->n_joints, mr = d->multires, mrv = d->multires_views;
+    const int cin = nj * (1 + 2 * mr) + 3 * nj;
+    const int nk = 1 + 2 * mrv;
+    const int cv = 3 * nj * nk, cfc = d->framecode_ch;
+    const int ldv = W + cv + cfc;
+    for (int i = 0; i < d->net_depth; ++i)
+        if (!w->pts_w[i] || !w->pts_b[i]) return fail(ANERF_EINVAL, "missing pts_linears weight");
+    if (!w->alpha_w || !w->alpha_b || !w->feature_w || !w->feature_b || !w->views_w || !w->views_b || !w->rgb_w ||
+        !w->rgb_b)
+        return fail(ANERF_EINVAL, "missing head weight");
+    if (cfc && !w->codes) return fail(ANERF_EINVAL, "framecode weights missing");
+    offs.clear();
+    // [0] layer 0 u part, [1..D-1] activation parts, [D] layer 0 v part, [D+1, D+2] skip u / v parts,
+    // [D+3 ..] biases
+    offs.push_back(pk.add(pack_upart(w->pts_w[0], W, cin, nj, njh2, mr)));
+    for (int i = 1; i < d->net_depth; ++i) {
+        const bool sk = (i == d->skip + 1);
+        offs.push_back(pk.add(pack_layer(w->pts_w[i], W, sk ? cin + W : W, sk ? cin : 0, W)));
+    }
+    offs.push_back(pk.add(pack_vpart(w->pts_w[0], W, cin, nj, mr)));
+    const int skl = d->skip + 1;
+    if (skl < d->net_depth) {
+        offs.push_back(pk.add(pack_upart(w->pts_w[skl], W, cin + W, nj, njh2, mr)));
+        offs.push_back(pk.add(pack_vpart(w->pts_w[skl], W, cin + W, nj, mr)));
+    } else {
+        offs.push_back((size_t)-1);
+        offs.push_back((size_t)-1);
+    }
+    for (int i = 0; i < d->net_depth; ++i) offs.push_back(pk.add(pack_rowvec(w->pts_b[i], W, false)));
+    offs.push_back(pk.add(pack_rowvec(w->alpha_w, W, true)));                         // walpha
+    // feature_linear has no activation, so views_linears.0's feature block and feature_linear fuse
+    // into one layer on the last hidden state (nerf.py:110-112): W' = Wv_f Wf (WH x W) and
+    // b' = Wv_f bf + bv, formed in double and rounded once.  The feature layer disappears.
+    std::vector<float> wfused((size_t)WH * W), bfused(WH);
+    for (int n = 0; n < WH; ++n) {
+        std::vector<double> row(W, 0.0);
+        double bacc = (double)w->views_b[n];
+        for (int m = 0; m < W; ++m) {
+            const double v = (double)w->views_w[(size_t)n * ldv + m];
+            const float* wf = w->feature_w + (size_t)m * W;
+            for (int k = 0; k < W; ++k) row[k] += v * (double)wf[k];
+            bacc += v * (double)w->feature_b[m];
+        }
+        for (int k = 0; k < W; ++k) wfused[(size_t)n * W + k] = (float)row[k];
+        bfused[n] = (float)bacc;
+    }
+    offs.push_back(pk.add(std::vector<float>()));                                     // wfeat (fused away)
+    offs.push_back(pk.add(pack_rowvec(w->feature_b, W, false)));                      // bfeat (unused)
+    offs.push_back(pk.add(pack_layer(wfused.data(), WH, W, 0, W)));                   // wview = Wv_f Wf
+    {
+        const int tp = (3 * nk + 3) & ~3;
+        std::vector<float> t((size_t)nj * WH * tp, 0.0f);
+        for (int j = 0; j < nj; ++j)
+            for (int k = 0; k < nk; ++k)
+                for (int c = 0; c < 3; ++c)
+                    for (int n = 0; n < WH; ++n)
+                        t[((size_t)j * WH + n) * tp + k * 3 + c] = w->views_w[(size_t)n * ldv + W + k * 3 * nj + 3 * j + c];
+        offs.push_back(pk.add(t));                                                    // wvdir
+    }
+    {
+        std::vector<float> t((size_t)std::max(cfc, 1) * WH, 0.0f);
+        for (int m = 0; m < cfc; ++m)
+            for (int n = 0; n < WH; ++n) t[(size_t)m * WH + n] = w->views_w[(size_t)n * ldv + W + cv + m];
+        offs.push_back(pk.add(t));                                                    // wvcode
+    }
+    offs.push_back(pk.add(bfused));                                                   // bview = Wv_f bf + bv
+    {
+        std::vector<float> t;
+        for (int c = 0; c < 3; ++c) {
+            // [c][h][rb][16]
+            std::vector<float> v = pack_rowvec(w->rgb_w + (size_t)c * WH, WH, true);
+            t.insert(t.end(), v.begin(), v.end());
+        }
+        offs.push_back(pk.add(t));                                                    // wrgb
+    }
+    offs.push_back(pk.add(std::vector<float>(w->rgb_b, w->rgb_b + 3)));               // brgb
+    {
+        std::vector<float> t((size_t)(std::max(d->n_framecodes, 0) + 1) * std::max(cfc, 1), 0.0f);
+        if (cfc) {
+            std::memcpy(t.data(), w->codes, sizeof(float) * (size_t)d->n_framecodes * cfc);
+            for (int m = 0; m < cfc; ++m) {  // codes.weight.mean(0) = torch sum over dim 0 / n
+                float s;
+                host_row_sum<1>(w->codes + m, cfc, d->n_framecodes, &s);
+                t[(size_t)d->n_framecodes * cfc + m] = s / (float)d->n_framecodes;
+            }
+        }
+        offs.push_back(pk.add(t));                                                    // codes
+    }
+    return ANERF_OK;
+}
+
+static void bind_net(const anerf_model_desc* d, const float* base, const std::vector<size_t>& o, float balpha,
+                     NetDev& nd) {
+    std::memset(&nd, 0, sizeof(nd));
+    const int D = d->net_depth;
+    size_t k = 0;
+    nd.wl[0] = base + o[k++];
+    for (int i = 1; i < D; ++i) nd.wl[i] = base + o[k++];
+    nd.wl0v = base + o[k++];
+    nd.wskipu = o[k] == (size_t)-1 ? nullptr : base + o[k];
+    ++k;
+    nd.wskipv = o[k] == (size_t)-1 ? nullptr : base + o[k];
+    ++k;
+    for (int i = 0; i < D; ++i) nd.bl[i] = base + o[k++];
+    nd.walpha = base + o[k++];
+    nd.wfeat = base + o[k++];
+    nd.bfeat = base + o[k++];
+    nd.wview = base + o[k++];
+    nd.wvdir = base + o[k++];
+    nd.wvcode = base + o[k++];
+    nd.bview = base + o[k++];
+    nd.wrgb = base + o[k++];
+    nd.brgb = base + o[k++];
+    nd.codes = base + o[k++];
+    nd.balpha = balpha;
+}
+

@@ -1,0 +1,125 @@
+// anerf_types.hpp — device-side model / launch argument structs, diagnostic stamps, LDS plan.
+// Part of the single translation unit anerf_render.hip (included there, in order).
+#pragma once
+
+
+// Diagnostic build only (-DANERF_STAMPS): per-phase shader-cycle totals, summed over waves into
+// RenderArgs::stamps[16]; read only by tools/stamps.py, never part of an output.
+struct Stamps {
+#ifdef ANERF_STAMPS
+    unsigned long long last, acc[24];
+#endif
+};
+#ifdef ANERF_STAMPS
+#define STAMP_INIT(st)                                      \
+    do {                                                    \
+        (st).last = __builtin_amdgcn_s_memtime();           \
+        for (int i_ = 0; i_ < 24; ++i_) (st).acc[i_] = 0;   \
+    } while (0)
+#define STAMP(st, i)                                                      \
+    do {                                                                  \
+        __builtin_amdgcn_sched_barrier(0);                                \
+        const unsigned long long now_ = __builtin_amdgcn_s_memtime();     \
+        (st).acc[i] += now_ - (st).last;                                  \
+        (st).last = now_;                                                 \
+        __builtin_amdgcn_sched_barrier(0);                                \
+    } while (0)
+#define STAMP_FLUSH(st, ptr)                                              \
+    do {                                                                  \
+        if ((threadIdx.x & 63) == 0 && (ptr))                             \
+            for (int i_ = 0; i_ < 24; ++i_) atomicAdd((ptr) + i_, (st).acc[i_]); \
+    } while (0)
+#else
+#define STAMP_INIT(st) do { } while (0)
+#define STAMP(st, i) do { } while (0)
+#define STAMP_FLUSH(st, ptr) do { } while (0)
+#endif
+
+#define MAXL 16
+
+// ======================================================================= device model
+struct NetDev {
+    const float* wl[MAXL];   // packed layer weights; [0] bone-direction part of x, [i>0] activation (regs) part
+    const float* wl0v;       // layer 0, per-joint windowed part of x (dist, sin, cos)
+    const float* bl[MAXL];   // packed biases [RB][2][16]
+    const float* wskipu;     // skip layer, bone-direction part of x, or null
+    const float* wskipv;     // skip layer, per-joint windowed part of x
+    const float* walpha;     // [2][RB][16]
+    const float* wfeat;      // packed regs W->W
+    const float* bfeat;      // packed bias
+    const float* wview;      // packed regs W->W/2 (feature part of views_linears.0)
+    const float* wvdir;      // [NJ][W/2][28] direction part (k*3 + c, padded), transposed
+    const float* wvcode;     // [cfc][W/2] code part, transposed
+    const float* bview;      // [W/2]
+    const float* wrgb;       // [3][2][RBV][16]
+    const float* brgb;       // [3]
+    const float* codes;      // [n_codes + 1][cfc]: last row = eval-mode mean code
+    float balpha;
+};
+
+struct ModelDev {
+    int nj, njh2, ngh, D, skip, mr, mrv, use_cutoff, cutoff_inputs, cutoff_viewdir, cfc, n_codes, softplus;
+    int sparse;  // windowed features are exactly 0 where w == 0 (use_cutoff && cutoff_inputs)
+    float shift, B, tau, tau_v;
+    const float* cutoff;
+    const float* cutoff_v;
+    NetDev net[2];
+};
+
+struct RenderArgs {
+    const float* rb;
+    int64_t n;
+    int stride, S, I, R;
+    const float* skts;
+    const int32_t* ray_pose;
+    const float* cams;
+    const float* near;
+    const float* far;
+    float *rgb, *disp, *acc, *rgb0, *disp0, *acc0, *alpha, *alpha0;
+    float *dbg_z0, *dbg_raw0, *dbg_w0, *dbg_z1, *dbg_raw1;
+    unsigned long long* mfma_count;
+    unsigned long long* stamps;
+};
+
+// ======================================================================= LDS plan
+struct LdsPlan {
+    int ray, sk, zc, zf, raw, g, scr, bias, cut, uf, wv;  // float offsets (uf < 0: no u-feature store)
+    int total;                          // floats
+    int sk_stride, z_stride, raw_stride, g_stride, scr_stride, uf_stride, wv_stride;
+};
+
+__host__ __device__ inline int pad32(int x) { return (x + 31) & ~31; }
+
+__host__ __device__ inline LdsPlan make_plan(int R, int nj, int W, int S, int T, int mrv, int ngh, int D, int njh2,
+                                             bool with_uf) {
+    LdsPlan p;
+    const int wh = W / 2;
+    const int nk = 1 + 2 * mrv;
+    p.sk_stride = nj * 12;
+    p.z_stride = pad32(T > S ? T : S);
+    p.raw_stride = p.z_stride * 4;
+    p.g_stride = 2 * ngh * wh;
+    int scr_a = 8 * p.z_stride;          // composite / importance scratch
+    int scr_b = ((3 * nk + 3) & ~3) * nj + 256;  // trig table for G + per-part bias partials (256 / WH parts x WH)
+    p.scr_stride = (scr_a > scr_b ? scr_a : scr_b);
+    int o = 0;
+    p.ray = o; o += 16 * R;
+    p.sk = o; o += p.sk_stride * R;
+    p.zc = o; o += p.z_stride * R;
+    p.zf = o; o += p.z_stride * R;
+    p.raw = o; o += p.raw_stride * R;
+    p.g = o; o += p.g_stride * R;
+    p.scr = o; o += p.scr_stride * R;
+    o = (o + 3) & ~3;
+    p.bias = o; o += (D + 2) * W;  // the current net's hidden + feature biases, accumulator order; w_alpha
+    p.cut = o; o += 3 * nj;        // window: cutoff distances (points, view directions), live thresholds
+    o = (o + 3) & ~3;
+    p.uf_stride = 64 * 3 * njh2;   // per wave: the L0 bone directions, re-read by the skip layer
+    p.uf = with_uf ? o : -1;
+    if (with_uf) o += 4 * p.uf_stride;
+    p.wv_stride = 64 * njh2;       // per wave: view-direction window weights w'_j of the current block
+    p.wv = o; o += 4 * p.wv_stride;
+    p.total = (o + 3) & ~3;
+    return p;
+}
+
