@@ -171,7 +171,7 @@ __global__ __launch_bounds__(256, 1) void density_kernel(ModelDev M, DensityArgs
         f32x16 acc[RB], h[RB];
         JointMask mask;
         Ring ring;
-        mlp_trunk<W, MR>(M, net, lds + P.sk, lds + P.cut, px, py, pz, lane, lds + P.bias, uf, nullptr, acc, h, ring,
+        mlp_trunk<W, MR, false>(M, net, lds + P.sk, lds + P.cut, px, py, pz, lane, lds + P.bias, uf, nullptr, acc, h, ring,
                          mask, nullptr, st);
         // alpha_linear on relu(h_last), in the k-step order of the render path's fused alpha head
         float sig = 0.0f;

@@ -257,7 +257,7 @@ __device__ __forceinline__ void u_joint(const ModelDev& M, const JRow& r, bool v
 
 // The geometry of pair-of-pairs pp+1 is computed under the MFMAs of pp (software pipeline:
 // between two sched_barriers the scheduler interleaves the VALU with the async MFMAs).
-template <int RB>
+template <int RB, bool WV>
 __device__ __forceinline__ void u_part(f32x16 (&acc)[RB], const ModelDev& M, const float* __restrict__ wp,
                                        const float* __restrict__ sk, const float* __restrict__ cut, float px,
                                        float py, float pz, int lane, JointMask* mask, float* __restrict__ uf,
@@ -277,9 +277,9 @@ __device__ __forceinline__ void u_part(f32x16 (&acc)[RB], const ModelDev& M, con
     const int nj = M.nj, j0 = hh * njh2;
     JRow ra = load_row(sk, cut, j0, nj), rb2 = load_row(sk, cut, j0 + 1, nj);
     float wv0, wv1;
-    u_joint<true>(M, ra, j0 < nj, px, py, pz, f[0], f[1], f[2], lv0, wv0);
-    u_joint<true>(M, rb2, j0 + 1 < nj, px, py, pz, f[3], f[4], f[5], lv1, wv1);
-    if (wvo) {  // w'_j of k-step p of the view layer's direction part (joint p + h NJH2)
+    u_joint<WV>(M, ra, j0 < nj, px, py, pz, f[0], f[1], f[2], lv0, wv0);
+    u_joint<WV>(M, rb2, j0 + 1 < nj, px, py, pz, f[3], f[4], f[5], lv1, wv1);
+    if constexpr (WV) {  // w'_j of k-step p of the view layer's direction part (joint p + h NJH2)
         wvo[lane] = wv0;
         wvo[64 + lane] = wv1;
     }
@@ -320,16 +320,16 @@ __device__ __forceinline__ void u_part(f32x16 (&acc)[RB], const ModelDev& M, con
             }
             if (g == 0) {  // joint 2pp+2 from its prefetched row; then prefetch joint 2pp+4
                 float wv;
-                u_joint<true>(M, ra, j0 + 2 * pp + 2 < nj, px, py, pz, fn[0], fn[1], fn[2], ln0, wv);
+                u_joint<WV>(M, ra, j0 + 2 * pp + 2 < nj, px, py, pz, fn[0], fn[1], fn[2], ln0, wv);
                 pin(fn[0]), pin(fn[1]), pin(fn[2]), pin(ln0);
-                if (wvo && 2 * pp + 2 < njh2) wvo[(2 * pp + 2) * 64 + lane] = wv;
+                if constexpr (WV) wvo[min(2 * pp + 2, njh2) * 64 + lane] = wv;  // (row njh2: discard)
                 ra = load_row(sk, cut, j0 + 2 * pp + 4, nj);
             }
             if (g == 1) {
                 float wv;
-                u_joint<true>(M, rb2, j0 + 2 * pp + 3 < nj, px, py, pz, fn[3], fn[4], fn[5], ln1, wv);
+                u_joint<WV>(M, rb2, j0 + 2 * pp + 3 < nj, px, py, pz, fn[3], fn[4], fn[5], ln1, wv);
                 pin(fn[3]), pin(fn[4]), pin(fn[5]), pin(ln1);
-                if (wvo && 2 * pp + 3 < njh2) wvo[(2 * pp + 3) * 64 + lane] = wv;
+                if constexpr (WV) wvo[min(2 * pp + 3, njh2) * 64 + lane] = wv;
                 rb2 = load_row(sk, cut, j0 + 2 * pp + 5, nj);
             }
             interleave_mfma_valu<2 * RB, 8>();
@@ -508,7 +508,7 @@ __device__ __forceinline__ void view_dir_part(f32x16 (&acc)[RBV], const ModelDev
 // Encoder + density trunk of one 32-sample block: L0 (u and v parts), the hidden layers with the
 // skip; acc ends as the pre-activation of the last hidden layer.  `after_last` is the weight stream
 // that follows (the feature layer, or nothing for density-only queries).
-template <int W, int MR>
+template <int W, int MR, bool WV>
 __device__ __forceinline__ void mlp_trunk(const ModelDev& M, const NetDev& net, const float* __restrict__ sk,
                                           const float* __restrict__ cut, float px, float py, float pz, int lane,
                                           const float* __restrict__ bias, float* __restrict__ uf,
@@ -522,7 +522,7 @@ __device__ __forceinline__ void mlp_trunk(const ModelDev& M, const NetDev& net, 
     ring_preload<2 * RB>(ring, net.wl[0], lane);  // the u part's first groups, early
     load_bias<RB>(acc, bias, hh);
     STAMP(st, 10);
-    u_part<RB>(acc, M, net.wl[0], sk, cut, px, py, pz, lane, &mask, uf, wvo, ring, M.D > 1 ? net.wl[1] : after_last,
+    u_part<RB, WV>(acc, M, net.wl[0], sk, cut, px, py, pz, lane, &mask, uf, wvo, ring, M.D > 1 ? net.wl[1] : after_last,
                st);
     STAMP(st, 8);
     v_part<RB, MR>(acc, M, net.wl0v, sk, cut, px, py, pz, lane, mask, st);
@@ -538,7 +538,8 @@ __device__ __forceinline__ void mlp_trunk(const ModelDev& M, const NetDev& net, 
             if (uf)
                 u_part_lds<RB>(acc, M, net.wskipu, uf, lane, ring, after);
             else
-                u_part<RB>(acc, M, net.wskipu, sk, cut, px, py, pz, lane, nullptr, nullptr, nullptr, ring, after, st);
+                u_part<RB, false>(acc, M, net.wskipu, sk, cut, px, py, pz, lane, nullptr, nullptr, nullptr, ring, after,
+                                  st);
             v_part<RB, MR>(acc, M, net.wskipv, sk, cut, px, py, pz, lane, mask, st);
             STAMP(st, 12);
         }
@@ -567,7 +568,7 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
     f32x16 acc[RB], h[RB];
     JointMask mask;
     Ring ring;
-    mlp_trunk<W, MR>(M, net, sk, cut, px, py, pz, lane, bias, uf, wvp, acc, h, ring, mask, net.wview, st);
+    mlp_trunk<W, MR, true>(M, net, sk, cut, px, py, pz, lane, bias, uf, wvp, acc, h, ring, mask, net.wview, st);
     // views_linears.0 with feature_linear fused in (W' = Wv_f Wf, see pack_net) on relu(h_last),
     // alpha_linear folded into its groups (same relu'd B operands), + the factorised
     // direction / code / bias part from G, then relu

@@ -117,7 +117,7 @@ __host__ __device__ inline LdsPlan make_plan(int R, int nj, int W, int S, int T,
     p.uf_stride = 64 * 3 * njh2;   // per wave: the L0 bone directions, re-read by the skip layer
     p.uf = with_uf ? o : -1;
     if (with_uf) o += 4 * p.uf_stride;
-    p.wv_stride = 64 * njh2;       // per wave: view-direction window weights w'_j of the current block
+    p.wv_stride = 64 * (njh2 + 1);  // per wave: view-direction windows w'_j of the block (+ a discard row)
     p.wv = o; o += 4 * p.wv_stride;
     p.total = (o + 3) & ~3;
     return p;
