@@ -65,6 +65,10 @@ __device__ __forceinline__ float relu(float x) { return x < 0.0f ? 0.0f : x; }
 // MLP activation relu in one VALU op: signed-integer max of the bit pattern maps every float with
 // the sign bit set to +0 and keeps the rest (incl. +NaN, which is what the GPU generates and what
 // the host NaN fill produces).  Differs from relu only in -0 -> +0 and -NaN -> 0.
+// x if m else +0.0, as an integer AND (never turned into a branch; free beside f32 MFMAs)
+__device__ __forceinline__ float mask_f(float x, bool m) {
+    return __builtin_bit_cast(float, __builtin_bit_cast(int, x) & -(int)m);
+}
 __device__ __forceinline__ float relu_act(float x) {
     return __builtin_bit_cast(float, max(__builtin_bit_cast(int, x), 0));
 }

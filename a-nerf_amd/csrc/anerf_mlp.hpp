@@ -238,9 +238,9 @@ __device__ __forceinline__ void u_joint(const ModelDev& M, const JRow& r, bool v
     float qx = fmaf(r.a[3], 1.0f, fmaf(r.a[2], pz, fmaf(r.a[1], py, r.a[0] * px)));
     float qy = fmaf(r.b[3], 1.0f, fmaf(r.b[2], pz, fmaf(r.b[1], py, r.b[0] * px)));
     float qz = fmaf(r.c[3], 1.0f, fmaf(r.c[2], pz, fmaf(r.c[1], py, r.c[0] * px)));
-    qx = valid ? qx : 0.0f;
-    qy = valid ? qy : 0.0f;
-    qz = valid ? qz : 0.0f;
+    qx = mask_f(qx, valid);
+    qy = mask_f(qy, valid);
+    qz = mask_f(qz, valid);
     const float d2 = fmaf(qz, qz, fmaf(qy, qy, qx * qx));
     const float inv = __builtin_amdgcn_rsqf(fmaxf(d2, 1e-24f));
     u0 = qx * inv;
@@ -251,7 +251,9 @@ __device__ __forceinline__ void u_joint(const ModelDev& M, const JRow& r, bool v
         const float d = __builtin_amdgcn_sqrtf(d2);
         const float e = __builtin_amdgcn_exp2f(-(M.tau_v * (d - r.cv)) * 1.44269504f);
         const float w = 1.0f - __builtin_amdgcn_rcpf(1.0f + e);
-        wv = (valid && M.cutoff_viewdir) ? w : 0.0f;
+        // select by an integer mask: a ?: on an expensive operand becomes an exec-masked branch,
+        // which splits the MFMA region this math is interleaved into
+        wv = mask_f(w, valid & (M.cutoff_viewdir != 0));
     }
 }
 
@@ -389,7 +391,7 @@ __device__ __forceinline__ void v_geom(const ModelDev& M, const float* __restric
     joint_local(sk + 12 * j, px, py, pz, qx, qy, qz);
     dist = norm3(qx, qy, qz);
     const float wc = cutoff_w(M.tau, dist, cut[j]);
-    w = M.use_cutoff ? wc : 1.0f;
+    w = M.use_cutoff ? wc : 1.0f;  // (uniform)
 }
 
 template <int RB, int MR>
