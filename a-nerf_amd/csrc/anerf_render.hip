@@ -17,6 +17,7 @@
 //   anerf_mlp.hpp      MFMA building blocks: weight ring, dense layer, encoder streams, trunk
 //   anerf_stages.hpp   per-ray stages: view factor G, compositing, importance sampling
 //   anerf_kernels.hpp  __global__ kernels (render, density, near/far, rays, compose, encode)
+//   anerf_pose.hpp     pose -> skeleton transforms (kinematic chain, inverse)
 //   anerf_pack.hpp     host weight packing / model binding
 //   this file          the C ABI (include/anerf.h)
 //
@@ -42,6 +43,7 @@ using namespace anerf;
 #include "anerf_mlp.hpp"
 #include "anerf_stages.hpp"
 #include "anerf_kernels.hpp"
+#include "anerf_pose.hpp"
 #include "anerf_pack.hpp"
 
 #ifdef ANERF_STAMPS
@@ -419,6 +421,51 @@ int anerf_density_grid(const anerf_model* m, const float* axis, int32_t res1, co
     a.net = net;
     a.out = raw_out;
     return launch_density(m, a, stream);
+}
+
+int anerf_pose_kinematics(const float* bones, int32_t rot_dim, const float* rest, const int32_t* rest_idx,
+                          int64_t n_rest, const float* pelvis, float scale, const int32_t* parents, int32_t n_joints,
+                          int32_t root_id, int64_t n_frames, float* kps, float* skts, float* l2ws, float* rots,
+                          void* stream) {
+    if (n_frames < 0 || n_joints < 1 || n_joints > KIN_MAX_JOINTS || root_id < 0 || root_id >= n_joints || !parents)
+        return fail(ANERF_EINVAL, "anerf_pose_kinematics: bad skeleton arguments");
+    if (rot_dim != 3 && rot_dim != 6 && rot_dim != 9)
+        return fail(ANERF_EINVAL, "anerf_pose_kinematics: rot_dim must be 3 (axis-angle), 6 (6-D) or 9 (matrix)");
+    KinArgs a{};
+    // depth of every joint; parents must form a tree rooted at root_id
+    int depth[KIN_MAX_JOINTS];
+    for (int j = 0; j < n_joints; ++j) {
+        if (j != root_id && (parents[j] < 0 || parents[j] >= n_joints || parents[j] == j))
+            return fail(ANERF_EINVAL, "anerf_pose_kinematics: parent index out of range");
+        depth[j] = -1;
+    }
+    depth[root_id] = 0;
+    int max_depth = 0;
+    for (int j = 0; j < n_joints; ++j) {
+        int k = j, steps = 0;
+        while (depth[k] < 0 && steps <= n_joints) { k = parents[k]; ++steps; }
+        if (depth[k] < 0) return fail(ANERF_EINVAL, "anerf_pose_kinematics: parents contain a cycle");
+        int d = depth[k] + steps;  // assign depths along the path j -> k
+        for (int u = j; depth[u] < 0; u = parents[u]) depth[u] = d--;
+    }
+    for (int j = 0; j < n_joints; ++j) {
+        a.parent[j] = (int8_t)(j == root_id ? 0 : parents[j]);
+        a.depth[j] = (uint8_t)depth[j];
+        max_depth = std::max(max_depth, depth[j]);
+    }
+    if (n_frames == 0) return ANERF_OK;
+    if (!bones || !rest || n_rest < 1 || (!kps && !skts && !l2ws && !rots))
+        return fail(ANERF_EINVAL, "anerf_pose_kinematics: bad buffers");
+    a.bones = bones; a.rest = rest; a.rest_idx = rest_idx; a.pelvis = pelvis;
+    a.kps = kps; a.skts = skts; a.l2ws = l2ws; a.rots = rots;
+    a.n_frames = n_frames; a.n_rest = n_rest; a.scale = scale; a.rot_dim = rot_dim;
+    a.nj = n_joints; a.root = root_id; a.max_depth = max_depth;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const size_t lds = sizeof(double) * 12 * n_joints * KIN_WAVES;
+    hipLaunchKernelGGL(pose_kinematics_kernel, dim3((unsigned)((n_frames + KIN_WAVES - 1) / KIN_WAVES)),
+                       dim3(64 * KIN_WAVES), lds, st, a);
+    HIP_TRY(hipGetLastError());
+    return ANERF_OK;
 }
 
 }  // extern "C"

@@ -1,0 +1,196 @@
+"""Pose -> skeleton transforms on the GPU, mirroring the reference's
+`PoseOptLayer` forward path (core/pose_opt.py:240-445), `get_kinematic_chain_T`
+(core/pose_opt.py:448-479) and `get_smpl_l2ws` (core/utils/skeleton_utils.py:334-376).
+
+All of them reduce to one C-ABI call, `anerf_pose_kinematics` (include/anerf.h): a batched
+kinematic chain + inverse that produces the `skts` / `kps` the render path consumes, on the
+device, for any number of frames.  Forward only (the reference's pose optimisation needs the
+backward pass, a §8(f) row-2 item): tensors here carry no autograd graph.
+
+Differences from the reference, by design:
+* any tree skeleton up to 128 joints with any root (the reference's PoseOptLayer accepts only
+  SMPLSkeleton and `get_smpl_l2ws` assumes root 0 and parents < child);
+* float64 arithmetic inside the kernel, float32 outputs (the reference's PoseOptLayer runs in
+  float32 torch, get_smpl_l2ws in float64 numpy; both agree with this to float32 rounding);
+* `get_smpl_l2ws` needs an explicit rest pose (the SMPL template is not shipped here).
+"""
+from collections import namedtuple
+
+import numpy as np
+import torch
+
+from . import _lib
+from .synthetic import SMPL_PARENTS
+
+Skeleton = namedtuple("Skeleton", ["joint_names", "joint_trees", "root_id", "nonroot_id", "cutoffs",
+                                   "end_effectors"])
+
+# skeleton_utils.py:83-105 (topology only)
+SMPLSkeleton = Skeleton(
+    joint_names=["pelvis", "left_hip", "right_hip", "spine1", "left_knee", "right_knee", "spine2", "left_ankle",
+                 "right_ankle", "spine3", "left_foot", "right_foot", "neck", "left_collar", "right_collar",
+                 "head", "left_shoulder", "right_shoulder", "left_elbow", "right_elbow", "left_wrist",
+                 "right_wrist", "left_hand", "right_hand"],
+    joint_trees=SMPL_PARENTS.copy(), root_id=0, nonroot_id=list(range(1, 24)), cutoffs={},
+    end_effectors=[10, 11, 15, 22, 23])
+
+# skeleton_utils.py:61-81: root 14, parents not ordered by index
+CanonicalSkeleton = Skeleton(
+    joint_names=["head_top", "neck", "right_shoulder", "right_elbow", "right_wrist", "left_shoulder",
+                 "left_elbow", "left_wrist", "right_hip", "right_knee", "right_ankle", "left_hip", "left_knee",
+                 "left_ankle", "pelvis", "spine", "head"],
+    joint_trees=np.array([1, 15, 1, 2, 3, 1, 5, 6, 14, 8, 9, 14, 11, 12, 14, 14, 1]), root_id=14,
+    nonroot_id=[i for i in range(17) if i != 14], cutoffs={}, end_effectors=None)
+
+
+def _dev_f32(x, device):
+    if isinstance(x, torch.Tensor):
+        return x.detach().to(device=device, dtype=torch.float32).contiguous()
+    return torch.as_tensor(np.ascontiguousarray(x, dtype=np.float32), device=device)
+
+
+def pose_kinematics(bones, rest_pose, skel_type=SMPLSkeleton, pelvis=None, scale=1.0, rest_idx=None,
+                    device=None, outputs=("kps", "skts", "l2ws", "rots")):
+    """Batched kinematic chain: bones (F, NJ, 3|6|9) -> dict of float32 device tensors
+    kps (F, NJ, 3), skts (F, NJ, 4, 4), l2ws (F, NJ, 4, 4), rots (F, NJ, 3, 3).
+
+    rest_pose (NJ, 3) or (R, NJ, 3) with rest_idx (F,) selecting one per frame; pelvis (F, 3)
+    is added to every joint's translation; rest offsets are scaled by `scale`."""
+    if device is None:
+        device = bones.device if isinstance(bones, torch.Tensor) and bones.is_cuda else torch.device("cuda", 0)
+    lib = _lib.load()
+    b = _dev_f32(bones, device)
+    if b.dim() != 3 or b.shape[-1] not in (3, 6, 9):
+        raise ValueError("bones must be (F, NJ, 3 | 6 | 9)")
+    F, nj = int(b.shape[0]), int(b.shape[1])
+    rest = _dev_f32(rest_pose, device).reshape(-1, nj, 3)
+    ridx = None
+    if rest_idx is not None:
+        ridx = torch.as_tensor(np.asarray(rest_idx), dtype=torch.int32).to(device).contiguous()
+        if ridx.numel() != F:
+            raise ValueError("rest_idx must have one entry per frame")
+    elif rest.shape[0] != 1:
+        if rest.shape[0] != F:
+            raise ValueError("rest_pose (R, NJ, 3) needs rest_idx unless R == F")
+        ridx = torch.arange(F, dtype=torch.int32, device=device)
+    pel = None if pelvis is None else _dev_f32(pelvis, device).reshape(F, 3)
+    parents = np.ascontiguousarray(np.asarray(skel_type.joint_trees), dtype=np.int32)
+    if parents.shape[0] != nj:
+        raise ValueError(f"skeleton has {parents.shape[0]} joints, bones have {nj}")
+    out = {}
+    shapes = {"kps": (F, nj, 3), "skts": (F, nj, 4, 4), "l2ws": (F, nj, 4, 4), "rots": (F, nj, 3, 3)}
+    for k in outputs:
+        out[k] = torch.empty(shapes[k], dtype=torch.float32, device=device)
+    with torch.cuda.device(device):
+        rc = lib.anerf_pose_kinematics(_lib.ptr(b), b.shape[-1], _lib.ptr(rest), _lib.ptr(ridx), rest.shape[0],
+                                       _lib.ptr(pel), float(scale),
+                                       parents.ctypes.data_as(_lib.c_i32p), nj, int(skel_type.root_id), F,
+                                       _lib.ptr(out.get("kps")), _lib.ptr(out.get("skts")),
+                                       _lib.ptr(out.get("l2ws")), _lib.ptr(out.get("rots")),
+                                       _lib.stream_handle(device))
+    _lib.check(rc, "anerf_pose_kinematics")
+    return out
+
+
+def get_kinematic_chain_T(rest_pose, bones, skel_type=SMPLSkeleton):
+    """pose_opt.py:448-479 -> (kps, bones, skts, l2ws, rots)."""
+    o = pose_kinematics(bones, rest_pose, skel_type)
+    return o["kps"], bones, o["skts"], o["l2ws"], o["rots"]
+
+
+def get_smpl_l2ws(pose, rest_pose=None, scale=1.0, skel_type=SMPLSkeleton):
+    """skeleton_utils.py:334-376 for one pose (NJ, 3) or a batch (F, NJ, 3): local-to-world 4x4s
+    (float32 device tensor, float64 arithmetic)."""
+    if rest_pose is None:
+        raise ValueError("get_smpl_l2ws: pass rest_pose explicitly (the SMPL template is not shipped)")
+    p = pose if isinstance(pose, torch.Tensor) else torch.as_tensor(np.asarray(pose, dtype=np.float32))
+    single = p.dim() == 2
+    o = pose_kinematics(p[None] if single else p, rest_pose, skel_type, scale=scale, outputs=("l2ws",))
+    return o["l2ws"][0] if single else o["l2ws"]
+
+
+class PoseOptLayer:
+    """Forward path of the reference's PoseOptLayer (core/pose_opt.py:240-445) on the device.
+
+    kps (N, NJ, 3), bones (N, NJ, 3) axis-angle, rest_pose (1 | R, NJ, 3).  With kp_map /
+    kp_uidxs (multi-view), root bones are per index and the other bones are shared through
+    kp_map (pose_opt.py:318-332).  use_rot6d stores the 6-D parameters (pose_opt.py:284-289)."""
+
+    def __init__(self, kps, bones, rest_pose, skel_type=SMPLSkeleton, kp_map=None, kp_uidxs=None, use_cache=False,
+                 use_rot6d=False, beta=None, rest_pose_idxs=None, device=None):
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.skel_type = skel_type
+        self.root_id = skel_type.root_id
+        self.use_cache = use_cache
+        self.use_rot6d = use_rot6d
+        self.rest_pose_idxs = None if rest_pose_idxs is None else np.asarray(rest_pose_idxs)
+        self.beta = beta
+        self.rest_pose = _dev_f32(rest_pose, self.device).reshape(-1, len(skel_type.joint_trees), 3)
+        kps = _dev_f32(kps, self.device)
+        bones = _dev_f32(bones, self.device)
+        self.pelvis = kps[:, self.root_id].contiguous()
+        if use_rot6d:
+            nj = bones.shape[1]
+            rots = pose_kinematics(bones, self.rest_pose[:1], skel_type, outputs=("rots",))["rots"]
+            bones = rots[..., :3, :2].reshape(-1, nj, 6).contiguous()
+        if kp_map is None:
+            self.kp_map = self.kp_uidxs = None
+            self.bones = bones
+        else:
+            self.kp_map = torch.as_tensor(np.asarray(kp_map), dtype=torch.long, device=self.device)
+            self.kp_uidxs = torch.as_tensor(np.asarray(kp_uidxs), dtype=torch.long, device=self.device)
+            self.root_bones = bones[:, self.root_id].contiguous()
+            self.bones = bones[self.kp_uidxs, self.root_id + 1:].contiguous()
+        self.N_kps = self.pelvis.shape[0]
+        if use_cache:
+            self.update_cache()
+
+    def idx_to_params(self, idx):
+        idx = torch.as_tensor(np.asarray(idx), dtype=torch.long, device=self.device).view(-1)
+        pelvis = self.pelvis[idx]
+        if self.kp_map is None:
+            return pelvis, self.bones[idx]
+        root = self.root_bones[idx, None, :]
+        return pelvis, torch.cat([root, self.bones[self.kp_map[idx]]], dim=1)
+
+    def get_pelvis(self, idx=None):
+        return self.idx_to_params(np.arange(self.N_kps) if idx is None else idx)[0]
+
+    def get_rest_pose(self, kp_idxs=None, rest_pose_idxs=None):
+        if len(self.rest_pose) == 1:
+            return self.rest_pose
+        if rest_pose_idxs is not None:
+            return self.rest_pose[torch.as_tensor(np.asarray(rest_pose_idxs), device=self.device)]
+        return self.rest_pose[torch.as_tensor(self.rest_pose_idxs[np.asarray(kp_idxs)], device=self.device)]
+
+    def calculate_kinematic(self, idxs, rest_pose_idxs=None):
+        """-> kp (N, NJ, 3), bone (N, NJ, 3|6), skts (N, NJ, 4, 4), l2ws (N, NJ, 4, 4), rots (N, NJ, 3, 3)."""
+        if idxs is None:
+            idxs = np.arange(self.N_kps)
+        idxs = np.atleast_1d(np.asarray(idxs))
+        pelvis, bone = self.idx_to_params(idxs)
+        if len(self.rest_pose) == 1:
+            rest, ridx = self.rest_pose, None
+        elif rest_pose_idxs is not None:
+            rest, ridx = self.rest_pose, np.asarray(rest_pose_idxs)
+        else:
+            rest, ridx = self.rest_pose, self.rest_pose_idxs[idxs]
+        o = pose_kinematics(bone, rest, self.skel_type, pelvis=pelvis, rest_idx=ridx, device=self.device)
+        return o["kps"], bone, o["skts"], o["l2ws"], o["rots"]
+
+    def update_cache(self):
+        self.cache_kps, self.cache_bones, self.cache_skts, self.cache_l2ws, self.cache_rots = \
+            self.calculate_kinematic(np.arange(self.N_kps))
+
+    def forward(self, idxs, rest_pose_idxs=None):
+        if not self.use_cache:
+            return self.calculate_kinematic(idxs, rest_pose_idxs)
+        i = torch.as_tensor(np.asarray(idxs), dtype=torch.long, device=self.device)
+        return self.cache_kps[i], self.cache_bones[i], self.cache_skts[i], self.cache_l2ws[i], self.cache_rots[i]
+
+    __call__ = forward
+
+    def get_bones(self, idx=None):
+        if self.use_rot6d:
+            raise NotImplementedError("get_bones with use_rot6d needs matrix_to_axis_angle (not on this path)")
+        return self.idx_to_params(np.arange(self.N_kps) if idx is None else idx)[1]

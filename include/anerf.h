@@ -181,6 +181,22 @@ int anerf_density_points(const anerf_model* m, const float* pts, int64_t n_point
 int anerf_density_grid(const anerf_model* m, const float* axis, int32_t res1, const float* kp0, const float* skts,
                        int32_t net, float* raw_out, void* stream);
 
+/* Pose -> skeleton transforms for n_frames frames, replacing
+ *   PoseOptLayer.calculate_kinematic  core/pose_opt.py:372-445 (+ unrolled_kinematic_chain :482-521),
+ *   get_kinematic_chain_T              core/pose_opt.py:448-479,
+ *   get_smpl_l2ws + inv                core/utils/skeleton_utils.py:296-376.
+ * bones [F][NJ][rot_dim]: rot_dim 3 axis-angle (pytorch3d axis_angle_to_matrix, skeleton_utils.py:411),
+ * 6 the 6-D parameters (rot6d_to_rotmat, :420), 9 row-major 3x3 matrices; rest [n_rest][NJ][3],
+ * rest_idx [F] (NULL: rest 0; out-of-range index -> NaN outputs for that frame); pelvis [F][3] or NULL,
+ * added to every joint's translation; rest offsets are multiplied by scale.  parents [NJ] (HOST
+ * memory, the skeleton's joint_trees; the root's entry is ignored) must form a tree rooted at root_id,
+ * in any index order; NJ <= 128.  Outputs (any may be NULL): kps [F][NJ][3], skts = inverse(l2ws)
+ * [F][NJ][4][4], l2ws [F][NJ][4][4], rots [F][NJ][3][3].  Computed in float64, stored as float32. */
+int anerf_pose_kinematics(const float* bones, int32_t rot_dim, const float* rest, const int32_t* rest_idx,
+                          int64_t n_rest, const float* pelvis, float scale, const int32_t* parents, int32_t n_joints,
+                          int32_t root_id, int64_t n_frames, float* kps, float* skts, float* l2ws, float* rots,
+                          void* stream);
+
 #ifdef __cplusplus
 }
 #endif

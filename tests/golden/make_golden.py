@@ -315,6 +315,64 @@ def bbox_table(mods):
     print(f"wrote {path}")
 
 
+def kinematics_table(mods):
+    """Pose -> skeleton transforms from the reference's own functions:
+    * PoseOptLayer.calculate_kinematic (core/pose_opt.py:372-445, unrolled chain :482-521) with the
+      6-D rotation parameters (rot6d_to_rotmat, skeleton_utils.py:420-436, is plain torch; the
+      axis-angle branch needs pytorch3d, which is absent here, so it is not run);
+    * get_kinematic_chain_T (pose_opt.py:448-479) on 6-D rotations;
+    * get_smpl_l2ws (skeleton_utils.py:334-376, numpy float64 + scipy Rotation) on axis-angle bones
+      for SMPL-24 and the 65-joint stress skeleton, incl. zero and tiny rotation vectors."""
+    import torch
+    po = importlib.import_module("core.pose_opt")
+    sk = mods[4]
+    rs = np.random.RandomState(1234)
+    rows = {}
+    F = 6
+    parents, rest24 = anerf_syn.skeleton(24)
+    rest = (rest24 * 0.7).astype(np.float32)[None]
+    bones6 = rs.normal(size=(F, 24, 6)).astype(np.float32)
+    pelvis = rs.normal(scale=0.5, size=(F, 3)).astype(np.float32)
+    L = po.PoseOptLayer.__new__(po.PoseOptLayer)   # __init__ would call pytorch3d's axis_angle_to_matrix
+    torch.nn.Module.__init__(L)
+    L.skel_type, L.use_cache, L.unroll_kinematic_chain, L.use_rot6d = sk.SMPLSkeleton, False, True, True
+    L.rest_pose_idxs, L.kp_map, L.kp_uidxs, L.root_id, L.N_kps = None, None, None, 0, F
+    L.register_buffer("rest_pose", torch.tensor(rest))
+    L.register_parameter("pelvis", torch.nn.Parameter(torch.tensor(pelvis)))
+    L.register_parameter("bones", torch.nn.Parameter(torch.tensor(bones6)))
+    idxs = np.array([3, 0, 5, 3, 1], dtype=np.int64)
+    with torch.no_grad():
+        kp, bone, skts, l2ws, rots = L.calculate_kinematic(idxs)
+    rows.update(ck_bones6=bones6, ck_pelvis=pelvis, ck_rest=rest, ck_idxs=idxs, ck_kp=kp.numpy(),
+                ck_bone=bone.numpy(), ck_skts=skts.numpy(), ck_l2ws=l2ws.numpy(), ck_rots=rots.numpy())
+    with torch.no_grad():
+        kpsT, _, sktsT, l2wsT, rotsT = po.get_kinematic_chain_T(torch.tensor(rest), torch.tensor(bones6[:4]))
+    rows.update(ct_kps=kpsT.numpy(), ct_skts=sktsT.numpy(), ct_l2ws=l2wsT.numpy(), ct_rots=rotsT.numpy())
+    # get_smpl_l2ws: float64 numpy/scipy, SMPL-24 and 65 joints
+    for tag, nj in (("s24", 24), ("s65", 65)):
+        par, rst = anerf_syn.skeleton(nj)
+        skel = sk.SMPLSkeleton if nj == 24 else sk.Skeleton(
+            joint_names=[f"j{i}" for i in range(nj)], joint_trees=par, root_id=0,
+            nonroot_id=list(range(1, nj)), cutoffs={}, end_effectors=[])
+        bones = rs.normal(scale=0.4, size=(4, nj, 3)).astype(np.float32)
+        bones[0, 1] = 0.0
+        bones[0, 2] = [1e-5, -2e-5, 0.5e-5]
+        bones[1, 3] = [2e-4, 0.0, 0.0]
+        bones[2, 0] = [np.pi, 0.0, 0.0]
+        scale = 0.8
+        l2 = np.stack([sk.get_smpl_l2ws(b.astype(np.float64), rst.astype(np.float64), scale, skel_type=skel)
+                       for b in bones])
+        rows[f"gl_{tag}_bones"] = bones
+        rows[f"gl_{tag}_rest"] = rst
+        rows[f"gl_{tag}_parents"] = par.astype(np.int32)
+        rows[f"gl_{tag}_scale"] = np.array(scale)
+        rows[f"gl_{tag}_l2ws"] = l2
+        rows[f"gl_{tag}_skts"] = np.linalg.inv(l2)
+    path = os.path.join(HERE, "kinematics.npz")
+    np.savez_compressed(path, **rows)
+    print(f"wrote {path}")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default=None)
@@ -329,6 +387,8 @@ def main():
             make(name, cfg, mods, tmp)
     if not a.only or a.only == "bboxes":
         bbox_table(mods)
+    if not a.only or a.only == "kinematics":
+        kinematics_table(mods)
 
 
 if __name__ == "__main__":

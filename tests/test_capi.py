@@ -23,7 +23,8 @@ def test_header_declares_expected_entry_points():
     fns = header_functions()
     for f in ("anerf_model_create", "anerf_render_rays", "anerf_gen_rays", "anerf_near_far", "anerf_compose",
               "anerf_encode_points", "anerf_workspace_size", "anerf_last_error", "anerf_abi_version",
-              "anerf_density_points", "anerf_density_grid", "anerf_gen_rays_box", "anerf_compose_box"):
+              "anerf_density_points", "anerf_density_grid", "anerf_gen_rays_box", "anerf_compose_box",
+              "anerf_pose_kinematics"):
         assert f in fns
 
 

@@ -1,0 +1,224 @@
+"""Pose -> skeleton transforms.
+
+CPU: the restatement (oracle/kinematics.py) against tests/golden/kinematics.npz, which holds the
+reference's own outputs (make_golden.py:kinematics_table):
+  * PoseOptLayer.calculate_kinematic on 6-D rotations (float32 torch)   -> 2e-6 absolute
+  * get_kinematic_chain_T on 6-D rotations (float32 torch)              -> 2e-6 absolute
+  * get_smpl_l2ws (+ inv) on axis-angle, SMPL-24 and 65 joints (float64) -> 1e-12 absolute
+The axis-angle branch of calculate_kinematic needs pytorch3d, which is absent here: it is pinned
+through get_smpl_l2ws (scipy's from_rotvec is the same rotation).
+GPU (anerf_pose_kinematics through the C ABI; float64 inside, float32 out) against the goldens and
+the restatement: 4e-6 absolute on transforms (values <= 2), i.e. float32 rounding of the chain.
+"""
+import importlib
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "oracle"))
+
+import kinematics as okin  # noqa: E402
+
+syn = importlib.import_module("a-nerf_amd.synthetic")
+
+Z = np.load(os.path.join(HERE, "golden", "kinematics.npz"), allow_pickle=False)
+SMPL = syn.SMPL_PARENTS
+CANON_PARENTS = np.array([1, 15, 1, 2, 3, 1, 5, 6, 14, 8, 9, 14, 11, 12, 14, 14, 1])
+TOL_REF32 = 2e-6
+TOL_GPU = 4e-6
+
+
+# ---------------------------------------------------------------- CPU: restatement vs reference
+def test_oracle_calculate_kinematic_rot6d():
+    idx = Z["ck_idxs"]
+    kp, skts, l2ws, rots = okin.kinematic_chain(Z["ck_bones6"][idx], Z["ck_rest"][0], SMPL, 0, Z["ck_pelvis"][idx])
+    np.testing.assert_allclose(kp, Z["ck_kp"], atol=TOL_REF32, rtol=0)
+    np.testing.assert_allclose(l2ws, Z["ck_l2ws"], atol=TOL_REF32, rtol=0)
+    np.testing.assert_allclose(skts, Z["ck_skts"], atol=TOL_REF32, rtol=0)
+    np.testing.assert_allclose(rots, Z["ck_rots"], atol=TOL_REF32, rtol=0)
+
+
+def test_oracle_kinematic_chain_T():
+    kp, skts, l2ws, rots = okin.kinematic_chain(Z["ck_bones6"][:4], Z["ck_rest"][0], SMPL, 0)
+    np.testing.assert_allclose(kp, Z["ct_kps"], atol=TOL_REF32, rtol=0)
+    np.testing.assert_allclose(skts, Z["ct_skts"], atol=TOL_REF32, rtol=0)
+    np.testing.assert_allclose(rots, Z["ct_rots"], atol=TOL_REF32, rtol=0)
+
+
+@pytest.mark.parametrize("tag", ["s24", "s65"])
+def test_oracle_get_smpl_l2ws(tag):
+    _, skts, l2ws, _ = okin.kinematic_chain(Z[f"gl_{tag}_bones"], Z[f"gl_{tag}_rest"], Z[f"gl_{tag}_parents"], 0,
+                                            None, float(Z[f"gl_{tag}_scale"]))
+    np.testing.assert_allclose(l2ws, Z[f"gl_{tag}_l2ws"], atol=1e-12, rtol=0)
+    np.testing.assert_allclose(skts, Z[f"gl_{tag}_skts"], atol=1e-12, rtol=0)
+
+
+def test_oracle_topo_order_any_root():
+    order = okin.topo_order(CANON_PARENTS, 14)
+    assert order[0] == 14 and sorted(order) == list(range(17))
+    pos = {j: i for i, j in enumerate(order)}
+    assert all(pos[int(CANON_PARENTS[j])] < pos[j] for j in range(17) if j != 14)
+    with pytest.raises(ValueError):
+        okin.topo_order(np.array([0, 2, 1]), 0)
+
+
+# ---------------------------------------------------------------- GPU: anerf_pose_kinematics
+def _kin():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return importlib.import_module("a-nerf_amd.kinematics")
+
+
+def _np(t):
+    return t.detach().cpu().numpy().astype(np.float64)
+
+
+@pytest.mark.gpu
+def test_gpu_calculate_kinematic_rot6d_vs_reference():
+    kin = _kin()
+    idx = Z["ck_idxs"]
+    o = kin.pose_kinematics(Z["ck_bones6"][idx], Z["ck_rest"], kin.SMPLSkeleton, pelvis=Z["ck_pelvis"][idx])
+    for k, g in (("kps", "ck_kp"), ("l2ws", "ck_l2ws"), ("skts", "ck_skts"), ("rots", "ck_rots")):
+        np.testing.assert_allclose(_np(o[k]), Z[g], atol=TOL_GPU, rtol=0, err_msg=k)
+
+
+@pytest.mark.gpu
+def test_gpu_kinematic_chain_T_vs_reference():
+    kin = _kin()
+    kps, _, skts, l2ws, rots = kin.get_kinematic_chain_T(Z["ck_rest"], torch.tensor(Z["ck_bones6"][:4]).cuda())
+    np.testing.assert_allclose(_np(kps), Z["ct_kps"], atol=TOL_GPU, rtol=0)
+    np.testing.assert_allclose(_np(skts), Z["ct_skts"], atol=TOL_GPU, rtol=0)
+    np.testing.assert_allclose(_np(l2ws), Z["ct_l2ws"], atol=TOL_GPU, rtol=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tag", ["s24", "s65"])
+def test_gpu_get_smpl_l2ws_vs_reference(tag):
+    kin = _kin()
+    par = Z[f"gl_{tag}_parents"]
+    skel = kin.SMPLSkeleton if len(par) == 24 else kin.Skeleton([f"j{i}" for i in range(len(par))], par, 0,
+                                                                  list(range(1, len(par))), {}, [])
+    o = kin.pose_kinematics(Z[f"gl_{tag}_bones"], Z[f"gl_{tag}_rest"], skel, scale=float(Z[f"gl_{tag}_scale"]))
+    ref_l2ws = Z[f"gl_{tag}_l2ws"]
+    # float32 rounding of float64 results: within 1 ulp of the reference
+    np.testing.assert_allclose(_np(o["l2ws"]), ref_l2ws, atol=2.5e-7, rtol=1.2e-7)
+    np.testing.assert_allclose(_np(o["skts"]), Z[f"gl_{tag}_skts"], atol=5e-7, rtol=2.4e-7)
+    np.testing.assert_allclose(_np(o["kps"]), ref_l2ws[..., :3, 3], atol=2.5e-7, rtol=1.2e-7)
+    one = kin.get_smpl_l2ws(Z[f"gl_{tag}_bones"][0], Z[f"gl_{tag}_rest"], float(Z[f"gl_{tag}_scale"]), skel)
+    np.testing.assert_array_equal(_np(one), _np(o["l2ws"][0]))
+
+
+@pytest.mark.gpu
+def test_gpu_canonical_skeleton_root14_matches_restatement():
+    kin = _kin()
+    rs = np.random.RandomState(5)
+    F = 37
+    bones = rs.normal(scale=0.5, size=(F, 17, 3)).astype(np.float32)
+    rest = rs.normal(scale=0.3, size=(17, 3)).astype(np.float32)
+    pelvis = rs.normal(size=(F, 3)).astype(np.float32)
+    o = kin.pose_kinematics(bones, rest, kin.CanonicalSkeleton, pelvis=pelvis, scale=1.3)
+    kp, skts, l2ws, rots = okin.kinematic_chain(bones, rest, CANON_PARENTS, 14, pelvis, 1.3)
+    np.testing.assert_allclose(_np(o["l2ws"]), l2ws, atol=TOL_GPU, rtol=0)
+    np.testing.assert_allclose(_np(o["skts"]), skts, atol=TOL_GPU, rtol=0)
+    np.testing.assert_allclose(_np(o["kps"]), kp, atol=TOL_GPU, rtol=0)
+    np.testing.assert_allclose(_np(o["rots"]), rots, atol=TOL_GPU, rtol=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rot_dim", [3, 6, 9])
+def test_gpu_large_batch_all_rotation_forms(rot_dim):
+    kin = _kin()
+    rs = np.random.RandomState(rot_dim)
+    F = 4099
+    aa = rs.normal(scale=0.6, size=(F, 24, 3))
+    aa[::7, 3] = 0.0
+    aa[::11, 5] *= 1e-7
+    if rot_dim == 3:
+        bones = aa
+    else:
+        R = okin.axisang_to_rot(aa)
+        bones = R[..., :3, :2].reshape(F, 24, 6) if rot_dim == 6 else R.reshape(F, 24, 9)
+    bones = bones.astype(np.float32)
+    rest = syn.REST_POSE_24
+    o = kin.pose_kinematics(bones, rest, kin.SMPLSkeleton, pelvis=np.zeros((F, 3), np.float32))
+    kp, skts, l2ws, rots = okin.kinematic_chain(bones, rest, SMPL, 0)
+    np.testing.assert_allclose(_np(o["l2ws"]), l2ws, atol=TOL_GPU, rtol=0)
+    np.testing.assert_allclose(_np(o["skts"]), skts, atol=TOL_GPU, rtol=0)
+
+
+@pytest.mark.gpu
+def test_gpu_pose_opt_layer_multiview_and_rest_indices():
+    kin = _kin()
+    rs = np.random.RandomState(9)
+    N, U = 6, 3
+    kps = rs.normal(size=(N, 24, 3)).astype(np.float32)
+    bones = rs.normal(scale=0.4, size=(N, 24, 3)).astype(np.float32)
+    kp_map = np.array([0, 1, 2, 0, 1, 2])
+    kp_uidxs = np.array([0, 1, 2])
+    rests = np.stack([syn.REST_POSE_24, syn.REST_POSE_24 * 1.1]).astype(np.float32)
+    rest_pose_idxs = np.array([0, 1, 1, 0, 0, 1])
+    L = kin.PoseOptLayer(kps, bones, rests, kp_map=kp_map, kp_uidxs=kp_uidxs, rest_pose_idxs=rest_pose_idxs)
+    idxs = np.array([5, 0, 2, 2])
+    kp, bone, skts, l2ws, rots = L(idxs)
+    # expected: root bone of each index, other bones of its kp_map view, its own rest pose and pelvis
+    eb = np.concatenate([bones[idxs, :1], bones[kp_uidxs][kp_map[idxs], 1:]], axis=1)
+    ekp, eskts, el2ws, _ = okin.kinematic_chain(eb, rests[rest_pose_idxs[idxs]], SMPL, 0, kps[idxs, 0])
+    np.testing.assert_array_equal(_np(bone), eb)
+    np.testing.assert_allclose(_np(l2ws), el2ws, atol=TOL_GPU, rtol=0)
+    np.testing.assert_allclose(_np(skts), eskts, atol=TOL_GPU, rtol=0)
+    np.testing.assert_allclose(_np(kp), ekp, atol=TOL_GPU, rtol=0)
+    # rot6d storage gives the same transforms
+    L6 = kin.PoseOptLayer(kps, bones, rests[:1], use_rot6d=True, use_cache=True)
+    kp6, b6, skts6, _, _ = L6(idxs)
+    assert b6.shape[-1] == 6
+    ekp6, eskts6, _, _ = okin.kinematic_chain(bones[idxs], rests[0], SMPL, 0, kps[idxs, 0])
+    np.testing.assert_allclose(_np(skts6), eskts6, atol=TOL_GPU, rtol=0)
+
+
+@pytest.mark.gpu
+def test_gpu_errors_and_edge_cases():
+    kin = _kin()
+    _lib = importlib.import_module("a-nerf_amd._lib")
+    bad = kin.Skeleton(["a", "b", "c"], np.array([0, 2, 1]), 0, [1, 2], {}, [])
+    with pytest.raises(_lib.AnerfError, match="cycle"):
+        kin.pose_kinematics(np.zeros((2, 3, 3), np.float32), np.zeros((3, 3), np.float32), bad)
+    oob = kin.Skeleton(["a", "b"], np.array([0, 7]), 0, [1], {}, [])
+    with pytest.raises(_lib.AnerfError, match="out of range"):
+        kin.pose_kinematics(np.zeros((1, 2, 3), np.float32), np.zeros((2, 3), np.float32), oob)
+    o = kin.pose_kinematics(np.zeros((0, 24, 3), np.float32), syn.REST_POSE_24, kin.SMPLSkeleton)
+    assert o["skts"].shape == (0, 24, 4, 4)
+    # an out-of-range rest index poisons only its own frame
+    rests = np.stack([syn.REST_POSE_24] * 2)
+    o = kin.pose_kinematics(np.zeros((3, 24, 3), np.float32), rests, kin.SMPLSkeleton, rest_idx=[0, 5, 1])
+    s = _np(o["skts"])
+    assert np.isnan(s[1][:, :3]).all() and np.isfinite(s[[0, 2]]).all()
+    # identity pose: skts are pure translations by -rest
+    np.testing.assert_allclose(s[0][:, :3, 3], -syn.REST_POSE_24.astype(np.float64), atol=1e-7)
+
+
+@pytest.mark.gpu
+def test_gpu_skts_drive_the_renderer():
+    """skts produced on the device render the same frame as the host-chained synthetic skts."""
+    kin = _kin()
+    anerf = importlib.import_module("a-nerf_amd")
+    sc = syn.make_scene(n_joints=24, H=64, W=64, seed=3)
+    o = kin.pose_kinematics(sc["bones"].astype(np.float32), sc["rest"], kin.SMPLSkeleton)
+    np.testing.assert_allclose(_np(o["skts"]), sc["skts"], atol=TOL_GPU, rtol=0)
+    np.testing.assert_allclose(_np(o["kps"]), sc["kps"], atol=TOL_GPU, rtol=0)
+    cfg = anerf.RenderConfig(n_joints=24, netdepth=4, netwidth=128, N_samples=32, N_importance=0).validate()
+    ck = syn.make_checkpoint(11, n_joints=24, D=4, W=128, fine=False, tau=20.0)
+    kw = {"ray_caster": anerf.RayCaster(cfg, ck, device=0), "N_samples": 32, "N_importance": 0, "perturb": False,
+          "raw_noise_std": 0., "ray_noise_std": 0., "use_viewdirs": True, "preproc_kwargs": {"density_scale": 1.0},
+          "lindisp": False}
+    outs = []
+    for skts in (sc["skts"], _np(o["skts"]).astype(np.float32)):
+        # same kps for both: the pixel set comes from the host cylinder
+        outs.append(anerf.render_path(torch.from_numpy(sc["c2ws"]), (64, 64, sc["focal"]), 4096, kw,
+                                      kp=torch.from_numpy(sc["kps"]), skts=torch.from_numpy(skts), ret_acc=True,
+                                      ext_scale=0.001)[:3])
+    for a, b in zip(*outs):
+        np.testing.assert_allclose(a, b, atol=1e-4, rtol=0)
