@@ -18,6 +18,7 @@
 //   anerf_stages.hpp   per-ray stages: view factor G, compositing, importance sampling
 //   anerf_kernels.hpp  __global__ kernels (render, density, near/far, rays, compose, encode)
 //   anerf_pose.hpp     pose -> skeleton transforms (kinematic chain, inverse)
+//   anerf_boxes.hpp    bounding cylinder + 2-D pixel box per frame (kp_to_valid_rays)
 //   anerf_pack.hpp     host weight packing / model binding
 //   this file          the C ABI (include/anerf.h)
 //
@@ -44,6 +45,7 @@ using namespace anerf;
 #include "anerf_stages.hpp"
 #include "anerf_kernels.hpp"
 #include "anerf_pose.hpp"
+#include "anerf_boxes.hpp"
 #include "anerf_pack.hpp"
 
 #ifdef ANERF_STAMPS
@@ -464,6 +466,31 @@ int anerf_pose_kinematics(const float* bones, int32_t rot_dim, const float* rest
     const size_t lds = sizeof(double) * 12 * n_joints * KIN_WAVES;
     hipLaunchKernelGGL(pose_kinematics_kernel, dim3((unsigned)((n_frames + KIN_WAVES - 1) / KIN_WAVES)),
                        dim3(64 * KIN_WAVES), lds, st, a);
+    HIP_TRY(hipGetLastError());
+    return ANERF_OK;
+}
+
+int anerf_kp_boxes(const float* kps, const float* cyls_in, int64_t n_kp, int32_t n_joints, int32_t root_id,
+                   double ext_scale, const float* w2cs, const float* focals, const int32_t* offsets, int64_t n_frames,
+                   int32_t H, int32_t W, const double* cap_dirs, float* cyls_out, int32_t* boxes_out, void* stream) {
+    if (n_kp < 1 || n_frames < 0 || H <= 0 || W <= 0 || (!kps && !cyls_in))
+        return fail(ANERF_EINVAL, "anerf_kp_boxes: bad arguments");
+    if (kps && (n_joints < 1 || root_id < 0 || root_id >= n_joints))
+        return fail(ANERF_EINVAL, "anerf_kp_boxes: bad skeleton arguments");
+    if (n_frames > 0 && (!w2cs || !focals || !boxes_out)) return fail(ANERF_EINVAL, "anerf_kp_boxes: bad buffers");
+    BoxArgs a{};
+    a.kps = kps; a.cyls_in = cyls_in; a.w2cs = w2cs; a.focals = focals; a.offsets = offsets;
+    a.cap_dirs = cap_dirs; a.cyls_out = cyls_out; a.boxes_out = boxes_out;
+    a.n_kp = n_kp; a.n_frames = n_frames; a.nj = n_joints; a.root = root_id; a.H = H; a.W = W;
+    // Python floats meeting float32 arrays: rounded to float32 first (numpy NEP 50)
+    const double ext = 250.0 * ext_scale;
+    a.ext = (float)ext;
+    a.ext_top = (float)(ext * 1.6);
+    a.ext_bot = (float)(ext * 1.1);
+    const int64_t waves = std::max(n_frames, cyls_out ? n_kp : (int64_t)0);
+    if (waves == 0) return ANERF_OK;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(kp_boxes_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, a);
     HIP_TRY(hipGetLastError());
     return ANERF_OK;
 }

@@ -125,3 +125,56 @@ def valid_pixels(c2ws, H, W, focal, kps=None, cylinders=None, ext_scale=0.00035,
         idxs.append(box_pixels(tl, br, w))
         boxes.append((tl, br))
     return idxs, cylinders, boxes
+
+
+# float64 (cos, sin) of the 50 cap angles exactly as numpy computes them (cylinder_to_box_2d)
+_CAP_ANGLES = np.linspace(0.0, 2 * np.pi, 50)
+CAP_DIRS = np.ascontiguousarray(np.stack([np.cos(_CAP_ANGLES), np.sin(_CAP_ANGLES)], axis=-1))
+_cap_dev = {}
+
+
+def device_boxes(c2ws, H, W, focal, kps=None, cylinders=None, ext_scale=0.00035, centers=None, device=None):
+    """valid_pixels with the cylinder and box computed on the GPU (anerf_kp_boxes).
+
+    kps (P, NJ, 3) / cylinders (P, 5) may be device tensors (e.g. from kinematics.PoseOptLayer): they
+    never leave the device; only the (F, 4) integer boxes come back.  The extrinsics
+    inv(swap_mat(c2w)) are computed on the host with numpy, as the reference does (4x4 per camera).
+    Returns (cylinders (P, 5) float32 device tensor, bboxes list[(tl, br)] int32 like valid_pixels)."""
+    import torch
+    from . import _lib
+    if not isinstance(H, int) or not isinstance(W, int):
+        raise NotImplementedError("device_boxes: one image size for all frames")
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    c2ws = np.asarray(c2ws, dtype=np.float32)
+    F = c2ws.shape[0]
+    w2cs = np.stack([_extrinsic_from_c2w(c) for c in c2ws]).astype(np.float32)
+    fo = []
+    for i in range(F):
+        f = np.asarray(focal if isinstance(focal, float) else focal[i], dtype=np.float32).reshape(-1)
+        fo.append((f[0], f[1] if f.size >= 2 else f[0]))
+    focals = np.asarray(fo, dtype=np.float32)
+    src = kps if kps is not None else cylinders
+    if src is None:
+        raise ValueError("need kps or cylinders")
+    src = torch.as_tensor(src).to(device=dev, dtype=torch.float32).contiguous()
+    n_kp = int(src.shape[0])
+    nj = int(src.shape[1]) if kps is not None else 0
+    if dev not in _cap_dev:
+        _cap_dev[dev] = torch.from_numpy(CAP_DIRS).to(dev)
+    cyl = torch.empty(n_kp, 5, device=dev, dtype=torch.float32)
+    boxes = torch.empty(F, 4, device=dev, dtype=torch.int32)
+    w2c_d = torch.from_numpy(w2cs).to(dev)
+    foc_d = torch.from_numpy(focals).to(dev)
+    cen_d = None
+    if centers is not None:   # int(center[0]), int(center[1]) on the host, as cylinder_to_box_2d does
+        offs = np.array([[int(c[0]), int(c[1])] for c in centers], dtype=np.int32)
+        cen_d = torch.from_numpy(offs).to(dev)
+    lib = _lib.load()
+    with torch.cuda.device(dev):
+        rc = lib.anerf_kp_boxes(_lib.ptr(src) if kps is not None else None, None if kps is not None else _lib.ptr(src),
+                                n_kp, nj, 0, float(ext_scale), _lib.ptr(w2c_d), _lib.ptr(foc_d), _lib.ptr(cen_d), F,
+                                H, W, _lib.ptr(_cap_dev[dev]), _lib.ptr(cyl), _lib.ptr(boxes), _lib.stream_handle(dev))
+    _lib.check(rc, "anerf_kp_boxes")
+    b = boxes.cpu().numpy()
+    bboxes = [(b[i, :2].copy(), b[i, 2:].copy()) for i in range(F)]
+    return cyl, bboxes

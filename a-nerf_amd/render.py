@@ -95,10 +95,18 @@ def render_frames(render_poses, hwf, chunk, render_kwargs, centers=None, kp=None
     n_frames = poses_np.shape[0]
     if kp is None and cyls is None:
         raise NotImplementedError("full-image rendering without a skeleton bounding cylinder is not implemented")
-    valid_idxs, cyl_params, bboxes = host_rays.valid_pixels(
-        poses_np, H, W, focal, kps=_to_np(kp), cylinders=_to_np(cyls), ext_scale=ext_scale,
-        centers=None if centers is None else _to_np(centers))
-    cyl_params = torch.from_numpy(np.ascontiguousarray(cyl_params))
+    on_dev = any(torch.is_tensor(x) and x.is_cuda for x in (kp, cyls)) and isinstance(H, int) and isinstance(W, int)
+    if on_dev:
+        # skeleton already on the device (e.g. kinematics.PoseOptLayer): cylinder and box there too
+        cyl_params, bboxes = host_rays.device_boxes(poses_np, H, W, focal, kps=kp, cylinders=cyls,
+                                                    ext_scale=ext_scale,
+                                                    centers=None if centers is None else _to_np(centers), device=dev)
+        valid_idxs = [host_rays.box_pixels(tl, br, W) for tl, br in bboxes]
+    else:
+        valid_idxs, cyl_params, bboxes = host_rays.valid_pixels(
+            poses_np, H, W, focal, kps=_to_np(kp), cylinders=_to_np(cyls), ext_scale=ext_scale,
+            centers=None if centers is None else _to_np(centers))
+        cyl_params = torch.from_numpy(np.ascontiguousarray(cyl_params))
     lib = _lib.load()
     st = _lib.stream_handle(dev)
     frames = range(n_frames) if frame_ids is None else frame_ids

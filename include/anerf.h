@@ -197,6 +197,20 @@ int anerf_pose_kinematics(const float* bones, int32_t rot_dim, const float* rest
                           int32_t root_id, int64_t n_frames, float* kps, float* skts, float* l2ws, float* rots,
                           void* stream);
 
+/* Bounding cylinder and 2-D pixel box of every frame on the device, the host
+ * half of kp_to_valid_rays (core/utils/ray_utils.py:83-136): get_kp_bounding_cylinder
+ * (skeleton_utils.py:542-592; extend_mm 250, top/bot expand 1.6/1.1, head '-y') of kps [n_kp][NJ][3]
+ * (or the given cylinders cyls_in [n_kp][5] when kps is NULL), then cylinder_to_box_2d
+ * (skeleton_utils.py:607-694) for frame i with cylinder i % n_kp, extrinsic w2cs [F][4][4] =
+ * float32 inv(swap_mat(c2w)) (nerf_c2w_to_extrinsic, computed by the caller as the reference does),
+ * focals [F][2] float32 (fx, fy), offsets [F][2] = int(center) or NULL (int(W/2), int(H/2)), cap_dirs [50][2] =
+ * float64 (cos, sin) of linspace(0, 2 pi, 50) as numpy computes them (NULL: device cos/sin).
+ * Outputs cyls_out [n_kp][5] float32 (optional) and boxes_out [F][4] int32 = (x0, y0, x1, y1):
+ * pixels y in [y0, y1), x in [x0, x1) — the integers the reference computes. */
+int anerf_kp_boxes(const float* kps, const float* cyls_in, int64_t n_kp, int32_t n_joints, int32_t root_id,
+                   double ext_scale, const float* w2cs, const float* focals, const int32_t* offsets, int64_t n_frames,
+                   int32_t H, int32_t W, const double* cap_dirs, float* cyls_out, int32_t* boxes_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

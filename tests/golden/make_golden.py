@@ -315,6 +315,45 @@ def bbox_table(mods):
     print(f"wrote {path}")
 
 
+def random_boxes_table(mods, n=400):
+    """Cylinders and integer boxes of n random frames straight from the reference's
+    get_kp_bounding_cylinder + cylinder_to_box_2d (the calls kp_to_valid_rays makes,
+    ray_utils.py:89-123): random poses, camera distances / yaws / pitches, focals (scalar or
+    (fx, fy)), principal points and image sizes, incl. boxes clipped at the image border."""
+    sk = mods[4]
+    rs = np.random.RandomState(777)
+    parents, rest = anerf_syn.skeleton(24)
+    rows = {k: [] for k in ("kps", "c2w", "focal", "center", "has_center", "hw", "cyl", "tl", "br")}
+    for _ in range(n):
+        bones = rs.normal(scale=0.3, size=(24, 3))
+        bones[0] = [np.pi, 0.0, 0.0] + rs.normal(scale=0.3, size=3)
+        l2ws = anerf_syn.pose_l2ws(bones, rest * rs.uniform(0.5, 1.5), parents)
+        kps = (l2ws[:, :3, 3] + rs.normal(scale=0.3, size=3)).astype(np.float32)
+        c2w = anerf_syn.camera_c2w(distance=rs.uniform(2.5, 9.0), yaw=rs.uniform(-np.pi, np.pi))
+        pitch = rs.uniform(-0.3, 0.3)
+        rx = np.array([[1, 0, 0, 0], [0, np.cos(pitch), -np.sin(pitch), 0], [0, np.sin(pitch), np.cos(pitch), 0],
+                       [0, 0, 0, 1]])
+        c2w = (rx @ c2w).astype(np.float32)
+        H, W = int(rs.choice([64, 200, 512, 1000])), int(rs.choice([64, 256, 512, 777]))
+        f = np.array([rs.uniform(0.8, 2.0) * H, rs.uniform(0.8, 2.0) * H]) if rs.rand() < 0.3 else \
+            np.array([rs.uniform(0.8, 2.0) * H] * 2)
+        has_c = rs.rand() < 0.3
+        center = np.array([rs.uniform(0.3, 0.7) * W, rs.uniform(0.3, 0.7) * H]) if has_c else np.zeros(2)
+        ext = 0.001
+        cyl = sk.get_kp_bounding_cylinder(kps[None], skel_type=sk.SMPLSkeleton, ext_scale=ext, extend_mm=250,
+                                          top_expand_ratio=1.6, bot_expand_ratio=1.1, head="-y")[0]
+        cyl = np.asarray(cyl, dtype=np.float32)   # torch.FloatTensor(cylinder_params) in kp_to_valid_rays
+        w2c = sk.nerf_c2w_to_extrinsic(c2w)
+        focal = float(f[0]) if f[0] == f[1] else f
+        tl, br, _ = sk.cylinder_to_box_2d(cyl, [H, W, focal], w2c, center=center if has_c else None)
+        for k, v in (("kps", kps), ("c2w", c2w), ("focal", f), ("center", center), ("has_center", has_c),
+                     ("hw", (H, W)), ("cyl", cyl), ("tl", tl), ("br", br)):
+            rows[k].append(np.asarray(v))
+    path = os.path.join(HERE, "boxes_random.npz")
+    np.savez_compressed(path, **{k: np.stack(v) for k, v in rows.items()})
+    print(f"wrote {path}")
+
+
 def kinematics_table(mods):
     """Pose -> skeleton transforms from the reference's own functions:
     * PoseOptLayer.calculate_kinematic (core/pose_opt.py:372-445, unrolled chain :482-521) with the
@@ -389,6 +428,8 @@ def main():
         bbox_table(mods)
     if not a.only or a.only == "kinematics":
         kinematics_table(mods)
+    if not a.only or a.only == "boxes_random":
+        random_boxes_table(mods)
 
 
 if __name__ == "__main__":

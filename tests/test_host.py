@@ -87,3 +87,27 @@ def test_synthetic_skeleton_chain_is_rigid():
         a = np.linalg.norm(sc["kps"][0][j] - sc["kps"][0][p])
         b = np.linalg.norm(syn.REST_POSE_24[j] - syn.REST_POSE_24[p])
         assert abs(a - b) < 1e-5
+
+
+RANDOM_BOXES = np.load(os.path.join(HERE, "golden", "boxes_random.npz"))
+
+
+def _random_frame(z, i):
+    H, W = (int(v) for v in z["hw"][i])
+    f = z["focal"][i]
+    focal = float(f[0]) if f[0] == f[1] else f.copy()
+    centers = z["center"][i:i + 1] if z["has_center"][i] else None
+    return H, W, focal, centers
+
+
+def test_random_boxes_bit_exact_vs_reference():
+    """400 random poses / cameras / focals / principal points / image sizes: the host restatement
+    gives the reference's get_kp_bounding_cylinder + cylinder_to_box_2d integers exactly."""
+    z = RANDOM_BOXES
+    for i in range(z["kps"].shape[0]):
+        H, W, focal, centers = _random_frame(z, i)
+        _, cyls, boxes = rays.valid_pixels(z["c2w"][i:i + 1], H, W, focal if isinstance(focal, float) else [focal],
+                                           kps=z["kps"][i:i + 1], ext_scale=0.001, centers=centers)
+        np.testing.assert_array_equal(cyls[0], z["cyl"][i])
+        np.testing.assert_array_equal(boxes[0][0], z["tl"][i])
+        np.testing.assert_array_equal(boxes[0][1], z["br"][i])
