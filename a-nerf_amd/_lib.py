@@ -19,6 +19,8 @@ c_i32p = ctypes.POINTER(ctypes.c_int32)
 c_i64p = ctypes.POINTER(ctypes.c_int64)
 
 ANERF_PREC_FP32 = 0
+ANERF_PREC_BF16X3 = 1
+PRECISIONS = {"fp32": ANERF_PREC_FP32, "bf16x3": ANERF_PREC_BF16X3}
 
 
 class ModelDesc(ctypes.Structure):

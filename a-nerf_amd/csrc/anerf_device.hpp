@@ -14,6 +14,7 @@
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 namespace anerf {
 
@@ -22,6 +23,19 @@ namespace anerf {
 // B[l>>5][l&31]; D row = (r&3) + 8(r>>2) + 4(l>>5), col = l&31 for register r.
 __device__ __forceinline__ f32x16 mfma_f32_32x32x2(float a, float b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// v_mfma_f32_32x32x16_bf16: lane l supplies A[l&31][8(l>>5) + j] and B[8(l>>5) + j][l&31], j = 0..7;
+// same C/D layout as the f32 form.  Products of bf16 are exact in the f32 accumulation.
+__device__ __forceinline__ f32x16 mfma_bf16_32x32x16(bf16x8 a, bf16x8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+// bf16x3 product: a b ~= a_hi b_hi + a_hi b_lo + a_lo b_hi (the dropped a_lo b_lo is 2^-16 smaller),
+// small terms first
+__device__ __forceinline__ f32x16 mfma_x3(bf16x8 ah, bf16x8 al, bf16x8 bh, bf16x8 bl, f32x16 c) {
+    c = mfma_bf16_32x32x16(al, bh, c);
+    c = mfma_bf16_32x32x16(ah, bl, c);
+    return mfma_bf16_32x32x16(ah, bh, c);
 }
 
 // output row (within a 32-row block) held by register r of lane-half h

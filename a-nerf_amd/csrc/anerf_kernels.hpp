@@ -3,7 +3,7 @@
 #pragma once
 
 // ======================================================================= fused render kernel
-template <int W, int MR>
+template <int W, int MR, int PREC>
 __global__ __launch_bounds__(256, 1) void render_kernel(ModelDev M, RenderArgs A, LdsPlan P) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     constexpr int WH = W / 2;
@@ -56,7 +56,7 @@ __global__ __launch_bounds__(256, 1) void render_kernel(ModelDev M, RenderArgs A
         const int nb = (n + 31) / 32;
         for (int b = wave; b < nr * nb; b += 4) {
             const int r = b / nb, s0 = (b % nb) * 32;
-            mlp_block<W, MR>(M, net, lds + P.ray + 16 * r, lds + P.sk + P.sk_stride * r, lds + P.cut,
+            mlp_block<W, MR, PREC>(M, net, lds + P.ray + 16 * r, lds + P.sk + P.sk_stride * r, lds + P.cut,
                              lds + zoff + P.z_stride * r, n, s0, lds + P.g + P.g_stride * r,
                              lds + P.raw + P.raw_stride * r, lane, A.mfma_count, lds + P.bias,
                              (P.uf >= 0 && M.skip + 1 < M.D) ? lds + P.uf + wave * P.uf_stride : nullptr,
@@ -171,7 +171,7 @@ __global__ __launch_bounds__(256, 1) void density_kernel(ModelDev M, DensityArgs
         f32x16 acc[RB], h[RB];
         JointMask mask;
         Ring ring;
-        mlp_trunk<W, MR, false>(M, net, lds + P.sk, lds + P.cut, px, py, pz, lane, lds + P.bias, uf, nullptr, acc, h, ring,
+        mlp_trunk<W, MR, false, 0>(M, net, lds + P.sk, lds + P.cut, px, py, pz, lane, lds + P.bias, uf, nullptr, acc, h, ring,
                          mask, nullptr, st);
         // alpha_linear on relu(h_last), in the k-step order of the render path's fused alpha head
         float sig = 0.0f;

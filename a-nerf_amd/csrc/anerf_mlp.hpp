@@ -132,6 +132,96 @@ __device__ __forceinline__ void mlp_layer(f32x16 (&out)[RBO], f32x16 (&ain)[RBI]
     }
 }
 
+// ---- bf16x3 form of mlp_layer for the dense RBI*32 -> RBO*32 activation parts (ANERF_PREC_BF16X3).
+// One v_mfma_f32_32x32x16_bf16 covers 16 k (vs 2 for the f32 form); the x = x_hi + x_lo split of an
+// operand costs 3 of them per product, ~5.3x the f32 MFMA rate.  The B operands are the previous
+// layer's accumulators: relu, then registers 8s..8s+7 of block rb -> fragments hi/lo of k-step s,
+// kept in h[rb] as [hi s0 | lo s0 | hi s1 | lo s1] (4 registers each).  Same lead / k-major group
+// schedule as mlp_layer (pack_layer_x3), 6 MFMAs per 16-float group.
+__device__ __forceinline__ bf16x8 frag_of(const f32x16& v, int f) {
+    return __builtin_bit_cast(bf16x8, f32x4{v[4 * f], v[4 * f + 1], v[4 * f + 2], v[4 * f + 3]});
+}
+__device__ __forceinline__ bf16x8 frag_of(const float (&v)[16], int f) {
+    return __builtin_bit_cast(bf16x8, f32x4{v[4 * f], v[4 * f + 1], v[4 * f + 2], v[4 * f + 3]});
+}
+__device__ __forceinline__ f32x16 split_block(const f32x16& a) {
+    f32x16 o;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        bf16x8 hi, lo;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) hi[j] = (__bf16)relu_act(a[8 * s + j]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) lo[j] = (__bf16)(relu_act(a[8 * s + j]) - (float)hi[j]);
+        const f32x4 h4 = __builtin_bit_cast(f32x4, hi), l4 = __builtin_bit_cast(f32x4, lo);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            o[8 * s + e] = h4[e];
+            o[8 * s + 4 + e] = l4[e];
+        }
+    }
+    return o;
+}
+
+template <int RBO, int RBI>
+__device__ __forceinline__ void mlp_layer_x3(f32x16 (&out)[RBO], f32x16 (&ain)[RBI], f32x16 (&h)[RBI],
+                                             const float* __restrict__ bias, const float* __restrict__ wp, int lane,
+                                             Ring& ring, const float* __restrict__ next) {
+    static_assert(RBO <= RBI && RBO % 2 == 0, "x3 layer shape");
+    constexpr int NG = RBO + (RBI - 1) * RBO;
+    const int hh = lane >> 5;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(wp);
+    const __amdgpu_buffer_rsrc_t rn = make_rsrc(next);
+    auto convert = [&](int rb) {
+        h[rb] = split_block(ain[rb]);
+        if (rb < RBO) {
+            const f32x4* p = reinterpret_cast<const f32x4*>(bias + (rb * 2 + hh) * 16);
+            const f32x4 v0 = p[0], v1 = p[1], v2 = p[2], v3 = p[3];
+            out[rb] = f32x16{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3],
+                             v2[0], v2[1], v2[2], v2[3], v3[0], v3[1], v3[2], v3[3]};
+        }
+    };
+    auto prefetch = [&](int g) {
+        if (g + 2 < NG)
+            load_group<16>(ring.v[(g + 2) % 4], rs, lane, g + 2);
+        else if (NG % 4 == 0 && next)
+            load_group<16>(ring.v[(g + 2) % 4], rn, lane, g + 2 - NG);
+    };
+    convert(0);
+#pragma clang loop unroll(full)
+    for (int g = 0; g < RBO; ++g) {  // lead groups: output block g, input block 0
+        __builtin_amdgcn_sched_barrier(0);
+        prefetch(g);
+        const float (&a)[16] = ring.v[g % 4];
+#pragma clang loop unroll(full)
+        for (int s = 1; s >= 0; --s)  // (last-loaded fragments first)
+            out[g] = mfma_x3(frag_of(a, 2 * s), frag_of(a, 2 * s + 1), frag_of(h[0], 2 * s), frag_of(h[0], 2 * s + 1),
+                             out[g]);
+        if (g + 1 < RBO) {
+            convert(g + 1);
+        } else {
+#pragma clang loop unroll(full)
+            for (int rb = RBO; rb < RBI; ++rb) convert(rb);
+        }
+    }
+#pragma clang loop unroll(full)
+    for (int ib = 1; ib < RBI; ++ib) {
+#pragma clang loop unroll(full)
+        for (int s = 0; s < 2; ++s) {
+            const bf16x8 bh = frag_of(h[ib], 2 * s), bl = frag_of(h[ib], 2 * s + 1);
+#pragma clang loop unroll(full)
+            for (int p = 0; p < RBO / 2; ++p) {
+                const int g = RBO + (ib - 1) * RBO + s * (RBO / 2) + p;
+                __builtin_amdgcn_sched_barrier(0);
+                prefetch(g);
+                const float (&a)[16] = ring.v[g % 4];
+                out[2 * p + 1] = mfma_x3(frag_of(a, 2), frag_of(a, 3), bh, bl, out[2 * p + 1]);
+                out[2 * p] = mfma_x3(frag_of(a, 0), frag_of(a, 1), bh, bl, out[2 * p]);
+            }
+        }
+    }
+}
+
 // The MLP input x = [v (k*NJ + j), r (NJ*NV + 3j + c)] is split into two k-streams:
 //  * the bone-direction part u_j = q_j/|q_j| (never windowed): k-step 3p+c pairs joint p (lane
 //    half 0) with joint p + NJH2 (half 1); this pass also ballots the cutoff window per joint;
@@ -510,7 +600,7 @@ __device__ __forceinline__ void view_dir_part(f32x16 (&acc)[RBV], const ModelDev
 // Encoder + density trunk of one 32-sample block: L0 (u and v parts), the hidden layers with the
 // skip; acc ends as the pre-activation of the last hidden layer.  `after_last` is the weight stream
 // that follows (the feature layer, or nothing for density-only queries).
-template <int W, int MR, bool WV>
+template <int W, int MR, bool WV, int P>
 __device__ __forceinline__ void mlp_trunk(const ModelDev& M, const NetDev& net, const float* __restrict__ sk,
                                           const float* __restrict__ cut, float px, float py, float pz, int lane,
                                           const float* __restrict__ bias, float* __restrict__ uf,
@@ -524,16 +614,20 @@ __device__ __forceinline__ void mlp_trunk(const ModelDev& M, const NetDev& net, 
     ring_preload<2 * RB>(ring, net.wl[0], lane);  // the u part's first groups, early
     load_bias<RB>(acc, bias, hh);
     STAMP(st, 10);
-    u_part<RB, WV>(acc, M, net.wl[0], sk, cut, px, py, pz, lane, &mask, uf, wvo, ring, M.D > 1 ? net.wl[1] : after_last,
+    const float* const* wl = P ? net.wl3 : net.wl;  // hidden-layer streams of this precision
+    u_part<RB, WV>(acc, M, net.wl[0], sk, cut, px, py, pz, lane, &mask, uf, wvo, ring, M.D > 1 ? wl[1] : after_last,
                st);
     STAMP(st, 8);
     v_part<RB, MR>(acc, M, net.wl0v, sk, cut, px, py, pz, lane, mask, st);
     STAMP(st, 9);
     for (int L = 1; L < M.D; ++L) {
-        const float* after = L + 1 < M.D ? net.wl[L + 1] : after_last;
+        const float* after = L + 1 < M.D ? wl[L + 1] : after_last;
         const bool skl = (L == M.skip + 1);
-        mlp_layer<RB, RB, true, true, false>(acc, acc, h, bias + L * W, net.wl[L], lane, ring,
-                                             skl ? (HANDOFF ? net.wskipu : nullptr) : after, nullptr, nosig);
+        const float* nxt = skl ? (HANDOFF ? net.wskipu : nullptr) : after;
+        if constexpr (P == 1)
+            mlp_layer_x3<RB, RB>(acc, acc, h, bias + L * W, wl[L], lane, ring, nxt);
+        else
+            mlp_layer<RB, RB, true, true, false>(acc, acc, h, bias + L * W, wl[L], lane, ring, nxt, nullptr, nosig);
         STAMP(st, 11);
         if (skl) {  // x part after the h part
             if (!HANDOFF) ring_preload<2 * RB>(ring, net.wskipu, lane);
@@ -549,7 +643,7 @@ __device__ __forceinline__ void mlp_trunk(const ModelDev& M, const NetDev& net, 
 }
 
 // One 32-sample block of one ray through a whole NeRF: raw (rgb, sigma) into LDS.
-template <int W, int MR>
+template <int W, int MR, int P>
 __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __restrict__ ray,
                           const float* __restrict__ sk, const float* __restrict__ cut, const float* __restrict__ z,
                           int n, int s0,
@@ -570,7 +664,7 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
     f32x16 acc[RB], h[RB];
     JointMask mask;
     Ring ring;
-    mlp_trunk<W, MR, true>(M, net, sk, cut, px, py, pz, lane, bias, uf, wvp, acc, h, ring, mask, net.wview, st);
+    mlp_trunk<W, MR, true, P>(M, net, sk, cut, px, py, pz, lane, bias, uf, wvp, acc, h, ring, mask, net.wview, st);
     // views_linears.0 with feature_linear fused in (W' = Wv_f Wf, see pack_net) on relu(h_last),
     // alpha_linear folded into its groups (same relu'd B operands), + the factorised
     // direction / code / bias part from G, then relu
@@ -599,9 +693,14 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
     if (mfma_count && lane == 0) {  // exact MFMA work of this block (wave-uniform quantities)
         const int act = __builtin_popcountll(mask.m0) + __builtin_popcountll(mask.m1);
         const int xk = 3 * M.njh2 + act * VPart<MR>::KB;  // k-steps of one x part
-        long long k = (long long)xk * RB + (long long)(M.D - 1) * (W / 2) * RB + (long long)(W / 2) * RBV +
-                      (long long)(M.njh2 + 1) * RBV;
+        long long k = (long long)xk * RB + (long long)(W / 2) * RBV + (long long)(M.njh2 + 1) * RBV;
         if (M.skip + 1 < M.D) k += (long long)xk * RB;
+        const long long hid = (long long)(M.D - 1) * RB * RB;  // 32x32 blocks of the hidden layers
+        if (P == 1) {
+            atomicAdd(mfma_count + 1, (unsigned long long)(hid * 2 * 3));  // 2 k16-steps x 3 per block
+        } else {
+            k += hid * 16;
+        }
         atomicAdd(mfma_count, (unsigned long long)k);
     }
     if (hh == 0 && s0 + sl < n) {

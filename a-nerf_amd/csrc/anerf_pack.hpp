@@ -76,6 +76,54 @@ std::vector<float> pack_layer(const float* Wt, int n_out, int ld, int col_off, i
     });
 }
 
+// ---- bf16x3 split of the dense layers (ANERF_PREC_BF16X3): w = w_hi + w_lo, each bf16 (RNE)
+uint16_t bf16_rne(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    if ((u & 0x7f800000u) == 0x7f800000u) return (uint16_t)((u >> 16) | ((u & 0xffffu) ? 0x40u : 0u));
+    return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+float bf16_to_f(uint16_t b) {
+    const uint32_t u = (uint32_t)b << 16;
+    float f;
+    std::memcpy(&f, &u, 4);
+    return f;
+}
+
+// dense layer for mlp_layer_x3 (v_mfma_f32_32x32x16_bf16): a group is 4 fragments of 8 bf16 per
+// lane (one b128 each).  Fragment (ob, ib, s) of lane l = (r, h), element j holds
+// W[32 ob + r][col_off + 32 ib + 16 s + 8 (j >> 2) + 4 h + (j & 3)] (the k order of an accumulator
+// tile used as B operand, registers 8s..8s+7).  Lead groups g < RBO: [hi, lo] of (g, 0, 0) and
+// (g, 0, 1); then per input block ib >= 1, k-step s, output pair (2p, 2p+1): [hi, lo] of both.
+std::vector<float> pack_layer_x3(const float* Wt, int n_out, int ld, int col_off, int n_in) {
+    const int RBO = n_out / 32, RBI = n_in / 32;
+    const int ng = RBO + (RBI - 1) * RBO;
+    return pack_groups(ng, 16, [&](int g, int sl, int l) {
+        const int f = sl >> 2, e = sl & 3;  // fragment, bf16 pair within it
+        int ob, ib, s;
+        if (g < RBO) {
+            ob = g, ib = 0, s = f >> 1;
+        } else {
+            const int idx = g - RBO, r = idx % RBO;
+            ib = 1 + idx / RBO, s = r / (RBO / 2), ob = 2 * (r % (RBO / 2)) + (f >> 1);
+        }
+        const bool lo = f & 1;
+        const int h = l >> 5, row = 32 * ob + (l & 31);
+        uint32_t bits = 0;
+        for (int jj = 0; jj < 2; ++jj) {
+            const int j = 2 * e + jj;
+            const int col = col_off + 32 * ib + 16 * s + 8 * (j >> 2) + 4 * h + (j & 3);
+            const float w = Wt[(size_t)row * ld + col];
+            const uint16_t hi = bf16_rne(w);
+            const uint16_t v = lo ? bf16_rne(w - bf16_to_f(hi)) : hi;
+            bits |= (uint32_t)v << (16 * jj);
+        }
+        float out;
+        std::memcpy(&out, &bits, 4);
+        return out;
+    });
+}
+
 // bone-direction part: k-step q = 3p + c, half h -> joint p + h*njh2, column nv*nj + 3j + c;
 // groups of 2 k-steps x RB blocks (slot float 2 rb + t)
 std::vector<float> pack_upart(const float* Wt, int n_out, int ld, int nj, int njh2, int mr) {
@@ -270,6 +318,10 @@ static int pack_net(const anerf_model_desc* d, int njh2, const anerf_net_weights
         }
         offs.push_back(pk.add(t));                                                    // codes
     }
+    for (int i = 1; i < d->net_depth; ++i) {                                          // bf16x3 hidden layers
+        const bool sk = (i == d->skip + 1);
+        offs.push_back(pk.add(pack_layer_x3(w->pts_w[i], W, sk ? cin + W : W, sk ? cin : 0, W)));
+    }
     return ANERF_OK;
 }
 
@@ -296,6 +348,7 @@ static void bind_net(const anerf_model_desc* d, const float* base, const std::ve
     nd.wrgb = base + o[k++];
     nd.brgb = base + o[k++];
     nd.codes = base + o[k++];
+    for (int i = 1; i < D; ++i) nd.wl3[i] = base + o[k++];
     nd.balpha = balpha;
 }
 

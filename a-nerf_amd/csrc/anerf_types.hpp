@@ -54,6 +54,7 @@ struct NetDev {
     const float* wrgb;       // [3][2][RBV][16]
     const float* brgb;       // [3]
     const float* codes;      // [n_codes + 1][cfc]: last row = eval-mode mean code
+    const float* wl3[MAXL];  // [i>0] activation parts as bf16x3 fragments (pack_layer_x3)
     float balpha;
 };
 

@@ -191,7 +191,7 @@ class RayCaster:
         if debug or count_mfma:
             dbg = _lib.Debug()
         if count_mfma:
-            self.last_mfma = torch.zeros(1, device=dev, dtype=torch.int64)
+            self.last_mfma = torch.zeros(2, device=dev, dtype=torch.int64)  # [f32 MFMAs, bf16 MFMAs]
             dbg.mfma_count = ctypes.cast(self.last_mfma.data_ptr(), ctypes.POINTER(ctypes.c_uint64))
         if debug:
             dd = {"near": torch.empty(n, **f32), "far": torch.empty(n, **f32), "z_coarse": torch.empty(n, S, **f32),
@@ -205,7 +205,8 @@ class RayCaster:
         ws, need = self.model.workspace(n, S, I)
         rc = _lib.load().anerf_render_rays(
             self.model.handle, _lib.ptr(rb), rb.shape[1], n, _lib.ptr(skt_tab), _lib.ptr(cyl_tab),
-            skt_tab.shape[0], _lib.ptr(pose), _lib.ptr(cam_t), S, I, int(chunk or max(n, 1)), _lib.ANERF_PREC_FP32,
+            skt_tab.shape[0], _lib.ptr(pose), _lib.ptr(cam_t), S, I, int(chunk or max(n, 1)),
+            _lib.PRECISIONS[self.cfg.precision],
             _lib.ptr(out["rgb_map"]), _lib.ptr(out["disp_map"]), _lib.ptr(out["acc_map"]),
             _lib.ptr(out.get("rgb0")), _lib.ptr(out.get("disp0")), _lib.ptr(out.get("acc0")),
             _lib.ptr(out["alpha"]), _lib.ptr(out.get("alpha0")), ctypes.byref(dbg) if dbg else None,

@@ -35,7 +35,10 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 BASELINE = json.load(open(os.path.join(REPO, "BASELINE.json")))
-FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md, FP32 matrix
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md, FP32 matrix (1024 SIMDs x 64 FLOP/clk x 2.4 GHz)
+BF16_MFMA_PEAK_TFLOPS = 2516.6  # MI355X_MICROARCH.md, BF16 dense (1024 SIMDs x 1024 FLOP/clk x 2.4 GHz)
+FLOP_F32_MFMA = 32 * 32 * 2 * 2     # v_mfma_f32_32x32x2_f32
+FLOP_BF16_MFMA = 32 * 32 * 16 * 2   # v_mfma_f32_32x32x16_bf16
 
 
 def parse():
@@ -49,6 +52,8 @@ def parse():
     ap.add_argument("--importance", type=int, default=128)
     ap.add_argument("--cpu-rays", type=int, default=20000, help="rays in the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16x3"],
+                    help="MLP arithmetic (include/anerf.h ANERF_PREC_*)")
     return ap.parse_args()
 
 
@@ -84,7 +89,7 @@ def main():
 
     H = W = a.res
     S, I = a.samples, a.importance
-    cfg = anerf.RenderConfig(n_joints=a.joints, N_samples=S, N_importance=I).validate()
+    cfg = anerf.RenderConfig(n_joints=a.joints, N_samples=S, N_importance=I, precision=a.precision).validate()
     ck = syn.make_checkpoint(13, n_joints=a.joints, D=8, W=256, fine=I > 0, tau=79.6)
     sc = syn.make_scene(n_joints=a.joints, H=H, W=W, seed=13 + rank)
     rc = anerf.RayCaster(cfg, ck, device=local)
@@ -144,8 +149,11 @@ def main():
     rc.render_rays(rb, S, skts=skts.expand(n, -1, -1, -1), cyls=cyl.expand(n, -1), N_importance=I, chunk=4096,
                    ret_alpha=False, count_mfma=True)
     torch.cuda.synchronize()
-    mfma = int(rc.last_mfma.item())
-    flop_exec = mfma * 32 * 32 * 2 * 2          # v_mfma_f32_32x32x2_f32: 2048 MAC
+    n_f32, n_bf16 = (int(v) for v in rc.last_mfma.tolist())
+    flop_exec = n_f32 * FLOP_F32_MFMA + n_bf16 * FLOP_BF16_MFMA
+    # the launch's MFMA work at each pipe's peak rate: the time the MFMA pipes must be busy
+    t_mfma = n_f32 * FLOP_F32_MFMA / (FP32_MFMA_PEAK_TFLOPS * 1e12) + n_bf16 * FLOP_BF16_MFMA / (BF16_MFMA_PEAK_TFLOPS * 1e12)
+    peak_tf = flop_exec / t_mfma / 1e12  # = 157.3 for fp32; the instruction-mix-weighted peak otherwise
     flop_ray = anerf.flops_per_sample(cfg) * anerf.samples_per_ray(cfg)  # SURVEY §8(d), reference work
     achieved_tf = flop_exec / (kern_ms * 1e-3) / 1e12
     ref_equiv_tf = flop_ray * n / (kern_ms * 1e-3) / 1e12
@@ -171,16 +179,19 @@ def main():
         line = {
             "metric": BASELINE["metric"], "value": round(value, 1), "unit": "rays/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(1e3 * elapsed / a.steps, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "fp32" if a.precision == "fp32" else "bf16x3 (split-fp32 hidden layers, fp32 accumulate; fp32 elsewhere)",
             "data": "synthetic (seeded SMPL-24 pose + seeded 8x256 weights; no dataset/checkpoint offline)",
             "config": {"workload": f"config3: {H}x{W} frame, {S}+{I} samples, {a.joints}-joint, 8x256 MLP, "
                                    f"one frame per GPU per step", "rays_per_frame": n,
                        "parallelism": f"frame-per-rank x{world}"},
-            "roofline": {"bound": "mfma", "achieved": round(achieved_tf, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_MFMA_PEAK_TFLOPS, 4),
+            "roofline": {"bound": "mfma", "achieved": round(achieved_tf, 2), "peak": round(peak_tf, 1),
+                         "unit": "TFLOP/s", "frac": round(achieved_tf / peak_tf, 4),
                          "traffic": traffic, "kernel_ms": round(kern_ms, 3),
-                         "flop": "executed MFMA FLOPs per launch (device counter) / launch time",
-                         "mfma_per_launch": mfma, "reference_flop_per_ray": flop_ray,
+                         "flop": "executed MFMA FLOPs per launch (device counters) / launch time; peak = the "
+                                 "FP32 (157.3) and BF16 (2516.6 TF) MFMA peaks weighted by this launch's mix",
+                         "mfma_f32_per_launch": n_f32, "mfma_bf16_per_launch": n_bf16,
+                         "reference_flop_per_ray": flop_ray,
                          "reference_equivalent_tflops": round(ref_equiv_tf, 2)},
             "cpu_baseline": cpu,
         }

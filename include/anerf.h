@@ -43,8 +43,13 @@ enum {
     ANERF_ENOMEM = -4
 };
 
-/* arithmetic used for the MLP contractions */
-enum { ANERF_PREC_FP32 = 0 };
+/* arithmetic used for the MLP contractions:
+ *   ANERF_PREC_FP32   every contraction on v_mfma_f32_32x32x2_f32 (exact fp32 products);
+ *   ANERF_PREC_BF16X3 the dense hidden layers split as x = x_hi + x_lo (bf16, round to nearest even)
+ *                     and computed as x_hi w_hi + x_hi w_lo + x_lo w_hi on v_mfma_f32_32x32x16_bf16
+ *                     with fp32 accumulation (~16-bit operands, products exact): outputs within
+ *                     1e-5 of the fp32 path on the reference fixtures; encoder and view parts fp32. */
+enum { ANERF_PREC_FP32 = 0, ANERF_PREC_BF16X3 = 1 };
 
 typedef struct anerf_model anerf_model;
 

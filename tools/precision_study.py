@@ -1,0 +1,78 @@
+"""Precision study: max-abs error of the render outputs when every MLP GEMM runs as
+  * bf16x3: x = x_hi + x_lo, W = W_hi + W_lo (bf16, round-to-nearest-even), y = x_hi W_hi + x_hi W_lo + x_lo W_hi
+    with exact products accumulated in fp32 (what v_mfma_f32_32x32x16_bf16 computes);
+  * bf16: y = bf16(x) bf16(W), fp32 accumulate;
+against the fp32 golden outputs of the reference (tests/golden/*.npz), on the reference's own render
+path (F.linear patched).  Runs only in the build container (imports /root/reference).
+
+Usage: python tools/precision_study.py [names...]
+"""
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+import make_golden as mg  # noqa: E402
+
+_lin = F.linear
+
+
+def _split(x):
+    hi = x.to(torch.bfloat16).float()
+    lo = (x - hi).to(torch.bfloat16).float()
+    return hi, lo
+
+
+def lin_bf16x3(x, w, b=None):
+    xh, xl = _split(x)
+    wh, wl = _split(w)
+    y = _lin(xh.double(), wh.double()).float()  # exact products; fp32-accumulate order is immaterial here
+    y = y + _lin(xh.double(), wl.double()).float() + _lin(xl.double(), wh.double()).float()
+    return y if b is None else y + b
+
+
+def lin_bf16(x, w, b=None):
+    y = _lin(x.to(torch.bfloat16).double(), w.to(torch.bfloat16).double()).float()
+    return y if b is None else y + b
+
+
+def run(name, mode, mods, tmp):
+    cfg = mg.CONFIGS[name]
+    z = np.load(os.path.join(REPO, "tests", "golden", name + ".npz"), allow_pickle=False)
+    args, kw, ck = mg.build_reference(mods, cfg, os.path.join(tmp, name + mode))
+    sc = mg.scene_for(cfg)
+    sc["cyls"] = z["cyls"]
+    o, d = torch.from_numpy(z["rays_o"]), torch.from_numpy(z["rays_d"])
+    cams = z["cams"] if "cams" in z.files else None
+    F.linear = {"bf16x3": lin_bf16x3, "bf16": lin_bf16, "fp32": _lin}[mode]
+    torch.nn.modules.linear.F.linear = F.linear
+    try:
+        ret = mg.render_subset(mods, kw, o, d, sc, cams=cams)
+    finally:
+        F.linear = _lin
+        torch.nn.modules.linear.F.linear = _lin
+    errs = {k: float(np.abs(ret[k] - z["out_" + k]).max()) for k in ("rgb_map", "disp_map", "acc_map", "rgb0")
+            if k in ret and "out_" + k in z.files}
+    return errs
+
+
+def main():
+    import tempfile
+    names = sys.argv[1:] or ["c2_256_s64_d8w256", "c3_512_s64i128_d8w256", "c4_512_s64i128_j65",
+                             "v1_mr10_w64_d4", "fc_64_s32i32_d4w128"]
+    torch.set_num_threads(8)
+    mods = mg.import_reference()
+    with tempfile.TemporaryDirectory() as tmp:
+        for n in names:
+            for mode in ("fp32", "bf16x3", "bf16"):
+                print(n, mode, run(n, mode, mods, tmp), flush=True)
+
+
+if __name__ == "__main__":
+    main()
