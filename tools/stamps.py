@@ -27,7 +27,8 @@ def main():
     lib.anerf_diag_set_stamps.argtypes = [ctypes.c_void_p]
     H = 512
     tau = float(sys.argv[1]) if len(sys.argv) > 1 else 79.6
-    cfg = anerf.RenderConfig(N_samples=64, N_importance=128).validate()
+    prec = os.environ.get("ANERF_PRECISION", "fp32")
+    cfg = anerf.RenderConfig(N_samples=64, N_importance=128, precision=prec).validate()
     ck = syn.make_checkpoint(13, n_joints=24, D=8, W=256, fine=True, tau=tau)
     sc = syn.make_scene(n_joints=24, H=H, W=H, seed=13)
     rc = anerf.RayCaster(cfg, ck)
@@ -42,7 +43,7 @@ def main():
     torch.cuda.synchronize()
     v = st.cpu().numpy().astype(np.float64)
     tot = v[0:24].sum()  # top-level phases + the MLP sub-phases (stamped separately)
-    print(f"tau={tau}: total wave-cycles {tot:.3e}")
+    print(f"tau={tau} precision={prec}: total wave-cycles {tot:.3e}")
     for i, nm in NAMES.items():
         print(f"{nm:34s} {100 * v[i] / tot:6.2f} %")
 
