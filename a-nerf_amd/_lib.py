@@ -20,7 +20,8 @@ c_i64p = ctypes.POINTER(ctypes.c_int64)
 
 ANERF_PREC_FP32 = 0
 ANERF_PREC_BF16X3 = 1
-PRECISIONS = {"fp32": ANERF_PREC_FP32, "bf16x3": ANERF_PREC_BF16X3}
+ANERF_PREC_BF16X6 = 2
+PRECISIONS = {"fp32": ANERF_PREC_FP32, "bf16x3": ANERF_PREC_BF16X3, "bf16x6": ANERF_PREC_BF16X6}
 
 
 class ModelDesc(ctypes.Structure):

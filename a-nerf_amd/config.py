@@ -32,8 +32,9 @@ class RenderConfig:
     single_net: bool = False
     chunk: int = 4096
     ext_scale: float = 0.001
-    # MLP arithmetic: "fp32" (fp32 MFMA everywhere, the parity default) or "bf16x3" (hidden layers as
-    # split-bf16 products on the bf16 MFMA pipe, fp32 accumulation; see include/anerf.h)
+    # MLP arithmetic: "fp32" (fp32 MFMA everywhere, the parity default), "bf16x6" (hidden layers as
+    # three-way split-bf16 products on the bf16 MFMA pipe, fp32-accurate) or "bf16x3" (two-way split,
+    # ~16-bit operands); fp32 accumulation in all (see include/anerf.h)
     precision: str = "fp32"
     extra: dict = field(default_factory=dict)
 
@@ -57,8 +58,8 @@ class RenderConfig:
             raise NotImplementedError(f"density activation {self.density_type} is undefined")
         if self.opt_framecode and self.n_framecodes <= 0:
             raise ValueError("opt_framecode needs n_framecodes > 0")
-        if self.precision not in ("fp32", "bf16x3"):
-            raise ValueError(f"precision={self.precision!r}: 'fp32' or 'bf16x3'")
+        if self.precision not in ("fp32", "bf16x6", "bf16x3"):
+            raise ValueError(f"precision={self.precision!r}: 'fp32', 'bf16x6' or 'bf16x3'")
         if self.n_joints < 1 or self.n_joints > 128:
             raise NotImplementedError(f"n_joints={self.n_joints} outside [1, 128]")
         for k in ("normalize_cutoff", "cut_to_dist", "cutoff_shift", "freq_schedule", "cutoff_bones"):

@@ -222,6 +222,129 @@ __device__ __forceinline__ void mlp_layer_x3(f32x16 (&out)[RBO], f32x16 (&ain)[R
     }
 }
 
+// ---- bf16x6 form (ANERF_PREC_BF16X6): x = x0 + x1 + x2 and w = w0 + w1 + w2 (bf16 RNE of the
+// running remainder; x - x0 and x - x0 - x1 are exact in f32), product ~= sum over i + j <= 2 of
+// x_i w_j: six v_mfma_f32_32x32x16_bf16 per 16 k, the dropped terms below 2^-26 of the product.
+// The activations stay f32 (relu'd) in h[]; one input block (16 values = 2 k16-steps) is split
+// into T (2 x 3 fragments) while the previous block's MFMAs run.  Weight groups are 12 floats
+// (fragments w0, w1, w2 of one (ob, ib, s)), prefetched 3 groups ahead in the 4-slot ring.
+struct X6Frag {
+    bf16x8 p[3];
+};
+
+__device__ __forceinline__ X6Frag split3(const f32x16& a, int s) {
+    X6Frag t;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float x = a[8 * s + j];
+        const __bf16 b0 = (__bf16)x;
+        const float r1 = x - (float)b0;
+        const __bf16 b1 = (__bf16)r1;
+        const float r2 = r1 - (float)b1;
+        t.p[0][j] = b0;
+        t.p[1][j] = b1;
+        t.p[2][j] = (__bf16)r2;
+    }
+    return t;
+}
+
+__device__ __forceinline__ f32x16 mfma_x6(const float (&w)[16], const X6Frag& x, f32x16 c) {
+    const bf16x8 w0 = frag_of(w, 0), w1 = frag_of(w, 1), w2 = frag_of(w, 2);
+    c = mfma_bf16_32x32x16(w2, x.p[0], c);  // small terms first
+    c = mfma_bf16_32x32x16(w1, x.p[1], c);
+    c = mfma_bf16_32x32x16(w0, x.p[2], c);
+    c = mfma_bf16_32x32x16(w1, x.p[0], c);
+    c = mfma_bf16_32x32x16(w0, x.p[1], c);
+    return mfma_bf16_32x32x16(w0, x.p[0], c);
+}
+
+// OUT_SAME: out aliases ain (hidden layers: out[rb] = bias once ain[rb] is consumed); otherwise out
+// starts at zero (the view layer).  ALPHA folds sig += w_alpha . h in the fp32 path's k order.
+template <int RBO, int RBI, bool OUT_SAME, bool ALPHA>
+__device__ __forceinline__ void mlp_layer_x6(f32x16 (&out)[RBO], f32x16 (&ain)[RBI], f32x16 (&h)[RBI],
+                                             const float* __restrict__ bias, const float* __restrict__ wp, int lane,
+                                             Ring& ring, bool preloaded, const float* __restrict__ next,
+                                             const float* __restrict__ wa, float& sig) {
+    static_assert(RBO <= RBI, "x6 layer shape");
+    constexpr int NG = 2 * RBO * RBI;
+    constexpr int PD = 3;  // prefetch distance (groups)
+    const int hh = lane >> 5;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(wp);
+    const __amdgpu_buffer_rsrc_t rn = make_rsrc(next);
+    auto convert = [&](int rb) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) h[rb][i] = relu_act(ain[rb][i]);
+        if (OUT_SAME && rb < RBO) {
+            const f32x4* p = reinterpret_cast<const f32x4*>(bias + (rb * 2 + hh) * 16);
+            const f32x4 v0 = p[0], v1 = p[1], v2 = p[2], v3 = p[3];
+            out[rb] = f32x16{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3],
+                             v2[0], v2[1], v2[2], v2[3], v3[0], v3[1], v3[2], v3[3]};
+        }
+    };
+    auto alpha = [&](int ib, int s) {  // k = 16 ib + 8 s + j, the order of mlp_layer's fold
+        if constexpr (ALPHA) {
+            const f32x4* w4 = reinterpret_cast<const f32x4*>(wa + hh * 16 * RBI + 16 * ib + 8 * s);
+            const f32x4 u0 = w4[0], u1 = w4[1];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) sig = fmaf(j < 4 ? u0[j] : u1[j - 4], h[ib][8 * s + j], sig);
+        }
+    };
+    if constexpr (!OUT_SAME) {
+#pragma unroll
+        for (int rb = 0; rb < RBO; ++rb) out[rb] = f32x16{0};
+    }
+    auto prefetch = [&](int g) {  // group g + PD of this layer, or the next x6 layer's first groups
+        if (g + PD < NG)
+            load_group<12>(ring.v[(g + PD) % 4], rs, lane, g + PD);
+        else if (NG % 4 == 0 && next)
+            load_group<12>(ring.v[(g + PD) % 4], rn, lane, g + PD - NG);
+    };
+    if (!preloaded) {
+#pragma unroll
+        for (int g = 0; g < PD; ++g) load_group<12>(ring.v[g], rs, lane, g);
+    }
+    convert(0);
+    X6Frag T[2] = {split3(h[0], 0), split3(h[0], 1)};
+#pragma clang loop unroll(full)
+    for (int g = 0; g < 2 * RBO; ++g) {  // lead groups: output block g/2, input block 0, k16-step g&1
+        __builtin_amdgcn_sched_barrier(0);
+        prefetch(g);
+        const int ob = g >> 1, s = g & 1;
+        out[ob] = mfma_x6(ring.v[g % 4], T[s], out[ob]);
+        if (ob == 0) alpha(0, s);
+        if (s == 1) {
+            if (ob + 1 < RBO) {
+                convert(ob + 1);
+            } else {
+#pragma clang loop unroll(full)
+                for (int rb = RBO; rb < RBI; ++rb) convert(rb);
+            }
+        }
+    }
+    X6Frag Tn[2];
+    if (RBI > 1) Tn[0] = split3(h[1], 0), Tn[1] = split3(h[1], 1);
+#pragma clang loop unroll(full)
+    for (int ib = 1; ib < RBI; ++ib) {
+        T[0] = Tn[0];
+        T[1] = Tn[1];
+#pragma clang loop unroll(full)
+        for (int s = 0; s < 2; ++s) {
+#pragma clang loop unroll(full)
+            for (int ob = 0; ob < RBO; ++ob) {
+                const int g = 2 * RBO + (ib - 1) * 2 * RBO + s * RBO + ob;
+                __builtin_amdgcn_sched_barrier(0);
+                prefetch(g);
+                out[ob] = mfma_x6(ring.v[g % 4], T[s], out[ob]);
+                if (ib + 1 < RBI) {  // the next input block's split under these MFMAs
+                    if (RBO >= 2 && s == 0 && ob < 2) Tn[ob] = split3(h[ib + 1], ob);
+                    if (RBO == 1) Tn[s] = split3(h[ib + 1], s);
+                }
+                if (ob == RBO - 1) alpha(ib, s);
+            }
+        }
+    }
+}
+
 // The MLP input x = [v (k*NJ + j), r (NJ*NV + 3j + c)] is split into two k-streams:
 //  * the bone-direction part u_j = q_j/|q_j| (never windowed): k-step 3p+c pairs joint p (lane
 //    half 0) with joint p + NJH2 (half 1); this pass also ballots the cutoff window per joint;
@@ -601,7 +724,7 @@ __device__ __forceinline__ void view_dir_part(f32x16 (&acc)[RBV], const ModelDev
 // skip; acc ends as the pre-activation of the last hidden layer.  `after_last` is the weight stream
 // that follows (the feature layer, or nothing for density-only queries).
 template <int W, int MR, bool WV, int P>
-__device__ __forceinline__ void mlp_trunk(const ModelDev& M, const NetDev& net, const float* __restrict__ sk,
+__device__ __forceinline__ bool mlp_trunk(const ModelDev& M, const NetDev& net, const float* __restrict__ sk,
                                           const float* __restrict__ cut, float px, float py, float pz, int lane,
                                           const float* __restrict__ bias, float* __restrict__ uf,
                                           float* __restrict__ wvo, f32x16 (&acc)[W / 32], f32x16 (&h)[W / 32],
@@ -614,23 +737,36 @@ __device__ __forceinline__ void mlp_trunk(const ModelDev& M, const NetDev& net, 
     ring_preload<2 * RB>(ring, net.wl[0], lane);  // the u part's first groups, early
     load_bias<RB>(acc, bias, hh);
     STAMP(st, 10);
-    const float* const* wl = P ? net.wl3 : net.wl;  // hidden-layer streams of this precision
-    u_part<RB, WV>(acc, M, net.wl[0], sk, cut, px, py, pz, lane, &mask, uf, wvo, ring, M.D > 1 ? wl[1] : after_last,
-               st);
+    const float* const* wl = P == 2 ? net.wl6 : (P ? net.wl3 : net.wl);  // hidden-layer streams of this precision
+    // (bf16x6 layers have 12-float groups: the phases before them do not prefetch into the ring for them)
+    u_part<RB, WV>(acc, M, net.wl[0], sk, cut, px, py, pz, lane, &mask, uf, wvo, ring,
+                   M.D > 1 ? (P == 2 ? nullptr : wl[1]) : after_last, st);
     STAMP(st, 8);
     v_part<RB, MR>(acc, M, net.wl0v, sk, cut, px, py, pz, lane, mask, st);
     STAMP(st, 9);
+    bool pre6 = false;
     for (int L = 1; L < M.D; ++L) {
         const float* after = L + 1 < M.D ? wl[L + 1] : after_last;
         const bool skl = (L == M.skip + 1);
-        const float* nxt = skl ? (HANDOFF ? net.wskipu : nullptr) : after;
-        if constexpr (P == 1)
-            mlp_layer_x3<RB, RB>(acc, acc, h, bias + L * W, wl[L], lane, ring, nxt);
-        else
-            mlp_layer<RB, RB, true, true, false>(acc, acc, h, bias + L * W, wl[L], lane, ring, nxt, nullptr, nosig);
+        if constexpr (P == 2) {
+            const float* nxt6 = skl ? nullptr : after;  // the next x6 layer, or after_last (also x6 form)
+            mlp_layer_x6<RB, RB, true, false>(acc, acc, h, bias + L * W, wl[L], lane, ring, pre6, nxt6, nullptr,
+                                              nosig);
+            pre6 = nxt6 != nullptr;
+            if (skl) {  // the skip x part preloads its own groups; the phase after it loads itself
+                ring_preload<2 * RB>(ring, net.wskipu, lane);
+                after = nullptr;
+            }
+        } else {
+            const float* nxt = skl ? (HANDOFF ? net.wskipu : nullptr) : after;
+            if constexpr (P == 1)
+                mlp_layer_x3<RB, RB>(acc, acc, h, bias + L * W, wl[L], lane, ring, nxt);
+            else
+                mlp_layer<RB, RB, true, true, false>(acc, acc, h, bias + L * W, wl[L], lane, ring, nxt, nullptr, nosig);
+            if (skl && !HANDOFF) ring_preload<2 * RB>(ring, net.wskipu, lane);
+        }
         STAMP(st, 11);
         if (skl) {  // x part after the h part
-            if (!HANDOFF) ring_preload<2 * RB>(ring, net.wskipu, lane);
             if (uf)
                 u_part_lds<RB>(acc, M, net.wskipu, uf, lane, ring, after);
             else
@@ -640,6 +776,7 @@ __device__ __forceinline__ void mlp_trunk(const ModelDev& M, const NetDev& net, 
             STAMP(st, 12);
         }
     }
+    return pre6;  // (bf16x6: after_last's first groups are in the ring)
 }
 
 // One 32-sample block of one ray through a whole NeRF: raw (rgb, sigma) into LDS.
@@ -664,14 +801,19 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
     f32x16 acc[RB], h[RB];
     JointMask mask;
     Ring ring;
-    mlp_trunk<W, MR, true, P>(M, net, sk, cut, px, py, pz, lane, bias, uf, wvp, acc, h, ring, mask, net.wview, st);
+    const bool pre = mlp_trunk<W, MR, true, P>(M, net, sk, cut, px, py, pz, lane, bias, uf, wvp, acc, h, ring, mask,
+                                               P == 2 ? net.wview6 : net.wview, st);
     // views_linears.0 with feature_linear fused in (W' = Wv_f Wf, see pack_net) on relu(h_last),
     // alpha_linear folded into its groups (same relu'd B operands), + the factorised
     // direction / code / bias part from G, then relu
     float sig = 0.0f;
     f32x16 av[RBV];
-    mlp_layer<RBV, RB, true, false, true>(av, acc, h, nullptr, net.wview, lane, ring, nullptr, bias + (M.D + 1) * W,
-                                          sig);
+    if constexpr (P == 2)
+        mlp_layer_x6<RBV, RB, false, true>(av, acc, h, nullptr, net.wview6, lane, ring, pre, nullptr,
+                                           bias + (M.D + 1) * W, sig);
+    else
+        mlp_layer<RBV, RB, true, false, true>(av, acc, h, nullptr, net.wview, lane, ring, nullptr,
+                                              bias + (M.D + 1) * W, sig);
     STAMP(st, 16);
     sig += __shfl_xor(sig, 32);
     sig += net.balpha;
@@ -693,11 +835,15 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
     if (mfma_count && lane == 0) {  // exact MFMA work of this block (wave-uniform quantities)
         const int act = __builtin_popcountll(mask.m0) + __builtin_popcountll(mask.m1);
         const int xk = 3 * M.njh2 + act * VPart<MR>::KB;  // k-steps of one x part
-        long long k = (long long)xk * RB + (long long)(W / 2) * RBV + (long long)(M.njh2 + 1) * RBV;
+        long long k = (long long)xk * RB + (long long)(M.njh2 + 1) * RBV;
+        if (P == 2)
+            atomicAdd(mfma_count + 1, (unsigned long long)(RBV * RB * 2 * 6));  // view layer, bf16x6
+        else
+            k += (long long)(W / 2) * RBV;
         if (M.skip + 1 < M.D) k += (long long)xk * RB;
         const long long hid = (long long)(M.D - 1) * RB * RB;  // 32x32 blocks of the hidden layers
-        if (P == 1) {
-            atomicAdd(mfma_count + 1, (unsigned long long)(hid * 2 * 3));  // 2 k16-steps x 3 per block
+        if (P != 0) {
+            atomicAdd(mfma_count + 1, (unsigned long long)(hid * 2 * 3 * P));  // 2 k16-steps x 3 (x6) per block
         } else {
             k += hid * 16;
         }

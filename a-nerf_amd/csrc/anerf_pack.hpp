@@ -124,6 +124,41 @@ std::vector<float> pack_layer_x3(const float* Wt, int n_out, int ld, int col_off
     });
 }
 
+// ---- bf16x6 split (ANERF_PREC_BF16X6): w = w0 + w1 + w2, each bf16 (RNE of the running remainder;
+// the remainders are exact in fp32), so w0 + w1 + w2 carries >= 24 significant bits of w.
+// Groups of 12 floats = fragments [w0, w1, w2] of (ob, ib, s) (element j as in pack_layer_x3).
+// Order: lead groups 2 ob + s (input block 0), then per input block ib >= 1, k-step s, block ob.
+std::vector<float> pack_layer_x6(const float* Wt, int n_out, int ld, int col_off, int n_in) {
+    const int RBO = n_out / 32, RBI = n_in / 32;
+    const int ng = 2 * RBO * RBI;
+    return pack_groups(ng, 12, [&](int g, int sl, int l) {
+        const int f = sl >> 2, e = sl & 3;  // fragment (split part), bf16 pair within it
+        int ob, ib, s;
+        if (g < 2 * RBO) {
+            ob = g >> 1, ib = 0, s = g & 1;
+        } else {
+            const int idx = g - 2 * RBO;
+            ib = 1 + idx / (2 * RBO), s = (idx / RBO) & 1, ob = idx % RBO;
+        }
+        const int h = l >> 5, row = 32 * ob + (l & 31);
+        uint32_t bits = 0;
+        for (int jj = 0; jj < 2; ++jj) {
+            const int j = 2 * e + jj;
+            const int col = col_off + 32 * ib + 16 * s + 8 * (j >> 2) + 4 * h + (j & 3);
+            float r = Wt[(size_t)row * ld + col];
+            uint16_t v = 0;
+            for (int p = 0; p <= f; ++p) {
+                v = bf16_rne(r);
+                r -= bf16_to_f(v);
+            }
+            bits |= (uint32_t)v << (16 * jj);
+        }
+        float out;
+        std::memcpy(&out, &bits, 4);
+        return out;
+    });
+}
+
 // bone-direction part: k-step q = 3p + c, half h -> joint p + h*njh2, column nv*nj + 3j + c;
 // groups of 2 k-steps x RB blocks (slot float 2 rb + t)
 std::vector<float> pack_upart(const float* Wt, int n_out, int ld, int nj, int njh2, int mr) {
@@ -322,6 +357,11 @@ static int pack_net(const anerf_model_desc* d, int njh2, const anerf_net_weights
         const bool sk = (i == d->skip + 1);
         offs.push_back(pk.add(pack_layer_x3(w->pts_w[i], W, sk ? cin + W : W, sk ? cin : 0, W)));
     }
+    for (int i = 1; i < d->net_depth; ++i) {                                          // bf16x6 hidden layers
+        const bool sk = (i == d->skip + 1);
+        offs.push_back(pk.add(pack_layer_x6(w->pts_w[i], W, sk ? cin + W : W, sk ? cin : 0, W)));
+    }
+    offs.push_back(pk.add(pack_layer_x6(wfused.data(), WH, W, 0, W)));               // wview6
     return ANERF_OK;
 }
 
@@ -349,6 +389,8 @@ static void bind_net(const anerf_model_desc* d, const float* base, const std::ve
     nd.brgb = base + o[k++];
     nd.codes = base + o[k++];
     for (int i = 1; i < D; ++i) nd.wl3[i] = base + o[k++];
+    for (int i = 1; i < D; ++i) nd.wl6[i] = base + o[k++];
+    nd.wview6 = base + o[k++];
     nd.balpha = balpha;
 }
 

@@ -194,7 +194,7 @@ int anerf_render_rays(const anerf_model* m, const float* ray_batch, int32_t ray_
     if (!m) return fail(ANERF_EINVAL, "model is NULL");
     if (n_rays < 0) return fail(ANERF_EINVAL, "n_rays < 0");
     if (n_rays == 0) return ANERF_OK;
-    if (precision != ANERF_PREC_FP32 && precision != ANERF_PREC_BF16X3) return fail(ANERF_EINVAL, "unsupported precision");
+    if (precision != ANERF_PREC_FP32 && precision != ANERF_PREC_BF16X3 && precision != ANERF_PREC_BF16X6) return fail(ANERF_EINVAL, "unsupported precision");
     if (!ray_batch || ray_stride < 8 || !skts || !cyls || n_poses < 1 || !rgb || !disp || !acc)
         return fail(ANERF_EINVAL, "anerf_render_rays: bad arguments");
     if (n_samples < 2 || n_samples > 1024 || n_importance < 0 || n_importance > 2048)
@@ -269,7 +269,8 @@ int anerf_render_rays(const anerf_model* m, const float* ray_batch, int32_t ray_
     const int mr = m->desc.multires;
 #define ANERF_LAUNCH(WW, MM)                                                                         \
     do {                                                                                            \
-        auto kfn = precision == ANERF_PREC_BF16X3 ? render_kernel<WW, MM, 1> : render_kernel<WW, MM, 0>; \
+        auto kfn = precision == ANERF_PREC_BF16X3 ? render_kernel<WW, MM, 1>                       \
+                 : precision == ANERF_PREC_BF16X6 ? render_kernel<WW, MM, 2> : render_kernel<WW, MM, 0>; \
         HIP_TRY(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,  \
                                     (int)lds_bytes));                                               \
         hipLaunchKernelGGL(kfn, dim3(grid), dim3(256), lds_bytes, st, m->md, a, P);                \

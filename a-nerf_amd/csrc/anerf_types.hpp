@@ -55,6 +55,8 @@ struct NetDev {
     const float* brgb;       // [3]
     const float* codes;      // [n_codes + 1][cfc]: last row = eval-mode mean code
     const float* wl3[MAXL];  // [i>0] activation parts as bf16x3 fragments (pack_layer_x3)
+    const float* wl6[MAXL];  // [i>0] activation parts as bf16x6 fragments (pack_layer_x6)
+    const float* wview6;     // wview as bf16x6 fragments
     float balpha;
 };
 

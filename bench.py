@@ -52,7 +52,7 @@ def parse():
     ap.add_argument("--importance", type=int, default=128)
     ap.add_argument("--cpu-rays", type=int, default=20000, help="rays in the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16x3"],
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16x6", "bf16x3"],
                     help="MLP arithmetic (include/anerf.h ANERF_PREC_*)")
     return ap.parse_args()
 

@@ -48,8 +48,13 @@ enum {
  *   ANERF_PREC_BF16X3 the dense hidden layers split as x = x_hi + x_lo (bf16, round to nearest even)
  *                     and computed as x_hi w_hi + x_hi w_lo + x_lo w_hi on v_mfma_f32_32x32x16_bf16
  *                     with fp32 accumulation (~16-bit operands, products exact): outputs within
- *                     1e-5 of the fp32 path on the reference fixtures; encoder and view parts fp32. */
-enum { ANERF_PREC_FP32 = 0, ANERF_PREC_BF16X3 = 1 };
+ *                     1e-5 of the fp32 path on the reference fixtures; encoder and view parts fp32;
+ *   ANERF_PREC_BF16X6 the dense hidden layers split three ways, x = x0 + x1 + x2 (bf16 RNE of the running
+ *                     remainder, >= 24 significant bits, like fp32) and computed as the six products
+ *                     with i + j <= 2 of x_i w_j on v_mfma_f32_32x32x16_bf16, fp32 accumulation: the
+ *                     dropped terms are below 2^-26 of each product, under fp32's own rounding of
+ *                     a product (2^-24), so the contraction is fp32-accurate; encoder and view parts fp32. */
+enum { ANERF_PREC_FP32 = 0, ANERF_PREC_BF16X3 = 1, ANERF_PREC_BF16X6 = 2 };
 
 typedef struct anerf_model anerf_model;
 

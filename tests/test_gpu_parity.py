@@ -343,6 +343,35 @@ def test_render_rays_bf16x3_matches_reference_golden(name):
             assert np.quantile(dd, 0.999) <= 2e-5, f"{name} {k}: bf16x3 vs fp32"
 
 
+@pytest.mark.parametrize("name", NAMES)
+def test_render_rays_bf16x6_matches_reference_golden(name):
+    """ANERF_PREC_BF16X6 (three-way split-bf16 hidden layers, fp32-accurate products) meets the 1e-4
+    bar against the reference and agrees with the fp32 path to fp32 summation-order level (99.9 % of
+    the composited outputs within 2e-6)."""
+    g = Golden(name)
+    cams = g["cams"] if g.has("cams") else None
+    out = _render(_caster_prec(g, "bf16x6"), g, g.ray_batch(), cams=cams)
+    out32 = _render(_caster(g), g, g.ray_batch(), cams=cams)
+    for k in ("rgb_map", "disp_map", "acc_map", "rgb0", "disp0", "acc0"):
+        if g.has("out_" + k):
+            d = _maxdiff(out[k], g["out_" + k])
+            assert d <= TOL, f"{name} {k}: max |gpu bf16x6 - reference| = {d:.3e}"
+            dd = np.abs(np.asarray(out[k], np.float64) - np.asarray(out32[k], np.float64)).ravel()
+            assert np.quantile(dd, 0.999) <= 2e-6, f"{name} {k}: bf16x6 vs fp32 {np.quantile(dd, 0.999):.3e}"
+
+
+def test_bf16x6_executes_bf16_mfmas():
+    g = Golden("c3_512_s64i128_d8w256")
+    rc = _caster_prec(g, "bf16x6")
+    _render(rc, g, g.ray_batch()[:64], count_mfma=True)
+    n_f32, n_bf16 = (int(v) for v in rc.last_mfma.tolist())
+    rc32 = _caster(g)
+    _render(rc32, g, g.ray_batch()[:64], count_mfma=True)
+    f32_only = int(rc32.last_mfma[0].item())
+    # each 32x32 block of a hidden layer: 16 f32 MFMAs (k = 2 each) -> 2 k16-steps x 6 bf16 MFMAs
+    assert n_bf16 > 0 and (f32_only - n_f32) * 12 == n_bf16 * 16
+
+
 def test_bf16x3_executes_bf16_mfmas():
     g = Golden("c3_512_s64i128_d8w256")
     rc = _caster_prec(g, "bf16x3")

@@ -37,6 +37,25 @@ def lin_bf16x3(x, w, b=None):
     return y if b is None else y + b
 
 
+def _split3(x):
+    p0 = x.to(torch.bfloat16).float()
+    r = x - p0
+    p1 = r.to(torch.bfloat16).float()
+    p2 = (r - p1).to(torch.bfloat16).float()
+    return p0, p1, p2
+
+
+def lin_bf16x6(x, w, b=None):
+    xs, ws = _split3(x), _split3(w)
+    y = None
+    for i in range(3):
+        for j in range(3 - i):
+            t = _lin(xs[i].double(), ws[j].double())
+            y = t if y is None else y + t
+    y = y.float()
+    return y if b is None else y + b
+
+
 def lin_bf16(x, w, b=None):
     y = _lin(x.to(torch.bfloat16).double(), w.to(torch.bfloat16).double()).float()
     return y if b is None else y + b
@@ -50,7 +69,7 @@ def run(name, mode, mods, tmp):
     sc["cyls"] = z["cyls"]
     o, d = torch.from_numpy(z["rays_o"]), torch.from_numpy(z["rays_d"])
     cams = z["cams"] if "cams" in z.files else None
-    F.linear = {"bf16x3": lin_bf16x3, "bf16": lin_bf16, "fp32": _lin}[mode]
+    F.linear = {"bf16x6": lin_bf16x6, "bf16x3": lin_bf16x3, "bf16": lin_bf16, "fp32": _lin}[mode]
     torch.nn.modules.linear.F.linear = F.linear
     try:
         ret = mg.render_subset(mods, kw, o, d, sc, cams=cams)
@@ -70,7 +89,7 @@ def main():
     mods = mg.import_reference()
     with tempfile.TemporaryDirectory() as tmp:
         for n in names:
-            for mode in ("fp32", "bf16x3", "bf16"):
+            for mode in ("fp32", "bf16x6", "bf16x3", "bf16"):
                 print(n, mode, run(n, mode, mods, tmp), flush=True)
 
 
