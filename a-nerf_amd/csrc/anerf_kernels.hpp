@@ -142,7 +142,7 @@ __host__ __device__ inline LdsPlan make_density_plan(int nj, int W, int D, int n
     return p;
 }
 
-template <int W, int MR>
+template <int W, int MR, int PREC>
 __global__ __launch_bounds__(256, 1) void density_kernel(ModelDev M, DensityArgs A, LdsPlan P) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     constexpr int RB = W / 32;
@@ -171,7 +171,7 @@ __global__ __launch_bounds__(256, 1) void density_kernel(ModelDev M, DensityArgs
         f32x16 acc[RB], h[RB];
         JointMask mask;
         Ring ring;
-        mlp_trunk<W, MR, false, 0>(M, net, lds + P.sk, lds + P.cut, px, py, pz, lane, lds + P.bias, uf, nullptr, acc, h, ring,
+        mlp_trunk<W, MR, false, PREC>(M, net, lds + P.sk, lds + P.cut, px, py, pz, lane, lds + P.bias, uf, nullptr, acc, h, ring,
                          mask, nullptr, st);
         // alpha_linear on relu(h_last), in the k-step order of the render path's fused alpha head
         float sig = 0.0f;

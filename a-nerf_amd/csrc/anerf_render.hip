@@ -363,7 +363,9 @@ int anerf_encode_points(const anerf_model* m, const float* skts, const float* pt
     return ANERF_OK;
 }
 
-static int launch_density(const anerf_model* m, DensityArgs a, void* stream) {
+static int launch_density(const anerf_model* m, DensityArgs a, int32_t precision, void* stream) {
+    if (precision != ANERF_PREC_FP32 && precision != ANERF_PREC_BF16X3 && precision != ANERF_PREC_BF16X6)
+        return fail(ANERF_EINVAL, "unsupported precision");
     if (a.n == 0) return ANERF_OK;
     int dev = -1;
     HIP_TRY(hipGetDevice(&dev));
@@ -379,7 +381,8 @@ static int launch_density(const anerf_model* m, DensityArgs a, void* stream) {
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
 #define ANERF_LAUNCH(WW, MM)                                                                         \
     do {                                                                                            \
-        auto kfn = density_kernel<WW, MM>;                                                          \
+        auto kfn = precision == ANERF_PREC_BF16X3 ? density_kernel<WW, MM, 1>                      \
+                 : precision == ANERF_PREC_BF16X6 ? density_kernel<WW, MM, 2> : density_kernel<WW, MM, 0>; \
         HIP_TRY(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,  \
                                     (int)lds_bytes));                                               \
         hipLaunchKernelGGL(kfn, dim3(grid), dim3(256), lds_bytes, st, m->md, a, P);                \
@@ -397,7 +400,7 @@ static int launch_density(const anerf_model* m, DensityArgs a, void* stream) {
 }
 
 int anerf_density_points(const anerf_model* m, const float* pts, int64_t n_points, const float* skts, int32_t net,
-                         float* raw_out, void* stream) {
+                         int32_t precision, float* raw_out, void* stream) {
     if (!m || n_points < 0) return fail(ANERF_EINVAL, "anerf_density_points: bad arguments");
     if (n_points == 0) return ANERF_OK;
     if (!pts || !skts || !raw_out) return fail(ANERF_EINVAL, "anerf_density_points: bad arguments");
@@ -408,11 +411,11 @@ int anerf_density_points(const anerf_model* m, const float* pts, int64_t n_point
     a.skts = skts;
     a.net = net;
     a.out = raw_out;
-    return launch_density(m, a, stream);
+    return launch_density(m, a, precision, stream);
 }
 
 int anerf_density_grid(const anerf_model* m, const float* axis, int32_t res1, const float* kp0, const float* skts,
-                       int32_t net, float* raw_out, void* stream) {
+                       int32_t net, int32_t precision, float* raw_out, void* stream) {
     if (!m || !axis || !kp0 || !skts || !raw_out || res1 < 1) return fail(ANERF_EINVAL, "anerf_density_grid: bad arguments");
     DensityArgs a;
     std::memset(&a, 0, sizeof(a));
@@ -423,7 +426,7 @@ int anerf_density_grid(const anerf_model* m, const float* axis, int32_t res1, co
     a.skts = skts;
     a.net = net;
     a.out = raw_out;
-    return launch_density(m, a, stream);
+    return launch_density(m, a, precision, stream);
 }
 
 int anerf_pose_kinematics(const float* bones, int32_t rot_dim, const float* rest, const int32_t* rest_idx,

@@ -112,8 +112,8 @@ class RayCaster:
         sk = self._one_pose(skts, dev)
         out = torch.empty(p.shape[0], device=dev, dtype=torch.float32)
         _lib.check(_lib.load().anerf_density_points(self.model.handle, _lib.ptr(p), p.shape[0], _lib.ptr(sk),
-                                                    self._net_index(network), _lib.ptr(out),
-                                                    _lib.stream_handle(dev)), "anerf_density_points")
+                                                    self._net_index(network), _lib.PRECISIONS[self.cfg.precision],
+                                                    _lib.ptr(out), _lib.stream_handle(dev)), "anerf_density_points")
         return out.reshape(*shape, 1)
 
     @torch.no_grad()
@@ -130,7 +130,8 @@ class RayCaster:
         sk = self._one_pose(skts, dev)
         out = torch.empty((res1, res1, res1), device=dev, dtype=torch.float32)
         _lib.check(_lib.load().anerf_density_grid(self.model.handle, _lib.ptr(axis), res1, _lib.ptr(kp0),
-                                                  _lib.ptr(sk), self._net_index(network), _lib.ptr(out),
+                                                  _lib.ptr(sk), self._net_index(network),
+                                                  _lib.PRECISIONS[self.cfg.precision], _lib.ptr(out),
                                                   _lib.stream_handle(dev)), "anerf_density_grid")
         return out
 

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define ANERF_ABI_VERSION 1
+#define ANERF_ABI_VERSION 2
 
 enum {
     ANERF_OK = 0,
@@ -181,15 +181,15 @@ int anerf_encode_points(const anerf_model* m, const float* skts, const float* pt
 
 /* Raw density (alpha_linear output, before the density activation) of the trunk of one network at
  * points pts [n][3] in world space, one pose skts [NJ][4][4]: _get_density_fwd_fn's fwd_fn.
- * net: 0 coarse, 1 fine, -1 the reference's default (fine if the model has one). */
+ * net: 0 coarse, 1 fine, -1 the reference's default (fine if the model has one); precision ANERF_PREC_*. */
 int anerf_density_points(const anerf_model* m, const float* pts, int64_t n_points, const float* skts, int32_t net,
-                         float* raw_out, void* stream);
+                         int32_t precision, float* raw_out, void* stream);
 
 /* The same on render_mesh_density's grid, generated on the device: raw_out [res1][res1][res1],
  * element (a, b, c) at (axis[b], axis[a], axis[c]) + kp0 (numpy 'xy' meshgrid order), where
  * axis [res1] = float32(linspace(-radius, radius, res1)) and kp0 [3] = kps[0, 0]. */
 int anerf_density_grid(const anerf_model* m, const float* axis, int32_t res1, const float* kp0, const float* skts,
-                       int32_t net, float* raw_out, void* stream);
+                       int32_t net, int32_t precision, float* raw_out, void* stream);
 
 /* Pose -> skeleton transforms for n_frames frames, replacing
  *   PoseOptLayer.calculate_kinematic  core/pose_opt.py:372-445 (+ unrolled_kinematic_chain :482-521),

@@ -268,6 +268,25 @@ def test_density_matches_oracle_both_nets_and_ragged():
     assert empty.shape == (0, 1)
 
 
+@pytest.mark.parametrize("precision", ["bf16x6", "bf16x3"])
+def test_density_split_precisions(precision):
+    """Density queries in the split-bf16 modes: the reference goldens within 1e-4 and the fp32 path
+    within 2e-6 (bf16x6, fp32-accurate products) / 5e-5 (bf16x3) on the config-3 fine net."""
+    import dataclasses
+    g = Golden("dm_fine_d8w256")
+    rc = anerf.RayCaster(dataclasses.replace(g.cfg, precision=precision), g.ckpt)
+    rc32 = _caster(g)
+    pts = torch.from_numpy(g["pts"]).reshape(-1, 1, 3)
+    args = (pts, torch.from_numpy(g["kps"]), torch.from_numpy(g["skts"]), torch.from_numpy(g["bones"]))
+    out = rc(*args, render_kwargs={}, fwd_type="density").cpu().numpy()
+    out32 = rc32(*args, render_kwargs={}, fwd_type="density").cpu().numpy()
+    assert _maxdiff(out, g["pts_density"]) <= TOL_DENSITY
+    assert _maxdiff(out, out32) <= (2e-6 if precision == "bf16x6" else 5e-5)
+    grid = rc(kps=torch.from_numpy(g["kps"]), skts=torch.from_numpy(g["skts"]), bones=torch.from_numpy(g["bones"]),
+              radius=g.meta["radius"], res=g.meta["res"], render_kwargs={}, netchunk=1024, fwd_type="mesh")
+    assert _maxdiff(grid.cpu().numpy(), g["grid_density"]) <= TOL_DENSITY
+
+
 def test_density_grid_equals_points_path():
     """The device-generated grid is the reference's numpy grid: grid and explicit points agree bit-exactly."""
     orc = _oracle()

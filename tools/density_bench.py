@@ -28,7 +28,8 @@ def trunk_flops(cfg):
 
 def main():
     res = int(sys.argv[1]) if len(sys.argv) > 1 else 255
-    cfg = anerf.RenderConfig(N_samples=64, N_importance=128).validate()
+    prec = sys.argv[2] if len(sys.argv) > 2 else "fp32"
+    cfg = anerf.RenderConfig(N_samples=64, N_importance=128, precision=prec).validate()
     ck = syn.make_checkpoint(13, n_joints=24, D=8, W=256, fine=True, tau=79.6)
     sc = syn.make_scene(n_joints=24, H=512, W=512, seed=13)
     rc = anerf.RayCaster(cfg, ck)
@@ -47,7 +48,7 @@ def main():
     n = (res + 1) ** 3
     fl = trunk_flops(cfg)
     print(json.dumps({"metric": "density grid points/s (fwd_type='mesh', res=%d, config3 fine net)" % res,
-                      "value": round(n / (ms * 1e-3), 1), "unit": "points/s", "points": n, "ms": round(ms, 3),
+                      "value": round(n / (ms * 1e-3), 1), "unit": "points/s", "precision": prec, "points": n, "ms": round(ms, 3),
                       "dense_trunk_flop_per_point": fl,
                       "dense_equivalent_tflops": round(fl * n / (ms * 1e-3) / 1e12, 2),
                       "frac_of_fp32_mfma_peak": round(fl * n / (ms * 1e-3) / 1e12 / 157.3, 4),

@@ -21,9 +21,11 @@ grep -E "passed|failed|FAILED|Error" gpurun_out/pytest_gpu.log | tail -15
 echo "== bench (default, with CPU baseline)"
 timeout -k 10 300 python bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/bench.err || { tail -20 gpurun_out/bench.err; exit 1; }
 cat gpurun_out/${TAG}_bench.json
-echo "== density"
-timeout -k 10 300 python tools/density_bench.py > gpurun_out/${TAG}_density.json 2> gpurun_out/density.err || { tail -20 gpurun_out/density.err; exit 1; }
-cat gpurun_out/${TAG}_density.json
+for p in fp32 bf16x6; do
+  echo "== density $p"
+  timeout -k 10 300 python tools/density_bench.py 255 $p > gpurun_out/${TAG}_density_$p.json 2> gpurun_out/density.err || { tail -20 gpurun_out/density.err; exit 1; }
+  cat gpurun_out/${TAG}_density_$p.json
+done
 echo "== rocprof"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o run --output-format csv -- python3 bench.py --steps 4 --warmup 1 --no-cpu > gpurun_out/prof.log 2>&1 || { echo "rocprof failed"; tail -20 gpurun_out/prof.log; exit 1; }
 find gpurun_out/prof_${TAG} -name "*stats*"
