@@ -39,13 +39,18 @@ __global__ __launch_bounds__(256, 1) void render_kernel(ModelDev M, RenderArgs A
         const float nearv = lds[P.ray + 16 * r + 7], farv = lds[P.ray + 16 * r + 8];
         lds[P.zc + P.z_stride * r + s] = nearv * (1.0f - t) + farv * t;
     }
+    if (A.pass0 == 1)  // fine-only launch: the sorted fine z of the coarse launch
+        for (int idx = tid; idx < nr * T; idx += blockDim.x) {
+            const int r = idx / T, s = idx % T;
+            lds[P.zf + P.z_stride * r + s] = A.zf_ws[(ray0 + r) * T + s];
+        }
     __syncthreads();
 
     Stamps st;
     STAMP_INIT(st);
     STAMP(st, 0);
     const int n_pass = I > 0 ? 2 : 1;
-    for (int pass = 0; pass < n_pass; ++pass) {
+    for (int pass = A.pass0; pass < min(A.pass1, n_pass); ++pass) {
         const NetDev& net = M.net[pass];
         const int n = pass == 0 ? S : T;
         const int zoff = pass == 0 ? P.zc : P.zf;
@@ -110,6 +115,11 @@ __global__ __launch_bounds__(256, 1) void render_kernel(ModelDev M, RenderArgs A
         __syncthreads();
         STAMP(st, 3 + 2 * pass);
     }
+    if (I > 0 && A.pass1 == 1)  // coarse-only launch: hand the fine z over
+        for (int idx = tid; idx < nr * T; idx += blockDim.x) {
+            const int r = idx / T, s = idx % T;
+            A.zf_ws[(ray0 + r) * T + s] = lds[P.zf + P.z_stride * r + s];
+        }
     STAMP_FLUSH(st, A.stamps);
 }
 

@@ -222,40 +222,58 @@ __device__ __forceinline__ void mlp_layer_x3(f32x16 (&out)[RBO], f32x16 (&ain)[R
     }
 }
 
-// ---- bf16x6 form (ANERF_PREC_BF16X6): x = x0 + x1 + x2 and w = w0 + w1 + w2 (bf16 RNE of the
-// running remainder; x - x0 and x - x0 - x1 are exact in f32), product ~= sum over i + j <= 2 of
-// x_i w_j: six v_mfma_f32_32x32x16_bf16 per 16 k, the dropped terms below 2^-26 of the product.
-// The activations stay f32 (relu'd) in h[]; one input block (16 values = 2 k16-steps) is split
-// into T (2 x 3 fragments) while the previous block's MFMAs run.  Weight groups are 12 floats
-// (fragments w0, w1, w2 of one (ob, ib, s)), prefetched 3 groups ahead in the 4-slot ring.
-struct X6Frag {
-    bf16x8 p[3];
+// ---- bf16x6 form (ANERF_PREC_BF16X6): x = x0 + x1 + x2 and w = w0 + w1 + w2, product ~= the six
+// x_i w_j with i + j <= 2: six v_mfma_f32_32x32x16_bf16 per 16 k.  Weights are split on the host
+// (bf16 RNE of the running remainder).  Activations are split here by TRUNCATION, with integer
+// masks: x0 = x & 0xffff0000, r = x - x0 (exact), x1 = r & 0xffff0000, x2 = r - x1 (exact, <= 8
+// significant bits, so it is a bf16), i.e. x = x0 + x1 + x2 exactly; the dropped x1 w2 + x2 w1 +
+// x2 w2 are below 2^-23 of |x w| (fp32 product rounding is 2^-24).  Packing two values per dword is
+// one v_perm_b32 per component.
+// The activations stay f32 (relu'd) in h[]; the split of input block ib + 1 (8 value pairs ->
+// T[2] = 2 k16-steps x 3 components x 4 dwords) is spread one pair at a time over the groups of
+// block ib, so the VALU work sits in the MFMA gaps (a v_mfma_f32_32x32x16_bf16 hides ~5 single-issue
+// VALU instructions, MI355X_MICROARCH.md), and so are the relu / bias conversions of the lead
+// groups.  Weight groups are 12 floats (fragments w0, w1, w2 of one (ob, ib, s)), prefetched 3
+// groups ahead in the 4-slot ring.
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+struct X6T {
+    unsigned d[3][4];
+    __device__ __forceinline__ bf16x8 frag(int c) const {
+        return __builtin_bit_cast(bf16x8, u32x4{d[c][0], d[c][1], d[c][2], d[c][3]});
+    }
 };
 
-__device__ __forceinline__ X6Frag split3(const f32x16& a, int s) {
-    X6Frag t;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const float x = a[8 * s + j];
-        const __bf16 b0 = (__bf16)x;
-        const float r1 = x - (float)b0;
-        const __bf16 b1 = (__bf16)r1;
-        const float r2 = r1 - (float)b1;
-        t.p[0][j] = b0;
-        t.p[1][j] = b1;
-        t.p[2][j] = (__bf16)r2;
-    }
-    return t;
+// values a, b -> dword q of the three components (a in the low half: element 2q of the fragment)
+__device__ __forceinline__ void split3_pair(float a, float b, X6T& t, int q) {
+    const unsigned ua = __builtin_bit_cast(unsigned, a), ub = __builtin_bit_cast(unsigned, b);
+    const float ra = a - __builtin_bit_cast(float, ua & 0xffff0000u);
+    const float rb = b - __builtin_bit_cast(float, ub & 0xffff0000u);
+    const unsigned ura = __builtin_bit_cast(unsigned, ra), urb = __builtin_bit_cast(unsigned, rb);
+    const float qa = ra - __builtin_bit_cast(float, ura & 0xffff0000u);
+    const float qb = rb - __builtin_bit_cast(float, urb & 0xffff0000u);
+    t.d[0][q] = __builtin_amdgcn_perm(ub, ua, 0x07060302u);
+    t.d[1][q] = __builtin_amdgcn_perm(urb, ura, 0x07060302u);
+    t.d[2][q] = __builtin_amdgcn_perm(__builtin_bit_cast(unsigned, qb), __builtin_bit_cast(unsigned, qa), 0x07060302u);
 }
 
-__device__ __forceinline__ f32x16 mfma_x6(const float (&w)[16], const X6Frag& x, f32x16 c) {
+// value pair p (0..7) of a 16-value input block: k16-step p >> 2, dword p & 3
+__device__ __forceinline__ void split3_block_pair(const f32x16& hb, X6T (&t)[2], int p) {
+    const int s = p >> 2, q = p & 3;
+#if ANERF_X6_PROBE == 2  // (diagnostic builds of tools/probe only: no split arithmetic)
+    t[s].d[0][q] = t[s].d[1][q] = t[s].d[2][q] = __builtin_bit_cast(unsigned, hb[8 * s + 2 * q]);
+    return;
+#endif
+    split3_pair(hb[8 * s + 2 * q], hb[8 * s + 2 * q + 1], t[s], q);
+}
+
+__device__ __forceinline__ f32x16 mfma_x6(const float (&w)[16], const X6T& x, f32x16 c) {
     const bf16x8 w0 = frag_of(w, 0), w1 = frag_of(w, 1), w2 = frag_of(w, 2);
-    c = mfma_bf16_32x32x16(w2, x.p[0], c);  // small terms first
-    c = mfma_bf16_32x32x16(w1, x.p[1], c);
-    c = mfma_bf16_32x32x16(w0, x.p[2], c);
-    c = mfma_bf16_32x32x16(w1, x.p[0], c);
-    c = mfma_bf16_32x32x16(w0, x.p[1], c);
-    return mfma_bf16_32x32x16(w0, x.p[0], c);
+    c = mfma_bf16_32x32x16(w2, x.frag(0), c);  // small terms first
+    c = mfma_bf16_32x32x16(w1, x.frag(1), c);
+    c = mfma_bf16_32x32x16(w0, x.frag(2), c);
+    c = mfma_bf16_32x32x16(w1, x.frag(0), c);
+    c = mfma_bf16_32x32x16(w0, x.frag(1), c);
+    return mfma_bf16_32x32x16(w0, x.frag(0), c);
 }
 
 // OUT_SAME: out aliases ain (hidden layers: out[rb] = bias once ain[rb] is consumed); otherwise out
@@ -268,17 +286,21 @@ __device__ __forceinline__ void mlp_layer_x6(f32x16 (&out)[RBO], f32x16 (&ain)[R
     static_assert(RBO <= RBI, "x6 layer shape");
     constexpr int NG = 2 * RBO * RBI;
     constexpr int PD = 3;  // prefetch distance (groups)
+    constexpr int NQ = 2 * RBO;  // groups per input block
     const int hh = lane >> 5;
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(wp);
     const __amdgpu_buffer_rsrc_t rn = make_rsrc(next);
-    auto convert = [&](int rb) {
+    auto convert_half = [&](int rb, int half) {  // relu of 8 inputs (+ their 8 bias outputs)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) h[rb][i] = relu_act(ain[rb][i]);
+        for (int i = 8 * half; i < 8 * half + 8; ++i) h[rb][i] = relu_act(ain[rb][i]);
         if (OUT_SAME && rb < RBO) {
-            const f32x4* p = reinterpret_cast<const f32x4*>(bias + (rb * 2 + hh) * 16);
-            const f32x4 v0 = p[0], v1 = p[1], v2 = p[2], v3 = p[3];
-            out[rb] = f32x16{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3],
-                             v2[0], v2[1], v2[2], v2[3], v3[0], v3[1], v3[2], v3[3]};
+            const f32x4* p = reinterpret_cast<const f32x4*>(bias + (rb * 2 + hh) * 16 + 8 * half);
+            const f32x4 v0 = p[0], v1 = p[1];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                out[rb][8 * half + e] = v0[e];
+                out[rb][8 * half + 4 + e] = v1[e];
+            }
         }
     };
     auto alpha = [&](int ib, int s) {  // k = 16 ib + 8 s + j, the order of mlp_layer's fold
@@ -294,52 +316,67 @@ __device__ __forceinline__ void mlp_layer_x6(f32x16 (&out)[RBO], f32x16 (&ain)[R
         for (int rb = 0; rb < RBO; ++rb) out[rb] = f32x16{0};
     }
     auto prefetch = [&](int g) {  // group g + PD of this layer, or the next x6 layer's first groups
+#if ANERF_X6_PROBE == 1  // (diagnostic builds of tools/probe only: no weight loads)
+        return;
+#elif ANERF_X6_PROBE == 3  // (diagnostic: loads from a 4-group, L1-resident footprint)
+        load_group<12>(ring.v[(g + PD) % 4], rs, lane, (g + PD) % 4);
+        return;
+#endif
         if (g + PD < NG)
             load_group<12>(ring.v[(g + PD) % 4], rs, lane, g + PD);
         else if (NG % 4 == 0 && next)
             load_group<12>(ring.v[(g + PD) % 4], rn, lane, g + PD - NG);
     };
+    // group (of the NQ - q0 groups from q0 on) that splits pair p of the next block
+    auto pair_group = [](int p, int q0) { return q0 + (p * (NQ - q0 > 0 ? NQ - q0 : 1)) / 8; };
     if (!preloaded) {
 #pragma unroll
         for (int g = 0; g < PD; ++g) load_group<12>(ring.v[g], rs, lane, g);
     }
-    convert(0);
-    X6Frag T[2] = {split3(h[0], 0), split3(h[0], 1)};
+    convert_half(0, 0);
+    convert_half(0, 1);
+    X6T T[2], Tn[2];
+#pragma unroll
+    for (int p = 0; p < 8; ++p) split3_block_pair(h[0], T, p);
+    // lead groups: output block g/2, input block 0, k16-step g&1; block ob + 1 is converted (a half
+    // per group) under the MFMAs of block ob; block 1's split follows from group 2 on
+    constexpr int QL = NQ > 2 ? 2 : NQ;  // first lead group that may split block 1
 #pragma clang loop unroll(full)
-    for (int g = 0; g < 2 * RBO; ++g) {  // lead groups: output block g/2, input block 0, k16-step g&1
+    for (int g = 0; g < NQ; ++g) {
         __builtin_amdgcn_sched_barrier(0);
         prefetch(g);
         const int ob = g >> 1, s = g & 1;
         out[ob] = mfma_x6(ring.v[g % 4], T[s], out[ob]);
         if (ob == 0) alpha(0, s);
-        if (s == 1) {
-            if (ob + 1 < RBO) {
-                convert(ob + 1);
-            } else {
-#pragma clang loop unroll(full)
-                for (int rb = RBO; rb < RBI; ++rb) convert(rb);
-            }
+        if (ob + 1 < RBI && (ob + 1 < RBO || ob == 0)) convert_half(ob + 1, s);
+        if (RBI > 1) {
+#pragma unroll
+            for (int p = 0; p < 8; ++p)
+                if (pair_group(p, QL) == (g < QL ? -1 : g) || (g == NQ - 1 && pair_group(p, QL) > g))
+                    split3_block_pair(h[1], Tn, p);
         }
     }
-    X6Frag Tn[2];
-    if (RBI > 1) Tn[0] = split3(h[1], 0), Tn[1] = split3(h[1], 1);
 #pragma clang loop unroll(full)
     for (int ib = 1; ib < RBI; ++ib) {
         T[0] = Tn[0];
         T[1] = Tn[1];
+        // blocks >= max(RBO, 2) are converted under the first two groups of the block before them
+        const bool conv_next = ib + 1 < RBI && ib + 1 >= (RBO > 2 ? RBO : 2);
+        const int q0 = conv_next ? (NQ > 2 ? 2 : NQ) : 0;
 #pragma clang loop unroll(full)
-        for (int s = 0; s < 2; ++s) {
-#pragma clang loop unroll(full)
-            for (int ob = 0; ob < RBO; ++ob) {
-                const int g = 2 * RBO + (ib - 1) * 2 * RBO + s * RBO + ob;
-                __builtin_amdgcn_sched_barrier(0);
-                prefetch(g);
-                out[ob] = mfma_x6(ring.v[g % 4], T[s], out[ob]);
-                if (ib + 1 < RBI) {  // the next input block's split under these MFMAs
-                    if (RBO >= 2 && s == 0 && ob < 2) Tn[ob] = split3(h[ib + 1], ob);
-                    if (RBO == 1) Tn[s] = split3(h[ib + 1], s);
-                }
-                if (ob == RBO - 1) alpha(ib, s);
+        for (int q = 0; q < NQ; ++q) {
+            const int s = q / RBO, ob = q % RBO;
+            const int g = NQ + (ib - 1) * NQ + q;
+            __builtin_amdgcn_sched_barrier(0);
+            prefetch(g);
+            out[ob] = mfma_x6(ring.v[g % 4], T[s], out[ob]);
+            if (ob == RBO - 1) alpha(ib, s);
+            if (ib + 1 < RBI) {
+                if (conv_next && q < 2) convert_half(ib + 1, q);
+#pragma unroll
+                for (int p = 0; p < 8; ++p)
+                    if (pair_group(p, q0) == q || (q == NQ - 1 && pair_group(p, q0) > q))
+                        split3_block_pair(h[ib + 1], Tn, p);
             }
         }
     }

@@ -31,6 +31,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -145,9 +146,15 @@ static size_t ws_near_far_bytes(int64_t n) {
     return 3 * al(sizeof(float) * (size_t)n) + al((size_t)n);
 }
 
+// the coarse -> fine hand-off of the two-launch schedule (anerf_render_rays): n x T floats
+static size_t ws_zf_bytes(int64_t n, int32_t n_samples, int32_t n_importance) {
+    return n_importance > 0 ? (((size_t)n * (size_t)(n_samples + n_importance) * 4 + 255) & ~(size_t)255) : 0;
+}
+
 size_t anerf_workspace_size(const anerf_model* m, int64_t n_rays, int32_t n_samples, int32_t n_importance) {
-    (void)m; (void)n_samples; (void)n_importance;
-    return ws_near_far_bytes(n_rays > 0 ? n_rays : 1);
+    (void)m;
+    const int64_t n = n_rays > 0 ? n_rays : 1;
+    return ws_near_far_bytes(n) + ws_zf_bytes(n, n_samples, n_importance);
 }
 
 static int launch_near_far(const float* rb, int stride, int64_t n, const float* cyls, const int32_t* ray_pose,
@@ -183,6 +190,15 @@ int anerf_near_far(const float* ray_batch, int32_t ray_stride, int64_t n_rays, c
     HIP_TRY(hipMemcpyAsync(near_out, np_, sizeof(float) * n_rays, hipMemcpyDeviceToDevice, st));
     HIP_TRY(hipMemcpyAsync(far_out, fp_, sizeof(float) * n_rays, hipMemcpyDeviceToDevice, st));
     return ANERF_OK;
+}
+
+// ANERF_FUSED_PASSES=1: both passes in one launch (the earlier schedule; A/B measurements only)
+static bool fused_passes() {
+    static const bool v = [] {
+        const char* e = std::getenv("ANERF_FUSED_PASSES");
+        return e && e[0] == '1';
+    }();
+    return v;
 }
 
 int anerf_render_rays(const anerf_model* m, const float* ray_batch, int32_t ray_stride, int64_t n_rays,
@@ -264,6 +280,11 @@ int anerf_render_rays(const anerf_model* m, const float* ray_batch, int32_t ray_
 #ifdef ANERF_STAMPS
     a.stamps = g_stamps;
 #endif
+    // With importance sampling the coarse and the fine pass run as two launches: every CU then
+    // streams one network's weights at a time, which fit an XCD's 4 MB L2 (both together do not);
+    // the fine z lists (T floats per ray) go through the workspace.
+    const int pstep = (I > 0 && !fused_passes()) ? 1 : 2;
+    a.zf_ws = I > 0 ? reinterpret_cast<float*>((char*)workspace + ws_near_far_bytes(n_rays)) : nullptr;
     const unsigned grid = (unsigned)((n_rays + R - 1) / R);
     const size_t lds_bytes = (size_t)P.total * 4;
     const int mr = m->desc.multires;
@@ -273,7 +294,11 @@ int anerf_render_rays(const anerf_model* m, const float* ray_batch, int32_t ray_
                  : precision == ANERF_PREC_BF16X6 ? render_kernel<WW, MM, 2> : render_kernel<WW, MM, 0>; \
         HIP_TRY(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,  \
                                     (int)lds_bytes));                                               \
-        hipLaunchKernelGGL(kfn, dim3(grid), dim3(256), lds_bytes, st, m->md, a, P);                \
+        for (int p0 = 0; p0 < 2; p0 += pstep) {                                                     \
+            a.pass0 = p0;                                                                           \
+            a.pass1 = p0 + pstep;                                                                   \
+            hipLaunchKernelGGL(kfn, dim3(grid), dim3(256), lds_bytes, st, m->md, a, P);            \
+        }                                                                                           \
     } while (0)
     if (W == 256 && mr == 7) ANERF_LAUNCH(256, 7);
     else if (W == 128 && mr == 7) ANERF_LAUNCH(128, 7);

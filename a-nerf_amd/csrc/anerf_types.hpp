@@ -82,6 +82,8 @@ struct RenderArgs {
     float *dbg_z0, *dbg_raw0, *dbg_w0, *dbg_z1, *dbg_raw1;
     unsigned long long* mfma_count;
     unsigned long long* stamps;
+    int pass0, pass1;  // passes [pass0, pass1) of this launch (0 coarse, 1 fine)
+    float* zf_ws;      // n x T: the fine pass's sorted z, handed from the coarse launch to the fine one
 };
 
 // ======================================================================= LDS plan

@@ -37,6 +37,13 @@ sys.path.insert(0, REPO)
 BASELINE = json.load(open(os.path.join(REPO, "BASELINE.json")))
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md, FP32 matrix (1024 SIMDs x 64 FLOP/clk x 2.4 GHz)
 BF16_MFMA_PEAK_TFLOPS = 2516.6  # MI355X_MICROARCH.md, BF16 dense (1024 SIMDs x 1024 FLOP/clk x 2.4 GHz)
+DTYPE = {
+    "fp32": "fp32",
+    "bf16x6": "fp32-accurate split bf16 (hidden + view layers: x = x0+x1+x2, W = W0+W1+W2, six bf16 MFMA "
+              "products per term, fp32 accumulate; encoder, layer 0, compositing fp32)",
+    "bf16x3": "split bf16 (hidden layers: x = hi+lo, W = hi+lo, three bf16 MFMA products, fp32 accumulate; "
+              "fp32 elsewhere)",
+}
 FLOP_F32_MFMA = 32 * 32 * 2 * 2     # v_mfma_f32_32x32x2_f32
 FLOP_BF16_MFMA = 32 * 32 * 16 * 2   # v_mfma_f32_32x32x16_bf16
 
@@ -52,21 +59,22 @@ def parse():
     ap.add_argument("--importance", type=int, default=128)
     ap.add_argument("--cpu-rays", type=int, default=20000, help="rays in the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16x6", "bf16x3"],
+    ap.add_argument("--precision", default="bf16x6", choices=["fp32", "bf16x6", "bf16x3"],
                     help="MLP arithmetic (include/anerf.h ANERF_PREC_*)")
     return ap.parse_args()
 
 
-def traffic_from_profiles():
-    """Per-launch HBM bytes of render_kernel from the committed rocprofv3 --pmc summary, if any."""
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")))
-    if not files:
-        return None
-    try:
-        d = json.load(open(files[-1]))
-        return d.get("render_kernel_hbm_bytes_per_launch")
-    except Exception:
-        return None
+def traffic_from_profiles(precision):
+    """Per-launch HBM bytes of render_kernel from the newest committed rocprofv3 --pmc summary of
+    this precision mode (profiles/*pmc*.json, field "precision"; untagged files are fp32)."""
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        if d.get("precision", "fp32") == precision and "render_kernel_hbm_bytes_per_launch" in d:
+            return d["render_kernel_hbm_bytes_per_launch"]
+    return None
 
 
 def main():
@@ -157,7 +165,7 @@ def main():
     flop_ray = anerf.flops_per_sample(cfg) * anerf.samples_per_ray(cfg)  # SURVEY §8(d), reference work
     achieved_tf = flop_exec / (kern_ms * 1e-3) / 1e12
     ref_equiv_tf = flop_ray * n / (kern_ms * 1e-3) / 1e12
-    traffic = traffic_from_profiles()
+    traffic = traffic_from_profiles(a.precision)
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
@@ -180,7 +188,7 @@ def main():
             "metric": BASELINE["metric"], "value": round(value, 1), "unit": "rays/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(1e3 * elapsed / a.steps, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "fp32" if a.precision == "fp32" else "bf16x3 (split-fp32 hidden layers, fp32 accumulate; fp32 elsewhere)",
+            "dtype": DTYPE[a.precision],
             "data": "synthetic (seeded SMPL-24 pose + seeded 8x256 weights; no dataset/checkpoint offline)",
             "config": {"workload": f"config3: {H}x{W} frame, {S}+{I} samples, {a.joints}-joint, 8x256 MLP, "
                                    f"one frame per GPU per step", "rays_per_frame": n,

