@@ -313,17 +313,12 @@ __global__ void compose_scatter_kernel(const float* __restrict__ rgb, const floa
     if (out_acc) out_acc[p] = a;
 }
 
-// full torch-order feature vectors (encode_inputs + embedders), one thread per point
-__global__ void encode_points_kernel(ModelDev M, const float* __restrict__ skts, const float* __restrict__ pts,
-                                     const float* __restrict__ dirs, int64_t n, float* __restrict__ feat) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int nj = M.nj, nv = 1 + 2 * M.mr, nk = 1 + 2 * M.mrv;
+// one full torch-order feature vector (encode_inputs + embedders, core/raycasters.py:476-555 and
+// cutoff_embedder.py:111-174) of point p and ray direction d under the joint transforms S (NJ x 16)
+__device__ void encode_row(const ModelDev& M, const float* __restrict__ skts, float px, float py, float pz, float dx,
+                           float dy, float dz, float* __restrict__ f) {
+    const int nj = M.nj, nv = 1 + 2 * M.mr;
     const int cx = nj * nv + 3 * nj;
-    const int F = cx + 3 * nj * nk;
-    float* f = feat + i * F;
-    const float px = pts[3 * i], py = pts[3 * i + 1], pz = pts[3 * i + 2];
-    const float dx = dirs[3 * i], dy = dirs[3 * i + 1], dz = dirs[3 * i + 2];
     for (int j = 0; j < nj; ++j) {
         float S[12];
         for (int r = 0; r < 3; ++r)
@@ -358,5 +353,15 @@ __global__ void encode_points_kernel(ModelDev M, const float* __restrict__ skts,
             }
         }
     }
+}
+
+// full torch-order feature vectors, one thread per point
+__global__ void encode_points_kernel(ModelDev M, const float* __restrict__ skts, const float* __restrict__ pts,
+                                     const float* __restrict__ dirs, int64_t n, float* __restrict__ feat) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int F = M.nj * (1 + 2 * M.mr) + 3 * M.nj + 3 * M.nj * (1 + 2 * M.mrv);
+    encode_row(M, skts, pts[3 * i], pts[3 * i + 1], pts[3 * i + 2], dirs[3 * i], dirs[3 * i + 1], dirs[3 * i + 2],
+               feat + i * F);
 }
 

@@ -45,6 +45,7 @@ using namespace anerf;
 #include "anerf_mlp.hpp"
 #include "anerf_stages.hpp"
 #include "anerf_kernels.hpp"
+#include "anerf_train.hpp"
 #include "anerf_pose.hpp"
 #include "anerf_boxes.hpp"
 #include "anerf_pack.hpp"
@@ -384,6 +385,111 @@ int anerf_encode_points(const anerf_model* m, const float* skts, const float* pt
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(encode_points_kernel, dim3((unsigned)((n_points + 127) / 128)), dim3(128), 0, st, m->md, skts,
                        pts, dirs, n_points, feat_out);
+    HIP_TRY(hipGetLastError());
+    return ANERF_OK;
+}
+
+// ======================================================================= training stages
+// (driven by a-nerf_amd/train.py, the MLP between them is torch autograd)
+static inline unsigned blocks_of(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
+
+int anerf_train_samples(const float* near_in, const float* far_in, int64_t n_rays, int32_t n_samples,
+                        const float* t_rand, float* z_out, void* stream) {
+    if (n_rays < 0 || n_samples < 2 || !near_in || !far_in || !z_out)
+        return fail(ANERF_EINVAL, "anerf_train_samples: bad arguments");
+    if (n_rays == 0) return ANERF_OK;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(train_z_kernel, dim3(blocks_of(n_rays * n_samples, 256)), dim3(256), 0, st, near_in, far_in,
+                       n_rays, n_samples, t_rand, z_out);
+    HIP_TRY(hipGetLastError());
+    return ANERF_OK;
+}
+
+static int check_train_rays(const anerf_model* m, const float* ray_batch, int32_t ray_stride, int64_t n_rays,
+                            const float* z, int32_t n_samples, const float* skts, int32_t n_poses,
+                            const int32_t* ray_pose) {
+    if (!m || !ray_batch || ray_stride < 6 || n_rays < 0 || !z || n_samples < 1 || !skts)
+        return fail(ANERF_EINVAL, "bad arguments");
+    if (!ray_pose && n_poses != n_rays) return fail(ANERF_EINVAL, "per-ray skeletons need n_poses == n_rays");
+    if (ray_pose && n_poses < 1) return fail(ANERF_EINVAL, "n_poses < 1");
+    return ANERF_OK;
+}
+
+int anerf_train_encode(const anerf_model* m, const float* ray_batch, int32_t ray_stride, int64_t n_rays,
+                       const float* z, int32_t n_samples, const float* skts, int32_t n_poses, const int32_t* ray_pose,
+                       float* feat_out, void* stream) {
+    int rc = check_train_rays(m, ray_batch, ray_stride, n_rays, z, n_samples, skts, n_poses, ray_pose);
+    if (rc) return rc;
+    if (!feat_out) return fail(ANERF_EINVAL, "anerf_train_encode: feat_out is NULL");
+    if (n_rays == 0) return ANERF_OK;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(train_encode_kernel, dim3(blocks_of(n_rays * n_samples, 128)), dim3(128), 0, st, m->md,
+                       ray_batch, ray_stride, n_rays, z, n_samples, skts, ray_pose, feat_out);
+    HIP_TRY(hipGetLastError());
+    return ANERF_OK;
+}
+
+int anerf_train_encode_backward(const anerf_model* m, const float* ray_batch, int32_t ray_stride, int64_t n_rays,
+                                const float* z, int32_t n_samples, const float* skts, int32_t n_poses,
+                                const int32_t* ray_pose, const float* grad_feat, float* grad_skts, void* stream) {
+    int rc = check_train_rays(m, ray_batch, ray_stride, n_rays, z, n_samples, skts, n_poses, ray_pose);
+    if (rc) return rc;
+    if (!grad_feat || !grad_skts) return fail(ANERF_EINVAL, "anerf_train_encode_backward: NULL gradient");
+    if (n_rays == 0) return ANERF_OK;
+    if (n_rays > 0x7fffffff) return fail(ANERF_EINVAL, "too many rays for one launch");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(train_encode_backward_kernel, dim3((unsigned)n_rays), dim3(64), 0, st, m->md, ray_batch,
+                       ray_stride, n_rays, z, n_samples, skts, ray_pose, grad_feat, grad_skts);
+    HIP_TRY(hipGetLastError());
+    return ANERF_OK;
+}
+
+int anerf_train_composite(const anerf_model* m, const float* raw, const float* z, const float* ray_batch,
+                          int32_t ray_stride, int64_t n_rays, int32_t n_samples, const float* noise, float* rgb,
+                          float* disp, float* acc, float* weights, float* alpha, float* trans, void* stream) {
+    if (!m || !raw || !z || !ray_batch || ray_stride < 6 || n_rays < 0 || n_samples < 1 || !rgb || !disp || !acc ||
+        !weights || !alpha || !trans)
+        return fail(ANERF_EINVAL, "anerf_train_composite: bad arguments");
+    if (n_rays == 0) return ANERF_OK;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(train_composite_kernel, dim3(blocks_of(n_rays, 64)), dim3(64), 0, st, m->md, raw, z, ray_batch,
+                       ray_stride, n_rays, n_samples, noise, rgb, disp, acc, weights, alpha, trans);
+    HIP_TRY(hipGetLastError());
+    return ANERF_OK;
+}
+
+int anerf_train_composite_backward(const anerf_model* m, const float* raw, const float* z, const float* ray_batch,
+                                   int32_t ray_stride, int64_t n_rays, int32_t n_samples, const float* noise,
+                                   const float* weights, const float* alpha, const float* trans, const float* g_rgb,
+                                   const float* g_disp, const float* g_acc, const float* g_weights,
+                                   const float* g_alpha, float* g_raw, void* stream) {
+    if (!m || !raw || !z || !ray_batch || ray_stride < 6 || n_rays < 0 || n_samples < 1 || !weights || !alpha ||
+        !trans || !g_raw)
+        return fail(ANERF_EINVAL, "anerf_train_composite_backward: bad arguments");
+    if (n_rays == 0) return ANERF_OK;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(train_composite_backward_kernel, dim3(blocks_of(n_rays, 64)), dim3(64), 0, st, m->md, raw, z,
+                       ray_batch, ray_stride, n_rays, n_samples, noise, weights, alpha, trans, g_rgb, g_disp, g_acc,
+                       g_weights, g_alpha, g_raw);
+    HIP_TRY(hipGetLastError());
+    return ANERF_OK;
+}
+
+int anerf_train_importance(const float* z, const float* weights, int64_t n_rays, int32_t n_samples,
+                           int32_t n_importance, const float* u, float* z_all, void* stream) {
+    if (!z || !weights || !z_all || n_rays < 0 || n_samples < 3 || n_importance < 1 || n_samples > 1024 ||
+        n_importance > 2048)
+        return fail(ANERF_EINVAL, "anerf_train_importance: bad arguments");
+    if (n_rays == 0) return ANERF_OK;
+    if (n_rays > 0x7fffffff) return fail(ANERF_EINVAL, "too many rays for one launch");
+    const int T = n_samples + n_importance;
+    const size_t lds = (size_t)(3 * pad32(T) + 3 * n_samples + T + 32) * 4;
+    if (lds > 160 * 1024) return fail(ANERF_EINVAL, "n_samples + n_importance too large");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    HIP_TRY(hipFuncSetAttribute((const void*)train_importance_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds));
+    hipLaunchKernelGGL(train_importance_kernel, dim3((unsigned)n_rays), dim3(64), lds, st, z, weights, n_rays,
+                       n_samples, n_importance, u, z_all);
     HIP_TRY(hipGetLastError());
     return ANERF_OK;
 }

@@ -216,8 +216,10 @@ __device__ __forceinline__ bool z_eq(float a, float b) { return a == b || (a != 
 
 // isample_from_lineseg + sample_pdf(det) + sort (ray_utils.py:157-201, 255-289) for ray slot r.
 // weights w (S) in scr; writes sorted z_all (S+I) to zf.
+// u: the I uniform samples of this ray (training, det=False: torch.rand), or NULL for the
+// deterministic linspace of eval.
 __device__ void importance(const float* zc, const float* w, int S, int I, float* zf, float* scr2, bool active,
-                           int lane) {
+                           int lane, const float* u_rand = nullptr) {
     const int nb = S - 1;  // bins = mids
     float* mids = scr2;
     float* wp = scr2 + nb;
@@ -257,7 +259,7 @@ __device__ void importance(const float* zc, const float* w, int S, int I, float*
     wave_sync();
     if (active) {
         for (int k = lane; k < I; k += 64) {
-            const float u = torch_linspace01(k, I);
+            const float u = u_rand ? u_rand[k] : torch_linspace01(k, I);
             int lo = 0, hi = nb;  // searchsorted(right=True) over nb cdf entries
             while (lo < hi) {
                 const int mid = (lo + hi) >> 1;

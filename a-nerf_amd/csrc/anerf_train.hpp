@@ -1,0 +1,318 @@
+// anerf_train.hpp — training-mode stages of RayCaster.render_rays: stratified
+// samples, the encoder forward and backward (gradient to the skeleton transforms, i.e. to the pose
+// optimisation), raw2outputs forward and backward, and stochastic importance sampling.  The MLP
+// between them runs as plain fp32 GEMMs (hipBLASLt through torch autograd, a-nerf_amd/train.py).
+// Random numbers are inputs (t_rand, noise, u), so a caller can feed the reference's draws.
+// Part of the single translation unit anerf_render.hip (included there, in order).
+#pragma once
+
+// sample_from_lineseg with perturb > 0 (core/utils/ray_utils.py:204-251): z = linspace between
+// near and far, then lower + (upper - lower) * t_rand inside the mid-point intervals.  t_rand NULL:
+// the deterministic samples (perturb = 0).  One thread per sample.
+__global__ void train_z_kernel(const float* __restrict__ nearp, const float* __restrict__ farp, int64_t n, int S,
+                               const float* __restrict__ t_rand, float* __restrict__ z) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= n * S) return;
+    const int64_t i = idx / S;
+    const int s = (int)(idx % S);
+    const float nr = nearp[i], fr = farp[i];
+    auto zl = [&](int k) {
+        const float t = torch_linspace01(k, S);
+        return nr * (1.0f - t) + fr * t;
+    };
+    const float zs = zl(s);
+    float zv = zs;
+    if (t_rand) {
+        const float upper = s + 1 < S ? 0.5f * (zl(s + 1) + zs) : zs;
+        const float lower = s > 0 ? 0.5f * (zs + zl(s - 1)) : zs;
+        zv = lower + (upper - lower) * t_rand[idx];
+    }
+    z[idx] = zv;
+}
+
+// encode_inputs over a ray batch: sample s of ray i at p = o + d z (sample_pts,
+// raycasters.py:650-663), pose ray_pose[i] (or i when per_ray), feature row [v | r | d] of
+// encode_row.  One thread per sample.
+__global__ void train_encode_kernel(ModelDev M, const float* __restrict__ rb, int stride, int64_t n,
+                                    const float* __restrict__ z, int ns, const float* __restrict__ skts,
+                                    const int32_t* __restrict__ ray_pose, float* __restrict__ feat) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= n * ns) return;
+    const int64_t i = idx / ns;
+    const int64_t pose = ray_pose ? ray_pose[i] : i;
+    const float* ray = rb + i * stride;
+    const float zz = z[idx];
+    const float px = ray[0] + ray[3] * zz, py = ray[1] + ray[4] * zz, pz = ray[2] + ray[5] * zz;
+    const int F = M.nj * (1 + 2 * M.mr) + 3 * M.nj + 3 * M.nj * (1 + 2 * M.mrv);
+    encode_row(M, skts + pose * M.nj * 16, px, py, pz, ray[3], ray[4], ray[5], feat + idx * F);
+}
+
+// d feature / d inputs of encode_row for one (sample, joint): accumulates dL/dS[0:3, 0:4] (12
+// values, row-major) of joint j given the feature gradients g (one row).  Same flags and forms as
+// encode_row (cutoff windows w = 1 - sigmoid(tau (dist - c)), dw/ddist = -tau w (1 - w);
+// F.normalize x / max(|x|, 1e-12); torch.norm's gradient 0 at 0).
+__device__ __forceinline__ void encode_row_grad_joint(const ModelDev& M, const float* __restrict__ S, int j,
+                                                      float px, float py, float pz, float dx, float dy, float dz,
+                                                      const float* __restrict__ g, float (&gS)[12]) {
+    const int nj = M.nj, nv = 1 + 2 * M.mr;
+    const int cx = nj * nv + 3 * nj;
+    float qx, qy, qz;
+    joint_local(S, px, py, pz, qx, qy, qz);
+    const float dist = norm3(qx, qy, qz);
+    // ---- distance block
+    const bool cut = M.use_cutoff != 0, cut_in = M.use_cutoff && M.cutoff_inputs;
+    const float w = cut ? cutoff_w(M.tau, dist, M.cutoff[j]) : 1.0f;
+    float g_dist = 0.0f, g_w = 0.0f;
+    const float g0 = g[j];
+    if (cut_in) {
+        g_dist += g0 * w;
+        g_w += g0 * dist;
+    } else {
+        g_dist += g0;
+    }
+    for (int fi = 0; fi < M.mr; ++fi) {
+        const float fr = (float)(1 << fi);
+        float s, c;
+        sincosf(dist * fr, &s, &c);
+        const float gs = g[(1 + 2 * fi) * nj + j], gc = g[(2 + 2 * fi) * nj + j];
+        g_w += gs * s + gc * c;
+        g_dist += (gs * c - gc * s) * w * fr;
+    }
+    if (cut) g_dist += g_w * (-M.tau * w * (1.0f - w));
+    // ---- bone direction u = q / max(|q|, eps)
+    float gqx, gqy, gqz;
+    {
+        const float gux = g[nj * nv + 3 * j], guy = g[nj * nv + 3 * j + 1], guz = g[nj * nv + 3 * j + 2];
+        if (dist > 1e-12f) {
+            const float ux = qx / dist, uy = qy / dist, uz = qz / dist;
+            const float dot = ux * gux + uy * guy + uz * guz;
+            gqx = (gux - ux * dot) / dist;
+            gqy = (guy - uy * dot) / dist;
+            gqz = (guz - uz * dot) / dist;
+        } else {
+            gqx = gux / 1e-12f;
+            gqy = guy / 1e-12f;
+            gqz = guz / 1e-12f;
+        }
+    }
+    // ---- view direction e = R d / max(|R d|, eps), window on dist
+    float ex, ey, ez;
+    joint_rot(S, dx, dy, dz, ex, ey, ez);
+    const float enr = norm3(ex, ey, ez);
+    const float en = fmaxf(enr, 1e-12f);
+    const float e[3] = {ex / en, ey / en, ez / en};
+    const bool cutv = M.cutoff_viewdir != 0;
+    const float wv = cutv ? cutoff_w(M.tau_v, dist, M.cutoff_v[j]) : 1.0f;
+    float ge[3] = {0.0f, 0.0f, 0.0f}, g_wv = 0.0f;
+    for (int c = 0; c < 3; ++c) {
+        const float gv0 = g[cx + 3 * j + c];
+        if (cutv && M.cutoff_inputs) {
+            ge[c] += gv0 * wv;
+            g_wv += gv0 * e[c];
+        } else {
+            ge[c] += gv0;
+        }
+        for (int fi = 0; fi < M.mrv; ++fi) {
+            const float fr = (float)(1 << fi);
+            float s, co;
+            sincosf(e[c] * fr, &s, &co);
+            const float gs = g[cx + (1 + 2 * fi) * 3 * nj + 3 * j + c], gc = g[cx + (2 + 2 * fi) * 3 * nj + 3 * j + c];
+            g_wv += gs * s + gc * co;
+            ge[c] += (gs * co - gc * s) * wv * fr;
+        }
+    }
+    if (cutv) g_dist += g_wv * (-M.tau_v * wv * (1.0f - wv));
+    float gex, gey, gez;
+    if (enr > 1e-12f) {
+        const float dot = e[0] * ge[0] + e[1] * ge[1] + e[2] * ge[2];
+        gex = (ge[0] - e[0] * dot) / enr;
+        gey = (ge[1] - e[1] * dot) / enr;
+        gez = (ge[2] - e[2] * dot) / enr;
+    } else {
+        gex = ge[0] / 1e-12f;
+        gey = ge[1] / 1e-12f;
+        gez = ge[2] / 1e-12f;
+    }
+    // ---- dist = |q|
+    if (dist > 0.0f) {
+        gqx += g_dist * qx / dist;
+        gqy += g_dist * qy / dist;
+        gqz += g_dist * qz / dist;
+    }
+    // q = A p + t, e_raw = A d
+    const float gq[3] = {gqx, gqy, gqz}, gr[3] = {gex, gey, gez};
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        gS[4 * r + 0] += gq[r] * px + gr[r] * dx;
+        gS[4 * r + 1] += gq[r] * py + gr[r] * dy;
+        gS[4 * r + 2] += gq[r] * pz + gr[r] * dz;
+        gS[4 * r + 3] += gq[r];
+    }
+}
+
+// Encoder backward: dL/dskts from dL/dfeat.  One wave per ray (its samples over the lanes), per
+// joint a wave reduction of the 12 sums, accumulated into grad_skts[pose] (atomic: rays may
+// share a pose).  grad_skts rows 3 (the [0 0 0 1] row) get no gradient, as in the reference.
+__global__ __launch_bounds__(64) void train_encode_backward_kernel(ModelDev M, const float* __restrict__ rb,
+                                                                   int stride, int64_t n, const float* __restrict__ z,
+                                                                   int ns, const float* __restrict__ skts,
+                                                                   const int32_t* __restrict__ ray_pose,
+                                                                   const float* __restrict__ gfeat,
+                                                                   float* __restrict__ gskts) {
+    const int64_t i = blockIdx.x;
+    if (i >= n) return;
+    const int lane = threadIdx.x;
+    const int64_t pose = ray_pose ? ray_pose[i] : i;
+    const float* ray = rb + i * stride;
+    const int F = M.nj * (1 + 2 * M.mr) + 3 * M.nj + 3 * M.nj * (1 + 2 * M.mrv);
+    const float* Sp = skts + pose * M.nj * 16;
+    for (int j = 0; j < M.nj; ++j) {
+        float S[12];
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 4; ++c) S[4 * r + c] = Sp[j * 16 + 4 * r + c];
+        float gS[12] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+        for (int s = lane; s < ns; s += 64) {
+            const float zz = z[i * ns + s];
+            const float px = ray[0] + ray[3] * zz, py = ray[1] + ray[4] * zz, pz = ray[2] + ray[5] * zz;
+            encode_row_grad_joint(M, S, j, px, py, pz, ray[3], ray[4], ray[5], gfeat + (i * ns + s) * F, gS);
+        }
+#pragma unroll
+        for (int k = 0; k < 12; ++k) {
+            const float v = wave_sum(gS[k]);
+            if (lane == 0 && v != 0.0f) atomicAdd(gskts + (pose * M.nj + j) * 16 + k, v);
+        }
+    }
+}
+
+// raw2outputs (core/networks/nerf.py:150-205) with the training noise: sigma = act(raw/B + noise),
+// alpha = 1 - exp(-sigma delta), weights = alpha * exclusive cumprod(1 - alpha + 1e-10) (torch's CPU
+// cumprod accumulates in double), rgb / depth / acc sums, disp with the isclose(acc, 0) zeroing.
+// Also writes the transmittance (the exclusive cumprod) for the backward.  One thread per ray.
+__device__ __forceinline__ float density_act_grad(const ModelDev& M, float x) {
+    if (!M.softplus) return x > 0.0f ? 1.0f : 0.0f;  // relu: grad * (result > 0)
+    const float y = x - M.shift;                     // softplus(beta 1, threshold 20)
+    if (y > 20.0f) return 1.0f;
+    const float e = expf(y);
+    return e / (e + 1.0f);
+}
+
+__global__ void train_composite_kernel(ModelDev M, const float* __restrict__ raw, const float* __restrict__ z,
+                                       const float* __restrict__ rb, int stride, int64_t n, int ns,
+                                       const float* __restrict__ noise, float* __restrict__ rgb,
+                                       float* __restrict__ disp, float* __restrict__ acc, float* __restrict__ wts,
+                                       float* __restrict__ alpha, float* __restrict__ trans) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float* ray = rb + i * stride;
+    const float dn = norm3(ray[3], ray[4], ray[5]);
+    const float* zr = z + i * ns;
+    const float* rr = raw + i * ns * 4;
+    double T = 1.0;
+    float sa = 0.0f, sd = 0.0f, sr = 0.0f, sg = 0.0f, sb = 0.0f;
+    for (int s = 0; s < ns; ++s) {
+        float dist = (s + 1 < ns) ? (zr[s + 1] - zr[s]) : 1e10f;
+        dist = dist * dn;
+        const float x = rr[4 * s + 3] / M.B + (noise ? noise[i * ns + s] : 0.0f);
+        const float a = 1.0f - expf(-density_act(M, x) * dist);
+        const float t = (float)T;
+        T *= (double)((1.0f - a) + 1e-10f);
+        const float w = a * t;
+        alpha[i * ns + s] = a;
+        trans[i * ns + s] = t;
+        wts[i * ns + s] = w;
+        sa += w;
+        sd += w * zr[s];
+        sr += w * (sigmoid(rr[4 * s + 0]) * 1.002f - 0.001f);
+        sg += w * (sigmoid(rr[4 * s + 1]) * 1.002f - 0.001f);
+        sb += w * (sigmoid(rr[4 * s + 2]) * 1.002f - 0.001f);
+    }
+    const float ratio = sd / (sa + 1e-10f);
+    float dsp = 1.0f / fmaxf(ratio, 1e-10f);
+    if (ratio != ratio) dsp = ratio;
+    if (fabsf(sa) <= 1e-8f) dsp = 0.0f;
+    rgb[3 * i] = sr;
+    rgb[3 * i + 1] = sg;
+    rgb[3 * i + 2] = sb;
+    disp[i] = dsp;
+    acc[i] = sa < 1.0f ? sa : 1.0f;
+}
+
+// Backward of train_composite_kernel: dL/draw (N x ns x 4) from dL/d{rgb, disp, acc, weights, alpha}
+// (any may be NULL = zero).  With G_s = dL/dw_s, the transmittance factors f_s = 1 - alpha_s + 1e-10
+// and P_s their exclusive product: dL/dalpha_s = G_s P_s + galpha_s - P_s R_s, where
+// R_s = sum_{k>s} G_k alpha_k prod_{s<m<k} f_m runs backwards as R_{s-1} = G_s alpha_s + f_s R_s
+// (no division by f_s); then dalpha/dsigma = exp(-sigma delta) delta, the activation's gradient, 1/B;
+// rgb: w_s g_rgb 1.002 sigmoid'(raw).  One thread per ray.
+__global__ void train_composite_backward_kernel(ModelDev M, const float* __restrict__ raw, const float* __restrict__ z,
+                                                const float* __restrict__ rb, int stride, int64_t n, int ns,
+                                                const float* __restrict__ noise, const float* __restrict__ wts,
+                                                const float* __restrict__ alpha, const float* __restrict__ trans,
+                                                const float* __restrict__ g_rgb, const float* __restrict__ g_disp,
+                                                const float* __restrict__ g_acc, const float* __restrict__ g_w,
+                                                const float* __restrict__ g_alpha, float* __restrict__ g_raw) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float* ray = rb + i * stride;
+    const float dn = norm3(ray[3], ray[4], ray[5]);
+    const float* zr = z + i * ns;
+    const float* rr = raw + i * ns * 4;
+    const float* wr = wts + i * ns;
+    float sa = 0.0f, sd = 0.0f;
+    for (int s = 0; s < ns; ++s) {
+        sa += wr[s];
+        sd += wr[s] * zr[s];
+    }
+    const float gr = g_rgb ? g_rgb[3 * i] : 0.0f, gg = g_rgb ? g_rgb[3 * i + 1] : 0.0f,
+                gb = g_rgb ? g_rgb[3 * i + 2] : 0.0f;
+    const float ga = (g_acc && sa < 1.0f) ? g_acc[i] : 0.0f;  // torch.minimum(sum w, 1)
+    // disp = mask / max(1e-10, depth / (W + 1e-10)):  d disp / d w_s = -mask / r^2 (z_s - r) / (W + 1e-10)
+    float gd_r = 0.0f, r = 0.0f;
+    const float den = sa + 1e-10f;
+    if (g_disp) {
+        r = sd / den;
+        if (r > 1e-10f && !(fabsf(sa) <= 1e-8f)) gd_r = -g_disp[i] / (r * r);
+    }
+    double R = 0.0;
+    for (int s = ns - 1; s >= 0; --s) {
+        const float c0 = sigmoid(rr[4 * s + 0]), c1 = sigmoid(rr[4 * s + 1]), c2 = sigmoid(rr[4 * s + 2]);
+        const float w = wr[s], a = alpha[i * ns + s], P = trans[i * ns + s];
+        float G = gr * (c0 * 1.002f - 0.001f) + gg * (c1 * 1.002f - 0.001f) + gb * (c2 * 1.002f - 0.001f) + ga;
+        if (gd_r != 0.0f) G += gd_r * (zr[s] - r) / den;
+        if (g_w) G += g_w[i * ns + s];
+        const float gal = G * P + (g_alpha ? g_alpha[i * ns + s] : 0.0f) - (float)((double)P * R);
+        R = (double)G * (double)a + (double)((1.0f - a) + 1e-10f) * R;
+        float dist = (s + 1 < ns) ? (zr[s + 1] - zr[s]) : 1e10f;
+        dist = dist * dn;
+        const float x = rr[4 * s + 3] / M.B + (noise ? noise[i * ns + s] : 0.0f);
+        const float sig = density_act(M, x);
+        const float gsig = gal * expf(-sig * dist) * dist;
+        float* go = g_raw + (i * ns + s) * 4;
+        go[3] = gsig * density_act_grad(M, x) / M.B;
+        go[0] = w * gr * 1.002f * c0 * (1.0f - c0);
+        go[1] = w * gg * 1.002f * c1 * (1.0f - c1);
+        go[2] = w * gb * 1.002f * c2 * (1.0f - c2);
+    }
+}
+
+// isample_from_lineseg + sample_pdf (det=False: u from torch.rand) + sort, training form of the
+// render kernel's importance(): one wave per ray, LDS scratch.  z_all (N x (S+I)) sorted.
+__global__ __launch_bounds__(64) void train_importance_kernel(const float* __restrict__ z,
+                                                              const float* __restrict__ wts, int64_t n, int S, int I,
+                                                              const float* __restrict__ u, float* __restrict__ z_all) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int64_t i = blockIdx.x;
+    if (i >= n) return;
+    const int lane = threadIdx.x, T = S + I;
+    const int zs = pad32(T);
+    float* zc = lds;
+    float* w = lds + zs;
+    float* zf = lds + 2 * zs;
+    float* scr2 = lds + 3 * zs;
+    for (int s = lane; s < S; s += 64) {
+        zc[s] = z[i * S + s];
+        w[s] = wts[i * S + s];
+    }
+    wave_sync();
+    importance(zc, w, S, I, zf, scr2, true, lane, u ? u + i * I : nullptr);
+    for (int s = lane; s < T; s += 64) z_all[i * T + s] = zf[s];
+}

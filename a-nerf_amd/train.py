@@ -1,0 +1,334 @@
+"""Training-mode render path: `RayCaster.render_rays` with stratified
+sampling (`perturb`), density noise (`raw_noise_std`), stochastic importance sampling and
+gradients to the networks AND to the skeleton transforms (A-NeRF's pose optimisation).
+
+Mirrors `core/raycasters.py:361-474` (training branch of `RayCaster.forward`, :349-359) and the
+loss of `Trainer._compute_nerf_loss` (`core/trainer.py:350-381`).  The per-sample stages run as
+HIP kernels through the C ABI (include/anerf.h, `anerf_train_*`): sample placement, the skeleton-
+relative encoding and its backward (dL/dskts), raw2outputs and its backward, importance sampling.
+The MLP between them is plain fp32 GEMMs under torch autograd (hipBLASLt), with the reference's
+concatenations (`cat([x, h])` at the skip, `cat([feature, views(, code)])` at the view layer)
+replaced by split weight blocks, so no concatenated activation is ever materialised.
+
+Random numbers: torch's generator on the device by default; pass `rand={"t_rand": (N,S),
+"noise0": (N,S), "u": (N,I), "noise1": (N,S+I)}` (standard-uniform / standard-normal draws) to
+reproduce a given draw — the parity tests feed the reference's.
+"""
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib
+from .config import RenderConfig
+from .model import DeviceModel
+
+
+def _stream(dev):
+    return _lib.stream_handle(dev)
+
+
+# ----------------------------------------------------------------------------- autograd stages
+class _Encode(torch.autograd.Function):
+    """encode_inputs of every sample (raycasters.py:476-555): features [N*S, F]; backward -> dL/dskts."""
+
+    @staticmethod
+    def forward(ctx, skts, model, rb, z, ray_pose):
+        n, ns = z.shape
+        cfg = model.cfg
+        F_ = cfg.feature_dim
+        feat = torch.empty(n * ns, F_, device=z.device, dtype=torch.float32)
+        n_poses = skts.shape[0]
+        _lib.check(_lib.load().anerf_train_encode(model.handle, _lib.ptr(rb), rb.shape[1], n, _lib.ptr(z), ns,
+                                                  _lib.ptr(skts), n_poses, _lib.ptr(ray_pose), _lib.ptr(feat),
+                                                  _stream(z.device)), "anerf_train_encode")
+        ctx.model = model
+        ctx.save_for_backward(skts, rb, z, ray_pose if ray_pose is not None else torch.empty(0))
+        ctx.has_pose = ray_pose is not None
+        return feat
+
+    @staticmethod
+    def backward(ctx, g_feat):
+        skts, rb, z, ray_pose = ctx.saved_tensors
+        if not ctx.needs_input_grad[0]:
+            return None, None, None, None, None
+        n, ns = z.shape
+        g = torch.zeros_like(skts)
+        gf = g_feat.contiguous()
+        _lib.check(_lib.load().anerf_train_encode_backward(
+            ctx.model.handle, _lib.ptr(rb), rb.shape[1], n, _lib.ptr(z), ns, _lib.ptr(skts), skts.shape[0],
+            _lib.ptr(ray_pose if ctx.has_pose else None), _lib.ptr(gf), _lib.ptr(g), _stream(z.device)),
+            "anerf_train_encode_backward")
+        return g, None, None, None, None
+
+
+class _Composite(torch.autograd.Function):
+    """NeRF.raw2outputs (nerf.py:150-205) with noise: rgb, disp, acc, weights, alpha."""
+
+    @staticmethod
+    def forward(ctx, raw, model, z, rb, noise):
+        n, ns = z.shape
+        dev = z.device
+        f32 = dict(device=dev, dtype=torch.float32)
+        rgb, disp, acc = torch.empty(n, 3, **f32), torch.empty(n, **f32), torch.empty(n, **f32)
+        w, a, tr = torch.empty(n, ns, **f32), torch.empty(n, ns, **f32), torch.empty(n, ns, **f32)
+        raw = raw.contiguous()
+        _lib.check(_lib.load().anerf_train_composite(model.handle, _lib.ptr(raw), _lib.ptr(z), _lib.ptr(rb),
+                                                     rb.shape[1], n, ns, _lib.ptr(noise), _lib.ptr(rgb),
+                                                     _lib.ptr(disp), _lib.ptr(acc), _lib.ptr(w), _lib.ptr(a),
+                                                     _lib.ptr(tr), _stream(dev)), "anerf_train_composite")
+        ctx.model = model
+        ctx.has_noise = noise is not None
+        ctx.save_for_backward(raw, z, rb, noise if noise is not None else torch.empty(0), w, a, tr)
+        return rgb, disp, acc, w, a
+
+    @staticmethod
+    def backward(ctx, g_rgb, g_disp, g_acc, g_w, g_a):
+        raw, z, rb, noise, w, a, tr = ctx.saved_tensors
+        n, ns = z.shape
+        g_raw = torch.empty_like(raw)
+        c = lambda t: None if t is None else t.contiguous()  # noqa: E731
+        _lib.check(_lib.load().anerf_train_composite_backward(
+            ctx.model.handle, _lib.ptr(raw), _lib.ptr(z), _lib.ptr(rb), rb.shape[1], n, ns,
+            _lib.ptr(noise if ctx.has_noise else None), _lib.ptr(w), _lib.ptr(a), _lib.ptr(tr), _lib.ptr(c(g_rgb)),
+            _lib.ptr(c(g_disp)), _lib.ptr(c(g_acc)), _lib.ptr(c(g_w)), _lib.ptr(c(g_a)), _lib.ptr(g_raw),
+            _stream(z.device)), "anerf_train_composite_backward")
+        return g_raw, None, None, None, None
+
+
+# ----------------------------------------------------------------------------- networks
+class Optcodes(nn.Module):
+    """core/networks/embedding.py:6-46 (training: codes(idx); eval with all idx < 0: the mean code)."""
+
+    def __init__(self, n_codes, code_ch):
+        super().__init__()
+        self.codes = nn.Embedding(n_codes, code_ch)
+
+    def forward(self, idx):
+        idx = idx.reshape(-1)
+        if not self.training and bool((idx.max() < 0).item()):
+            return self.codes.weight.mean(0, keepdim=True).expand(len(idx), -1)
+        return self.codes(idx.long())
+
+
+class NeRF(nn.Module):
+    """Parameters with the names of core/networks/nerf.py:57-88 (state_dict-compatible); forward
+    on the split feature buffer [x | views] of the encoder."""
+
+    def __init__(self, cfg):
+        super().__init__()
+        W, D = cfg.netwidth, cfg.netdepth
+        self.cfg = cfg
+        self.skips = tuple(cfg.skips)
+        self.dnet = cfg.input_ch + cfg.input_ch_bones
+        self.pts_linears = nn.ModuleList(
+            [nn.Linear(self.dnet, W)] + [nn.Linear(W + self.dnet if i in self.skips else W, W) for i in range(D - 1)])
+        self.alpha_linear = nn.Linear(W, 1)
+        self.feature_linear = nn.Linear(W, W)
+        self.views_linears = nn.ModuleList([nn.Linear(W + cfg.input_ch_views + cfg.framecode_ch, W // 2)])
+        self.rgb_linear = nn.Linear(W // 2, 3)
+        if cfg.opt_framecode:
+            self.framecodes = Optcodes(cfg.n_framecodes, cfg.framecode_size)
+
+    def forward(self, feat, cams=None):
+        """feat [M, F] = [v | r | views] -> raw [M, 4] (rgb, alpha): forward_density + forward_view."""
+        x = feat[:, :self.dnet]
+        views = feat[:, self.dnet:]
+        h = x
+        for i, lin in enumerate(self.pts_linears):
+            if i > 0 and (i - 1) in self.skips:  # cat([input_pts, h]) @ W.T = x @ Wx.T + h @ Wh.T
+                h = F.relu(F.linear(x, lin.weight[:, :self.dnet]) + F.linear(h, lin.weight[:, self.dnet:], lin.bias))
+            else:
+                h = F.relu(lin(h))
+        alpha = self.alpha_linear(h)
+        feature = self.feature_linear(h)
+        W = feature.shape[1]
+        vl = self.views_linears[0]
+        nv = self.cfg.input_ch_views
+        g = F.linear(feature, vl.weight[:, :W]) + F.linear(views, vl.weight[:, W:W + nv], vl.bias)
+        if self.cfg.opt_framecode:
+            g = g + F.linear(self.framecodes(cams), vl.weight[:, W + nv:])
+        g = F.relu(g)
+        rgb = self.rgb_linear(g)
+        return torch.cat([rgb, alpha], -1)
+
+
+class _Embed(nn.Module):
+    """CutoffEmbedder state (cutoff_embedder.py:60-95): cutoff_dist (not trained), tau buffer."""
+
+    def __init__(self, n_joints):
+        super().__init__()
+        self.cutoff_dist = nn.Parameter(torch.zeros(n_joints), requires_grad=False)
+        self.register_buffer("tau", torch.tensor(20.0))
+
+
+class TrainRayCaster(nn.Module):
+    """Trainable RayCaster (core/raycasters.py:326-474): nn.Module with the reference's
+    state_dict layout (network_fn.*, network_fine.*, embed_fn.*, embeddirs_fn.*).  In training
+    mode `forward`/`render_rays` run the stochastic, differentiable render path; in eval mode
+    they delegate to the fused HIP render kernel (weights repacked when they changed)."""
+
+    def __init__(self, cfg, ckpt=None, device=None):
+        super().__init__()
+        self.cfg = cfg.validate()
+        if cfg.precision != "fp32":
+            pass  # the eval delegate uses cfg.precision; training is fp32
+        dev = torch.device(f"cuda:{torch.cuda.current_device() if device is None else int(device)}")
+        self.network_fn = NeRF(cfg)
+        self.network_fine = NeRF(cfg) if cfg.N_importance > 0 else None
+        self.embed_fn = _Embed(cfg.n_joints)
+        self.embeddirs_fn = _Embed(cfg.n_joints)
+        if ckpt is not None:
+            self.load_checkpoint(ckpt)
+        self.to(dev)
+        self._dev = dev
+        self._consts = None  # DeviceModel holding the encoder / density constants (cutoffs, tau, B)
+        self._eval = None
+        self._eval_version = None
+
+    # -- checkpoints in the reference's key layout (raycasters.py:752-788)
+    def load_checkpoint(self, ck):
+        def t(v):
+            return torch.as_tensor(v).float()
+        self.network_fn.load_state_dict({k: t(v) for k, v in ck["network_fn_state_dict"].items()})
+        if self.network_fine is not None:
+            self.network_fine.load_state_dict({k: t(v) for k, v in ck["network_fine_state_dict"].items()})
+        for mod, key in ((self.embed_fn, "embed_state_dict"), (self.embeddirs_fn, "embeddirs_state_dict")):
+            mod.load_state_dict({k: t(v) for k, v in ck[key].items()})
+        self._consts = None
+        self._eval = None
+
+    def checkpoint(self):
+        def sd(m):
+            return {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
+        ck = {"network_fn_state_dict": sd(self.network_fn), "embed_state_dict": sd(self.embed_fn),
+              "embedbones_state_dict": {}, "embeddirs_state_dict": sd(self.embeddirs_fn)}
+        if self.network_fine is not None:
+            ck["network_fine_state_dict"] = sd(self.network_fine)
+        return ck
+
+    def _version(self):
+        return tuple(p._version for p in self.parameters()) + tuple(b._version for b in self.buffers())
+
+    def _constants(self):
+        if self._consts is None:
+            self._consts = DeviceModel(self.cfg, self.checkpoint(), device=self._dev.index)
+        return self._consts
+
+    def eval_caster(self):
+        """The fused eval RayCaster over the current weights (repacked only after they changed)."""
+        from .raycaster import RayCaster
+        v = self._version()
+        if self._eval is None or v != self._eval_version:
+            self._eval = RayCaster(self.cfg, self.checkpoint(), device=self._dev.index)
+            self._eval_version = v
+        return self._eval
+
+    def forward(self, *args, fwd_type="", **kwargs):
+        if fwd_type:
+            return self.eval_caster()(*args, fwd_type=fwd_type, **kwargs)
+        if not self.training:
+            with torch.no_grad():
+                return self.eval_caster().render_rays(*args, **kwargs)
+        return self.render_rays(*args, **kwargs)
+
+    # -- the training render path
+    def render_rays(self, ray_batch, N_samples, kp_batch=None, skts=None, cyls=None, bones=None, cams=None,
+                    subject_idxs=None, retraw=False, lindisp=False, perturb=0., N_importance=0, network_fine=None,
+                    raw_noise_std=0., ray_noise_std=0., verbose=False, ext_scale=0.001, pytest=False,
+                    preproc_kwargs=None, nerf_type="nerf", rand=None, chunk=None):
+        """core/raycasters.py:361-474 with autograd: gradients reach the networks' parameters and
+        `skts` (when it requires grad).  `rand` overrides the random draws (module docstring)."""
+        if lindisp:
+            raise NotImplementedError("lindisp sampling is not implemented")
+        if ray_noise_std:
+            raise NotImplementedError("ray_noise_std > 0 is not implemented")
+        if subject_idxs is not None:
+            raise NotImplementedError("multi-subject training (subject_idxs) is not implemented")
+        if skts is None or cyls is None:
+            raise ValueError("skts and cyls are required")
+        cfg = self.cfg
+        B = cfg.density_scale
+        if preproc_kwargs and preproc_kwargs.get("density_scale", B) != B:
+            raise ValueError("density_scale differs from the model's configuration")
+        dev = self._dev
+        rand = rand or {}
+        model = self._constants()
+        rb = ray_batch.to(dev, torch.float32).detach().contiguous()
+        n = rb.shape[0]
+        S, I = int(N_samples), int(N_importance)
+        nj = cfg.n_joints
+        if I > 0 and self.network_fine is None:
+            raise ValueError("N_importance > 0 needs a fine network")
+        # skeletons: one per ray (the reference's layout, gradients flow back through any expand)
+        sk = skts.to(dev, torch.float32)
+        if sk.dim() == 3:
+            sk = sk.unsqueeze(0)
+        sk = sk.expand(n, nj, 4, 4).contiguous() if sk.shape[0] != n else sk.contiguous()
+        cyl = cyls.to(dev, torch.float32).detach()
+        cyl = cyl.expand(n, 5).contiguous() if cyl.dim() == 1 or cyl.shape[0] != n else cyl.contiguous()
+        pose = torch.arange(n, device=dev, dtype=torch.int32)
+        # near / far in the bounding cylinder (+ the chunk NaN fill)
+        nearv = torch.empty(n, device=dev, dtype=torch.float32)
+        farv = torch.empty(n, device=dev, dtype=torch.float32)
+        ws, need = model.workspace(n, S, 0)
+        _lib.check(_lib.load().anerf_near_far(_lib.ptr(rb), rb.shape[1], n, _lib.ptr(cyl), _lib.ptr(pose),
+                                              int(chunk or max(n, 1)), _lib.ptr(nearv), _lib.ptr(farv),
+                                              _lib.ptr(ws), need, _stream(dev)), "anerf_near_far")
+        stochastic = perturb > 0
+        t_rand = rand.get("t_rand")
+        if stochastic and t_rand is None:
+            t_rand = torch.rand(n, S, device=dev)
+        t_rand = t_rand.to(dev, torch.float32).contiguous() if stochastic else None
+        z = torch.empty(n, S, device=dev, dtype=torch.float32)
+        _lib.check(_lib.load().anerf_train_samples(_lib.ptr(nearv), _lib.ptr(farv), n, S, _lib.ptr(t_rand),
+                                                   _lib.ptr(z), _stream(dev)), "anerf_train_samples")
+        cam_t = None
+        if cfg.opt_framecode:
+            if cams is None:
+                raise ValueError("this model uses framecodes: cams are required")
+            cam_t = cams.to(dev).reshape(n)
+
+        def noise_for(key, ns):
+            if raw_noise_std <= 0:
+                return None
+            g = rand.get(key)
+            g = torch.randn(n, ns, device=dev) if g is None else g.to(dev, torch.float32)
+            return (g * raw_noise_std * B).contiguous()
+
+        def run(net, zz, noise):
+            ns = zz.shape[1]
+            feat = _Encode.apply(sk, model, rb, zz, None)
+            raw = net(feat, None if cam_t is None else cam_t.repeat_interleave(ns))
+            return _Composite.apply(raw.reshape(n, ns, 4), model, zz, rb, noise)
+
+        rgb, disp, acc, w, a = run(self.network_fn, z, noise_for("noise0", S))
+        out = {"rgb_map": rgb, "disp_map": disp, "acc_map": acc, "alpha": a}
+        if I > 0:
+            u = rand.get("u")
+            if stochastic and u is None:
+                u = torch.rand(n, I, device=dev)
+            u = u.to(dev, torch.float32).contiguous() if stochastic else None
+            z_all = torch.empty(n, S + I, device=dev, dtype=torch.float32)
+            wd = w.detach().contiguous()
+            _lib.check(_lib.load().anerf_train_importance(_lib.ptr(z), _lib.ptr(wd), n, S, I, _lib.ptr(u),
+                                                          _lib.ptr(z_all), _stream(dev)), "anerf_train_importance")
+            rgb1, disp1, acc1, w1, a1 = run(self.network_fine, z_all, noise_for("noise1", S + I))
+            out = {"rgb_map": rgb1, "disp_map": disp1, "acc_map": acc1, "alpha": a1,
+                   "rgb0": rgb, "disp0": disp, "acc0": acc, "alpha0": a}
+        return out
+
+
+def nerf_loss(preds, target, bgs=None, use_background=False, coarse_weight=1.0):
+    """Trainer._compute_nerf_loss with loss_fn MSE (core/trainer.py:350-381): the rgb loss of the fine
+    and (weighted) coarse outputs, background composited with (1 - acc) when use_background."""
+    def one(rgb, acc):
+        if use_background:
+            rgb = rgb + (1.0 - acc)[..., None] * (1.0 if bgs is None else bgs)
+        return F.mse_loss(rgb, target, reduction="mean")
+    loss = one(preds["rgb_map"], preds["acc_map"])
+    if "rgb0" in preds:
+        loss = loss + one(preds["rgb0"], preds["acc0"]) * coarse_weight
+    return loss
+
+
+__all__ = ["TrainRayCaster", "NeRF", "nerf_loss", "RenderConfig"]

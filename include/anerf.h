@@ -22,6 +22,17 @@
  *   anerf_density_points    RayCaster.render_pts_density (fwd_type='density')  core/raycasters.py:597-648
  *   anerf_density_grid      RayCaster.render_mesh_density (fwd_type='mesh')    core/raycasters.py:579-595
  *                           (called by run_render.render_mesh)                 run_render.py:970-986
+ *   anerf_pose_kinematics   PoseOptLayer.calculate_kinematic, get_smpl_l2ws    core/pose_opt.py:372-521,
+ *                                                                              core/utils/skeleton_utils.py:296-376
+ *   anerf_kp_boxes          kp_to_valid_rays' cylinder + pixel box             core/utils/ray_utils.py:83-136
+ * Training stages of render_rays (perturb, raw noise, stochastic importance sampling, gradients):
+ *   anerf_train_samples     sample_from_lineseg (perturb > 0)                  core/utils/ray_utils.py:204-251
+ *   anerf_train_encode      sample_pts + encode_inputs (+ embedders)           core/raycasters.py:476-555, 650-663
+ *   anerf_train_encode_backward   autograd of the same to skts (pose opt.)     core/encoders.py:8-37, 101-193,
+ *                                                                              core/cutoff_embedder.py:111-174
+ *   anerf_train_composite   NeRF.raw2outputs with raw_noise_std                core/networks/nerf.py:150-205
+ *   anerf_train_composite_backward   its autograd
+ *   anerf_train_importance  isample_from_lineseg + sample_pdf(det=False) + sort core/utils/ray_utils.py:157-201, 255-289
  */
 #ifndef ANERF_H
 #define ANERF_H
@@ -33,7 +44,7 @@
 extern "C" {
 #endif
 
-#define ANERF_ABI_VERSION 2
+#define ANERF_ABI_VERSION 3
 
 enum {
     ANERF_OK = 0,
@@ -49,11 +60,12 @@ enum {
  *                     and computed as x_hi w_hi + x_hi w_lo + x_lo w_hi on v_mfma_f32_32x32x16_bf16
  *                     with fp32 accumulation (~16-bit operands, products exact): outputs within
  *                     1e-5 of the fp32 path on the reference fixtures; encoder and view parts fp32;
- *   ANERF_PREC_BF16X6 the dense hidden layers split three ways, x = x0 + x1 + x2 (bf16 RNE of the running
- *                     remainder, >= 24 significant bits, like fp32) and computed as the six products
+ *   ANERF_PREC_BF16X6 the dense hidden layers and the fused view layer split three ways: activations
+ *                     x = x0 + x1 + x2 exactly (truncation: 8 + 8 + 8 significant bits), weights
+ *                     w = w0 + w1 + w2 (bf16 RNE of the running remainder), computed as the six products
  *                     with i + j <= 2 of x_i w_j on v_mfma_f32_32x32x16_bf16, fp32 accumulation: the
- *                     dropped terms are below 2^-26 of each product, under fp32's own rounding of
- *                     a product (2^-24), so the contraction is fp32-accurate; encoder and view parts fp32. */
+ *                     dropped terms are below 2^-23 of each product (fp32 rounds a product to 2^-24),
+ *                     so the contraction is fp32-accurate; encoder, layer 0 and heads fp32. */
 enum { ANERF_PREC_FP32 = 0, ANERF_PREC_BF16X3 = 1, ANERF_PREC_BF16X6 = 2 };
 
 typedef struct anerf_model anerf_model;
@@ -220,6 +232,47 @@ int anerf_pose_kinematics(const float* bones, int32_t rot_dim, const float* rest
 int anerf_kp_boxes(const float* kps, const float* cyls_in, int64_t n_kp, int32_t n_joints, int32_t root_id,
                    double ext_scale, const float* w2cs, const float* focals, const int32_t* offsets, int64_t n_frames,
                    int32_t H, int32_t W, const double* cap_dirs, float* cyls_out, int32_t* boxes_out, void* stream);
+
+/* ---- Training stages.  All pointers are device pointers; random numbers are
+ * inputs (torch.rand / torch.randn draws of the caller), so a run can reproduce the reference's. */
+
+/* z [N][S] of sample_from_lineseg: linspace(near, far) (torch.linspace's float32 values), then with
+ * t_rand [N][S] (NULL: perturb = 0) lower + (upper - lower) t_rand inside the mid-point intervals. */
+int anerf_train_samples(const float* near_in, const float* far_in, int64_t n_rays, int32_t n_samples,
+                        const float* t_rand, float* z_out, void* stream);
+
+/* Features feat_out [N][S][F] (the layout of anerf_encode_points) of the points o + d z of the rays
+ * ray_batch [N][ray_stride] (o = cols 0-2, d = cols 3-5) at z [N][S]; the rays' skeletons are
+ * skts [n_poses][NJ][4][4] with ray_pose [N] (NULL: one skeleton per ray, n_poses == N). */
+int anerf_train_encode(const anerf_model* m, const float* ray_batch, int32_t ray_stride, int64_t n_rays,
+                       const float* z, int32_t n_samples, const float* skts, int32_t n_poses, const int32_t* ray_pose,
+                       float* feat_out, void* stream);
+
+/* dL/dskts of anerf_train_encode given dL/dfeat [N][S][F], ACCUMULATED into grad_skts
+ * [n_poses][NJ][4][4] (row 3 of every transform untouched; the caller zeroes the buffer). */
+int anerf_train_encode_backward(const anerf_model* m, const float* ray_batch, int32_t ray_stride, int64_t n_rays,
+                                const float* z, int32_t n_samples, const float* skts, int32_t n_poses,
+                                const int32_t* ray_pose, const float* grad_feat, float* grad_skts, void* stream);
+
+/* raw2outputs of raw [N][S][4] at z [N][S] with noise [N][S] (= randn * raw_noise_std * B, added to
+ * raw_sigma / B; NULL: none): rgb [N][3], disp [N], acc [N], weights, alpha and the exclusive
+ * transmittance trans [N][S] (kept for the backward). */
+int anerf_train_composite(const anerf_model* m, const float* raw, const float* z, const float* ray_batch,
+                          int32_t ray_stride, int64_t n_rays, int32_t n_samples, const float* noise, float* rgb,
+                          float* disp, float* acc, float* weights, float* alpha, float* trans, void* stream);
+
+/* g_raw [N][S][4] from the gradients of the outputs of anerf_train_composite (g_rgb [N][3], g_disp,
+ * g_acc [N], g_weights, g_alpha [N][S]; any may be NULL = zero) and its saved weights/alpha/trans. */
+int anerf_train_composite_backward(const anerf_model* m, const float* raw, const float* z, const float* ray_batch,
+                                   int32_t ray_stride, int64_t n_rays, int32_t n_samples, const float* noise,
+                                   const float* weights, const float* alpha, const float* trans, const float* g_rgb,
+                                   const float* g_disp, const float* g_acc, const float* g_weights,
+                                   const float* g_alpha, float* g_raw, void* stream);
+
+/* z_all [N][S+I] (sorted) of isample_from_lineseg: sample_pdf over the mid-points with the coarse
+ * weights [N][S] at u [N][I] (NULL: det=True, torch.linspace), merged with z [N][S]. */
+int anerf_train_importance(const float* z, const float* weights, int64_t n_rays, int32_t n_samples,
+                           int32_t n_importance, const float* u, float* z_all, void* stream);
 
 #ifdef __cplusplus
 }

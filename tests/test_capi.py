@@ -24,7 +24,9 @@ def test_header_declares_expected_entry_points():
     for f in ("anerf_model_create", "anerf_render_rays", "anerf_gen_rays", "anerf_near_far", "anerf_compose",
               "anerf_encode_points", "anerf_workspace_size", "anerf_last_error", "anerf_abi_version",
               "anerf_density_points", "anerf_density_grid", "anerf_gen_rays_box", "anerf_compose_box",
-              "anerf_pose_kinematics", "anerf_kp_boxes"):
+              "anerf_pose_kinematics", "anerf_kp_boxes", "anerf_train_samples", "anerf_train_encode",
+              "anerf_train_encode_backward", "anerf_train_composite", "anerf_train_composite_backward",
+              "anerf_train_importance"):
         assert f in fns
 
 
