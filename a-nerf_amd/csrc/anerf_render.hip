@@ -423,7 +423,8 @@ int anerf_train_encode(const anerf_model* m, const float* ray_batch, int32_t ray
     if (!feat_out) return fail(ANERF_EINVAL, "anerf_train_encode: feat_out is NULL");
     if (n_rays == 0) return ANERF_OK;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    hipLaunchKernelGGL(train_encode_kernel, dim3(blocks_of(n_rays * n_samples, 128)), dim3(128), 0, st, m->md,
+    hipLaunchKernelGGL(train_encode_kernel, dim3(blocks_of(n_rays * n_samples * m->desc.n_joints, 256)), dim3(256), 0,
+                       st, m->md,
                        ray_batch, ray_stride, n_rays, z, n_samples, skts, ray_pose, feat_out);
     HIP_TRY(hipGetLastError());
     return ANERF_OK;
@@ -436,9 +437,10 @@ int anerf_train_encode_backward(const anerf_model* m, const float* ray_batch, in
     if (rc) return rc;
     if (!grad_feat || !grad_skts) return fail(ANERF_EINVAL, "anerf_train_encode_backward: NULL gradient");
     if (n_rays == 0) return ANERF_OK;
-    if (n_rays > 0x7fffffff) return fail(ANERF_EINVAL, "too many rays for one launch");
+    const int64_t nb = n_rays * ((m->desc.n_joints + 3) / 4);
+    if (nb > 0x7fffffff) return fail(ANERF_EINVAL, "too many rays for one launch");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    hipLaunchKernelGGL(train_encode_backward_kernel, dim3((unsigned)n_rays), dim3(64), 0, st, m->md, ray_batch,
+    hipLaunchKernelGGL(train_encode_backward_kernel, dim3((unsigned)nb), dim3(256), 0, st, m->md, ray_batch,
                        ray_stride, n_rays, z, n_samples, skts, ray_pose, grad_feat, grad_skts);
     HIP_TRY(hipGetLastError());
     return ANERF_OK;

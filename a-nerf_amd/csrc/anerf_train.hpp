@@ -32,19 +32,61 @@ __global__ void train_z_kernel(const float* __restrict__ nearp, const float* __r
 
 // encode_inputs over a ray batch: sample s of ray i at p = o + d z (sample_pts,
 // raycasters.py:650-663), pose ray_pose[i] (or i when per_ray), feature row [v | r | d] of
-// encode_row.  One thread per sample.
+// encode_row.  One thread per (sample, joint): consecutive lanes are consecutive joints, so every
+// feature k (layout k NJ + j) is written by contiguous lanes.
+__device__ __forceinline__ void encode_joint(const ModelDev& M, const float* __restrict__ S, int j, float px,
+                                             float py, float pz, float dx, float dy, float dz, float* __restrict__ f) {
+    const int nj = M.nj, nv = 1 + 2 * M.mr;
+    const int cx = nj * nv + 3 * nj;
+    float qx, qy, qz;
+    joint_local(S, px, py, pz, qx, qy, qz);
+    const float dist = norm3(qx, qy, qz);
+    const float dn = fmaxf(dist, 1e-12f);
+    const float w = M.use_cutoff ? cutoff_w(M.tau, dist, M.cutoff[j]) : 1.0f;
+    f[j] = (M.use_cutoff && M.cutoff_inputs) ? dist * w : dist;
+    for (int fi = 0; fi < M.mr; ++fi) {
+        float s, c;
+        sincos_rr(dist * (float)(1 << fi), s, c);
+        f[(1 + 2 * fi) * nj + j] = s * w;
+        f[(2 + 2 * fi) * nj + j] = c * w;
+    }
+    f[nj * nv + 3 * j + 0] = qx / dn;
+    f[nj * nv + 3 * j + 1] = qy / dn;
+    f[nj * nv + 3 * j + 2] = qz / dn;
+    float ex, ey, ez;
+    joint_rot(S, dx, dy, dz, ex, ey, ez);
+    const float en = fmaxf(norm3(ex, ey, ez), 1e-12f);
+    const float e[3] = {ex / en, ey / en, ez / en};
+    const float wv = M.cutoff_viewdir ? cutoff_w(M.tau_v, dist, M.cutoff_v[j]) : 1.0f;
+    for (int c = 0; c < 3; ++c) {
+        f[cx + 3 * j + c] = (M.cutoff_viewdir && M.cutoff_inputs) ? e[c] * wv : e[c];
+        for (int fi = 0; fi < M.mrv; ++fi) {
+            float s, co;
+            sincos_rr(e[c] * (float)(1 << fi), s, co);
+            f[cx + (1 + 2 * fi) * 3 * nj + 3 * j + c] = s * wv;
+            f[cx + (2 + 2 * fi) * 3 * nj + 3 * j + c] = co * wv;
+        }
+    }
+}
+
 __global__ void train_encode_kernel(ModelDev M, const float* __restrict__ rb, int stride, int64_t n,
                                     const float* __restrict__ z, int ns, const float* __restrict__ skts,
                                     const int32_t* __restrict__ ray_pose, float* __restrict__ feat) {
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= n * ns) return;
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int nj = M.nj;
+    if (t >= n * ns * nj) return;
+    const int64_t idx = t / nj;
+    const int j = (int)(t % nj);
     const int64_t i = idx / ns;
     const int64_t pose = ray_pose ? ray_pose[i] : i;
     const float* ray = rb + i * stride;
     const float zz = z[idx];
     const float px = ray[0] + ray[3] * zz, py = ray[1] + ray[4] * zz, pz = ray[2] + ray[5] * zz;
-    const int F = M.nj * (1 + 2 * M.mr) + 3 * M.nj + 3 * M.nj * (1 + 2 * M.mrv);
-    encode_row(M, skts + pose * M.nj * 16, px, py, pz, ray[3], ray[4], ray[5], feat + idx * F);
+    const int F = nj * (1 + 2 * M.mr) + 3 * nj + 3 * nj * (1 + 2 * M.mrv);
+    const f32x4* sp = reinterpret_cast<const f32x4*>(skts + (pose * nj + j) * 16);
+    const f32x4 r0 = sp[0], r1 = sp[1], r2 = sp[2];
+    const float S[12] = {r0[0], r0[1], r0[2], r0[3], r1[0], r1[1], r1[2], r1[3], r2[0], r2[1], r2[2], r2[3]};
+    encode_joint(M, S, j, px, py, pz, ray[3], ray[4], ray[5], feat + idx * F);
 }
 
 // d feature / d inputs of encode_row for one (sample, joint): accumulates dL/dS[0:3, 0:4] (12
@@ -73,7 +115,7 @@ __device__ __forceinline__ void encode_row_grad_joint(const ModelDev& M, const f
     for (int fi = 0; fi < M.mr; ++fi) {
         const float fr = (float)(1 << fi);
         float s, c;
-        sincosf(dist * fr, &s, &c);
+        sincos_rr(dist * fr, s, c);
         const float gs = g[(1 + 2 * fi) * nj + j], gc = g[(2 + 2 * fi) * nj + j];
         g_w += gs * s + gc * c;
         g_dist += (gs * c - gc * s) * w * fr;
@@ -115,7 +157,7 @@ __device__ __forceinline__ void encode_row_grad_joint(const ModelDev& M, const f
         for (int fi = 0; fi < M.mrv; ++fi) {
             const float fr = (float)(1 << fi);
             float s, co;
-            sincosf(e[c] * fr, &s, &co);
+            sincos_rr(e[c] * fr, s, co);
             const float gs = g[cx + (1 + 2 * fi) * 3 * nj + 3 * j + c], gc = g[cx + (2 + 2 * fi) * 3 * nj + 3 * j + c];
             g_wv += gs * s + gc * co;
             ge[c] += (gs * co - gc * s) * wv * fr;
@@ -150,37 +192,37 @@ __device__ __forceinline__ void encode_row_grad_joint(const ModelDev& M, const f
     }
 }
 
-// Encoder backward: dL/dskts from dL/dfeat.  One wave per ray (its samples over the lanes), per
-// joint a wave reduction of the 12 sums, accumulated into grad_skts[pose] (atomic: rays may
-// share a pose).  grad_skts rows 3 (the [0 0 0 1] row) get no gradient, as in the reference.
-__global__ __launch_bounds__(64) void train_encode_backward_kernel(ModelDev M, const float* __restrict__ rb,
-                                                                   int stride, int64_t n, const float* __restrict__ z,
-                                                                   int ns, const float* __restrict__ skts,
-                                                                   const int32_t* __restrict__ ray_pose,
-                                                                   const float* __restrict__ gfeat,
-                                                                   float* __restrict__ gskts) {
-    const int64_t i = blockIdx.x;
-    if (i >= n) return;
-    const int lane = threadIdx.x;
+// Encoder backward: dL/dskts from dL/dfeat.  Block = (ray, 4 joints), one wave per joint with the
+// ray's samples over the lanes; a wave reduction of the 12 sums per joint, accumulated into
+// grad_skts[pose] (atomic: rays may share a pose).  Rows 3 (the [0 0 0 1] row) get no gradient,
+// as in the reference.
+__global__ __launch_bounds__(256) void train_encode_backward_kernel(ModelDev M, const float* __restrict__ rb,
+                                                                    int stride, int64_t n, const float* __restrict__ z,
+                                                                    int ns, const float* __restrict__ skts,
+                                                                    const int32_t* __restrict__ ray_pose,
+                                                                    const float* __restrict__ gfeat,
+                                                                    float* __restrict__ gskts) {
+    const int ngrp = (M.nj + 3) / 4;
+    const int64_t i = blockIdx.x / ngrp;
+    const int j = (int)(blockIdx.x % ngrp) * 4 + (threadIdx.x >> 6);
+    if (i >= n || j >= M.nj) return;
+    const int lane = threadIdx.x & 63;
     const int64_t pose = ray_pose ? ray_pose[i] : i;
     const float* ray = rb + i * stride;
     const int F = M.nj * (1 + 2 * M.mr) + 3 * M.nj + 3 * M.nj * (1 + 2 * M.mrv);
-    const float* Sp = skts + pose * M.nj * 16;
-    for (int j = 0; j < M.nj; ++j) {
-        float S[12];
-        for (int r = 0; r < 3; ++r)
-            for (int c = 0; c < 4; ++c) S[4 * r + c] = Sp[j * 16 + 4 * r + c];
-        float gS[12] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-        for (int s = lane; s < ns; s += 64) {
-            const float zz = z[i * ns + s];
-            const float px = ray[0] + ray[3] * zz, py = ray[1] + ray[4] * zz, pz = ray[2] + ray[5] * zz;
-            encode_row_grad_joint(M, S, j, px, py, pz, ray[3], ray[4], ray[5], gfeat + (i * ns + s) * F, gS);
-        }
+    const f32x4* sp = reinterpret_cast<const f32x4*>(skts + (pose * M.nj + j) * 16);
+    const f32x4 r0 = sp[0], r1 = sp[1], r2 = sp[2];
+    const float S[12] = {r0[0], r0[1], r0[2], r0[3], r1[0], r1[1], r1[2], r1[3], r2[0], r2[1], r2[2], r2[3]};
+    float gS[12] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    for (int s = lane; s < ns; s += 64) {
+        const float zz = z[i * ns + s];
+        const float px = ray[0] + ray[3] * zz, py = ray[1] + ray[4] * zz, pz = ray[2] + ray[5] * zz;
+        encode_row_grad_joint(M, S, j, px, py, pz, ray[3], ray[4], ray[5], gfeat + (i * ns + s) * F, gS);
+    }
 #pragma unroll
-        for (int k = 0; k < 12; ++k) {
-            const float v = wave_sum(gS[k]);
-            if (lane == 0 && v != 0.0f) atomicAdd(gskts + (pose * M.nj + j) * 16 + k, v);
-        }
+    for (int k = 0; k < 12; ++k) {
+        const float v = wave_sum(gS[k]);
+        if (lane == 0 && v != 0.0f) atomicAdd(gskts + (pose * M.nj + j) * 16 + k, v);
     }
 }
 

@@ -96,6 +96,40 @@ class _Composite(torch.autograd.Function):
 
 
 # ----------------------------------------------------------------------------- networks
+def _splitk_wgrad(gy, x):
+    """gy^T x for the weight gradient of a linear layer over M = rays x samples rows: M is in the
+    hundred-thousands and out x in is at most 256 x 1080, so one GEMM has too few output tiles to
+    fill 256 CUs; split M into c slabs (a batched GEMM) and sum the c partial products."""
+    m = gy.shape[0]
+    c = 1
+    while c < 64 and m % (2 * c) == 0 and m // (2 * c) >= 1024:
+        c *= 2
+    if c == 1:
+        return gy.t().mm(x)
+    return torch.bmm(gy.reshape(c, m // c, -1).transpose(1, 2), x.reshape(c, m // c, -1)).sum(0)
+
+
+class _Linear(torch.autograd.Function):
+    """F.linear whose weight gradient is a split-M batched GEMM (_splitk_wgrad)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.has_b = b is not None
+        return F.linear(x, w, b)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        gx = gy.mm(w) if ctx.needs_input_grad[0] else None
+        gw = _splitk_wgrad(gy, x) if ctx.needs_input_grad[1] else None
+        gb = gy.sum(0) if ctx.has_b and ctx.needs_input_grad[2] else None
+        return gx, gw, gb
+
+
+def _lin(x, w, b=None):
+    return _Linear.apply(x, w, b)
+
 class Optcodes(nn.Module):
     """core/networks/embedding.py:6-46 (training: codes(idx); eval with all idx < 0: the mean code)."""
 
@@ -136,19 +170,19 @@ class NeRF(nn.Module):
         h = x
         for i, lin in enumerate(self.pts_linears):
             if i > 0 and (i - 1) in self.skips:  # cat([input_pts, h]) @ W.T = x @ Wx.T + h @ Wh.T
-                h = F.relu(F.linear(x, lin.weight[:, :self.dnet]) + F.linear(h, lin.weight[:, self.dnet:], lin.bias))
+                h = F.relu(_lin(x, lin.weight[:, :self.dnet]) + _lin(h, lin.weight[:, self.dnet:], lin.bias))
             else:
-                h = F.relu(lin(h))
-        alpha = self.alpha_linear(h)
-        feature = self.feature_linear(h)
+                h = F.relu(_lin(h, lin.weight, lin.bias))
+        alpha = _lin(h, self.alpha_linear.weight, self.alpha_linear.bias)
+        feature = _lin(h, self.feature_linear.weight, self.feature_linear.bias)
         W = feature.shape[1]
         vl = self.views_linears[0]
         nv = self.cfg.input_ch_views
-        g = F.linear(feature, vl.weight[:, :W]) + F.linear(views, vl.weight[:, W:W + nv], vl.bias)
+        g = _lin(feature, vl.weight[:, :W]) + _lin(views, vl.weight[:, W:W + nv], vl.bias)
         if self.cfg.opt_framecode:
-            g = g + F.linear(self.framecodes(cams), vl.weight[:, W + nv:])
+            g = g + _lin(self.framecodes(cams), vl.weight[:, W + nv:])
         g = F.relu(g)
-        rgb = self.rgb_linear(g)
+        rgb = _lin(g, self.rgb_linear.weight, self.rgb_linear.bias)
         return torch.cat([rgb, alpha], -1)
 
 

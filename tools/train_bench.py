@@ -1,0 +1,97 @@
+"""Training-step benchmark at the reference's training configuration
+(configs/surreal/surreal.txt: N_rand 2048 rays, N_samples 64, N_importance 16, 8x256 nets,
+raw_noise_std 1, perturb 1, rays drawn from N_sample_images 128 images, i.e. 128 skeletons with pose
+optimisation on): one step = render_rays forward + the MSE/background loss + backward (networks and
+the per-image skeleton deltas) + Adam.  Synthetic scene and seeded weights.
+
+Prints one JSON line: training rays/s, steps/s, the MLP's GEMM FLOPs (3 x forward: the input
+gradient is needed for the pose gradient) and their rate against the FP32 matrix peak.
+Usage: python tools/train_bench.py [--steps K] [--warmup W] [--rays N]
+"""
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+FP32_MFMA_PEAK_TFLOPS = 157.3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--rays", type=int, default=2048)
+    ap.add_argument("--images", type=int, default=128)
+    ap.add_argument("--samples", type=int, default=64)
+    ap.add_argument("--importance", type=int, default=16)
+    a = ap.parse_args()
+    anerf = importlib.import_module("a-nerf_amd")
+    syn = importlib.import_module("a-nerf_amd.synthetic")
+    train = importlib.import_module("a-nerf_amd.train")
+    dev = torch.device("cuda:0")
+    S, I, n = a.samples, a.importance, a.rays
+    cfg = anerf.RenderConfig(N_samples=S, N_importance=I).validate()
+    ck = syn.make_checkpoint(13, n_joints=24, D=8, W=256, fine=True, tau=20.0)
+    sc = syn.make_scene(n_joints=24, H=512, W=512, seed=13, n_frames=a.images, yaw_step=2 * np.pi / a.images)
+    idx, cyls, _ = anerf.rays.valid_pixels(sc["c2ws"], 512, 512, sc["focal"], kps=sc["kps"], ext_scale=0.001)
+    rng = np.random.default_rng(0)
+    tr = train.TrainRayCaster(cfg, ck).train()
+    skts = torch.from_numpy(sc["skts"]).to(dev)
+    delta = torch.zeros_like(skts, requires_grad=True)  # pose optimisation variable per image
+    opt = torch.optim.Adam(list(tr.parameters()) + [delta], lr=5e-4)
+
+    def batch():
+        img = rng.integers(0, a.images, n)
+        rays = np.empty((n, 11), np.float32)
+        for f in np.unique(img):
+            sel = np.nonzero(img == f)[0]
+            pix = rng.choice(idx[f], len(sel))
+            y, x = pix // 512, pix % 512
+            c2w = sc["c2ws"][f].astype(np.float64)
+            d = np.stack([(x - 256.0) / sc["focal"], -(y - 256.0) / sc["focal"], -np.ones(len(sel))], -1) @ c2w[:3, :3].T
+            rays[sel, 0:3] = c2w[:3, 3]
+            rays[sel, 3:6] = d
+            rays[sel, 8:11] = d / np.linalg.norm(d, axis=-1, keepdims=True)
+        rays[:, 6], rays[:, 7] = 0.0, 1.0
+        return (torch.from_numpy(rays).to(dev), torch.from_numpy(img).to(dev),
+                torch.from_numpy(cyls[img]).to(dev), torch.rand(n, 3, device=dev))
+
+    batches = [batch() for _ in range(4)]
+
+    def step(b):
+        rb, img, cy, tgt = b
+        opt.zero_grad(set_to_none=True)
+        out = tr.render_rays(rb, S, skts=(skts + delta)[img], cyls=cy, perturb=1.0, N_importance=I,
+                             raw_noise_std=1.0)
+        loss = train.nerf_loss(out, tgt, bgs=1.0, use_background=True)
+        loss.backward()
+        opt.step()
+        return loss
+
+    for i in range(a.warmup):
+        step(batches[i % 4])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        step(batches[i % 4])
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / a.steps
+    flop = 3 * anerf.flops_per_sample(cfg) * n * anerf.samples_per_ray(cfg)
+    print(json.dumps({
+        "metric": "training rays/s (render_rays fwd + loss + bwd + Adam; N_rand 2048, 64+16 samples, 8x256, "
+                  "128 images with pose optimisation)",
+        "value": round(n / dt, 1), "unit": "rays/s", "ms_per_step": round(1e3 * dt, 3), "steps": a.steps,
+        "dtype": "fp32", "mlp_gemm_flop_per_step": flop, "mlp_tflops": round(flop / dt / 1e12, 2),
+        "frac_of_fp32_mfma_peak": round(flop / dt / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4),
+        "data": "synthetic (seeded SMPL-24 poses, 128 cameras on a circle, seeded weights)"}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
