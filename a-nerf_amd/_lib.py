@@ -95,6 +95,12 @@ SIGNATURES = {
                                              ctypes.c_int64, ctypes.c_void_p, ctypes.c_float, c_i32p,
                                              ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p,
                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "anerf_pose_kinematics_backward": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+                                                      ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_float,
+                                                      c_i32p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64,
+                                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                      ctypes.c_void_p]),
     "anerf_kp_boxes": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
                                       ctypes.c_int32, ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,

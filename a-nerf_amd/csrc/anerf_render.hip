@@ -562,20 +562,17 @@ int anerf_density_grid(const anerf_model* m, const float* axis, int32_t res1, co
     return launch_density(m, a, precision, stream);
 }
 
-int anerf_pose_kinematics(const float* bones, int32_t rot_dim, const float* rest, const int32_t* rest_idx,
-                          int64_t n_rest, const float* pelvis, float scale, const int32_t* parents, int32_t n_joints,
-                          int32_t root_id, int64_t n_frames, float* kps, float* skts, float* l2ws, float* rots,
-                          void* stream) {
-    if (n_frames < 0 || n_joints < 1 || n_joints > KIN_MAX_JOINTS || root_id < 0 || root_id >= n_joints || !parents)
-        return fail(ANERF_EINVAL, "anerf_pose_kinematics: bad skeleton arguments");
+// skeleton tables of KinArgs: parents must form a tree rooted at root_id (any index order)
+static int kin_setup(KinArgs& a, int32_t rot_dim, const int32_t* parents, int32_t n_joints, int32_t root_id,
+                     const char* who) {
+    if (n_joints < 1 || n_joints > KIN_MAX_JOINTS || root_id < 0 || root_id >= n_joints || !parents)
+        return fail(ANERF_EINVAL, std::string(who) + ": bad skeleton arguments");
     if (rot_dim != 3 && rot_dim != 6 && rot_dim != 9)
-        return fail(ANERF_EINVAL, "anerf_pose_kinematics: rot_dim must be 3 (axis-angle), 6 (6-D) or 9 (matrix)");
-    KinArgs a{};
-    // depth of every joint; parents must form a tree rooted at root_id
+        return fail(ANERF_EINVAL, std::string(who) + ": rot_dim must be 3 (axis-angle), 6 (6-D) or 9 (matrix)");
     int depth[KIN_MAX_JOINTS];
     for (int j = 0; j < n_joints; ++j) {
         if (j != root_id && (parents[j] < 0 || parents[j] >= n_joints || parents[j] == j))
-            return fail(ANERF_EINVAL, "anerf_pose_kinematics: parent index out of range");
+            return fail(ANERF_EINVAL, std::string(who) + ": parent index out of range");
         depth[j] = -1;
     }
     depth[root_id] = 0;
@@ -583,7 +580,7 @@ int anerf_pose_kinematics(const float* bones, int32_t rot_dim, const float* rest
     for (int j = 0; j < n_joints; ++j) {
         int k = j, steps = 0;
         while (depth[k] < 0 && steps <= n_joints) { k = parents[k]; ++steps; }
-        if (depth[k] < 0) return fail(ANERF_EINVAL, "anerf_pose_kinematics: parents contain a cycle");
+        if (depth[k] < 0) return fail(ANERF_EINVAL, std::string(who) + ": parents contain a cycle");
         int d = depth[k] + steps;  // assign depths along the path j -> k
         for (int u = j; depth[u] < 0; u = parents[u]) depth[u] = d--;
     }
@@ -592,17 +589,55 @@ int anerf_pose_kinematics(const float* bones, int32_t rot_dim, const float* rest
         a.depth[j] = (uint8_t)depth[j];
         max_depth = std::max(max_depth, depth[j]);
     }
+    a.rot_dim = rot_dim;
+    a.nj = n_joints;
+    a.root = root_id;
+    a.max_depth = max_depth;
+    return ANERF_OK;
+}
+
+int anerf_pose_kinematics(const float* bones, int32_t rot_dim, const float* rest, const int32_t* rest_idx,
+                          int64_t n_rest, const float* pelvis, float scale, const int32_t* parents, int32_t n_joints,
+                          int32_t root_id, int64_t n_frames, float* kps, float* skts, float* l2ws, float* rots,
+                          void* stream) {
+    if (n_frames < 0) return fail(ANERF_EINVAL, "anerf_pose_kinematics: n_frames < 0");
+    KinArgs a{};
+    int rc = kin_setup(a, rot_dim, parents, n_joints, root_id, "anerf_pose_kinematics");
+    if (rc) return rc;
     if (n_frames == 0) return ANERF_OK;
     if (!bones || !rest || n_rest < 1 || (!kps && !skts && !l2ws && !rots))
         return fail(ANERF_EINVAL, "anerf_pose_kinematics: bad buffers");
     a.bones = bones; a.rest = rest; a.rest_idx = rest_idx; a.pelvis = pelvis;
     a.kps = kps; a.skts = skts; a.l2ws = l2ws; a.rots = rots;
-    a.n_frames = n_frames; a.n_rest = n_rest; a.scale = scale; a.rot_dim = rot_dim;
-    a.nj = n_joints; a.root = root_id; a.max_depth = max_depth;
+    a.n_frames = n_frames; a.n_rest = n_rest; a.scale = scale;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const size_t lds = sizeof(double) * 12 * n_joints * KIN_WAVES;
     hipLaunchKernelGGL(pose_kinematics_kernel, dim3((unsigned)((n_frames + KIN_WAVES - 1) / KIN_WAVES)),
                        dim3(64 * KIN_WAVES), lds, st, a);
+    HIP_TRY(hipGetLastError());
+    return ANERF_OK;
+}
+
+int anerf_pose_kinematics_backward(const float* bones, int32_t rot_dim, const float* rest, const int32_t* rest_idx,
+                                   int64_t n_rest, const float* pelvis, float scale, const int32_t* parents,
+                                   int32_t n_joints, int32_t root_id, int64_t n_frames, const float* g_kps,
+                                   const float* g_skts, const float* g_l2ws, const float* g_rots, float* g_bones,
+                                   float* g_pelvis, void* stream) {
+    if (n_frames < 0) return fail(ANERF_EINVAL, "anerf_pose_kinematics_backward: n_frames < 0");
+    KinArgs a{};
+    int rc = kin_setup(a, rot_dim, parents, n_joints, root_id, "anerf_pose_kinematics_backward");
+    if (rc) return rc;
+    if (n_frames == 0) return ANERF_OK;
+    if (!bones || !rest || n_rest < 1 || !g_bones) return fail(ANERF_EINVAL, "anerf_pose_kinematics_backward: bad buffers");
+    a.bones = bones; a.rest = rest; a.rest_idx = rest_idx; a.pelvis = pelvis;
+    a.n_frames = n_frames; a.n_rest = n_rest; a.scale = scale;
+    KinGradArgs g{g_kps, g_skts, g_l2ws, g_rots, g_bones, g_pelvis};
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const size_t lds = sizeof(double) * 36 * n_joints * KINB_WAVES;
+    HIP_TRY(hipFuncSetAttribute((const void*)pose_kinematics_backward_kernel,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(pose_kinematics_backward_kernel, dim3((unsigned)((n_frames + KINB_WAVES - 1) / KINB_WAVES)),
+                       dim3(64 * KINB_WAVES), lds, st, a, g);
     HIP_TRY(hipGetLastError());
     return ANERF_OK;
 }

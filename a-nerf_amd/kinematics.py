@@ -4,8 +4,11 @@
 
 All of them reduce to one C-ABI call, `anerf_pose_kinematics` (include/anerf.h): a batched
 kinematic chain + inverse that produces the `skts` / `kps` the render path consumes, on the
-device, for any number of frames.  Forward only (the reference's pose optimisation needs the
-backward pass, a §8(f) row-2 item): tensors here carry no autograd graph.
+device, for any number of frames.  It is differentiable: `anerf_pose_kinematics_backward`
+(the reference's autograd through the chain and torch.inverse) takes the gradients of
+kps / skts / l2ws / rots back to the rotation parameters and the pelvis, so PoseOptLayer is an
+nn.Module whose `bones` / `pelvis` (/ `root_bones`) are trained by A-NeRF's pose optimisation
+together with the training render path (a-nerf_amd/train.py).
 
 Differences from the reference, by design:
 * any tree skeleton up to 128 joints with any root (the reference's PoseOptLayer accepts only
@@ -49,17 +52,64 @@ def _dev_f32(x, device):
     return torch.as_tensor(np.ascontiguousarray(x, dtype=np.float32), device=device)
 
 
+class _Kinematics(torch.autograd.Function):
+    """anerf_pose_kinematics with its backward (gradients to bones and pelvis)."""
+
+    @staticmethod
+    def forward(ctx, b, pel, rest, ridx, parents, root_id, scale, device, outputs):
+        lib = _lib.load()
+        F, nj = int(b.shape[0]), int(b.shape[1])
+        shapes = {"kps": (F, nj, 3), "skts": (F, nj, 4, 4), "l2ws": (F, nj, 4, 4), "rots": (F, nj, 3, 3)}
+        out = {k: torch.empty(shapes[k], dtype=torch.float32, device=device) for k in outputs}
+        with torch.cuda.device(device):
+            rc = lib.anerf_pose_kinematics(_lib.ptr(b), b.shape[-1], _lib.ptr(rest), _lib.ptr(ridx), rest.shape[0],
+                                           _lib.ptr(pel), float(scale), parents.ctypes.data_as(_lib.c_i32p), nj,
+                                           int(root_id), F, _lib.ptr(out.get("kps")), _lib.ptr(out.get("skts")),
+                                           _lib.ptr(out.get("l2ws")), _lib.ptr(out.get("rots")),
+                                           _lib.stream_handle(device))
+        _lib.check(rc, "anerf_pose_kinematics")
+        ctx.save_for_backward(b, pel if pel is not None else torch.empty(0), rest,
+                              ridx if ridx is not None else torch.empty(0))
+        ctx.meta = (pel is not None, ridx is not None, parents, root_id, scale, device, tuple(outputs))
+        return tuple(out[k] for k in outputs)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        b, pel, rest, ridx = ctx.saved_tensors
+        has_pel, has_ridx, parents, root_id, scale, device, outputs = ctx.meta
+        g = {k: (None if gk is None else gk.contiguous()) for k, gk in zip(outputs, grads)}
+        gb = torch.empty_like(b)
+        gp = torch.empty(b.shape[0], 3, dtype=torch.float32, device=device) if has_pel else None
+        lib = _lib.load()
+        with torch.cuda.device(device):
+            rc = lib.anerf_pose_kinematics_backward(
+                _lib.ptr(b), b.shape[-1], _lib.ptr(rest), _lib.ptr(ridx if has_ridx else None), rest.shape[0],
+                _lib.ptr(pel if has_pel else None), float(scale), parents.ctypes.data_as(_lib.c_i32p), int(b.shape[1]),
+                int(root_id), int(b.shape[0]), _lib.ptr(g.get("kps")), _lib.ptr(g.get("skts")),
+                _lib.ptr(g.get("l2ws")), _lib.ptr(g.get("rots")), _lib.ptr(gb), _lib.ptr(gp),
+                _lib.stream_handle(device))
+        _lib.check(rc, "anerf_pose_kinematics_backward")
+        return gb, gp, None, None, None, None, None, None, None
+
+
+def _dev_f32_grad(x, device):
+    """float32 contiguous device tensor that keeps the autograd graph of a tensor input."""
+    if isinstance(x, torch.Tensor):
+        return x.to(device=device, dtype=torch.float32).contiguous()
+    return torch.as_tensor(np.ascontiguousarray(x, dtype=np.float32), device=device)
+
+
 def pose_kinematics(bones, rest_pose, skel_type=SMPLSkeleton, pelvis=None, scale=1.0, rest_idx=None,
                     device=None, outputs=("kps", "skts", "l2ws", "rots")):
     """Batched kinematic chain: bones (F, NJ, 3|6|9) -> dict of float32 device tensors
     kps (F, NJ, 3), skts (F, NJ, 4, 4), l2ws (F, NJ, 4, 4), rots (F, NJ, 3, 3).
 
     rest_pose (NJ, 3) or (R, NJ, 3) with rest_idx (F,) selecting one per frame; pelvis (F, 3)
-    is added to every joint's translation; rest offsets are scaled by `scale`."""
+    is added to every joint's translation; rest offsets are scaled by `scale`.  Differentiable
+    w.r.t. `bones` and `pelvis` when they are tensors that require grad."""
     if device is None:
         device = bones.device if isinstance(bones, torch.Tensor) and bones.is_cuda else torch.device("cuda", 0)
-    lib = _lib.load()
-    b = _dev_f32(bones, device)
+    b = _dev_f32_grad(bones, device)
     if b.dim() != 3 or b.shape[-1] not in (3, 6, 9):
         raise ValueError("bones must be (F, NJ, 3 | 6 | 9)")
     F, nj = int(b.shape[0]), int(b.shape[1])
@@ -73,23 +123,13 @@ def pose_kinematics(bones, rest_pose, skel_type=SMPLSkeleton, pelvis=None, scale
         if rest.shape[0] != F:
             raise ValueError("rest_pose (R, NJ, 3) needs rest_idx unless R == F")
         ridx = torch.arange(F, dtype=torch.int32, device=device)
-    pel = None if pelvis is None else _dev_f32(pelvis, device).reshape(F, 3)
+    pel = None if pelvis is None else _dev_f32_grad(pelvis, device).reshape(F, 3)
     parents = np.ascontiguousarray(np.asarray(skel_type.joint_trees), dtype=np.int32)
     if parents.shape[0] != nj:
         raise ValueError(f"skeleton has {parents.shape[0]} joints, bones have {nj}")
-    out = {}
-    shapes = {"kps": (F, nj, 3), "skts": (F, nj, 4, 4), "l2ws": (F, nj, 4, 4), "rots": (F, nj, 3, 3)}
-    for k in outputs:
-        out[k] = torch.empty(shapes[k], dtype=torch.float32, device=device)
-    with torch.cuda.device(device):
-        rc = lib.anerf_pose_kinematics(_lib.ptr(b), b.shape[-1], _lib.ptr(rest), _lib.ptr(ridx), rest.shape[0],
-                                       _lib.ptr(pel), float(scale),
-                                       parents.ctypes.data_as(_lib.c_i32p), nj, int(skel_type.root_id), F,
-                                       _lib.ptr(out.get("kps")), _lib.ptr(out.get("skts")),
-                                       _lib.ptr(out.get("l2ws")), _lib.ptr(out.get("rots")),
-                                       _lib.stream_handle(device))
-    _lib.check(rc, "anerf_pose_kinematics")
-    return out
+    outs = _Kinematics.apply(b, pel, rest, ridx, parents, int(skel_type.root_id), float(scale), device,
+                             tuple(outputs))
+    return dict(zip(outputs, outs))
 
 
 def get_kinematic_chain_T(rest_pose, bones, skel_type=SMPLSkeleton):
@@ -109,15 +149,18 @@ def get_smpl_l2ws(pose, rest_pose=None, scale=1.0, skel_type=SMPLSkeleton):
     return o["l2ws"][0] if single else o["l2ws"]
 
 
-class PoseOptLayer:
-    """Forward path of the reference's PoseOptLayer (core/pose_opt.py:240-445) on the device.
+class PoseOptLayer(torch.nn.Module):
+    """The reference's PoseOptLayer (core/pose_opt.py:240-445) on the device, trainable: `pelvis`
+    (N, 3) and `bones` (N, NJ, 3|6) — with kp_map, `root_bones` (N, 3|6) and the shared per-view
+    `bones` (U, NJ-1, 3|6) — are nn.Parameters (pose_opt.py:276-295); calculate_kinematic runs the
+    batched chain + inverse with its backward (anerf_pose_kinematics[_backward]).
 
-    kps (N, NJ, 3), bones (N, NJ, 3) axis-angle, rest_pose (1 | R, NJ, 3).  With kp_map /
-    kp_uidxs (multi-view), root bones are per index and the other bones are shared through
-    kp_map (pose_opt.py:318-332).  use_rot6d stores the 6-D parameters (pose_opt.py:284-289)."""
+    kps (N, NJ, 3), bones (N, NJ, 3) axis-angle, rest_pose (1 | R, NJ, 3).  use_rot6d stores the
+    6-D parameters (pose_opt.py:284-289)."""
 
     def __init__(self, kps, bones, rest_pose, skel_type=SMPLSkeleton, kp_map=None, kp_uidxs=None, use_cache=False,
                  use_rot6d=False, beta=None, rest_pose_idxs=None, device=None):
+        super().__init__()
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.skel_type = skel_type
         self.root_id = skel_type.root_id
@@ -125,22 +168,25 @@ class PoseOptLayer:
         self.use_rot6d = use_rot6d
         self.rest_pose_idxs = None if rest_pose_idxs is None else np.asarray(rest_pose_idxs)
         self.beta = beta
-        self.rest_pose = _dev_f32(rest_pose, self.device).reshape(-1, len(skel_type.joint_trees), 3)
+        self.register_buffer("rest_pose",
+                             _dev_f32(rest_pose, self.device).reshape(-1, len(skel_type.joint_trees), 3))
         kps = _dev_f32(kps, self.device)
         bones = _dev_f32(bones, self.device)
-        self.pelvis = kps[:, self.root_id].contiguous()
+        self.pelvis = torch.nn.Parameter(kps[:, self.root_id].contiguous())
         if use_rot6d:
             nj = bones.shape[1]
-            rots = pose_kinematics(bones, self.rest_pose[:1], skel_type, outputs=("rots",))["rots"]
+            with torch.no_grad():
+                rots = pose_kinematics(bones, self.rest_pose[:1], skel_type, outputs=("rots",))["rots"]
             bones = rots[..., :3, :2].reshape(-1, nj, 6).contiguous()
         if kp_map is None:
             self.kp_map = self.kp_uidxs = None
-            self.bones = bones
+            self.bones = torch.nn.Parameter(bones)
         else:
-            self.kp_map = torch.as_tensor(np.asarray(kp_map), dtype=torch.long, device=self.device)
-            self.kp_uidxs = torch.as_tensor(np.asarray(kp_uidxs), dtype=torch.long, device=self.device)
-            self.root_bones = bones[:, self.root_id].contiguous()
-            self.bones = bones[self.kp_uidxs, self.root_id + 1:].contiguous()
+            self.register_buffer("kp_map", torch.as_tensor(np.asarray(kp_map), dtype=torch.long, device=self.device))
+            self.register_buffer("kp_uidxs",
+                                 torch.as_tensor(np.asarray(kp_uidxs), dtype=torch.long, device=self.device))
+            self.root_bones = torch.nn.Parameter(bones[:, self.root_id].contiguous())
+            self.bones = torch.nn.Parameter(bones[self.kp_uidxs, self.root_id + 1:].contiguous())
         self.N_kps = self.pelvis.shape[0]
         if use_cache:
             self.update_cache()
@@ -178,6 +224,7 @@ class PoseOptLayer:
         o = pose_kinematics(bone, rest, self.skel_type, pelvis=pelvis, rest_idx=ridx, device=self.device)
         return o["kps"], bone, o["skts"], o["l2ws"], o["rots"]
 
+    @torch.no_grad()
     def update_cache(self):
         self.cache_kps, self.cache_bones, self.cache_skts, self.cache_l2ws, self.cache_rots = \
             self.calculate_kinematic(np.arange(self.N_kps))
@@ -187,8 +234,6 @@ class PoseOptLayer:
             return self.calculate_kinematic(idxs, rest_pose_idxs)
         i = torch.as_tensor(np.asarray(idxs), dtype=torch.long, device=self.device)
         return self.cache_kps[i], self.cache_bones[i], self.cache_skts[i], self.cache_l2ws[i], self.cache_rots[i]
-
-    __call__ = forward
 
     def get_bones(self, idx=None):
         if self.use_rot6d:

@@ -23,6 +23,7 @@
  *   anerf_density_grid      RayCaster.render_mesh_density (fwd_type='mesh')    core/raycasters.py:579-595
  *                           (called by run_render.render_mesh)                 run_render.py:970-986
  *   anerf_pose_kinematics   PoseOptLayer.calculate_kinematic, get_smpl_l2ws    core/pose_opt.py:372-521,
+ *   anerf_pose_kinematics_backward   its autograd (pose optimisation)
  *                                                                              core/utils/skeleton_utils.py:296-376
  *   anerf_kp_boxes          kp_to_valid_rays' cylinder + pixel box             core/utils/ray_utils.py:83-136
  * Training stages of render_rays (perturb, raw noise, stochastic importance sampling, gradients):
@@ -218,6 +219,17 @@ int anerf_pose_kinematics(const float* bones, int32_t rot_dim, const float* rest
                           int64_t n_rest, const float* pelvis, float scale, const int32_t* parents, int32_t n_joints,
                           int32_t root_id, int64_t n_frames, float* kps, float* skts, float* l2ws, float* rots,
                           void* stream);
+
+/* Backward of anerf_pose_kinematics (the pose-optimisation gradient: PoseOptLayer's autograd,
+ * core/pose_opt.py:372-445 + torch.inverse): with the same inputs and the gradients of its outputs
+ * (g_kps [F][NJ][3], g_skts / g_l2ws [F][NJ][4][4], g_rots [F][NJ][3][3]; any may be NULL = zero),
+ * writes g_bones [F][NJ][rot_dim] and, when not NULL, g_pelvis [F][3] (overwritten, not accumulated).
+ * The chain is recomputed in float64. */
+int anerf_pose_kinematics_backward(const float* bones, int32_t rot_dim, const float* rest, const int32_t* rest_idx,
+                                   int64_t n_rest, const float* pelvis, float scale, const int32_t* parents,
+                                   int32_t n_joints, int32_t root_id, int64_t n_frames, const float* g_kps,
+                                   const float* g_skts, const float* g_l2ws, const float* g_rots, float* g_bones,
+                                   float* g_pelvis, void* stream);
 
 /* Bounding cylinder and 2-D pixel box of every frame on the device, the host
  * half of kp_to_valid_rays (core/utils/ray_utils.py:83-136): get_kp_bounding_cylinder

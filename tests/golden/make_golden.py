@@ -412,6 +412,44 @@ def kinematics_table(mods):
     print(f"wrote {path}")
 
 
+def kinematics_grad_table(mods):
+    """Pose-optimisation gradients from the reference's own autograd:
+    PoseOptLayer.calculate_kinematic on 6-D rotations (the axis-angle branch needs pytorch3d, absent
+    here) with repeated indices, loss = sum of seeded weights times kp, skts (all 16 entries, the
+    gradient torch.inverse propagates), l2ws and rots; stores d loss / d bones (6-D) and / d pelvis."""
+    import torch
+    po = importlib.import_module("core.pose_opt")
+    sk = mods[4]
+    rs = np.random.RandomState(4321)
+    F = 6
+    parents, rest24 = anerf_syn.skeleton(24)
+    rest = (rest24 * 0.7).astype(np.float32)[None]
+    bones6 = rs.normal(size=(F, 24, 6)).astype(np.float32)
+    pelvis = rs.normal(scale=0.5, size=(F, 3)).astype(np.float32)
+    L = po.PoseOptLayer.__new__(po.PoseOptLayer)   # __init__ would call pytorch3d's axis_angle_to_matrix
+    torch.nn.Module.__init__(L)
+    L.skel_type, L.use_cache, L.unroll_kinematic_chain, L.use_rot6d = sk.SMPLSkeleton, False, True, True
+    L.rest_pose_idxs, L.kp_map, L.kp_uidxs, L.root_id, L.N_kps = None, None, None, 0, F
+    L.register_buffer("rest_pose", torch.tensor(rest))
+    L.register_parameter("pelvis", torch.nn.Parameter(torch.tensor(pelvis)))
+    L.register_parameter("bones", torch.nn.Parameter(torch.tensor(bones6)))
+    idxs = np.array([3, 0, 5, 3, 1], dtype=np.int64)
+    kp, bone, skts, l2ws, rots = L.calculate_kinematic(idxs)
+    n = len(idxs)
+    w = {"kp": rs.normal(size=(n, 24, 3)), "skts": rs.normal(size=(n, 24, 4, 4)),
+         "l2ws": rs.normal(size=(n, 24, 4, 4)), "rots": rs.normal(size=(n, 24, 3, 3))}
+    w = {k: v.astype(np.float32) for k, v in w.items()}
+    loss = ((kp * torch.tensor(w["kp"])).sum() + (skts * torch.tensor(w["skts"])).sum() +
+            (l2ws * torch.tensor(w["l2ws"])).sum() + (rots * torch.tensor(w["rots"])).sum())
+    loss.backward()
+    rows = dict(bones6=bones6, pelvis=pelvis, rest=rest, idxs=idxs, loss=np.float64(loss.item()),
+                g_bones6=L.bones.grad.numpy(), g_pelvis=L.pelvis.grad.numpy(),
+                **{"w_" + k: v for k, v in w.items()})
+    path = os.path.join(HERE, "kinematics_grad.npz")
+    np.savez_compressed(path, **rows)
+    print(f"wrote {path}")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default=None)
@@ -428,6 +466,8 @@ def main():
         bbox_table(mods)
     if not a.only or a.only == "kinematics":
         kinematics_table(mods)
+    if not a.only or a.only == "kinematics_grad":
+        kinematics_grad_table(mods)
     if not a.only or a.only == "boxes_random":
         random_boxes_table(mods)
 
