@@ -196,6 +196,10 @@ def main():
             "roofline": {"bound": "mfma", "achieved": round(achieved_tf, 2), "peak": round(peak_tf, 1),
                          "unit": "TFLOP/s", "frac": round(achieved_tf / peak_tf, 4),
                          "traffic": traffic, "kernel_ms": round(kern_ms, 3),
+                         "launches_per_step": 2 if I > 0 else 1,
+                         "timing": "HIP events on the launch stream around anerf_render_rays: the coarse and the "
+                                   "fine render_kernel launch (+ near/far, 0.2 %); rocprofv3's render_kernel "
+                                   "average x launches_per_step agrees (profiles/)",
                          "flop": "executed MFMA FLOPs per launch (device counters) / launch time; peak = the "
                                  "FP32 (157.3) and BF16 (2516.6 TF) MFMA peaks weighted by this launch's mix",
                          "mfma_f32_per_launch": n_f32, "mfma_bf16_per_launch": n_bf16,

@@ -1,13 +1,15 @@
 #!/bin/bash
-# GPU-box session: bench (all precisions), parity tests, density bench, rocprofv3 kernel stats.
-# Each GPU step has its own limit; a crash/timeout ends the session (test failures, rc 1, do not).
+# GPU-box session: bench (all precisions + the default line with the CPU baseline), parity tests,
+# density bench, rocprofv3 kernel stats of the default bench, HBM PMC passes (default precision),
+# training bench + its kernel stats.  Each GPU step has its own limit; a crash/timeout ends the
+# session (test failures, rc 1, do not).
 #   TAG=r01_v6 bash tools/gpu_session.sh
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${TAG:-run}
-for p in ${PRECS:-fp32 bf16x6 bf16x3}; do
+for p in ${PRECS:-bf16x6 fp32 bf16x3}; do
   echo "== bench $p"
   timeout -k 10 300 python bench.py --no-cpu --precision $p > gpurun_out/${TAG}_bench_$p.json 2> gpurun_out/bench_$p.err || { tail -20 gpurun_out/bench_$p.err; exit 1; }
   cat gpurun_out/${TAG}_bench_$p.json
@@ -29,4 +31,10 @@ done
 echo "== rocprof"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o run --output-format csv -- python3 bench.py --steps 4 --warmup 1 --no-cpu > gpurun_out/prof.log 2>&1 || { echo "rocprof failed"; tail -20 gpurun_out/prof.log; exit 1; }
 find gpurun_out/prof_${TAG} -name "*stats*"
+echo "== pmc"
+PREC=bf16x6 bash tools/gpu_pmc.sh || exit 1
+echo "== train"
+timeout -k 10 300 python tools/train_bench.py > gpurun_out/${TAG}_train_bench.json 2> gpurun_out/train.err || { tail -20 gpurun_out/train.err; exit 1; }
+cat gpurun_out/${TAG}_train_bench.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_train_${TAG} -o run --output-format csv -- python3 tools/train_bench.py --steps 5 --warmup 1 > gpurun_out/prof_train.log 2>&1 || { echo "rocprof train failed"; tail -20 gpurun_out/prof_train.log; exit 1; }
 exit $rc

@@ -18,16 +18,24 @@ def rows(path, kernel="render_kernel"):
     return out
 
 
+def per_call(d, launches):
+    """sum every counter over the render_kernel dispatches, per render_rays call (`launches` launches)"""
+    tot = {}
+    for v in d.values():
+        for k, x in v.items():
+            tot[k] = tot.get(k, 0.0) + x
+    calls = len(d) / launches
+    return {k: x / calls for k, x in tot.items()}, int(calls)
+
+
 def main():
     base, out_path = sys.argv[1], sys.argv[2]
     label = sys.argv[3] if len(sys.argv) > 3 else ""
     prec = sys.argv[4] if len(sys.argv) > 4 else "fp32"
-    fetch = rows(os.path.join(base, "pmc_fetch", "run_counter_collection.csv"))
-    write = rows(os.path.join(base, "pmc_write", "run_counter_collection.csv"))
-    sq = rows(os.path.join(base, "pmc_sq", "run_counter_collection.csv"))
-    f = next(iter(fetch.values()))
-    w = next(iter(write.values()))
-    s = next(iter(sq.values()))
+    launches = int(sys.argv[5]) if len(sys.argv) > 5 else 2  # coarse + fine launch per render_rays call
+    f, calls = per_call(rows(os.path.join(base, "pmc_fetch", "run_counter_collection.csv")), launches)
+    w, _ = per_call(rows(os.path.join(base, "pmc_write", "run_counter_collection.csv")), launches)
+    s, _ = per_call(rows(os.path.join(base, "pmc_sq", "run_counter_collection.csv")), launches)
     hbm = 2 * f["FETCH_SIZE"] * 1024 + w["WRITE_SIZE"] * 1024
     clock = s["GRBM_GUI_ACTIVE"] / 8 / (s["ns"] * 1e-9) / 1e9
     busy = s["SQ_INSTS_MFMA"] / 1024 * 64 / (s["ns"] * 1e-9 * clock * 1e9)
@@ -35,12 +43,14 @@ def main():
         "kernel": "render_kernel<256,7> " + label,
         "precision": prec,
         "source": "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE | SQ_INSTS_VALU SQ_INSTS_MFMA SQ_WAVES SQ_BUSY_CYCLES "
-                  "GRBM_GUI_ACTIVE (separate passes) --kernel-trace -- python3 bench.py --steps 1 --warmup 0 --no-cpu --precision <precision>",
-        "dispatches": len(fetch),
+                  "GRBM_GUI_ACTIVE (separate passes) --kernel-trace -- python3 bench.py --steps 1 --warmup 0 --no-cpu "
+                  "--precision <precision>",
+        "unit": f"per render_rays call of one config-3 frame = {launches} render_kernel launches (coarse, fine); "
+                f"{calls} calls profiled",
         "FETCH_SIZE_KB_per_launch": f["FETCH_SIZE"],
         "WRITE_SIZE_KB_per_launch": w["WRITE_SIZE"],
         "render_kernel_hbm_bytes_per_launch": int(hbm),
-        "hbm_bytes_note": "2 x FETCH_SIZE x 1024 (gfx950 half-count correction) + WRITE_SIZE x 1024",
+        "hbm_bytes_note": "2 x FETCH_SIZE x 1024 (gfx950 half-count correction) + WRITE_SIZE x 1024, per call",
         "SQ_INSTS_MFMA": s["SQ_INSTS_MFMA"],
         "SQ_INSTS_VALU": s["SQ_INSTS_VALU"],
         "SQ_WAVES": s["SQ_WAVES"],
@@ -48,7 +58,7 @@ def main():
         "kernel_ns": s["ns"],
         "effective_clock_GHz": round(clock, 4),
         "mfma_pipe_busy_frac": round(busy, 4) if prec == "fp32" else None,
-        "mfma_busy_note": "SQ_INSTS_MFMA / 1024 SIMDs x 64 cycles (v_mfma_f32_32x32x2_f32) / (kernel time x clock)",
+        "mfma_busy_note": "fp32 only: SQ_INSTS_MFMA / 1024 SIMDs x 64 cycles (v_mfma_f32_32x32x2_f32) / (time x clock)",
         "valu_per_mfma": round(s["SQ_INSTS_VALU"] / s["SQ_INSTS_MFMA"], 3),
     }
     json.dump(res, open(out_path, "w"), indent=1)
