@@ -97,8 +97,8 @@ class RenderConfig:
         """Build from a run_nerf.config_parser() namespace (or anything with those attributes)."""
         g = lambda k, d=None: getattr(args, k, d)  # noqa: E731
         extra = {k: g(k) for k in ("normalize_cutoff", "cut_to_dist", "cutoff_shift", "freq_schedule",
-                                   "cutoff_bones", "kp_dist_type", "bone_type", "view_type", "pts_tr_type")
-                 if g(k) is not None}
+                                   "cutoff_bones", "kp_dist_type", "bone_type", "view_type", "pts_tr_type",
+                                   "cutoff_mm") if g(k) is not None}
         cfg = cls(n_joints=n_joints, netdepth=g("netdepth", 8), netwidth=g("netwidth", 256),
                   multires=g("multires", 7), multires_views=g("multires_views", 4),
                   multires_bones=g("multires_bones", 0), use_cutoff=bool(g("use_cutoff", True)),

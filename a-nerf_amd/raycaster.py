@@ -225,11 +225,35 @@ def load_checkpoint(path):
     return ck
 
 
+class _EvalView:
+    """render_kwargs_test's ray caster over a TrainRayCaster: always the fused eval kernel on the
+    CURRENT weights (the reference shares one module between its train and test kwargs)."""
+
+    def __init__(self, trainable):
+        self._t = trainable
+
+    @property
+    def model(self):
+        return self._t.eval_caster().model
+
+    def __call__(self, *args, **kwargs):
+        return self._t.eval_caster()(*args, **kwargs)
+
+    def __getattr__(self, name):
+        return getattr(self._t.eval_caster(), name)
+
+
 def create_raycaster(args, data_attrs, device=None, ckpt=None):
-    """Mirror of core/raycasters.py:17-184 for rendering.
+    """Mirror of core/raycasters.py:17-184.
 
     Returns (render_kwargs_train, render_kwargs_test, start, grad_vars, optimizer, ckpt) like the
-    reference; training objects are None (training is not implemented)."""
+    reference: the train kwargs hold a `train.TrainRayCaster` (the reference's perturb /
+    raw_noise_std flags), the test kwargs a view that renders the same weights with the fused eval
+    kernel; `optimizer` is Adam(lr=args.lrate, betas=(0.9, 0.999)) over the trainable parameters,
+    restored from the checkpoint unless `finetune` (load_ckpt_from_path,
+    core/utils/run_nerf_helpers.py:6-17).  Without a checkpoint (or with no_reload) the networks
+    start from torch's default initialisation, as in the reference."""
+    from .train import TrainRayCaster
     skel = data_attrs["skel_type"]
     nj = len(skel.joint_names) if hasattr(skel, "joint_names") else int(skel)
     cfg = RenderConfig.from_args(args, nj)
@@ -241,15 +265,20 @@ def create_raycaster(args, data_attrs, device=None, ckpt=None):
         else:
             paths = sorted(p for p in glob.glob(os.path.join(args.basedir, args.expname, "*")) if "tar" in
                            os.path.basename(p) and "pose" not in os.path.basename(p))
-        if not paths or getattr(args, "no_reload", False):
-            raise ValueError("no checkpoint to render (the reference would render random weights)")
-        ckpt = load_checkpoint(paths[-1])
-        start = int(ckpt.get("global_step", 0))
-    rc = RayCaster(cfg, ckpt, device=device)
-    render_kwargs_test = {
-        "ray_caster": rc, "perturb": False, "N_importance": cfg.N_importance, "N_samples": cfg.N_samples,
-        "use_viewdirs": cfg.use_viewdirs, "raw_noise_std": 0., "ray_noise_std": 0., "ext_scale": cfg.ext_scale,
-        "preproc_kwargs": {"density_scale": cfg.density_scale}, "lindisp": False,
-        "nerf_type": getattr(args, "nerf_type", "nerf"),
-    }
-    return None, render_kwargs_test, start, [], None, ckpt
+        if paths and not getattr(args, "no_reload", False):
+            ckpt = load_checkpoint(paths[-1])
+            start = 0 if getattr(args, "finetune", False) else int(ckpt.get("global_step", 0))
+    caster = TrainRayCaster(cfg, ckpt, device=device)
+    grad_vars = [p for p in caster.parameters() if p.requires_grad]
+    optimizer = torch.optim.Adam(params=grad_vars, lr=getattr(args, "lrate", 5e-4), betas=(0.9, 0.999))
+    if ckpt is not None and "optimizer_state_dict" in ckpt and not getattr(args, "finetune", False):
+        optimizer.load_state_dict(ckpt["optimizer_state_dict"])
+    common = {"N_importance": cfg.N_importance, "N_samples": cfg.N_samples, "use_viewdirs": cfg.use_viewdirs,
+              "ext_scale": cfg.ext_scale, "preproc_kwargs": {"density_scale": cfg.density_scale},
+              "lindisp": False, "nerf_type": getattr(args, "nerf_type", "nerf")}
+    render_kwargs_train = {"ray_caster": caster, "perturb": getattr(args, "perturb", 1.0),
+                           "raw_noise_std": getattr(args, "raw_noise_std", 0.0),
+                           "ray_noise_std": getattr(args, "ray_noise_std", 0.0), **common}
+    render_kwargs_test = {"ray_caster": _EvalView(caster), "perturb": False, "raw_noise_std": 0.,
+                          "ray_noise_std": 0., **common}
+    return render_kwargs_train, render_kwargs_test, start, grad_vars, optimizer, ckpt

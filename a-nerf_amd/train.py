@@ -189,9 +189,9 @@ class NeRF(nn.Module):
 class _Embed(nn.Module):
     """CutoffEmbedder state (cutoff_embedder.py:60-95): cutoff_dist (not trained), tau buffer."""
 
-    def __init__(self, n_joints):
+    def __init__(self, n_joints, cutoff_dist):
         super().__init__()
-        self.cutoff_dist = nn.Parameter(torch.zeros(n_joints), requires_grad=False)
+        self.cutoff_dist = nn.Parameter(torch.full((n_joints,), float(cutoff_dist)), requires_grad=False)
         self.register_buffer("tau", torch.tensor(20.0))
 
 
@@ -209,8 +209,10 @@ class TrainRayCaster(nn.Module):
         dev = torch.device(f"cuda:{torch.cuda.current_device() if device is None else int(device)}")
         self.network_fn = NeRF(cfg)
         self.network_fine = NeRF(cfg) if cfg.N_importance > 0 else None
-        self.embed_fn = _Embed(cfg.n_joints)
-        self.embeddirs_fn = _Embed(cfg.n_joints)
+        # fresh models: cutoff_mm (default 500, run_nerf.py:416) x ext_scale (raycasters.py:33), tau 20
+        cut = float(cfg.extra.get("cutoff_mm", 500.0)) * cfg.ext_scale
+        self.embed_fn = _Embed(cfg.n_joints, cut)
+        self.embeddirs_fn = _Embed(cfg.n_joints, cut)
         if ckpt is not None:
             self.load_checkpoint(ckpt)
         self.to(dev)
@@ -247,6 +249,11 @@ class TrainRayCaster(nn.Module):
         if self._consts is None:
             self._consts = DeviceModel(self.cfg, self.checkpoint(), device=self._dev.index)
         return self._consts
+
+    @property
+    def model(self):
+        """The DeviceModel holding the encoder / compositing constants (device index for `render`)."""
+        return self._constants()
 
     def eval_caster(self):
         """The fused eval RayCaster over the current weights (repacked only after they changed)."""

@@ -161,3 +161,40 @@ def test_adam_steps_reduce_loss_and_move_pose():
         losses.append(loss.item())
     assert np.mean(losses[-5:]) < 0.8 * np.mean(losses[:5]), losses
     assert float(delta.detach().abs().max()) > 0.0
+
+
+def test_create_raycaster_training_drop_in(tmp_path):
+    """create_raycaster (core/raycasters.py:17-184) returns train kwargs with the trainable caster,
+    grad_vars and Adam; one core.trainer.render-style step through anerf.render trains it, and the
+    test kwargs render the updated weights with the fused kernel."""
+    import argparse
+    kin = importlib.import_module("a-nerf_amd.kinematics")
+    g = Golden("t1_s32i16_d4w128")
+    m = g.meta
+    args = argparse.Namespace(netdepth=4, netwidth=128, N_samples=m["S"], N_importance=m["I"], use_cutoff=True,
+                              cutoff_inputs=True, cutoff_viewdir=True, use_viewdirs=True, perturb=1.0,
+                              raw_noise_std=1.0, lrate=5e-4, basedir=str(tmp_path), expname="x", no_reload=False,
+                              ft_path=None, ext_scale=0.001, chunk=4096)
+    os_ = importlib.import_module("os")
+    os_.makedirs(tmp_path / "x", exist_ok=True)
+    tr_kw, te_kw, start, grad_vars, opt, ck = anerf.create_raycaster(args, {"skel_type": kin.SMPLSkeleton},
+                                                                     device=0, ckpt=g.ckpt)
+    assert start == 0
+    assert len(grad_vars) == len([p for p in tr_kw["ray_caster"].parameters() if p.requires_grad])
+    dev = torch.device("cuda:0")
+    rays = torch.from_numpy(g["rays"]).to(dev)
+    sk = torch.from_numpy(g["skts"]).to(dev)
+    cy = torch.from_numpy(g["cyls"]).to(dev)
+    te0 = anerf.render(None, None, None, chunk=4096, rays=(rays[:, :3], rays[:, 3:6]), skts=sk, cyls=cy, **te_kw)
+    ref = anerf.RayCaster(g.cfg, g.ckpt).render_rays(rays, m["S"], skts=sk, cyls=cy, N_importance=m["I"])
+    assert torch.equal(te0["rgb_map"], ref["rgb_map"])
+    out = anerf.render(None, None, None, chunk=4096, rays=(rays[:, :3], rays[:, 3:6]), skts=sk, cyls=cy, **tr_kw)
+    loss = train.nerf_loss(out, torch.from_numpy(g["target"]).to(dev))
+    loss.backward()
+    opt.step()
+    te1 = anerf.render(None, None, None, chunk=4096, rays=(rays[:, :3], rays[:, 3:6]), skts=sk, cyls=cy, **te_kw)
+    assert not torch.equal(te1["rgb_map"], te0["rgb_map"])
+    # no checkpoint: torch's default initialisation, as the reference
+    tr_kw2, *_ = anerf.create_raycaster(args, {"skel_type": kin.SMPLSkeleton}, device=0)
+    assert isinstance(tr_kw2["ray_caster"], train.TrainRayCaster)
+    assert torch.allclose(tr_kw2["ray_caster"].embed_fn.cutoff_dist, torch.full((24,), 0.5, device=dev))
