@@ -629,6 +629,93 @@ __device__ __forceinline__ void u_part_lds(f32x16 (&acc)[RB], const ModelDev& M,
     if (next) ring_preload<16>(sh, next, lane);
 }
 
+// ---- bf16x6 bone-direction parts (P == 2, layer 0 and the skip layer)
+// VALU pass: the 3 NJH2 bone-direction features of this lane (sample l & 31, joints h NJH2 ..
+// h NJH2 + NJH2 - 1) into the wave's LDS store as [q][64 lanes] (q = 3 p + c: conflict-free
+// b32 rows), the per-joint live ballots (JointMask) and the view windows w'_j — what u_part
+// computes under its f32 MFMAs.  The two x parts then read the features from LDS.
+template <bool WV>
+__device__ __forceinline__ void u_features_lds(const ModelDev& M, const float* __restrict__ sk,
+                                               const float* __restrict__ cut, float px, float py, float pz, int lane,
+                                               JointMask* mask, float* __restrict__ uf, float* __restrict__ wvo) {
+    const int hh = lane >> 5, njh2 = M.njh2, nj = M.nj, j0 = hh * njh2;
+    uint64_t m0 = 0, m1 = 0;
+    JRow r = load_row(sk, cut, j0, nj);
+    for (int p = 0; p < njh2; ++p) {
+        const JRow rn = load_row(sk, cut, j0 + min(p + 1, njh2 - 1), nj);
+        float u0, u1, u2, wv;
+        bool live;
+        u_joint<WV>(M, r, j0 + p < nj, px, py, pz, u0, u1, u2, live, wv);
+        uf[(3 * p + 0) * 64 + lane] = u0;
+        uf[(3 * p + 1) * 64 + lane] = u1;
+        uf[(3 * p + 2) * 64 + lane] = u2;
+        if constexpr (WV) wvo[p * 64 + lane] = wv;
+        const uint64_t b = __ballot(live);
+        const int jb = p + njh2;
+        if (b & 0xffffffffull) {
+            if (p < 64) m0 |= 1ull << p; else m1 |= 1ull << (p - 64);
+        }
+        if (b >> 32) {
+            if (jb < 64) m0 |= 1ull << jb; else m1 |= 1ull << (jb - 64);
+        }
+        r = rn;
+    }
+    if (mask) {
+        mask->m0 = m0;
+        mask->m1 = m1;
+    }
+}
+
+// One x part's bone-direction contraction from the LDS features as bf16x6: k16-step s takes
+// features 8 s .. 8 s + 7 of each lane half (zero past 3 NJH2), split by truncation (split3_pair);
+// the next step's 8 features are read from LDS in its first group and split, a pair per group,
+// in groups 4..7 (the LDS latency is covered by four groups of MFMAs).  Weight groups (s, rb) of 12
+// floats with the 3-group prefetch in the 4-slot ring (RB % 4 == 0 keeps every slot index static);
+// `preloaded`: groups 0..2 are already in slots 0..2 (issued before the VALU feature pass, or by
+// the previous layer).
+template <int RB>
+__device__ __forceinline__ void u_part_x6_preload(const float* __restrict__ wp, int lane, Ring& ring) {
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(wp);
+#pragma unroll
+    for (int g = 0; g < 3; ++g) load_group<12>(ring.v[g], rs, lane, g);
+}
+
+template <int RB>
+__device__ __forceinline__ void u_part_x6(f32x16 (&acc)[RB], const ModelDev& M, const float* __restrict__ wp,
+                                          const float* __restrict__ uf, int lane, Ring& ring, bool preloaded) {
+    static_assert(RB % 4 == 0 && RB >= 4, "u_part_x6 needs RB % 4 == 0");
+    constexpr int PD = 3;
+    const int nq = 3 * M.njh2, ns = (nq + 7) / 8, ng = ns * RB;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(wp);
+    if (!preloaded) u_part_x6_preload<RB>(wp, lane, ring);
+    // Every group issues its loads and every step its LDS reads unconditionally (clamped: the last
+    // groups reload the last group, the last step reads features it does not use), so the
+    // compiler's counted vmcnt / lgkmcnt waits stay exact: a conditional load makes them drain.
+    auto feat = [&](int q) { return mask_f(uf[min(q, nq - 1) * 64 + lane], q < nq); };
+    X6T cur[1], nxt[1];
+    float fn[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) split3_pair(feat(2 * e), feat(2 * e + 1), cur[0], e);
+    for (int s = 0; s < ns; ++s) {
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) {
+            const int g = s * RB + rb;
+            __builtin_amdgcn_sched_barrier(0);
+            load_group<12>(ring.v[(rb + PD) % 4], rs, lane, min(g + PD, ng - 1));
+            if (rb == 0) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) fn[j] = feat(8 * (s + 1) + j);
+            }
+            acc[rb] = mfma_x6(ring.v[rb % 4], cur[0], acc[rb]);
+            if (rb >= RB - 4) {
+                const int e = rb - (RB - 4);
+                split3_pair(fn[2 * e], fn[2 * e + 1], nxt[0], e);
+            }
+        }
+        cur[0] = nxt[0];
+    }
+}
+
 template <int MR>
 struct VPart {
     static constexpr int KB = ((MR + 1) + 1) & ~1;  // k-steps per joint (even)
@@ -771,13 +858,23 @@ __device__ __forceinline__ bool mlp_trunk(const ModelDev& M, const NetDev& net, 
     const int hh = lane >> 5;
     float nosig = 0.0f;
     constexpr bool HANDOFF = (2 * RB == 16);  // u-part groups have the regs layers' group size
-    ring_preload<2 * RB>(ring, net.wl[0], lane);  // the u part's first groups, early
+    // bf16x6 with the LDS feature store: features in a VALU pass, both bone-direction parts as x6
+    constexpr bool UX6 = (P == 2) && (RB % 4 == 0);
+    const bool ux6 = UX6 && uf != nullptr && M.ux6;
+    if (!ux6) ring_preload<2 * RB>(ring, net.wl[0], lane);  // the u part's first groups, early
     load_bias<RB>(acc, bias, hh);
     STAMP(st, 10);
     const float* const* wl = P == 2 ? net.wl6 : (P ? net.wl3 : net.wl);  // hidden-layer streams of this precision
-    // (bf16x6 layers have 12-float groups: the phases before them do not prefetch into the ring for them)
-    u_part<RB, WV>(acc, M, net.wl[0], sk, cut, px, py, pz, lane, &mask, uf, wvo, ring,
-                   M.D > 1 ? (P == 2 ? nullptr : wl[1]) : after_last, st);
+    if (ux6) {
+        if constexpr (UX6) u_part_x6_preload<RB>(net.wu6, lane, ring);  // (latency under the VALU pass)
+        u_features_lds<WV>(M, sk, cut, px, py, pz, lane, &mask, uf, wvo);
+        STAMP(st, 14);
+        if constexpr (UX6) u_part_x6<RB>(acc, M, net.wu6, uf, lane, ring, true);
+    } else {
+        // (bf16x6 layers have 12-float groups: the phases before them do not prefetch into the ring for them)
+        u_part<RB, WV>(acc, M, net.wl[0], sk, cut, px, py, pz, lane, &mask, uf, wvo, ring,
+                       M.D > 1 ? (P == 2 ? nullptr : wl[1]) : after_last, st);
+    }
     STAMP(st, 8);
     v_part<RB, MR>(acc, M, net.wl0v, sk, cut, px, py, pz, lane, mask, st);
     STAMP(st, 9);
@@ -786,12 +883,13 @@ __device__ __forceinline__ bool mlp_trunk(const ModelDev& M, const NetDev& net, 
         const float* after = L + 1 < M.D ? wl[L + 1] : after_last;
         const bool skl = (L == M.skip + 1);
         if constexpr (P == 2) {
-            const float* nxt6 = skl ? nullptr : after;  // the next x6 layer, or after_last (also x6 form)
+            // the next x6 phase: the next layer, after_last, or the skip layer's x6 bone-direction part
+            const float* nxt6 = skl ? (ux6 ? net.wskipu6 : nullptr) : after;
             mlp_layer_x6<RB, RB, true, false>(acc, acc, h, bias + L * W, wl[L], lane, ring, pre6, nxt6, nullptr,
                                               nosig);
-            pre6 = nxt6 != nullptr;
+            pre6 = nxt6 != nullptr && !skl;  // (the skip x part consumes its preloaded groups itself)
             if (skl) {  // the skip x part preloads its own groups; the phase after it loads itself
-                ring_preload<2 * RB>(ring, net.wskipu, lane);
+                if (!ux6) ring_preload<2 * RB>(ring, net.wskipu, lane);
                 after = nullptr;
             }
         } else {
@@ -804,7 +902,9 @@ __device__ __forceinline__ bool mlp_trunk(const ModelDev& M, const NetDev& net, 
         }
         STAMP(st, 11);
         if (skl) {  // x part after the h part
-            if (uf)
+            if (ux6) {
+                if constexpr (UX6) u_part_x6<RB>(acc, M, net.wskipu6, uf, lane, ring, true);
+            } else if (uf)
                 u_part_lds<RB>(acc, M, net.wskipu, uf, lane, ring, after);
             else
                 u_part<RB, false>(acc, M, net.wskipu, sk, cut, px, py, pz, lane, nullptr, nullptr, nullptr, ring, after,
@@ -871,8 +971,13 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
     STAMP(st, 13);
     if (mfma_count && lane == 0) {  // exact MFMA work of this block (wave-uniform quantities)
         const int act = __builtin_popcountll(mask.m0) + __builtin_popcountll(mask.m1);
-        const int xk = 3 * M.njh2 + act * VPart<MR>::KB;  // k-steps of one x part
+        const bool ux6 = (P == 2) && (RB % 4 == 0) && uf != nullptr && M.ux6;  // as in mlp_trunk
+        const int xk = (ux6 ? 0 : 3 * M.njh2) + act * VPart<MR>::KB;   // f32 k-steps of one x part
         long long k = (long long)xk * RB + (long long)(M.njh2 + 1) * RBV;
+        if (ux6) {
+            const int nx = (M.skip + 1 < M.D) ? 2 : 1;
+            atomicAdd(mfma_count + 1, (unsigned long long)(nx * ((3 * M.njh2 + 7) / 8) * RB * 6));
+        }
         if (P == 2)
             atomicAdd(mfma_count + 1, (unsigned long long)(RBV * RB * 2 * 6));  // view layer, bf16x6
         else

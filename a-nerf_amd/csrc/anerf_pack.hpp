@@ -171,6 +171,31 @@ std::vector<float> pack_upart(const float* Wt, int n_out, int ld, int nj, int nj
     });
 }
 
+// bone-direction part as bf16x6 groups for u_part_x6: k16-step s, lane half h, element j -> feature
+// q = 8 s + j of that half (joint h njh2 + q / 3, component q % 3; zero past 3 njh2 or nj), column
+// nv nj + 3 joint + comp; groups (s, rb) of 12 floats = fragments w0, w1, w2 (as pack_layer_x6).
+std::vector<float> pack_upart_x6(const float* Wt, int n_out, int ld, int nj, int njh2, int mr) {
+    const int nv = 1 + 2 * mr, RB = n_out / 32, nq = 3 * njh2, ns = (nq + 7) / 8;
+    return pack_groups(ns * RB, 12, [&](int g, int sl, int l) {
+        const int s = g / RB, rb = g % RB, f = sl >> 2, e = sl & 3;
+        const int h = l >> 5, row = 32 * rb + (l & 31);
+        uint32_t bits = 0;
+        for (int jj = 0; jj < 2; ++jj) {
+            const int q = 8 * s + 2 * e + jj, joint = q / 3 + h * njh2, c = q % 3;
+            float r = (q < nq && joint < nj) ? Wt[(size_t)row * ld + nv * nj + 3 * joint + c] : 0.0f;
+            uint16_t v = 0;
+            for (int p = 0; p <= f; ++p) {
+                v = bf16_rne(r);
+                r -= bf16_to_f(v);
+            }
+            bits |= (uint32_t)v << (16 * jj);
+        }
+        float out;
+        std::memcpy(&out, &bits, 4);
+        return out;
+    });
+}
+
 // windowed part, per joint j: k-step t < mr -> (sin_t, cos_t) = columns ((1+2t)NJ + j, (2+2t)NJ + j);
 // t == mr -> (dist, pad); padded to an even count.  Layout [joint][group][RB][64][2].
 std::vector<float> pack_vpart(const float* Wt, int n_out, int ld, int nj, int mr) {
@@ -362,6 +387,11 @@ static int pack_net(const anerf_model_desc* d, int njh2, const anerf_net_weights
         offs.push_back(pk.add(pack_layer_x6(w->pts_w[i], W, sk ? cin + W : W, sk ? cin : 0, W)));
     }
     offs.push_back(pk.add(pack_layer_x6(wfused.data(), WH, W, 0, W)));               // wview6
+    offs.push_back(pk.add(pack_upart_x6(w->pts_w[0], W, cin, nj, njh2, mr)));          // wu6 (layer 0)
+    if (skl < d->net_depth)                                                           // wskipu6
+        offs.push_back(pk.add(pack_upart_x6(w->pts_w[skl], W, cin + W, nj, njh2, mr)));
+    else
+        offs.push_back((size_t)-1);
     return ANERF_OK;
 }
 
@@ -391,6 +421,9 @@ static void bind_net(const anerf_model_desc* d, const float* base, const std::ve
     for (int i = 1; i < D; ++i) nd.wl3[i] = base + o[k++];
     for (int i = 1; i < D; ++i) nd.wl6[i] = base + o[k++];
     nd.wview6 = base + o[k++];
+    nd.wu6 = base + o[k++];
+    nd.wskipu6 = o[k] == (size_t)-1 ? nullptr : base + o[k];
+    ++k;
     nd.balpha = balpha;
 }
 

@@ -119,6 +119,10 @@ int anerf_model_create(const anerf_model_desc* desc, const anerf_net_weights* co
     md.cfc = desc->framecode_ch;
     md.n_codes = desc->n_framecodes;
     md.softplus = desc->density_softplus;
+    {  // bf16x6 bone-direction parts (u_part_x6); ANERF_UX6=0 keeps them on the f32 MFMA (A/B only)
+        const char* e = std::getenv("ANERF_UX6");
+        md.ux6 = !(e && e[0] == '0');
+    }
     md.shift = desc->softplus_shift;
     md.B = desc->density_scale;
     md.tau = embed->tau;

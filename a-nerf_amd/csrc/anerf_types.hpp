@@ -57,12 +57,15 @@ struct NetDev {
     const float* wl3[MAXL];  // [i>0] activation parts as bf16x3 fragments (pack_layer_x3)
     const float* wl6[MAXL];  // [i>0] activation parts as bf16x6 fragments (pack_layer_x6)
     const float* wview6;     // wview as bf16x6 fragments
+    const float* wu6;        // layer 0 bone-direction part as bf16x6 fragments (pack_upart_x6)
+    const float* wskipu6;    // the skip layer's, or null
     float balpha;
 };
 
 struct ModelDev {
     int nj, njh2, ngh, D, skip, mr, mrv, use_cutoff, cutoff_inputs, cutoff_viewdir, cfc, n_codes, softplus;
     int sparse;  // windowed features are exactly 0 where w == 0 (use_cutoff && cutoff_inputs)
+    int ux6;     // bf16x6: bone-direction parts as x6 from the LDS feature store (u_part_x6)
     float shift, B, tau, tau_v;
     const float* cutoff;
     const float* cutoff_v;

@@ -388,8 +388,13 @@ def test_bf16x6_executes_bf16_mfmas():
     rc32 = _caster(g)
     _render(rc32, g, g.ray_batch()[:64], count_mfma=True)
     f32_only = int(rc32.last_mfma[0].item())
-    # each 32x32 block of a hidden layer: 16 f32 MFMAs (k = 2 each) -> 2 k16-steps x 6 bf16 MFMAs
-    assert n_bf16 > 0 and (f32_only - n_f32) * 12 == n_bf16 * 16
+    # per 32-sample block (W 256: RB 8, RBV 4, 7 hidden layers, NJH2 12, skip layer present):
+    #   hidden 32x32 blocks: 16 f32 MFMAs (k = 2) -> 12 bf16 (2 k16-steps x 6)
+    #   fused view layer (128 x 256): 64 x 4 f32 -> 4 x 8 x 12 bf16
+    #   two bone-direction x parts (36 features): 36 x 8 f32 -> ceil(36 / 8) x 8 x 6 bf16 each
+    f32_removed = 7 * 64 * 16 + 128 * 4 + 2 * 36 * 8
+    bf16_added = 7 * 64 * 12 + 4 * 8 * 12 + 2 * 5 * 8 * 6
+    assert n_bf16 > 0 and (f32_only - n_f32) * bf16_added == n_bf16 * f32_removed
 
 
 def test_bf16x3_executes_bf16_mfmas():
