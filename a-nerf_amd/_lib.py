@@ -11,7 +11,7 @@ import os
 import torch  # noqa: F401  (must be loaded before the HIP library, see module docstring)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libanerf_hip.so")
+LIB_PATH = os.environ.get("ANERF_LIB_PATH") or os.path.join(HERE, "libanerf_hip.so")  # (override: A/B of builds)
 
 MAXL = 16
 c_f = ctypes.POINTER(ctypes.c_float)

@@ -289,7 +289,7 @@ __device__ __forceinline__ void mlp_layer_x6(f32x16 (&out)[RBO], f32x16 (&ain)[R
     constexpr int NQ = 2 * RBO;  // groups per input block
     const int hh = lane >> 5;
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(wp);
-    const __amdgpu_buffer_rsrc_t rn = make_rsrc(next);
+    const __amdgpu_buffer_rsrc_t rn = make_rsrc(next ? next : wp);
     auto convert_half = [&](int rb, int half) {  // relu of 8 inputs (+ their 8 bias outputs)
 #pragma unroll
         for (int i = 8 * half; i < 8 * half + 8; ++i) h[rb][i] = relu_act(ain[rb][i]);
@@ -315,7 +315,11 @@ __device__ __forceinline__ void mlp_layer_x6(f32x16 (&out)[RBO], f32x16 (&ain)[R
 #pragma unroll
         for (int rb = 0; rb < RBO; ++rb) out[rb] = f32x16{0};
     }
-    auto prefetch = [&](int g) {  // group g + PD of this layer, or the next x6 layer's first groups
+    // group g + PD of this layer, or the next x6 phase's first groups; without a next phase the
+    // last group is reloaded instead (harmless): loads issued on every path keep the compiler's
+    // counted vmcnt waits exact (a conditional load makes the following waits drain to 0)
+    const bool has_next = next != nullptr;
+    auto prefetch = [&](int g) {
 #if ANERF_X6_PROBE == 1  // (diagnostic builds of tools/probe only: no weight loads)
         return;
 #elif ANERF_X6_PROBE == 3  // (diagnostic: loads from a 4-group, L1-resident footprint)
@@ -324,8 +328,8 @@ __device__ __forceinline__ void mlp_layer_x6(f32x16 (&out)[RBO], f32x16 (&ain)[R
 #endif
         if (g + PD < NG)
             load_group<12>(ring.v[(g + PD) % 4], rs, lane, g + PD);
-        else if (NG % 4 == 0 && next)
-            load_group<12>(ring.v[(g + PD) % 4], rn, lane, g + PD - NG);
+        else if (NG % 4 == 0)
+            load_group<12>(ring.v[(g + PD) % 4], rn, lane, has_next ? g + PD - NG : NG - 1);
     };
     // group (of the NQ - q0 groups from q0 on) that splits pair p of the next block
     auto pair_group = [](int p, int q0) { return q0 + (p * (NQ - q0 > 0 ? NQ - q0 : 1)) / 8; };
@@ -860,7 +864,7 @@ __device__ __forceinline__ bool mlp_trunk(const ModelDev& M, const NetDev& net, 
     constexpr bool HANDOFF = (2 * RB == 16);  // u-part groups have the regs layers' group size
     // bf16x6 with the LDS feature store: features in a VALU pass, both bone-direction parts as x6
     constexpr bool UX6 = (P == 2) && (RB % 4 == 0);
-    const bool ux6 = UX6 && uf != nullptr && M.ux6;
+    const bool ux6 = UX6 && M.ux6 && uf != nullptr;
     if (!ux6) ring_preload<2 * RB>(ring, net.wl[0], lane);  // the u part's first groups, early
     load_bias<RB>(acc, bias, hh);
     STAMP(st, 10);
@@ -884,7 +888,9 @@ __device__ __forceinline__ bool mlp_trunk(const ModelDev& M, const NetDev& net, 
         const bool skl = (L == M.skip + 1);
         if constexpr (P == 2) {
             // the next x6 phase: the next layer, after_last, or the skip layer's x6 bone-direction part
-            const float* nxt6 = skl ? (ux6 ? net.wskipu6 : nullptr) : after;
+            // (selected by uniform values only: uf is a per-wave LDS pointer, derived from threadIdx,
+            // and a pointer selected by it becomes a VGPR whose buffer loads waterfall)
+            const float* nxt6 = skl ? ((UX6 && M.ux6) ? net.wskipu6 : nullptr) : after;
             mlp_layer_x6<RB, RB, true, false>(acc, acc, h, bias + L * W, wl[L], lane, ring, pre6, nxt6, nullptr,
                                               nosig);
             pre6 = nxt6 != nullptr && !skl;  // (the skip x part consumes its preloaded groups itself)
