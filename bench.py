@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--importance", type=int, default=128)
     ap.add_argument("--cpu-rays", type=int, default=20000, help="rays in the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--also", default="fp32,bf16x3",
+                    help="other precision modes timed on the same frame afterwards (rank 0, N=1; '' = none)")
     ap.add_argument("--precision", default="bf16x6", choices=["fp32", "bf16x6", "bf16x3"],
                     help="MLP arithmetic (include/anerf.h ANERF_PREC_*)")
     return ap.parse_args()
@@ -167,6 +169,34 @@ def main():
     ref_equiv_tf = flop_ray * n / (kern_ms * 1e-3) / 1e12
     traffic = traffic_from_profiles(a.precision)
 
+    # the other precision modes on the same frame (kernel time of render_rays, HIP events), N=1 only
+    others = {}
+    if rank == 0 and world == 1:
+        for p in [x for x in a.also.split(",") if x and x != a.precision]:
+            rcp = anerf.RayCaster(anerf.RenderConfig(n_joints=a.joints, N_samples=S, N_importance=I,
+                                                     precision=p).validate(), ck, device=local)
+            ts = []
+            for it in range(4):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                rcp.render_rays(rb, S, skts=skts.expand(n, -1, -1, -1), cyls=cyl.expand(n, -1), N_importance=I,
+                                chunk=4096, ret_alpha=False)
+                e1.record()
+                torch.cuda.synchronize()
+                if it:
+                    ts.append(e0.elapsed_time(e1))
+            rcp.render_rays(rb, S, skts=skts.expand(n, -1, -1, -1), cyls=cyl.expand(n, -1), N_importance=I,
+                            chunk=4096, ret_alpha=False, count_mfma=True)
+            torch.cuda.synchronize()
+            pf, pb = (int(v) for v in rcp.last_mfma.tolist())
+            pms = float(np.mean(ts))
+            pflop = pf * FLOP_F32_MFMA + pb * FLOP_BF16_MFMA
+            ppeak = pflop / (pf * FLOP_F32_MFMA / (FP32_MFMA_PEAK_TFLOPS * 1e12) +
+                             pb * FLOP_BF16_MFMA / (BF16_MFMA_PEAK_TFLOPS * 1e12)) / 1e12
+            others[p] = {"rays_per_s_kernel": round(n / (pms * 1e-3), 1), "kernel_ms": round(pms, 3),
+                         "roofline_frac": round(pflop / (pms * 1e-3) / 1e12 / ppeak, 4), "dtype": DTYPE[p]}
+            del rcp
+
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -206,6 +236,7 @@ def main():
                          "reference_flop_per_ray": flop_ray,
                          "reference_equivalent_tflops": round(ref_equiv_tf, 2)},
             "cpu_baseline": cpu,
+            "other_precisions": others or None,
         }
         print(json.dumps(line), flush=True)
     if dist:

@@ -11,7 +11,7 @@ export TMPDIR=/tmp
 TAG=${TAG:-run}
 for p in ${PRECS:-bf16x6 fp32 bf16x3}; do
   echo "== bench $p"
-  timeout -k 10 300 python bench.py --no-cpu --precision $p > gpurun_out/${TAG}_bench_$p.json 2> gpurun_out/bench_$p.err || { tail -20 gpurun_out/bench_$p.err; exit 1; }
+  timeout -k 10 300 python bench.py --no-cpu --also "" --precision $p > gpurun_out/${TAG}_bench_$p.json 2> gpurun_out/bench_$p.err || { tail -20 gpurun_out/bench_$p.err; exit 1; }
   cat gpurun_out/${TAG}_bench_$p.json
 done
 echo "== pytest"
