@@ -59,6 +59,10 @@ def parse():
     ap.add_argument("--importance", type=int, default=128)
     ap.add_argument("--cpu-rays", type=int, default=20000, help="rays in the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--shard", default="frames", choices=["frames", "pixels"],
+                    help="frames: one frame per rank (weak scaling, no collective); pixels: ONE frame per step "
+                         "split into whole 4096-ray chunks across the ranks + an RCCL all-gather of the ray "
+                         "outputs (strong scaling, BASELINE config 5's layout)")
     ap.add_argument("--also", default="fp32,bf16x3",
                     help="other precision modes timed on the same frame afterwards (rank 0, N=1; '' = none)")
     ap.add_argument("--precision", default="bf16x6", choices=["fp32", "bf16x6", "bf16x3"],
@@ -101,7 +105,8 @@ def main():
     S, I = a.samples, a.importance
     cfg = anerf.RenderConfig(n_joints=a.joints, N_samples=S, N_importance=I, precision=a.precision).validate()
     ck = syn.make_checkpoint(13, n_joints=a.joints, D=8, W=256, fine=I > 0, tau=79.6)
-    sc = syn.make_scene(n_joints=a.joints, H=H, W=W, seed=13 + rank)
+    pixels = a.shard == "pixels"
+    sc = syn.make_scene(n_joints=a.joints, H=H, W=W, seed=13 if pixels else 13 + rank)
     rc = anerf.RayCaster(cfg, ck, device=local)
     idxs, cyls, boxes = anerf.rays.valid_pixels(sc["c2ws"], H, W, sc["focal"], kps=sc["kps"], ext_scale=0.001)
     (x0, y0), (x1, y1) = (int(v) for v in boxes[0][0]), (int(v) for v in boxes[0][1])
@@ -115,6 +120,7 @@ def main():
     aimg = torch.empty(H * W, device=dev)
     st = _lib.stream_handle(dev)
     ev = []
+    dmod = importlib.import_module("a-nerf_amd.distributed")
 
     def step(record):
         _lib.check(lib.anerf_gen_rays_box(_lib.ptr(c2w), H, W, sc["focal"], sc["focal"], 0.0, 0.0, 0, x0, y0, x1, y1,
@@ -122,8 +128,16 @@ def main():
         if record:
             e0 = torch.cuda.Event(enable_timing=True)
             e0.record()
-        out = rc.render_rays(rb, S, skts=skts.expand(n, -1, -1, -1), cyls=cyl.expand(n, -1), N_importance=I,
-                             chunk=4096, ret_alpha=False)
+        if pixels:  # this rank's whole-chunk range of the frame, then one all-gather (distributed.py)
+            out = dmod.render_rays_sharded(
+                lambda r: rc.render_rays(r, S, skts=skts.expand(r.shape[0], -1, -1, -1),
+                                         cyls=cyl.expand(r.shape[0], -1), N_importance=I, chunk=4096,
+                                         ret_alpha=False), rb, 4096) if dist else \
+                rc.render_rays(rb, S, skts=skts.expand(n, -1, -1, -1), cyls=cyl.expand(n, -1), N_importance=I,
+                               chunk=4096, ret_alpha=False)
+        else:
+            out = rc.render_rays(rb, S, skts=skts.expand(n, -1, -1, -1), cyls=cyl.expand(n, -1), N_importance=I,
+                                 chunk=4096, ret_alpha=False)
         if record:
             e1 = torch.cuda.Event(enable_timing=True)
             e1.record()
@@ -147,7 +161,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in ev]))
-    rays_job = n * a.steps
+    rays_job = n * a.steps / (world if pixels else 1)  # pixels: the ranks share one frame per step
     if dist:
         t = torch.tensor([elapsed, float(rays_job)], device=dev, dtype=torch.float64)
         tmax = t[:1].clone()
@@ -155,9 +169,12 @@ def main():
         tdist.all_reduce(t[1:], op=tdist.ReduceOp.SUM)
         elapsed, rays_job = float(tmax.item()), float(t[1].item())
 
-    # executed MFMA work of one launch (exact device-side counter, one extra untimed launch)
-    rc.render_rays(rb, S, skts=skts.expand(n, -1, -1, -1), cyls=cyl.expand(n, -1), N_importance=I, chunk=4096,
-                   ret_alpha=False, count_mfma=True)
+    # executed MFMA work of one launch (exact device-side counter, one extra untimed launch) over the
+    # rays this rank renders per step (pixels mode: its whole-chunk share of the frame)
+    s0, s1 = dmod.chunk_ranges(n, 4096, world)[rank] if (pixels and dist) else (0, n)
+    n_mine = s1 - s0
+    rc.render_rays(rb[s0:s1], S, skts=skts.expand(n_mine, -1, -1, -1), cyls=cyl.expand(n_mine, -1), N_importance=I,
+                   chunk=4096, ret_alpha=False, count_mfma=True)
     torch.cuda.synchronize()
     n_f32, n_bf16 = (int(v) for v in rc.last_mfma.tolist())
     flop_exec = n_f32 * FLOP_F32_MFMA + n_bf16 * FLOP_BF16_MFMA
@@ -166,7 +183,7 @@ def main():
     peak_tf = flop_exec / t_mfma / 1e12  # = 157.3 for fp32; the instruction-mix-weighted peak otherwise
     flop_ray = anerf.flops_per_sample(cfg) * anerf.samples_per_ray(cfg)  # SURVEY §8(d), reference work
     achieved_tf = flop_exec / (kern_ms * 1e-3) / 1e12
-    ref_equiv_tf = flop_ray * n / (kern_ms * 1e-3) / 1e12
+    ref_equiv_tf = flop_ray * n_mine / (kern_ms * 1e-3) / 1e12
     traffic = traffic_from_profiles(a.precision)
 
     # the other precision modes on the same frame (kernel time of render_rays, HIP events), N=1 only
@@ -217,12 +234,14 @@ def main():
         line = {
             "metric": BASELINE["metric"], "value": round(value, 1), "unit": "rays/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(1e3 * elapsed / a.steps, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "higher_is_better": True, "scaling": "strong" if pixels else "weak", "vs_baseline": None,
             "dtype": DTYPE[a.precision],
             "data": "synthetic (seeded SMPL-24 pose + seeded 8x256 weights; no dataset/checkpoint offline)",
-            "config": {"workload": f"config3: {H}x{W} frame, {S}+{I} samples, {a.joints}-joint, 8x256 MLP, "
-                                   f"one frame per GPU per step", "rays_per_frame": n,
-                       "parallelism": f"frame-per-rank x{world}"},
+            "config": {"workload": f"config3: {H}x{W} frame, {S}+{I} samples, {a.joints}-joint, 8x256 MLP, " +
+                                   (f"one frame per step split over {world} GPU(s) in whole 4096-ray chunks + RCCL "
+                                    f"all-gather" if pixels else "one frame per GPU per step"),
+                       "rays_per_frame": n,
+                       "parallelism": f"{'pixel-shard' if pixels else 'frame-per-rank'} x{world}"},
             "roofline": {"bound": "mfma", "achieved": round(achieved_tf, 2), "peak": round(peak_tf, 1),
                          "unit": "TFLOP/s", "frac": round(achieved_tf / peak_tf, 4),
                          "traffic": traffic, "kernel_ms": round(kern_ms, 3),
