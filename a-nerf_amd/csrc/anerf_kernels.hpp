@@ -42,7 +42,7 @@ __global__ __launch_bounds__(256, 1) void render_kernel(ModelDev M, RenderArgs A
     if (A.pass0 == 1)  // fine-only launch: the sorted fine z of the coarse launch
         for (int idx = tid; idx < nr * T; idx += blockDim.x) {
             const int r = idx / T, s = idx % T;
-            lds[P.zf + P.z_stride * r + s] = A.zf_ws[(ray0 + r) * T + s];
+            lds[P.zf + P.z_stride * r + s] = __builtin_nontemporal_load(A.zf_ws + (ray0 + r) * T + s);
         }
     __syncthreads();
 
@@ -118,7 +118,8 @@ __global__ __launch_bounds__(256, 1) void render_kernel(ModelDev M, RenderArgs A
     if (I > 0 && A.pass1 == 1)  // coarse-only launch: hand the fine z over
         for (int idx = tid; idx < nr * T; idx += blockDim.x) {
             const int r = idx / T, s = idx % T;
-            A.zf_ws[(ray0 + r) * T + s] = lds[P.zf + P.z_stride * r + s];
+            // (non-temporal: 0.8 KB per ray streams through L2 and would evict weight groups)
+            __builtin_nontemporal_store(lds[P.zf + P.z_stride * r + s], A.zf_ws + (ray0 + r) * T + s);
         }
     STAMP_FLUSH(st, A.stamps);
 }

@@ -29,7 +29,7 @@ for p in fp32 bf16x6; do
   cat gpurun_out/${TAG}_density_$p.json
 done
 echo "== rocprof"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o run --output-format csv -- python3 bench.py --steps 4 --warmup 1 --no-cpu > gpurun_out/prof.log 2>&1 || { echo "rocprof failed"; tail -20 gpurun_out/prof.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o run --output-format csv -- python3 bench.py --steps 4 --warmup 1 --no-cpu --also "" > gpurun_out/prof.log 2>&1 || { echo "rocprof failed"; tail -20 gpurun_out/prof.log; exit 1; }
 find gpurun_out/prof_${TAG} -name "*stats*"
 echo "== pmc"
 PREC=bf16x6 bash tools/gpu_pmc.sh || exit 1

@@ -8,6 +8,9 @@ import os
 import sys
 
 
+PREC_TEMPLATE = {"fp32": 0, "bf16x3": 1, "bf16x6": 2}
+
+
 def rows(path, kernel="render_kernel"):
     out = {}
     with open(path) as f:
@@ -33,9 +36,10 @@ def main():
     label = sys.argv[3] if len(sys.argv) > 3 else ""
     prec = sys.argv[4] if len(sys.argv) > 4 else "fp32"
     launches = int(sys.argv[5]) if len(sys.argv) > 5 else 2  # coarse + fine launch per render_rays call
-    f, calls = per_call(rows(os.path.join(base, "pmc_fetch", "run_counter_collection.csv")), launches)
-    w, _ = per_call(rows(os.path.join(base, "pmc_write", "run_counter_collection.csv")), launches)
-    s, _ = per_call(rows(os.path.join(base, "pmc_sq", "run_counter_collection.csv")), launches)
+    kern = f"render_kernel<256, 7, {PREC_TEMPLATE[prec]}>"  # this precision's instance only
+    f, calls = per_call(rows(os.path.join(base, "pmc_fetch", "run_counter_collection.csv"), kern), launches)
+    w, _ = per_call(rows(os.path.join(base, "pmc_write", "run_counter_collection.csv"), kern), launches)
+    s, _ = per_call(rows(os.path.join(base, "pmc_sq", "run_counter_collection.csv"), kern), launches)
     hbm = 2 * f["FETCH_SIZE"] * 1024 + w["WRITE_SIZE"] * 1024
     clock = s["GRBM_GUI_ACTIVE"] / 8 / (s["ns"] * 1e-9) / 1e9
     busy = s["SQ_INSTS_MFMA"] / 1024 * 64 / (s["ns"] * 1e-9 * clock * 1e9)
