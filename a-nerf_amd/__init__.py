@@ -8,7 +8,8 @@ run_nerf.py).
 from .config import RenderConfig, flops_per_sample, samples_per_ray
 from .raycaster import RayCaster, create_raycaster, load_checkpoint
 from .render import batchify_rays, render, render_path, render_frames
-from . import rays, synthetic, train
+from . import dataset, rays, synthetic, train
+from .dataset import RayImageDataset, RayImageSampler
 
 __all__ = ["RenderConfig", "RayCaster", "create_raycaster", "load_checkpoint", "render", "render_path",
-           "render_frames", "batchify_rays", "rays", "synthetic", "flops_per_sample", "samples_per_ray"]
+           "render_frames", "batchify_rays", "rays", "synthetic", "dataset", "RayImageDataset", "RayImageSampler", "flops_per_sample", "samples_per_ray"]

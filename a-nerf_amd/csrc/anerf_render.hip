@@ -48,6 +48,7 @@ using namespace anerf;
 #include "anerf_train.hpp"
 #include "anerf_pose.hpp"
 #include "anerf_boxes.hpp"
+#include "anerf_batch.hpp"
 #include "anerf_pack.hpp"
 
 #ifdef ANERF_STAMPS
@@ -667,6 +668,32 @@ int anerf_kp_boxes(const float* kps, const float* cyls_in, int64_t n_kp, int32_t
     if (waves == 0) return ANERF_OK;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(kp_boxes_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, a);
+    HIP_TRY(hipGetLastError());
+    return ANERF_OK;
+}
+
+int anerf_ray_batch(const uint8_t* imgs, const uint8_t* masks, const uint8_t* bgs, const int64_t* bg_idx,
+                    const float* c2ws, const float* focals, const float* centers, int64_t n_rows, int64_t n_bg,
+                    int32_t H, int32_t W, const int64_t* rows, int64_t n_img, const int64_t* pixels, int64_t n_per,
+                    int32_t mask_img, float* rays_out, float* target_out, float* fg_out, float* bg_out,
+                    int32_t* bad_out, void* stream) {
+    if (n_img < 0 || n_per < 0 || H <= 0 || W <= 0 || n_rows < 1)
+        return fail(ANERF_EINVAL, "anerf_ray_batch: bad sizes");
+    if (n_img == 0 || n_per == 0) return ANERF_OK;
+    if (!imgs || !c2ws || !focals || !rows || !pixels || !rays_out || !target_out)
+        return fail(ANERF_EINVAL, "anerf_ray_batch: missing buffer");
+    if (bgs && (!bg_idx || n_bg < 1)) return fail(ANERF_EINVAL, "anerf_ray_batch: backgrounds need bg_idx and n_bg");
+    if (mask_img && !(bgs && masks)) return fail(ANERF_EINVAL, "anerf_ray_batch: mask_img needs masks and backgrounds");
+    if (bg_out && !bgs) return fail(ANERF_EINVAL, "anerf_ray_batch: bg_out without backgrounds");
+    if (fg_out && !masks) return fail(ANERF_EINVAL, "anerf_ray_batch: fg_out without masks");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    RayBatchArgs a{};
+    a.imgs = imgs; a.masks = masks; a.bgs = bgs; a.bg_idx = bg_idx; a.c2ws = c2ws; a.focals = focals;
+    a.centers = centers; a.rows = rows; a.pix = pixels; a.n_rows = n_rows; a.n_bg = bgs ? n_bg : 1;
+    a.n_img = n_img; a.n_per = n_per; a.H = H; a.W = W; a.mask_img = mask_img;
+    a.rays = rays_out; a.target = target_out; a.fg = fg_out; a.bg = bg_out; a.bad = bad_out;
+    const int64_t n = n_img * n_per;
+    hipLaunchKernelGGL(ray_batch_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a);
     HIP_TRY(hipGetLastError());
     return ANERF_OK;
 }

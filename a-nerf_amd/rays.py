@@ -61,8 +61,9 @@ def _intrinsic(focal):
     return np.array([[fx, 0, 0, 0], [0, fy, 0, 0], [0, 0, 1, 0]], dtype=np.float32)
 
 
-def cylinder_box(cyl, H, W, focal, c2w, center=None):
-    """2-D integer box (tl, br) of one cylinder (5,) seen by camera c2w (4,4)."""
+def cylinder_box(cyl, H, W, focal, c2w, center=None, scale=1.0):
+    """2-D integer box (tl, br) of one cylinder (5,) seen by camera c2w (4,4); `scale` grows it about
+    its centre as cylinder_to_box_2d(..., scale) does (skeleton_utils.py:672-682)."""
     cyl = np.asarray(cyl)
     root, radius = cyl[..., :2][None], cyl[..., 2:3][None]
     top, bot = cyl[..., 3:4][None], cyl[..., 4:5][None]
@@ -91,6 +92,16 @@ def cylinder_box(cyl, H, W, focal, c2w, center=None):
     tl[:, 1] += oy
     br[:, 0] += ox
     br[:, 1] += oy
+    if scale != 1.0:
+        # float64 half-extents and centre, stored back into the int32 boxes (truncation)
+        half_w = (max_x - min_x) * 0.5 * scale
+        half_h = (max_y - min_y) * 0.5 * scale
+        cx = (br[:, 0] + tl[:, 0]).copy() * 0.5
+        cy = (br[:, 1] + tl[:, 1]).copy() * 0.5
+        tl[:, 0] = cx - half_w
+        br[:, 0] = cx + half_w
+        tl[:, 1] = cy - half_h
+        br[:, 1] = cy + half_h
     tl[:, 0] = np.clip(tl[:, 0], 0, W - 1)
     br[:, 0] = np.clip(br[:, 0], 0, W - 1)
     tl[:, 1] = np.clip(tl[:, 1], 0, H - 1)

@@ -26,6 +26,8 @@
  *   anerf_pose_kinematics_backward   its autograd (pose optimisation)
  *                                                                              core/utils/skeleton_utils.py:296-376
  *   anerf_kp_boxes          kp_to_valid_rays' cylinder + pixel box             core/utils/ray_utils.py:83-136
+ *   anerf_ray_batch         BaseH5Dataset.__getitem__ + ray_collate_fn (the    core/dataset.py:57-105, 259-275,
+ *                           training ray sampler) over HBM-resident images     346-364, 796-802
  * Training stages of render_rays (perturb, raw noise, stochastic importance sampling, gradients):
  *   anerf_train_samples     sample_from_lineseg (perturb > 0)                  core/utils/ray_utils.py:204-251
  *   anerf_train_encode      sample_pts + encode_inputs (+ embedders)           core/raycasters.py:476-555, 650-663
@@ -45,7 +47,7 @@
 extern "C" {
 #endif
 
-#define ANERF_ABI_VERSION 3
+#define ANERF_ABI_VERSION 4
 
 enum {
     ANERF_OK = 0,
@@ -244,6 +246,24 @@ int anerf_pose_kinematics_backward(const float* bones, int32_t rot_dim, const fl
 int anerf_kp_boxes(const float* kps, const float* cyls_in, int64_t n_kp, int32_t n_joints, int32_t root_id,
                    double ext_scale, const float* w2cs, const float* focals, const int32_t* offsets, int64_t n_frames,
                    int32_t H, int32_t W, const double* cap_dirs, float* cyls_out, int32_t* boxes_out, void* stream);
+
+/* Training ray batch of the image dataset (the `.h5` ray sampler):
+ * BaseH5Dataset.__getitem__ (core/dataset.py:57-105) for n_img images at once in ray_collate_fn's
+ * flattened layout (core/dataset.py:796-802), from uint8 images resident on the device.  Inputs (the
+ * .h5 arrays): imgs [n_rows][H*W][3], masks [n_rows][H*W] (NULL: fg = 1), bgs [n_bg][H*W][3] with
+ * bg_idx [n_rows] (NULL: no backgrounds), c2ws [n_rows][4][4] float32, focals [n_rows] float32,
+ * centers [n_rows][2] float32 (NULL: image centre); rows [n_img] = dataset row of each batch image,
+ * pixels [n_img][n_per] = its sampled pixel indices y*W + x (drawn by the caller: the reference's
+ * numpy RNG, sample_pixels core/dataset.py:277-323).  Outputs: rays_out [2][n][3] (rays_o, rays_d of
+ * get_rays :346-364, including its isclose(c2w, I) shortcut), target_out [n][3] (get_img_data
+ * :259-275; img * fg + (1 - fg) * bg when mask_img and bgs), fg_out [n] and bg_out [n][3] (optional),
+ * n = n_img * n_per.  An out-of-range row, pixel or bg_idx makes that ray's outputs NaN and sets
+ * *bad_out = 1 (device int32, may be NULL; the check guards the reads either way). */
+int anerf_ray_batch(const uint8_t* imgs, const uint8_t* masks, const uint8_t* bgs, const int64_t* bg_idx,
+                    const float* c2ws, const float* focals, const float* centers, int64_t n_rows, int64_t n_bg,
+                    int32_t H, int32_t W, const int64_t* rows, int64_t n_img, const int64_t* pixels, int64_t n_per,
+                    int32_t mask_img, float* rays_out, float* target_out, float* fg_out, float* bg_out,
+                    int32_t* bad_out, void* stream);
 
 /* ---- Training stages.  All pointers are device pointers; random numbers are
  * inputs (torch.rand / torch.randn draws of the caller), so a run can reproduce the reference's. */
