@@ -83,6 +83,13 @@ def traffic_from_profiles(precision):
     return None
 
 
+def _config_name(H, S, I, nj):
+    """BASELINE.json's config numbering (SURVEY §8(d)); other shapes are 'custom'."""
+    known = {(256, 64, 0, 24): "config2", (512, 64, 128, 24): "config3", (512, 64, 128, 65): "config4",
+             (1024, 64, 128, 24): "config5"}
+    return known.get((H, S, I, nj), "custom")
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -184,7 +191,8 @@ def main():
     flop_ray = anerf.flops_per_sample(cfg) * anerf.samples_per_ray(cfg)  # SURVEY §8(d), reference work
     achieved_tf = flop_exec / (kern_ms * 1e-3) / 1e12
     ref_equiv_tf = flop_ray * n_mine / (kern_ms * 1e-3) / 1e12
-    traffic = traffic_from_profiles(a.precision)
+    # the committed PMC summaries are of config 3's frame; other shapes report null
+    traffic = traffic_from_profiles(a.precision) if _config_name(H, S, I, a.joints) == "config3" else None
 
     # the other precision modes on the same frame (kernel time of render_rays, HIP events), N=1 only
     others = {}
@@ -237,7 +245,7 @@ def main():
             "higher_is_better": True, "scaling": "strong" if pixels else "weak", "vs_baseline": None,
             "dtype": DTYPE[a.precision],
             "data": "synthetic (seeded SMPL-24 pose + seeded 8x256 weights; no dataset/checkpoint offline)",
-            "config": {"workload": f"config3: {H}x{W} frame, {S}+{I} samples, {a.joints}-joint, 8x256 MLP, " +
+            "config": {"workload": f"{_config_name(H, S, I, a.joints)}: {H}x{W} frame, {S}+{I} samples, {a.joints}-joint, 8x256 MLP, " +
                                    (f"one frame per step split over {world} GPU(s) in whole 4096-ray chunks + RCCL "
                                     f"all-gather" if pixels else "one frame per GPU per step"),
                        "rays_per_frame": n,

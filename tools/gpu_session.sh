@@ -32,7 +32,17 @@ echo "== rocprof"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o run --output-format csv -- python3 bench.py --steps 4 --warmup 1 --no-cpu --also "" > gpurun_out/prof.log 2>&1 || { echo "rocprof failed"; tail -20 gpurun_out/prof.log; exit 1; }
 find gpurun_out/prof_${TAG} -name "*stats*"
 echo "== pmc"
-PREC=bf16x6 bash tools/gpu_pmc.sh || exit 1
+for p in ${PMC_PRECS:-bf16x6}; do
+  PREC=$p bash tools/gpu_pmc.sh || exit 1
+done
+echo "== configs 2 and 4"
+timeout -k 10 300 python bench.py --no-cpu --also "" --joints 65 > gpurun_out/${TAG}_bench_cfg4_joints65.json 2> gpurun_out/cfg.err || { tail -20 gpurun_out/cfg.err; exit 1; }
+timeout -k 10 300 python bench.py --no-cpu --also "" --res 256 --importance 0 > gpurun_out/${TAG}_bench_cfg2_res256.json 2> gpurun_out/cfg.err || { tail -20 gpurun_out/cfg.err; exit 1; }
+cat gpurun_out/${TAG}_bench_cfg4_joints65.json gpurun_out/${TAG}_bench_cfg2_res256.json
+echo "== dataset ray sampler"
+timeout -k 10 200 python tools/dataset_bench.py > gpurun_out/${TAG}_dataset_bench.json 2> gpurun_out/ds.err || { tail -20 gpurun_out/ds.err; exit 1; }
+cat gpurun_out/${TAG}_dataset_bench.json
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_ds_${TAG} -o run --output-format csv -- python3 tools/dataset_bench.py > gpurun_out/prof_ds.log 2>&1 || { echo "rocprof dataset failed"; tail -20 gpurun_out/prof_ds.log; exit 1; }
 echo "== train"
 timeout -k 10 300 python tools/train_bench.py > gpurun_out/${TAG}_train_bench.json 2> gpurun_out/train.err || { tail -20 gpurun_out/train.err; exit 1; }
 cat gpurun_out/${TAG}_train_bench.json
