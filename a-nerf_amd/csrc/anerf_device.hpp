@@ -133,6 +133,56 @@ __device__ inline float np_pairwise_sum(const float* a, int64_t n) {
     return vals[0];
 }
 
+// The same tree split for a workgroup: the leaves (<= 128 elements, left to right) are listed once,
+// summed by many threads, then combined in the tree's order.  np_pairwise_leaves returns the leaf
+// count, or -1 when there are more than `cap`.
+__device__ inline int np_pairwise_leaves(int64_t n, int* off, int* cnt, int cap) {
+    int64_t st_off[64], st_n[64];
+    int ns = 1, nl = 0;
+    st_off[0] = 0; st_n[0] = n;
+    while (ns > 0) {
+        --ns;
+        const int64_t o = st_off[ns], c = st_n[ns];
+        if (c <= 128) {
+            if (nl == cap) return -1;
+            off[nl] = (int)o; cnt[nl] = (int)c; ++nl;
+        } else {
+            int64_t n2 = c / 2;
+            n2 -= n2 % 8;
+            st_off[ns] = o + n2; st_n[ns] = c - n2; ++ns;   // right half after the left one
+            st_off[ns] = o; st_n[ns] = n2; ++ns;
+        }
+    }
+    return nl;
+}
+
+// np_pairwise_sum given the leaf sums in left-to-right order
+__device__ inline float np_pairwise_combine(const float* leaf, int64_t n) {
+    int64_t node_n[64];
+    int node_exp[64];
+    float vals[64];
+    int ns = 1, vs = 0, k = 0;
+    node_n[0] = n; node_exp[0] = 0;
+    while (ns > 0) {
+        --ns;
+        const int64_t cnt = node_n[ns];
+        if (cnt <= 128) {
+            vals[vs++] = leaf[k++];
+        } else if (!node_exp[ns]) {
+            int64_t n2 = cnt / 2;
+            n2 -= n2 % 8;
+            node_exp[ns] = 1; ++ns;
+            node_n[ns] = cnt - n2; node_exp[ns] = 0; ++ns;
+            node_n[ns] = n2; node_exp[ns] = 0; ++ns;
+        } else {
+            const float r = vals[--vs];
+            const float l = vals[--vs];
+            vals[vs++] = l + r;
+        }
+    }
+    return vals[0];
+}
+
 // ---- torch CPU float32 sum (aten SumKernel cascade_sum; see oracle/anerf_oracle.c) ----
 __device__ __forceinline__ int ceil_log2_i64(int64_t x) {
     int r = 0;

@@ -222,28 +222,43 @@ __global__ void near_far_kernel(const float* __restrict__ rb, int stride, int64_
 }
 
 // one workgroup per chunk: NaN rows <- np.nanmean of the chunk (ray_utils.py:328-342)
+constexpr int NF_LEAVES = 1024;  // leaves of <= 128 rays: chunks up to ~65 k rays in parallel
+
 __global__ void nan_fill_kernel(const float* __restrict__ rb, int stride, int64_t n, int chunk,
                                 float* __restrict__ near_io, float* __restrict__ far_io,
                                 const uint8_t* __restrict__ qnan, float* __restrict__ scratch) {
     const int64_t c0 = (int64_t)blockIdx.x * chunk;
     const int64_t c1 = min(c0 + chunk, n);
-    __shared__ int any;
+    const int64_t m = c1 - c0;
+    __shared__ int any, n_leaves, valid[2];
     __shared__ float means[2];
-    if (threadIdx.x == 0) any = 0;
+    __shared__ int leaf_off[NF_LEAVES], leaf_cnt[NF_LEAVES];
+    __shared__ float leaf_sum[NF_LEAVES];
+    if (threadIdx.x == 0) { any = 0; valid[0] = valid[1] = 0; }
     __syncthreads();
     for (int64_t i = c0 + threadIdx.x; i < c1; i += blockDim.x)
         if (near_io[i] != near_io[i]) any = 1;
     __syncthreads();
     if (!any) return;
+    if (threadIdx.x == 0) n_leaves = np_pairwise_leaves(m, leaf_off, leaf_cnt, NF_LEAVES);
     float* buf = scratch + c0;  // NaN -> 0 copies, one vector at a time
     for (int v = 0; v < 2; ++v) {
         const float* src = v == 0 ? near_io : far_io;
-        for (int64_t i = c0 + threadIdx.x; i < c1; i += blockDim.x) buf[i - c0] = (src[i] != src[i]) ? 0.0f : src[i];
+        int mine = 0;
+        for (int64_t i = c0 + threadIdx.x; i < c1; i += blockDim.x) {
+            const float x = src[i];
+            buf[i - c0] = (x != x) ? 0.0f : x;
+            mine += (x == x);
+        }
+        atomicAdd(&valid[v], mine);
+        __syncthreads();
+        // numpy's pairwise sum (np.nanmean, ray_utils.py:332): leaves in parallel, then the tree
+        if (n_leaves >= 0)
+            for (int k = threadIdx.x; k < n_leaves; k += blockDim.x) leaf_sum[k] = np_leaf_sum(buf + leaf_off[k], leaf_cnt[k]);
         __syncthreads();
         if (threadIdx.x == 0) {
-            int64_t cnt = 0;
-            for (int64_t i = c0; i < c1; ++i) cnt += (src[i] == src[i]);
-            means[v] = cnt ? (float)((double)np_pairwise_sum(buf, c1 - c0) / (double)cnt) : __int_as_float(0x7fc00000);
+            const float sum = n_leaves >= 0 ? np_pairwise_combine(leaf_sum, m) : np_pairwise_sum(buf, m);
+            means[v] = valid[v] ? (float)((double)sum / (double)valid[v]) : __int_as_float(0x7fc00000);
         }
         __syncthreads();
     }

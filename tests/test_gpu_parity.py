@@ -127,6 +127,39 @@ def test_render_rays_matches_oracle(name):
             assert _maxdiff(out[k], ref[k]) <= TOL, k
 
 
+@pytest.mark.parametrize("chunk", [4096, 1000, 32768, 150000])
+def test_near_far_nan_fill_chunks_bit_exact(chunk):
+    """Hazard H1 at many chunk sizes: random rays, about half missing the cylinder (whole chunks of
+    misses included), near/far + the chunk nanmean fill bit-exact against the oracle.  150,000 rays
+    in one chunk exceed the kernel's parallel leaf table (1,024 leaves) and take its serial path."""
+    orc = _oracle()
+    g = Golden("c3_512_s64i128_d8w256")
+    om = orc.OracleModel(g.cfg, g.ckpt)
+    rng = np.random.default_rng(chunk)
+    n = 150000
+    rb = np.zeros((n, 11), np.float32)
+    rb[:, 0:3] = rng.normal(0, 0.5, (n, 3)) + np.array([0, 0, 6.0])
+    d = rng.normal(0, 1.0, (n, 3)) * np.array([0.3, 0.3, 1.0]) - np.array([0, 0, 1.0])
+    rb[:, 3:6] = d
+    rb[:, 7] = 1.0
+    rb[30000:40000, 3:6] = [0.0, 0.0, 1.0]      # pointing away from the body: a run of misses
+    cyl = g["cyls"][0:1]
+    near_o, far_o, _, _ = om.near_far(rb, cyl, chunk=chunk)
+    lib = _lib.load()
+    rb_d = torch.from_numpy(rb).cuda()
+    cyl_d = torch.from_numpy(np.ascontiguousarray(cyl, np.float32)).cuda()
+    pose = torch.zeros(n, dtype=torch.int32, device="cuda")
+    near = torch.empty(n, device="cuda")
+    far = torch.empty(n, device="cuda")
+    ws = torch.empty(16 * n + (1 << 16), dtype=torch.uint8, device="cuda")
+    _lib.check(lib.anerf_near_far(_lib.ptr(rb_d), 11, n, _lib.ptr(cyl_d), _lib.ptr(pose), chunk, _lib.ptr(near),
+                                  _lib.ptr(far), _lib.ptr(ws), ws.numel(), _lib.stream_handle()), "anerf_near_far")
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(near.cpu().numpy(), near_o)
+    np.testing.assert_array_equal(far.cpu().numpy(), far_o)
+    assert not np.isnan(near_o).any()   # every miss filled (chunk mean, or the ray's own 0 / 1)
+
+
 def test_encode_points_matches_oracle():
     orc = _oracle()
     g = Golden("c3_512_s64i128_d8w256")
