@@ -130,6 +130,55 @@ class _Linear(torch.autograd.Function):
 def _lin(x, w, b=None):
     return _Linear.apply(x, w, b)
 
+
+class _Linear2(torch.autograd.Function):
+    """a @ wa.T + b @ wb.T + bias (the skip layer's cat([x, h]) and the view layer's cat([feature,
+    views]) with the weight split by columns): the second product accumulates into the first
+    GEMM's output (beta = 1), so neither direction launches a separate add."""
+
+    @staticmethod
+    def forward(ctx, a, wa, b, wb, bias):
+        ctx.save_for_backward(a, wa, b, wb)
+        ctx.has_bias = bias is not None
+        out = F.linear(b, wb, bias)
+        return out.addmm_(a, wa.t())
+
+    @staticmethod
+    def backward(ctx, g):
+        a, wa, b, wb = ctx.saved_tensors
+        need = ctx.needs_input_grad
+        ga = g.mm(wa) if need[0] else None
+        gwa = _splitk_wgrad(g, a) if need[1] else None
+        gb = g.mm(wb) if need[2] else None
+        gwb = _splitk_wgrad(g, b) if need[3] else None
+        gbias = g.sum(0) if ctx.has_bias and need[4] else None
+        return ga, gwa, gb, gwb, gbias
+
+
+class _Heads(torch.autograd.Function):
+    """alpha_linear and feature_linear on the same h: the gradient of h is one GEMM plus a rank-1
+    update accumulated into it (no separate add of two [M, W] gradients)."""
+
+    @staticmethod
+    def forward(ctx, h, wa, ba, wf, bf):
+        ctx.save_for_backward(h, wa, wf)
+        return F.linear(h, wa, ba), F.linear(h, wf, bf)
+
+    @staticmethod
+    def backward(ctx, g_alpha, g_feat):
+        h, wa, wf = ctx.saved_tensors
+        need = ctx.needs_input_grad
+        if g_alpha is None:
+            g_alpha = torch.zeros(h.shape[0], wa.shape[0], device=h.device, dtype=h.dtype)
+        if g_feat is None:
+            g_feat = torch.zeros(h.shape[0], wf.shape[0], device=h.device, dtype=h.dtype)
+        gh = g_feat.mm(wf).addmm_(g_alpha, wa) if need[0] else None
+        gwa = _splitk_wgrad(g_alpha, h) if need[1] else None
+        gba = g_alpha.sum(0) if need[2] else None
+        gwf = _splitk_wgrad(g_feat, h) if need[3] else None
+        gbf = g_feat.sum(0) if need[4] else None
+        return gh, gwa, gba, gwf, gbf
+
 class Optcodes(nn.Module):
     """core/networks/embedding.py:6-46 (training: codes(idx); eval with all idx < 0: the mean code)."""
 
@@ -170,15 +219,15 @@ class NeRF(nn.Module):
         h = x
         for i, lin in enumerate(self.pts_linears):
             if i > 0 and (i - 1) in self.skips:  # cat([input_pts, h]) @ W.T = x @ Wx.T + h @ Wh.T
-                h = F.relu(_lin(x, lin.weight[:, :self.dnet]) + _lin(h, lin.weight[:, self.dnet:], lin.bias))
+                h = F.relu(_Linear2.apply(x, lin.weight[:, :self.dnet], h, lin.weight[:, self.dnet:], lin.bias))
             else:
                 h = F.relu(_lin(h, lin.weight, lin.bias))
-        alpha = _lin(h, self.alpha_linear.weight, self.alpha_linear.bias)
-        feature = _lin(h, self.feature_linear.weight, self.feature_linear.bias)
+        alpha, feature = _Heads.apply(h, self.alpha_linear.weight, self.alpha_linear.bias,
+                                      self.feature_linear.weight, self.feature_linear.bias)
         W = feature.shape[1]
         vl = self.views_linears[0]
         nv = self.cfg.input_ch_views
-        g = _lin(feature, vl.weight[:, :W]) + _lin(views, vl.weight[:, W:W + nv], vl.bias)
+        g = _Linear2.apply(feature, vl.weight[:, :W], views, vl.weight[:, W:W + nv], vl.bias)
         if self.cfg.opt_framecode:
             g = g + _lin(self.framecodes(cams), vl.weight[:, W + nv:])
         g = F.relu(g)
