@@ -155,6 +155,42 @@ class _Linear2(torch.autograd.Function):
         return ga, gwa, gb, gwb, gbias
 
 
+class _SplitCols(torch.autograd.Function):
+    """(x, x, views) = (feat[:, :d] twice, feat[:, d:]): x feeds layer 0 and the skip layer through
+    separate outputs, so the backward writes dL/dfeat once — the two x gradients summed straight
+    into its first columns, the views gradient into the rest — instead of autograd's sum of the x
+    gradients plus two zero-filled full-width slice gradients and their sum."""
+
+    @staticmethod
+    def forward(ctx, feat, d):
+        ctx.shape = feat.shape
+        ctx.d = d
+        return feat[:, :d], feat[:, :d], feat[:, d:]
+
+    @staticmethod
+    def backward(ctx, gx0, gx1, gv):
+        m, f = ctx.shape
+        d = ctx.d
+        g = None
+        for t in (gx0, gx1, gv):
+            if t is not None:
+                g = torch.empty(m, f, device=t.device, dtype=t.dtype)
+                break
+        if g is None:
+            return None, None
+        if gx0 is not None and gx1 is not None:
+            torch.add(gx0, gx1, out=g[:, :d])
+        elif gx0 is not None or gx1 is not None:
+            g[:, :d] = gx0 if gx0 is not None else gx1
+        else:
+            g[:, :d] = 0
+        if gv is not None:
+            g[:, d:] = gv
+        else:
+            g[:, d:] = 0
+        return g, None
+
+
 class _Heads(torch.autograd.Function):
     """alpha_linear and feature_linear on the same h: the gradient of h is one GEMM plus a rank-1
     update accumulated into it (no separate add of two [M, W] gradients)."""
@@ -214,12 +250,12 @@ class NeRF(nn.Module):
 
     def forward(self, feat, cams=None):
         """feat [M, F] = [v | r | views] -> raw [M, 4] (rgb, alpha): forward_density + forward_view."""
-        x = feat[:, :self.dnet]
-        views = feat[:, self.dnet:]
+        x, x_skip, views = _SplitCols.apply(feat, self.dnet)
         h = x
         for i, lin in enumerate(self.pts_linears):
             if i > 0 and (i - 1) in self.skips:  # cat([input_pts, h]) @ W.T = x @ Wx.T + h @ Wh.T
-                h = F.relu(_Linear2.apply(x, lin.weight[:, :self.dnet], h, lin.weight[:, self.dnet:], lin.bias))
+                h = F.relu(_Linear2.apply(x_skip, lin.weight[:, :self.dnet], h, lin.weight[:, self.dnet:],
+                                          lin.bias))
             else:
                 h = F.relu(_lin(h, lin.weight, lin.bias))
         alpha, feature = _Heads.apply(h, self.alpha_linear.weight, self.alpha_linear.bias,
