@@ -131,28 +131,54 @@ def _lin(x, w, b=None):
     return _Linear.apply(x, w, b)
 
 
+class _LinearReLU(torch.autograd.Function):
+    """relu(F.linear(x, w, b)) with bias and relu in the GEMM's epilogue (torch._addmm_activation),
+    so the forward launches no separate relu; backward masks by the saved output as relu does."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        out = torch._addmm_activation(b, x, w.t(), use_gelu=False)
+        ctx.save_for_backward(x, w, out)
+        return out
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w, out = ctx.saved_tensors
+        gp = torch.ops.aten.threshold_backward(gy, out, 0.0)
+        need = ctx.needs_input_grad
+        gx = gp.mm(w) if need[0] else None
+        gw = _splitk_wgrad(gp, x) if need[1] else None
+        gb = gp.sum(0) if need[2] else None
+        return gx, gw, gb
+
+
 class _Linear2(torch.autograd.Function):
     """a @ wa.T + b @ wb.T + bias (the skip layer's cat([x, h]) and the view layer's cat([feature,
     views]) with the weight split by columns): the second product accumulates into the first
     GEMM's output (beta = 1), so neither direction launches a separate add."""
 
     @staticmethod
-    def forward(ctx, a, wa, b, wb, bias):
-        ctx.save_for_backward(a, wa, b, wb)
+    def forward(ctx, a, wa, b, wb, bias, relu=False):
         ctx.has_bias = bias is not None
-        out = F.linear(b, wb, bias)
-        return out.addmm_(a, wa.t())
+        ctx.relu = relu
+        out = F.linear(b, wb, bias).addmm_(a, wa.t())
+        if relu:
+            out.relu_()
+        ctx.save_for_backward(a, wa, b, wb, out if relu else None)
+        return out
 
     @staticmethod
     def backward(ctx, g):
-        a, wa, b, wb = ctx.saved_tensors
+        a, wa, b, wb, out = ctx.saved_tensors
+        if ctx.relu:
+            g = torch.ops.aten.threshold_backward(g, out, 0.0)
         need = ctx.needs_input_grad
         ga = g.mm(wa) if need[0] else None
         gwa = _splitk_wgrad(g, a) if need[1] else None
         gb = g.mm(wb) if need[2] else None
         gwb = _splitk_wgrad(g, b) if need[3] else None
         gbias = g.sum(0) if ctx.has_bias and need[4] else None
-        return ga, gwa, gb, gwb, gbias
+        return ga, gwa, gb, gwb, gbias, None
 
 
 class _SplitCols(torch.autograd.Function):
@@ -254,19 +280,19 @@ class NeRF(nn.Module):
         h = x
         for i, lin in enumerate(self.pts_linears):
             if i > 0 and (i - 1) in self.skips:  # cat([input_pts, h]) @ W.T = x @ Wx.T + h @ Wh.T
-                h = F.relu(_Linear2.apply(x_skip, lin.weight[:, :self.dnet], h, lin.weight[:, self.dnet:],
-                                          lin.bias))
+                h = _Linear2.apply(x_skip, lin.weight[:, :self.dnet], h, lin.weight[:, self.dnet:], lin.bias, True)
             else:
-                h = F.relu(_lin(h, lin.weight, lin.bias))
+                h = _LinearReLU.apply(h, lin.weight, lin.bias)
         alpha, feature = _Heads.apply(h, self.alpha_linear.weight, self.alpha_linear.bias,
                                       self.feature_linear.weight, self.feature_linear.bias)
         W = feature.shape[1]
         vl = self.views_linears[0]
         nv = self.cfg.input_ch_views
-        g = _Linear2.apply(feature, vl.weight[:, :W], views, vl.weight[:, W:W + nv], vl.bias)
         if self.cfg.opt_framecode:
-            g = g + _lin(self.framecodes(cams), vl.weight[:, W + nv:])
-        g = F.relu(g)
+            g = _Linear2.apply(feature, vl.weight[:, :W], views, vl.weight[:, W:W + nv], vl.bias)
+            g = F.relu(g + _lin(self.framecodes(cams), vl.weight[:, W + nv:]))
+        else:
+            g = _Linear2.apply(feature, vl.weight[:, :W], views, vl.weight[:, W:W + nv], vl.bias, True)
         rgb = _lin(g, self.rgb_linear.weight, self.rgb_linear.bias)
         return torch.cat([rgb, alpha], -1)
 
