@@ -257,9 +257,10 @@ def main():
                          "timing": "HIP events on the launch stream around anerf_render_rays: the coarse and the "
                                    "fine render_kernel launch (+ near/far, 0.2 %); rocprofv3's render_kernel "
                                    "average x launches_per_step agrees (profiles/)",
-                         "flop": "executed MFMA FLOPs per launch (device counters) / launch time; peak = the "
-                                 "FP32 (157.3) and BF16 (2516.6 TF) MFMA peaks weighted by this launch's mix",
-                         "mfma_f32_per_launch": n_f32, "mfma_bf16_per_launch": n_bf16,
+                         "flop": "executed MFMA FLOPs of one step's launches (device counters) / their time "
+                                 "(kernel_ms), the same ratio as per launch; peak = the FP32 (157.3) and BF16 "
+                                 "(2516.6 TF) MFMA peaks weighted by the step's instruction mix; traffic per step",
+                         "mfma_f32_per_step": n_f32, "mfma_bf16_per_step": n_bf16,
                          "reference_flop_per_ray": flop_ray,
                          "reference_equivalent_tflops": round(ref_equiv_tf, 2)},
             "cpu_baseline": cpu,
