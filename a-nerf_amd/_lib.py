@@ -31,7 +31,7 @@ class ModelDesc(ctypes.Structure):
                 ("cutoff_viewdir", ctypes.c_int32), ("framecode_ch", ctypes.c_int32),
                 ("n_framecodes", ctypes.c_int32), ("density_softplus", ctypes.c_int32),
                 ("softplus_shift", ctypes.c_float), ("density_scale", ctypes.c_float),
-                ("has_fine", ctypes.c_int32)]
+                ("has_fine", ctypes.c_int32), ("single_net", ctypes.c_int32)]
 
 
 class NetWeights(ctypes.Structure):
@@ -57,6 +57,7 @@ SIGNATURES = {
                                           ctypes.POINTER(NetWeights), ctypes.POINTER(EmbedParams), ctypes.c_int,
                                           ctypes.POINTER(ctypes.c_void_p)]),
     "anerf_model_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "anerf_model_set_embed": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(EmbedParams)]),
     "anerf_model_bytes": (ctypes.c_size_t, [ctypes.c_void_p]),
     "anerf_workspace_size": (ctypes.c_size_t, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]),
     "anerf_render_rays": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64,
@@ -71,7 +72,7 @@ SIGNATURES = {
                                       ctypes.c_void_p, ctypes.c_int64, ctypes.c_float, ctypes.c_float,
                                       ctypes.c_void_p, ctypes.c_void_p]),
     "anerf_near_far": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p,
-                                      ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
     "anerf_encode_points": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                            ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
@@ -131,7 +132,8 @@ SIGNATURES = {
                                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                       ctypes.c_void_p, ctypes.c_void_p]),
     "anerf_train_importance": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
-                                              ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+                                              ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+                                              ctypes.c_void_p, ctypes.c_void_p]),
 }
 
 _lib = None

@@ -1,4 +1,10 @@
-"""Build libanerf_hip.so in-tree (hipcc, gfx950).  Used by __graft_entry__.build()."""
+"""Build libanerf_hip.so in-tree (hipcc, gfx950).  Used by __graft_entry__.build().
+
+Rebuilds are content-addressed: a sha256 over the compiler command, every file under csrc/ and
+include/anerf.h is stored next to the library (`libanerf_hip.so.stamp`).  A shipped binary whose
+stamp does not match the sources is rebuilt, never reused because of its mtime.
+"""
+import hashlib
 import os
 import subprocess
 import sys
@@ -6,27 +12,44 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = [os.path.join(HERE, "csrc", "anerf_render.hip")]
 OUT = os.path.join(HERE, "libanerf_hip.so")
+STAMP = OUT + ".stamp"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize", "-fPIC", "-shared",
          "-Wno-unused-result"]
 
 
-def needs_build():
-    if not os.path.exists(OUT):
-        return True
-    t = os.path.getmtime(OUT)
-    deps = SRC + [os.path.join(HERE, "csrc", f) for f in os.listdir(os.path.join(HERE, "csrc"))]
+def source_hash():
+    """sha256 over the flags and the bytes of csrc/* + include/anerf.h (sorted by name)."""
+    h = hashlib.sha256()
+    h.update(" ".join(FLAGS).encode())
+    csrc = os.path.join(HERE, "csrc")
+    deps = sorted(os.path.join(csrc, f) for f in os.listdir(csrc))
     deps.append(os.path.join(os.path.dirname(HERE), "include", "anerf.h"))
-    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+    for d in deps:
+        if os.path.isfile(d):
+            h.update(os.path.basename(d).encode())
+            with open(d, "rb") as f:
+                h.update(f.read())
+    return h.hexdigest()
+
+
+def stamp_matches():
+    if not (os.path.exists(OUT) and os.path.exists(STAMP)):
+        return False
+    with open(STAMP) as f:
+        return f.read().strip() == source_hash()
 
 
 def build(force=False, verbose=True):
-    if not force and not needs_build():
+    if not force and stamp_matches():
         return OUT
+    digest = source_hash()
     cmd = [HIPCC] + FLAGS + ["-o", OUT] + SRC
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
+    with open(STAMP, "w") as f:
+        f.write(digest + "\n")
     return OUT
 
 

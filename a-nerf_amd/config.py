@@ -43,8 +43,6 @@ class RenderConfig:
             raise NotImplementedError("use_viewdirs=False (output_linear head) is not implemented")
         if self.multires_bones != 0:
             raise NotImplementedError("multires_bones > 0 is not implemented (configs use 0)")
-        if self.single_net:
-            raise NotImplementedError("single_net is not implemented yet")
         if len(self.skips) != 1 or self.skips[0] < 0:
             # a skip index >= netdepth-1 is never reached (D=4 configs): no skip layer
             raise NotImplementedError(f"skips={self.skips}: exactly one skip index is supported")
@@ -52,8 +50,8 @@ class RenderConfig:
             raise NotImplementedError(f"netwidth={self.netwidth}: multiples of 64 up to 256 are supported")
         if self.netdepth < 2 or self.netdepth > 16:
             raise NotImplementedError(f"netdepth={self.netdepth} outside [2, 16]")
-        if self.multires not in (7, 10) or self.multires_views != 4:
-            raise NotImplementedError("kernel instances exist for multires in {7, 10} and multires_views == 4")
+        if self.multires not in (7, 10) or self.multires_views not in (0, 4):
+            raise NotImplementedError("kernel instances exist for multires in {7, 10} and multires_views in {0, 4}")
         if self.density_type not in ("relu", "softplus"):
             raise NotImplementedError(f"density activation {self.density_type} is undefined")
         if self.opt_framecode and self.n_framecodes <= 0:

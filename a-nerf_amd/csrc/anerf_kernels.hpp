@@ -29,7 +29,9 @@ __global__ __launch_bounds__(256, 1) void render_kernel(ModelDev M, RenderArgs A
         const int r = idx / (M.nj * 12), e = idx % (M.nj * 12);
         const int j = e / 12, c = e % 12;
         const int pose = __float_as_int(lds[P.ray + 16 * r + 10]);
-        lds[P.sk + P.sk_stride * r + e] = A.skts[((int64_t)pose * M.nj + j) * 16 + c];
+        // (an out-of-range pose index renders NaN and is never dereferenced)
+        lds[P.sk + P.sk_stride * r + e] = (pose >= 0 && pose < A.n_poses) ? A.skts[((int64_t)pose * M.nj + j) * 16 + c]
+                                                                           : __int_as_float(0x7fc00000);
     }
     stage_cut(M, lds + P.cut, tid);
     // coarse samples (sample_from_lineseg, ray_utils.py:218-224)
@@ -54,16 +56,25 @@ __global__ __launch_bounds__(256, 1) void render_kernel(ModelDev M, RenderArgs A
         const NetDev& net = M.net[pass];
         const int n = pass == 0 ? S : T;
         const int zoff = pass == 0 ? P.zc : P.zf;
-        stage_bias<W>(M, net, lds + P.bias, tid);  // (synced below)
-        compute_view_factor<WH, 4>(M, net, lds, P, nr, tid, st);
+        // single_net fine pass (raycasters.py:462-468): the same network on the I new samples only
+        // (z_is, left by importance() in the ray's scratch at 6 z_stride), raws after the coarse ones
+        // (cat([raw, raw_is]) order), merged by sorted_idx below; biases and G are still in LDS
+        const bool only_new = pass == 1 && M.single_net;
+        if (!only_new) {
+            stage_bias<W>(M, net, lds + P.bias, tid);  // (synced below)
+            if (M.mrv == 0) compute_view_factor<WH, 0>(M, net, lds, P, nr, tid, st);
+            else compute_view_factor<WH, 4>(M, net, lds, P, nr, tid, st);
+        }
         STAMP(st, 1);
         // ---- MLP over 32-sample blocks, round-robin over the 4 waves
-        const int nb = (n + 31) / 32;
+        const int nm = only_new ? I : n;
+        const int nb = (nm + 31) / 32;
         for (int b = wave; b < nr * nb; b += 4) {
             const int r = b / nb, s0 = (b % nb) * 32;
+            const float* zr = only_new ? lds + P.scr + P.scr_stride * r + 6 * P.z_stride : lds + zoff + P.z_stride * r;
+            float* rawr = lds + P.raw + P.raw_stride * r + (only_new ? 4 * S : 0);
             mlp_block<W, MR, PREC>(M, net, lds + P.ray + 16 * r, lds + P.sk + P.sk_stride * r, lds + P.cut,
-                             lds + zoff + P.z_stride * r, n, s0, lds + P.g + P.g_stride * r,
-                             lds + P.raw + P.raw_stride * r, lane, A.mfma_count, lds + P.bias,
+                             zr, nm, s0, lds + P.g + P.g_stride * r, rawr, lane, A.mfma_count, lds + P.bias,
                              (P.uf >= 0 && M.skip + 1 < M.D) ? lds + P.uf + wave * P.uf_stride : nullptr,
                              lds + P.wv + wave * P.wv_stride, st);
         }
@@ -77,8 +88,19 @@ __global__ __launch_bounds__(256, 1) void render_kernel(ModelDev M, RenderArgs A
             const int64_t i = ray0 + r;
             const float* ray = lds + P.ray + 16 * min(r, R - 1);
             const float* z = lds + zoff + P.z_stride * min(r, R - 1);
-            const float* raw = lds + P.raw + P.raw_stride * min(r, R - 1);
+            float* raw = lds + P.raw + P.raw_stride * min(r, R - 1);
             float* scr = lds + P.scr + P.scr_stride * min(r, R - 1);
+            if (only_new) {  // raw = cat([raw, raw_is])[sorted_idx] (_merge_encodings on 'raw', :466-468)
+                const int* src = reinterpret_cast<const int*>(scr + 7 * P.z_stride);
+                if (active)
+                    for (int k = lane; k < T; k += 64)
+                        *reinterpret_cast<f32x4*>(scr + 4 * k) = *reinterpret_cast<const f32x4*>(raw + 4 * src[k]);
+                wave_sync();
+                if (active)
+                    for (int k = lane; k < T; k += 64)
+                        *reinterpret_cast<f32x4*>(raw + 4 * k) = *reinterpret_cast<const f32x4*>(scr + 4 * k);
+                wave_sync();
+            }
             const bool final_pass = pass == n_pass - 1;
             float* o_rgb = final_pass ? A.rgb : A.rgb0;
             float* o_disp = final_pass ? A.disp : A.disp0;
@@ -109,7 +131,9 @@ __global__ __launch_bounds__(256, 1) void render_kernel(ModelDev M, RenderArgs A
             if (pass == 0 && I > 0) {
                 if (active && A.dbg_w0)
                     for (int s = lane; s < S; s += 64) A.dbg_w0[i * S + s] = scr[s];
-                importance(z, scr, S, I, lds + P.zf + P.z_stride * min(r, R - 1), scr + P.z_stride, active, lane);
+                importance(z, scr, S, I, lds + P.zf + P.z_stride * min(r, R - 1), scr + P.z_stride, active, lane,
+                           nullptr, M.single_net != 0, M.single_net ? reinterpret_cast<int*>(scr + 7 * P.z_stride) : nullptr,
+                           M.single_net ? scr + 6 * P.z_stride : nullptr);
             }
         }
         __syncthreads();
@@ -196,12 +220,18 @@ __global__ __launch_bounds__(256, 1) void density_kernel(ModelDev M, DensityArgs
 
 // ======================================================================= small kernels
 __global__ void near_far_kernel(const float* __restrict__ rb, int stride, int64_t n, const float* __restrict__ cyls,
-                                const int32_t* __restrict__ ray_pose, float* __restrict__ near_out,
+                                const int32_t* __restrict__ ray_pose, int n_poses, float* __restrict__ near_out,
                                 float* __restrict__ far_out, uint8_t* __restrict__ qnan) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const float* r = rb + i * stride;
-    const float* cy = cyls + 5 * (ray_pose ? ray_pose[i] : 0);
+    const int pose = ray_pose ? ray_pose[i] : 0;
+    if (pose < 0 || pose >= n_poses) {  // out-of-range pose index: a miss (filled by the chunk mean)
+        near_out[i] = far_out[i] = __int_as_float(0x7fc00000);
+        qnan[i] = 1;
+        return;
+    }
+    const float* cy = cyls + 5 * pose;
     const float nearv = r[6], farv = r[7];
     // g_axes = [0, -1]: the x-z ground plane (ray_utils.py:292-327)
     const float rn0 = r[0] + r[3] * nearv, rn1 = r[2] + r[5] * nearv;

@@ -279,7 +279,9 @@ static int validate_desc(const anerf_model_desc* d) {
         return fail(ANERF_EINVAL, "net_width must be 64, 128 or 256");
     if (d->net_depth < 2 || d->net_depth > MAXL) return fail(ANERF_EINVAL, "net_depth outside [2, 16]");
     if (d->multires != 7 && d->multires != 10) return fail(ANERF_EINVAL, "multires must be 7 or 10");
-    if (d->multires_views != 4) return fail(ANERF_EINVAL, "multires_views must be 4 (the reference default)");
+    if (d->multires_views != 4 && d->multires_views != 0)
+        return fail(ANERF_EINVAL, "multires_views must be 4 (the reference default) or 0 (surreal_single.txt)");
+    if (d->single_net && d->has_fine) return fail(ANERF_EINVAL, "single_net models have no separate fine network");
     if (d->n_joints < 1 || d->n_joints > 128) return fail(ANERF_EINVAL, "n_joints outside [1, 128]");
     if (d->skip < 0) return fail(ANERF_EINVAL, "skip must be >= 0");
     if (d->framecode_ch < 0 || d->framecode_ch > 64) return fail(ANERF_EINVAL, "framecode_ch outside [0, 64]");

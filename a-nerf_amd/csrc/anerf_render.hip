@@ -124,6 +124,7 @@ int anerf_model_create(const anerf_model_desc* desc, const anerf_net_weights* co
         const char* e = std::getenv("ANERF_UX6");
         md.ux6 = !(e && e[0] == '0');
     }
+    md.single_net = desc->single_net ? 1 : 0;
     md.shift = desc->softplus_shift;
     md.B = desc->density_scale;
     md.tau = embed->tau;
@@ -146,6 +147,26 @@ int anerf_model_destroy(anerf_model* m) {
 
 size_t anerf_model_bytes(const anerf_model* m) { return m ? m->dev_bytes : 0; }
 
+int anerf_model_set_embed(anerf_model* m, const anerf_embed_params* embed) {
+    if (!m || !embed) return fail(ANERF_EINVAL, "anerf_model_set_embed: NULL argument");
+    if (embed->cutoff_dist || embed->cutoff_dist_v) {
+        const size_t nb = sizeof(float) * (size_t)m->desc.n_joints;
+        int prev = 0;
+        HIP_TRY(hipGetDevice(&prev));
+        HIP_TRY(hipSetDevice(m->device));
+        hipError_t e = hipDeviceSynchronize();
+        if (e == hipSuccess && embed->cutoff_dist)
+            e = hipMemcpy(const_cast<float*>(m->md.cutoff), embed->cutoff_dist, nb, hipMemcpyHostToDevice);
+        if (e == hipSuccess && embed->cutoff_dist_v)
+            e = hipMemcpy(const_cast<float*>(m->md.cutoff_v), embed->cutoff_dist_v, nb, hipMemcpyHostToDevice);
+        hipSetDevice(prev);
+        if (e != hipSuccess) return fail(ANERF_EHIP, std::string("anerf_model_set_embed: ") + hipGetErrorString(e));
+    }
+    m->md.tau = embed->tau;
+    m->md.tau_v = embed->tau_v;
+    return ANERF_OK;
+}
+
 static size_t ws_near_far_bytes(int64_t n) {
     // near, far, fill scratch (floats) + qnan flags, each 256-byte aligned
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
@@ -164,7 +185,7 @@ size_t anerf_workspace_size(const anerf_model* m, int64_t n_rays, int32_t n_samp
 }
 
 static int launch_near_far(const float* rb, int stride, int64_t n, const float* cyls, const int32_t* ray_pose,
-                           int chunk, char* ws, float** near_o, float** far_o, hipStream_t st) {
+                           int n_poses, int chunk, char* ws, float** near_o, float** far_o, hipStream_t st) {
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     float* nearp = reinterpret_cast<float*>(ws);
     float* farp = reinterpret_cast<float*>(ws + al(sizeof(float) * n));
@@ -172,7 +193,7 @@ static int launch_near_far(const float* rb, int stride, int64_t n, const float* 
     uint8_t* qnan = reinterpret_cast<uint8_t*>(ws + 3 * al(sizeof(float) * n));
     const int bs = 256;
     hipLaunchKernelGGL(near_far_kernel, dim3((unsigned)((n + bs - 1) / bs)), dim3(bs), 0, st, rb, stride, n, cyls,
-                       ray_pose, nearp, farp, qnan);
+                       ray_pose, n_poses, nearp, farp, qnan);
     const int64_t nchunks = (n + chunk - 1) / chunk;
     hipLaunchKernelGGL(nan_fill_kernel, dim3((unsigned)nchunks), dim3(256), 0, st, rb, stride, n, chunk, nearp, farp,
                        qnan, scratch);
@@ -182,16 +203,17 @@ static int launch_near_far(const float* rb, int stride, int64_t n, const float* 
     return ANERF_OK;
 }
 
-int anerf_near_far(const float* ray_batch, int32_t ray_stride, int64_t n_rays, const float* cyls,
+int anerf_near_far(const float* ray_batch, int32_t ray_stride, int64_t n_rays, const float* cyls, int32_t n_poses,
                    const int32_t* ray_pose, int32_t chunk, float* near_out, float* far_out, void* workspace,
                    size_t workspace_bytes, void* stream) {
     if (n_rays <= 0) return ANERF_OK;
-    if (!ray_batch || !cyls || !near_out || !far_out || ray_stride < 8 || chunk <= 0)
+    if (!ray_batch || !cyls || !near_out || !far_out || ray_stride < 8 || chunk <= 0 || n_poses < 1)
         return fail(ANERF_EINVAL, "anerf_near_far: bad arguments");
     if (!workspace || workspace_bytes < ws_near_far_bytes(n_rays)) return fail(ANERF_EWORKSPACE, "workspace too small");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     float *np_, *fp_;
-    int rc = launch_near_far(ray_batch, ray_stride, n_rays, cyls, ray_pose, chunk, (char*)workspace, &np_, &fp_, st);
+    int rc = launch_near_far(ray_batch, ray_stride, n_rays, cyls, ray_pose, n_poses, chunk,
+                             (char*)workspace, &np_, &fp_, st);
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(near_out, np_, sizeof(float) * n_rays, hipMemcpyDeviceToDevice, st));
     HIP_TRY(hipMemcpyAsync(far_out, fp_, sizeof(float) * n_rays, hipMemcpyDeviceToDevice, st));
@@ -221,7 +243,8 @@ int anerf_render_rays(const anerf_model* m, const float* ray_batch, int32_t ray_
         return fail(ANERF_EINVAL, "anerf_render_rays: bad arguments");
     if (n_samples < 2 || n_samples > 1024 || n_importance < 0 || n_importance > 2048)
         return fail(ANERF_EINVAL, "n_samples must be in [2, 1024], n_importance in [0, 2048]");
-    if (n_importance > 0 && !m->desc.has_fine) return fail(ANERF_EINVAL, "n_importance > 0 needs a fine network");
+    if (n_importance > 0 && !m->desc.has_fine && !m->desc.single_net)
+        return fail(ANERF_EINVAL, "n_importance > 0 needs a fine network (or a single_net model)");
     if (n_importance > 0 && n_samples < 3) return fail(ANERF_EINVAL, "importance sampling needs n_samples >= 3");
     if (m->desc.framecode_ch > 0 && !cams) return fail(ANERF_EINVAL, "model uses framecodes: cams required");
     if (chunk <= 0) return fail(ANERF_EINVAL, "chunk must be > 0");
@@ -233,7 +256,8 @@ int anerf_render_rays(const anerf_model* m, const float* ray_batch, int32_t ray_
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
 
     float *nearp, *farp;
-    int rc = launch_near_far(ray_batch, ray_stride, n_rays, cyls, ray_pose, chunk, (char*)workspace, &nearp, &farp, st);
+    int rc = launch_near_far(ray_batch, ray_stride, n_rays, cyls, ray_pose, n_poses, chunk, (char*)workspace, &nearp,
+                             &farp, st);
     if (rc) return rc;
     if (debug && debug->near) HIP_TRY(hipMemcpyAsync(debug->near, nearp, 4 * n_rays, hipMemcpyDeviceToDevice, st));
     if (debug && debug->far) HIP_TRY(hipMemcpyAsync(debug->far, farp, 4 * n_rays, hipMemcpyDeviceToDevice, st));
@@ -263,6 +287,7 @@ int anerf_render_rays(const anerf_model* m, const float* ray_batch, int32_t ray_
     a.I = I;
     a.R = R;
     a.skts = skts;
+    a.n_poses = n_poses;
     a.ray_pose = ray_pose;
     a.cams = cams;
     a.near = nearp;
@@ -289,7 +314,8 @@ int anerf_render_rays(const anerf_model* m, const float* ray_batch, int32_t ray_
     // With importance sampling the coarse and the fine pass run as two launches: every CU then
     // streams one network's weights at a time, which fit an XCD's 4 MB L2 (both together do not);
     // the fine z lists (T floats per ray) go through the workspace.
-    const int pstep = (I > 0 && !fused_passes()) ? 1 : 2;
+    // (single_net: one network, so one launch; the fine pass reuses the coarse raws, biases and G in LDS)
+    const int pstep = (I > 0 && !fused_passes() && !m->desc.single_net) ? 1 : 2;
     a.zf_ws = I > 0 ? reinterpret_cast<float*>((char*)workspace + ws_near_far_bytes(n_rays)) : nullptr;
     const unsigned grid = (unsigned)((n_rays + R - 1) / R);
     const size_t lds_bytes = (size_t)P.total * 4;
@@ -430,7 +456,7 @@ int anerf_train_encode(const anerf_model* m, const float* ray_batch, int32_t ray
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(train_encode_kernel, dim3(blocks_of(n_rays * n_samples * m->desc.n_joints, 256)), dim3(256), 0,
                        st, m->md,
-                       ray_batch, ray_stride, n_rays, z, n_samples, skts, ray_pose, feat_out);
+                       ray_batch, ray_stride, n_rays, z, n_samples, skts, ray_pose, n_poses, feat_out);
     HIP_TRY(hipGetLastError());
     return ANERF_OK;
 }
@@ -446,7 +472,7 @@ int anerf_train_encode_backward(const anerf_model* m, const float* ray_batch, in
     if (nb > 0x7fffffff) return fail(ANERF_EINVAL, "too many rays for one launch");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(train_encode_backward_kernel, dim3((unsigned)nb), dim3(256), 0, st, m->md, ray_batch,
-                       ray_stride, n_rays, z, n_samples, skts, ray_pose, grad_feat, grad_skts);
+                       ray_stride, n_rays, z, n_samples, skts, ray_pose, n_poses, grad_feat, grad_skts);
     HIP_TRY(hipGetLastError());
     return ANERF_OK;
 }
@@ -483,20 +509,21 @@ int anerf_train_composite_backward(const anerf_model* m, const float* raw, const
 }
 
 int anerf_train_importance(const float* z, const float* weights, int64_t n_rays, int32_t n_samples,
-                           int32_t n_importance, const float* u, float* z_all, void* stream) {
+                           int32_t n_importance, const float* u, int32_t single_net, float* z_all,
+                           int32_t* sorted_idx, void* stream) {
     if (!z || !weights || !z_all || n_rays < 0 || n_samples < 3 || n_importance < 1 || n_samples > 1024 ||
         n_importance > 2048)
         return fail(ANERF_EINVAL, "anerf_train_importance: bad arguments");
     if (n_rays == 0) return ANERF_OK;
     if (n_rays > 0x7fffffff) return fail(ANERF_EINVAL, "too many rays for one launch");
     const int T = n_samples + n_importance;
-    const size_t lds = (size_t)(3 * pad32(T) + 3 * n_samples + T + 32) * 4;
+    const size_t lds = (size_t)(3 * pad32(T) + 3 * n_samples + 2 * T + 32) * 4;
     if (lds > 160 * 1024) return fail(ANERF_EINVAL, "n_samples + n_importance too large");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     HIP_TRY(hipFuncSetAttribute((const void*)train_importance_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds));
     hipLaunchKernelGGL(train_importance_kernel, dim3((unsigned)n_rays), dim3(64), lds, st, z, weights, n_rays,
-                       n_samples, n_importance, u, z_all);
+                       n_samples, n_importance, u, single_net, z_all, sorted_idx);
     HIP_TRY(hipGetLastError());
     return ANERF_OK;
 }
@@ -509,6 +536,7 @@ static int launch_density(const anerf_model* m, DensityArgs a, int32_t precision
     HIP_TRY(hipGetDevice(&dev));
     if (dev != m->device) return fail(ANERF_EINVAL, "current device differs from the model's device");
     if (a.net < 0) a.net = m->desc.has_fine ? 1 : 0;  // the reference's default network (raycasters.py:616-620)
+    if (a.net == 1 && m->desc.single_net) a.net = 0;  // network_fine is network_fn
     if (a.net > 1 || (a.net == 1 && !m->desc.has_fine)) return fail(ANERF_EINVAL, "no such network");
     const int W = m->desc.net_width, mr = m->desc.multires;
     const LdsPlan P = make_density_plan(m->desc.n_joints, W, m->desc.net_depth, m->njh2);

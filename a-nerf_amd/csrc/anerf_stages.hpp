@@ -218,8 +218,14 @@ __device__ __forceinline__ bool z_eq(float a, float b) { return a == b || (a != 
 // weights w (S) in scr; writes sorted z_all (S+I) to zf.
 // u: the I uniform samples of this ray (training, det=False: torch.rand), or NULL for the
 // deterministic linspace of eval.
+// single_net (is_only, ray_utils.py:270-277): the weights are 0.5 (max(w_l, w_k) + max(w_k, w_u)) + 0.01
+// instead of w_k; src (optional) receives sorted_idx (src[rank] = index into cat([z, z_is])) and
+// zis (optional) the I new samples in sample order.
+__device__ __forceinline__ float torch_maximum(float a, float b) { return (a != a || a > b) ? a : b; }
+
 __device__ void importance(const float* zc, const float* w, int S, int I, float* zf, float* scr2, bool active,
-                           int lane, const float* u_rand = nullptr) {
+                           int lane, const float* u_rand = nullptr, bool is_only = false, int* src = nullptr,
+                           float* zis = nullptr) {
     const int nb = S - 1;  // bins = mids
     float* mids = scr2;
     float* wp = scr2 + nb;
@@ -227,7 +233,14 @@ __device__ void importance(const float* zc, const float* w, int S, int I, float*
     float* zall = scr2 + 3 * nb + 1;  // S + I unsorted
     if (active) {
         for (int i = lane; i < nb; i += 64) mids[i] = 0.5f * (zc[i + 1] + zc[i]);
-        for (int i = lane; i < nb - 1; i += 64) wp[i] = w[i + 1] + 1e-5f;
+        if (is_only) {
+            for (int i = lane; i < nb - 1; i += 64) {
+                const float t = torch_maximum(w[i], w[i + 1]) + torch_maximum(w[i + 1], w[i + 2]);
+                wp[i] = (0.5f * t + 0.01f) + 1e-5f;
+            }
+        } else {
+            for (int i = lane; i < nb - 1; i += 64) wp[i] = w[i + 1] + 1e-5f;
+        }
     }
     wave_sync();
     if (active) {
@@ -271,7 +284,9 @@ __device__ void importance(const float* zc, const float* w, int S, int I, float*
             float denom = ca - cb;
             if (denom < 1e-5f) denom = 1.0f;
             const float t = (u - cb) / denom;
-            zall[S + k] = bb + t * (ba - bb);
+            const float zk = bb + t * (ba - bb);
+            zall[S + k] = zk;
+            if (zis) zis[k] = zk;
         }
         for (int i = lane; i < S; i += 64) zall[i] = zc[i];
     }
@@ -301,6 +316,7 @@ __device__ void importance(const float* zc, const float* w, int S, int I, float*
                     rank = (e - S) + lo;
                 }
                 zf[rank] = v;
+                if (src) src[rank] = e;
             }
         } else {
             for (int e = lane; e < T; e += 64) {
@@ -311,6 +327,7 @@ __device__ void importance(const float* zc, const float* w, int S, int I, float*
                     rank += z_less(x, v) || (z_eq(x, v) && f < e);
                 }
                 zf[rank] = v;
+                if (src) src[rank] = e;
             }
         }
     }

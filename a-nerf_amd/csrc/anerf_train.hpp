@@ -71,7 +71,7 @@ __device__ __forceinline__ void encode_joint(const ModelDev& M, const float* __r
 
 __global__ void train_encode_kernel(ModelDev M, const float* __restrict__ rb, int stride, int64_t n,
                                     const float* __restrict__ z, int ns, const float* __restrict__ skts,
-                                    const int32_t* __restrict__ ray_pose, float* __restrict__ feat) {
+                                    const int32_t* __restrict__ ray_pose, int n_poses, float* __restrict__ feat) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int nj = M.nj;
     if (t >= n * ns * nj) return;
@@ -83,8 +83,14 @@ __global__ void train_encode_kernel(ModelDev M, const float* __restrict__ rb, in
     const float zz = z[idx];
     const float px = ray[0] + ray[3] * zz, py = ray[1] + ray[4] * zz, pz = ray[2] + ray[5] * zz;
     const int F = nj * (1 + 2 * M.mr) + 3 * nj + 3 * nj * (1 + 2 * M.mrv);
-    const f32x4* sp = reinterpret_cast<const f32x4*>(skts + (pose * nj + j) * 16);
-    const f32x4 r0 = sp[0], r1 = sp[1], r2 = sp[2];
+    f32x4 r0, r1, r2;
+    if (pose >= 0 && pose < n_poses) {
+        const f32x4* sp = reinterpret_cast<const f32x4*>(skts + (pose * nj + j) * 16);
+        r0 = sp[0], r1 = sp[1], r2 = sp[2];
+    } else {  // out-of-range pose index: NaN features, no out-of-bounds read
+        const float q = __int_as_float(0x7fc00000);
+        r0 = r1 = r2 = f32x4{q, q, q, q};
+    }
     const float S[12] = {r0[0], r0[1], r0[2], r0[3], r1[0], r1[1], r1[2], r1[3], r2[0], r2[1], r2[2], r2[3]};
     encode_joint(M, S, j, px, py, pz, ray[3], ray[4], ray[5], feat + idx * F);
 }
@@ -201,7 +207,7 @@ __device__ __forceinline__ void encode_row_grad_joint(const ModelDev& M, const f
 __global__ __launch_bounds__(256) void train_encode_backward_kernel(ModelDev M, const float* __restrict__ rb,
                                                                     int stride, int64_t n, const float* __restrict__ z,
                                                                     int ns, const float* __restrict__ skts,
-                                                                    const int32_t* __restrict__ ray_pose,
+                                                                    const int32_t* __restrict__ ray_pose, int n_poses,
                                                                     const float* __restrict__ gfeat,
                                                                     float* __restrict__ gskts) {
     __shared__ float red[4][4][12];
@@ -210,11 +216,12 @@ __global__ __launch_bounds__(256) void train_encode_backward_kernel(ModelDev M, 
     const int j0 = (int)(blockIdx.x % ngrp) * 4;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int jj = lane & 3, j = j0 + jj;
-    const bool live = i < n && j < M.nj;
+    // (an out-of-range pose index contributes no gradient and is never dereferenced)
+    const int64_t pose = i < n ? (ray_pose ? ray_pose[i] : i) : 0;
+    const bool pose_ok = pose >= 0 && pose < n_poses;
+    const bool live = i < n && j < M.nj && pose_ok;
     float gS[12] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-    int64_t pose = 0;
     if (live) {
-        pose = ray_pose ? ray_pose[i] : i;
         const float* ray = rb + i * stride;
         const int F = M.nj * (1 + 2 * M.mr) + 3 * M.nj + 3 * M.nj * (1 + 2 * M.mrv);
         const f32x4* sp = reinterpret_cast<const f32x4*>(skts + (pose * M.nj + j) * 16);
@@ -238,10 +245,9 @@ __global__ __launch_bounds__(256) void train_encode_backward_kernel(ModelDev M, 
     __syncthreads();
     if (threadIdx.x < 48) {
         const int jq = threadIdx.x / 12, k = threadIdx.x % 12;
-        if (i < n && j0 + jq < M.nj) {
+        if (i < n && j0 + jq < M.nj && pose_ok) {
             const float v = (red[0][jq][k] + red[1][jq][k]) + (red[2][jq][k] + red[3][jq][k]);
-            const int64_t ps = ray_pose ? ray_pose[i] : i;
-            if (v != 0.0f) atomicAdd(gskts + (ps * M.nj + j0 + jq) * 16 + k, v);
+            if (v != 0.0f) atomicAdd(gskts + (pose * M.nj + j0 + jq) * 16 + k, v);
         }
     }
 }
@@ -360,7 +366,9 @@ __global__ void train_composite_backward_kernel(ModelDev M, const float* __restr
 // render kernel's importance(): one wave per ray, LDS scratch.  z_all (N x (S+I)) sorted.
 __global__ __launch_bounds__(64) void train_importance_kernel(const float* __restrict__ z,
                                                               const float* __restrict__ wts, int64_t n, int S, int I,
-                                                              const float* __restrict__ u, float* __restrict__ z_all) {
+                                                              const float* __restrict__ u, int is_only,
+                                                              float* __restrict__ z_all,
+                                                              int32_t* __restrict__ sorted_idx) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int64_t i = blockIdx.x;
     if (i >= n) return;
@@ -375,6 +383,10 @@ __global__ __launch_bounds__(64) void train_importance_kernel(const float* __res
         w[s] = wts[i * S + s];
     }
     wave_sync();
-    importance(zc, w, S, I, zf, scr2, true, lane, u ? u + i * I : nullptr);
-    for (int s = lane; s < T; s += 64) z_all[i * T + s] = zf[s];
+    int* src = reinterpret_cast<int*>(scr2 + 3 * S + T + 32);  // (after importance()'s scratch)
+    importance(zc, w, S, I, zf, scr2, true, lane, u ? u + i * I : nullptr, is_only != 0, sorted_idx ? src : nullptr);
+    for (int s = lane; s < T; s += 64) {
+        z_all[i * T + s] = zf[s];
+        if (sorted_idx) sorted_idx[i * T + s] = src[s];
+    }
 }

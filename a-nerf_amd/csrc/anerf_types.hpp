@@ -66,6 +66,7 @@ struct ModelDev {
     int nj, njh2, ngh, D, skip, mr, mrv, use_cutoff, cutoff_inputs, cutoff_viewdir, cfc, n_codes, softplus;
     int sparse;  // windowed features are exactly 0 where w == 0 (use_cutoff && cutoff_inputs)
     int ux6;     // bf16x6: bone-direction parts as x6 from the LDS feature store (u_part_x6)
+    int single_net;  // one network for both passes; the fine pass evaluates only the I new samples
     float shift, B, tau, tau_v;
     const float* cutoff;
     const float* cutoff_v;
@@ -76,6 +77,7 @@ struct RenderArgs {
     const float* rb;
     int64_t n;
     int stride, S, I, R;
+    int n_poses;
     const float* skts;
     const int32_t* ray_pose;
     const float* cams;

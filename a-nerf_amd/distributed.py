@@ -66,6 +66,32 @@ def render_rays_sharded(render_fn, ray_batch, chunk, group=None):
     return {"rgb_map": full[:, 0:3], "disp_map": full[:, 3], "acc_map": full[:, 4]}
 
 
+class ShardGather:
+    """The all-gather of render_rays_sharded with its sizes fixed up front (chunk_ranges is known on
+    every rank): per call ONE all_gather_into_tensor of a [world * m, 5] buffer (m = the largest
+    range) and one row gather that drops the padding — no size exchange, no host sync.
+    __call__(out) -> dict(rgb_map, disp_map, acc_map) of the whole ray list, ray order."""
+
+    def __init__(self, n_rays, chunk, world, device, group=None):
+        self.ranges = chunk_ranges(n_rays, chunk, world)
+        self.m = max(max(s1 - s0 for s0, s1 in self.ranges), 1)
+        self.group = group
+        rows = [torch.arange(r * self.m, r * self.m + (s1 - s0)) for r, (s0, s1) in enumerate(self.ranges)]
+        self.rows = torch.cat(rows).to(device)
+        self.local = torch.zeros(self.m, 5, device=device, dtype=torch.float32)
+        self.full = torch.empty(world * self.m, 5, device=device, dtype=torch.float32)
+
+    def __call__(self, out):
+        if out is not None:
+            k = out["rgb_map"].shape[0]
+            self.local[:k, 0:3] = out["rgb_map"].reshape(-1, 3)
+            self.local[:k, 3] = out["disp_map"].reshape(-1)
+            self.local[:k, 4] = out["acc_map"].reshape(-1)
+        dist.all_gather_into_tensor(self.full, self.local, group=self.group)
+        g = self.full.index_select(0, self.rows)
+        return {"rgb_map": g[:, 0:3].contiguous(), "disp_map": g[:, 3].contiguous(), "acc_map": g[:, 4].contiguous()}
+
+
 def gather_frames(local_frames, n_frames, group=None):
     """All-gather per-rank frames ([F_local, H, W, C] tensors) back into frame order."""
     rank, world = dist.get_rank(group), dist.get_world_size(group)

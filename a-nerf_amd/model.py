@@ -43,9 +43,18 @@ class DeviceModel:
         d.density_softplus = int(cfg.density_type == "softplus")
         d.softplus_shift, d.density_scale = cfg.softplus_shift, cfg.density_scale
         fine_sd = ckpt.get("network_fine_state_dict")
+        coarse_sd = ckpt["network_fn_state_dict"]
+        if cfg.single_net:
+            # network_fine IS network_fn (core/raycasters.py:101-104); RayCaster.load_state_dict loads
+            # network_fn_state_dict, then network_fine_state_dict into the same module (:768-788), so
+            # the latter wins when a checkpoint has both
+            if fine_sd is not None:
+                coarse_sd = fine_sd
+            fine_sd = None
+        d.single_net = int(cfg.single_net)
         d.has_fine = int(fine_sd is not None and cfg.N_importance > 0)
         self.has_fine = bool(d.has_fine)
-        coarse = self._net(ckpt["network_fn_state_dict"])
+        coarse = self._net(coarse_sd)
         fine = self._net(fine_sd) if d.has_fine else None
         e, ev = ckpt["embed_state_dict"], ckpt["embeddirs_state_dict"]
         emb = _lib.EmbedParams()
@@ -76,6 +85,19 @@ class DeviceModel:
         w.rgb_w, w.rgb_b = self._p(sd["rgb_linear.weight"]), self._p(sd["rgb_linear.bias"])
         w.codes = self._p(sd["framecodes.codes.weight"]) if cfg.opt_framecode else None
         return w
+
+    def set_embed(self, embed_sd, embeddirs_sd, cutoffs=True):
+        """New tau (and cutoff_dist) of the two embedders without repacking the weights
+        (anerf_model_set_embed): the training tau schedule."""
+        emb = _lib.EmbedParams()
+        keep = []
+        emb.tau = float(_np(embed_sd["tau"]).reshape(-1)[0])
+        emb.tau_v = float(_np(embeddirs_sd["tau"]).reshape(-1)[0])
+        if cutoffs:
+            a, b = _np(embed_sd["cutoff_dist"]), _np(embeddirs_sd["cutoff_dist"])
+            keep += [a, b]
+            emb.cutoff_dist, emb.cutoff_dist_v = a.ctypes.data_as(_lib.c_f), b.ctypes.data_as(_lib.c_f)
+        _lib.check(_lib.load().anerf_model_set_embed(self.handle, ctypes.byref(emb)), "anerf_model_set_embed")
 
     @property
     def nbytes(self):

@@ -83,7 +83,7 @@ class RayCaster:
         if network in ("coarse", 0):
             return 0
         if network in ("fine", 1):
-            if not self.model.has_fine:
+            if not self.model.has_fine and not self.cfg.single_net:  # (single_net: fine IS coarse)
                 raise ValueError("this model has no fine network")
             return 1
         raise ValueError(f"network must be None, 'coarse' or 'fine', got {network!r}")

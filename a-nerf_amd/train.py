@@ -298,12 +298,30 @@ class NeRF(nn.Module):
 
 
 class _Embed(nn.Module):
-    """CutoffEmbedder state (cutoff_embedder.py:60-95): cutoff_dist (not trained), tau buffer."""
+    """CutoffEmbedder state (cutoff_embedder.py:60-95): cutoff_dist (not trained), tau buffer, and
+    its tau schedule (update_threshold / update_tau / get_tau, :101-102, 176-183)."""
+
+    init_tau = 20.0
 
     def __init__(self, n_joints, cutoff_dist):
         super().__init__()
         self.cutoff_dist = nn.Parameter(torch.full((n_joints,), float(cutoff_dist)), requires_grad=False)
-        self.register_buffer("tau", torch.tensor(20.0))
+        self.register_buffer("tau", torch.tensor(self.init_tau))
+
+    def get_tau(self):
+        return self.tau.item()
+
+    def update_threshold(self, global_step, tau_step, tau_rate, alpha_step=None, alpha_target=None):
+        self.update_tau(global_step, tau_step, tau_rate)
+        # update_alpha is a no-op without freq_schedule (RenderConfig rejects freq_schedule)
+
+    def update_tau(self, global_step, step, rate):
+        """tau = (20 * rate ** (global_step / (step * 1000))).clamp(max=2000), the reference's own
+        expression and dtype flow (cutoff_embedder.py:181-183), written into the buffer in place."""
+        with torch.no_grad():
+            new = (self.init_tau * torch.ones_like(self.tau) * rate ** (global_step / float(step * 1000))).clamp(
+                max=2000.)
+            self.tau.copy_(new)
 
 
 class TrainRayCaster(nn.Module):
@@ -317,9 +335,17 @@ class TrainRayCaster(nn.Module):
         self.cfg = cfg.validate()
         if cfg.precision != "fp32":
             pass  # the eval delegate uses cfg.precision; training is fp32
-        dev = torch.device(f"cuda:{torch.cuda.current_device() if device is None else int(device)}")
+        if isinstance(device, (str, torch.device)):
+            dev = torch.device(device)  # (a CPU device holds the parameters only: checkpoints, no rendering)
+        else:
+            dev = torch.device(f"cuda:{torch.cuda.current_device() if device is None else int(device)}")
         self.network_fn = NeRF(cfg)
-        self.network_fine = NeRF(cfg) if cfg.N_importance > 0 else None
+        # single_net: network_fine IS network_fn (core/raycasters.py:98-104); the module is registered
+        # under both names, so state_dict() has both keys, as the reference's does
+        if cfg.N_importance > 0:
+            self.network_fine = self.network_fn if cfg.single_net else NeRF(cfg)
+        else:
+            self.network_fine = None
         # fresh models: cutoff_mm (default 500, run_nerf.py:416) x ext_scale (raycasters.py:33), tau 20
         cut = float(cfg.extra.get("cutoff_mm", 500.0)) * cfg.ext_scale
         self.embed_fn = _Embed(cfg.n_joints, cut)
@@ -329,15 +355,33 @@ class TrainRayCaster(nn.Module):
         self.to(dev)
         self._dev = dev
         self._consts = None  # DeviceModel holding the encoder / density constants (cutoffs, tau, B)
+        self._consts_embed = None
         self._eval = None
         self._eval_version = None
+        self._eval_embed = None
+
+    @property
+    def module(self):
+        """The reference's Trainer reaches the caster through nn.DataParallel's `.module`
+        (core/trainer.py:263-270); here the caster is its own module."""
+        return self
+
+    def update_embed_fns(self, global_step, args):
+        """core/raycasters.py:731-748: the tau schedule of both embedders (args.cutoff_step,
+        args.cutoff_rate); the kernels pick the new tau up at the next launch."""
+        if getattr(args, "freq_schedule", False):
+            raise NotImplementedError("--freq_schedule is not implemented")
+        for e in (self.embed_fn, self.embeddirs_fn):
+            e.update_threshold(global_step, args.cutoff_step, args.cutoff_rate,
+                               getattr(args, "freq_schedule_step", 5), getattr(args, "multires", 7) - 1)
 
     # -- checkpoints in the reference's key layout (raycasters.py:752-788)
     def load_checkpoint(self, ck):
         def t(v):
             return torch.as_tensor(v).float()
         self.network_fn.load_state_dict({k: t(v) for k, v in ck["network_fn_state_dict"].items()})
-        if self.network_fine is not None:
+        # (single_net: the same module again; the fine keys load last and win, as in raycasters.py:768-788)
+        if self.network_fine is not None and "network_fine_state_dict" in ck:
             self.network_fine.load_state_dict({k: t(v) for k, v in ck["network_fine_state_dict"].items()})
         for mod, key in ((self.embed_fn, "embed_state_dict"), (self.embeddirs_fn, "embeddirs_state_dict")):
             mod.load_state_dict({k: t(v) for k, v in ck[key].items()})
@@ -345,8 +389,10 @@ class TrainRayCaster(nn.Module):
         self._eval = None
 
     def checkpoint(self):
+        """The reference's checkpoint layout (raycasters.py:752-766) with CPU tensors: torch.save of it
+        loads with torch.load(weights_only=True) and nn.Module.load_state_dict on either side."""
         def sd(m):
-            return {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
+            return {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
         ck = {"network_fn_state_dict": sd(self.network_fn), "embed_state_dict": sd(self.embed_fn),
               "embedbones_state_dict": {}, "embeddirs_state_dict": sd(self.embeddirs_fn)}
         if self.network_fine is not None:
@@ -354,11 +400,26 @@ class TrainRayCaster(nn.Module):
         return ck
 
     def _version(self):
-        return tuple(p._version for p in self.parameters()) + tuple(b._version for b in self.buffers())
+        """Identity + version of every network tensor (a tensor replaced by assignment changes the
+        identity, an in-place update the version)."""
+        nets = [self.network_fn] + ([self.network_fine] if self.network_fine is not None else [])
+        return tuple((p.data_ptr(), p._version) for n in nets for p in n.parameters())
+
+    def _embed_version(self):
+        return tuple((t.data_ptr(), t._version) for e in (self.embed_fn, self.embeddirs_fn)
+                     for t in (e.tau, e.cutoff_dist))
+
+    def _embed_state(self):
+        return ({"tau": self.embed_fn.tau, "cutoff_dist": self.embed_fn.cutoff_dist},
+                {"tau": self.embeddirs_fn.tau, "cutoff_dist": self.embeddirs_fn.cutoff_dist})
 
     def _constants(self):
         if self._consts is None:
             self._consts = DeviceModel(self.cfg, self.checkpoint(), device=self._dev.index)
+            self._consts_embed = self._embed_version()
+        elif self._embed_version() != self._consts_embed:  # tau schedule: no repack
+            self._consts.set_embed(*self._embed_state())
+            self._consts_embed = self._embed_version()
         return self._consts
 
     @property
@@ -367,12 +428,17 @@ class TrainRayCaster(nn.Module):
         return self._constants()
 
     def eval_caster(self):
-        """The fused eval RayCaster over the current weights (repacked only after they changed)."""
+        """The fused eval RayCaster over the current weights (repacked only after they changed; a new
+        tau / cutoff reaches it without a repack)."""
         from .raycaster import RayCaster
         v = self._version()
         if self._eval is None or v != self._eval_version:
             self._eval = RayCaster(self.cfg, self.checkpoint(), device=self._dev.index)
             self._eval_version = v
+            self._eval_embed = self._embed_version()
+        elif self._embed_version() != self._eval_embed:
+            self._eval.model.set_embed(*self._embed_state())
+            self._eval_embed = self._embed_version()
         return self._eval
 
     def forward(self, *args, fwd_type="", **kwargs):
@@ -423,7 +489,7 @@ class TrainRayCaster(nn.Module):
         nearv = torch.empty(n, device=dev, dtype=torch.float32)
         farv = torch.empty(n, device=dev, dtype=torch.float32)
         ws, need = model.workspace(n, S, 0)
-        _lib.check(_lib.load().anerf_near_far(_lib.ptr(rb), rb.shape[1], n, _lib.ptr(cyl), _lib.ptr(pose),
+        _lib.check(_lib.load().anerf_near_far(_lib.ptr(rb), rb.shape[1], n, _lib.ptr(cyl), n, _lib.ptr(pose),
                                               int(chunk or max(n, 1)), _lib.ptr(nearv), _lib.ptr(farv),
                                               _lib.ptr(ws), need, _stream(dev)), "anerf_near_far")
         stochastic = perturb > 0
@@ -447,13 +513,16 @@ class TrainRayCaster(nn.Module):
             g = torch.randn(n, ns, device=dev) if g is None else g.to(dev, torch.float32)
             return (g * raw_noise_std * B).contiguous()
 
-        def run(net, zz, noise):
+        def raw_of(net, zz):
             ns = zz.shape[1]
             feat = _Encode.apply(sk, model, rb, zz, None)
-            raw = net(feat, None if cam_t is None else cam_t.repeat_interleave(ns))
-            return _Composite.apply(raw.reshape(n, ns, 4), model, zz, rb, noise)
+            return net(feat, None if cam_t is None else cam_t.repeat_interleave(ns)).reshape(n, ns, 4)
 
-        rgb, disp, acc, w, a = run(self.network_fn, z, noise_for("noise0", S))
+        def composite(raw, zz, noise):
+            return _Composite.apply(raw, model, zz, rb, noise)
+
+        raw0 = raw_of(self.network_fn, z)
+        rgb, disp, acc, w, a = composite(raw0, z, noise_for("noise0", S))
         out = {"rgb_map": rgb, "disp_map": disp, "acc_map": acc, "alpha": a}
         if I > 0:
             u = rand.get("u")
@@ -461,10 +530,21 @@ class TrainRayCaster(nn.Module):
                 u = torch.rand(n, I, device=dev)
             u = u.to(dev, torch.float32).contiguous() if stochastic else None
             z_all = torch.empty(n, S + I, device=dev, dtype=torch.float32)
+            sidx = torch.empty(n, S + I, device=dev, dtype=torch.int32) if cfg.single_net else None
             wd = w.detach().contiguous()
             _lib.check(_lib.load().anerf_train_importance(_lib.ptr(z), _lib.ptr(wd), n, S, I, _lib.ptr(u),
-                                                          _lib.ptr(z_all), _stream(dev)), "anerf_train_importance")
-            rgb1, disp1, acc1, w1, a1 = run(self.network_fine, z_all, noise_for("noise1", S + I))
+                                                          int(cfg.single_net), _lib.ptr(z_all), _lib.ptr(sidx),
+                                                          _stream(dev)), "anerf_train_importance")
+            if cfg.single_net:
+                # raycasters.py:462-468: the one network on the I new samples only, then
+                # raw = cat([raw, raw_is])[sorted_idx] (gradients reach both through the gather)
+                si = sidx.long()
+                z_is = torch.empty_like(z_all).scatter_(1, si, z_all)[:, S:].contiguous()
+                raw_cat = torch.cat([raw0, raw_of(self.network_fn, z_is)], 1)
+                raw1 = torch.gather(raw_cat, 1, si[..., None].expand(-1, -1, 4))
+            else:
+                raw1 = raw_of(self.network_fine, z_all)
+            rgb1, disp1, acc1, w1, a1 = composite(raw1, z_all, noise_for("noise1", S + I))
             out = {"rgb_map": rgb1, "disp_map": disp1, "acc_map": acc1, "alpha": a1,
                    "rgb0": rgb, "disp0": disp, "acc0": acc, "alpha0": a}
         return out

@@ -1,24 +1,30 @@
-"""Benchmark: rays/s of the A-NeRF render path at BASELINE.json config 3.
+"""Benchmark: rays/s of the A-NeRF render path (BASELINE.json configs 3 and 5).
 
-A "step" renders one synthetic 512x512 frame (64 coarse + 128 importance samples, 24-joint
-skeleton, 8x256 MLP): ray generation from the frame's bounding-cylinder pixel list, the fused
-render kernel, and frame composition — all on the GPU with inputs resident in HBM (the
-box of kp_to_valid_rays is computed on the host before the timed region; the pixels are
-enumerated on the device).
+A "step" renders one synthetic frame (64 coarse + 128 importance samples, 24-joint skeleton,
+8x256 MLP): ray generation from the frame's bounding-cylinder pixel list, the fused render
+kernel, and frame composition — all on the GPU with inputs resident in HBM (the pixel list of
+kp_to_valid_rays is computed on the host before the timed region).
 
-Multi-GPU (launched by torch.distributed.run): each rank renders its own frame (a different
-pose) per step — frames are independent, so there is no collective in the data path and
-scaling is weak; rank 0 reports total rays / max-over-ranks time.
+* N = 1 (default): config 3, one 512x512 frame per step.
+* N > 1 (launched by torch.distributed.run; default `--shard pixels --res 1024`): config 5, the
+  north star's layout — ONE 1024x1024 frame per step whose ray list is cut into whole 4096-ray
+  chunks across the ranks (each rank generates and renders only its range), then one RCCL
+  all-gather of the 20 B/ray outputs assembles the frame on every rank (strong scaling).
+  `--shard frames` keeps the weak-scaling layout (one independent frame per rank, no collective).
+Rank 0 reports the job's rays / max-over-ranks time.
 
 Extra JSON fields:
-  roofline      dominant kernel (render_kernel) vs the FP32 MFMA peak, per-launch duration
-                from HIP events on the launch stream; `achieved` counts the MFMA FLOPs the
-                launch executes (exact device counter: the kernel skips MFMAs on inputs that
-                the cutoff window makes exactly zero, so it executes fewer FLOPs than the
-                reference's 1,723,648 per sample x 256 samples per ray);
-                `reference_equivalent_tflops` prices the same launch at the reference's FLOPs
-  cpu_baseline  the C oracle (oracle/anerf_oracle.c, OpenMP) on a bounded sample of the same
-                frame's rays, rank 0 at N=1 only
+  roofline      dominant kernel (render_kernel, coarse + fine launch) against the peak of the MFMA
+                pipe its MLP runs on: `achieved` = the reference's algorithmic FLOPs (SURVEY §8(d):
+                1,723,648 per sample x 256 samples per ray) / the launches' time (HIP events on the
+                launch stream), `frac` = achieved / peak; `frac_executed` prices the MFMA
+                instructions the launches actually issue (kernel-side tally, agrees with PMC
+                SQ_INSTS_MFMA) against the instruction-mix-weighted peak — it differs because the
+                kernel skips exact-zero cutoff-window k-steps and fuses feature_linear (fewer FLOPs)
+                and splits operands for fp32 accuracy (more FLOPs)
+  parity        N = 1: the oracle's outputs for the CPU-baseline sample of the frame's rays (near /
+                far from the whole frame's chunks) against the GPU's; exits non-zero above 1e-4
+  cpu_baseline  the C oracle (oracle/anerf_oracle.c, OpenMP) on that bounded sample, rank 0 at N=1
 """
 import argparse
 import glob
@@ -53,16 +59,18 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--res", type=int, default=512)
+    ap.add_argument("--res", type=int, default=None, help="frame size (default 512; 1024 in pixels mode at N > 1)")
+    ap.add_argument("--tau", type=float, default=79.6, help="cutoff temperature of the synthetic checkpoint")
     ap.add_argument("--joints", type=int, default=24)
     ap.add_argument("--samples", type=int, default=64)
     ap.add_argument("--importance", type=int, default=128)
     ap.add_argument("--cpu-rays", type=int, default=20000, help="rays in the CPU-baseline sample")
-    ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--shard", default="frames", choices=["frames", "pixels"],
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline (and its parity check)")
+    ap.add_argument("--no-tau20", action="store_true", help="skip the tau = 20 kernel timing")
+    ap.add_argument("--shard", default=None, choices=["frames", "pixels"],
                     help="frames: one frame per rank (weak scaling, no collective); pixels: ONE frame per step "
                          "split into whole 4096-ray chunks across the ranks + an RCCL all-gather of the ray "
-                         "outputs (strong scaling, BASELINE config 5's layout)")
+                         "outputs (strong scaling, BASELINE config 5's layout; the default at N > 1)")
     ap.add_argument("--also", default="fp32,bf16x3",
                     help="other precision modes timed on the same frame afterwards (rank 0, N=1; '' = none)")
     ap.add_argument("--precision", default="bf16x6", choices=["fp32", "bf16x6", "bf16x3"],
@@ -90,29 +98,77 @@ def _config_name(H, S, I, nj):
     return known.get((H, S, I, nj), "custom")
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def kernel_time(rc, rb, S, I, skts, cyl, reps=4):
+    """Mean HIP-event time (ms) of render_rays on rb (first of reps+1 calls discarded) and the
+    launches' MFMA tally (one extra counted call)."""
+    n = rb.shape[0]
+    ts = []
+    for it in range(reps + 1):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        rc.render_rays(rb, S, skts=skts.expand(n, -1, -1, -1), cyls=cyl.expand(n, -1), N_importance=I, chunk=4096,
+                       ret_alpha=False)
+        e1.record()
+        torch.cuda.synchronize()
+        if it:
+            ts.append(e0.elapsed_time(e1))
+    rc.render_rays(rb, S, skts=skts.expand(n, -1, -1, -1), cyls=cyl.expand(n, -1), N_importance=I, chunk=4096,
+                   ret_alpha=False, count_mfma=True)
+    torch.cuda.synchronize()
+    return float(np.mean(ts)), tuple(int(v) for v in rc.last_mfma.tolist())
+
+
+def mix_peak(n_f32, n_bf16):
+    """Instruction-mix-weighted MFMA peak (TFLOP/s) and the executed FLOPs of a tally."""
+    flop = n_f32 * FLOP_F32_MFMA + n_bf16 * FLOP_BF16_MFMA
+    t = n_f32 * FLOP_F32_MFMA / (FP32_MFMA_PEAK_TFLOPS * 1e12) + n_bf16 * FLOP_BF16_MFMA / (BF16_MFMA_PEAK_TFLOPS * 1e12)
+    return flop / t / 1e12, flop
+
+
+def pipe_peak(precision):
+    """Peak of the MFMA pipe the precision mode's MLP runs on (the algorithmic roofline's peak)."""
+    return FP32_MFMA_PEAK_TFLOPS if precision == "fp32" else BF16_MFMA_PEAK_TFLOPS
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
+    shard = a.shard or ("pixels" if dist else "frames")
+    pixels = shard == "pixels"
+    if a.res is None:
+        a.res = 1024 if (pixels and dist) else 512
+    backend = None
     if dist:
         import torch.distributed as tdist
         torch.cuda.set_device(local)
         tdist.init_process_group("nccl")
+        backend = tdist.get_backend()
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
 
     anerf = importlib.import_module("a-nerf_amd")
     syn = importlib.import_module("a-nerf_amd.synthetic")
     _lib = importlib.import_module("a-nerf_amd._lib")
+    dmod = importlib.import_module("a-nerf_amd.distributed")
     lib = _lib.load()
 
     H = W = a.res
     S, I = a.samples, a.importance
     cfg = anerf.RenderConfig(n_joints=a.joints, N_samples=S, N_importance=I, precision=a.precision).validate()
-    ck = syn.make_checkpoint(13, n_joints=a.joints, D=8, W=256, fine=I > 0, tau=79.6)
-    pixels = a.shard == "pixels"
+    ck = syn.make_checkpoint(13, n_joints=a.joints, D=8, W=256, fine=I > 0, tau=a.tau)
     sc = syn.make_scene(n_joints=a.joints, H=H, W=W, seed=13 if pixels else 13 + rank)
     rc = anerf.RayCaster(cfg, ck, device=local)
     idxs, cyls, boxes = anerf.rays.valid_pixels(sc["c2ws"], H, W, sc["focal"], kps=sc["kps"], ext_scale=0.001)
@@ -121,37 +177,54 @@ def main():
     c2w = torch.from_numpy(np.ascontiguousarray(sc["c2ws"][0][:3, :4])).to(dev)
     skts = torch.from_numpy(sc["skts"][0:1]).to(dev)
     cyl = torch.from_numpy(cyls[0:1]).to(dev)
-    rb = torch.empty(n, 11, device=dev)
     img = torch.empty(H * W, 3, device=dev)
     dimg = torch.empty(H * W, device=dev)
     aimg = torch.empty(H * W, device=dev)
     st = _lib.stream_handle(dev)
     ev = []
-    dmod = importlib.import_module("a-nerf_amd.distributed")
+    sharded = pixels and dist
+    # this rank's rays: pixels mode at N > 1 = its whole-chunk range of the frame's ray list (generated
+    # from the resident pixel indices, nothing else); otherwise the whole box
+    s0, s1 = dmod.chunk_ranges(n, 4096, world)[rank] if sharded else (0, n)
+    n_mine = s1 - s0
+    rb = torch.empty(max(n_mine, 1), 11, device=dev)[:n_mine]
+    if sharded:
+        idx_all = torch.from_numpy(np.ascontiguousarray(idxs[0], np.int64)).to(dev)
+        idx_mine = idx_all[s0:s1].contiguous()
+        gather = dmod.ShardGather(n, 4096, world, dev)
+    last = {}
+
+    def render(r):
+        m = r.shape[0]
+        return rc.render_rays(r, S, skts=skts.expand(m, -1, -1, -1), cyls=cyl.expand(m, -1), N_importance=I,
+                              chunk=4096, ret_alpha=False)
 
     def step(record):
-        _lib.check(lib.anerf_gen_rays_box(_lib.ptr(c2w), H, W, sc["focal"], sc["focal"], 0.0, 0.0, 0, x0, y0, x1, y1,
-                                          0.0, 1.0, _lib.ptr(rb), st), "gen_rays_box")
+        if sharded:
+            if n_mine:
+                _lib.check(lib.anerf_gen_rays(_lib.ptr(c2w), H, W, sc["focal"], sc["focal"], 0.0, 0.0, 0,
+                                              _lib.ptr(idx_mine), n_mine, 0.0, 1.0, _lib.ptr(rb), st), "gen_rays")
+        else:
+            _lib.check(lib.anerf_gen_rays_box(_lib.ptr(c2w), H, W, sc["focal"], sc["focal"], 0.0, 0.0, 0, x0, y0, x1,
+                                              y1, 0.0, 1.0, _lib.ptr(rb), st), "gen_rays_box")
         if record:
             e0 = torch.cuda.Event(enable_timing=True)
             e0.record()
-        if pixels:  # this rank's whole-chunk range of the frame, then one all-gather (distributed.py)
-            out = dmod.render_rays_sharded(
-                lambda r: rc.render_rays(r, S, skts=skts.expand(r.shape[0], -1, -1, -1),
-                                         cyls=cyl.expand(r.shape[0], -1), N_importance=I, chunk=4096,
-                                         ret_alpha=False), rb, 4096) if dist else \
-                rc.render_rays(rb, S, skts=skts.expand(n, -1, -1, -1), cyls=cyl.expand(n, -1), N_importance=I,
-                               chunk=4096, ret_alpha=False)
-        else:
-            out = rc.render_rays(rb, S, skts=skts.expand(n, -1, -1, -1), cyls=cyl.expand(n, -1), N_importance=I,
-                                 chunk=4096, ret_alpha=False)
+        out = render(rb) if n_mine else None
         if record:
             e1 = torch.cuda.Event(enable_timing=True)
             e1.record()
             ev.append((e0, e1))
-        _lib.check(lib.anerf_compose_box(_lib.ptr(out["rgb_map"]), _lib.ptr(out["disp_map"]),
-                                         _lib.ptr(out["acc_map"]), x0, y0, x1, y1, None, 0, H, W, _lib.ptr(img),
-                                         _lib.ptr(dimg), _lib.ptr(aimg), st), "compose_box")
+        if sharded:  # one RCCL all-gather of (rgb, disp, acc), then every rank composes the frame
+            out = gather(out)
+            _lib.check(lib.anerf_compose(_lib.ptr(out["rgb_map"]), _lib.ptr(out["disp_map"]), _lib.ptr(out["acc_map"]),
+                                         _lib.ptr(idx_all), n, None, 0, H * W, _lib.ptr(img), _lib.ptr(dimg),
+                                         _lib.ptr(aimg), st), "compose")
+        else:
+            _lib.check(lib.anerf_compose_box(_lib.ptr(out["rgb_map"]), _lib.ptr(out["disp_map"]),
+                                             _lib.ptr(out["acc_map"]), x0, y0, x1, y1, None, 0, H, W, _lib.ptr(img),
+                                             _lib.ptr(dimg), _lib.ptr(aimg), st), "compose_box")
+        last["out"] = out
 
     for _ in range(a.warmup):
         step(False)
@@ -168,7 +241,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in ev]))
-    rays_job = n * a.steps / (world if pixels else 1)  # pixels: the ranks share one frame per step
+    rays_job = n * a.steps / (world if sharded else 1)  # pixels: the ranks share one frame per step
     if dist:
         t = torch.tensor([elapsed, float(rays_job)], device=dev, dtype=torch.float64)
         tmax = t[:1].clone()
@@ -176,99 +249,108 @@ def main():
         tdist.all_reduce(t[1:], op=tdist.ReduceOp.SUM)
         elapsed, rays_job = float(tmax.item()), float(t[1].item())
 
-    # executed MFMA work of one launch (exact device-side counter, one extra untimed launch) over the
-    # rays this rank renders per step (pixels mode: its whole-chunk share of the frame)
-    s0, s1 = dmod.chunk_ranges(n, 4096, world)[rank] if (pixels and dist) else (0, n)
-    n_mine = s1 - s0
-    rc.render_rays(rb[s0:s1], S, skts=skts.expand(n_mine, -1, -1, -1), cyls=cyl.expand(n_mine, -1), N_importance=I,
+    # the launches' MFMA work (kernel-side tally of one extra, untimed call over this rank's rays)
+    rc.render_rays(rb, S, skts=skts.expand(n_mine, -1, -1, -1), cyls=cyl.expand(n_mine, -1), N_importance=I,
                    chunk=4096, ret_alpha=False, count_mfma=True)
     torch.cuda.synchronize()
     n_f32, n_bf16 = (int(v) for v in rc.last_mfma.tolist())
-    flop_exec = n_f32 * FLOP_F32_MFMA + n_bf16 * FLOP_BF16_MFMA
-    # the launch's MFMA work at each pipe's peak rate: the time the MFMA pipes must be busy
-    t_mfma = n_f32 * FLOP_F32_MFMA / (FP32_MFMA_PEAK_TFLOPS * 1e12) + n_bf16 * FLOP_BF16_MFMA / (BF16_MFMA_PEAK_TFLOPS * 1e12)
-    peak_tf = flop_exec / t_mfma / 1e12  # = 157.3 for fp32; the instruction-mix-weighted peak otherwise
+    peak_exec, flop_exec = mix_peak(n_f32, n_bf16)
     flop_ray = anerf.flops_per_sample(cfg) * anerf.samples_per_ray(cfg)  # SURVEY §8(d), reference work
-    achieved_tf = flop_exec / (kern_ms * 1e-3) / 1e12
-    ref_equiv_tf = flop_ray * n_mine / (kern_ms * 1e-3) / 1e12
+    achieved_alg = flop_ray * n_mine / (kern_ms * 1e-3) / 1e12
+    achieved_exec = flop_exec / (kern_ms * 1e-3) / 1e12
+    peak = pipe_peak(a.precision)
     # the committed PMC summaries are of config 3's frame; other shapes report null
     traffic = traffic_from_profiles(a.precision) if _config_name(H, S, I, a.joints) == "config3" else None
 
-    # the other precision modes on the same frame (kernel time of render_rays, HIP events), N=1 only
-    others = {}
+    # N = 1 extras on the same frame: the other precision modes, and this mode at tau = 20 (the untrained
+    # value: wider cutoff windows, more live joints per block than tau = 79.6)
+    others, tau20 = {}, None
     if rank == 0 and world == 1:
         for p in [x for x in a.also.split(",") if x and x != a.precision]:
             rcp = anerf.RayCaster(anerf.RenderConfig(n_joints=a.joints, N_samples=S, N_importance=I,
                                                      precision=p).validate(), ck, device=local)
-            ts = []
-            for it in range(4):
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                rcp.render_rays(rb, S, skts=skts.expand(n, -1, -1, -1), cyls=cyl.expand(n, -1), N_importance=I,
-                                chunk=4096, ret_alpha=False)
-                e1.record()
-                torch.cuda.synchronize()
-                if it:
-                    ts.append(e0.elapsed_time(e1))
-            rcp.render_rays(rb, S, skts=skts.expand(n, -1, -1, -1), cyls=cyl.expand(n, -1), N_importance=I,
-                            chunk=4096, ret_alpha=False, count_mfma=True)
-            torch.cuda.synchronize()
-            pf, pb = (int(v) for v in rcp.last_mfma.tolist())
-            pms = float(np.mean(ts))
-            pflop = pf * FLOP_F32_MFMA + pb * FLOP_BF16_MFMA
-            ppeak = pflop / (pf * FLOP_F32_MFMA / (FP32_MFMA_PEAK_TFLOPS * 1e12) +
-                             pb * FLOP_BF16_MFMA / (BF16_MFMA_PEAK_TFLOPS * 1e12)) / 1e12
+            pms, (pf, pb) = kernel_time(rcp, rb, S, I, skts, cyl)
+            ppeak, pflop = mix_peak(pf, pb)
             others[p] = {"rays_per_s_kernel": round(n / (pms * 1e-3), 1), "kernel_ms": round(pms, 3),
-                         "roofline_frac": round(pflop / (pms * 1e-3) / 1e12 / ppeak, 4), "dtype": DTYPE[p]}
+                         "frac": round(flop_ray * n / (pms * 1e-3) / 1e12 / pipe_peak(p), 4),
+                         "frac_executed": round(pflop / (pms * 1e-3) / 1e12 / ppeak, 4), "dtype": DTYPE[p]}
             del rcp
+        if a.tau != 20.0 and not a.no_tau20:
+            ck20 = syn.make_checkpoint(13, n_joints=a.joints, D=8, W=256, fine=I > 0, tau=20.0)
+            rc20 = anerf.RayCaster(cfg, ck20, device=local)
+            tms, (tf, tb) = kernel_time(rc20, rb, S, I, skts, cyl)
+            tpeak, tflop = mix_peak(tf, tb)
+            tau20 = {"tau": 20.0, "rays_per_s_kernel": round(n / (tms * 1e-3), 1), "kernel_ms": round(tms, 3),
+                     "frac": round(flop_ray * n / (tms * 1e-3) / 1e12 / peak, 4),
+                     "frac_executed": round(tflop / (tms * 1e-3) / 1e12 / tpeak, 4)}
+            del rc20
 
-    cpu = None
+    cpu, parity = None, None
     if rank == 0 and world == 1 and not a.no_cpu:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import oracle
         cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
         om = oracle.OracleModel(cfg, ck)
         rb_h = rb.cpu().numpy()
+        near_f, far_f, _, _ = om.near_far(rb_h, cyls[0:1], chunk=4096)  # the whole frame's chunk NaN fill
         sel = np.linspace(0, n - 1, min(a.cpu_rays, n)).astype(np.int64)
         t1 = time.perf_counter()
-        om.render_rays(rb_h[sel], sc["skts"][0], cyls[0:1], chunk=4096, nthreads=cores)
+        ref = om.render_rays(rb_h[sel], sc["skts"][0], cyls[0:1], chunk=4096, nthreads=cores, near=near_f[sel],
+                             far=far_f[sel])
         dt = time.perf_counter() - t1
         cpu = {"value": round(len(sel) / dt, 2), "unit": "rays/s", "cores": cores, "kind": "port",
+               "cpu_model": cpu_model(),
                "sample": f"{len(sel)} rays evenly spaced over the frame's {n} bbox rays, C oracle "
                          f"(oracle/anerf_oracle.c, OpenMP {cores} threads), {dt:.1f} s wall"}
+        out = last["out"]
+        sel_d = torch.from_numpy(sel).to(dev)
+        errs = {k: float(np.abs(out[k].index_select(0, sel_d).cpu().numpy().astype(np.float64) -
+                                ref[k].astype(np.float64)).max()) for k in ("rgb_map", "disp_map", "acc_map")}
+        parity = {"rays": int(len(sel)), "max_abs_err": {k: float(f"{v:.3e}") for k, v in errs.items()},
+                  "tol": 1e-4, "ok": bool(max(errs.values()) <= 1e-4),
+                  "against": "C oracle (pinned to the reference's golden fixtures) on the same rays, near/far "
+                             "from the whole frame's 4096-ray chunks"}
 
     if rank == 0:
         value = rays_job / elapsed
+        workload = (f"{_config_name(H, S, I, a.joints)}: {H}x{W} frame, {S}+{I} samples, {a.joints}-joint, 8x256 MLP, "
+                    + (f"one frame per step split over {world} GPU(s) in whole 4096-ray chunks + RCCL all-gather"
+                       if sharded else "one frame per GPU per step"))
         line = {
             "metric": BASELINE["metric"], "value": round(value, 1), "unit": "rays/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(1e3 * elapsed / a.steps, 3),
-            "higher_is_better": True, "scaling": "strong" if pixels else "weak", "vs_baseline": None,
+            "higher_is_better": True, "scaling": "strong" if sharded else "weak", "vs_baseline": None,
             "dtype": DTYPE[a.precision],
             "data": "synthetic (seeded SMPL-24 pose + seeded 8x256 weights; no dataset/checkpoint offline)",
-            "config": {"workload": f"{_config_name(H, S, I, a.joints)}: {H}x{W} frame, {S}+{I} samples, {a.joints}-joint, 8x256 MLP, " +
-                                   (f"one frame per step split over {world} GPU(s) in whole 4096-ray chunks + RCCL "
-                                    f"all-gather" if pixels else "one frame per GPU per step"),
-                       "rays_per_frame": n,
-                       "parallelism": f"{'pixel-shard' if pixels else 'frame-per-rank'} x{world}"},
-            "roofline": {"bound": "mfma", "achieved": round(achieved_tf, 2), "peak": round(peak_tf, 1),
-                         "unit": "TFLOP/s", "frac": round(achieved_tf / peak_tf, 4),
+            "config": {"workload": workload, "rays_per_frame": n, "tau": a.tau,
+                       "parallelism": f"{'pixel-shard' if sharded else 'frame-per-rank'} x{world}",
+                       "n_ranks": world, "backend": backend},
+            "roofline": {"bound": "mfma", "achieved": round(achieved_alg, 2), "peak": round(peak, 1),
+                         "unit": "TFLOP/s", "frac": round(achieved_alg / peak, 4),
                          "traffic": traffic, "kernel_ms": round(kern_ms, 3),
                          "launches_per_step": 2 if I > 0 else 1,
+                         "flop": "algorithmic: the reference's MLP FLOPs (SURVEY §8(d), reference_flop_per_ray x "
+                                 "this rank's rays per step) / kernel_ms; peak = the MFMA pipe of this precision "
+                                 "mode (BF16 dense 2516.6 TF for the split-bf16 modes, FP32 matrix 157.3 TF for fp32); "
+                                 "traffic = PMC HBM bytes per step (both launches)",
                          "timing": "HIP events on the launch stream around anerf_render_rays: the coarse and the "
                                    "fine render_kernel launch (+ near/far, 0.2 %); rocprofv3's render_kernel "
                                    "average x launches_per_step agrees (profiles/)",
-                         "flop": "executed MFMA FLOPs of one step's launches (device counters) / their time "
-                                 "(kernel_ms), the same ratio as per launch; peak = the FP32 (157.3) and BF16 "
-                                 "(2516.6 TF) MFMA peaks weighted by the step's instruction mix; traffic per step",
+                         "achieved_executed": round(achieved_exec, 2), "peak_executed_mix": round(peak_exec, 1),
+                         "frac_executed": round(achieved_exec / peak_exec, 4),
+                         "mfma_tally": "kernel-side tally of issued MFMA instructions (agrees with PMC SQ_INSTS_MFMA)",
                          "mfma_f32_per_step": n_f32, "mfma_bf16_per_step": n_bf16,
-                         "reference_flop_per_ray": flop_ray,
-                         "reference_equivalent_tflops": round(ref_equiv_tf, 2)},
+                         "reference_flop_per_ray": flop_ray},
+            "parity": parity,
+            "tau20": tau20,
             "cpu_baseline": cpu,
             "other_precisions": others or None,
         }
         print(json.dumps(line), flush=True)
     if dist:
         tdist.destroy_process_group()
+    if parity is not None and not parity["ok"]:
+        sys.exit(f"parity check failed: {parity['max_abs_err']} > 1e-4")
 
 
 if __name__ == "__main__":

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define ANERF_ABI_VERSION 4
+#define ANERF_ABI_VERSION 5
 
 enum {
     ANERF_OK = 0,
@@ -80,7 +80,7 @@ typedef struct {
     int32_t net_width;       /* netwidth W: 64, 128 or 256 */
     int32_t skip;            /* skips=[skip]; layer skip+1 consumes [x, h]; >= D-1 means none */
     int32_t multires;        /* kp positional-encoding frequencies (7) */
-    int32_t multires_views;  /* view-direction frequencies (4) */
+    int32_t multires_views;  /* view-direction frequencies: 4 (default) or 0 (surreal_single.txt) */
     int32_t use_cutoff;      /* --use_cutoff */
     int32_t cutoff_inputs;   /* --cutoff_inputs */
     int32_t cutoff_viewdir;  /* --cutoff_viewdir */
@@ -90,6 +90,10 @@ typedef struct {
     float softplus_shift;
     float density_scale;     /* B in raw2outputs */
     int32_t has_fine;        /* a separate network_fine exists (N_importance > 0, !single_net) */
+    int32_t single_net;      /* --single_net: network_fine IS network_fn (raycasters.py:101-104); the fine
+                                pass evaluates only the I new samples and merges raws (:462-468), the
+                                importance weights are 0.5 (max(w_l,w_k) + max(w_k,w_u)) + 0.01
+                                (ray_utils.py:270-277); requires has_fine == 0 */
 } anerf_model_desc;
 
 /* HOST pointers to one NeRF's weights, torch nn.Linear layout [out][in] (core/networks/nerf.py:57-88). */
@@ -124,7 +128,9 @@ typedef struct {
     float* weights0;  /* [N][S] */
     float* z_fine;    /* [N][S+I] sorted merged samples */
     float* raw_fine;  /* [N][S+I][4] */
-    unsigned long long* mfma_count; /* [1] += v_mfma_f32_32x32x2_f32 instructions issued (work counter) */
+    unsigned long long* mfma_count; /* [2] += MFMA instructions issued, a kernel-side tally of the
+                                       work (agrees with PMC SQ_INSTS_MFMA): [0] v_mfma_f32_32x32x2_f32,
+                                       [1] v_mfma_f32_32x32x16_bf16 (bf16x3 / bf16x6 modes) */
 } anerf_debug;
 
 int anerf_abi_version(void);
@@ -135,6 +141,12 @@ int anerf_model_create(const anerf_model_desc* desc, const anerf_net_weights* co
                        const anerf_net_weights* fine, const anerf_embed_params* embed, int device,
                        anerf_model** out);
 int anerf_model_destroy(anerf_model* m);
+/* Replace the embedders' state of a model without repacking its weights: tau / tau_v always,
+ * cutoff_dist / cutoff_dist_v when not NULL (then synchronously, after the device has drained).
+ * Launches issued afterwards use the new values: the tau schedule of training
+ * (RayCaster.update_embed_fns -> CutoffEmbedder.update_tau, core/raycasters.py:731-748,
+ * core/cutoff_embedder.py:176-183).  Not thread-safe against concurrent launches on the model. */
+int anerf_model_set_embed(anerf_model* m, const anerf_embed_params* embed);
 /* bytes of packed device weights held by the model */
 size_t anerf_model_bytes(const anerf_model* m);
 
@@ -184,8 +196,9 @@ int anerf_compose_box(const float* rgb, const float* disp, const float* acc, int
                       int32_t y1, const float* bg, int32_t white_bkgd, int32_t H, int32_t W, float* out_rgb,
                       float* out_disp, float* out_acc, void* stream);
 
-/* Stage: near/far of get_near_far_in_cylinder with the per-chunk NaN fill. */
-int anerf_near_far(const float* ray_batch, int32_t ray_stride, int64_t n_rays, const float* cyls,
+/* Stage: near/far of get_near_far_in_cylinder with the per-chunk NaN fill; cyls [n_poses][5], ray_pose
+ * [n_rays] or NULL (pose 0); a ray whose pose index is outside [0, n_poses) is treated as a miss. */
+int anerf_near_far(const float* ray_batch, int32_t ray_stride, int64_t n_rays, const float* cyls, int32_t n_poses,
                    const int32_t* ray_pose, int32_t chunk, float* near_out, float* far_out, void* workspace,
                    size_t workspace_bytes, void* stream);
 
@@ -275,7 +288,9 @@ int anerf_train_samples(const float* near_in, const float* far_in, int64_t n_ray
 
 /* Features feat_out [N][S][F] (the layout of anerf_encode_points) of the points o + d z of the rays
  * ray_batch [N][ray_stride] (o = cols 0-2, d = cols 3-5) at z [N][S]; the rays' skeletons are
- * skts [n_poses][NJ][4][4] with ray_pose [N] (NULL: one skeleton per ray, n_poses == N). */
+ * skts [n_poses][NJ][4][4] with ray_pose [N] (NULL: one skeleton per ray, n_poses == N).  A ray
+ * whose ray_pose is outside [0, n_poses) gets NaN features (and no gradient in the backward); the
+ * index is never dereferenced. */
 int anerf_train_encode(const anerf_model* m, const float* ray_batch, int32_t ray_stride, int64_t n_rays,
                        const float* z, int32_t n_samples, const float* skts, int32_t n_poses, const int32_t* ray_pose,
                        float* feat_out, void* stream);
@@ -302,9 +317,12 @@ int anerf_train_composite_backward(const anerf_model* m, const float* raw, const
                                    const float* g_alpha, float* g_raw, void* stream);
 
 /* z_all [N][S+I] (sorted) of isample_from_lineseg: sample_pdf over the mid-points with the coarse
- * weights [N][S] at u [N][I] (NULL: det=True, torch.linspace), merged with z [N][S]. */
+ * weights [N][S] at u [N][I] (NULL: det=True, torch.linspace), merged with z [N][S].  single_net != 0
+ * uses is_only's weights 0.5 (max(w_l, w_k) + max(w_k, w_u)) + 0.01 (ray_utils.py:270-277).
+ * sorted_idx [N][S+I] (optional): torch.sort's indices into cat([z, z_samples]) (ties: values equal). */
 int anerf_train_importance(const float* z, const float* weights, int64_t n_rays, int32_t n_samples,
-                           int32_t n_importance, const float* u, float* z_all, void* stream);
+                           int32_t n_importance, const float* u, int32_t single_net, float* z_all,
+                           int32_t* sorted_idx, void* stream);
 
 #ifdef __cplusplus
 }

@@ -51,6 +51,7 @@ typedef struct {
     const float* cutoff;   /* embed_fn.cutoff_dist (NJ)     */
     const float* cutoff_v; /* embeddirs_fn.cutoff_dist (NJ) */
     int has_fine;
+    int single_net; /* network_fine IS network_fn; fine pass on the I new samples only (raycasters.py:462-468) */
     oracle_net coarse, fine;
 } oracle_model;
 
@@ -529,11 +530,10 @@ static void ray_code(const oracle_model* m, const oracle_net* net, const float* 
     }
 }
 
-/* One pass (encode + MLP + composite) over n samples z of ray i */
-static void ray_pass(const oracle_model* m, const oracle_net* net, const float* o, const float* d,
-                     const float* skts, const float* code, const float* z, int n, float* feat, float* raw,
-                     float* codes_rows, float* buf, float* rgb, float* disp, float* acc, float* weights,
-                     float* alpha) {
+/* encode + MLP over n samples z of one ray: raw [n][4] */
+static void ray_raw(const oracle_model* m, const oracle_net* net, const float* o, const float* d,
+                    const float* skts, const float* code, const float* z, int n, float* feat, float* raw,
+                    float* codes_rows, float* buf) {
     int F = oracle_feature_dim(m);
     int cfc = m->framecode_ch;
     for (int s = 0; s < n; ++s) {
@@ -548,18 +548,45 @@ static void ray_pass(const oracle_model* m, const oracle_net* net, const float* 
         network_forward(m, net, feat + (size_t)s0 * F, nb, cfc ? codes_rows + (size_t)s0 * cfc : NULL,
                         raw + 4 * s0, buf);
     }
+}
+
+/* One pass (encode + MLP + composite) over n samples z of ray i */
+static void ray_pass(const oracle_model* m, const oracle_net* net, const float* o, const float* d,
+                     const float* skts, const float* code, const float* z, int n, float* feat, float* raw,
+                     float* codes_rows, float* buf, float* rgb, float* disp, float* acc, float* weights,
+                     float* alpha) {
+    ray_raw(m, net, o, d, skts, code, z, n, feat, raw, codes_rows, buf);
     raw2outputs(m, raw, z, n, d, rgb, disp, acc, weights, alpha, buf);
 }
 
+/* torch.maximum: NaN if either operand is NaN */
+static float torch_maximum_(float a, float b) { return (isnan(a) || a > b) ? a : b; }
+
+/* argsort of z[0..n) by value (NaN last), ties by index: torch.sort's values (hazard H9) */
+static _Thread_local const float* g_sort_keys;  /* per OpenMP thread */
+static int cmp_idx(const void* a, const void* b) {
+    int i = *(const int*)a, j = *(const int*)b;
+    int c = cmp_float(g_sort_keys + i, g_sort_keys + j);
+    return c ? c : (i > j) - (i < j);
+}
+
+/* near_in / far_in (optional, both or neither): the rays' near / far after the chunk NaN fill,
+ * e.g. of the whole frame when rb is a sample of its rays (the fill couples a chunk's rays). */
 int oracle_render_rays(const oracle_model* m, const float* rb, int stride, int64_t n, const float* skts,
                        const float* cyls, const int32_t* ray_pose, const float* cams, int S, int I, int chunk,
                        int nthreads, float* rgb, float* disp, float* acc, float* rgb0, float* disp0,
-                       float* acc0, float* alpha, float* alpha0, float* z_out) {
+                       float* acc0, float* alpha, float* alpha0, float* z_out, const float* near_in,
+                       const float* far_in) {
     if (n <= 0) return 0;
-    if (I > 0 && !m->has_fine) return -1;
+    if (I > 0 && !m->has_fine && !m->single_net) return -1;
     float* near = (float*)malloc(sizeof(float) * n);
     float* far = (float*)malloc(sizeof(float) * n);
-    oracle_near_far(rb, stride, n, cyls, ray_pose, chunk, near, far, NULL);
+    if (near_in && far_in) {
+        memcpy(near, near_in, sizeof(float) * n);
+        memcpy(far, far_in, sizeof(float) * n);
+    } else {
+        oracle_near_far(rb, stride, n, cyls, ray_pose, chunk, near, far, NULL);
+    }
     const int T = S + I;
     const int F = oracle_feature_dim(m);
     const int cfc = m->framecode_ch;
@@ -583,6 +610,9 @@ int oracle_render_rays(const oracle_model* m, const float* rb, int stride, int64
         float* al = (float*)malloc(sizeof(float) * T);
         float* mids = (float*)malloc(sizeof(float) * S);
         float* cdf = (float*)malloc(sizeof(float) * 2 * S);
+        float* zm = (float*)malloc(sizeof(float) * T);
+        float* rawm = (float*)malloc(sizeof(float) * 4 * T);
+        int* order = (int*)malloc(sizeof(int) * T);
         float code[64];
 #pragma omp for schedule(dynamic, 4)
         for (int64_t i = 0; i < n; ++i) {
@@ -610,6 +640,31 @@ int oracle_render_rays(const oracle_model* m, const float* rb, int stride, int64
             if (alpha0) memcpy(alpha0 + (size_t)i * S, al, sizeof(float) * S);
             /* isample_from_lineseg (ray_utils.py:255-289) */
             for (int s = 0; s + 1 < S; ++s) mids[s] = 0.5f * (z[s + 1] + z[s]);
+            if (m->single_net) {
+                /* is_only weights (ray_utils.py:270-277), written over w[0..S-2) (read left to right) */
+                for (int k = 0; k + 2 < S; ++k)
+                    w[k] = 0.5f * (torch_maximum_(w[k], w[k + 1]) + torch_maximum_(w[k + 1], w[k + 2])) + 0.01f;
+                sample_pdf(mids, w, S - 1, I, uv, z + S, cdf);
+                /* the same net on the I new samples only, raws after the coarse ones (cat order),
+                 * then both merged by sorted_idx (raycasters.py:462-468) */
+                ray_raw(m, &m->coarse, o, d, sk, code, z + S, I, feat, raw + 4 * S, codes_rows, buf);
+                for (int k = 0; k < T; ++k) order[k] = k;
+                g_sort_keys = z;
+                qsort(order, (size_t)T, sizeof(int), cmp_idx);
+                for (int k = 0; k < T; ++k) {
+                    zm[k] = z[order[k]];
+                    memcpy(rawm + 4 * k, raw + 4 * order[k], 4 * sizeof(float));
+                }
+                memcpy(z, zm, sizeof(float) * T);
+                float f_rgb[3], f_disp, f_acc;
+                raw2outputs(m, rawm, z, T, d, f_rgb, &f_disp, &f_acc, w, al, buf);
+                for (int c = 0; c < 3; ++c) rgb[3 * i + c] = f_rgb[c];
+                disp[i] = f_disp;
+                acc[i] = f_acc;
+                if (alpha) memcpy(alpha + (size_t)i * T, al, sizeof(float) * T);
+                if (z_out) memcpy(z_out + (size_t)i * T, z, sizeof(float) * T);
+                continue;
+            }
             sample_pdf(mids, w + 1, S - 1, I, uv, z + S, cdf);
             qsort(z, (size_t)T, sizeof(float), cmp_float);
             ray_code(m, &m->fine, cams, i, code);
@@ -622,6 +677,7 @@ int oracle_render_rays(const oracle_model* m, const float* rb, int stride, int64
             if (z_out) memcpy(z_out + (size_t)i * T, z, sizeof(float) * T);
         }
         free(feat); free(raw); free(buf); free(codes_rows); free(z); free(w); free(al); free(mids); free(cdf);
+        free(zm); free(rawm); free(order);
     }
     free(near); free(far); free(tv); free(uv);
     return 0;

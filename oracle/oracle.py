@@ -28,7 +28,8 @@ class _Model(ctypes.Structure):
                 ("framecode_ch", ctypes.c_int), ("n_framecodes", ctypes.c_int),
                 ("density_softplus", ctypes.c_int), ("softplus_shift", ctypes.c_float),
                 ("density_scale", ctypes.c_float), ("tau", ctypes.c_float), ("tau_v", ctypes.c_float),
-                ("cutoff", _f), ("cutoff_v", _f), ("has_fine", ctypes.c_int), ("coarse", _Net), ("fine", _Net)]
+                ("cutoff", _f), ("cutoff_v", _f), ("has_fine", ctypes.c_int), ("single_net", ctypes.c_int),
+                ("coarse", _Net), ("fine", _Net)]
 
 
 def build():
@@ -78,8 +79,12 @@ class OracleModel:
         e, ev = ckpt["embed_state_dict"], ckpt["embeddirs_state_dict"]
         m.tau, m.tau_v = float(np.asarray(e["tau"])), float(np.asarray(ev["tau"]))
         m.cutoff, m.cutoff_v = self._k(e["cutoff_dist"]), self._k(ev["cutoff_dist"])
-        self._net(m.coarse, ckpt["network_fn_state_dict"])
         fine = ckpt.get("network_fine_state_dict")
+        coarse = ckpt["network_fn_state_dict"]
+        if cfg.single_net:  # network_fine IS network_fn; load_state_dict loads the fine keys last
+            coarse, fine = (fine if fine is not None else coarse), None
+        m.single_net = int(cfg.single_net)
+        self._net(m.coarse, coarse)
         m.has_fine = int(fine is not None)
         if fine is not None:
             self._net(m.fine, fine)
@@ -164,8 +169,10 @@ class OracleModel:
         return out
 
     def render_rays(self, ray_batch, skts, cyls, ray_pose=None, cams=None, N_samples=None, N_importance=None,
-                    chunk=4096, nthreads=0, with_z=False):
-        """render_rays over a whole ray list (chunked NaN fill), returns the reference's output dict."""
+                    chunk=4096, nthreads=0, with_z=False, near=None, far=None):
+        """render_rays over a whole ray list (chunked NaN fill), returns the reference's output dict.
+        near / far: the rays' filled near / far (e.g. from near_far() of the whole frame when ray_batch
+        is a sample of its rays), instead of the fill over this list's chunks."""
         cfg = self.cfg
         S = cfg.N_samples if N_samples is None else N_samples
         I = cfg.N_importance if N_importance is None else N_importance
@@ -186,7 +193,8 @@ class OracleModel:
         rc = lib().oracle_render_rays(self.ref, _p(rb), stride, ctypes.c_int64(n), _p(_f32(skts)), _p(_f32(cyls)),
                                       rp.ctypes.data_as(_i32) if rp is not None else None, _p(cm), S, I, chunk,
                                       nthreads, _p(rgb), _p(disp), _p(acc), _p(extra[0]), _p(extra[1]),
-                                      _p(extra[2]), _p(alpha), _p(extra[3]), _p(z))
+                                      _p(extra[2]), _p(alpha), _p(extra[3]), _p(z),
+                                      _p(None if near is None else _f32(near)), _p(None if far is None else _f32(far)))
         if rc != 0:
             raise RuntimeError(f"oracle_render_rays failed ({rc})")
         if with_z:

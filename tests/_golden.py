@@ -16,7 +16,9 @@ NAMES = ["c1_64_s32_d4w128", "c2_256_s64_d8w256", "c3_512_s64i128_d8w256", "c4_5
          "h1_nanfill_s32i16_d4w128", "fc_64_s32i32_d4w128",
          # flag variants: multires 10 + width 64; softplus density without view cutoff; unwindowed
          # distance input; no cutoff window at all
-         "v1_mr10_w64_d4", "v2_softplus_nocutview", "v3_nocutinputs", "v4_nocutoff"]
+         "v1_mr10_w64_d4", "v2_softplus_nocutview", "v3_nocutinputs", "v4_nocutoff",
+         # configs/surreal/surreal_single.txt (single_net, multires_views 0, 96 + 48); tau at its ceiling
+         "s1_single_s96i48_mrv0", "t2000_512_s64i128"]
 
 
 class Golden:
@@ -38,9 +40,12 @@ class Golden:
                                        chunk=m["chunk"], ext_scale=m["ext_scale"], multires=m.get("mr", 7),
                                        use_cutoff="--use_cutoff" not in drop,
                                        cutoff_inputs="--cutoff_inputs" not in drop,
-                                       cutoff_viewdir="--cutoff_viewdir" not in drop, **kw).validate()
+                                       cutoff_viewdir="--cutoff_viewdir" not in drop,
+                                       multires_views=m.get("mrv", 4), single_net=m.get("single", False),
+                                       **kw).validate()
         self.ckpt = syn.make_checkpoint(m["seed"], n_joints=m["NJ"], D=m["D"], W=m["W"], fine=m["I"] > 0,
-                                        tau=m["tau"], use_framecode=fc, n_framecodes=5, multires=m.get("mr", 7))
+                                        tau=m["tau"], use_framecode=fc, n_framecodes=5, multires=m.get("mr", 7),
+                                        multires_views=m.get("mrv", 4))
         assert syn.checkpoint_sha256(self.ckpt) == m["sha256"], "synthetic weights drifted from the fixture"
 
     def __getitem__(self, k):

@@ -106,6 +106,13 @@ CONFIGS = {
                            drop=["--cutoff_inputs"]),
     "v4_nocutoff": dict(H=128, NJ=24, S=32, I=16, D=4, W=128, tau=20.0, kind="rays", n_rays=128, seed=24,
                         drop=["--use_cutoff", "--cutoff_inputs", "--cutoff_viewdir"]),
+    # configs/surreal/surreal_single.txt: single_net (one network, fine pass on the I new samples only,
+    # max-filtered importance weights), multires_views 0, 96 + 48 samples; the checkpoint carries two
+    # different network state dicts (load_state_dict loads network_fine's last into the shared module)
+    "s1_single_s96i48_mrv0": dict(H=256, NJ=24, S=96, I=48, D=8, W=256, tau=20.0, kind="rays", n_rays=192, seed=31,
+                                  mrv=0, single=True),
+    # the tau schedule's ceiling (CutoffEmbedder.update_tau clamps at 2000): the sharpest window
+    "t2000_512_s64i128": dict(H=512, NJ=24, S=64, I=128, D=8, W=256, tau=2000.0, kind="rays", n_rays=256, seed=32),
 }
 
 
@@ -116,13 +123,15 @@ def build_reference(mods, cfg, tmp):
     use_fc = cfg["kind"] == "framecode"
     argv = ["--N_samples", str(cfg["S"]), "--N_importance", str(cfg["I"]),
             "--netdepth", str(cfg["D"]), "--netwidth", str(cfg["W"]),
-            "--multires", str(cfg.get("mr", 7)), "--multires_views", "4",
+            "--multires", str(cfg.get("mr", 7)), "--multires_views", str(cfg.get("mrv", 4)),
             "--use_cutoff", "--cutoff_viewdir", "--cutoff_inputs", "--use_viewdirs",
             "--ext_scale", "0.001", "--chunk", "4096", "--no_reload",
             "--basedir", tmp, "--expname", "x"]
     argv = [a for a in argv if a not in cfg.get("drop", [])] + cfg.get("flags", [])
     if use_fc:
         argv += ["--opt_framecode", "--n_framecodes", "5"]
+    if cfg.get("single"):
+        argv += ["--single_net"]
     args = run_nerf.config_parser().parse_args(argv)
     os.makedirs(os.path.join(tmp, "x"), exist_ok=True)
     parents, rest = anerf_syn.skeleton(NJ)
@@ -135,7 +144,8 @@ def build_reference(mods, cfg, tmp):
                   "joint_coords": np.zeros((NJ, 3, 3), np.float32)}
     _, render_kwargs, _, _, _, _ = raycasters.create_raycaster(args, data_attrs)
     ck = anerf_syn.make_checkpoint(cfg["seed"], n_joints=NJ, D=cfg["D"], W=cfg["W"], fine=cfg["I"] > 0,
-                                   tau=cfg["tau"], use_framecode=use_fc, n_framecodes=5, multires=cfg.get("mr", 7))
+                                   tau=cfg["tau"], use_framecode=use_fc, n_framecodes=5, multires=cfg.get("mr", 7),
+                                   multires_views=cfg.get("mrv", 4))
     ck_t = {k: {n: torch.from_numpy(np.array(v)) for n, v in d.items()} for k, d in ck.items()}
     rc = render_kwargs["ray_caster"]
     rc.load_state_dict(ck_t, strict=True)
@@ -203,11 +213,16 @@ def stage_dump(mods, render_kwargs, o, d, sc, n_stage, cams=None):
         out.update(near=near.numpy(), far=far.numpy(), z=z.numpy(), feat=feat[:, :4].numpy(),
                    raw=raw.numpy(), weights=ret["weights"].numpy())
         if I > 0:
-            pts_is, z_all, z_is, sidx = rc.sample_pts_is(o, d, z, ret["weights"], I, det=True, is_only=False)
+            single = bool(rc.single_net)
+            pts_is, z_all, z_is, sidx = rc.sample_pts_is(o, d, z, ret["weights"], I, det=True, is_only=single)
             enc_is = rc.encode_inputs(pts_is, [o[:, None, :], d[:, None, :]], kp, skts, bones, cam_idxs=cam_t,
                                       subject_idxs=None, joint_coords=jc, network=rc.network_fine, **pk)
-            merged = rc._merge_encodings(enc, enc_is, sidx, n, S + I)
-            raw_f = rc.run_network(merged, rc.network_fine)
+            if single:  # raycasters.py:462-468
+                raw_is = rc.run_network(enc_is, rc.network_fine)
+                raw_f = rc._merge_encodings({"raw": raw}, {"raw": raw_is}, sidx, n, S + I)["raw"]
+            else:
+                merged = rc._merge_encodings(enc, enc_is, sidx, n, S + I)
+                raw_f = rc.run_network(merged, rc.network_fine)
             out.update(z_is=z_is.numpy(), z_all=z_all.numpy(), raw_f=raw_f.numpy())
     return {"stage_" + k: v for k, v in out.items()}
 
@@ -251,7 +266,7 @@ def make(name, cfg, mods, tmp):
     meta = dict(seed=cfg["seed"], sha256=sha, NJ=cfg["NJ"], S=cfg["S"], I=cfg["I"], D=cfg["D"], W=cfg["W"],
                 tau=cfg["tau"], H=sc["H"], focal=sc["focal"], ext_scale=0.001, chunk=4096,
                 framecode=int(cfg["kind"] == "framecode"), mr=cfg.get("mr", 7), flags=cfg.get("flags", []),
-                drop=cfg.get("drop", []))
+                drop=cfg.get("drop", []), mrv=cfg.get("mrv", 4), single=bool(cfg.get("single", False)))
     data = {"c2ws": sc["c2ws"], "kps": sc["kps"], "skts": sc["skts"], "bones": sc["bones"]}
     (o, d), vidx, cyls, (tl, br) = rays_for(mods, sc)
     sc["cyls"] = cyls

@@ -29,6 +29,13 @@ CONFIGS = {
                              n_poses=2),
     "t3_softplus_fc": dict(H=128, NJ=24, S=32, I=16, D=4, W=128, tau=20.0, kind="framecode", seed=33, n_rays=64,
                            n_poses=2, flags=["--density_type", "softplus", "--softplus_shift", "1.0"]),
+    # the tau schedule: RayCaster.update_embed_fns at global step 250,000 (cutoff_step 250, rate 10:
+    # tau = 20 * 10 ** 1 = 200) before the step, from a checkpoint at tau 20
+    "t4_tau200": dict(H=128, NJ=24, S=32, I=16, D=4, W=128, tau=20.0, kind="rays", seed=34, n_rays=64, n_poses=2,
+                      global_step=250000, cutoff_step=250, cutoff_rate=10.0),
+    # single_net + multires_views 0 (configs/surreal/surreal_single.txt's flags, smaller net)
+    "t5_single_mrv0": dict(H=128, NJ=24, S=48, I=24, D=4, W=128, tau=20.0, kind="rays", seed=35, n_rays=64,
+                           n_poses=2, mrv=0, single=True),
 }
 FULL_LIMIT = 20000   # parameters with more entries are sampled
 SAMPLE = 4096
@@ -94,6 +101,10 @@ def make(name, cfg, mods, tmp):
     kp_t = torch.from_numpy(sc["kps"][pose])
     bones_t = torch.from_numpy(sc["bones"][pose])
     rc.train()
+    if "global_step" in cfg:
+        args.cutoff_step, args.cutoff_rate = cfg["cutoff_step"], cfg["cutoff_rate"]
+        rc.update_embed_fns(cfg["global_step"], args)
+    taus = (float(rc.embed_fn.get_tau()), float(rc.embeddirs_fn.get_tau()))
     torch.rand, torch.randn = fake("rand"), fake("randn")
     try:
         ret = rc(torch.from_numpy(rb), S, kp_batch=kp_t, skts=skts_t, cyls=torch.from_numpy(cyl), bones=bones_t,
@@ -110,7 +121,9 @@ def make(name, cfg, mods, tmp):
     meta = dict(seed=cfg["seed"], sha256=mg.anerf_syn.checkpoint_sha256(ck), NJ=NJ, S=S, I=I, D=cfg["D"],
                 W=cfg["W"], tau=cfg["tau"], H=sc["H"], focal=sc["focal"], ext_scale=0.001, chunk=4096,
                 framecode=int(cfg["kind"] == "framecode"), mr=7, flags=cfg.get("flags", []), drop=[],
-                raw_noise_std=1.0, n_poses=P)
+                raw_noise_std=1.0, n_poses=P, mrv=cfg.get("mrv", 4), single=bool(cfg.get("single", False)),
+                global_step=cfg.get("global_step"), cutoff_step=cfg.get("cutoff_step"),
+                cutoff_rate=cfg.get("cutoff_rate"), tau_step=taus)
     data = dict(rays=rb, pose=pose, skts=sc["skts"][pose], kps=sc["kps"][pose], bones=sc["bones"][pose], cyls=cyl,
                 target=target, bg=bg, loss=np.float32(loss.item()), grad_skts=skts_t.grad.numpy(),
                 **{"rand_" + k: v for k, v in draws.items()},

@@ -47,6 +47,11 @@ def _worker(rank, world, port, q):
             return {k: torch.from_numpy(v) for k, v in o.items()}
 
         out = D.render_rays_sharded(render_fn, rb, chunk=4096)
+        # the static-size gather bench.py uses (one all_gather_into_tensor, padding dropped)
+        s0, s1 = D.chunk_ranges(rb.shape[0], 4096, world)[rank]
+        sg = D.ShardGather(rb.shape[0], 4096, world, torch.device("cpu"))(render_fn(rb[s0:s1]))
+        for k in out:
+            assert torch.equal(sg[k], out[k]), k
         frames = torch.arange(5 * 4 * 4 * 3, dtype=torch.float32).reshape(5, 4, 4, 3)
         mine = frames[D.frame_ids(5, rank, world)]
         full = D.gather_frames(mine, 5)

@@ -1,0 +1,97 @@
+"""Full-size frames on the GPU against the CPU oracle.
+
+* Configs 3 and 4 (512^2, 64 + 128 samples, 24 / 65 joints, 8x256): a whole frame rendered in
+  4096-ray chunks; >= 8,192 evenly spaced rays of it compared with the oracle at 1e-4 (the oracle
+  gets the frame's own near / far, i.e. the chunk NaN fill of the whole frame, hazard H1).
+* Config 5 (1024^2): the north star's multi-GPU split — the ray list cut into
+  distributed.chunk_ranges(n, 4096, 8) shards rendered separately and concatenated — is bit-identical
+  to the whole-frame render, in the default and the fp32 precision; 4,096 evenly spaced rays match the
+  oracle at 1e-4.  (The RCCL all-gather itself is covered by tests/test_distributed.py over gloo.)
+The oracle is pinned to the reference's golden fixtures (tests/test_oracle_golden.py).
+"""
+import importlib
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+
+pytestmark = pytest.mark.gpu
+
+anerf = importlib.import_module("a-nerf_amd")
+syn = importlib.import_module("a-nerf_amd.synthetic")
+dmod = importlib.import_module("a-nerf_amd.distributed")
+_lib = importlib.import_module("a-nerf_amd._lib")
+
+TOL = 1e-4
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _cuda():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _frame(H, nj, seed, tau):
+    sc = syn.make_scene(n_joints=nj, H=H, W=H, seed=seed)
+    ck = syn.make_checkpoint(seed, n_joints=nj, D=8, W=256, fine=True, tau=tau)
+    idx, cyls, boxes = anerf.rays.valid_pixels(sc["c2ws"], H, H, sc["focal"], kps=sc["kps"], ext_scale=0.001)
+    (x0, y0), (x1, y1) = (int(v) for v in boxes[0][0]), (int(v) for v in boxes[0][1])
+    n = (x1 - x0) * (y1 - y0)
+    assert n == len(idx[0])
+    c2w = torch.from_numpy(np.ascontiguousarray(sc["c2ws"][0][:3, :4])).cuda()
+    rb = torch.empty(n, 11, device="cuda")
+    _lib.check(_lib.load().anerf_gen_rays_box(_lib.ptr(c2w), H, H, sc["focal"], sc["focal"], 0.0, 0.0, 0, x0, y0, x1,
+                                              y1, 0.0, 1.0, _lib.ptr(rb), _lib.stream_handle()), "gen_rays_box")
+    torch.cuda.synchronize()
+    return sc, ck, cyls, rb
+
+
+def _render(rc, rb, sc, cyls):
+    n = rb.shape[0]
+    sk = torch.from_numpy(sc["skts"][0:1]).cuda().expand(n, -1, -1, -1)
+    cy = torch.from_numpy(cyls[0:1]).cuda().expand(n, -1)
+    return rc.render_rays(rb, 64, skts=sk, cyls=cy, N_importance=128, chunk=4096, ret_alpha=False)
+
+
+def _oracle_check(cfg, ck, sc, cyls, rb, out, n_sample):
+    import oracle
+    om = oracle.OracleModel(cfg, ck)
+    rb_h = rb.cpu().numpy()
+    near, far, _, _ = om.near_far(rb_h, cyls[0:1], chunk=4096)
+    sel = np.linspace(0, rb_h.shape[0] - 1, n_sample).astype(np.int64)
+    ref = om.render_rays(rb_h[sel], sc["skts"][0], cyls[0:1], chunk=4096, near=near[sel], far=far[sel])
+    for k in ("rgb_map", "disp_map", "acc_map", "rgb0", "disp0", "acc0"):
+        got = out[k].cpu().numpy()[sel]
+        d = float(np.abs(got.astype(np.float64) - ref[k]).max())
+        assert d <= TOL, f"{k}: max |gpu - oracle| = {d:.3e} over {n_sample} rays"
+
+
+@pytest.mark.parametrize("nj,precision", [(24, "bf16x6"), (24, "fp32"), (65, "bf16x6")])
+def test_full_frame_matches_oracle_on_8192_rays(nj, precision):
+    seed = 13 if nj == 24 else 14
+    sc, ck, cyls, rb = _frame(512, nj, seed, 79.6 if nj == 24 else 20.0)
+    cfg = anerf.RenderConfig(n_joints=nj, N_samples=64, N_importance=128, precision=precision).validate()
+    rc = anerf.RayCaster(cfg, ck)
+    out = _render(rc, rb, sc, cyls)
+    torch.cuda.synchronize()
+    _oracle_check(cfg, ck, sc, cyls, rb, out, 8192)
+
+
+@pytest.mark.parametrize("precision", ["bf16x6", "fp32"])
+def test_config5_pixel_shards_are_bit_identical(precision):
+    sc, ck, cyls, rb = _frame(1024, 24, 13, 79.6)
+    n = rb.shape[0]
+    assert n > 700_000
+    cfg = anerf.RenderConfig(N_samples=64, N_importance=128, precision=precision).validate()
+    rc = anerf.RayCaster(cfg, ck)
+    whole = _render(rc, rb, sc, cyls)
+    parts = [_render(rc, rb[s0:s1], sc, cyls) for s0, s1 in dmod.chunk_ranges(n, 4096, 8)]
+    torch.cuda.synchronize()
+    for k in ("rgb_map", "disp_map", "acc_map", "rgb0", "disp0", "acc0"):
+        assert torch.equal(torch.cat([p[k] for p in parts], 0), whole[k]), k
+    if precision == "bf16x6":
+        _oracle_check(cfg, ck, sc, cyls, rb, whole, 4096)

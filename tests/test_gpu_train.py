@@ -23,7 +23,7 @@ pytestmark = pytest.mark.gpu
 anerf = importlib.import_module("a-nerf_amd")
 train = importlib.import_module("a-nerf_amd.train")
 
-TRAIN = ["t1_s32i16_d4w128", "t2_s64i16_d8w256", "t3_softplus_fc"]
+TRAIN = ["t1_s32i16_d4w128", "t2_s64i16_d8w256", "t3_softplus_fc", "t4_tau200", "t5_single_mrv0"]
 TOL = 1e-4
 TOL_ALPHA = 2e-3
 GRAD_REL = 2e-3
@@ -45,6 +45,12 @@ def _run(name):
     m = g.meta
     tr = train.TrainRayCaster(g.cfg, g.ckpt).train()
     dev = torch.device("cuda:0")
+    if m.get("global_step") is not None:
+        # Trainer.train_batch's call (core/trainer.py:263-265), through the DataParallel-style alias
+        import argparse
+        tr.module.update_embed_fns(m["global_step"], argparse.Namespace(
+            cutoff_step=m["cutoff_step"], cutoff_rate=m["cutoff_rate"], freq_schedule_step=5, multires=7))
+        assert (tr.module.embed_fn.get_tau(), tr.module.embeddirs_fn.get_tau()) == tuple(m["tau_step"])
     c = lambda k: torch.from_numpy(g[k]).to(dev)  # noqa: E731
     sk = c("skts").clone().requires_grad_(True)
     rand = {k: c("rand_" + k) for k in ("t_rand", "noise0", "u", "noise1")}
@@ -198,3 +204,45 @@ def test_create_raycaster_training_drop_in(tmp_path):
     tr_kw2, *_ = anerf.create_raycaster(args, {"skel_type": kin.SMPLSkeleton}, device=0)
     assert isinstance(tr_kw2["ray_caster"], train.TrainRayCaster)
     assert torch.allclose(tr_kw2["ray_caster"].embed_fn.cutoff_dist, torch.full((24,), 0.5, device=dev))
+
+
+def test_tau_schedule_reaches_eval_kernel_without_repack():
+    """update_embed_fns changes tau for the training stages AND the fused eval delegate; the eval
+    model is updated in place (anerf_model_set_embed), and matches a RayCaster built at that tau."""
+    import argparse
+    g = Golden("t4_tau200")
+    m = g.meta
+    tr = train.TrainRayCaster(g.cfg, g.ckpt).eval()
+    dev = torch.device("cuda:0")
+    rb, sk, cy = (torch.from_numpy(g[k]).to(dev) for k in ("rays", "skts", "cyls"))
+    out20 = tr(rb, m["S"], skts=sk, cyls=cy, N_importance=m["I"])
+    handle = tr.eval_caster().model.handle.value
+    tr.module.update_embed_fns(m["global_step"], argparse.Namespace(cutoff_step=m["cutoff_step"],
+                                                                    cutoff_rate=m["cutoff_rate"]))
+    out200 = tr(rb, m["S"], skts=sk, cyls=cy, N_importance=m["I"])
+    assert tr.eval_caster().model.handle.value == handle          # no repack
+    assert not torch.equal(out200["rgb_map"], out20["rgb_map"])
+    ck = {k: dict(v) for k, v in g.ckpt.items()}
+    for e in ("embed_state_dict", "embeddirs_state_dict"):
+        ck[e]["tau"] = np.array(200.0, np.float32)
+    ref = anerf.RayCaster(g.cfg, ck).render_rays(rb, m["S"], skts=sk, cyls=cy, N_importance=m["I"])
+    for k in ("rgb_map", "disp_map", "acc_map", "rgb0"):
+        assert torch.equal(out200[k], ref[k]), k
+
+
+def test_checkpoint_round_trip_through_torch_save(tmp_path):
+    """checkpoint() -> torch.save -> load_checkpoint (weights_only) -> TrainRayCaster renders the same."""
+    g = Golden("t1_s32i16_d4w128")
+    m = g.meta
+    tr = train.TrainRayCaster(g.cfg, g.ckpt).eval()
+    with torch.no_grad():
+        tr.network_fine.rgb_linear.bias.add_(0.25)
+    path = tmp_path / "000100.tar"
+    torch.save(tr.checkpoint(), path)
+    tr2 = train.TrainRayCaster(g.cfg, anerf.raycaster.load_checkpoint(str(path))).eval()
+    dev = torch.device("cuda:0")
+    rb, sk, cy = (torch.from_numpy(g[k]).to(dev) for k in ("rays", "skts", "cyls"))
+    a = tr(rb, m["S"], skts=sk, cyls=cy, N_importance=m["I"])
+    b = tr2(rb, m["S"], skts=sk, cyls=cy, N_importance=m["I"])
+    for k in ("rgb_map", "disp_map", "acc_map", "rgb0"):
+        assert torch.equal(a[k], b[k]), k

@@ -53,3 +53,53 @@ def test_parameter_names_match_reference_gradients():
     ref = {k[len("grad_fn__"):] for k in g.d if k.startswith("grad_fn__") and not k.endswith("__idx")
            and not k.endswith("__norm")}
     assert ref and ref == names
+
+
+def test_tau_schedule_follows_update_tau():
+    """update_embed_fns -> CutoffEmbedder.update_tau (core/cutoff_embedder.py:181-183):
+    20 * rate ** (step / (cutoff_step * 1000)) clamped at 2000, float32, in both embedders."""
+    import argparse
+    g = Golden("t1_s32i16_d4w128")
+    tr = train.TrainRayCaster(g.cfg, g.ckpt, device="cpu")
+    args = argparse.Namespace(cutoff_step=250, cutoff_rate=10.0, freq_schedule_step=5, multires=7)
+    for step, want in ((0, 20.0), (250000, 200.0), (500000, 2000.0), (10 ** 7, 2000.0), (123457, None)):
+        tr.module.update_embed_fns(step, args)
+        with np.errstate(over="ignore"):
+            exp = np.float32(np.float32(20.0) * np.float32(10.0 ** (step / 250000.0)))
+        exp = min(exp, np.float32(2000.0))
+        assert tr.embed_fn.get_tau() == tr.embeddirs_fn.get_tau() == float(exp)
+        if want is not None:
+            assert abs(tr.embed_fn.get_tau() - want) <= 1e-3 * want
+    assert tr.module is tr
+
+
+def test_checkpoint_is_tensors_and_round_trips(tmp_path):
+    """checkpoint() holds CPU tensors in the reference's layout: torch.save -> torch.load(weights_only)
+    -> nn.Module.load_state_dict on a fresh module (the reference's loader) and back."""
+    g = Golden("t3_softplus_fc")
+    tr = train.TrainRayCaster(g.cfg, g.ckpt, device="cpu")
+    ck = tr.checkpoint()
+    for top in ("network_fn_state_dict", "network_fine_state_dict", "embed_state_dict", "embeddirs_state_dict"):
+        assert all(isinstance(v, torch.Tensor) and v.device.type == "cpu" for v in ck[top].values()), top
+    path = tmp_path / "ck.tar"
+    torch.save(ck, path)
+    ld = torch.load(path, weights_only=True)
+    fresh = train.NeRF(g.cfg)
+    fresh.load_state_dict(ld["network_fine_state_dict"])
+    for k, v in fresh.state_dict().items():
+        assert torch.equal(v, ck["network_fine_state_dict"][k]), k
+    tr2 = train.TrainRayCaster(g.cfg, ld, device="cpu")
+    for (k, a), (_, b) in zip(tr.state_dict().items(), tr2.state_dict().items()):
+        assert torch.equal(a, b), k
+
+
+def test_single_net_shares_one_module_and_fine_keys_win():
+    """single_net: network_fine IS network_fn (raycasters.py:98-104), both keys in the state dict;
+    a checkpoint with two different nets loads network_fine's last (RayCaster.load_state_dict)."""
+    g = Golden("t5_single_mrv0")
+    tr = train.TrainRayCaster(g.cfg, g.ckpt, device="cpu")
+    assert tr.network_fine is tr.network_fn
+    ck = tr.checkpoint()
+    assert set(ck["network_fn_state_dict"]) == set(ck["network_fine_state_dict"])
+    for k, v in ck["network_fn_state_dict"].items():
+        assert torch.equal(v, torch.as_tensor(g.ckpt["network_fine_state_dict"][k])), k

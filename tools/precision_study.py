@@ -56,6 +56,40 @@ def lin_bf16x6(x, w, b=None):
     return y if b is None else y + b
 
 
+def _pow2_scale(a, dim=None):
+    """Power-of-2 factor putting max|a| (per row when dim is given) into [2^14, 2^15): fp16 range."""
+    m = a.abs().amax(dim=dim, keepdim=True) if dim is not None else a.abs().max()
+    e = torch.floor(torch.log2(torch.where(m > 0, m, torch.ones_like(m))))
+    return torch.exp2(14.0 - e)
+
+
+def _split16(x):
+    hi = x.half().float()
+    lo = (x - hi).half().float()
+    return hi, lo
+
+
+def lin_fp16x3(x, w, b=None):
+    """x = x0 + x1, W = W0 + W1 in fp16 after power-of-2 scaling (per sample row for x, per tensor for W),
+    y = (x0 W0 + x0 W1 + x1 W0) / scales: three fp16 MFMA products with fp32 accumulation."""
+    sx, sw = _pow2_scale(x, dim=-1), _pow2_scale(w)
+    x0, x1 = _split16(x * sx)
+    w0, w1 = _split16(w * sw)
+    y = (_lin(x0.double(), w0.double()) + _lin(x0.double(), w1.double()) + _lin(x1.double(), w0.double()))
+    y = (y / (sx.double() * sw.double())).float()
+    return y if b is None else y + b
+
+
+def lin_fp16x4(x, w, b=None):
+    sx, sw = _pow2_scale(x, dim=-1), _pow2_scale(w)
+    x0, x1 = _split16(x * sx)
+    w0, w1 = _split16(w * sw)
+    y = (_lin(x0.double(), w0.double()) + _lin(x0.double(), w1.double()) + _lin(x1.double(), w0.double()) +
+         _lin(x1.double(), w1.double()))
+    y = (y / (sx.double() * sw.double())).float()
+    return y if b is None else y + b
+
+
 def lin_bf16(x, w, b=None):
     y = _lin(x.to(torch.bfloat16).double(), w.to(torch.bfloat16).double()).float()
     return y if b is None else y + b
@@ -69,7 +103,8 @@ def run(name, mode, mods, tmp):
     sc["cyls"] = z["cyls"]
     o, d = torch.from_numpy(z["rays_o"]), torch.from_numpy(z["rays_d"])
     cams = z["cams"] if "cams" in z.files else None
-    F.linear = {"bf16x6": lin_bf16x6, "bf16x3": lin_bf16x3, "bf16": lin_bf16, "fp32": _lin}[mode]
+    F.linear = {"bf16x6": lin_bf16x6, "bf16x3": lin_bf16x3, "bf16": lin_bf16, "fp32": _lin, "fp16x3": lin_fp16x3,
+                "fp16x4": lin_fp16x4}[mode]
     torch.nn.modules.linear.F.linear = F.linear
     try:
         ret = mg.render_subset(mods, kw, o, d, sc, cams=cams)
@@ -89,7 +124,7 @@ def main():
     mods = mg.import_reference()
     with tempfile.TemporaryDirectory() as tmp:
         for n in names:
-            for mode in ("fp32", "bf16x6", "bf16x3", "bf16"):
+            for mode in os.environ.get("MODES", "fp32,bf16x6,fp16x4,fp16x3,bf16x3,bf16").split(","):
                 print(n, mode, run(n, mode, mods, tmp), flush=True)
 
 
