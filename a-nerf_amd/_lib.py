@@ -21,7 +21,9 @@ c_i64p = ctypes.POINTER(ctypes.c_int64)
 ANERF_PREC_FP32 = 0
 ANERF_PREC_BF16X3 = 1
 ANERF_PREC_BF16X6 = 2
-PRECISIONS = {"fp32": ANERF_PREC_FP32, "bf16x3": ANERF_PREC_BF16X3, "bf16x6": ANERF_PREC_BF16X6}
+ANERF_PREC_FP16X3 = 3
+PRECISIONS = {"fp32": ANERF_PREC_FP32, "bf16x3": ANERF_PREC_BF16X3, "bf16x6": ANERF_PREC_BF16X6,
+              "fp16x3": ANERF_PREC_FP16X3}
 
 
 class ModelDesc(ctypes.Structure):

@@ -206,12 +206,14 @@ __global__ __launch_bounds__(256, 1) void density_kernel(ModelDev M, DensityArgs
         f32x16 acc[RB], h[RB];
         JointMask mask;
         Ring ring;
+        int es = 0;
         mlp_trunk<W, MR, false, PREC>(M, net, lds + P.sk, lds + P.cut, px, py, pz, lane, lds + P.bias, uf, nullptr, acc, h, ring,
-                         mask, nullptr, st);
+                         mask, nullptr, st, es);
         // alpha_linear on relu(h_last), in the k-step order of the render path's fused alpha head
         float sig = 0.0f;
 #pragma unroll
         for (int q = 0; q < W / 2; ++q) sig = fmaf(wa[q], relu_act(acc[q >> 4][q & 15]), sig);
+        if constexpr (PREC == 3) sig *= pow2f(-es);  // (fp16x3: the last layer's units)
         sig += __shfl_xor(sig, 32);
         sig += net.balpha;
         if (hh == 0 && s_out < A.n) A.out[s_out] = sig;

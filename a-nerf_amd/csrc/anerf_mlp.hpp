@@ -260,7 +260,8 @@ __device__ __forceinline__ void split3_pair(float a, float b, X6T& t, int q) {
 __device__ __forceinline__ void split3_block_pair(const f32x16& hb, X6T (&t)[2], int p) {
     const int s = p >> 2, q = p & 3;
 #if ANERF_X6_PROBE == 2  // (diagnostic builds of tools/probe only: no split arithmetic)
-    t[s].d[0][q] = t[s].d[1][q] = t[s].d[2][q] = __builtin_bit_cast(unsigned, hb[8 * s + 2 * q]);
+    const float v = hb[8 * s + 2 * q];
+    t[s].d[0][q] = t[s].d[1][q] = t[s].d[2][q] = __builtin_bit_cast(unsigned, v);
     return;
 #endif
     split3_pair(hb[8 * s + 2 * q], hb[8 * s + 2 * q + 1], t[s], q);
@@ -381,6 +382,189 @@ __device__ __forceinline__ void mlp_layer_x6(f32x16 (&out)[RBO], f32x16 (&ain)[R
                 for (int p = 0; p < 8; ++p)
                     if (pair_group(p, q0) == q || (q == NQ - 1 && pair_group(p, q0) > q))
                         split3_block_pair(h[ib + 1], Tn, p);
+            }
+        }
+    }
+}
+
+// ---- fp16x3 form (ANERF_PREC_FP16X3): per-sample power-of-two scaling, then x = x0 + x1 and
+// w = w0 + w1 in fp16 (22 significant bits each), product ~= x0 w0 + x0 w1 + x1 w0: three
+// v_mfma_f32_32x32x16_f16 per 16 k (half of bf16x6's six) with exact fp16 products and fp32
+// accumulation; the dropped x1 w1 is ~2^-22 of |x w|.  fp16's narrow exponent range is handled by
+// scaling: the weights of a layer by 2^ew on the host (max |w| in [2^10, 2^11)), the input of every
+// sample (the 32-sample block's column, a lane and its partner lane l ^ 32) by t = 2^shift so its
+// largest relu'd activation lies in [2^10, 2^11) — values far below the sample's maximum lose
+// only what is below ~2^-34 of that maximum.  (Measured on gfx950: with both operands' maxima at
+// 2^13..2^15 — products ~2^28, 16-term dot products past ~2^31 — the f16 MFMA returned wrong sums
+// for some samples; at 2^12 and below it matched the fp32 path.  2^10 leaves a 2^5 margin.)
+// The accumulators then hold the layer's output times 2^es (es = a per-sample integer: all scales
+// are exact powers of two, so the scaling itself never rounds); the next layer rescales from
+// there, the skip layer's x parts scale their B operands to it and the heads unscale.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+struct H3T {
+    unsigned d[2][4];
+    __device__ __forceinline__ f16x8 frag(int c) const {
+        return __builtin_bit_cast(f16x8, u32x4{d[c][0], d[c][1], d[c][2], d[c][3]});
+    }
+};
+
+__device__ __forceinline__ float pow2f(int e) { return __builtin_bit_cast(float, (e + 127) << 23); }  // |e| <= 126
+
+// values a, b (relu'd, in the input's units) times t -> dword q of the two fp16 components: the high
+// part rounds x to 11 significant bits in the f32 encoding (exact in fp16), the low part is the
+// exact remainder rounded toward zero to fp16
+__device__ __forceinline__ void split2_pair(float a, float b, float t, H3T& T, int q) {
+    const float xa = a * t, xb = b * t;
+    const float ha = __builtin_bit_cast(float, (__builtin_bit_cast(unsigned, xa) + 0x1000u) & 0xffffe000u);
+    const float hb = __builtin_bit_cast(float, (__builtin_bit_cast(unsigned, xb) + 0x1000u) & 0xffffe000u);
+    T.d[0][q] = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_pkrtz(ha, hb));
+    T.d[1][q] = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_pkrtz(xa - ha, xb - hb));
+}
+
+__device__ __forceinline__ void split2_block_pair(const f32x16& hb, float t, H3T (&T)[2], int p) {
+    const int s = p >> 2, q = p & 3;
+    split2_pair(hb[8 * s + 2 * q], hb[8 * s + 2 * q + 1], t, T[s], q);
+}
+
+__device__ __forceinline__ f32x16 mfma_f16_32x32x16(f16x8 a, f16x8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+// group `half` (0 / 1) of a 16-float ring slot: fragments w0 (floats 8 half .. +3), w1 (+4 .. +7)
+__device__ __forceinline__ f32x16 mfma_h3(const float (&w)[16], int half, const H3T& x, f32x16 c) {
+    const int o = 8 * half;
+    const f16x8 w0 = __builtin_bit_cast(f16x8, f32x4{w[o], w[o + 1], w[o + 2], w[o + 3]});
+    const f16x8 w1 = __builtin_bit_cast(f16x8, f32x4{w[o + 4], w[o + 5], w[o + 6], w[o + 7]});
+    c = mfma_f16_32x32x16(w1, x.frag(0), c);  // small terms first
+    c = mfma_f16_32x32x16(w0, x.frag(1), c);
+    return mfma_f16_32x32x16(w0, x.frag(0), c);
+}
+
+// The input scale t = 2^shift of one sample: its largest relu'd input (signed-integer max of the
+// bit patterns, 0 for all-negative / zero inputs; NaN stays large) over this lane's and the partner
+// lane's values, scaled into [2^10, 2^11).  es: exponent of the units the input is in; on return the units of this layer's
+// output, es + shift + ew, kept within [-100, 60] so that bias * 2^es stays finite.
+template <int RBI>
+__device__ __forceinline__ float h3_scale(const f32x16 (&a)[RBI], int& es, int ew, int top) {
+    int m = 0;
+#pragma unroll
+    for (int rb = 0; rb < RBI; ++rb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            // (through a scalar: hipcc's __builtin_bit_cast of an ext-vector element lvalue reads
+            // element 0 of the vector, whatever the index)
+            const float v = a[rb][i];
+            m = max(m, __builtin_bit_cast(int, v));
+        }
+    m = max(m, __shfl_xor(m, 32));
+    int shift = m > 0 ? top - (m >> 23) : 0;  // (m >> 23: the biased exponent; top = 127 + 10)
+    shift = min(shift, 60 - es - ew);
+    shift = max(shift, -100 - es - ew);
+    shift = min(max(shift, -126), 126);
+    es += shift + ew;
+    return pow2f(shift);
+}
+
+// mlp_layer_x6's schedule with 8-float groups (3 MFMAs each), two groups per ring slot (slot
+// (g / 2) % 4, prefetched 3 slots = 6 groups ahead).  OUT_SAME layers alias out and ain; bias * 2^es
+// initialises the outputs.  ALPHA folds sig += w_alpha . h with h in the INPUT's units.
+template <int RBO, int RBI, bool OUT_SAME, bool ALPHA>
+__device__ __forceinline__ void mlp_layer_h3(f32x16 (&out)[RBO], f32x16 (&ain)[RBI], f32x16 (&h)[RBI],
+                                             const float* __restrict__ bias, const float* __restrict__ wp, int lane,
+                                             Ring& ring, bool preloaded, const float* __restrict__ next,
+                                             const float* __restrict__ wa, float& sig, int& es, int ew, int top) {
+    static_assert(RBO <= RBI, "h3 layer shape");
+    constexpr int NG = 2 * RBO * RBI;
+    constexpr int NS = NG / 2;  // ring slots of this layer
+    constexpr int PS = 3;       // prefetch distance (slots)
+    constexpr int NQ = 2 * RBO;  // groups per input block
+    const int hh = lane >> 5;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(wp);
+    const __amdgpu_buffer_rsrc_t rn = make_rsrc(next ? next : wp);
+    const float t = h3_scale<RBI>(ain, es, ew, top);
+    const float S = pow2f(es);
+    auto convert_half = [&](int rb, int half) {  // relu of 8 inputs (+ their 8 scaled bias outputs)
+#pragma unroll
+        for (int i = 8 * half; i < 8 * half + 8; ++i) h[rb][i] = relu_act(ain[rb][i]);
+        if (OUT_SAME && rb < RBO) {
+            const f32x4* p = reinterpret_cast<const f32x4*>(bias + (rb * 2 + hh) * 16 + 8 * half);
+            const f32x4 v0 = p[0], v1 = p[1];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                out[rb][8 * half + e] = v0[e] * S;
+                out[rb][8 * half + 4 + e] = v1[e] * S;
+            }
+        }
+    };
+    auto alpha = [&](int ib, int s) {  // k = 16 ib + 8 s + j, the order of mlp_layer's fold
+        if constexpr (ALPHA) {
+            const f32x4* w4 = reinterpret_cast<const f32x4*>(wa + hh * 16 * RBI + 16 * ib + 8 * s);
+            const f32x4 u0 = w4[0], u1 = w4[1];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) sig = fmaf(j < 4 ? u0[j] : u1[j - 4], h[ib][8 * s + j], sig);
+        }
+    };
+    if constexpr (!OUT_SAME) {
+#pragma unroll
+        for (int rb = 0; rb < RBO; ++rb) out[rb] = f32x16{0};
+    }
+    // slot G + PS of this layer at its first group, or the next h3 phase's first slots (this layer's
+    // last slot again without one: harmless; unconditional loads keep the counted vmcnt waits exact)
+    const bool has_next = next != nullptr;
+    auto prefetch = [&](int g) {
+        if (g & 1) return;
+        const int G = g >> 1;
+        if (G + PS < NS)
+            load_group<16>(ring.v[(G + PS) % 4], rs, lane, G + PS);
+        else if (NS % 4 == 0)
+            load_group<16>(ring.v[(G + PS) % 4], rn, lane, has_next ? G + PS - NS : NS - 1);
+    };
+    auto pair_group = [](int p, int q0) { return q0 + (p * (NQ - q0 > 0 ? NQ - q0 : 1)) / 8; };
+    if (!preloaded) {
+#pragma unroll
+        for (int G = 0; G < PS && G < NS; ++G) load_group<16>(ring.v[G], rs, lane, G);
+    }
+    convert_half(0, 0);
+    convert_half(0, 1);
+    H3T T[2], Tn[2];
+#pragma unroll
+    for (int p = 0; p < 8; ++p) split2_block_pair(h[0], t, T, p);
+    constexpr int QL = NQ > 2 ? 2 : NQ;
+#pragma clang loop unroll(full)
+    for (int g = 0; g < NQ; ++g) {
+        __builtin_amdgcn_sched_barrier(0);
+        prefetch(g);
+        const int ob = g >> 1, s = g & 1;
+        out[ob] = mfma_h3(ring.v[(g >> 1) % 4], g & 1, T[s], out[ob]);
+        if (ob == 0) alpha(0, s);
+        if (ob + 1 < RBI && (ob + 1 < RBO || ob == 0)) convert_half(ob + 1, s);
+        if (RBI > 1) {
+#pragma unroll
+            for (int p = 0; p < 8; ++p)
+                if (pair_group(p, QL) == (g < QL ? -1 : g) || (g == NQ - 1 && pair_group(p, QL) > g))
+                    split2_block_pair(h[1], t, Tn, p);
+        }
+    }
+#pragma clang loop unroll(full)
+    for (int ib = 1; ib < RBI; ++ib) {
+        T[0] = Tn[0];
+        T[1] = Tn[1];
+        const bool conv_next = ib + 1 < RBI && ib + 1 >= (RBO > 2 ? RBO : 2);
+        const int q0 = conv_next ? (NQ > 2 ? 2 : NQ) : 0;
+#pragma clang loop unroll(full)
+        for (int q = 0; q < NQ; ++q) {
+            const int s = q / RBO, ob = q % RBO;
+            const int g = NQ + (ib - 1) * NQ + q;
+            __builtin_amdgcn_sched_barrier(0);
+            prefetch(g);
+            out[ob] = mfma_h3(ring.v[(g >> 1) % 4], g & 1, T[s], out[ob]);
+            if (ob == RBO - 1) alpha(ib, s);
+            if (ib + 1 < RBI) {
+                if (conv_next && q < 2) convert_half(ib + 1, q);
+#pragma unroll
+                for (int p = 0; p < 8; ++p)
+                    if (pair_group(p, q0) == q || (q == NQ - 1 && pair_group(p, q0) > q))
+                        split2_block_pair(h[ib + 1], t, Tn, p);
             }
         }
     }
@@ -518,7 +702,7 @@ __device__ __forceinline__ void u_part(f32x16 (&acc)[RB], const ModelDev& M, con
                                        const float* __restrict__ sk, const float* __restrict__ cut, float px,
                                        float py, float pz, int lane, JointMask* mask, float* __restrict__ uf,
                                        float* __restrict__ wvo, Ring& sh, const float* __restrict__ next,
-                                       Stamps& st) {
+                                       Stamps& st, float xs = 1.0f) {
     const int hh = lane >> 5;
     const int njh2 = M.njh2;
     const int npp = njh2 / 2;
@@ -570,7 +754,7 @@ __device__ __forceinline__ void u_part(f32x16 (&acc)[RB], const ModelDev& M, con
             load_u_group<RB>(ring[(g + 2) % 3], rs, lane, gn);
 #pragma unroll
             for (int t = 0; t < 2; ++t) {
-                const float b = f[2 * g + t];
+                const float b = f[2 * g + t] * xs;
 #pragma unroll
                 for (int rb = 0; rb < RB; ++rb) acc[rb] = mfma_f32_32x32x2(ring[g % 3][rb][t], b, acc[rb]);
             }
@@ -607,7 +791,7 @@ __device__ __forceinline__ void u_part(f32x16 (&acc)[RB], const ModelDev& M, con
 template <int RB>
 __device__ __forceinline__ void u_part_lds(f32x16 (&acc)[RB], const ModelDev& M, const float* __restrict__ wp,
                                            const float* __restrict__ uf, int lane, Ring& sh,
-                                           const float* __restrict__ next) {
+                                           const float* __restrict__ next, float xs = 1.0f) {
     const int total_groups = 3 * (M.njh2 / 2);
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(wp);
     const f32x2* ub = reinterpret_cast<const f32x2*>(uf) + lane;
@@ -626,7 +810,7 @@ __device__ __forceinline__ void u_part_lds(f32x16 (&acc)[RB], const ModelDev& M,
 #pragma unroll
             for (int t = 0; t < 2; ++t)
 #pragma unroll
-                for (int rb = 0; rb < RB; ++rb) acc[rb] = mfma_f32_32x32x2(ring[gg][rb][t], bc[t], acc[rb]);
+                for (int rb = 0; rb < RB; ++rb) acc[rb] = mfma_f32_32x32x2(ring[gg][rb][t], bc[t] * xs, acc[rb]);
             bc = bn;
         }
     }
@@ -686,7 +870,8 @@ __device__ __forceinline__ void u_part_x6_preload(const float* __restrict__ wp, 
 
 template <int RB>
 __device__ __forceinline__ void u_part_x6(f32x16 (&acc)[RB], const ModelDev& M, const float* __restrict__ wp,
-                                          const float* __restrict__ uf, int lane, Ring& ring, bool preloaded) {
+                                          const float* __restrict__ uf, int lane, Ring& ring, bool preloaded,
+                                          float xs = 1.0f) {
     static_assert(RB % 4 == 0 && RB >= 4, "u_part_x6 needs RB % 4 == 0");
     constexpr int PD = 3;
     const int nq = 3 * M.njh2, ns = (nq + 7) / 8, ng = ns * RB;
@@ -695,7 +880,8 @@ __device__ __forceinline__ void u_part_x6(f32x16 (&acc)[RB], const ModelDev& M, 
     // Every group issues its loads and every step its LDS reads unconditionally (clamped: the last
     // groups reload the last group, the last step reads features it does not use), so the
     // compiler's counted vmcnt / lgkmcnt waits stay exact: a conditional load makes them drain.
-    auto feat = [&](int q) { return mask_f(uf[min(q, nq - 1) * 64 + lane], q < nq); };
+    // (xs: a power of two, so the scaled features split exactly as the unscaled ones)
+    auto feat = [&](int q) { return mask_f(uf[min(q, nq - 1) * 64 + lane] * xs, q < nq); };
     X6T cur[1], nxt[1];
     float fn[8];
 #pragma unroll
@@ -738,7 +924,7 @@ __device__ __forceinline__ void v_geom(const ModelDev& M, const float* __restric
 template <int RB, int MR>
 __device__ __forceinline__ void v_part(f32x16 (&acc)[RB], const ModelDev& M, const float* __restrict__ wp,
                                        const float* __restrict__ sk, const float* __restrict__ cut, float px,
-                                       float py, float pz, int lane, JointMask mask, Stamps& st) {
+                                       float py, float pz, int lane, JointMask mask, Stamps& st, float xs = 1.0f) {
     constexpr int GB = VPart<MR>::GB;
     constexpr int KB = VPart<MR>::KB;
     constexpr int PER = (MR + GB - 2) / (GB - 1);  // sin/cos terms of the next joint per group 1..GB-1
@@ -759,13 +945,14 @@ __device__ __forceinline__ void v_part(f32x16 (&acc)[RB], const ModelDev& M, con
     {
         float dist, w;
         v_geom(M, sk, cut, j, px, py, pz, dist, w);
+        w *= xs;  // (a power of two: the products equal the unscaled ones times xs exactly)
 #pragma unroll
         for (int t = 0; t < MR; ++t) {
             float sn, cs;
             sincos_rr(dist * (float)(1 << t), sn, cs);
             f[t] = (hh ? cs : sn) * w;
         }
-        f[MR] = hh ? 0.0f : (dist_in ? dist * w : dist);
+        f[MR] = hh ? 0.0f : (dist_in ? dist * w : dist * xs);
 #pragma unroll
         for (int t = MR + 1; t < KB; ++t) f[t] = 0.0f;
     }
@@ -796,6 +983,7 @@ __device__ __forceinline__ void v_part(f32x16 (&acc)[RB], const ModelDev& M, con
             // next joint's features under these MFMAs
             if (g == 0) {
                 v_geom(M, sk, cut, jg, px, py, pz, dn, wn);
+                wn *= xs;
                 pin(dn), pin(wn);
             } else {
 #pragma unroll
@@ -808,7 +996,7 @@ __device__ __forceinline__ void v_part(f32x16 (&acc)[RB], const ModelDev& M, con
             }
             interleave_mfma_valu<2 * RB, 8>();
         }
-        fn[MR] = hh ? 0.0f : (dist_in ? dn * wn : dn);
+        fn[MR] = hh ? 0.0f : (dist_in ? dn * wn : dn * xs);
 #pragma unroll
         for (int t = MR + 1; t < KB; ++t) fn[t] = 0.0f;
 #pragma unroll
@@ -824,7 +1012,7 @@ __device__ __forceinline__ void v_part(f32x16 (&acc)[RB], const ModelDev& M, con
 // values of the next k-step are read under the current k-step's MFMAs.
 template <int RBV>
 __device__ __forceinline__ void view_dir_part(f32x16 (&acc)[RBV], const ModelDev& M, const float* __restrict__ G,
-                                              const float* __restrict__ wvp, int lane) {
+                                              const float* __restrict__ wvp, int lane, float bs = 1.0f) {
     constexpr int WH = RBV * 32;
     const int hh = lane >> 5, sl = lane & 31;
     const int njh2 = M.njh2;
@@ -832,14 +1020,15 @@ __device__ __forceinline__ void view_dir_part(f32x16 (&acc)[RBV], const ModelDev
     float gv[RBV];
 #pragma unroll
     for (int rb = 0; rb < RBV; ++rb) gv[rb] = G[col(0) * WH + sl + 32 * rb];
-    float b = wvp[lane];
+    // (bs: the units of acc, 2^es for the fp16x3 view layer: the B operands carry it)
+    float b = wvp[lane] * bs;
     for (int p = 0; p <= njh2; ++p) {
         __builtin_amdgcn_sched_barrier(0);
         const int pn = min(p + 1, njh2);
         float gn[RBV];
 #pragma unroll
         for (int rb = 0; rb < RBV; ++rb) gn[rb] = G[col(pn) * WH + sl + 32 * rb];
-        const float bn = pn < njh2 ? wvp[pn * 64 + lane] : (hh ? 0.0f : 1.0f);
+        const float bn = pn < njh2 ? wvp[pn * 64 + lane] * bs : (hh ? 0.0f : bs);
 #pragma unroll
         for (int rb = 0; rb < RBV; ++rb) acc[rb] = mfma_f32_32x32x2(gv[rb], b, acc[rb]);
 #pragma unroll
@@ -857,18 +1046,19 @@ __device__ __forceinline__ bool mlp_trunk(const ModelDev& M, const NetDev& net, 
                                           const float* __restrict__ bias, float* __restrict__ uf,
                                           float* __restrict__ wvo, f32x16 (&acc)[W / 32], f32x16 (&h)[W / 32],
                                           Ring& ring, JointMask& mask, const float* __restrict__ after_last,
-                                          Stamps& st) {
+                                          Stamps& st, int& es) {
     constexpr int RB = W / 32;
     const int hh = lane >> 5;
     float nosig = 0.0f;
+    es = 0;  // (fp16x3: the exponent of the accumulators' units, see mlp_layer_h3)
     constexpr bool HANDOFF = (2 * RB == 16);  // u-part groups have the regs layers' group size
-    // bf16x6 with the LDS feature store: features in a VALU pass, both bone-direction parts as x6
-    constexpr bool UX6 = (P == 2) && (RB % 4 == 0);
+    // bf16x6 / fp16x3 with the LDS feature store: features in a VALU pass, both bone-direction parts as x6
+    constexpr bool UX6 = (P >= 2) && (RB % 4 == 0);
     const bool ux6 = UX6 && M.ux6 && uf != nullptr;
     if (!ux6) ring_preload<2 * RB>(ring, net.wl[0], lane);  // the u part's first groups, early
     load_bias<RB>(acc, bias, hh);
     STAMP(st, 10);
-    const float* const* wl = P == 2 ? net.wl6 : (P ? net.wl3 : net.wl);  // hidden-layer streams of this precision
+    const float* const* wl = P == 3 ? net.wlh : (P == 2 ? net.wl6 : (P ? net.wl3 : net.wl));  // hidden-layer streams
     if (ux6) {
         if constexpr (UX6) u_part_x6_preload<RB>(net.wu6, lane, ring);  // (latency under the VALU pass)
         u_features_lds<WV>(M, sk, cut, px, py, pz, lane, &mask, uf, wvo);
@@ -877,7 +1067,7 @@ __device__ __forceinline__ bool mlp_trunk(const ModelDev& M, const NetDev& net, 
     } else {
         // (bf16x6 layers have 12-float groups: the phases before them do not prefetch into the ring for them)
         u_part<RB, WV>(acc, M, net.wl[0], sk, cut, px, py, pz, lane, &mask, uf, wvo, ring,
-                       M.D > 1 ? (P == 2 ? nullptr : wl[1]) : after_last, st);
+                       M.D > 1 ? (P >= 2 ? nullptr : wl[1]) : after_last, st);
     }
     STAMP(st, 8);
     v_part<RB, MR>(acc, M, net.wl0v, sk, cut, px, py, pz, lane, mask, st);
@@ -886,7 +1076,19 @@ __device__ __forceinline__ bool mlp_trunk(const ModelDev& M, const NetDev& net, 
     for (int L = 1; L < M.D; ++L) {
         const float* after = L + 1 < M.D ? wl[L + 1] : after_last;
         const bool skl = (L == M.skip + 1);
-        if constexpr (P == 2) {
+        if constexpr (P == 3) {
+            // the next h3 phase (the next hidden layer or the view layer) is prefetched; not across the
+            // skip layer's x parts, which load themselves and scale their B operands by 2^es (the
+            // units the h part left in the accumulators)
+            const float* nxth = skl ? nullptr : after;
+            mlp_layer_h3<RB, RB, true, false>(acc, acc, h, bias + L * W, wl[L], lane, ring, pre6, nxth, nullptr,
+                                              nosig, es, net.ewl[L], M.h3_top);
+            pre6 = nxth != nullptr;
+            if (skl) {  // the f32 skip x parts take their first groups from the ring (the x6 one loads itself)
+                if (!ux6) ring_preload<2 * RB>(ring, net.wskipu, lane);
+                after = nullptr;
+            }
+        } else if constexpr (P == 2) {
             // the next x6 phase: the next layer, after_last, or the skip layer's x6 bone-direction part
             // (selected by uniform values only: uf is a per-wave LDS pointer, derived from threadIdx,
             // and a pointer selected by it becomes a VGPR whose buffer loads waterfall)
@@ -907,19 +1109,20 @@ __device__ __forceinline__ bool mlp_trunk(const ModelDev& M, const NetDev& net, 
             if (skl && !HANDOFF) ring_preload<2 * RB>(ring, net.wskipu, lane);
         }
         STAMP(st, 11);
-        if (skl) {  // x part after the h part
+        if (skl) {  // x part after the h part (in the h part's units: B operands times xs)
+            const float xs = P == 3 ? pow2f(es) : 1.0f;
             if (ux6) {
-                if constexpr (UX6) u_part_x6<RB>(acc, M, net.wskipu6, uf, lane, ring, true);
+                if constexpr (UX6) u_part_x6<RB>(acc, M, net.wskipu6, uf, lane, ring, P == 2, xs);
             } else if (uf)
-                u_part_lds<RB>(acc, M, net.wskipu, uf, lane, ring, after);
+                u_part_lds<RB>(acc, M, net.wskipu, uf, lane, ring, after, xs);
             else
                 u_part<RB, false>(acc, M, net.wskipu, sk, cut, px, py, pz, lane, nullptr, nullptr, nullptr, ring, after,
-                                  st);
-            v_part<RB, MR>(acc, M, net.wskipv, sk, cut, px, py, pz, lane, mask, st);
+                                  st, xs);
+            v_part<RB, MR>(acc, M, net.wskipv, sk, cut, px, py, pz, lane, mask, st, xs);
             STAMP(st, 12);
         }
     }
-    return pre6;  // (bf16x6: after_last's first groups are in the ring)
+    return pre6;  // (bf16x6 / fp16x3: after_last's first groups are in the ring)
 }
 
 // One 32-sample block of one ray through a whole NeRF: raw (rgb, sigma) into LDS.
@@ -944,14 +1147,20 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
     f32x16 acc[RB], h[RB];
     JointMask mask;
     Ring ring;
+    int es = 0;
     const bool pre = mlp_trunk<W, MR, true, P>(M, net, sk, cut, px, py, pz, lane, bias, uf, wvp, acc, h, ring, mask,
-                                               P == 2 ? net.wview6 : net.wview, st);
+                                               P == 3 ? net.wviewh : (P == 2 ? net.wview6 : net.wview), st, es);
     // views_linears.0 with feature_linear fused in (W' = Wv_f Wf, see pack_net) on relu(h_last),
     // alpha_linear folded into its groups (same relu'd B operands), + the factorised
     // direction / code / bias part from G, then relu
     float sig = 0.0f;
     f32x16 av[RBV];
-    if constexpr (P == 2)
+    if constexpr (P == 3) {
+        const int es_h = es;  // the alpha head sums the last hidden layer's activations, in its units
+        mlp_layer_h3<RBV, RB, false, true>(av, acc, h, nullptr, net.wviewh, lane, ring, pre, nullptr,
+                                           bias + (M.D + 1) * W, sig, es, net.ew_view, M.h3_top);
+        sig *= pow2f(-es_h);
+    } else if constexpr (P == 2)
         mlp_layer_x6<RBV, RB, false, true>(av, acc, h, nullptr, net.wview6, lane, ring, pre, nullptr,
                                            bias + (M.D + 1) * W, sig);
     else
@@ -960,7 +1169,7 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
     STAMP(st, 16);
     sig += __shfl_xor(sig, 32);
     sig += net.balpha;
-    view_dir_part<RBV>(av, M, G, wvp, lane);
+    view_dir_part<RBV>(av, M, G, wvp, lane, P == 3 ? pow2f(es) : 1.0f);
     STAMP(st, 17);
     float rgb[3];
 #pragma unroll
@@ -972,26 +1181,27 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
 #pragma unroll
             for (int i = 0; i < 16; ++i) a += wr[rb * 16 + i] * relu_act(av[rb][i]);
         a += __shfl_xor(a, 32);
+        if constexpr (P == 3) a *= pow2f(-es);  // (the view layer's units)
         rgb[c] = a + net.brgb[c];
     }
     STAMP(st, 13);
     if (mfma_count && lane == 0) {  // exact MFMA work of this block (wave-uniform quantities)
         const int act = __builtin_popcountll(mask.m0) + __builtin_popcountll(mask.m1);
-        const bool ux6 = (P == 2) && (RB % 4 == 0) && uf != nullptr && M.ux6;  // as in mlp_trunk
+        const bool ux6 = (P >= 2) && (RB % 4 == 0) && uf != nullptr && M.ux6;  // as in mlp_trunk
         const int xk = (ux6 ? 0 : 3 * M.njh2) + act * VPart<MR>::KB;   // f32 k-steps of one x part
         long long k = (long long)xk * RB + (long long)(M.njh2 + 1) * RBV;
         if (ux6) {
             const int nx = (M.skip + 1 < M.D) ? 2 : 1;
             atomicAdd(mfma_count + 1, (unsigned long long)(nx * ((3 * M.njh2 + 7) / 8) * RB * 6));
         }
-        if (P == 2)
-            atomicAdd(mfma_count + 1, (unsigned long long)(RBV * RB * 2 * 6));  // view layer, bf16x6
+        if (P >= 2)  // view layer, bf16x6 / fp16x3
+            atomicAdd(mfma_count + 1, (unsigned long long)(RBV * RB * 2 * (P == 2 ? 6 : 3)));
         else
             k += (long long)(W / 2) * RBV;
         if (M.skip + 1 < M.D) k += (long long)xk * RB;
         const long long hid = (long long)(M.D - 1) * RB * RB;  // 32x32 blocks of the hidden layers
         if (P != 0) {
-            atomicAdd(mfma_count + 1, (unsigned long long)(hid * 2 * 3 * P));  // 2 k16-steps x 3 (x6) per block
+            atomicAdd(mfma_count + 1, (unsigned long long)(hid * 2 * (P == 2 ? 6 : 3)));  // 2 k16-steps x products
         } else {
             k += hid * 16;
         }

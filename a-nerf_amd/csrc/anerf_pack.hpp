@@ -159,6 +159,91 @@ std::vector<float> pack_layer_x6(const float* Wt, int n_out, int ld, int col_off
     });
 }
 
+// ---- fp16x3 split (ANERF_PREC_FP16X3): the block is scaled by 2^ew (max |w| 2^ew in [2^10, 2^11),
+// see anerf_mlp.hpp on the f16 MFMA's range), then w = w0 + w1, each fp16 (RNE of the
+// running remainder), i.e. >= 22 significant bits.  Groups (ob, ib, s) in pack_layer_x6's order,
+// 8 floats each (fragments w0, w1, element j as in pack_layer_x3), two consecutive groups per
+// 16-float ring slot.
+uint16_t f16_rne(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    const uint32_t sign = (u >> 16) & 0x8000u;
+    const uint32_t a = u & 0x7fffffffu;
+    if (a >= 0x7f800000u) return (uint16_t)(sign | 0x7c00u | (a > 0x7f800000u ? 0x200u : 0u));
+    if (a >= 0x477ff000u) return (uint16_t)(sign | 0x7c00u);  // rounds past 65504: inf
+    if (a < 0x38800000u) {  // below 2^-14: fp16 subnormal (or zero), units of 2^-24
+        const double q = (double)(*reinterpret_cast<const float*>(&a)) * 16777216.0;
+        return (uint16_t)(sign | (uint32_t)std::nearbyint(q));
+    }
+    const uint32_t e = (a >> 23) - 112, m = a & 0x7fffffu;
+    uint32_t h = (e << 10) | (m >> 13);
+    const uint32_t rem = m & 0x1fffu;
+    if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) ++h;
+    return (uint16_t)(sign | h);
+}
+float f16_to_f(uint16_t b) {
+    const uint32_t sign = (uint32_t)(b & 0x8000u) << 16, e = (b >> 10) & 0x1fu, m = b & 0x3ffu;
+    uint32_t u;
+    if (e == 0) {
+        const float v = (float)m * 5.9604644775390625e-08f;  // m 2^-24 (exact)
+        std::memcpy(&u, &v, 4);
+        u |= sign;
+    } else if (e == 31) {
+        u = sign | 0x7f800000u | (m << 13);
+    } else {
+        u = sign | ((e + 112) << 23) | (m << 13);
+    }
+    float f;
+    std::memcpy(&f, &u, 4);
+    return f;
+}
+
+// fp16x3 operand range: maxima in [2^T, 2^(T+1)), T = 10 (ANERF_H3_TARGET overrides: A/B studies only)
+int h3_target() {
+    const char* e = std::getenv("ANERF_H3_TARGET");
+    return e ? std::atoi(e) : 10;
+}
+
+// power-of-two exponent ew with max |W[:, col_off : col_off + n_in]| 2^ew in [2^T, 2^(T+1))
+int h3_exponent(const float* Wt, int n_out, int ld, int col_off, int n_in) {
+    float mx = 0.0f;
+    for (int r = 0; r < n_out; ++r)
+        for (int c = 0; c < n_in; ++c) mx = std::max(mx, std::fabs(Wt[(size_t)r * ld + col_off + c]));
+    if (!(mx > 0.0f) || !std::isfinite(mx)) return 0;
+    int e;
+    std::frexp(mx, &e);  // mx in [2^(e-1), 2^e)
+    return std::max(-100, std::min(100, h3_target() + 1 - e));
+}
+
+std::vector<float> pack_layer_h3(const float* Wt, int n_out, int ld, int col_off, int n_in, int ew) {
+    const int RBO = n_out / 32, RBI = n_in / 32;
+    const int ng = 2 * RBO * RBI;
+    const float sc = std::ldexp(1.0f, ew);
+    return pack_groups(ng / 2, 16, [&](int gg, int sl, int l) {
+        const int g = 2 * gg + (sl >> 3), f = (sl >> 2) & 1, e = sl & 3;  // group, fragment, f16 pair
+        int ob, ib, s;
+        if (g < 2 * RBO) {
+            ob = g >> 1, ib = 0, s = g & 1;
+        } else {
+            const int idx = g - 2 * RBO;
+            ib = 1 + idx / (2 * RBO), s = (idx / RBO) & 1, ob = idx % RBO;
+        }
+        const int h = l >> 5, row = 32 * ob + (l & 31);
+        uint32_t bits = 0;
+        for (int jj = 0; jj < 2; ++jj) {
+            const int j = 2 * e + jj;
+            const int col = col_off + 32 * ib + 16 * s + 8 * (j >> 2) + 4 * h + (j & 3);
+            const float w = Wt[(size_t)row * ld + col] * sc;  // (exact: a power of two)
+            const uint16_t w0 = f16_rne(w);
+            const uint16_t v = f ? f16_rne(w - f16_to_f(w0)) : w0;
+            bits |= (uint32_t)v << (16 * jj);
+        }
+        float out;
+        std::memcpy(&out, &bits, 4);
+        return out;
+    });
+}
+
 // bone-direction part: k-step q = 3p + c, half h -> joint p + h*njh2, column nv*nj + 3j + c;
 // groups of 2 k-steps x RB blocks (slot float 2 rb + t)
 std::vector<float> pack_upart(const float* Wt, int n_out, int ld, int nj, int njh2, int mr) {
@@ -394,6 +479,18 @@ static int pack_net(const anerf_model_desc* d, int njh2, const anerf_net_weights
         offs.push_back(pk.add(pack_upart_x6(w->pts_w[skl], W, cin + W, nj, njh2, mr)));
     else
         offs.push_back((size_t)-1);
+    for (int i = 1; i < d->net_depth; ++i) {                                          // fp16x3 hidden layers
+        const bool sk = (i == d->skip + 1);
+        const int ld = sk ? cin + W : W, c0 = sk ? cin : 0;
+        const int ew = h3_exponent(w->pts_w[i], W, ld, c0, W);
+        offs.push_back((size_t)(int64_t)ew);  // (exponent, read back by bind_net)
+        offs.push_back(pk.add(pack_layer_h3(w->pts_w[i], W, ld, c0, W, ew)));
+    }
+    {
+        const int ew = h3_exponent(wfused.data(), WH, W, 0, W);
+        offs.push_back((size_t)(int64_t)ew);
+        offs.push_back(pk.add(pack_layer_h3(wfused.data(), WH, W, 0, W, ew)));     // wviewh
+    }
     return ANERF_OK;
 }
 
@@ -426,6 +523,12 @@ static void bind_net(const anerf_model_desc* d, const float* base, const std::ve
     nd.wu6 = base + o[k++];
     nd.wskipu6 = o[k] == (size_t)-1 ? nullptr : base + o[k];
     ++k;
+    for (int i = 1; i < D; ++i) {
+        nd.ewl[i] = (int)(int64_t)o[k++];
+        nd.wlh[i] = base + o[k++];
+    }
+    nd.ew_view = (int)(int64_t)o[k++];
+    nd.wviewh = base + o[k++];
     nd.balpha = balpha;
 }
 

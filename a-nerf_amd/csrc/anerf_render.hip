@@ -125,6 +125,7 @@ int anerf_model_create(const anerf_model_desc* desc, const anerf_net_weights* co
         md.ux6 = !(e && e[0] == '0');
     }
     md.single_net = desc->single_net ? 1 : 0;
+    md.h3_top = 127 + h3_target();
     md.shift = desc->softplus_shift;
     md.B = desc->density_scale;
     md.tau = embed->tau;
@@ -238,7 +239,7 @@ int anerf_render_rays(const anerf_model* m, const float* ray_batch, int32_t ray_
     if (!m) return fail(ANERF_EINVAL, "model is NULL");
     if (n_rays < 0) return fail(ANERF_EINVAL, "n_rays < 0");
     if (n_rays == 0) return ANERF_OK;
-    if (precision != ANERF_PREC_FP32 && precision != ANERF_PREC_BF16X3 && precision != ANERF_PREC_BF16X6) return fail(ANERF_EINVAL, "unsupported precision");
+    if (precision < ANERF_PREC_FP32 || precision > ANERF_PREC_FP16X3) return fail(ANERF_EINVAL, "unsupported precision");
     if (!ray_batch || ray_stride < 8 || !skts || !cyls || n_poses < 1 || !rgb || !disp || !acc)
         return fail(ANERF_EINVAL, "anerf_render_rays: bad arguments");
     if (n_samples < 2 || n_samples > 1024 || n_importance < 0 || n_importance > 2048)
@@ -323,7 +324,8 @@ int anerf_render_rays(const anerf_model* m, const float* ray_batch, int32_t ray_
 #define ANERF_LAUNCH(WW, MM)                                                                         \
     do {                                                                                            \
         auto kfn = precision == ANERF_PREC_BF16X3 ? render_kernel<WW, MM, 1>                       \
-                 : precision == ANERF_PREC_BF16X6 ? render_kernel<WW, MM, 2> : render_kernel<WW, MM, 0>; \
+                 : precision == ANERF_PREC_BF16X6 ? render_kernel<WW, MM, 2>                       \
+                 : precision == ANERF_PREC_FP16X3 ? render_kernel<WW, MM, 3> : render_kernel<WW, MM, 0>; \
         HIP_TRY(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,  \
                                     (int)lds_bytes));                                               \
         for (int p0 = 0; p0 < 2; p0 += pstep) {                                                     \
@@ -529,8 +531,7 @@ int anerf_train_importance(const float* z, const float* weights, int64_t n_rays,
 }
 
 static int launch_density(const anerf_model* m, DensityArgs a, int32_t precision, void* stream) {
-    if (precision != ANERF_PREC_FP32 && precision != ANERF_PREC_BF16X3 && precision != ANERF_PREC_BF16X6)
-        return fail(ANERF_EINVAL, "unsupported precision");
+    if (precision < ANERF_PREC_FP32 || precision > ANERF_PREC_FP16X3) return fail(ANERF_EINVAL, "unsupported precision");
     if (a.n == 0) return ANERF_OK;
     int dev = -1;
     HIP_TRY(hipGetDevice(&dev));
@@ -548,7 +549,8 @@ static int launch_density(const anerf_model* m, DensityArgs a, int32_t precision
 #define ANERF_LAUNCH(WW, MM)                                                                         \
     do {                                                                                            \
         auto kfn = precision == ANERF_PREC_BF16X3 ? density_kernel<WW, MM, 1>                      \
-                 : precision == ANERF_PREC_BF16X6 ? density_kernel<WW, MM, 2> : density_kernel<WW, MM, 0>; \
+                 : precision == ANERF_PREC_BF16X6 ? density_kernel<WW, MM, 2>                      \
+                 : precision == ANERF_PREC_FP16X3 ? density_kernel<WW, MM, 3> : density_kernel<WW, MM, 0>; \
         HIP_TRY(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,  \
                                     (int)lds_bytes));                                               \
         hipLaunchKernelGGL(kfn, dim3(grid), dim3(256), lds_bytes, st, m->md, a, P);                \

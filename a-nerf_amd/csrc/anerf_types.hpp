@@ -59,6 +59,9 @@ struct NetDev {
     const float* wview6;     // wview as bf16x6 fragments
     const float* wu6;        // layer 0 bone-direction part as bf16x6 fragments (pack_upart_x6)
     const float* wskipu6;    // the skip layer's, or null
+    const float* wlh[MAXL];  // [i>0] activation parts as fp16x3 fragments (pack_layer_h3), scaled by 2^ewl[i]
+    const float* wviewh;     // wview as fp16x3 fragments, scaled by 2^ew_view
+    int ewl[MAXL], ew_view;
     float balpha;
 };
 
@@ -67,6 +70,7 @@ struct ModelDev {
     int sparse;  // windowed features are exactly 0 where w == 0 (use_cutoff && cutoff_inputs)
     int ux6;     // bf16x6: bone-direction parts as x6 from the LDS feature store (u_part_x6)
     int single_net;  // one network for both passes; the fine pass evaluates only the I new samples
+    int h3_top;      // fp16x3: biased exponent the largest scaled activation of a sample gets (127 + 10)
     float shift, B, tau, tau_v;
     const float* cutoff;
     const float* cutoff_v;

@@ -47,6 +47,10 @@ DTYPE = {
     "fp32": "fp32",
     "bf16x6": "fp32-accurate split bf16 (hidden + view layers: x = x0+x1+x2, W = W0+W1+W2, six bf16 MFMA "
               "products per term, fp32 accumulate; encoder, layer 0, compositing fp32)",
+    "fp16x3": "fp32-class split fp16 (hidden + view layers: exact power-of-two scaling per layer (weights) and per "
+              "sample (activations), x = x0+x1, W = W0+W1 in fp16 (22 significant bits each), three fp16 MFMA "
+              "products, fp32 accumulate; bone-direction parts bf16x6; encoder, layer 0 windowed part, compositing "
+              "fp32)",
     "bf16x3": "split bf16 (hidden layers: x = hi+lo, W = hi+lo, three bf16 MFMA products, fp32 accumulate; "
               "fp32 elsewhere)",
 }
@@ -71,9 +75,9 @@ def parse():
                     help="frames: one frame per rank (weak scaling, no collective); pixels: ONE frame per step "
                          "split into whole 4096-ray chunks across the ranks + an RCCL all-gather of the ray "
                          "outputs (strong scaling, BASELINE config 5's layout; the default at N > 1)")
-    ap.add_argument("--also", default="fp32,bf16x3",
+    ap.add_argument("--also", default="fp32,bf16x6,bf16x3",
                     help="other precision modes timed on the same frame afterwards (rank 0, N=1; '' = none)")
-    ap.add_argument("--precision", default="bf16x6", choices=["fp32", "bf16x6", "bf16x3"],
+    ap.add_argument("--precision", default="fp16x3", choices=["fp32", "bf16x6", "fp16x3", "bf16x3"],
                     help="MLP arithmetic (include/anerf.h ANERF_PREC_*)")
     return ap.parse_args()
 

@@ -334,10 +334,11 @@ def test_density_matches_oracle_both_nets_and_ragged():
     assert empty.shape == (0, 1)
 
 
-@pytest.mark.parametrize("precision", ["bf16x6", "bf16x3"])
+@pytest.mark.parametrize("precision", ["bf16x6", "fp16x3", "bf16x3"])
 def test_density_split_precisions(precision):
-    """Density queries in the split-bf16 modes: the reference goldens within 1e-4 and the fp32 path
-    within 2e-6 (bf16x6, fp32-accurate products) / 5e-5 (bf16x3) on the config-3 fine net."""
+    """Density queries in the split modes: the reference goldens within 1e-4 and the fp32 path
+    within 2e-6 (bf16x6, fp32-accurate products; fp16x3, 22-bit operands) / 5e-5 (bf16x3) on the
+    config-3 fine net."""
     import dataclasses
     g = Golden("dm_fine_d8w256")
     rc = anerf.RayCaster(dataclasses.replace(g.cfg, precision=precision), g.ckpt)
@@ -347,7 +348,7 @@ def test_density_split_precisions(precision):
     out = rc(*args, render_kwargs={}, fwd_type="density").cpu().numpy()
     out32 = rc32(*args, render_kwargs={}, fwd_type="density").cpu().numpy()
     assert _maxdiff(out, g["pts_density"]) <= TOL_DENSITY
-    assert _maxdiff(out, out32) <= (2e-6 if precision == "bf16x6" else 5e-5)
+    assert _maxdiff(out, out32) <= (5e-5 if precision == "bf16x3" else 2e-6)
     grid = rc(kps=torch.from_numpy(g["kps"]), skts=torch.from_numpy(g["skts"]), bones=torch.from_numpy(g["bones"]),
               radius=g.meta["radius"], res=g.meta["res"], render_kwargs={}, netchunk=1024, fwd_type="mesh")
     assert _maxdiff(grid.cpu().numpy(), g["grid_density"]) <= TOL_DENSITY
@@ -428,38 +429,41 @@ def test_render_rays_bf16x3_matches_reference_golden(name):
             assert np.quantile(dd, 0.999) <= 2e-5, f"{name} {k}: bf16x3 vs fp32"
 
 
+@pytest.mark.parametrize("precision", ["bf16x6", "fp16x3"])
 @pytest.mark.parametrize("name", NAMES)
-def test_render_rays_bf16x6_matches_reference_golden(name):
-    """ANERF_PREC_BF16X6 (three-way split-bf16 hidden layers, fp32-accurate products) meets the 1e-4
-    bar against the reference and agrees with the fp32 path to fp32 summation-order level (99.9 % of
-    the composited outputs within 1e-5: the fixtures' largest outputs go through sigmoid/exp of raw
-    values ~10, where a 1-ulp difference of a layer sum becomes a few e-6)."""
+def test_render_rays_split_matches_reference_golden(name, precision):
+    """ANERF_PREC_BF16X6 (three-way split-bf16 hidden layers, fp32-accurate products) and
+    ANERF_PREC_FP16X3 (scaled two-way split-fp16, 22-bit operands) meet the 1e-4 bar against the
+    reference and agree with the fp32 path to fp32 summation-order level (99.9 % of the composited
+    outputs within 1e-5: the fixtures' largest outputs go through sigmoid/exp of raw values ~10,
+    where a 1-ulp difference of a layer sum becomes a few e-6)."""
     g = Golden(name)
     cams = g["cams"] if g.has("cams") else None
-    out = _render(_caster_prec(g, "bf16x6"), g, g.ray_batch(), cams=cams)
+    out = _render(_caster_prec(g, precision), g, g.ray_batch(), cams=cams)
     out32 = _render(_caster(g), g, g.ray_batch(), cams=cams)
     for k in ("rgb_map", "disp_map", "acc_map", "rgb0", "disp0", "acc0"):
         if g.has("out_" + k):
             d = _maxdiff(out[k], g["out_" + k])
-            assert d <= TOL, f"{name} {k}: max |gpu bf16x6 - reference| = {d:.3e}"
+            assert d <= TOL, f"{name} {k}: max |gpu {precision} - reference| = {d:.3e}"
             dd = np.abs(np.asarray(out[k], np.float64) - np.asarray(out32[k], np.float64)).ravel()
-            assert np.quantile(dd, 0.999) <= 1e-5, f"{name} {k}: bf16x6 vs fp32 {np.quantile(dd, 0.999):.3e}"
+            assert np.quantile(dd, 0.999) <= 1e-5, f"{name} {k}: {precision} vs fp32 {np.quantile(dd, 0.999):.3e}"
 
 
-def test_bf16x6_executes_bf16_mfmas():
+@pytest.mark.parametrize("precision,per_block", [("bf16x6", 12), ("fp16x3", 6)])
+def test_split_modes_execute_16bit_mfmas(precision, per_block):
     g = Golden("c3_512_s64i128_d8w256")
-    rc = _caster_prec(g, "bf16x6")
+    rc = _caster_prec(g, precision)
     _render(rc, g, g.ray_batch()[:64], count_mfma=True)
     n_f32, n_bf16 = (int(v) for v in rc.last_mfma.tolist())
     rc32 = _caster(g)
     _render(rc32, g, g.ray_batch()[:64], count_mfma=True)
     f32_only = int(rc32.last_mfma[0].item())
     # per 32-sample block (W 256: RB 8, RBV 4, 7 hidden layers, NJH2 12, skip layer present):
-    #   hidden 32x32 blocks: 16 f32 MFMAs (k = 2) -> 12 bf16 (2 k16-steps x 6)
-    #   fused view layer (128 x 256): 64 x 4 f32 -> 4 x 8 x 12 bf16
-    #   two bone-direction x parts (36 features): 36 x 8 f32 -> ceil(36 / 8) x 8 x 6 bf16 each
+    #   hidden 32x32 blocks: 16 f32 MFMAs (k = 2) -> 2 k16-steps x 6 (bf16x6) or x 3 (fp16x3)
+    #   fused view layer (128 x 256): 64 x 4 f32 -> 4 x 8 x per_block
+    #   two bone-direction x parts (36 features, bf16x6 in both modes): 36 x 8 f32 -> ceil(36 / 8) x 8 x 6
     f32_removed = 7 * 64 * 16 + 128 * 4 + 2 * 36 * 8
-    bf16_added = 7 * 64 * 12 + 4 * 8 * 12 + 2 * 5 * 8 * 6
+    bf16_added = 7 * 64 * per_block + 4 * 8 * per_block + 2 * 5 * 8 * 6
     assert n_bf16 > 0 and (f32_only - n_f32) * bf16_added == n_bf16 * f32_removed
 
 

@@ -57,15 +57,22 @@ def lin_bf16x6(x, w, b=None):
 
 
 def _pow2_scale(a, dim=None):
-    """Power-of-2 factor putting max|a| (per row when dim is given) into [2^14, 2^15): fp16 range."""
+    """Power-of-2 factor putting max|a| (per row when dim is given) into [2^10, 2^11), as the kernel."""
     m = a.abs().amax(dim=dim, keepdim=True) if dim is not None else a.abs().max()
     e = torch.floor(torch.log2(torch.where(m > 0, m, torch.ones_like(m))))
-    return torch.exp2(14.0 - e)
+    return torch.exp2(10.0 - e)
+
+
+def _ftz16(h):
+    """fp16 with subnormals flushed to zero (ANERF_FTZ16=1: what an MFMA that flushes f16 inputs sees)."""
+    if os.environ.get("ANERF_FTZ16") == "1":
+        h = torch.where(h.abs() < 2.0 ** -14, torch.zeros_like(h), h)
+    return h
 
 
 def _split16(x):
-    hi = x.half().float()
-    lo = (x - hi).half().float()
+    hi = _ftz16(x.half()).float()
+    lo = _ftz16((x - hi).half()).float()
     return hi, lo
 
 
