@@ -476,7 +476,7 @@ __device__ __forceinline__ void mlp_layer_h3(f32x16 (&out)[RBO], f32x16 (&ain)[R
     static_assert(RBO <= RBI, "h3 layer shape");
     constexpr int NG = 2 * RBO * RBI;
     constexpr int NS = NG / 2;  // ring slots of this layer
-    constexpr int PS = 3;       // prefetch distance (slots)
+    constexpr int PS = 2;       // prefetch distance (slots)
     constexpr int NQ = 2 * RBO;  // groups per input block
     const int hh = lane >> 5;
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(wp);

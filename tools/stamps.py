@@ -12,7 +12,7 @@ import torch
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 _lib = importlib.import_module("a-nerf_amd._lib")
-_lib.LIB_PATH = os.path.join(REPO, "tools", os.environ.get("ANERF_STAMPS_LIB", "libanerf_hip_stamps.so"))
+_lib.LIB_PATH = os.path.join(REPO, "tools", os.environ.get("ANERF_STAMPS_LIB", "ab/libanerf_hip_stamps.so"))
 anerf = importlib.import_module("a-nerf_amd")
 syn = importlib.import_module("a-nerf_amd.synthetic")
 NAMES = {0: "prologue", 1: "view factor G (G + bias column)", 7: "  view factor: bias staging + trig table", 2: "MLP coarse", 3: "composite+importance", 4: "MLP fine",
