@@ -22,6 +22,7 @@ ANERF_PREC_FP32 = 0
 ANERF_PREC_BF16X3 = 1
 ANERF_PREC_BF16X6 = 2
 ANERF_PREC_FP16X3 = 3
+ANERF_FLAG_LINDISP = 0x100  # OR-ed into the precision argument (include/anerf.h)
 PRECISIONS = {"fp32": ANERF_PREC_FP32, "bf16x3": ANERF_PREC_BF16X3, "bf16x6": ANERF_PREC_BF16X6,
               "fp16x3": ANERF_PREC_FP16X3}
 
@@ -115,14 +116,14 @@ SIGNATURES = {
                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                        ctypes.c_void_p, ctypes.c_void_p]),
     "anerf_train_samples": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
-                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+                                           ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]),
     "anerf_train_encode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64,
                                           ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32,
-                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "anerf_train_encode_backward": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64,
                                                    ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32,
                                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                                                   ctypes.c_void_p]),
+                                                   ctypes.c_void_p, ctypes.c_void_p]),
     "anerf_train_composite": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                              ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p,
                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,

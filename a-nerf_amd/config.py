@@ -30,6 +30,7 @@ class RenderConfig:
     N_samples: int = 64
     N_importance: int = 0
     single_net: bool = False
+    lindisp: bool = False  # --lindisp: sample in inverse depth (render_kwargs['lindisp'], ray_utils.py:223-226)
     chunk: int = 4096
     ext_scale: float = 0.001
     # MLP arithmetic: "fp32" (fp32 MFMA everywhere, the parity default), "bf16x6" (hidden layers as
@@ -40,7 +41,11 @@ class RenderConfig:
 
     def validate(self):
         if not self.use_viewdirs:
-            raise NotImplementedError("use_viewdirs=False (output_linear head) is not implemented")
+            # (the reference itself cannot run this: create_raycaster leaves embeddirs_fn = None
+            # (core/raycasters.py:66-67) and encode_inputs calls it (:538) -> TypeError; recorded by
+            # tests/golden/probe_reference_flags.py in reference_flags.json)
+            raise NotImplementedError("use_viewdirs=False: the reference raises TypeError on this path "
+                                      "(core/raycasters.py:67, 538); not implemented")
         if self.multires_bones != 0:
             raise NotImplementedError("multires_bones > 0 is not implemented (configs use 0)")
         if len(self.skips) != 1 or self.skips[0] < 0:
@@ -106,6 +111,7 @@ class RenderConfig:
                   density_type=g("density_type", "relu"), softplus_shift=g("softplus_shift", 1.0),
                   density_scale=g("density_scale", 1.0), N_samples=g("N_samples", 64),
                   N_importance=g("N_importance", 0), single_net=bool(g("single_net", False)),
+                  lindisp=bool(g("lindisp", False)),
                   chunk=g("chunk", 4096), ext_scale=g("ext_scale", 0.001), extra=extra)
         return cfg.validate()
 

@@ -48,6 +48,14 @@ __device__ __forceinline__ float torch_linspace01(int i, int n) {
     return (i < n / 2) ? (float)((double)step * i) : (float)(1.0 - (double)step * (n - 1 - i));
 }
 
+// sample_from_lineseg's z at t (core/utils/ray_utils.py:223-226): near (1 - t) + far t, or with
+// lindisp 1 / (1/near (1 - t) + 1/far t) — torch's float32 operations in its order (correctly rounded
+// divisions; near = 0 gives inf and the IEEE results torch gives)
+__host__ __device__ __forceinline__ float lineseg_z(float nr, float fr, float t, bool lindisp) {
+    if (!lindisp) return nr * (1.0f - t) + fr * t;
+    return 1.0f / ((1.0f / nr) * (1.0f - t) + (1.0f / fr) * t);
+}
+
 __device__ __forceinline__ float norm3(float a, float b, float c) { return sqrtf(fmaf(c, c, fmaf(b, b, a * a))); }
 __device__ __forceinline__ float norm2(float a, float b) { return sqrtf(fmaf(b, b, a * a)); }
 // Branch-free sin/cos (ocml's sincosf branches to a Payne-Hanek path for large arguments, which

@@ -39,7 +39,7 @@ __global__ __launch_bounds__(256, 1) void render_kernel(ModelDev M, RenderArgs A
         const int r = idx / S, s = idx % S;
         const float t = torch_linspace01(s, S);
         const float nearv = lds[P.ray + 16 * r + 7], farv = lds[P.ray + 16 * r + 8];
-        lds[P.zc + P.z_stride * r + s] = nearv * (1.0f - t) + farv * t;
+        lds[P.zc + P.z_stride * r + s] = lineseg_z(nearv, farv, t, A.lindisp != 0);
     }
     if (A.pass0 == 1)  // fine-only launch: the sorted fine z of the coarse launch
         for (int idx = tid; idx < nr * T; idx += blockDim.x) {

@@ -239,6 +239,9 @@ int anerf_render_rays(const anerf_model* m, const float* ray_batch, int32_t ray_
     if (!m) return fail(ANERF_EINVAL, "model is NULL");
     if (n_rays < 0) return fail(ANERF_EINVAL, "n_rays < 0");
     if (n_rays == 0) return ANERF_OK;
+    const int flags = precision & ~0xff;  // ANERF_FLAG_* bits above the precision mode
+    precision &= 0xff;
+    if (flags & ~ANERF_FLAG_LINDISP) return fail(ANERF_EINVAL, "unknown flags in the precision argument");
     if (precision < ANERF_PREC_FP32 || precision > ANERF_PREC_FP16X3) return fail(ANERF_EINVAL, "unsupported precision");
     if (!ray_batch || ray_stride < 8 || !skts || !cyls || n_poses < 1 || !rgb || !disp || !acc)
         return fail(ANERF_EINVAL, "anerf_render_rays: bad arguments");
@@ -301,6 +304,7 @@ int anerf_render_rays(const anerf_model* m, const float* ray_batch, int32_t ray_
     a.acc0 = acc0;
     a.alpha = alpha;
     a.alpha0 = alpha0;
+    a.lindisp = (flags & ANERF_FLAG_LINDISP) ? 1 : 0;
     if (debug) {
         a.dbg_z0 = debug->z_coarse;
         a.dbg_raw0 = debug->raw_coarse;
@@ -427,13 +431,14 @@ int anerf_encode_points(const anerf_model* m, const float* skts, const float* pt
 static inline unsigned blocks_of(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 
 int anerf_train_samples(const float* near_in, const float* far_in, int64_t n_rays, int32_t n_samples,
-                        const float* t_rand, float* z_out, void* stream) {
+                        const float* t_rand, int32_t flags, float* z_out, void* stream) {
+    if (flags & ~ANERF_FLAG_LINDISP) return fail(ANERF_EINVAL, "anerf_train_samples: unknown flags");
     if (n_rays < 0 || n_samples < 2 || !near_in || !far_in || !z_out)
         return fail(ANERF_EINVAL, "anerf_train_samples: bad arguments");
     if (n_rays == 0) return ANERF_OK;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(train_z_kernel, dim3(blocks_of(n_rays * n_samples, 256)), dim3(256), 0, st, near_in, far_in,
-                       n_rays, n_samples, t_rand, z_out);
+                       n_rays, n_samples, t_rand, (flags & ANERF_FLAG_LINDISP) ? 1 : 0, z_out);
     HIP_TRY(hipGetLastError());
     return ANERF_OK;
 }
@@ -450,7 +455,7 @@ static int check_train_rays(const anerf_model* m, const float* ray_batch, int32_
 
 int anerf_train_encode(const anerf_model* m, const float* ray_batch, int32_t ray_stride, int64_t n_rays,
                        const float* z, int32_t n_samples, const float* skts, int32_t n_poses, const int32_t* ray_pose,
-                       float* feat_out, void* stream) {
+                       const float* pts_noise, float* feat_out, void* stream) {
     int rc = check_train_rays(m, ray_batch, ray_stride, n_rays, z, n_samples, skts, n_poses, ray_pose);
     if (rc) return rc;
     if (!feat_out) return fail(ANERF_EINVAL, "anerf_train_encode: feat_out is NULL");
@@ -458,14 +463,15 @@ int anerf_train_encode(const anerf_model* m, const float* ray_batch, int32_t ray
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(train_encode_kernel, dim3(blocks_of(n_rays * n_samples * m->desc.n_joints, 256)), dim3(256), 0,
                        st, m->md,
-                       ray_batch, ray_stride, n_rays, z, n_samples, skts, ray_pose, n_poses, feat_out);
+                       ray_batch, ray_stride, n_rays, z, n_samples, skts, ray_pose, n_poses, pts_noise, feat_out);
     HIP_TRY(hipGetLastError());
     return ANERF_OK;
 }
 
 int anerf_train_encode_backward(const anerf_model* m, const float* ray_batch, int32_t ray_stride, int64_t n_rays,
                                 const float* z, int32_t n_samples, const float* skts, int32_t n_poses,
-                                const int32_t* ray_pose, const float* grad_feat, float* grad_skts, void* stream) {
+                                const int32_t* ray_pose, const float* pts_noise, const float* grad_feat,
+                                float* grad_skts, void* stream) {
     int rc = check_train_rays(m, ray_batch, ray_stride, n_rays, z, n_samples, skts, n_poses, ray_pose);
     if (rc) return rc;
     if (!grad_feat || !grad_skts) return fail(ANERF_EINVAL, "anerf_train_encode_backward: NULL gradient");
@@ -474,7 +480,7 @@ int anerf_train_encode_backward(const anerf_model* m, const float* ray_batch, in
     if (nb > 0x7fffffff) return fail(ANERF_EINVAL, "too many rays for one launch");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(train_encode_backward_kernel, dim3((unsigned)nb), dim3(256), 0, st, m->md, ray_batch,
-                       ray_stride, n_rays, z, n_samples, skts, ray_pose, n_poses, grad_feat, grad_skts);
+                       ray_stride, n_rays, z, n_samples, skts, ray_pose, n_poses, pts_noise, grad_feat, grad_skts);
     HIP_TRY(hipGetLastError());
     return ANERF_OK;
 }

@@ -10,15 +10,14 @@
 // near and far, then lower + (upper - lower) * t_rand inside the mid-point intervals.  t_rand NULL:
 // the deterministic samples (perturb = 0).  One thread per sample.
 __global__ void train_z_kernel(const float* __restrict__ nearp, const float* __restrict__ farp, int64_t n, int S,
-                               const float* __restrict__ t_rand, float* __restrict__ z) {
+                               const float* __restrict__ t_rand, int lindisp, float* __restrict__ z) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= n * S) return;
     const int64_t i = idx / S;
     const int s = (int)(idx % S);
     const float nr = nearp[i], fr = farp[i];
     auto zl = [&](int k) {
-        const float t = torch_linspace01(k, S);
-        return nr * (1.0f - t) + fr * t;
+        return lineseg_z(nr, fr, torch_linspace01(k, S), lindisp != 0);
     };
     const float zs = zl(s);
     float zv = zs;
@@ -71,7 +70,8 @@ __device__ __forceinline__ void encode_joint(const ModelDev& M, const float* __r
 
 __global__ void train_encode_kernel(ModelDev M, const float* __restrict__ rb, int stride, int64_t n,
                                     const float* __restrict__ z, int ns, const float* __restrict__ skts,
-                                    const int32_t* __restrict__ ray_pose, int n_poses, float* __restrict__ feat) {
+                                    const int32_t* __restrict__ ray_pose, int n_poses,
+                                    const float* __restrict__ pts_noise, float* __restrict__ feat) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int nj = M.nj;
     if (t >= n * ns * nj) return;
@@ -81,7 +81,10 @@ __global__ void train_encode_kernel(ModelDev M, const float* __restrict__ rb, in
     const int64_t pose = ray_pose ? ray_pose[i] : i;
     const float* ray = rb + i * stride;
     const float zz = z[idx];
-    const float px = ray[0] + ray[3] * zz, py = ray[1] + ray[4] * zz, pz = ray[2] + ray[5] * zz;
+    float px = ray[0] + ray[3] * zz, py = ray[1] + ray[4] * zz, pz = ray[2] + ray[5] * zz;
+    if (pts_noise) {  // sample_pts' ray_noise_std (raycasters.py:660-661): pts + randn * std
+        px += pts_noise[3 * idx], py += pts_noise[3 * idx + 1], pz += pts_noise[3 * idx + 2];
+    }
     const int F = nj * (1 + 2 * M.mr) + 3 * nj + 3 * nj * (1 + 2 * M.mrv);
     f32x4 r0, r1, r2;
     if (pose >= 0 && pose < n_poses) {
@@ -208,6 +211,7 @@ __global__ __launch_bounds__(256) void train_encode_backward_kernel(ModelDev M, 
                                                                     int stride, int64_t n, const float* __restrict__ z,
                                                                     int ns, const float* __restrict__ skts,
                                                                     const int32_t* __restrict__ ray_pose, int n_poses,
+                                                                    const float* __restrict__ pts_noise,
                                                                     const float* __restrict__ gfeat,
                                                                     float* __restrict__ gskts) {
     __shared__ float red[4][4][12];
@@ -229,7 +233,11 @@ __global__ __launch_bounds__(256) void train_encode_backward_kernel(ModelDev M, 
         const float S[12] = {r0[0], r0[1], r0[2], r0[3], r1[0], r1[1], r1[2], r1[3], r2[0], r2[1], r2[2], r2[3]};
         for (int s = wave * 16 + (lane >> 2); s < ns; s += 64) {
             const float zz = z[i * ns + s];
-            const float px = ray[0] + ray[3] * zz, py = ray[1] + ray[4] * zz, pz = ray[2] + ray[5] * zz;
+            float px = ray[0] + ray[3] * zz, py = ray[1] + ray[4] * zz, pz = ray[2] + ray[5] * zz;
+            if (pts_noise) {
+                const float* q = pts_noise + 3 * (i * ns + s);
+                px += q[0], py += q[1], pz += q[2];
+            }
             encode_row_grad_joint(M, S, j, px, py, pz, ray[3], ray[4], ray[5], gfeat + (i * ns + s) * F, gS);
         }
     }

@@ -93,6 +93,7 @@ struct RenderArgs {
     unsigned long long* stamps;
     int pass0, pass1;  // passes [pass0, pass1) of this launch (0 coarse, 1 fine)
     float* zf_ws;      // n x T: the fine pass's sorted z, handed from the coarse launch to the fine one
+    int lindisp;       // sample_from_lineseg in inverse depth (ANERF_FLAG_LINDISP)
 };
 
 // ======================================================================= LDS plan

@@ -5,8 +5,8 @@ dict of `_collect_outputs`, :711-724) and the model factory `create_raycaster`
 (:17-184).  `render_rays` keeps the reference signature; what the reference does in a
 dozen ATen ops per stage happens in one fused launch (`anerf_render_rays`).
 
-Supported: eval-mode rendering (`perturb=0`, `raw_noise_std=0`, `ray_noise_std=0`,
-`lindisp=False`), any per-ray poses (`skts`/`cyls` may be expanded views of one pose —
+Supported: eval-mode rendering (`perturb=0`, `raw_noise_std=0`, `ray_noise_std=0`; `lindisp`
+either way), any per-ray poses (`skts`/`cyls` may be expanded views of one pose —
 detected without copying — or genuinely per-ray), framecodes via `cams`; density-only
 queries `fwd_type='density'` / `'mesh'` (`render_pts_density` / `render_mesh_density`,
 :579-648).  Anything else raises `NotImplementedError`; nothing silently falls back to the CPU.
@@ -146,8 +146,6 @@ class RayCaster:
         i.e. per batchify chunk, so the default is the whole batch."""
         if perturb or raw_noise_std or ray_noise_std:
             raise NotImplementedError("stochastic sampling / noise (training mode) is not implemented")
-        if lindisp:
-            raise NotImplementedError("lindisp sampling is not implemented")
         if subject_idxs is not None:
             raise NotImplementedError("multi-subject rendering (subject_idxs) is not implemented")
         if preproc_kwargs:
@@ -207,7 +205,7 @@ class RayCaster:
         rc = _lib.load().anerf_render_rays(
             self.model.handle, _lib.ptr(rb), rb.shape[1], n, _lib.ptr(skt_tab), _lib.ptr(cyl_tab),
             skt_tab.shape[0], _lib.ptr(pose), _lib.ptr(cam_t), S, I, int(chunk or max(n, 1)),
-            _lib.PRECISIONS[self.cfg.precision],
+            _lib.PRECISIONS[self.cfg.precision] | (_lib.ANERF_FLAG_LINDISP if lindisp else 0),
             _lib.ptr(out["rgb_map"]), _lib.ptr(out["disp_map"]), _lib.ptr(out["acc_map"]),
             _lib.ptr(out.get("rgb0")), _lib.ptr(out.get("disp0")), _lib.ptr(out.get("acc0")),
             _lib.ptr(out["alpha"]), _lib.ptr(out.get("alpha0")), ctypes.byref(dbg) if dbg else None,
@@ -275,7 +273,7 @@ def create_raycaster(args, data_attrs, device=None, ckpt=None):
         optimizer.load_state_dict(ckpt["optimizer_state_dict"])
     common = {"N_importance": cfg.N_importance, "N_samples": cfg.N_samples, "use_viewdirs": cfg.use_viewdirs,
               "ext_scale": cfg.ext_scale, "preproc_kwargs": {"density_scale": cfg.density_scale},
-              "lindisp": False, "nerf_type": getattr(args, "nerf_type", "nerf")}
+              "lindisp": cfg.lindisp, "nerf_type": getattr(args, "nerf_type", "nerf")}
     render_kwargs_train = {"ray_caster": caster, "perturb": getattr(args, "perturb", 1.0),
                            "raw_noise_std": getattr(args, "raw_noise_std", 0.0),
                            "ray_noise_std": getattr(args, "ray_noise_std", 0.0), **common}

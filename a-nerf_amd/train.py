@@ -11,8 +11,9 @@ concatenations (`cat([x, h])` at the skip, `cat([feature, views(, code)])` at th
 replaced by split weight blocks, so no concatenated activation is ever materialised.
 
 Random numbers: torch's generator on the device by default; pass `rand={"t_rand": (N,S),
-"noise0": (N,S), "u": (N,I), "noise1": (N,S+I)}` (standard-uniform / standard-normal draws) to
-reproduce a given draw — the parity tests feed the reference's.
+"noise0": (N,S), "u": (N,I), "noise1": (N,S+I)}` (standard-uniform / standard-normal draws; with
+ray_noise_std also "pts_noise0": (N,S,3), "pts_noise1": (N,I,3)) to reproduce a given draw — the
+parity tests feed the reference's.
 """
 import torch
 import torch.nn as nn
@@ -32,33 +33,36 @@ class _Encode(torch.autograd.Function):
     """encode_inputs of every sample (raycasters.py:476-555): features [N*S, F]; backward -> dL/dskts."""
 
     @staticmethod
-    def forward(ctx, skts, model, rb, z, ray_pose):
+    def forward(ctx, skts, model, rb, z, ray_pose, pts_noise=None):
         n, ns = z.shape
         cfg = model.cfg
         F_ = cfg.feature_dim
         feat = torch.empty(n * ns, F_, device=z.device, dtype=torch.float32)
         n_poses = skts.shape[0]
         _lib.check(_lib.load().anerf_train_encode(model.handle, _lib.ptr(rb), rb.shape[1], n, _lib.ptr(z), ns,
-                                                  _lib.ptr(skts), n_poses, _lib.ptr(ray_pose), _lib.ptr(feat),
-                                                  _stream(z.device)), "anerf_train_encode")
+                                                  _lib.ptr(skts), n_poses, _lib.ptr(ray_pose), _lib.ptr(pts_noise),
+                                                  _lib.ptr(feat), _stream(z.device)), "anerf_train_encode")
         ctx.model = model
-        ctx.save_for_backward(skts, rb, z, ray_pose if ray_pose is not None else torch.empty(0))
+        e = torch.empty(0)
+        ctx.save_for_backward(skts, rb, z, ray_pose if ray_pose is not None else e,
+                              pts_noise if pts_noise is not None else e)
         ctx.has_pose = ray_pose is not None
+        ctx.has_noise = pts_noise is not None
         return feat
 
     @staticmethod
     def backward(ctx, g_feat):
-        skts, rb, z, ray_pose = ctx.saved_tensors
+        skts, rb, z, ray_pose, pts_noise = ctx.saved_tensors
         if not ctx.needs_input_grad[0]:
-            return None, None, None, None, None
+            return None, None, None, None, None, None
         n, ns = z.shape
         g = torch.zeros_like(skts)
         gf = g_feat.contiguous()
         _lib.check(_lib.load().anerf_train_encode_backward(
             ctx.model.handle, _lib.ptr(rb), rb.shape[1], n, _lib.ptr(z), ns, _lib.ptr(skts), skts.shape[0],
-            _lib.ptr(ray_pose if ctx.has_pose else None), _lib.ptr(gf), _lib.ptr(g), _stream(z.device)),
-            "anerf_train_encode_backward")
-        return g, None, None, None, None
+            _lib.ptr(ray_pose if ctx.has_pose else None), _lib.ptr(pts_noise if ctx.has_noise else None),
+            _lib.ptr(gf), _lib.ptr(g), _stream(z.device)), "anerf_train_encode_backward")
+        return g, None, None, None, None, None
 
 
 class _Composite(torch.autograd.Function):
@@ -456,10 +460,6 @@ class TrainRayCaster(nn.Module):
                     preproc_kwargs=None, nerf_type="nerf", rand=None, chunk=None):
         """core/raycasters.py:361-474 with autograd: gradients reach the networks' parameters and
         `skts` (when it requires grad).  `rand` overrides the random draws (module docstring)."""
-        if lindisp:
-            raise NotImplementedError("lindisp sampling is not implemented")
-        if ray_noise_std:
-            raise NotImplementedError("ray_noise_std > 0 is not implemented")
         if subject_idxs is not None:
             raise NotImplementedError("multi-subject training (subject_idxs) is not implemented")
         if skts is None or cyls is None:
@@ -499,7 +499,8 @@ class TrainRayCaster(nn.Module):
         t_rand = t_rand.to(dev, torch.float32).contiguous() if stochastic else None
         z = torch.empty(n, S, device=dev, dtype=torch.float32)
         _lib.check(_lib.load().anerf_train_samples(_lib.ptr(nearv), _lib.ptr(farv), n, S, _lib.ptr(t_rand),
-                                                   _lib.ptr(z), _stream(dev)), "anerf_train_samples")
+                                                   _lib.ANERF_FLAG_LINDISP if lindisp else 0, _lib.ptr(z),
+                                                   _stream(dev)), "anerf_train_samples")
         cam_t = None
         if cfg.opt_framecode:
             if cams is None:
@@ -513,15 +514,24 @@ class TrainRayCaster(nn.Module):
             g = torch.randn(n, ns, device=dev) if g is None else g.to(dev, torch.float32)
             return (g * raw_noise_std * B).contiguous()
 
-        def raw_of(net, zz):
+        def pts_noise_for(key, ns):
+            """sample_pts / sample_pts_is' `randn_like(pts) * ray_noise_std` (raycasters.py:660-661, 673-674)."""
+            if ray_noise_std <= 0:
+                return None
+            g = rand.get(key)
+            g = torch.randn(n, ns, 3, device=dev) if g is None else g.to(dev, torch.float32)
+            return (g * ray_noise_std).contiguous()
+
+        def raw_of(net, zz, pn=None):
             ns = zz.shape[1]
-            feat = _Encode.apply(sk, model, rb, zz, None)
+            feat = _Encode.apply(sk, model, rb, zz, None, pn)
             return net(feat, None if cam_t is None else cam_t.repeat_interleave(ns)).reshape(n, ns, 4)
 
         def composite(raw, zz, noise):
             return _Composite.apply(raw, model, zz, rb, noise)
 
-        raw0 = raw_of(self.network_fn, z)
+        pn0 = pts_noise_for("pts_noise0", S)
+        raw0 = raw_of(self.network_fn, z, pn0)
         rgb, disp, acc, w, a = composite(raw0, z, noise_for("noise0", S))
         out = {"rgb_map": rgb, "disp_map": disp, "acc_map": acc, "alpha": a}
         if I > 0:
@@ -530,20 +540,28 @@ class TrainRayCaster(nn.Module):
                 u = torch.rand(n, I, device=dev)
             u = u.to(dev, torch.float32).contiguous() if stochastic else None
             z_all = torch.empty(n, S + I, device=dev, dtype=torch.float32)
-            sidx = torch.empty(n, S + I, device=dev, dtype=torch.int32) if cfg.single_net else None
+            want_idx = cfg.single_net or pn0 is not None
+            sidx = torch.empty(n, S + I, device=dev, dtype=torch.int32) if want_idx else None
             wd = w.detach().contiguous()
             _lib.check(_lib.load().anerf_train_importance(_lib.ptr(z), _lib.ptr(wd), n, S, I, _lib.ptr(u),
                                                           int(cfg.single_net), _lib.ptr(z_all), _lib.ptr(sidx),
                                                           _stream(dev)), "anerf_train_importance")
+            # the new samples' points get their own ray noise; the merged coarse samples keep theirs
+            # (the reference merges the coarse encodings, raycasters.py:456-466)
+            pn_is = pts_noise_for("pts_noise1", I)
             if cfg.single_net:
                 # raycasters.py:462-468: the one network on the I new samples only, then
                 # raw = cat([raw, raw_is])[sorted_idx] (gradients reach both through the gather)
                 si = sidx.long()
                 z_is = torch.empty_like(z_all).scatter_(1, si, z_all)[:, S:].contiguous()
-                raw_cat = torch.cat([raw0, raw_of(self.network_fn, z_is)], 1)
+                raw_cat = torch.cat([raw0, raw_of(self.network_fn, z_is, pn_is)], 1)
                 raw1 = torch.gather(raw_cat, 1, si[..., None].expand(-1, -1, 4))
             else:
-                raw1 = raw_of(self.network_fine, z_all)
+                pn1 = None
+                if pn0 is not None:
+                    pn1 = torch.gather(torch.cat([pn0, pn_is], 1), 1,
+                                       sidx.long()[..., None].expand(-1, -1, 3)).contiguous()
+                raw1 = raw_of(self.network_fine, z_all, pn1)
             rgb1, disp1, acc1, w1, a1 = composite(raw1, z_all, noise_for("noise1", S + I))
             out = {"rgb_map": rgb1, "disp_map": disp1, "acc_map": acc1, "alpha": a1,
                    "rgb0": rgb, "disp0": disp, "acc0": acc, "alpha0": a}

@@ -76,6 +76,10 @@ enum {
  *                     the dropped x1 w1 ~2^-22 of |x w|): half of bf16x6's MFMAs at comparable accuracy;
  *                     bone-direction parts as in bf16x6; encoder, layer 0's windowed part and heads fp32. */
 enum { ANERF_PREC_FP32 = 0, ANERF_PREC_BF16X3 = 1, ANERF_PREC_BF16X6 = 2, ANERF_PREC_FP16X3 = 3 };
+/* Flags OR-ed into anerf_render_rays' precision argument (and anerf_train_samples' flags):
+ *   ANERF_FLAG_LINDISP  sample linearly in inverse depth, z = 1 / (1/near (1 - t) + 1/far t)
+ *                       (render_rays(lindisp=True), core/utils/ray_utils.py:223-226) */
+enum { ANERF_FLAG_LINDISP = 0x100 };
 
 typedef struct anerf_model anerf_model;
 
@@ -290,22 +294,25 @@ int anerf_ray_batch(const uint8_t* imgs, const uint8_t* masks, const uint8_t* bg
 /* z [N][S] of sample_from_lineseg: linspace(near, far) (torch.linspace's float32 values), then with
  * t_rand [N][S] (NULL: perturb = 0) lower + (upper - lower) t_rand inside the mid-point intervals. */
 int anerf_train_samples(const float* near_in, const float* far_in, int64_t n_rays, int32_t n_samples,
-                        const float* t_rand, float* z_out, void* stream);
+                        const float* t_rand, int32_t flags /* ANERF_FLAG_LINDISP or 0 */, float* z_out,
+                        void* stream);
 
 /* Features feat_out [N][S][F] (the layout of anerf_encode_points) of the points o + d z of the rays
  * ray_batch [N][ray_stride] (o = cols 0-2, d = cols 3-5) at z [N][S]; the rays' skeletons are
  * skts [n_poses][NJ][4][4] with ray_pose [N] (NULL: one skeleton per ray, n_poses == N).  A ray
  * whose ray_pose is outside [0, n_poses) gets NaN features (and no gradient in the backward); the
- * index is never dereferenced. */
+ * index is never dereferenced.  pts_noise [N][S][3] (NULL: none) is added to the points, sample_pts'
+ * `pts + randn_like(pts) * ray_noise_std` (core/raycasters.py:660-661): pass randn * ray_noise_std. */
 int anerf_train_encode(const anerf_model* m, const float* ray_batch, int32_t ray_stride, int64_t n_rays,
                        const float* z, int32_t n_samples, const float* skts, int32_t n_poses, const int32_t* ray_pose,
-                       float* feat_out, void* stream);
+                       const float* pts_noise, float* feat_out, void* stream);
 
-/* dL/dskts of anerf_train_encode given dL/dfeat [N][S][F], ACCUMULATED into grad_skts
+/* dL/dskts of anerf_train_encode (same z and pts_noise) given dL/dfeat [N][S][F], ACCUMULATED into grad_skts
  * [n_poses][NJ][4][4] (row 3 of every transform untouched; the caller zeroes the buffer). */
 int anerf_train_encode_backward(const anerf_model* m, const float* ray_batch, int32_t ray_stride, int64_t n_rays,
                                 const float* z, int32_t n_samples, const float* skts, int32_t n_poses,
-                                const int32_t* ray_pose, const float* grad_feat, float* grad_skts, void* stream);
+                                const int32_t* ray_pose, const float* pts_noise, const float* grad_feat,
+                                float* grad_skts, void* stream);
 
 /* raw2outputs of raw [N][S][4] at z [N][S] with noise [N][S] (= randn * raw_noise_std * B, added to
  * raw_sigma / B; NULL: none): rgb [N][3], disp [N], acc [N], weights, alpha and the exclusive

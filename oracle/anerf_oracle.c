@@ -52,6 +52,7 @@ typedef struct {
     const float* cutoff_v; /* embeddirs_fn.cutoff_dist (NJ) */
     int has_fine;
     int single_net; /* network_fine IS network_fn; fine pass on the I new samples only (raycasters.py:462-468) */
+    int lindisp;    /* sample_from_lineseg in inverse depth (ray_utils.py:223-226) */
     oracle_net coarse, fine;
 } oracle_model;
 
@@ -621,7 +622,9 @@ int oracle_render_rays(const oracle_model* m, const float* rb, int stride, int64
             const float* d = r + 3;
             const float* sk = skts + (size_t)16 * m->nj * (ray_pose ? ray_pose[i] : 0);
             /* sample_from_lineseg (ray_utils.py:218-229) */
-            for (int s = 0; s < S; ++s) z[s] = near[i] * (1.0f - tv[s]) + far[i] * tv[s];
+            for (int s = 0; s < S; ++s)
+                z[s] = m->lindisp ? 1.0f / ((1.0f / near[i]) * (1.0f - tv[s]) + (1.0f / far[i]) * tv[s])
+                                  : near[i] * (1.0f - tv[s]) + far[i] * tv[s];
             ray_code(m, &m->coarse, cams, i, code);
             float c_rgb[3], c_disp, c_acc;
             ray_pass(m, &m->coarse, o, d, sk, code, z, S, feat, raw, codes_rows, buf, c_rgb, &c_disp, &c_acc, w,

@@ -29,6 +29,7 @@ class _Model(ctypes.Structure):
                 ("density_softplus", ctypes.c_int), ("softplus_shift", ctypes.c_float),
                 ("density_scale", ctypes.c_float), ("tau", ctypes.c_float), ("tau_v", ctypes.c_float),
                 ("cutoff", _f), ("cutoff_v", _f), ("has_fine", ctypes.c_int), ("single_net", ctypes.c_int),
+                ("lindisp", ctypes.c_int),
                 ("coarse", _Net), ("fine", _Net)]
 
 
@@ -84,6 +85,7 @@ class OracleModel:
         if cfg.single_net:  # network_fine IS network_fn; load_state_dict loads the fine keys last
             coarse, fine = (fine if fine is not None else coarse), None
         m.single_net = int(cfg.single_net)
+        m.lindisp = int(cfg.lindisp)
         self._net(m.coarse, coarse)
         m.has_fine = int(fine is not None)
         if fine is not None:

@@ -18,7 +18,9 @@ NAMES = ["c1_64_s32_d4w128", "c2_256_s64_d8w256", "c3_512_s64i128_d8w256", "c4_5
          # distance input; no cutoff window at all
          "v1_mr10_w64_d4", "v2_softplus_nocutview", "v3_nocutinputs", "v4_nocutoff",
          # configs/surreal/surreal_single.txt (single_net, multires_views 0, 96 + 48); tau at its ceiling
-         "s1_single_s96i48_mrv0", "t2000_512_s64i128"]
+         "s1_single_s96i48_mrv0", "t2000_512_s64i128",
+         # --lindisp (inverse-depth samples)
+         "l1_lindisp_s32i16_d4w128"]
 
 
 class Golden:
@@ -42,6 +44,7 @@ class Golden:
                                        cutoff_inputs="--cutoff_inputs" not in drop,
                                        cutoff_viewdir="--cutoff_viewdir" not in drop,
                                        multires_views=m.get("mrv", 4), single_net=m.get("single", False),
+                                       lindisp="--lindisp" in flags or bool(m.get("lindisp", False)),
                                        **kw).validate()
         self.ckpt = syn.make_checkpoint(m["seed"], n_joints=m["NJ"], D=m["D"], W=m["W"], fine=m["I"] > 0,
                                         tau=m["tau"], use_framecode=fc, n_framecodes=5, multires=m.get("mr", 7),

@@ -113,6 +113,9 @@ CONFIGS = {
                                   mrv=0, single=True),
     # the tau schedule's ceiling (CutoffEmbedder.update_tau clamps at 2000): the sharpest window
     "t2000_512_s64i128": dict(H=512, NJ=24, S=64, I=128, D=8, W=256, tau=2000.0, kind="rays", n_rays=256, seed=32),
+    # --lindisp: samples linear in inverse depth (sample_from_lineseg, ray_utils.py:223-226)
+    "l1_lindisp_s32i16_d4w128": dict(H=128, NJ=24, S=32, I=16, D=4, W=128, tau=20.0, kind="rays", n_rays=128,
+                                     seed=25, flags=["--lindisp"]),
 }
 
 
@@ -203,7 +206,7 @@ def stage_dump(mods, render_kwargs, o, d, sc, n_stage, cams=None):
     out = {}
     with torch.no_grad():
         near, far = ray_utils.get_near_far_in_cylinder(o, d, cyl, near=torch.zeros(n, 1), far=torch.ones(n, 1))
-        pts, z = rc.sample_pts(o, d, near, far, n, S, 0.0, False)
+        pts, z = rc.sample_pts(o, d, near, far, n, S, 0.0, bool(render_kwargs.get("lindisp", False)))
         jc = rc.get_subject_joint_coords(None, pts.device)
         enc = rc.encode_inputs(pts, [o[:, None, :], d[:, None, :]], kp, skts, bones, cam_idxs=cam_t,
                                subject_idxs=None, joint_coords=jc, network=rc.network, **pk)

@@ -36,6 +36,12 @@ CONFIGS = {
     # single_net + multires_views 0 (configs/surreal/surreal_single.txt's flags, smaller net)
     "t5_single_mrv0": dict(H=128, NJ=24, S=48, I=24, D=4, W=128, tau=20.0, kind="rays", seed=35, n_rays=64,
                            n_poses=2, mrv=0, single=True),
+    # --lindisp and --ray_noise_std (sample_pts / sample_pts_is add randn_like(pts) * std,
+    # raycasters.py:660-661, 673-674): two more recorded draws of shape (N, S, 3) and (N, I, 3)
+    "t6_lindisp_raynoise": dict(H=128, NJ=24, S=32, I=16, D=4, W=128, tau=20.0, kind="rays", seed=36, n_rays=64,
+                                n_poses=2, lindisp=True, ray_noise_std=0.01),
+    "t7_single_raynoise": dict(H=128, NJ=24, S=32, I=16, D=4, W=128, tau=20.0, kind="rays", seed=37, n_rays=64,
+                               n_poses=2, single=True, ray_noise_std=0.02),
 }
 FULL_LIMIT = 20000   # parameters with more entries are sampled
 SAMPLE = 4096
@@ -77,19 +83,28 @@ def make(name, cfg, mods, tmp):
              "noise0": rng.standard_normal((n, S), dtype=np.float32),
              "u": rng.random((n, I), dtype=np.float32),
              "noise1": rng.standard_normal((n, T), dtype=np.float32)}
+    rns = float(cfg.get("ray_noise_std", 0.0))
+    if rns > 0:
+        draws["pts_noise0"] = rng.standard_normal((n, S, 3), dtype=np.float32)
+        draws["pts_noise1"] = rng.standard_normal((n, I, 3), dtype=np.float32)
     target = rng.random((n, 3), dtype=np.float32)
     bg = rng.random((n, 3), dtype=np.float32)
     cams = None
     if cfg["kind"] == "framecode":
         cams = (np.arange(n) % 5).astype(np.float32)
 
-    queue = [("rand", draws["t_rand"]), ("randn", draws["noise0"]), ("rand", draws["u"]),
-             ("randn", draws["noise1"])]
-    real_rand, real_randn = torch.rand, torch.randn
+    # the reference's draw order: t_rand (sample_from_lineseg), [points noise (sample_pts)], raw noise
+    # (raw2outputs), u (sample_pdf), [points noise of the new samples (sample_pts_is)], raw noise
+    queue = [("rand", draws["t_rand"])] + ([("randn_like", draws["pts_noise0"])] if rns > 0 else []) + \
+            [("randn", draws["noise0"]), ("rand", draws["u"])] + \
+            ([("randn_like", draws["pts_noise1"])] if rns > 0 else []) + [("randn", draws["noise1"])]
+    real_rand, real_randn, real_randn_like = torch.rand, torch.randn, torch.randn_like
 
     def fake(kind):
         def fn(*shape, **kw):
             k, arr = queue.pop(0)
+            if kind == "randn_like":
+                shape = (tuple(shape[0].shape),)
             shp = tuple(shape[0]) if len(shape) == 1 and not isinstance(shape[0], int) else tuple(shape)
             assert k == kind and shp == arr.shape, (kind, shp, k, arr.shape)
             return torch.from_numpy(arr.copy())
@@ -105,13 +120,13 @@ def make(name, cfg, mods, tmp):
         args.cutoff_step, args.cutoff_rate = cfg["cutoff_step"], cfg["cutoff_rate"]
         rc.update_embed_fns(cfg["global_step"], args)
     taus = (float(rc.embed_fn.get_tau()), float(rc.embeddirs_fn.get_tau()))
-    torch.rand, torch.randn = fake("rand"), fake("randn")
+    torch.rand, torch.randn, torch.randn_like = fake("rand"), fake("randn"), fake("randn_like")
     try:
         ret = rc(torch.from_numpy(rb), S, kp_batch=kp_t, skts=skts_t, cyls=torch.from_numpy(cyl), bones=bones_t,
                  cams=None if cams is None else torch.from_numpy(cams), perturb=1.0, N_importance=I,
-                 raw_noise_std=1.0, preproc_kwargs=pk)
+                 raw_noise_std=1.0, lindisp=bool(cfg.get("lindisp", False)), ray_noise_std=rns, preproc_kwargs=pk)
     finally:
-        torch.rand, torch.randn = real_rand, real_randn
+        torch.rand, torch.randn, torch.randn_like = real_rand, real_randn, real_randn_like
     assert not queue, "the reference drew fewer random tensors than expected"
     tgt, bgt = torch.from_numpy(target), torch.from_numpy(bg)
     # Trainer._compute_nerf_loss (MSE, use_background) on fine and coarse outputs
@@ -123,7 +138,8 @@ def make(name, cfg, mods, tmp):
                 framecode=int(cfg["kind"] == "framecode"), mr=7, flags=cfg.get("flags", []), drop=[],
                 raw_noise_std=1.0, n_poses=P, mrv=cfg.get("mrv", 4), single=bool(cfg.get("single", False)),
                 global_step=cfg.get("global_step"), cutoff_step=cfg.get("cutoff_step"),
-                cutoff_rate=cfg.get("cutoff_rate"), tau_step=taus)
+                cutoff_rate=cfg.get("cutoff_rate"), tau_step=taus, lindisp=bool(cfg.get("lindisp", False)),
+                ray_noise_std=rns)
     data = dict(rays=rb, pose=pose, skts=sc["skts"][pose], kps=sc["kps"][pose], bones=sc["bones"][pose], cyls=cyl,
                 target=target, bg=bg, loss=np.float32(loss.item()), grad_skts=skts_t.grad.numpy(),
                 **{"rand_" + k: v for k, v in draws.items()},

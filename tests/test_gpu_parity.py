@@ -52,6 +52,7 @@ def _render(rc, g, rb, **kw):
     skts = torch.from_numpy(g["skts"][0:1]).to(dev).expand(n, -1, -1, -1)
     cyls = torch.from_numpy(g["cyls"][0:1]).to(dev).expand(n, -1)
     cams = kw.pop("cams", None)
+    kw.setdefault("lindisp", g.cfg.lindisp)
     out = rc.render_rays(torch.from_numpy(rb).to(dev), g.cfg.N_samples, skts=skts, cyls=cyls,
                          cams=None if cams is None else torch.from_numpy(cams).to(dev),
                          N_importance=g.cfg.N_importance, chunk=4096, **kw)

@@ -23,7 +23,8 @@ pytestmark = pytest.mark.gpu
 anerf = importlib.import_module("a-nerf_amd")
 train = importlib.import_module("a-nerf_amd.train")
 
-TRAIN = ["t1_s32i16_d4w128", "t2_s64i16_d8w256", "t3_softplus_fc", "t4_tau200", "t5_single_mrv0"]
+TRAIN = ["t1_s32i16_d4w128", "t2_s64i16_d8w256", "t3_softplus_fc", "t4_tau200", "t5_single_mrv0",
+         "t6_lindisp_raynoise", "t7_single_raynoise"]
 TOL = 1e-4
 TOL_ALPHA = 2e-3
 GRAD_REL = 2e-3
@@ -53,9 +54,11 @@ def _run(name):
         assert (tr.module.embed_fn.get_tau(), tr.module.embeddirs_fn.get_tau()) == tuple(m["tau_step"])
     c = lambda k: torch.from_numpy(g[k]).to(dev)  # noqa: E731
     sk = c("skts").clone().requires_grad_(True)
-    rand = {k: c("rand_" + k) for k in ("t_rand", "noise0", "u", "noise1")}
+    rand = {k: c("rand_" + k) for k in ("t_rand", "noise0", "u", "noise1", "pts_noise0", "pts_noise1")
+            if g.has("rand_" + k)}
     out = tr.render_rays(c("rays"), m["S"], skts=sk, cyls=c("cyls"), cams=c("cams") if g.has("cams") else None,
-                         perturb=1.0, N_importance=m["I"], raw_noise_std=m["raw_noise_std"], rand=rand)
+                         perturb=1.0, N_importance=m["I"], raw_noise_std=m["raw_noise_std"], rand=rand,
+                         lindisp=m.get("lindisp", False), ray_noise_std=m.get("ray_noise_std", 0.0))
     loss = _loss(out, c("target"), c("bg"))
     loss.backward()
     torch.cuda.synchronize()

@@ -52,6 +52,24 @@ def test_config_rejects_unsupported_flags():
     cfg().validate()
 
 
+def test_no_viewdirs_refusal_matches_the_reference():
+    """use_viewdirs=False is refused up front; the reference itself cannot run it either: its
+    render_rays raises TypeError at encode_inputs' call of embeddirs_fn = None (recorded from the
+    reference by tests/golden/probe_reference_flags.py)."""
+    import json
+    with open(os.path.join(os.path.dirname(__file__), "golden", "reference_flags.json")) as f:
+        rec = json.load(f)["use_viewdirs=False"]
+    assert rec["raises"] == "TypeError" and "core/raycasters.py:538" in rec["reference_frames"]
+    with pytest.raises(NotImplementedError, match="raycasters.py:67, 538"):
+        config.RenderConfig(use_viewdirs=False).validate()
+
+
+def test_config_lindisp_from_args():
+    args = types.SimpleNamespace(lindisp=True, N_samples=32)
+    assert config.RenderConfig.from_args(args, 24).lindisp
+    assert not config.RenderConfig.from_args(types.SimpleNamespace(), 24).lindisp
+
+
 def test_config_from_args_matches_surreal_config():
     args = types.SimpleNamespace(netdepth=8, netwidth=256, multires=7, multires_views=4, use_cutoff=True,
                                  cutoff_inputs=True, cutoff_viewdir=True, use_viewdirs=True, N_samples=64,
