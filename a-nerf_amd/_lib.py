@@ -23,6 +23,7 @@ ANERF_PREC_BF16X3 = 1
 ANERF_PREC_BF16X6 = 2
 ANERF_PREC_FP16X3 = 3
 ANERF_FLAG_LINDISP = 0x100  # OR-ed into the precision argument (include/anerf.h)
+MLP_PRECISIONS = {"bf16x3": 3, "bf16x6": 6}  # ANERF_MLP_BF16X3 / _BF16X6 (training MLP GEMMs)
 PRECISIONS = {"fp32": ANERF_PREC_FP32, "bf16x3": ANERF_PREC_BF16X3, "bf16x6": ANERF_PREC_BF16X6,
               "fp16x3": ANERF_PREC_FP16X3}
 
@@ -50,6 +51,17 @@ class EmbedParams(ctypes.Structure):
 class Debug(ctypes.Structure):
     _fields_ = [("near", c_f), ("far", c_f), ("z_coarse", c_f), ("raw_coarse", c_f), ("weights0", c_f),
                 ("z_fine", c_f), ("raw_fine", c_f), ("mfma_count", ctypes.POINTER(ctypes.c_uint64))]
+
+
+class Seg(ctypes.Structure):
+    """anerf_seg: a column segment of a GEMM operand."""
+    _fields_ = [("p", ctypes.c_void_p), ("ld", ctypes.c_int64), ("cols", ctypes.c_int32)]
+
+
+class OSeg(ctypes.Structure):
+    """anerf_oseg: a column segment of a GEMM output (+ relu' mask, accumulate)."""
+    _fields_ = [("p", ctypes.c_void_p), ("ld", ctypes.c_int64), ("cols", ctypes.c_int32), ("mask", ctypes.c_void_p),
+                ("ldm", ctypes.c_int64), ("accumulate", ctypes.c_int32)]
 
 
 # name -> (restype, argtypes); must cover every entry point of include/anerf.h
@@ -137,6 +149,18 @@ SIGNATURES = {
     "anerf_train_importance": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
                                               ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
                                               ctypes.c_void_p, ctypes.c_void_p]),
+    "anerf_mlp_split_bytes": (ctypes.c_size_t, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
+    "anerf_mlp_split_weights": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64,
+                                               ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]),
+    "anerf_mlp_gemm": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(Seg),
+                                      ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+                                      ctypes.c_int32, ctypes.POINTER(OSeg), ctypes.c_int32, ctypes.c_void_p]),
+    "anerf_mlp_wgrad_workspace": (ctypes.c_size_t, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]),
+    "anerf_mlp_wgrad": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                                       ctypes.c_int64, ctypes.POINTER(Seg), ctypes.c_int32, ctypes.c_int32,
+                                       ctypes.c_void_p,
+                                       ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+                                       ctypes.c_size_t, ctypes.c_void_p]),
 }
 
 _lib = None

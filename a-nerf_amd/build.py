@@ -10,7 +10,7 @@ import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SRC = [os.path.join(HERE, "csrc", "anerf_render.hip")]
+SRC = [os.path.join(HERE, "csrc", "anerf_render.hip"), os.path.join(HERE, "csrc", "anerf_gemm.hip")]
 OUT = os.path.join(HERE, "libanerf_hip.so")
 STAMP = OUT + ".stamp"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

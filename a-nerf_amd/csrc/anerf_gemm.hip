@@ -1,0 +1,753 @@
+// anerf_gemm.hip — the training MLP's linear layers on the bf16 MFMA pipe.
+//
+// Training runs the reference's NeRF (core/networks/nerf.py:94-148) forward and backward over
+// M = rays x samples rows (131 k - 164 k per step at the reference's N_rand 2048, 64 + 16 samples).
+// Every product here is fp32 in, fp32 out, with the operands split as x = x_hi + x_lo into two
+// bf16 values (round to nearest even, x_lo = bf16(x - x_hi)) and three v_mfma_f32_32x32x16_bf16
+// products x_lo w_hi + x_hi w_lo + x_hi w_hi accumulated in fp32 (the dropped x_lo w_lo is below
+// 2^-16 of |x w|): ~16 significant bits per operand, 5.3x the fp32 MFMA rate in MFMA cycles.
+//
+//   forward / input gradient (NT): C[m][n] = epi(sum_k A[m][k] B[n][k]); A = up to three fp32
+//     column segments (the reference's cat([x, h]) / cat([feature, views, code]) never built),
+//     split into LDS as it is staged; B = the layer's weight (forward) or its transpose (input
+//     gradient), split once per step into bf16 planes (anerf_mlp_split_weights).  Epilogue: + bias,
+//     relu (forward); relu' mask by the saved activation (> 0) and accumulate (backward); the output
+//     is up to three column segments (e.g. the view layer's input gradient: feature part, the
+//     encoder's view columns, the framecodes).
+//   weight gradient (TN): dW[n][k] = sum_m dY[m][n] X[m][k] over M split into slabs, one partial
+//     tile per (slab, tile) in a workspace, summed in a second launch in slab order (deterministic,
+//     no atomics); the bias gradient sum_m dY[m][n] is summed from the staged dY in the same pass.
+//
+// Tiles: 128 x 128 outputs per 256-thread workgroup (4 waves, 2 x 2, each 64 x 64 = 2 x 2 blocks
+// of 32 x 32), BK = 32 (two k16 steps), LDS [row][k] bf16 planes with a 40-element pitch (80 B: the
+// 16 lanes of a ds_read_b128 group hit 16 distinct 4-bank groups), two stages (80 KB: two
+// workgroups per CU).  One barrier per k-step: the next tile's global loads are issued before the
+// MFMAs of the current one and written to the other stage after them.  Workgroups are mapped so
+// the column tiles of one row tile (which re-read the same A rows) run on one XCD's L2.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdlib>
+#include <string>
+
+#include "../../include/anerf.h"
+
+int anerf_internal_fail(int code, const char* msg);  // anerf_render.hip: sets anerf_last_error()
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BM = 128, BN = 128, NTHR = 256;
+constexpr int MAXSEG = 3;
+
+// NPL planes per operand: 2 = bf16x3 (x = x0 + x1; products x1 w0, x0 w1, x0 w0), 3 = bf16x6
+// (x = x0 + x1 + x2; the six products with i + j <= 2, fp32-accurate: the dropped terms are below
+// 2^-23 of |x w|).  BK = the k extent of one staged step; LDP = its LDS row pitch (BK + 8 bf16:
+// conflict-free ds_read_b128 for 16 consecutive rows at 80 / 48 bytes per row).
+template <int NPL>
+struct Geo {
+    static constexpr int BK = 16;
+    static constexpr int LDP = BK + 8;
+    static constexpr int PLANE = BM * LDP;
+    static constexpr int STAGE = 2 * NPL * PLANE;  // A planes, then B planes
+    static constexpr int LDS_BYTES = 2 * STAGE * 2;
+    static constexpr int E = BK / 2;  // elements one thread stages per operand row / column
+};
+
+struct SegD {
+    const float* p;
+    long long ld;
+    int start, cols;
+    int vec;  // float4 loads allowed (ld, start, pointer 16-byte aligned)
+};
+struct OSegD {
+    float* p;
+    long long ld;
+    int start, cols;
+    const float* mask;
+    long long ldm;
+    int accum;
+};
+
+struct NTArgs {
+    long long M;
+    int N, K;
+    SegD a[MAXSEG];
+    int na;
+    const unsigned short* b;  // split weights, fragment-major (split_weights_kernel)
+    int bplane_blocks;        // 32-column blocks of B (padded)
+    int ksteps;               // k16 steps of B (padded)
+    const float* bias;
+    int relu;
+    OSegD c[MAXSEG];
+    int nc;
+    int tiles_n, total;
+    int dbg;  // diagnostic ablations (ANERF_GEMM_DBG): 1 no stores, 2 B fragments of step 0 only, 4 A of step 0 only
+};
+
+struct TNArgs {
+    long long M;
+    int N, K;  // dW is N x K
+    const float* dy;
+    long long lddy;
+    SegD x[MAXSEG];
+    int nx;
+    int tiles_k, tiles, total, splits;
+    long long rows_per_split;
+    float* ws;   // [splits][Npad][Kpad]
+    float* wsb;  // [splits][Npad] bias partials, or null
+    int npad, kpad;
+};
+
+// 8 values -> NPL bf16 fragments (round to nearest even of the running remainder)
+template <int NPL>
+__device__ __forceinline__ void split8(const float* v, u32x4 (&out)[NPL]) {
+    float r[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = v[j];
+#pragma unroll
+    for (int p = 0; p < NPL; ++p) {
+        bf16x8 h;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) h[j] = (__bf16)r[j];
+        if (p + 1 < NPL) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) r[j] -= (float)h[j];
+        }
+        out[p] = __builtin_bit_cast(u32x4, h);
+    }
+}
+
+// logical tile of a workgroup: the hardware deals workgroups round-robin over the 8 XCDs; this
+// bijection gives each XCD a contiguous run of logical ids (MI355X guide, "XCD swizzle")
+__device__ __forceinline__ int xcd_logical(int wg, int total) {
+    const int xcd = wg & 7, q = total >> 3, r = total & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (wg >> 3);
+}
+
+// One operand row over up to three column segments, resolved without indexing the argument
+// struct by a per-lane value (that compiles to dependent per-lane loads of the struct): the three
+// segments' row pointers are computed once and selected with v_cndmask per 4-column group.
+struct RowSrc {
+    unsigned long long p0, p1, p2;  // segment i's row address, minus its first column (indexed by k)
+    int start1, start2;             // first columns of segments 1 and 2 (K when absent)
+    int kmax4;                      // last 4-column group that is read (round_up(K, 4) - 4)
+};
+
+// (values pinned in registers: without the pin, clang folds the per-lane select between the three
+// pointers into an indexed load from a stack copy of the struct — scratch traffic in the k loop)
+__device__ __forceinline__ void pin64(unsigned long long& x) { asm volatile("" : "+v"(x)); }
+
+// rows past M read row M - 1 (finite; their outputs are never stored)
+__device__ __forceinline__ RowSrc row_src(const SegD* seg, int nseg, long long row, long long M, int K) {
+    RowSrc r;
+    const long long rr = row < M ? row : M - 1;
+    r.p0 = (unsigned long long)(seg[0].p + rr * seg[0].ld);
+    r.p1 = nseg > 1 ? (unsigned long long)(seg[1].p + rr * seg[1].ld - seg[1].start) : r.p0;
+    r.p2 = nseg > 2 ? (unsigned long long)(seg[2].p + rr * seg[2].ld - seg[2].start) : r.p0;
+    pin64(r.p0);
+    pin64(r.p1);
+    pin64(r.p2);
+    r.start1 = nseg > 1 ? seg[1].start : K;
+    r.start2 = nseg > 2 ? seg[2].start : K;
+    r.kmax4 = (K + 3) / 4 * 4 - 4;
+    return r;
+}
+
+typedef __attribute__((address_space(1))) const float gfloat;
+typedef __attribute__((address_space(1))) const f32x4 gf32x4;
+
+// The raw 4-column groups of the row at columns k .. k+E-1 (clamped to the last readable group;
+// live_groups() says which are past K and become zeros when staged).  Every load is
+// unconditional and nothing reads the loaded registers before staging, so the compiler's counted
+// vmcnt waits stay exact across the two-deep prefetch.  The host guarantees 4-column groups never
+// straddle segments and that a ragged last segment's columns up to round_up(K, 4) are readable
+// and finite (the B planes are zero there).
+template <int E>
+__device__ __forceinline__ void load_row(const RowSrc& r, int k, f32x4 (&v)[E / 4]) {
+    // (rvalue copies: a ?: between struct-field lvalues selects ADDRESSES, and clang then keeps the
+    // struct on the stack and loads through the selected address)
+    const unsigned long long q0 = r.p0, q1 = r.p1, q2 = r.p2;
+    const int s1 = r.start1, s2 = r.start2, km = r.kmax4;
+#pragma unroll
+    for (int g = 0; g < E / 4; ++g) {
+        const int kg = k + 4 * g;
+        const int kc = kg < km ? kg : km;
+        const bool in2 = kc >= s2, in1 = !in2 && kc >= s1;
+        const float* p = (const float*)(in2 ? q2 : (in1 ? q1 : q0));
+        v[g] = *(gf32x4*)(p + kc);
+    }
+}
+
+// split the E values of one operand row (columns k .. k+E-1; zeros from column K on) into the
+// NPL planes at `planes`
+template <int NPL, int E>
+__device__ __forceinline__ void store_split(unsigned short* planes, int row, int k, const float (&v)[E]) {
+    using G = Geo<NPL>;
+#pragma unroll
+    for (int h = 0; h < E / 8; ++h) {
+        u32x4 f[NPL];
+        split8<NPL>(v + 8 * h, f);
+#pragma unroll
+        for (int p = 0; p < NPL; ++p)
+            *reinterpret_cast<u32x4*>(planes + p * G::PLANE + row * G::LDP + k + 8 * h) = f[p];
+    }
+}
+
+template <int NPL, int E>
+__device__ __forceinline__ void store_split_groups(unsigned short* planes, int row, int k, int kcol, int K,
+                                                   const f32x4 (&q)[E / 4]) {
+    float v[E];
+#pragma unroll
+    for (int g = 0; g < E / 4; ++g)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[4 * g + e] = kcol + 4 * g < K ? q[g][e] : 0.0f;
+    store_split<NPL, E>(planes, row, k, v);
+}
+
+__device__ __forceinline__ f32x16 mfma(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// one staged step of a wave's 64 x 64 block: BK / 16 k16 steps, the products i + j <= NPL - 1,
+// smallest terms first
+template <int NPL>
+__device__ __forceinline__ void mma_step(const unsigned short* st, int wr, int wc, int lane, f32x16 (&acc)[2][2]) {
+    using G = Geo<NPL>;
+    const unsigned short* A = st;
+    const unsigned short* B = st + NPL * G::PLANE;
+    const int r = lane & 31, kh = 8 * (lane >> 5);
+#pragma unroll
+    for (int kk = 0; kk < G::BK / 16; ++kk) {
+        bf16x8 a[NPL][2], b[NPL][2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int ra = (64 * wr + 32 * i + r) * G::LDP + 16 * kk + kh;
+            const int rb = (64 * wc + 32 * i + r) * G::LDP + 16 * kk + kh;
+#pragma unroll
+            for (int p = 0; p < NPL; ++p) {
+                a[p][i] = *reinterpret_cast<const bf16x8*>(A + p * G::PLANE + ra);
+                b[p][i] = *reinterpret_cast<const bf16x8*>(B + p * G::PLANE + rb);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                f32x16 c = acc[i][j];
+                if constexpr (NPL == 3) {
+                    c = mfma(a[2][i], b[0][j], c);
+                    c = mfma(a[1][i], b[1][j], c);
+                    c = mfma(a[0][i], b[2][j], c);
+                }
+                c = mfma(a[1][i], b[0][j], c);
+                c = mfma(a[0][i], b[1][j], c);
+                acc[i][j] = mfma(a[0][i], b[0][j], c);
+            }
+    }
+}
+
+// ---------------------------------------------------------------- forward / input gradient
+// 128 rows x 256 columns per workgroup (4 waves, 2 x 2: 64 rows x 128 columns = 2 x 4 blocks each).
+// A (activations, fp32 from HBM) is split once per workgroup into LDS planes, two k16 steps of
+// loads in flight.  B (the split weights, a few hundred KB shared by every workgroup) is read
+// straight from L2 as MFMA fragments — its planes are stored fragment-major (1 KB per (32-column
+// block, k16 step, plane), lane order), so each fragment load is one contiguous 1 KB wave access —
+// and never touches LDS; the next step's fragments are loaded under the current step's MFMAs.
+constexpr int BNW = 256;
+
+template <int NPL>
+struct BFrag {
+    u32x4 v[NPL][4];  // [plane][column block of this wave]
+};
+
+template <int NPL>
+__global__ __launch_bounds__(NTHR, 1) void mlp_nt_kernel(NTArgs g) {
+    using G = Geo<NPL>;
+    constexpr int BK = G::BK, E = G::E;
+    static_assert(BK == 16 && E == 8, "one k16 step per stage");
+    extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
+    const int logical = xcd_logical(blockIdx.x, g.total);
+    const int mt = logical / g.tiles_n, nt = logical % g.tiles_n;
+    const long long m0 = (long long)mt * BM;
+    const int n0 = nt * BNW;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave >> 1, wc = wave & 1;
+    // staging: each wave stages 32 rows; lanes l and l + 32 the two 8-column halves of one row (the
+    // 8-lane groups of a ds_write_b128 then hit 8 distinct rows: conflict-free at the 48 B pitch)
+    const int lr = 32 * wave + (lane & 31), lq = E * (lane >> 5);
+    const int nk = (g.K + BK - 1) / BK;
+    const RowSrc src = row_src(g.a, g.na, m0 + lr, g.M, g.K);
+    // this wave's B fragments: column blocks nb0 .. nb0 + 3 (clamped to the last block of the
+    // padded planes: past N they are zero, and the outputs are not stored)
+    const int nb0 = (n0 + 128 * wc) / 32;
+    const int nbk = g.bplane_blocks;
+    const unsigned short* bl = g.b + lane * 8;
+
+    f32x16 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x16{0};
+
+    auto fetch_b = [&](int kt, BFrag<NPL>& f) {
+        kt = kt < nk ? kt : nk - 1;
+        if (g.dbg & 2) kt = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            int nb = nb0 + j;
+            nb = nb < nbk ? nb : nbk - 1;
+#pragma unroll
+            for (int p = 0; p < NPL; ++p)
+                f.v[p][j] = *reinterpret_cast<const u32x4*>(bl + (((long long)nb * g.ksteps + kt) * NPL + p) * 512);
+        }
+    };
+    auto fetch_a = [&](int kt, f32x4 (&av)[2]) {
+        kt = kt < nk ? kt : nk - 1;
+        if (g.dbg & 4) kt = 0;
+        load_row<E>(src, kt * BK + lq, av);
+    };
+    auto stage_a = [&](int s, int kt, const f32x4 (&av)[2]) {
+        store_split_groups<NPL, E>(lds + s * G::STAGE, lr, lq, kt * BK + lq, g.K, av);
+    };
+    auto step = [&](int s, const BFrag<NPL>& f) {
+        const unsigned short* A = lds + s * G::STAGE;
+        const int r = lane & 31, kh = 8 * (lane >> 5);
+        bf16x8 a[NPL][2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int p = 0; p < NPL; ++p)
+                a[p][i] = *reinterpret_cast<const bf16x8*>(A + p * G::PLANE + (64 * wr + 32 * i + r) * G::LDP + kh);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            bf16x8 b[NPL];
+#pragma unroll
+            for (int p = 0; p < NPL; ++p) b[p] = __builtin_bit_cast(bf16x8, f.v[p][j]);
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                f32x16 c = acc[i][j];
+                if constexpr (NPL == 3) {
+                    c = mfma(a[2][i], b[0], c);
+                    c = mfma(a[1][i], b[1], c);
+                    c = mfma(a[0][i], b[2], c);
+                }
+                c = mfma(a[1][i], b[0], c);
+                c = mfma(a[0][i], b[1], c);
+                acc[i][j] = mfma(a[0][i], b[0], c);
+            }
+        }
+    };
+    // register slots are compile-time (a runtime-indexed register array would force each load to
+    // complete on the spot); fetches past the last step reload it (unconditional loads keep the
+    // compiler's counted vmcnt waits exact)
+    f32x4 a0[2], a1[2];
+    BFrag<NPL> f0, f1;
+    fetch_a(0, a0);
+    fetch_a(1, a1);
+    fetch_b(0, f0);
+    stage_a(0, 0, a0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; kt += 2) {
+        fetch_a(kt + 2, a0);
+        fetch_b(kt + 1, f1);
+        step(0, f0);
+        if (kt + 1 < nk) stage_a(1, kt + 1, a1);
+        __syncthreads();
+        if (kt + 1 >= nk) break;
+        fetch_a(kt + 3, a1);
+        fetch_b(kt + 2, f0);
+        step(1, f1);
+        if (kt + 2 < nk) stage_a(0, kt + 2, a0);
+        __syncthreads();
+    }
+    // epilogue: lane holds column n = .. + (lane & 31), rows (r & 3) + 8 (r >> 2) + 4 (lane >> 5).
+    // The mask / accumulate operands of a 16-row block are loaded up front from clamped rows (no
+    // load under a per-element branch: each would wait for its own round trip).
+    const bool need_mask = g.c[0].mask || (g.nc > 1 && g.c[1].mask) || (g.nc > 2 && g.c[2].mask);
+    const bool need_acc = g.c[0].accum || (g.nc > 1 && g.c[1].accum) || (g.nc > 2 && g.c[2].accum);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int n = n0 + 128 * wc + 32 * j + (lane & 31);
+        if (n >= g.N) continue;
+        // output segment of column n, selected from rvalue copies of the uniform fields (see load_row)
+        const OSegD c0 = g.c[0], c1 = g.c[1], c2 = g.c[2];
+        const bool in2 = g.nc > 2 && n >= c2.start, in1 = !in2 && g.nc > 1 && n >= c1.start;
+        float* const op = in2 ? c2.p + 0 : (in1 ? c1.p + 0 : c0.p + 0);
+        if (!op) continue;  // a discarded segment (a gradient nobody needs)
+        const long long old = in2 ? c2.ld + 0 : (in1 ? c1.ld + 0 : c0.ld + 0);
+        const float* const mp = in2 ? c2.mask + 0 : (in1 ? c1.mask + 0 : c0.mask + 0);
+        const long long ldm = in2 ? c2.ldm + 0 : (in1 ? c1.ldm + 0 : c0.ldm + 0);
+        const int acc_out = in2 ? c2.accum + 0 : (in1 ? c1.accum + 0 : c0.accum + 0);
+        const int col = n - (in2 ? c2.start + 0 : (in1 ? c1.start + 0 : 0));
+        const float* const mq = mp ? mp : op;  // (a valid address when this segment has no mask)
+        const long long ldq = mp ? ldm : old;
+        const float b = g.bias ? g.bias[n] : 0.0f;
+        const int ldo = (int)old, ldmq = (int)ldq;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const long long mb = m0 + 64 * wr + 32 * i + 4 * (lane >> 5);
+            const int rows_left = (int)(g.M - mb < 32 ? g.M - mb : 32);  // rows mb + d, d < rows_left
+            float* const orow = op + mb * old + col;
+            const float* const mrow = mq + mb * ldq + col;
+            float mv[16], cv[16];
+            if (need_mask) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    int d = (r & 3) + 8 * (r >> 2);
+                    d = d < rows_left ? d : rows_left - 1;
+                    mv[r] = *(gfloat*)(mrow + d * ldmq);
+                }
+            }
+            if (need_acc) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    int d = (r & 3) + 8 * (r >> 2);
+                    d = d < rows_left ? d : rows_left - 1;
+                    cv[r] = *(gfloat*)(orow + d * ldo);
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int d = (r & 3) + 8 * (r >> 2);
+                float v = acc[i][j][r] + b;
+                if (g.relu) v = fmaxf(v, 0.0f);
+                if (need_mask && mp && !(mv[r] > 0.0f)) v = 0.0f;
+                if (need_acc && acc_out) v += cv[r];
+                if (d < rows_left && !(g.dbg & 1)) orow[d * ldo] = v;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- weight gradient
+template <int NPL>
+__global__ __launch_bounds__(NTHR, 2) void mlp_tn_kernel(TNArgs g) {
+    using G = Geo<NPL>;
+    constexpr int BK = G::BK, E = G::E;
+    extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
+    const int logical = xcd_logical(blockIdx.x, g.total);
+    const int split = logical / g.tiles, tile = logical % g.tiles;
+    const int nt = tile / g.tiles_k, kt_ = tile % g.tiles_k;
+    const int n0 = nt * BN, k0 = kt_ * BM;
+    const long long mlo = (long long)split * g.rows_per_split;
+    long long mhi = mlo + g.rows_per_split;
+    if (mhi > g.M) mhi = g.M;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int c = tid & 127, h = tid >> 7;  // staging: column, E-row half of the BK-row step
+    // this thread's columns: dY column n0 + c, X column k0 + c (segment resolved once)
+    const int n = n0 + c, k = k0 + c;
+    const bool nok = n < g.N, kok = k < g.K;
+    // (clamped columns: every load below is unconditional, the values past N / K are zeroed)
+    const int kq = kok ? k : 0;
+    const bool in2 = g.nx > 2 && kq >= g.x[2].start, in1 = !in2 && g.nx > 1 && kq >= g.x[1].start;
+    const float* xp = (in2 ? g.x[2].p + 0 : (in1 ? g.x[1].p + 0 : g.x[0].p + 0)) +
+                      (kq - (in2 ? g.x[2].start + 0 : (in1 ? g.x[1].start + 0 : 0)));
+    const long long xld = in2 ? g.x[2].ld + 0 : (in1 ? g.x[1].ld + 0 : g.x[0].ld + 0);
+    const float* yp = g.dy + (nok ? n : 0);
+    const bool do_bias = g.wsb != nullptr && kt_ == 0;
+    float bsum = 0.0f;
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{0};
+
+    // the NT kernel's two-slot pipeline; rows past the slab reload its last row and are zeroed when
+    // staged
+    float y0[E], x0[E], y1[E], x1[E];
+    const long long mlast = mhi > mlo ? mhi - 1 : mlo;
+    auto fetch = [&](long long mb, float (&yv)[E], float (&xv)[E]) {
+#pragma unroll
+        for (int j = 0; j < E; ++j) {
+            long long m = mb + E * h + j;
+            m = m < mlast ? m : mlast;
+            yv[j] = *(gfloat*)(yp + m * g.lddy);
+            xv[j] = *(gfloat*)(xp + m * xld);
+        }
+    };
+    auto stage = [&](int s, long long mb, const float (&yv)[E], const float (&xv)[E]) {
+        unsigned short* st = lds + s * G::STAGE;
+        float yz[E], xz[E];
+#pragma unroll
+        for (int j = 0; j < E; ++j) {
+            const bool ok = mb + E * h + j < mhi;
+            yz[j] = (ok && nok) ? yv[j] : 0.0f;
+            xz[j] = (ok && kok) ? xv[j] : 0.0f;
+        }
+        store_split<NPL, E>(st, c, E * h, yz);
+        store_split<NPL, E>(st + NPL * G::PLANE, c, E * h, xz);
+        if (do_bias) {
+#pragma unroll
+            for (int j = 0; j < E; ++j) bsum += yz[j];
+        }
+    };
+    const int nsteps = mhi > mlo ? (int)((mhi - mlo + BK - 1) / BK) : 0;
+    if (nsteps > 0) {
+        fetch(mlo, y0, x0);
+        fetch(mlo + BK, y1, x1);
+        stage(0, mlo, y0, x0);
+    }
+    __syncthreads();
+    for (int st = 0; st < nsteps; st += 2) {
+        fetch(mlo + (long long)(st + 2) * BK, y0, x0);
+        mma_step<NPL>(lds, wr, wc, lane, acc);
+        if (st + 1 < nsteps) stage(1, mlo + (long long)(st + 1) * BK, y1, x1);
+        __syncthreads();
+        if (st + 1 >= nsteps) break;
+        fetch(mlo + (long long)(st + 3) * BK, y1, x1);
+        mma_step<NPL>(lds + G::STAGE, wr, wc, lane, acc);
+        if (st + 2 < nsteps) stage(0, mlo + (long long)(st + 2) * BK, y0, x0);
+        __syncthreads();
+    }
+    float* wt = g.ws + (long long)split * g.npad * g.kpad;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int kc = k0 + 64 * wc + 32 * j + (lane & 31);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int nr = n0 + 64 * wr + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                wt[(long long)nr * g.kpad + kc] = acc[i][j][r];
+            }
+    }
+    if (do_bias) {  // (after the loop's last barrier the stages are free)
+        float* red = reinterpret_cast<float*>(lds);
+        if (h == 1) red[c] = bsum;
+        __syncthreads();
+        if (h == 0) g.wsb[(long long)split * g.npad + n] = bsum + red[c];
+    }
+}
+
+__global__ void mlp_reduce_kernel(const float* __restrict__ ws, const float* __restrict__ wsb, int splits, int npad,
+                                  int kpad, int N, int K, float* __restrict__ dw, long long lddw,
+                                  float* __restrict__ db, int accum) {
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long nk = (long long)N * K;
+    if (idx < nk) {
+        const int n = (int)(idx / K), k = (int)(idx % K);
+        const float* p = ws + (long long)n * kpad + k;
+        float s = 0.0f;
+        for (int t = 0; t < splits; ++t) s += p[(long long)t * npad * kpad];
+        float* o = dw + (long long)n * lddw + k;
+        *o = accum ? *o + s : s;
+    } else if (wsb && db && idx < nk + N) {
+        const int n = (int)(idx - nk);
+        float s = 0.0f;
+        for (int t = 0; t < splits; ++t) s += wsb[(long long)t * npad + n];
+        db[n] = accum ? db[n] + s : s;
+    }
+}
+
+// weight -> NPL bf16 planes in MFMA fragment order: for 32-row block nb, k16 step ks, plane p one
+// 1 KB run of 64 lanes x 8 bf16, lane l = row nb*32 + (l & 31), columns ks*16 + 8 (l >> 5) + 0..7
+// (the B operand lane map of v_mfma_f32_32x32x16_bf16), zero padded.  Rows are w's rows (or, when
+// transposed, w's columns).
+__global__ void split_weights_kernel(const float* __restrict__ w, int n, int k, long long ldw, int transpose,
+                                     int nblocks, int ksteps, int npl, unsigned short* __restrict__ out) {
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;  // one (nb, ks, lane, e)
+    const long long per = (long long)nblocks * ksteps * 512;
+    if (idx >= per) return;
+    const int e = (int)(idx & 7), l = (int)((idx >> 3) & 63);
+    const long long blk = idx >> 9;  // nb * ksteps + ks
+    const int ks = (int)(blk % ksteps), nb = (int)(blk / ksteps);
+    const int row = nb * 32 + (l & 31), col = ks * 16 + 8 * (l >> 5) + e;
+    const int rows = transpose ? k : n, cols = transpose ? n : k;
+    const int wn = transpose ? col : row, wk = transpose ? row : col;
+    float x = (row < rows && col < cols) ? w[(long long)wn * ldw + wk] : 0.0f;
+    for (int p = 0; p < npl; ++p) {
+        const __bf16 xh = (__bf16)x;
+        out[((blk * npl + p) << 9) + (l << 3) + e] = __builtin_bit_cast(unsigned short, xh);
+        x -= (float)xh;
+    }
+}
+
+inline int rup(long long x, int a) { return (int)((x + a - 1) / a * a); }
+
+constexpr int KPAD = 32;  // k padding of split weights (a multiple of both BKs)
+
+int planes_of(int precision) { return precision == ANERF_MLP_BF16X6 ? 3 : (precision == ANERF_MLP_BF16X3 ? 2 : 0); }
+
+// the dynamic LDS (80 / 72 KB) is above the default limit: raised once per kernel instance
+template <int NPL>
+hipError_t nt_attr() {
+    static const hipError_t e = hipFuncSetAttribute((const void*)mlp_nt_kernel<NPL>,
+                                                    hipFuncAttributeMaxDynamicSharedMemorySize, Geo<NPL>::LDS_BYTES);
+    return e;
+}
+template <int NPL>
+hipError_t tn_attr() {
+    static const hipError_t e = hipFuncSetAttribute((const void*)mlp_tn_kernel<NPL>,
+                                                    hipFuncAttributeMaxDynamicSharedMemorySize, Geo<NPL>::LDS_BYTES);
+    return e;
+}
+
+// Operand segments: every segment but the last a multiple of 4 columns, all 16-byte aligned with
+// ld % 4 == 0 (4-column groups never straddle segments; float4 loads); the last segment's row is
+// read up to round_up(cols, 4) columns (ld >= that; those columns must be finite).
+int set_segs(const anerf_seg* in, int n, int total, SegD* out) {
+    if (n < 1 || n > MAXSEG || !in) return anerf_internal_fail(ANERF_EINVAL, "1 to 3 operand segments");
+    int start = 0;
+    for (int i = 0; i < n; ++i) {
+        const bool last = i + 1 == n;
+        if (!in[i].p || in[i].cols < 1 || in[i].ld < (last ? (in[i].cols + 3) / 4 * 4 : in[i].cols))
+            return anerf_internal_fail(ANERF_EINVAL, "bad operand segment (ld < cols, rounded to 4 for the last)");
+        if (in[i].ld % 4 || (uintptr_t)in[i].p % 16 || (!last && in[i].cols % 4))
+            return anerf_internal_fail(ANERF_EINVAL, "operand segments need 16-byte aligned rows and, but for the "
+                                                     "last, a multiple of 4 columns");
+        out[i].p = in[i].p;
+        out[i].ld = in[i].ld;
+        out[i].start = start;
+        out[i].cols = in[i].cols;
+        out[i].vec = 1;
+        start += in[i].cols;
+    }
+    if (start != total) return anerf_internal_fail(ANERF_EINVAL, "operand segments do not add up to k");
+    return ANERF_OK;
+}
+
+int wgrad_plan(int64_t m, int32_t n, int32_t k, int* splits, long long* rows) {
+    const int tiles = ((n + BN - 1) / BN) * ((k + BM - 1) / BM);
+    long long s = (512 + tiles - 1) / tiles;         // ~512 workgroups (two per CU)
+    const long long smax = (m + 255) / 256;         // >= 256 rows per slab
+    if (s > smax) s = smax;
+    if (s < 1) s = 1;
+    long long r = (m + s - 1) / s;
+    r = (r + KPAD - 1) / KPAD * KPAD;
+    *rows = r;
+    *splits = (int)((m + r - 1) / r);
+    if (*splits < 1) *splits = 1;
+    return tiles;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t anerf_mlp_split_bytes(int32_t rows, int32_t cols, int32_t precision) {
+    return (size_t)2 * planes_of(precision) * rup(rows, 32) * rup(cols, 16);
+}
+
+int anerf_mlp_split_weights(const float* w, int32_t n, int32_t k, int64_t ldw, int32_t transpose, int32_t precision,
+                            void* out, void* stream) {
+    const int npl = planes_of(precision);
+    if (!w || !out || n < 1 || k < 1 || ldw < k || !npl)
+        return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_split_weights: bad arguments");
+    const int rows = transpose ? k : n, cols = transpose ? n : k;
+    const int nblocks = (rows + 31) / 32, ksteps = (cols + 15) / 16;
+    const long long tot = (long long)nblocks * ksteps * 512;
+    hipLaunchKernelGGL(split_weights_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), w, n, k, (long long)ldw, transpose, nblocks, ksteps, npl,
+                       static_cast<unsigned short*>(out));
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? ANERF_OK : anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));
+}
+
+int anerf_mlp_gemm(int64_t m, int32_t n, int32_t k, const anerf_seg* a, int32_t n_a, const void* b_split,
+                   int32_t precision, const float* bias, int32_t relu, const anerf_oseg* c, int32_t n_c, void* stream) {
+    const int npl = planes_of(precision);
+    if (m < 0 || n < 1 || k < 1 || !b_split || !c || n_c < 1 || n_c > MAXSEG || !npl)
+        return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_gemm: bad arguments");
+    if (m == 0) return ANERF_OK;
+    NTArgs g = {};
+    g.M = m;
+    g.N = n;
+    g.K = k;
+    int rc = set_segs(a, n_a, k, g.a);
+    if (rc) return rc;
+    g.na = n_a;
+    g.b = static_cast<const unsigned short*>(b_split);
+    g.bplane_blocks = (n + 31) / 32;
+    g.ksteps = (k + 15) / 16;
+    g.bias = bias;
+    g.relu = relu != 0;
+    int start = 0;
+    for (int i = 0; i < n_c; ++i) {
+        if (c[i].cols < 1 || (c[i].p && c[i].ld < c[i].cols))
+            return anerf_internal_fail(ANERF_EINVAL, "bad output segment");
+        g.c[i] = OSegD{c[i].p, c[i].ld, start, c[i].cols, c[i].mask, c[i].ldm, c[i].accumulate != 0};
+        start += c[i].cols;
+    }
+    if (start != n) return anerf_internal_fail(ANERF_EINVAL, "output segments do not add up to n");
+    g.nc = n_c;
+    g.tiles_n = (n + BNW - 1) / BNW;
+    static const int dbg = [] {
+        const char* e = std::getenv("ANERF_GEMM_DBG");
+        return e ? std::atoi(e) : 0;
+    }();
+    g.dbg = dbg;
+    const long long tiles = (long long)((m + BM - 1) / BM) * g.tiles_n;
+    if (tiles > 0x7fffffff) return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_gemm: too many tiles");
+    g.total = (int)tiles;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    hipError_t e = npl == 3 ? nt_attr<3>() : nt_attr<2>();
+    if (e != hipSuccess) return anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));
+    if (npl == 3)
+        hipLaunchKernelGGL(mlp_nt_kernel<3>, dim3((unsigned)tiles), dim3(NTHR), Geo<3>::LDS_BYTES, st, g);
+    else
+        hipLaunchKernelGGL(mlp_nt_kernel<2>, dim3((unsigned)tiles), dim3(NTHR), Geo<2>::LDS_BYTES, st, g);
+    e = hipGetLastError();
+    return e == hipSuccess ? ANERF_OK : anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));
+}
+
+size_t anerf_mlp_wgrad_workspace(int64_t m, int32_t n, int32_t k) {
+    int splits;
+    long long rows;
+    wgrad_plan(m, n, k, &splits, &rows);
+    return (size_t)4 * splits * rup(n, BN) * (rup(k, BM) + 1);
+}
+
+int anerf_mlp_wgrad(int64_t m, int32_t n, int32_t k, const float* dy, int64_t lddy, const anerf_seg* x, int32_t n_x,
+                    int32_t precision, float* dw, int64_t lddw, float* db, int32_t accumulate, void* workspace,
+                    size_t workspace_bytes, void* stream) {
+    const int npl = planes_of(precision);
+    if (m < 0 || n < 1 || k < 1 || !dy || lddy < n || !dw || lddw < k || !npl)
+        return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_wgrad: bad arguments");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    TNArgs g = {};
+    int rc = set_segs(x, n_x, k, g.x);
+    if (rc) return rc;
+    if (m == 0) {  // empty sum
+        if (!accumulate) {
+            hipError_t e = hipMemset2DAsync(dw, lddw * 4, 0, (size_t)k * 4, n, st);
+            if (e == hipSuccess && db) e = hipMemsetAsync(db, 0, (size_t)n * 4, st);
+            if (e != hipSuccess) return anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));
+        }
+        return ANERF_OK;
+    }
+    if (!workspace || workspace_bytes < anerf_mlp_wgrad_workspace(m, n, k))
+        return anerf_internal_fail(ANERF_EWORKSPACE, "anerf_mlp_wgrad: workspace too small");
+    g.M = m;
+    g.N = n;
+    g.K = k;
+    g.dy = dy;
+    g.lddy = lddy;
+    g.nx = n_x;
+    g.tiles = wgrad_plan(m, n, k, &g.splits, &g.rows_per_split);
+    g.tiles_k = (k + BM - 1) / BM;
+    g.npad = rup(n, BN);
+    g.kpad = rup(k, BM);
+    g.total = g.tiles * g.splits;
+    g.ws = static_cast<float*>(workspace);
+    g.wsb = db ? g.ws + (size_t)g.splits * g.npad * g.kpad : nullptr;
+    hipError_t e = npl == 3 ? tn_attr<3>() : tn_attr<2>();
+    if (e != hipSuccess) return anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));
+    if (npl == 3)
+        hipLaunchKernelGGL(mlp_tn_kernel<3>, dim3((unsigned)g.total), dim3(NTHR), Geo<3>::LDS_BYTES, st, g);
+    else
+        hipLaunchKernelGGL(mlp_tn_kernel<2>, dim3((unsigned)g.total), dim3(NTHR), Geo<2>::LDS_BYTES, st, g);
+    const long long outs = (long long)n * k + (db ? n : 0);
+    hipLaunchKernelGGL(mlp_reduce_kernel, dim3((unsigned)((outs + 255) / 256)), dim3(256), 0, st, g.ws, g.wsb,
+                       g.splits, g.npad, g.kpad, n, k, dw, (long long)lddw, db, accumulate != 0);
+    e = hipGetLastError();
+    return e == hipSuccess ? ANERF_OK : anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));
+}
+
+}  // extern "C"

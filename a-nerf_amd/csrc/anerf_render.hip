@@ -51,6 +51,8 @@ using namespace anerf;
 #include "anerf_batch.hpp"
 #include "anerf_pack.hpp"
 
+int anerf_internal_fail(int code, const char* msg) { return fail(code, msg); }  // for anerf_gemm.hip
+
 #ifdef ANERF_STAMPS
 static unsigned long long* g_stamps = nullptr;
 extern "C" void anerf_diag_set_stamps(unsigned long long* p) { g_stamps = p; }  // diagnostic build only

@@ -1,0 +1,242 @@
+"""The training MLP (NeRF.forward of core/networks/nerf.py:94-148 and its autograd) on the
+hand-written split-bf16 GEMMs of anerf_gemm.hip (`anerf_mlp_*` in include/anerf.h).
+
+One autograd Function runs the whole network: forward_density (pts_linears with the skip
+layer's cat([x, h])), alpha_linear and feature_linear (one GEMM with N = W + 1, the alpha row
+appended), views_linears[0] on cat([feature, views(, framecode)]) and rgb_linear — the
+concatenations are operand segments, never built.  Bias and relu run in the GEMM epilogue; the
+backward masks each input gradient by the saved relu output in the epilogue of the GEMM that
+produces it (so every gradient that flows is already the pre-activation gradient the weight
+gradient needs), writes the encoder-feature gradient in place (the skip layer's x part, then layer
+0 accumulating into it; the view columns from the view layer) and sums weight and bias gradients
+over the rows in one pass per layer.  Saved for the backward: the relu outputs of every layer.
+
+Precision (`train.NeRF.mlp`): "bf16x6" (default) splits both operands three ways into bf16 and
+sums the six products with i + j <= 2 (fp32-accurate, as the render kernel's bf16x6 mode);
+"bf16x3" two ways, three products (~16 significant bits per operand); fp32 accumulation in both
+(`anerf_gemm.hip`).  There is no CPU path: the library must be
+built and a GPU present.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+
+
+def _stream(dev):
+    return _lib.stream_handle(dev)
+
+
+def _seg(t, cols, off=0):
+    """anerf_seg over columns [off, off + cols) of a row-major 2-D tensor."""
+    return (t.data_ptr() + 4 * off, t.stride(0), cols)
+
+
+def _segs(lst):
+    arr = (_lib.Seg * len(lst))()
+    for i, (p, ld, c) in enumerate(lst):
+        arr[i].p, arr[i].ld, arr[i].cols = p, ld, c
+    return arr, len(lst)
+
+
+def _osegs(lst):
+    """[(tensor or None, ld, cols, col offset, mask tensor or None, accumulate)]"""
+    arr = (_lib.OSeg * len(lst))()
+    for i, (t, ld, cols, off, mask, acc) in enumerate(lst):
+        arr[i].p = None if t is None else t.data_ptr() + 4 * off
+        arr[i].ld, arr[i].cols = ld, cols
+        arr[i].mask = None if mask is None else mask.data_ptr()
+        arr[i].ldm = 0 if mask is None else mask.stride(0)
+        arr[i].accumulate = int(acc)
+    return arr, len(lst)
+
+
+def split_weight(w, transpose=False, prec=6):
+    """w [n, k] fp32 (contiguous rows) -> the bf16 planes of w (or w^T) as a uint8 buffer
+    (prec: 6 = ANERF_MLP_BF16X6, three planes; 3 = ANERF_MLP_BF16X3, two)."""
+    n, k = w.shape
+    rows, cols = (k, n) if transpose else (n, k)
+    lib = _lib.load()
+    out = torch.empty(lib.anerf_mlp_split_bytes(rows, cols, prec), device=w.device, dtype=torch.uint8)
+    _lib.check(lib.anerf_mlp_split_weights(_lib.ptr(w), n, k, w.stride(0), int(transpose), prec, _lib.ptr(out),
+                                           _stream(w.device)), "anerf_mlp_split_weights")
+    return out
+
+
+def gemm(m, n, k, a, b_split, bias, relu, outs, dev, prec=6):
+    sa, na = _segs(a)
+    so, no = _osegs(outs)
+    _lib.check(_lib.load().anerf_mlp_gemm(m, n, k, sa, na, _lib.ptr(b_split), prec, _lib.ptr(bias), int(relu), so,
+                                          no, _stream(dev)), "anerf_mlp_gemm")
+
+
+def wgrad(m, n, k, dy, x, dw, db, ws, dev, prec=6):
+    sx, nx = _segs(x)
+    _lib.check(_lib.load().anerf_mlp_wgrad(m, n, k, _lib.ptr(dy), dy.stride(0), sx, nx, prec, _lib.ptr(dw),
+                                           dw.stride(0), _lib.ptr(db), 0, _lib.ptr(ws), ws.numel(), _stream(dev)),
+               "anerf_mlp_wgrad")
+
+
+class _MLP(torch.autograd.Function):
+    """raw [M, 4] = NeRF(feat [M, F] (, codes [M, C])); params = the module's tensors in the order of
+    `NeRF.mlp_params()`."""
+
+    @staticmethod
+    def forward(ctx, shape, feat, codes, *params):
+        W, D, skip, dnet, nv, prec = shape
+        dev = feat.device
+        M, F = feat.shape
+        nl = D
+
+        def sw(w, t=False):
+            return split_weight(w, t, prec)
+
+        def mm(*a):
+            gemm(*a, prec=prec)
+        pw, pb = params[0:2 * nl:2], params[1:2 * nl:2]
+        wa, ba, wf, bf, wv, bv, wr, br = params[2 * nl:2 * nl + 8]
+        cfc = 0 if codes is None else codes.shape[1]
+        f32 = dict(device=dev, dtype=torch.float32)
+        segx = _seg(feat, dnet)
+        H = []
+        for i in range(D):
+            if i == 0:
+                a, k = [segx], dnet
+            elif i - 1 == skip:
+                a, k = [segx, _seg(H[-1], W)], dnet + W
+            else:
+                a, k = [_seg(H[-1], W)], W
+            h = torch.empty(M, W, **f32)
+            mm(M, W, k, a, sw(pw[i]), pb[i], True, [(h, W, W, 0, None, False)], dev)
+            H.append(h)
+        # feature_linear + alpha_linear as one GEMM (alpha in raw[:, 3]); no activation
+        raw = torch.empty(M, 4, **f32)
+        hf = torch.empty(M, W, **f32)
+        whead = torch.cat([wf, wa]).contiguous()
+        bhead = torch.cat([bf, ba]).contiguous()
+        mm(M, W + 1, W, [_seg(H[-1], W)], sw(whead), bhead, False,
+             [(hf, W, W, 0, None, False), (raw, 4, 1, 3, None, False)], dev)
+        # views_linears[0] on cat([feature, views(, framecode)]), relu
+        av = [_seg(hf, W), _seg(feat, nv, dnet)] + ([_seg(codes, cfc)] if cfc else [])
+        g = torch.empty(M, W // 2, **f32)
+        mm(M, W // 2, W + nv + cfc, av, sw(wv), bv, True, [(g, W // 2, W // 2, 0, None, False)], dev)
+        # rgb_linear into raw[:, :3]
+        mm(M, 3, W // 2, [_seg(g, W // 2)], sw(wr), br, False, [(raw, 4, 3, 0, None, False)], dev)
+        ctx.shape = shape
+        ctx.has_codes = codes is not None
+        ctx.save_for_backward(feat, codes if codes is not None else torch.empty(0), hf, g, whead, *H, *params)
+        return raw
+
+    @staticmethod
+    def backward(ctx, g_raw):
+        W, D, skip, dnet, nv, prec = ctx.shape
+
+        def sw(w, t=False):
+            return split_weight(w, t, prec)
+
+        def mm(*a):
+            gemm(*a, prec=prec)
+        saved = ctx.saved_tensors
+        feat, codes, hf, g, whead = saved[:5]
+        H = saved[5:5 + D]
+        params = saved[5 + D:]
+        codes = codes if ctx.has_codes else None
+        nl = D
+        pw = params[0:2 * nl:2]
+        wa, ba, wf, bf, wv, bv, wr, br = params[2 * nl:2 * nl + 8]
+        dev = feat.device
+        M, F = feat.shape
+        cfc = 0 if codes is None else codes.shape[1]
+        need_feat = ctx.needs_input_grad[1]
+        need_codes = ctx.has_codes and ctx.needs_input_grad[2]
+        f32 = dict(device=dev, dtype=torch.float32)
+        g_raw = g_raw.contiguous()
+        lib = _lib.load()
+        ws = [torch.empty(0, device=dev, dtype=torch.uint8)]  # grown to the largest layer's need
+        grads = [None] * len(params)
+
+        def wg(n, k, dy, x):
+            need = lib.anerf_mlp_wgrad_workspace(M, n, k)
+            if ws[0].numel() < need:
+                ws[0] = torch.empty(need, device=dev, dtype=torch.uint8)
+            dw = torch.empty(n, k, **f32)
+            db = torch.empty(n, **f32)
+            wgrad(M, n, k, dy, x, dw, db, ws[0], dev, prec)
+            return dw, db
+
+        # rgb_linear: input gradient masked by relu(view layer) > 0
+        gzv = torch.empty(M, W // 2, **f32)
+        mm(M, W // 2, 3, [_seg(g_raw, 3)], sw(wr, True), None, False,
+             [(gzv, W // 2, W // 2, 0, g, False)], dev)
+        grads[2 * nl + 6], grads[2 * nl + 7] = wg(3, W // 2, g_raw, [_seg(g, W // 2)])
+        # views_linears[0]: gradients of feature (into gha[:, :W]), view columns of feat, framecodes
+        gha = torch.empty(M, W + 4, **f32)  # [g_feature | g_alpha] (ld padded to 16 B)
+        gha[:, W].copy_(g_raw[:, 3])
+        gha[:, W + 1:].zero_()  # (read as the ragged last 4-column group; the B planes are zero there)
+        gfeat = torch.empty(M, F, **f32) if need_feat else None
+        gcodes = torch.empty(M, cfc, **f32) if need_codes else None
+        outs = [(gha, W + 4, W, 0, None, False), (gfeat, F, nv, dnet, None, False)]
+        if cfc:
+            outs.append((gcodes, cfc, cfc, 0, None, False))
+        nvo = W + (nv + cfc if (need_feat or need_codes) else 0)
+        mm(M, nvo, W // 2, [_seg(gzv, W // 2)], sw(wv, True), None, False,
+             outs if nvo > W else outs[:1], dev)
+        av = [_seg(hf, W), _seg(feat, nv, dnet)] + ([_seg(codes, cfc)] if cfc else [])
+        grads[2 * nl + 4], grads[2 * nl + 5] = wg(W // 2, W + nv + cfc, gzv, av)
+        # feature_linear + alpha_linear: one input gradient, masked by relu(last hidden) > 0
+        gz = torch.empty(M, W, **f32)
+        mm(M, W, W + 1, [_seg(gha, W + 1)], sw(whead, True), None, False,
+             [(gz, W, W, 0, H[-1], False)], dev)
+        dwh, dbh = wg(W + 1, W, gha, [_seg(H[-1], W)])
+        grads[2 * nl + 2], grads[2 * nl + 3] = dwh[:W], dbh[:W]  # feature_linear
+        grads[2 * nl + 0], grads[2 * nl + 1] = dwh[W:], dbh[W:]  # alpha_linear
+        # the trunk, last layer first
+        segx = _seg(feat, dnet)
+        wrote_x = False
+        for i in range(D - 1, -1, -1):
+            if i == 0:
+                a, k = [segx], dnet
+            elif i - 1 == skip:
+                a, k = [segx, _seg(H[i - 1], W)], dnet + W
+            else:
+                a, k = [_seg(H[i - 1], W)], W
+            grads[2 * i], grads[2 * i + 1] = wg(W, k, gz, a)
+            if i == 0:
+                if need_feat:
+                    mm(M, dnet, W, [_seg(gz, W)], sw(pw[0], True), None, False,
+                         [(gfeat, F, dnet, 0, None, wrote_x)], dev)
+                break
+            gprev = torch.empty(M, W, **f32)
+            if i - 1 == skip:  # [x | h] input: the x part into the feature gradient, the h part masked
+                mm(M, k, W, [_seg(gz, W)], sw(pw[i], True), None, False,
+                     [(gfeat if need_feat else None, F, dnet, 0, None, False), (gprev, W, W, 0, H[i - 1], False)],
+                     dev)
+                wrote_x = need_feat
+            else:
+                mm(M, W, W, [_seg(gz, W)], sw(pw[i], True), None, False,
+                     [(gprev, W, W, 0, H[i - 1], False)], dev)
+            gz = gprev
+        return (None, gfeat, gcodes, *grads)
+
+
+def nerf_forward(net, feat, codes=None):
+    """raw [M, 4] of `train.NeRF` on the split-bf16 GEMMs (same parameters, autograd included;
+    precision net.mlp: "bf16x6" or "bf16x3")."""
+    cfg = net.cfg
+    if feat.dtype != torch.float32 or not feat.is_contiguous():
+        feat = feat.float().contiguous()
+    if codes is not None:
+        codes = codes.float().contiguous()
+    W, D = cfg.netwidth, cfg.netdepth
+    skip = cfg.skips[0] if cfg.skips[0] < D - 1 else -1
+    shape = (W, D, skip, net.dnet, cfg.input_ch_views, _lib.MLP_PRECISIONS[net.mlp])
+    params = []
+    for lin in net.pts_linears:
+        params += [lin.weight, lin.bias]
+    params += [net.alpha_linear.weight, net.alpha_linear.bias, net.feature_linear.weight, net.feature_linear.bias,
+               net.views_linears[0].weight, net.views_linears[0].bias, net.rgb_linear.weight, net.rgb_linear.bias]
+    return _MLP.apply(shape, feat, codes, *params)
+
+
+__all__ = ["nerf_forward", "split_weight", "gemm", "wgrad"]

@@ -278,8 +278,17 @@ class NeRF(nn.Module):
         if cfg.opt_framecode:
             self.framecodes = Optcodes(cfg.n_framecodes, cfg.framecode_size)
 
+    # "bf16x6" / "bf16x3": the hand-written split-bf16 GEMMs (mlp.py / anerf_gemm.hip); "fp32": torch GEMMs
+    mlp = "bf16x6"
+
     def forward(self, feat, cams=None):
         """feat [M, F] = [v | r | views] -> raw [M, 4] (rgb, alpha): forward_density + forward_view."""
+        if self.mlp in ("bf16x6", "bf16x3"):
+            from . import mlp as _mlp
+            codes = self.framecodes(cams) if self.cfg.opt_framecode else None
+            return _mlp.nerf_forward(self, feat, codes)
+        if self.mlp != "fp32":
+            raise ValueError(f"mlp={self.mlp!r}: 'bf16x6', 'bf16x3' or 'fp32'")
         x, x_skip, views = _SplitCols.apply(feat, self.dnet)
         h = x
         for i, lin in enumerate(self.pts_linears):
@@ -334,11 +343,14 @@ class TrainRayCaster(nn.Module):
     mode `forward`/`render_rays` run the stochastic, differentiable render path; in eval mode
     they delegate to the fused HIP render kernel (weights repacked when they changed)."""
 
-    def __init__(self, cfg, ckpt=None, device=None):
+    def __init__(self, cfg, ckpt=None, device=None, mlp="bf16x6"):
+        """mlp: arithmetic of the training MLP — "bf16x6" (hand-written split-bf16 GEMMs on the MFMA
+        pipe, fp32-accurate, mlp.py), "bf16x3" (the same, ~16-bit operands) or "fp32" (torch GEMMs);
+        the eval delegate uses cfg.precision."""
         super().__init__()
         self.cfg = cfg.validate()
-        if cfg.precision != "fp32":
-            pass  # the eval delegate uses cfg.precision; training is fp32
+        if mlp not in ("bf16x6", "bf16x3", "fp32"):
+            raise ValueError(f"mlp={mlp!r}: 'bf16x6', 'bf16x3' or 'fp32'")
         if isinstance(device, (str, torch.device)):
             dev = torch.device(device)  # (a CPU device holds the parameters only: checkpoints, no rendering)
         else:
@@ -354,6 +366,9 @@ class TrainRayCaster(nn.Module):
         cut = float(cfg.extra.get("cutoff_mm", 500.0)) * cfg.ext_scale
         self.embed_fn = _Embed(cfg.n_joints, cut)
         self.embeddirs_fn = _Embed(cfg.n_joints, cut)
+        for net in (self.network_fn, self.network_fine):
+            if net is not None:
+                net.mlp = mlp
         if ckpt is not None:
             self.load_checkpoint(ckpt)
         self.to(dev)

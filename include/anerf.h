@@ -36,6 +36,11 @@
  *   anerf_train_composite   NeRF.raw2outputs with raw_noise_std                core/networks/nerf.py:150-205
  *   anerf_train_composite_backward   its autograd
  *   anerf_train_importance  isample_from_lineseg + sample_pdf(det=False) + sort core/utils/ray_utils.py:157-201, 255-289
+ * The training MLP's linears (NeRF.forward / autograd, core/networks/nerf.py:94-148; the reference runs
+ * them as torch addmm over cat()-ed inputs, core/raycasters.py:557-577):
+ *   anerf_mlp_split_weights a weight (or its transpose) as bf16 hi / lo planes, once per step
+ *   anerf_mlp_gemm          forward (bias, relu) and input-gradient (relu' mask, accumulate) products
+ *   anerf_mlp_wgrad         weight + bias gradients
  */
 #ifndef ANERF_H
 #define ANERF_H
@@ -47,7 +52,7 @@
 extern "C" {
 #endif
 
-#define ANERF_ABI_VERSION 5
+#define ANERF_ABI_VERSION 6
 
 enum {
     ANERF_OK = 0,
@@ -336,6 +341,51 @@ int anerf_train_composite_backward(const anerf_model* m, const float* raw, const
 int anerf_train_importance(const float* z, const float* weights, int64_t n_rays, int32_t n_samples,
                            int32_t n_importance, const float* u, int32_t single_net, float* z_all,
                            int32_t* sorted_idx, void* stream);
+
+/* ---- training MLP linears on the bf16 MFMA pipe, fp32 in / out with split-bf16 operands:
+ *   ANERF_MLP_BF16X6  x = x0 + x1 + x2, w likewise, the six products with i + j <= 2 (fp32-accurate:
+ *                     the dropped terms are below 2^-23 of |x w|), fp32 accumulation
+ *   ANERF_MLP_BF16X3  x = x0 + x1, three products (~16 significant bits per operand) */
+enum { ANERF_MLP_BF16X3 = 3, ANERF_MLP_BF16X6 = 6 };
+/*
+ * An operand is up to 3 column segments (the reference's torch.cat along features, never
+ * materialised here): segment i holds columns [sum of earlier cols, + cols) at p[row * ld + c]. */
+typedef struct {
+    const float* p;
+    int64_t ld;    /* row stride in floats (>= cols) */
+    int32_t cols;
+} anerf_seg;
+
+/* An output column segment: out[row * ld + c] = v, v *= (mask[row * ldm + c] > 0) when mask is set
+ * (relu backward by the saved activation), v += out[...] when accumulate; p NULL discards it. */
+typedef struct {
+    float* p;
+    int64_t ld;
+    int32_t cols;
+    const float* mask;
+    int64_t ldm;
+    int32_t accumulate;
+} anerf_oseg;
+
+/* Bytes of one split operand of `rows` x `cols` (anerf_mlp_split_weights' output). */
+size_t anerf_mlp_split_bytes(int32_t rows, int32_t cols, int32_t precision);
+/* w [n][k] (row stride ldw) -> bf16 planes (hi, then lo), zero padded; transpose != 0 splits w^T
+ * ([k][n], the B operand of an input gradient).  out: anerf_mlp_split_bytes(rows, cols) bytes. */
+int anerf_mlp_split_weights(const float* w, int32_t n, int32_t k, int64_t ldw, int32_t transpose,
+                            int32_t precision, void* out, void* stream);
+/* C[m][n] = act(sum_k A[m][k] B[n][k] + bias[n]); A: n_a segments adding up to k columns; B: split
+ * [n][k] (the forward's weight, or the transposed weight of an input gradient); bias NULL or [n];
+ * relu != 0 applies max(., 0); C: n_c segments adding up to n columns. */
+int anerf_mlp_gemm(int64_t m, int32_t n, int32_t k, const anerf_seg* a, int32_t n_a, const void* b_split,
+                   int32_t precision, const float* bias, int32_t relu, const anerf_oseg* c, int32_t n_c,
+                   void* stream);
+/* Workspace bytes of anerf_mlp_wgrad for these sizes. */
+size_t anerf_mlp_wgrad_workspace(int64_t m, int32_t n, int32_t k);
+/* dW[n][k] (+)= sum_m dY[m][n] X[m][k] and db[n] (+)= sum_m dY[m][n] (db may be NULL); X: n_x
+ * segments adding up to k columns.  Summed over row slabs in a fixed order (deterministic). */
+int anerf_mlp_wgrad(int64_t m, int32_t n, int32_t k, const float* dy, int64_t lddy, const anerf_seg* x, int32_t n_x,
+                    int32_t precision, float* dw, int64_t lddw, float* db, int32_t accumulate, void* workspace,
+                    size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,163 @@
+"""GPU numerics of the training MLP's split-bf16 GEMMs (a-nerf_amd/csrc/anerf_gemm.hip) against
+plain torch fp64 products of the same operands, and of the whole network (mlp.nerf_forward,
+forward + autograd) against the torch fp32 path of the same module.
+
+Bound for one product: bf16x3 keeps ~16 significant bits per operand (x = x0 + x1, bf16 RNE each;
+dropped x1 w1), so |C - C_ref| <= 2^-15 * (|A| |B|^T) + fp32 accumulation slack — the tests use
+4e-5 (|A| |B|^T) + 1e-6; bf16x6 (three planes, six products) is fp32-accurate: 2e-6 (|A| |B|^T) + 1e-6
+(fp32 accumulation of up to ~1000 terms).
+"""
+import importlib
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+mlp = importlib.import_module("a-nerf_amd.mlp")
+train = importlib.import_module("a-nerf_amd.train")
+anerf = importlib.import_module("a-nerf_amd")
+syn = importlib.import_module("a-nerf_amd.synthetic")
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _cuda():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+REL = {3: 4e-5, 6: 2e-6}
+
+
+def _bound(a, b, prec=3):
+    return REL[prec] * (a.double().abs() @ b.double().abs().t()) + 1e-6
+
+
+@pytest.mark.parametrize("prec", [3, 6])
+@pytest.mark.parametrize("m,n,ks", [(1000, 257, (256, 648, 16)), (4096, 256, (432, 256)), (77, 3, (128,)),
+                                    (130, 128, (904,)), (0, 64, (32,))])
+def test_gemm_forward_segments_bias_relu(m, n, ks, prec):
+    torch.manual_seed(m + n)
+    k = sum(ks)
+    parts = [torch.randn(m, c + 4, device=DEV)[:, :c] for c in ks]  # strided rows (ld = c + 4)
+    a = torch.cat(parts, 1) if m else torch.empty(0, k, device=DEV)
+    w = torch.randn(n, k, device=DEV) / k ** 0.5
+    b = torch.randn(n, device=DEV)
+    out = torch.full((m, n + 5), 7.0, device=DEV)
+    if m:
+        mlp.gemm(m, n, k, [mlp._seg(p, p.shape[1]) for p in parts], mlp.split_weight(w, False, prec), b, True,
+                 [(out, n + 5, n, 0, None, False)], torch.device(DEV), prec)
+    ref = torch.relu(a.double() @ w.double().t() + b.double())
+    assert torch.all(out[:, n:] == 7.0)  # nothing written past the segment
+    err = (out[:, :n].double() - ref).abs()
+    assert torch.all(err <= _bound(a, w, prec)), float(err.max())
+
+
+def test_gemm_rejects_misaligned_segments():
+    x = torch.randn(64, 35, device=DEV)
+    w = torch.randn(16, 34, device=DEV)
+    with pytest.raises(mlp._lib.AnerfError, match="16-byte aligned"):
+        mlp.gemm(64, 16, 34, [mlp._seg(x, 2), mlp._seg(x, 32, 2)], mlp.split_weight(w), None, False,
+                 [(torch.empty(64, 16, device=DEV), 16, 16, 0, None, False)], torch.device(DEV))
+    with pytest.raises(mlp._lib.AnerfError, match="ld < cols"):  # the last segment is read to a multiple of 4
+        z = torch.randn(64, 3, device=DEV)
+        mlp.gemm(64, 16, 3, [mlp._seg(z, 3)], mlp.split_weight(w[:, :3].contiguous()), None, False,
+                 [(torch.empty(64, 16, device=DEV), 16, 16, 0, None, False)], torch.device(DEV))
+
+
+@pytest.mark.parametrize("prec", [3, 6])
+def test_gemm_input_gradient_mask_accumulate_discard(prec):
+    torch.manual_seed(1)
+    m, k, n = 2000, 256, 688  # the skip layer's input gradient: [x (432) | h (256)]
+    gz = torch.randn(m, k, device=DEV)
+    w = torch.randn(k, n, device=DEV) / k ** 0.5  # the layer's weight [out = k][in = n]
+    h = torch.relu(torch.randn(m, 256, device=DEV))
+    gx = torch.randn(m, 432, device=DEV)
+    gx0 = gx.clone()
+    gh = torch.empty(m, 256, device=DEV)
+    mlp.gemm(m, n, k, [mlp._seg(gz, k)], mlp.split_weight(w, True, prec), None, False,
+             [(gx, 432, 432, 0, None, True), (gh, 256, 256, 0, h, False)], torch.device(DEV), prec)
+    full = gz.double() @ w.double()
+    bound = _bound(gz, w.t(), prec)
+    assert torch.all((gx.double() - (gx0.double() + full[:, :432])).abs() <= bound[:, :432] + 1e-6)
+    ref_h = torch.where(h > 0, full[:, 432:], torch.zeros_like(full[:, 432:]))
+    assert torch.all((gh.double() - ref_h).abs() <= bound[:, 432:])
+    # a discarded segment writes nothing
+    keep = gx.clone()
+    mlp.gemm(m, n, k, [mlp._seg(gz, k)], mlp.split_weight(w, True, prec), None, False,
+             [(None, 432, 432, 0, None, False), (gh, 256, 256, 0, h, False)], torch.device(DEV), prec)
+    assert torch.equal(gx, keep)
+
+
+@pytest.mark.parametrize("prec", [3, 6])
+@pytest.mark.parametrize("m,n,ks", [(131072, 256, (256,)), (5000, 257, (256,)), (3001, 3, (128,)),
+                                    (777, 128, (256, 648, 16)), (40, 256, (432, 256))])
+def test_wgrad_and_bias_gradient(m, n, ks, prec):
+    torch.manual_seed(m)
+    k = sum(ks)
+    dy = torch.randn(m, n + 1, device=DEV)[:, :n]
+    parts = [torch.randn(m, c, device=DEV) for c in ks]
+    x = torch.cat(parts, 1)
+    lib = mlp._lib.load()
+    ws = torch.empty(lib.anerf_mlp_wgrad_workspace(m, n, k), device=DEV, dtype=torch.uint8)
+    dw = torch.empty(n, k, device=DEV)
+    db = torch.empty(n, device=DEV)
+    mlp.wgrad(m, n, k, dy, [mlp._seg(p, p.shape[1]) for p in parts], dw, db, ws, torch.device(DEV), prec)
+    ref = dy.double().t() @ x.double()
+    bound = 2 * REL[prec] * (dy.double().abs().t() @ x.double().abs()) + 1e-5
+    assert torch.all((dw.double() - ref).abs() <= bound), float((dw.double() - ref).abs().max())
+    ref_b = dy.double().sum(0)
+    assert torch.all((db.double() - ref_b).abs() <= 1e-5 * dy.double().abs().sum(0) + 1e-5)
+
+
+def test_wgrad_is_deterministic():
+    torch.manual_seed(3)
+    m, n, k = 50000, 256, 256
+    dy, x = torch.randn(m, n, device=DEV), torch.randn(m, k, device=DEV)
+    lib = mlp._lib.load()
+    ws = torch.empty(lib.anerf_mlp_wgrad_workspace(m, n, k), device=DEV, dtype=torch.uint8)
+    outs = []
+    for _ in range(2):
+        dw, db = torch.empty(n, k, device=DEV), torch.empty(n, device=DEV)
+        mlp.wgrad(m, n, k, dy, [mlp._seg(x, k)], dw, db, ws, torch.device(DEV))
+        outs.append((dw, db))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("impl", ["bf16x6", "bf16x3"])
+@pytest.mark.parametrize("D,W,fc", [(8, 256, False), (4, 128, True)])
+def test_nerf_forward_backward_matches_fp32_module(D, W, fc, impl):
+    """The whole network (skip layer, heads, view layer, framecodes) and its autograd vs the same
+    module on torch's fp32 GEMMs."""
+    cfg = anerf.RenderConfig(netdepth=D, netwidth=W, opt_framecode=fc, n_framecodes=5 if fc else 0).validate()
+    ck = syn.make_checkpoint(5, n_joints=24, D=D, W=W, fine=False, use_framecode=fc, n_framecodes=5)
+    torch.manual_seed(0)
+    M = 3000
+    feat = (torch.rand(M, cfg.feature_dim, device=DEV) * 2 - 1)
+    cams = torch.randint(0, 5, (M,), device=DEV) if fc else None
+    gout = torch.randn(M, 4, device=DEV)
+    res = {}
+    for mode in (impl, "fp32"):
+        tr = train.TrainRayCaster(cfg, ck, mlp=mode).train()
+        net = tr.network_fn
+        f = feat.clone().requires_grad_(True)
+        raw = net(f, cams)
+        (raw * gout).sum().backward()
+        res[mode] = (raw.detach(), f.grad, {k: p.grad for k, p in net.named_parameters()})
+    raw_b, gf_b, gp_b = res[impl]
+    raw_f, gf_f, gp_f = res["fp32"]
+    assert float((raw_b - raw_f).abs().max()) <= 1e-4 * max(1.0, float(raw_f.abs().max()))
+    # gradients: relative Frobenius error (a pre-activation within rounding of 0 may take the other
+    # relu branch in either implementation; elementwise maxima are pinned by the reference goldens
+    # in test_gpu_train.py)
+    def rel(a, b):
+        return float((a.double() - b.double()).norm() / max(b.double().norm(), 1e-30))
+    row = ((gf_b.double() - gf_f.double()).norm(dim=1) / gf_f.double().norm(dim=1).clamp_min(1e-30))
+    q99 = float(torch.quantile(row.float(), 0.99))
+    print(f"{impl} feature gradient: rel {rel(gf_b, gf_f):.2e}, per-row 99% {q99:.2e}, max {float(row.max()):.2e}")
+    assert q99 <= 1e-3 and rel(gf_b, gf_f) <= 5e-3, (q99, rel(gf_b, gf_f))
+    for k in gp_f:
+        assert rel(gp_b[k], gp_f[k]) <= 5e-3, (k, rel(gp_b[k], gp_f[k]))

@@ -41,10 +41,10 @@ def _loss(out, tgt, bg):
             F.mse_loss(out["rgb0"] + (1 - out["acc0"])[:, None] * bg, tgt))
 
 
-def _run(name):
+def _run(name, mlp="bf16x6"):
     g = Golden(name)
     m = g.meta
-    tr = train.TrainRayCaster(g.cfg, g.ckpt).train()
+    tr = train.TrainRayCaster(g.cfg, g.ckpt, mlp=mlp).train()
     dev = torch.device("cuda:0")
     if m.get("global_step") is not None:
         # Trainer.train_batch's call (core/trainer.py:263-265), through the DataParallel-style alias
@@ -65,9 +65,11 @@ def _run(name):
     return g, tr, sk, out, loss
 
 
-@pytest.fixture(scope="module", params=TRAIN)
+# the training MLP on the hand-written split-bf16 GEMMs (bf16x6, the default) and on torch's fp32 GEMMs
+@pytest.fixture(scope="module", params=[(n, mlp) for n in TRAIN for mlp in ("bf16x6", "fp32")],
+                ids=lambda p: f"{p[0]}-{p[1]}")
 def run(request):
-    return _run(request.param)
+    return _run(*request.param)
 
 
 def test_train_outputs_match_reference(run):

@@ -34,6 +34,7 @@ def test_split_weight_nerf_matches_concatenating_reference():
         g = Golden(name)
         cfg = g.cfg
         net = train.NeRF(cfg).double()
+        net.mlp = "fp32"  # the torch form (the split-bf16 GEMMs are GPU-only: test_gpu_mlp.py)
         sd = {k: torch.from_numpy(np.asarray(v, np.float64)) for k, v in g.ckpt["network_fn_state_dict"].items()}
         net.load_state_dict(sd)
         feat = torch.from_numpy(np.random.default_rng(0).normal(size=(37, cfg.feature_dim)))
