@@ -39,6 +39,7 @@ namespace {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BM = 128, BN = 128, NTHR = 256;
@@ -79,14 +80,13 @@ struct NTArgs {
     SegD a[MAXSEG];
     int na;
     const unsigned short* b;  // split weights, fragment-major (split_weights_kernel)
-    int bplane_blocks;        // 32-column blocks of B (padded)
     int ksteps;               // k16 steps of B (padded)
     const float* bias;
     int relu;
     OSegD c[MAXSEG];
     int nc;
     int tiles_n, total;
-    int dbg;  // diagnostic ablations (ANERF_GEMM_DBG): 1 no stores, 2 B fragments of step 0 only, 4 A of step 0 only
+    unsigned long long* stamps;  // diagnostic timeline (ANERF_GEMM_STAMPS): [wg][wave][64] s_memtime, or null
 };
 
 struct TNArgs {
@@ -141,6 +141,13 @@ struct RowSrc {
 // (values pinned in registers: without the pin, clang folds the per-lane select between the three
 // pointers into an indexed load from a stack copy of the struct — scratch traffic in the k loop)
 __device__ __forceinline__ void pin64(unsigned long long& x) { asm volatile("" : "+v"(x)); }
+// a uniform kernel-argument value made opaque (in a VGPR) before per-lane selects between such
+// values: see pin64
+template <class T>
+__device__ __forceinline__ T opaque(T x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
 
 // rows past M read row M - 1 (finite; their outputs are never stored)
 __device__ __forceinline__ RowSrc row_src(const SegD* seg, int nseg, long long row, long long M, int K) {
@@ -252,84 +259,164 @@ __device__ __forceinline__ void mma_step(const unsigned short* st, int wr, int w
 }
 
 // ---------------------------------------------------------------- forward / input gradient
-// 128 rows x 256 columns per workgroup (4 waves, 2 x 2: 64 rows x 128 columns = 2 x 4 blocks each).
-// A (activations, fp32 from HBM) is split once per workgroup into LDS planes, two k16 steps of
-// loads in flight.  B (the split weights, a few hundred KB shared by every workgroup) is read
-// straight from L2 as MFMA fragments — its planes are stored fragment-major (1 KB per (32-column
-// block, k16 step, plane), lane order), so each fragment load is one contiguous 1 KB wave access —
-// and never touches LDS; the next step's fragments are loaded under the current step's MFMAs.
+// 128 rows x 256 columns per workgroup (4 waves, 2 x 2: 64 rows x 128 columns = 2 x 4 blocks each,
+// one wave per SIMD).  A (activations, fp32 from HBM) is staged 64 columns at a time: loaded into
+// registers a whole stage ahead (192 MFMAs per wave per stage cover the HBM latency), split once
+// per workgroup into NPL bf16 LDS planes; one barrier per stage.  B (the split weights, a few
+// hundred KB shared by every workgroup) is read straight from L2 as MFMA fragments — stored
+// fragment-major, 1 KB per (32-column block, k16 step, plane) in lane order, so each load is one
+// contiguous wave access — one k16 step ahead, and never touches LDS.
 constexpr int BNW = 256;
+constexpr int SK = 64;        // k columns per stage
+constexpr int SLDP = SK + 8;  // LDS row pitch (bf16): 144 B, an odd number of 16 B chunks
 
 template <int NPL>
-struct BFrag {
-    u32x4 v[NPL][4];  // [plane][column block of this wave]
+struct NTGeo {
+    static constexpr int PLANE = BM * SLDP;
+    static constexpr int STAGE = NPL * PLANE;
+    static constexpr int TAB = 2 * STAGE * 2;     // byte offset of the segment tables
+    static constexpr int LDS_BYTES = TAB + 256;
+};
+
+// operand / output segment tables in LDS: per-lane segment choices read their pointer and stride
+// from here (an indexed read of the kernel-argument struct makes clang copy it to scratch, and a
+// scratch access in the k loop waits out every outstanding load)
+struct SegTab {
+    const float* p[MAXSEG];
+    long long ld[MAXSEG];
+    float* op[MAXSEG];
+    long long old[MAXSEG];
+    const float* mask[MAXSEG];
+    long long ldm[MAXSEG];
 };
 
 template <int NPL>
+struct BFrag {
+    u32x4 v[NPL][2];  // [plane][column block of this wave]
+};
+
+template <int NPL>
+// diagnostic timeline: s_memtime at numbered points of wave (tid / 64) of the first 64 workgroups
+#define TL(i)                                                                                  \
+    do {                                                                                       \
+        if (tl) {                                                                              \
+            const unsigned long long t_ = __builtin_amdgcn_s_memtime();                        \
+            if (lane == 0 && (i) < 64) tl[(i)] = t_;                                           \
+        }                                                                                      \
+    } while (0)
+
 __global__ __launch_bounds__(NTHR, 1) void mlp_nt_kernel(NTArgs g) {
-    using G = Geo<NPL>;
-    constexpr int BK = G::BK, E = G::E;
-    static_assert(BK == 16 && E == 8, "one k16 step per stage");
+    using G = NTGeo<NPL>;
     extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
     const int logical = xcd_logical(blockIdx.x, g.total);
     const int mt = logical / g.tiles_n, nt = logical % g.tiles_n;
     const long long m0 = (long long)mt * BM;
     const int n0 = nt * BNW;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wr = wave >> 1, wc = wave & 1;
-    // staging: each wave stages 32 rows; lanes l and l + 32 the two 8-column halves of one row (the
-    // 8-lane groups of a ds_write_b128 then hit 8 distinct rows: conflict-free at the 48 B pitch)
-    const int lr = 32 * wave + (lane & 31), lq = E * (lane >> 5);
-    const int nk = (g.K + BK - 1) / BK;
-    const RowSrc src = row_src(g.a, g.na, m0 + lr, g.M, g.K);
-    // this wave's B fragments: column blocks nb0 .. nb0 + 3 (clamped to the last block of the
-    // padded planes: past N they are zero, and the outputs are not stored)
-    const int nb0 = (n0 + 128 * wc) / 32;
-    const int nbk = g.bplane_blocks;
-    const unsigned short* bl = g.b + lane * 8;
+    // waves 1 x 4: wave w computes all 128 rows x columns 64 w .. 64 w + 63 (4 x 2 blocks), so the
+    // four waves load disjoint B fragments (each fragment is read once per workgroup)
+    // (kernel-argument fields as locals: referencing `g` inside the lambdas makes clang copy the
+    // whole argument struct to scratch and reload fields from there in the loop)
+    const int Kd = g.K, ksteps = g.ksteps;
+    unsigned long long* const tl = (g.stamps && blockIdx.x < 64) ? g.stamps + (blockIdx.x * 4 + wave) * 64 : nullptr;
+    TL(0);
+    const unsigned short* const bbase = g.b;
+    const int nst = (Kd + SK - 1) / SK;  // stages
+    const int nk = (Kd + 15) / 16;        // k16 steps of the B planes
+    // staging: float4 f = i * 256 + tid (i = 0..7) is row f >> 4, columns 4 (f & 15) .. + 3 of the
+    // stage, so a wave loads 4 whole 256 B row pieces per instruction and writes 8 B per plane
+    const int sr = tid >> 4, sc = 4 * (tid & 15);
+    // segment row bases (row sr; row sr + 16 i adds 16 i ld)
+    const int na = g.na;
+    SegTab* const tab = reinterpret_cast<SegTab*>(reinterpret_cast<char*>(lds) + G::TAB);
+    if (tid < MAXSEG) {
+        const int t = tid < na ? tid : 0;
+        tab->p[tid] = g.a[t].p;
+        tab->ld[tid] = g.a[t].ld;
+        const int u = tid < g.nc ? tid : 0;
+        tab->op[tid] = g.c[u].p;
+        tab->old[tid] = g.c[u].ld;
+        tab->mask[tid] = g.c[u].mask;
+        tab->ldm[tid] = g.c[u].ldm;
+    }
+    const int st1 = na > 1 ? g.a[1].start : Kd, st2 = na > 2 ? g.a[2].start : Kd;
+    const int kmax4 = (Kd + 3) / 4 * 4 - 4;
+    const long long mlast = g.M - 1;
+    // this wave's B fragments: column blocks nb0 .. nb0 + 3 (the planes are zero padded to whole
+    // 256-column tiles, so no block index needs a clamp)
+    const int nb0 = (n0 + 64 * wave) / 32;
+    const long long bstride = (long long)ksteps * NPL * 512;  // elements per 32-column block
+    const unsigned short* bl = bbase + nb0 * bstride + lane * 8;
 
-    f32x16 acc[2][4];
+    f32x16 acc[4][2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x16{0};
+        for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{0};
 
     auto fetch_b = [&](int kt, BFrag<NPL>& f) {
         kt = kt < nk ? kt : nk - 1;
-        if (g.dbg & 2) kt = 0;
+        const unsigned short* bk = bl + (long long)kt * NPL * 512;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            int nb = nb0 + j;
-            nb = nb < nbk ? nb : nbk - 1;
+        for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int p = 0; p < NPL; ++p)
-                f.v[p][j] = *reinterpret_cast<const u32x4*>(bl + (((long long)nb * g.ksteps + kt) * NPL + p) * 512);
+            for (int p = 0; p < NPL; ++p) f.v[p][j] = *reinterpret_cast<const u32x4*>(bk + j * bstride + p * 512);
+    };
+    // the stage's 8 float4 of this thread: unconditional loads (clamped row / column, zeroed when
+    // staged), so the compiler's counted vmcnt waits stay exact
+    f32x4 R[8];
+    auto fetch_a = [&](int st) {
+        st = st < nst ? st : nst - 1;
+        int kc = st * SK + sc;
+        kc = kc < kmax4 ? kc : kmax4;
+        const int si = kc >= st2 ? 2 : (kc >= st1 ? 1 : 0);
+        const float* base = tab->p[si];
+        const long long ld = tab->ld[si];
+        const int col = kc - (si == 2 ? st2 : (si == 1 ? st1 : 0));
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            long long m = m0 + sr + 16 * i;
+            m = m < mlast ? m : mlast;
+            R[i] = *(gf32x4*)(base + m * ld + col);
         }
     };
-    auto fetch_a = [&](int kt, f32x4 (&av)[2]) {
-        kt = kt < nk ? kt : nk - 1;
-        if (g.dbg & 4) kt = 0;
-        load_row<E>(src, kt * BK + lq, av);
-    };
-    auto stage_a = [&](int s, int kt, const f32x4 (&av)[2]) {
-        store_split_groups<NPL, E>(lds + s * G::STAGE, lr, lq, kt * BK + lq, g.K, av);
-    };
-    auto step = [&](int s, const BFrag<NPL>& f) {
-        const unsigned short* A = lds + s * G::STAGE;
-        const int r = lane & 31, kh = 8 * (lane >> 5);
-        bf16x8 a[NPL][2];
+    auto stage_a = [&](int buf, int st) {
+        unsigned short* P = lds + buf * G::STAGE;
+        const bool live = st * SK + sc < Kd;  // (the last group of a ragged K is finite, B is 0 there)
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < 8; ++i) {
+            float r[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) r[e] = live ? R[i][e] : 0.0f;
+#pragma unroll
+            for (int p = 0; p < NPL; ++p) {
+                bf16x4 h;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) h[e] = (__bf16)r[e];
+                if (p + 1 < NPL) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) r[e] -= (float)h[e];
+                }
+                *reinterpret_cast<bf16x4*>(P + p * G::PLANE + (sr + 16 * i) * SLDP + sc) = h;
+            }
+        }
+    };
+    auto step = [&](int buf, int ks, const BFrag<NPL>& f) {
+        const unsigned short* A = lds + buf * G::STAGE;
+        const int r = lane & 31, kh = 16 * ks + 8 * (lane >> 5);
+        bf16x8 a[NPL][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int p = 0; p < NPL; ++p)
-                a[p][i] = *reinterpret_cast<const bf16x8*>(A + p * G::PLANE + (64 * wr + 32 * i + r) * G::LDP + kh);
+                a[p][i] = *reinterpret_cast<const bf16x8*>(A + p * G::PLANE + (32 * i + r) * SLDP + kh);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < 2; ++j) {
             bf16x8 b[NPL];
 #pragma unroll
             for (int p = 0; p < NPL; ++p) b[p] = __builtin_bit_cast(bf16x8, f.v[p][j]);
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
+            for (int i = 0; i < 4; ++i) {
                 f32x16 c = acc[i][j];
                 if constexpr (NPL == 3) {
                     c = mfma(a[2][i], b[0], c);
@@ -342,86 +429,159 @@ __global__ __launch_bounds__(NTHR, 1) void mlp_nt_kernel(NTArgs g) {
             }
         }
     };
-    // register slots are compile-time (a runtime-indexed register array would force each load to
-    // complete on the spot); fetches past the last step reload it (unconditional loads keep the
-    // compiler's counted vmcnt waits exact)
-    f32x4 a0[2], a1[2];
     BFrag<NPL> f0, f1;
-    fetch_a(0, a0);
-    fetch_a(1, a1);
+    __syncthreads();  // (the segment tables)
+    fetch_a(0);
     fetch_b(0, f0);
-    stage_a(0, 0, a0);
+    stage_a(0, 0);
+    TL(1);
+    fetch_a(1);
     __syncthreads();
-    for (int kt = 0; kt < nk; kt += 2) {
-        fetch_a(kt + 2, a0);
-        fetch_b(kt + 1, f1);
-        step(0, f0);
-        if (kt + 1 < nk) stage_a(1, kt + 1, a1);
+    TL(2);
+    // (sched_barrier after every fetch: without it the scheduler sinks the loads to their first use
+    // to save registers, and each fragment then waits out its full L2 round trip)
+    for (int st = 0; st < nst; ++st) {
+        const int buf = st & 1, k0 = 4 * st;
+        // four k16 steps; B fragments one step ahead in the other register set
+        fetch_b(k0 + 1, f1);
+        __builtin_amdgcn_sched_barrier(0);
+        step(buf, 0, f0);
+        __builtin_amdgcn_sched_barrier(0);
+        TL(3 + 8 * st);
+        fetch_b(k0 + 2, f0);
+        __builtin_amdgcn_sched_barrier(0);
+        step(buf, 1, f1);
+        __builtin_amdgcn_sched_barrier(0);
+        TL(4 + 8 * st);
+        fetch_b(k0 + 3, f1);
+        __builtin_amdgcn_sched_barrier(0);
+        step(buf, 2, f0);
+        __builtin_amdgcn_sched_barrier(0);
+        TL(5 + 8 * st);
+        fetch_b(k0 + 4, f0);
+        __builtin_amdgcn_sched_barrier(0);
+        step(buf, 3, f1);
+        __builtin_amdgcn_sched_barrier(0);
+        TL(6 + 8 * st);
+        if (st + 1 < nst) {
+            stage_a(buf ^ 1, st + 1);  // (its loads were issued a stage ago)
+            TL(7 + 8 * st);
+            fetch_a(st + 2);
+            __builtin_amdgcn_sched_barrier(0);
+        }
         __syncthreads();
-        if (kt + 1 >= nk) break;
-        fetch_a(kt + 3, a1);
-        fetch_b(kt + 2, f0);
-        step(1, f1);
-        if (kt + 2 < nk) stage_a(0, kt + 2, a0);
-        __syncthreads();
+        TL(8 + 8 * st);
     }
-    // epilogue: lane holds column n = .. + (lane & 31), rows (r & 3) + 8 (r >> 2) + 4 (lane >> 5).
-    // The mask / accumulate operands of a 16-row block are loaded up front from clamped rows (no
-    // load under a per-element branch: each would wait for its own round trip).
+    TL(60);
+    // epilogue through LDS, 64 rows at a time: the waves write their accumulators (lane = column
+    // (lane & 31), registers = rows (r & 3) + 8 (r >> 2) + 4 (lane >> 5)) into a [64][260] fp32
+    // tile, then every wave instruction handles one whole 1 KB output row with 16 B per lane
+    // (bias, relu, relu' mask, accumulate, segment split).  Writing the accumulators straight out
+    // scatters 128 B pieces over 64 rows per instruction and ran at a third of HBM speed.
+    constexpr int TP = 260;  // tile pitch (floats)
+    float* const tile = reinterpret_cast<float*>(lds);
+    const int cs1 = g.nc > 1 ? g.c[1].start : g.N, cs2 = g.nc > 2 ? g.c[2].start : g.N;
     const bool need_mask = g.c[0].mask || (g.nc > 1 && g.c[1].mask) || (g.nc > 2 && g.c[2].mask);
-    const bool need_acc = g.c[0].accum || (g.nc > 1 && g.c[1].accum) || (g.nc > 2 && g.c[2].accum);
+    const float* const bias = g.bias;
+    const int relu = g.relu;
+    const int Nd = g.N;
+    const long long Md = g.M;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int n = n0 + 128 * wc + 32 * j + (lane & 31);
-        if (n >= g.N) continue;
-        // output segment of column n, selected from rvalue copies of the uniform fields (see load_row)
-        const OSegD c0 = g.c[0], c1 = g.c[1], c2 = g.c[2];
-        const bool in2 = g.nc > 2 && n >= c2.start, in1 = !in2 && g.nc > 1 && n >= c1.start;
-        float* const op = in2 ? c2.p + 0 : (in1 ? c1.p + 0 : c0.p + 0);
-        if (!op) continue;  // a discarded segment (a gradient nobody needs)
-        const long long old = in2 ? c2.ld + 0 : (in1 ? c1.ld + 0 : c0.ld + 0);
-        const float* const mp = in2 ? c2.mask + 0 : (in1 ? c1.mask + 0 : c0.mask + 0);
-        const long long ldm = in2 ? c2.ldm + 0 : (in1 ? c1.ldm + 0 : c0.ldm + 0);
-        const int acc_out = in2 ? c2.accum + 0 : (in1 ? c1.accum + 0 : c0.accum + 0);
-        const int col = n - (in2 ? c2.start + 0 : (in1 ? c1.start + 0 : 0));
-        const float* const mq = mp ? mp : op;  // (a valid address when this segment has no mask)
-        const long long ldq = mp ? ldm : old;
-        const float b = g.bias ? g.bias[n] : 0.0f;
-        const int ldo = (int)old, ldmq = (int)ldq;
+    for (int hlf = 0; hlf < 2; ++hlf) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const long long mb = m0 + 64 * wr + 32 * i + 4 * (lane >> 5);
-            const int rows_left = (int)(g.M - mb < 32 ? g.M - mb : 32);  // rows mb + d, d < rows_left
-            float* const orow = op + mb * old + col;
-            const float* const mrow = mq + mb * ldq + col;
-            float mv[16], cv[16];
-            if (need_mask) {
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    int d = (r & 3) + 8 * (r >> 2);
-                    d = d < rows_left ? d : rows_left - 1;
-                    mv[r] = *(gfloat*)(mrow + d * ldmq);
+                    const int row = 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                    tile[row * TP + 64 * wave + 32 * j + (lane & 31)] = acc[2 * hlf + i][j][r];
+                }
+        __syncthreads();
+        // thread t: rows q * 4 + (t >> 6) (q = 0..15), columns 4 (t & 63) .. + 3
+        const int c4 = 4 * lane;
+        const int n = n0 + c4;
+        if (n < Nd) {
+            const int si = n >= cs2 ? 2 : (n >= cs1 ? 1 : 0);
+            float* const op = tab->op[si];
+            const long long old = tab->old[si];
+            const float* const mp = tab->mask[si];
+            const long long ldm = tab->ldm[si];
+            const int acc_out = si == 2 ? g.c[2].accum : (si == 1 ? g.c[1].accum : g.c[0].accum);
+            const int start = si == 2 ? cs2 : (si == 1 ? cs1 : 0);
+            const int col = n - start;
+            const int send = si == 2 ? Nd : (si == 1 ? cs2 : cs1);  // end of this segment
+            // the whole float4 inside one segment and 16 B aligned: vector path, else per element
+            const bool vec = n + 4 <= send && ((((uintptr_t)(op + col)) | (old * 4)) & 15) == 0 &&
+                             (!mp || ((((uintptr_t)(mp + col)) | (ldm * 4)) & 15) == 0);
+            f32x4 bv = {0.0f, 0.0f, 0.0f, 0.0f};
+            if (bias) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) bv[e] = n + e < Nd ? bias[n + e] : 0.0f;
+            }
+            // mask / accumulate operands of all 16 rows first (clamped rows: no load waits on a branch)
+            const bool need_acc = acc_out != 0;
+            f32x4 mk[16], ov[16];
+            if (vec && op && need_mask && mp) {
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    long long m = m0 + 64 * hlf + 4 * q + wave;
+                    m = m < Md ? m : Md - 1;
+                    mk[q] = *(gf32x4*)(mp + m * ldm + col);
                 }
             }
-            if (need_acc) {
+            if (vec && op && need_acc) {
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    int d = (r & 3) + 8 * (r >> 2);
-                    d = d < rows_left ? d : rows_left - 1;
-                    cv[r] = *(gfloat*)(orow + d * ldo);
+                for (int q = 0; q < 16; ++q) {
+                    long long m = m0 + 64 * hlf + 4 * q + wave;
+                    m = m < Md ? m : Md - 1;
+                    ov[q] = *(gf32x4*)(op + m * old + col);
                 }
             }
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int d = (r & 3) + 8 * (r >> 2);
-                float v = acc[i][j][r] + b;
-                if (g.relu) v = fmaxf(v, 0.0f);
-                if (need_mask && mp && !(mv[r] > 0.0f)) v = 0.0f;
-                if (need_acc && acc_out) v += cv[r];
-                if (d < rows_left && !(g.dbg & 1)) orow[d * ldo] = v;
+            for (int q = 0; q < 16; ++q) {
+                const int row = 4 * q + wave;
+                const long long m = m0 + 64 * hlf + row;
+                f32x4 v = *reinterpret_cast<const f32x4*>(tile + row * TP + c4);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    v[e] += bv[e];
+                    if (relu) v[e] = fmaxf(v[e], 0.0f);
+                }
+                if (vec) {
+                    if (op && m < Md) {
+                        if (need_mask && mp) {
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) v[e] = mk[q][e] > 0.0f ? v[e] : 0.0f;
+                        }
+                        if (need_acc) {
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) v[e] += ov[q][e];
+                        }
+                        *reinterpret_cast<f32x4*>(op + m * old + col) = v;
+                    }
+                } else if (m < Md) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int ne = n + e;
+                        if (ne >= Nd) break;
+                        const int se = ne >= cs2 ? 2 : (ne >= cs1 ? 1 : 0);
+                        float* const ope = tab->op[se];
+                        if (!ope) continue;
+                        const int ce = ne - (se == 2 ? cs2 : (se == 1 ? cs1 : 0));
+                        const float* const mpe = tab->mask[se];
+                        float x = v[e];
+                        if (mpe && !(mpe[m * tab->ldm[se] + ce] > 0.0f)) x = 0.0f;
+                        float* de = ope + m * tab->old[se] + ce;
+                        if (se == 2 ? g.c[2].accum : (se == 1 ? g.c[1].accum : g.c[0].accum)) x += *de;
+                        *de = x;
+                    }
+                }
             }
         }
+        __syncthreads();
     }
+    TL(61);
 }
 
 // ---------------------------------------------------------------- weight gradient
@@ -573,13 +733,25 @@ inline int rup(long long x, int a) { return (int)((x + a - 1) / a * a); }
 
 constexpr int KPAD = 32;  // k padding of split weights (a multiple of both BKs)
 
+// diagnostic timeline buffer (ANERF_GEMM_STAMPS=1): [64 workgroups][4 waves][64 points]
+unsigned long long* diag_stamps() {
+    static unsigned long long* const p = [] {
+        const char* e = std::getenv("ANERF_GEMM_STAMPS");
+        unsigned long long* q = nullptr;
+        if (e && e[0] == '1' && hipMalloc(&q, 64 * 4 * 64 * 8) != hipSuccess) q = nullptr;
+        if (q) (void)hipMemset(q, 0, 64 * 4 * 64 * 8);
+        return q;
+    }();
+    return p;
+}
+
 int planes_of(int precision) { return precision == ANERF_MLP_BF16X6 ? 3 : (precision == ANERF_MLP_BF16X3 ? 2 : 0); }
 
 // the dynamic LDS (80 / 72 KB) is above the default limit: raised once per kernel instance
 template <int NPL>
 hipError_t nt_attr() {
     static const hipError_t e = hipFuncSetAttribute((const void*)mlp_nt_kernel<NPL>,
-                                                    hipFuncAttributeMaxDynamicSharedMemorySize, Geo<NPL>::LDS_BYTES);
+                                                    hipFuncAttributeMaxDynamicSharedMemorySize, NTGeo<NPL>::LDS_BYTES);
     return e;
 }
 template <int NPL>
@@ -631,8 +803,11 @@ int wgrad_plan(int64_t m, int32_t n, int32_t k, int* splits, long long* rows) {
 
 extern "C" {
 
+// diagnostic: copy the last timeline of anerf_mlp_gemm (ANERF_GEMM_STAMPS=1) to host memory
+int anerf_mlp_diag_stamps(unsigned long long* host, size_t n);
+
 size_t anerf_mlp_split_bytes(int32_t rows, int32_t cols, int32_t precision) {
-    return (size_t)2 * planes_of(precision) * rup(rows, 32) * rup(cols, 16);
+    return (size_t)2 * planes_of(precision) * rup(rows, BNW) * rup(cols, 16);
 }
 
 int anerf_mlp_split_weights(const float* w, int32_t n, int32_t k, int64_t ldw, int32_t transpose, int32_t precision,
@@ -641,7 +816,7 @@ int anerf_mlp_split_weights(const float* w, int32_t n, int32_t k, int64_t ldw, i
     if (!w || !out || n < 1 || k < 1 || ldw < k || !npl)
         return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_split_weights: bad arguments");
     const int rows = transpose ? k : n, cols = transpose ? n : k;
-    const int nblocks = (rows + 31) / 32, ksteps = (cols + 15) / 16;
+    const int nblocks = (rows + BNW - 1) / BNW * (BNW / 32), ksteps = (cols + 15) / 16;  // whole 256-row tiles
     const long long tot = (long long)nblocks * ksteps * 512;
     hipLaunchKernelGGL(split_weights_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
                        reinterpret_cast<hipStream_t>(stream), w, n, k, (long long)ldw, transpose, nblocks, ksteps, npl,
@@ -664,7 +839,6 @@ int anerf_mlp_gemm(int64_t m, int32_t n, int32_t k, const anerf_seg* a, int32_t 
     if (rc) return rc;
     g.na = n_a;
     g.b = static_cast<const unsigned short*>(b_split);
-    g.bplane_blocks = (n + 31) / 32;
     g.ksteps = (k + 15) / 16;
     g.bias = bias;
     g.relu = relu != 0;
@@ -678,11 +852,7 @@ int anerf_mlp_gemm(int64_t m, int32_t n, int32_t k, const anerf_seg* a, int32_t 
     if (start != n) return anerf_internal_fail(ANERF_EINVAL, "output segments do not add up to n");
     g.nc = n_c;
     g.tiles_n = (n + BNW - 1) / BNW;
-    static const int dbg = [] {
-        const char* e = std::getenv("ANERF_GEMM_DBG");
-        return e ? std::atoi(e) : 0;
-    }();
-    g.dbg = dbg;
+    g.stamps = diag_stamps();
     const long long tiles = (long long)((m + BM - 1) / BM) * g.tiles_n;
     if (tiles > 0x7fffffff) return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_gemm: too many tiles");
     g.total = (int)tiles;
@@ -690,9 +860,9 @@ int anerf_mlp_gemm(int64_t m, int32_t n, int32_t k, const anerf_seg* a, int32_t 
     hipError_t e = npl == 3 ? nt_attr<3>() : nt_attr<2>();
     if (e != hipSuccess) return anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));
     if (npl == 3)
-        hipLaunchKernelGGL(mlp_nt_kernel<3>, dim3((unsigned)tiles), dim3(NTHR), Geo<3>::LDS_BYTES, st, g);
+        hipLaunchKernelGGL(mlp_nt_kernel<3>, dim3((unsigned)tiles), dim3(NTHR), NTGeo<3>::LDS_BYTES, st, g);
     else
-        hipLaunchKernelGGL(mlp_nt_kernel<2>, dim3((unsigned)tiles), dim3(NTHR), Geo<2>::LDS_BYTES, st, g);
+        hipLaunchKernelGGL(mlp_nt_kernel<2>, dim3((unsigned)tiles), dim3(NTHR), NTGeo<2>::LDS_BYTES, st, g);
     e = hipGetLastError();
     return e == hipSuccess ? ANERF_OK : anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));
 }
@@ -748,6 +918,13 @@ int anerf_mlp_wgrad(int64_t m, int32_t n, int32_t k, const float* dy, int64_t ld
                        g.splits, g.npad, g.kpad, n, k, dw, (long long)lddw, db, accumulate != 0);
     e = hipGetLastError();
     return e == hipSuccess ? ANERF_OK : anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));
+}
+
+int anerf_mlp_diag_stamps(unsigned long long* host, size_t n) {
+    unsigned long long* p = diag_stamps();
+    if (!p || !host) return ANERF_EINVAL;
+    if (n > 64 * 4 * 64) n = 64 * 4 * 64;
+    return hipMemcpy(host, p, n * 8, hipMemcpyDeviceToHost) == hipSuccess ? ANERF_OK : ANERF_EHIP;
 }
 
 }  // extern "C"

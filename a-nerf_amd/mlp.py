@@ -11,10 +11,10 @@ gradient needs), writes the encoder-feature gradient in place (the skip layer's 
 0 accumulating into it; the view columns from the view layer) and sums weight and bias gradients
 over the rows in one pass per layer.  Saved for the backward: the relu outputs of every layer.
 
-Precision (`train.NeRF.mlp`): "bf16x6" (default) splits both operands three ways into bf16 and
-sums the six products with i + j <= 2 (fp32-accurate, as the render kernel's bf16x6 mode);
-"bf16x3" two ways, three products (~16 significant bits per operand); fp32 accumulation in both
-(`anerf_gemm.hip`).  There is no CPU path: the library must be
+Precision (`train.NeRF.mlp`): "bf16x6" splits both operands three ways into bf16 and sums the six
+products with i + j <= 2 (fp32-accurate, as the render kernel's bf16x6 mode); "bf16x3" two ways,
+three products (~16 significant bits per operand); "mixed" (the default) runs the forward in
+bf16x6 and the backward in bf16x3; fp32 accumulation in all (`anerf_gemm.hip`).  There is no CPU path: the library must be
 built and a GPU present.
 """
 import ctypes
@@ -84,7 +84,7 @@ class _MLP(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, shape, feat, codes, *params):
-        W, D, skip, dnet, nv, prec = shape
+        W, D, skip, dnet, nv, prec, _ = shape
         dev = feat.device
         M, F = feat.shape
         nl = D
@@ -130,7 +130,7 @@ class _MLP(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g_raw):
-        W, D, skip, dnet, nv, prec = ctx.shape
+        W, D, skip, dnet, nv, _, prec = ctx.shape  # (the backward's own arithmetic)
 
         def sw(w, t=False):
             return split_weight(w, t, prec)
@@ -220,6 +220,12 @@ class _MLP(torch.autograd.Function):
         return (None, gfeat, gcodes, *grads)
 
 
+# mode -> (forward, backward) arithmetic (ANERF_MLP_BF16X6 = 6, _BF16X3 = 3).  "mixed": the forward
+# fp32-accurate (every relu decision as in fp32), the gradients with ~16-bit operands (relative
+# error ~1e-5, no branch decisions downstream of them)
+MODES = {"bf16x6": (6, 6), "bf16x3": (3, 3), "mixed": (6, 3)}
+
+
 def nerf_forward(net, feat, codes=None):
     """raw [M, 4] of `train.NeRF` on the split-bf16 GEMMs (same parameters, autograd included;
     precision net.mlp: "bf16x6" or "bf16x3")."""
@@ -230,7 +236,8 @@ def nerf_forward(net, feat, codes=None):
         codes = codes.float().contiguous()
     W, D = cfg.netwidth, cfg.netdepth
     skip = cfg.skips[0] if cfg.skips[0] < D - 1 else -1
-    shape = (W, D, skip, net.dnet, cfg.input_ch_views, _lib.MLP_PRECISIONS[net.mlp])
+    fwd, bwd = MODES[net.mlp]
+    shape = (W, D, skip, net.dnet, cfg.input_ch_views, fwd, bwd)
     params = []
     for lin in net.pts_linears:
         params += [lin.weight, lin.bias]

@@ -278,17 +278,18 @@ class NeRF(nn.Module):
         if cfg.opt_framecode:
             self.framecodes = Optcodes(cfg.n_framecodes, cfg.framecode_size)
 
-    # "bf16x6" / "bf16x3": the hand-written split-bf16 GEMMs (mlp.py / anerf_gemm.hip); "fp32": torch GEMMs
-    mlp = "bf16x6"
+    # "mixed" / "bf16x6" / "bf16x3": the hand-written split-bf16 GEMMs (mlp.py / anerf_gemm.hip); "fp32":
+    # torch GEMMs
+    mlp = "mixed"
 
     def forward(self, feat, cams=None):
         """feat [M, F] = [v | r | views] -> raw [M, 4] (rgb, alpha): forward_density + forward_view."""
-        if self.mlp in ("bf16x6", "bf16x3"):
+        if self.mlp in ("mixed", "bf16x6", "bf16x3"):
             from . import mlp as _mlp
             codes = self.framecodes(cams) if self.cfg.opt_framecode else None
             return _mlp.nerf_forward(self, feat, codes)
         if self.mlp != "fp32":
-            raise ValueError(f"mlp={self.mlp!r}: 'bf16x6', 'bf16x3' or 'fp32'")
+            raise ValueError(f"mlp={self.mlp!r}: 'mixed', 'bf16x6', 'bf16x3' or 'fp32'")
         x, x_skip, views = _SplitCols.apply(feat, self.dnet)
         h = x
         for i, lin in enumerate(self.pts_linears):
@@ -343,14 +344,15 @@ class TrainRayCaster(nn.Module):
     mode `forward`/`render_rays` run the stochastic, differentiable render path; in eval mode
     they delegate to the fused HIP render kernel (weights repacked when they changed)."""
 
-    def __init__(self, cfg, ckpt=None, device=None, mlp="bf16x6"):
-        """mlp: arithmetic of the training MLP — "bf16x6" (hand-written split-bf16 GEMMs on the MFMA
-        pipe, fp32-accurate, mlp.py), "bf16x3" (the same, ~16-bit operands) or "fp32" (torch GEMMs);
-        the eval delegate uses cfg.precision."""
+    def __init__(self, cfg, ckpt=None, device=None, mlp="mixed"):
+        """mlp: arithmetic of the training MLP — "mixed" (hand-written split-bf16 GEMMs on the MFMA pipe,
+        mlp.py: an fp32-accurate bf16x6 forward, a bf16x3 backward), "bf16x6" (fp32-accurate both
+        ways), "bf16x3" (~16-bit operands both ways) or "fp32" (torch GEMMs); the eval delegate
+        uses cfg.precision."""
         super().__init__()
         self.cfg = cfg.validate()
-        if mlp not in ("bf16x6", "bf16x3", "fp32"):
-            raise ValueError(f"mlp={mlp!r}: 'bf16x6', 'bf16x3' or 'fp32'")
+        if mlp not in ("mixed", "bf16x6", "bf16x3", "fp32"):
+            raise ValueError(f"mlp={mlp!r}: 'mixed', 'bf16x6', 'bf16x3' or 'fp32'")
         if isinstance(device, (str, torch.device)):
             dev = torch.device(device)  # (a CPU device holds the parameters only: checkpoints, no rendering)
         else:

@@ -127,7 +127,7 @@ def test_wgrad_is_deterministic():
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
 
 
-@pytest.mark.parametrize("impl", ["bf16x6", "bf16x3"])
+@pytest.mark.parametrize("impl", ["bf16x6", "mixed", "bf16x3"])
 @pytest.mark.parametrize("D,W,fc", [(8, 256, False), (4, 128, True)])
 def test_nerf_forward_backward_matches_fp32_module(D, W, fc, impl):
     """The whole network (skip layer, heads, view layer, framecodes) and its autograd vs the same

@@ -41,7 +41,7 @@ def _loss(out, tgt, bg):
             F.mse_loss(out["rgb0"] + (1 - out["acc0"])[:, None] * bg, tgt))
 
 
-def _run(name, mlp="bf16x6"):
+def _run(name, mlp="mixed"):
     g = Golden(name)
     m = g.meta
     tr = train.TrainRayCaster(g.cfg, g.ckpt, mlp=mlp).train()
@@ -65,8 +65,9 @@ def _run(name, mlp="bf16x6"):
     return g, tr, sk, out, loss
 
 
-# the training MLP on the hand-written split-bf16 GEMMs (bf16x6, the default) and on torch's fp32 GEMMs
-@pytest.fixture(scope="module", params=[(n, mlp) for n in TRAIN for mlp in ("bf16x6", "fp32")],
+# the training MLP on the hand-written split-bf16 GEMMs (mixed — the default — and bf16x6) and on torch's
+# fp32 GEMMs
+@pytest.fixture(scope="module", params=[(n, mlp) for n in TRAIN for mlp in ("mixed", "bf16x6", "fp32")],
                 ids=lambda p: f"{p[0]}-{p[1]}")
 def run(request):
     return _run(*request.param)
