@@ -585,11 +585,42 @@ __global__ __launch_bounds__(NTHR, 1) void mlp_nt_kernel(NTArgs g) {
 }
 
 // ---------------------------------------------------------------- weight gradient
+// dW tile 128 (n) x 128 (k) per workgroup over a slab of rows (4 waves, 2 x 2: 64 x 64 each).  Both
+// operands are activations read along their rows: a step stages 16 rows of dY (columns n0..) and of
+// X (columns k0..), a thread 8 consecutive columns of one row (a wave instruction reads four whole
+// 512 B row pieces), split into NPL bf16 planes kept row-major ([row][128] at a 320 B pitch, one
+// ds_write_b128 per plane).  The MFMA fragments (8 rows of one column) come back through the
+// hardware transpose read ds_read_b64_tr_b16, two per fragment, conflict-free at that pitch.
+// Loads are buffer loads through per-step descriptors whose range ends at the slab's last row, so
+// rows past the slab and columns outside the operand read zero without a clamp or a select; a
+// thread's offsets are constant over the whole slab.  Two LDS stages, two register sets in flight;
+// the partial tile leaves through LDS in full rows.  The bias gradient (k-tile 0) sums the staged
+// dY per column in a fixed order.
+constexpr int TSK = 16;                // rows per step
+constexpr int TPB = 320;               // plane row pitch, bytes (128 bf16 + 64: rows q*80 dwords apart)
+constexpr unsigned TOOB = 0x40000000u;  // a lane offset past every descriptor's range (ld < 2^24)
+
 template <int NPL>
+struct TNGeo {
+    static constexpr int PLANE = TSK * TPB;        // bytes
+    static constexpr int STAGE = 2 * NPL * PLANE;  // dY planes, then X planes
+    static constexpr int LDS_BYTES = 2 * STAGE > 128 * 132 * 4 ? 2 * STAGE : 128 * 132 * 4;
+};
+
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const float* p, long long ld, long long mb, long long mhi) {
+    long long rows = mhi - mb;
+    rows = rows < 0 ? 0 : (rows > TSK ? TSK : rows);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(p + mb * ld), 0, (int)(rows * ld * 4), 0x00020000);
+}
+
+template <int NPL, int NSEG>
 __global__ __launch_bounds__(NTHR, 2) void mlp_tn_kernel(TNArgs g) {
-    using G = Geo<NPL>;
-    constexpr int BK = G::BK, E = G::E;
-    extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
+    using G = TNGeo<NPL>;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds8[];
     const int logical = xcd_logical(blockIdx.x, g.total);
     const int split = logical / g.tiles, tile = logical % g.tiles;
     const int nt = tile / g.tiles_k, kt_ = tile % g.tiles_k;
@@ -599,19 +630,35 @@ __global__ __launch_bounds__(NTHR, 2) void mlp_tn_kernel(TNArgs g) {
     if (mhi > g.M) mhi = g.M;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wr = wave >> 1, wc = wave & 1;
-    const int c = tid & 127, h = tid >> 7;  // staging: column, E-row half of the BK-row step
-    // this thread's columns: dY column n0 + c, X column k0 + c (segment resolved once)
-    const int n = n0 + c, k = k0 + c;
-    const bool nok = n < g.N, kok = k < g.K;
-    // (clamped columns: every load below is unconditional, the values past N / K are zeroed)
-    const int kq = kok ? k : 0;
-    const bool in2 = g.nx > 2 && kq >= g.x[2].start, in1 = !in2 && g.nx > 1 && kq >= g.x[1].start;
-    const float* xp = (in2 ? g.x[2].p + 0 : (in1 ? g.x[1].p + 0 : g.x[0].p + 0)) +
-                      (kq - (in2 ? g.x[2].start + 0 : (in1 ? g.x[1].start + 0 : 0)));
-    const long long xld = in2 ? g.x[2].ld + 0 : (in1 ? g.x[1].ld + 0 : g.x[0].ld + 0);
-    const float* yp = g.dy + (nok ? n : 0);
+    // staging unit: row r of the step, columns c8 .. c8 + 7 of the tile
+    const int r = tid >> 4, c8 = 8 * (tid & 15);
+    const float* const dyp = g.dy;
+    const long long lddy = g.lddy;
+    const int nlim = (g.N + 3) / 4 * 4;
+    unsigned voy[2];
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+        const int col = n0 + c8 + 4 * f;
+        voy[f] = col < nlim ? (unsigned)(r * lddy + col) * 4u : TOOB;
+    }
+    const float* xp[NSEG];
+    long long xld[NSEG];
+    unsigned vox[2][NSEG];
+#pragma unroll
+    for (int sg = 0; sg < NSEG; ++sg) {
+        xp[sg] = g.x[sg].p;
+        xld[sg] = g.x[sg].ld;
+        const int st0 = g.x[sg].start, lim = st0 + (g.x[sg].cols + 3) / 4 * 4;
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+            const int col = k0 + c8 + 4 * f;
+            vox[f][sg] = col >= st0 && col < lim ? (unsigned)(r * xld[sg] + (col - st0)) * 4u : TOOB;
+        }
+    }
     const bool do_bias = g.wsb != nullptr && kt_ == 0;
-    float bsum = 0.0f;
+    float bsum[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bsum[e] = 0.0f;
 
     f32x16 acc[2][2];
 #pragma unroll
@@ -619,90 +666,191 @@ __global__ __launch_bounds__(NTHR, 2) void mlp_tn_kernel(TNArgs g) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{0};
 
-    // the NT kernel's two-slot pipeline; rows past the slab reload its last row and are zeroed when
-    // staged
-    float y0[E], x0[E], y1[E], x1[E];
-    const long long mlast = mhi > mlo ? mhi - 1 : mlo;
-    auto fetch = [&](long long mb, float (&yv)[E], float (&xv)[E]) {
+    struct Regs {
+        f32x4 y[2], x[2][NSEG];
+    };
+    auto fetch = [&](long long mb, Regs& R) {
+        const __amdgpu_buffer_rsrc_t ry = rows_rsrc(dyp, lddy, mb, mhi);
 #pragma unroll
-        for (int j = 0; j < E; ++j) {
-            long long m = mb + E * h + j;
-            m = m < mlast ? m : mlast;
-            yv[j] = *(gfloat*)(yp + m * g.lddy);
-            xv[j] = *(gfloat*)(xp + m * xld);
+        for (int f = 0; f < 2; ++f)
+            R.y[f] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ry, voy[f], 0, 0));
+#pragma unroll
+        for (int sg = 0; sg < NSEG; ++sg) {
+            const __amdgpu_buffer_rsrc_t rx = rows_rsrc(xp[sg], xld[sg], mb, mhi);
+#pragma unroll
+            for (int f = 0; f < 2; ++f)
+                R.x[f][sg] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, vox[f][sg], 0, 0));
         }
     };
-    auto stage = [&](int s, long long mb, const float (&yv)[E], const float (&xv)[E]) {
-        unsigned short* st = lds + s * G::STAGE;
-        float yz[E], xz[E];
+    // 8 values -> NPL planes of packed bf16 pairs (round to nearest even of the running remainder)
+    auto split_store = [&](float (&v)[8], unsigned char* dst) {
 #pragma unroll
-        for (int j = 0; j < E; ++j) {
-            const bool ok = mb + E * h + j < mhi;
-            yz[j] = (ok && nok) ? yv[j] : 0.0f;
-            xz[j] = (ok && kok) ? xv[j] : 0.0f;
+        for (int p = 0; p < NPL; ++p) {
+            u32x4 w;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const bf16x2 h = __builtin_convertvector((f32x2){v[2 * q], v[2 * q + 1]}, bf16x2);
+                w[q] = __builtin_bit_cast(unsigned, h);
+                if (p + 1 < NPL) {
+                    v[2 * q] -= (float)h[0];
+                    v[2 * q + 1] -= (float)h[1];
+                }
+            }
+            *reinterpret_cast<u32x4*>(dst + p * G::PLANE) = w;
         }
-        store_split<NPL, E>(st, c, E * h, yz);
-        store_split<NPL, E>(st + NPL * G::PLANE, c, E * h, xz);
+    };
+    auto stage = [&](int buf, const Regs& R) {
+        unsigned char* const P = lds8 + buf * G::STAGE + r * TPB + 2 * c8;
+        float y[8], x[8];
+#pragma unroll
+        for (int f = 0; f < 2; ++f)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                y[4 * f + e] = R.y[f][e];
+                // (through float rvalues: clang's bit_cast of a vector-element lvalue reads element 0)
+                const float x0 = R.x[f][0][e];
+                unsigned b = __builtin_bit_cast(unsigned, x0);
+#pragma unroll
+                for (int sg = 1; sg < NSEG; ++sg) {  // (one segment is live per lane, the others read 0)
+                    const float xs = R.x[f][sg][e];
+                    b |= __builtin_bit_cast(unsigned, xs);
+                }
+                x[4 * f + e] = __builtin_bit_cast(float, b);
+            }
         if (do_bias) {
 #pragma unroll
-            for (int j = 0; j < E; ++j) bsum += yz[j];
+            for (int e = 0; e < 8; ++e) bsum[e] += y[e];
         }
+        split_store(y, P);
+        split_store(x, P + NPL * G::PLANE);
     };
-    const int nsteps = mhi > mlo ? (int)((mhi - mlo + BK - 1) / BK) : 0;
-    if (nsteps > 0) {
-        fetch(mlo, y0, x0);
-        fetch(mlo + BK, y1, x1);
-        stage(0, mlo, y0, x0);
-    }
-    __syncthreads();
-    for (int st = 0; st < nsteps; st += 2) {
-        fetch(mlo + (long long)(st + 2) * BK, y0, x0);
-        mma_step<NPL>(lds, wr, wc, lane, acc);
-        if (st + 1 < nsteps) stage(1, mlo + (long long)(st + 1) * BK, y1, x1);
-        __syncthreads();
-        if (st + 1 >= nsteps) break;
-        fetch(mlo + (long long)(st + 3) * BK, y1, x1);
-        mma_step<NPL>(lds + G::STAGE, wr, wc, lane, acc);
-        if (st + 2 < nsteps) stage(0, mlo + (long long)(st + 2) * BK, y0, x0);
-        __syncthreads();
-    }
-    float* wt = g.ws + (long long)split * g.npad * g.kpad;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const int kc = k0 + 64 * wc + 32 * j + (lane & 31);
+    // fragment = rows 8h .. 8h + 7 of columns cb .. cb + 31: lane 4q + p of each 16-lane group
+    // addresses row q (+4) at column 4p of its half
+    const int h = lane >> 5, q = (lane >> 2) & 3, p4 = lane & 3, g1 = (lane >> 4) & 1;
+    const int frag_off = (8 * h + q) * TPB + 2 * (16 * g1 + 4 * p4);
+    auto frag = [&](const unsigned char* plane, int cb) {
+        const unsigned char* a = plane + frag_off + 2 * cb;
+        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)a);
+        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a + 4 * TPB));
+        return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    };
+    auto step = [&](int buf) {
+        const unsigned char* const P = lds8 + buf * G::STAGE;
+        bf16x8 a[NPL][2], b[NPL][2];
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int nr = n0 + 64 * wr + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-                wt[(long long)nr * g.kpad + kc] = acc[i][j][r];
+            for (int p = 0; p < NPL; ++p) {
+                a[p][i] = frag(P + p * G::PLANE, 64 * wr + 32 * i);
+                b[p][i] = frag(P + (NPL + p) * G::PLANE, 64 * wc + 32 * i);
             }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                f32x16 c = acc[i][j];
+                if constexpr (NPL == 3) {
+                    c = mfma(a[2][i], b[0][j], c);
+                    c = mfma(a[1][i], b[1][j], c);
+                    c = mfma(a[0][i], b[2][j], c);
+                }
+                c = mfma(a[1][i], b[0][j], c);
+                c = mfma(a[0][i], b[1][j], c);
+                acc[i][j] = mfma(a[0][i], b[0][j], c);
+            }
+    };
+    // two LDS stages, two register sets: the loads of step s + 2 fly during steps s and s + 1
+    const int nsteps = mhi > mlo ? (int)((mhi - mlo + TSK - 1) / TSK) : 0;
+    Regs R0, R1;
+    if (nsteps > 0) {
+        fetch(mlo, R0);
+        fetch(mlo + TSK, R1);
+        __builtin_amdgcn_sched_barrier(0);
+        stage(0, R0);
     }
-    if (do_bias) {  // (after the loop's last barrier the stages are free)
-        float* red = reinterpret_cast<float*>(lds);
-        if (h == 1) red[c] = bsum;
+    __syncthreads();
+    for (int st = 0; st < nsteps; st += 2) {
+        fetch(mlo + (long long)(st + 2) * TSK, R0);
+        __builtin_amdgcn_sched_barrier(0);  // (keep the loads ahead of the MFMAs)
+        step(0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (st + 1 < nsteps) stage(1, R1);
         __syncthreads();
-        if (h == 0) g.wsb[(long long)split * g.npad + n] = bsum + red[c];
+        if (st + 1 >= nsteps) break;
+        fetch(mlo + (long long)(st + 3) * TSK, R1);
+        __builtin_amdgcn_sched_barrier(0);
+        step(1);
+        __builtin_amdgcn_sched_barrier(0);
+        if (st + 2 < nsteps) stage(0, R0);
+        __syncthreads();
+    }
+    // partial tile through LDS ([128][132] fp32), then whole 512 B rows into the workspace
+    float* const tile_f = reinterpret_cast<float*>(lds8);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = 64 * wr + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                tile_f[row * 132 + 64 * wc + 32 * j + (lane & 31)] = acc[i][j][r];
+            }
+    __syncthreads();
+    float* const wt = g.ws + (long long)split * g.npad * g.kpad + (long long)n0 * g.kpad + k0;
+#pragma unroll 8
+    for (int q = 0; q < 16; ++q) {  // 256 threads = 8 rows x 32 float4 per pass
+        const int row = 8 * q + (tid >> 5);
+        const f32x4 v = *reinterpret_cast<const f32x4*>(tile_f + row * 132 + 4 * (tid & 31));
+        *reinterpret_cast<f32x4*>(wt + (long long)row * g.kpad + 4 * (tid & 31)) = v;
+    }
+    if (do_bias) {  // column sums over the 16 staging rows, in a fixed order
+        __syncthreads();
+        float* const red = tile_f;  // [16][128]
+#pragma unroll
+        for (int e = 0; e < 8; ++e) red[r * 128 + c8 + e] = bsum[e];
+        __syncthreads();
+        if (tid < 128) {
+            float t = red[tid];
+#pragma unroll
+            for (int w = 1; w < 16; ++w) t += red[w * 128 + tid];
+            g.wsb[(long long)split * g.npad + n0 + tid] = t;
+        }
     }
 }
 
-__global__ void mlp_reduce_kernel(const float* __restrict__ ws, const float* __restrict__ wsb, int splits, int npad,
-                                  int kpad, int N, int K, float* __restrict__ dw, long long lddw,
-                                  float* __restrict__ db, int accum) {
-    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    const long long nk = (long long)N * K;
-    if (idx < nk) {
-        const int n = (int)(idx / K), k = (int)(idx % K);
-        const float* p = ws + (long long)n * kpad + k;
-        float s = 0.0f;
-        for (int t = 0; t < splits; ++t) s += p[(long long)t * npad * kpad];
-        float* o = dw + (long long)n * lddw + k;
-        *o = accum ? *o + s : s;
-    } else if (wsb && db && idx < nk + N) {
-        const int n = (int)(idx - nk);
-        float s = 0.0f;
-        for (int t = 0; t < splits; ++t) s += wsb[(long long)t * npad + n];
-        db[n] = accum ? db[n] + s : s;
+// dst[row][col] (+)= sum over the slabs of src[t][row][col]: a workgroup takes 128 columns of one row,
+// 32 float4 column groups x 8 slab groups (each a contiguous run of slabs, 4 loads in flight), the 8
+// partial sums then added in slab-group order through LDS (deterministic).  src rows hold a multiple
+// of 128 columns (the workspace's padding).
+__global__ __launch_bounds__(256) void mlp_reduce_kernel(const float* __restrict__ src, int splits,
+                                                         long long split_stride, long long row_stride, int cols,
+                                                         float* __restrict__ dst, long long ldd, int accum) {
+    __shared__ f32x4 part[8][32];
+    const int cg = threadIdx.x & 31, sgi = threadIdx.x >> 5;
+    const int row = blockIdx.y, c0 = blockIdx.x * 128 + 4 * cg;
+    const int chunk = (splits + 7) / 8;
+    const int t0 = sgi * chunk, t1 = t0 + chunk < splits ? t0 + chunk : splits;
+    const float* p = src + row * row_stride + c0;
+    f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+    int t = t0;
+    for (; t + 4 <= t1; t += 4) {
+        f32x4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const f32x4*>(p + (t + u) * split_stride);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc += v[u];
+    }
+    for (; t < t1; ++t) acc += *reinterpret_cast<const f32x4*>(p + t * split_stride);
+    part[sgi][cg] = acc;
+    __syncthreads();
+    if (sgi == 0) {
+        f32x4 s = part[0][cg];
+#pragma unroll
+        for (int w = 1; w < 8; ++w) s += part[w][cg];
+        float* o = dst + row * ldd + c0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            if (c0 + e < cols) o[e] = accum ? o[e] + s[e] : s[e];
     }
 }
 
@@ -754,10 +902,10 @@ hipError_t nt_attr() {
                                                     hipFuncAttributeMaxDynamicSharedMemorySize, NTGeo<NPL>::LDS_BYTES);
     return e;
 }
-template <int NPL>
+template <int NPL, int NSEG>
 hipError_t tn_attr() {
-    static const hipError_t e = hipFuncSetAttribute((const void*)mlp_tn_kernel<NPL>,
-                                                    hipFuncAttributeMaxDynamicSharedMemorySize, Geo<NPL>::LDS_BYTES);
+    static const hipError_t e = hipFuncSetAttribute((const void*)mlp_tn_kernel<NPL, NSEG>,
+                                                    hipFuncAttributeMaxDynamicSharedMemorySize, TNGeo<NPL>::LDS_BYTES);
     return e;
 }
 
@@ -792,7 +940,7 @@ int wgrad_plan(int64_t m, int32_t n, int32_t k, int* splits, long long* rows) {
     if (s > smax) s = smax;
     if (s < 1) s = 1;
     long long r = (m + s - 1) / s;
-    r = (r + KPAD - 1) / KPAD * KPAD;
+    r = (r + 2 * TSK - 1) / (2 * TSK) * (2 * TSK);
     *rows = r;
     *splits = (int)((m + r - 1) / r);
     if (*splits < 1) *splits = 1;
@@ -880,6 +1028,14 @@ int anerf_mlp_wgrad(int64_t m, int32_t n, int32_t k, const float* dy, int64_t ld
     const int npl = planes_of(precision);
     if (m < 0 || n < 1 || k < 1 || !dy || lddy < n || !dw || lddw < k || !npl)
         return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_wgrad: bad arguments");
+    // dY is read as float4 groups of whole rows: 16 B aligned, ld a multiple of 4 and >= n rounded up
+    // to 4 (the padding columns only reach the discarded rows n.. of the tile)
+    if (lddy >= (1 << 24)) return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_wgrad: lddy >= 2^24");
+    for (int i = 0; i < n_x && x; ++i)
+        if (x[i].ld >= (1 << 24)) return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_wgrad: x ld >= 2^24");
+    if ((reinterpret_cast<uintptr_t>(dy) & 15) || (lddy & 3) || lddy < (n + 3) / 4 * 4)
+        return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_wgrad: dy must be 16 B aligned with ld % 4 == 0 "
+                                                 "and ld >= round_up(n, 4)");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     TNArgs g = {};
     int rc = set_segs(x, n_x, k, g.x);
@@ -907,15 +1063,26 @@ int anerf_mlp_wgrad(int64_t m, int32_t n, int32_t k, const float* dy, int64_t ld
     g.total = g.tiles * g.splits;
     g.ws = static_cast<float*>(workspace);
     g.wsb = db ? g.ws + (size_t)g.splits * g.npad * g.kpad : nullptr;
-    hipError_t e = npl == 3 ? tn_attr<3>() : tn_attr<2>();
-    if (e != hipSuccess) return anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));
-    if (npl == 3)
-        hipLaunchKernelGGL(mlp_tn_kernel<3>, dim3((unsigned)g.total), dim3(NTHR), Geo<3>::LDS_BYTES, st, g);
-    else
-        hipLaunchKernelGGL(mlp_tn_kernel<2>, dim3((unsigned)g.total), dim3(NTHR), Geo<2>::LDS_BYTES, st, g);
-    const long long outs = (long long)n * k + (db ? n : 0);
-    hipLaunchKernelGGL(mlp_reduce_kernel, dim3((unsigned)((outs + 255) / 256)), dim3(256), 0, st, g.ws, g.wsb,
-                       g.splits, g.npad, g.kpad, n, k, dw, (long long)lddw, db, accumulate != 0);
+    hipError_t e = hipSuccess;
+#define ANERF_TN_LAUNCH(P, S)                                                                         \
+    if (npl == P && n_x == S) {                                                                       \
+        e = tn_attr<P, S>();                                                                          \
+        if (e != hipSuccess) return anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));            \
+        hipLaunchKernelGGL((mlp_tn_kernel<P, S>), dim3((unsigned)g.total), dim3(NTHR), TNGeo<P>::LDS_BYTES, st, g); \
+    }
+    ANERF_TN_LAUNCH(3, 1)
+    ANERF_TN_LAUNCH(3, 2)
+    ANERF_TN_LAUNCH(3, 3)
+    ANERF_TN_LAUNCH(2, 1)
+    ANERF_TN_LAUNCH(2, 2)
+    ANERF_TN_LAUNCH(2, 3)
+#undef ANERF_TN_LAUNCH
+    hipLaunchKernelGGL(mlp_reduce_kernel, dim3((unsigned)(g.kpad / 128), (unsigned)n), dim3(256), 0, st, g.ws,
+                       g.splits, (long long)g.npad * g.kpad, (long long)g.kpad, k, dw, (long long)lddw,
+                       accumulate != 0);
+    if (db)
+        hipLaunchKernelGGL(mlp_reduce_kernel, dim3((unsigned)(g.npad / 128), 1u), dim3(256), 0, st, g.wsb, g.splits,
+                           (long long)g.npad, 0ll, n, db, 0ll, accumulate != 0);
     e = hipGetLastError();
     return e == hipSuccess ? ANERF_OK : anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));
 }

@@ -382,7 +382,9 @@ int anerf_mlp_gemm(int64_t m, int32_t n, int32_t k, const anerf_seg* a, int32_t 
 /* Workspace bytes of anerf_mlp_wgrad for these sizes. */
 size_t anerf_mlp_wgrad_workspace(int64_t m, int32_t n, int32_t k);
 /* dW[n][k] (+)= sum_m dY[m][n] X[m][k] and db[n] (+)= sum_m dY[m][n] (db may be NULL); X: n_x
- * segments adding up to k columns.  Summed over row slabs in a fixed order (deterministic). */
+ * segments adding up to k columns.  Summed over row slabs in a fixed order (deterministic).  dY is
+ * read in 4-column groups: 16 B aligned, lddy % 4 == 0, lddy >= round_up(n, 4) (columns n.. of the
+ * last group are read but reach no output). */
 int anerf_mlp_wgrad(int64_t m, int32_t n, int32_t k, const float* dy, int64_t lddy, const anerf_seg* x, int32_t n_x,
                     int32_t precision, float* dw, int64_t lddw, float* db, int32_t accumulate, void* workspace,
                     size_t workspace_bytes, void* stream);

@@ -98,7 +98,8 @@ def test_gemm_input_gradient_mask_accumulate_discard(prec):
 def test_wgrad_and_bias_gradient(m, n, ks, prec):
     torch.manual_seed(m)
     k = sum(ks)
-    dy = torch.randn(m, n + 1, device=DEV)[:, :n]
+    # dY rows padded past round_up(n, 4), the padding holding values that must reach no output
+    dy = torch.randn(m, (n + 3) // 4 * 4 + 4, device=DEV)[:, :n]
     parts = [torch.randn(m, c, device=DEV) for c in ks]
     x = torch.cat(parts, 1)
     lib = mlp._lib.load()
@@ -111,6 +112,18 @@ def test_wgrad_and_bias_gradient(m, n, ks, prec):
     assert torch.all((dw.double() - ref).abs() <= bound), float((dw.double() - ref).abs().max())
     ref_b = dy.double().sum(0)
     assert torch.all((db.double() - ref_b).abs() <= 1e-5 * dy.double().abs().sum(0) + 1e-5)
+
+
+def test_wgrad_rejects_unaligned_dy():
+    m, n, k = 64, 5, 16
+    lib = mlp._lib.load()
+    x = torch.randn(m, k, device=DEV)
+    ws = torch.empty(lib.anerf_mlp_wgrad_workspace(m, n, k), device=DEV, dtype=torch.uint8)
+    dw, db = torch.empty(n, k, device=DEV), torch.empty(n, device=DEV)
+    for dy in (torch.randn(m, n, device=DEV), torch.randn(m, 9, device=DEV)[:, :n],
+               torch.randn(m * 8 + 1, device=DEV)[1:].view(m, 8)[:, :n]):
+        with pytest.raises(mlp._lib.AnerfError, match="dy must be"):
+            mlp.wgrad(m, n, k, dy, [mlp._seg(x, k)], dw, db, ws, torch.device(DEV))
 
 
 def test_wgrad_is_deterministic():
