@@ -2,10 +2,11 @@
 //
 // Training runs the reference's NeRF (core/networks/nerf.py:94-148) forward and backward over
 // M = rays x samples rows (131 k - 164 k per step at the reference's N_rand 2048, 64 + 16 samples).
-// Every product here is fp32 in, fp32 out, with the operands split as x = x_hi + x_lo into two
-// bf16 values (round to nearest even, x_lo = bf16(x - x_hi)) and three v_mfma_f32_32x32x16_bf16
-// products x_lo w_hi + x_hi w_lo + x_hi w_hi accumulated in fp32 (the dropped x_lo w_lo is below
-// 2^-16 of |x w|): ~16 significant bits per operand, 5.3x the fp32 MFMA rate in MFMA cycles.
+// Every product here is fp32 in, fp32 out, with both operands split into bf16 planes (round to
+// nearest even of the running remainder) and v_mfma_f32_32x32x16_bf16 products accumulated in
+// fp32: bf16x3 = two planes, the three products x_lo w_hi + x_hi w_lo + x_hi w_hi (~16 significant
+// bits per operand); bf16x6 = three planes, the six products with i + j <= 2 (fp32-accurate).  The
+// training default ("mixed", mlp.py) runs the forward in bf16x6 and the backward in bf16x3.
 //
 //   forward / input gradient (NT): C[m][n] = epi(sum_k A[m][k] B[n][k]); A = up to three fp32
 //     column segments (the reference's cat([x, h]) / cat([feature, views, code]) never built),
@@ -18,12 +19,14 @@
 //     tile per (slab, tile) in a workspace, summed in a second launch in slab order (deterministic,
 //     no atomics); the bias gradient sum_m dY[m][n] is summed from the staged dY in the same pass.
 //
-// Tiles: 128 x 128 outputs per 256-thread workgroup (4 waves, 2 x 2, each 64 x 64 = 2 x 2 blocks
-// of 32 x 32), BK = 32 (two k16 steps), LDS [row][k] bf16 planes with a 40-element pitch (80 B: the
-// 16 lanes of a ds_read_b128 group hit 16 distinct 4-bank groups), two stages (80 KB: two
-// workgroups per CU).  One barrier per k-step: the next tile's global loads are issued before the
-// MFMAs of the current one and written to the other stage after them.  Workgroups are mapped so
-// the column tiles of one row tile (which re-read the same A rows) run on one XCD's L2.
+// Both kernels: 128 x 128 outputs per 256-thread workgroup, two workgroups per CU (<= 256 VGPRs,
+// <= 80 KB LDS each) so one workgroup's prologue and epilogue overlap the other's MFMAs.  fp32
+// operands arrive through buffer loads whose descriptors end at the tile's (slab's) last row, so
+// ragged rows and columns outside an operand segment read zero with no clamp or select; they are
+// split with v_cvt_pk_bf16_f32 into bf16 LDS planes (two stages, loads two steps ahead).  The
+// forward reads its A fragments row-wise (ds_read_b128); the weight gradient, whose operands are
+// both [m][.] activations, reads them column-wise with the hardware transpose ds_read_b64_tr_b16.
+// Workgroups are mapped so tiles that re-read the same rows run on one XCD's L2.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -41,23 +44,11 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int BM = 128, BN = 128, NTHR = 256;
 constexpr int MAXSEG = 3;
-
-// NPL planes per operand: 2 = bf16x3 (x = x0 + x1; products x1 w0, x0 w1, x0 w0), 3 = bf16x6
-// (x = x0 + x1 + x2; the six products with i + j <= 2, fp32-accurate: the dropped terms are below
-// 2^-23 of |x w|).  BK = the k extent of one staged step; LDP = its LDS row pitch (BK + 8 bf16:
-// conflict-free ds_read_b128 for 16 consecutive rows at 80 / 48 bytes per row).
-template <int NPL>
-struct Geo {
-    static constexpr int BK = 16;
-    static constexpr int LDP = BK + 8;
-    static constexpr int PLANE = BM * LDP;
-    static constexpr int STAGE = 2 * NPL * PLANE;  // A planes, then B planes
-    static constexpr int LDS_BYTES = 2 * STAGE * 2;
-    static constexpr int E = BK / 2;  // elements one thread stages per operand row / column
-};
 
 struct SegD {
     const float* p;
@@ -86,7 +77,6 @@ struct NTArgs {
     OSegD c[MAXSEG];
     int nc;
     int tiles_n, total;
-    unsigned long long* stamps;  // diagnostic timeline (ANERF_GEMM_STAMPS): [wg][wave][64] s_memtime, or null
 };
 
 struct TNArgs {
@@ -103,25 +93,6 @@ struct TNArgs {
     int npad, kpad;
 };
 
-// 8 values -> NPL bf16 fragments (round to nearest even of the running remainder)
-template <int NPL>
-__device__ __forceinline__ void split8(const float* v, u32x4 (&out)[NPL]) {
-    float r[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) r[j] = v[j];
-#pragma unroll
-    for (int p = 0; p < NPL; ++p) {
-        bf16x8 h;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) h[j] = (__bf16)r[j];
-        if (p + 1 < NPL) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) r[j] -= (float)h[j];
-        }
-        out[p] = __builtin_bit_cast(u32x4, h);
-    }
-}
-
 // logical tile of a workgroup: the hardware deals workgroups round-robin over the 8 XCDs; this
 // bijection gives each XCD a contiguous run of logical ids (MI355X guide, "XCD swizzle")
 __device__ __forceinline__ int xcd_logical(int wg, int total) {
@@ -129,459 +100,324 @@ __device__ __forceinline__ int xcd_logical(int wg, int total) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (wg >> 3);
 }
 
-// One operand row over up to three column segments, resolved without indexing the argument
-// struct by a per-lane value (that compiles to dependent per-lane loads of the struct): the three
-// segments' row pointers are computed once and selected with v_cndmask per 4-column group.
-struct RowSrc {
-    unsigned long long p0, p1, p2;  // segment i's row address, minus its first column (indexed by k)
-    int start1, start2;             // first columns of segments 1 and 2 (K when absent)
-    int kmax4;                      // last 4-column group that is read (round_up(K, 4) - 4)
-};
-
-// (values pinned in registers: without the pin, clang folds the per-lane select between the three
-// pointers into an indexed load from a stack copy of the struct — scratch traffic in the k loop)
-__device__ __forceinline__ void pin64(unsigned long long& x) { asm volatile("" : "+v"(x)); }
-// a uniform kernel-argument value made opaque (in a VGPR) before per-lane selects between such
-// values: see pin64
-template <class T>
-__device__ __forceinline__ T opaque(T x) {
-    asm volatile("" : "+v"(x));
-    return x;
-}
-
-// rows past M read row M - 1 (finite; their outputs are never stored)
-__device__ __forceinline__ RowSrc row_src(const SegD* seg, int nseg, long long row, long long M, int K) {
-    RowSrc r;
-    const long long rr = row < M ? row : M - 1;
-    r.p0 = (unsigned long long)(seg[0].p + rr * seg[0].ld);
-    r.p1 = nseg > 1 ? (unsigned long long)(seg[1].p + rr * seg[1].ld - seg[1].start) : r.p0;
-    r.p2 = nseg > 2 ? (unsigned long long)(seg[2].p + rr * seg[2].ld - seg[2].start) : r.p0;
-    pin64(r.p0);
-    pin64(r.p1);
-    pin64(r.p2);
-    r.start1 = nseg > 1 ? seg[1].start : K;
-    r.start2 = nseg > 2 ? seg[2].start : K;
-    r.kmax4 = (K + 3) / 4 * 4 - 4;
-    return r;
-}
-
-typedef __attribute__((address_space(1))) const float gfloat;
 typedef __attribute__((address_space(1))) const f32x4 gf32x4;
-
-// The raw 4-column groups of the row at columns k .. k+E-1 (clamped to the last readable group;
-// live_groups() says which are past K and become zeros when staged).  Every load is
-// unconditional and nothing reads the loaded registers before staging, so the compiler's counted
-// vmcnt waits stay exact across the two-deep prefetch.  The host guarantees 4-column groups never
-// straddle segments and that a ragged last segment's columns up to round_up(K, 4) are readable
-// and finite (the B planes are zero there).
-template <int E>
-__device__ __forceinline__ void load_row(const RowSrc& r, int k, f32x4 (&v)[E / 4]) {
-    // (rvalue copies: a ?: between struct-field lvalues selects ADDRESSES, and clang then keeps the
-    // struct on the stack and loads through the selected address)
-    const unsigned long long q0 = r.p0, q1 = r.p1, q2 = r.p2;
-    const int s1 = r.start1, s2 = r.start2, km = r.kmax4;
-#pragma unroll
-    for (int g = 0; g < E / 4; ++g) {
-        const int kg = k + 4 * g;
-        const int kc = kg < km ? kg : km;
-        const bool in2 = kc >= s2, in1 = !in2 && kc >= s1;
-        const float* p = (const float*)(in2 ? q2 : (in1 ? q1 : q0));
-        v[g] = *(gf32x4*)(p + kc);
-    }
-}
-
-// split the E values of one operand row (columns k .. k+E-1; zeros from column K on) into the
-// NPL planes at `planes`
-template <int NPL, int E>
-__device__ __forceinline__ void store_split(unsigned short* planes, int row, int k, const float (&v)[E]) {
-    using G = Geo<NPL>;
-#pragma unroll
-    for (int h = 0; h < E / 8; ++h) {
-        u32x4 f[NPL];
-        split8<NPL>(v + 8 * h, f);
-#pragma unroll
-        for (int p = 0; p < NPL; ++p)
-            *reinterpret_cast<u32x4*>(planes + p * G::PLANE + row * G::LDP + k + 8 * h) = f[p];
-    }
-}
-
-template <int NPL, int E>
-__device__ __forceinline__ void store_split_groups(unsigned short* planes, int row, int k, int kcol, int K,
-                                                   const f32x4 (&q)[E / 4]) {
-    float v[E];
-#pragma unroll
-    for (int g = 0; g < E / 4; ++g)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[4 * g + e] = kcol + 4 * g < K ? q[g][e] : 0.0f;
-    store_split<NPL, E>(planes, row, k, v);
-}
 
 __device__ __forceinline__ f32x16 mfma(const bf16x8& a, const bf16x8& b, const f32x16& c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
-// one staged step of a wave's 64 x 64 block: BK / 16 k16 steps, the products i + j <= NPL - 1,
-// smallest terms first
-template <int NPL>
-__device__ __forceinline__ void mma_step(const unsigned short* st, int wr, int wc, int lane, f32x16 (&acc)[2][2]) {
-    using G = Geo<NPL>;
-    const unsigned short* A = st;
-    const unsigned short* B = st + NPL * G::PLANE;
-    const int r = lane & 31, kh = 8 * (lane >> 5);
-#pragma unroll
-    for (int kk = 0; kk < G::BK / 16; ++kk) {
-        bf16x8 a[NPL][2], b[NPL][2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int ra = (64 * wr + 32 * i + r) * G::LDP + 16 * kk + kh;
-            const int rb = (64 * wc + 32 * i + r) * G::LDP + 16 * kk + kh;
-#pragma unroll
-            for (int p = 0; p < NPL; ++p) {
-                a[p][i] = *reinterpret_cast<const bf16x8*>(A + p * G::PLANE + ra);
-                b[p][i] = *reinterpret_cast<const bf16x8*>(B + p * G::PLANE + rb);
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                f32x16 c = acc[i][j];
-                if constexpr (NPL == 3) {
-                    c = mfma(a[2][i], b[0][j], c);
-                    c = mfma(a[1][i], b[1][j], c);
-                    c = mfma(a[0][i], b[2][j], c);
-                }
-                c = mfma(a[1][i], b[0][j], c);
-                c = mfma(a[0][i], b[1][j], c);
-                acc[i][j] = mfma(a[0][i], b[0][j], c);
-            }
-    }
-}
-
 // ---------------------------------------------------------------- forward / input gradient
-// 128 rows x 256 columns per workgroup (4 waves, 2 x 2: 64 rows x 128 columns = 2 x 4 blocks each,
-// one wave per SIMD).  A (activations, fp32 from HBM) is staged 64 columns at a time: loaded into
-// registers a whole stage ahead (192 MFMAs per wave per stage cover the HBM latency), split once
-// per workgroup into NPL bf16 LDS planes; one barrier per stage.  B (the split weights, a few
-// hundred KB shared by every workgroup) is read straight from L2 as MFMA fragments — stored
-// fragment-major, 1 KB per (32-column block, k16 step, plane) in lane order, so each load is one
-// contiguous wave access — one k16 step ahead, and never touches LDS.
-constexpr int BNW = 256;
-constexpr int SK = 64;        // k columns per stage
-constexpr int SLDP = SK + 8;  // LDS row pitch (bf16): 144 B, an odd number of 16 B chunks
+// 128 rows x 128 columns per workgroup, two workgroups per CU (4 waves; wave w computes all 128 rows
+// x columns 32 w .. 32 w + 31 = 4 blocks, so the waves read disjoint B fragments).  A (activations,
+// fp32 in HBM, up to three column segments) is staged 32 columns per step: buffer loads through
+// per-tile segment descriptors whose range ends at the last row (rows past M and columns outside a
+// segment read zero, so no clamp, no select, no zero fill), issued two steps ahead into two register
+// sets, split with v_cvt_pk_bf16_f32 into NPL bf16 planes ([row][k], 80 B pitch: conflict-free
+// ds_read_b128 fragment reads); two LDS stages, one barrier per step.  B (the split weights, a few
+// hundred KB shared by every workgroup) is read straight from L2 as MFMA fragments, stored
+// fragment-major (1 KB per 32-column block, k16 step and plane, in lane order), one k16 step ahead.
+// The epilogue goes through LDS in whole 512 B output rows (bias, relu, relu' mask, accumulate,
+// output segments); with two workgroups per CU one's epilogue and prologue overlap the other's MFMAs.
+constexpr int BNW = 256;      // row padding of the split weights (whole 256-row tiles)
+constexpr int NBN = 128;      // output columns per workgroup
+constexpr int SK = 32;        // k columns per step
+constexpr int SLDP = SK + 8;  // LDS row pitch (bf16): 80 B, an odd number of 16 B chunks
+constexpr unsigned NOOB = 0x80000000u;  // a lane offset past every descriptor's range
 
 template <int NPL>
 struct NTGeo {
-    static constexpr int PLANE = BM * SLDP;
+    static constexpr int PLANE = BM * SLDP;           // bf16 elements
     static constexpr int STAGE = NPL * PLANE;
-    static constexpr int TAB = 2 * STAGE * 2;     // byte offset of the segment tables
+    static constexpr int STAGES_BYTES = 2 * STAGE * 2;
+    static constexpr int TILE_BYTES = BM * 132 * 4;  // epilogue tile [128][132] fp32
+    static constexpr int TAB = STAGES_BYTES > TILE_BYTES ? STAGES_BYTES : TILE_BYTES;  // segment tables
     static constexpr int LDS_BYTES = TAB + 256;
 };
 
-// operand / output segment tables in LDS: per-lane segment choices read their pointer and stride
-// from here (an indexed read of the kernel-argument struct makes clang copy it to scratch, and a
-// scratch access in the k loop waits out every outstanding load)
+// output segment tables in LDS: per-lane segment choices read their pointer and stride from here
+// (an indexed read of the kernel-argument struct makes clang copy it to scratch)
 struct SegTab {
-    const float* p[MAXSEG];
-    long long ld[MAXSEG];
     float* op[MAXSEG];
     long long old[MAXSEG];
     const float* mask[MAXSEG];
     long long ldm[MAXSEG];
+    int accum[MAXSEG];
 };
 
-template <int NPL>
-struct BFrag {
-    u32x4 v[NPL][2];  // [plane][column block of this wave]
-};
-
-template <int NPL>
-// diagnostic timeline: s_memtime at numbered points of wave (tid / 64) of the first 64 workgroups
-#define TL(i)                                                                                  \
-    do {                                                                                       \
-        if (tl) {                                                                              \
-            const unsigned long long t_ = __builtin_amdgcn_s_memtime();                        \
-            if (lane == 0 && (i) < 64) tl[(i)] = t_;                                           \
-        }                                                                                      \
-    } while (0)
-
-__global__ __launch_bounds__(NTHR, 1) void mlp_nt_kernel(NTArgs g) {
+template <int NPL, int NSEG>
+__global__ __launch_bounds__(NTHR, 2) void mlp_nt_kernel(NTArgs g) {
     using G = NTGeo<NPL>;
     extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
     const int logical = xcd_logical(blockIdx.x, g.total);
     const int mt = logical / g.tiles_n, nt = logical % g.tiles_n;
     const long long m0 = (long long)mt * BM;
-    const int n0 = nt * BNW;
+    const int n0 = nt * NBN;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    // waves 1 x 4: wave w computes all 128 rows x columns 64 w .. 64 w + 63 (4 x 2 blocks), so the
-    // four waves load disjoint B fragments (each fragment is read once per workgroup)
     // (kernel-argument fields as locals: referencing `g` inside the lambdas makes clang copy the
     // whole argument struct to scratch and reload fields from there in the loop)
     const int Kd = g.K, ksteps = g.ksteps;
-    unsigned long long* const tl = (g.stamps && blockIdx.x < 64) ? g.stamps + (blockIdx.x * 4 + wave) * 64 : nullptr;
-    TL(0);
-    const unsigned short* const bbase = g.b;
-    const int nst = (Kd + SK - 1) / SK;  // stages
+    const long long Md = g.M;
+    const int nst = (Kd + SK - 1) / SK;  // steps
     const int nk = (Kd + 15) / 16;        // k16 steps of the B planes
-    // staging: float4 f = i * 256 + tid (i = 0..7) is row f >> 4, columns 4 (f & 15) .. + 3 of the
-    // stage, so a wave loads 4 whole 256 B row pieces per instruction and writes 8 B per plane
-    const int sr = tid >> 4, sc = 4 * (tid & 15);
-    // segment row bases (row sr; row sr + 16 i adds 16 i ld)
-    const int na = g.na;
     SegTab* const tab = reinterpret_cast<SegTab*>(reinterpret_cast<char*>(lds) + G::TAB);
     if (tid < MAXSEG) {
-        const int t = tid < na ? tid : 0;
-        tab->p[tid] = g.a[t].p;
-        tab->ld[tid] = g.a[t].ld;
         const int u = tid < g.nc ? tid : 0;
         tab->op[tid] = g.c[u].p;
         tab->old[tid] = g.c[u].ld;
         tab->mask[tid] = g.c[u].mask;
         tab->ldm[tid] = g.c[u].ldm;
+        tab->accum[tid] = g.c[u].accum;
     }
-    const int st1 = na > 1 ? g.a[1].start : Kd, st2 = na > 2 ? g.a[2].start : Kd;
-    const int kmax4 = (Kd + 3) / 4 * 4 - 4;
-    const long long mlast = g.M - 1;
-    // this wave's B fragments: column blocks nb0 .. nb0 + 3 (the planes are zero padded to whole
-    // 256-column tiles, so no block index needs a clamp)
-    const int nb0 = (n0 + 64 * wave) / 32;
+    // staging: rows sr + 32 i (i = 0..3), columns sc .. sc + 3 of the step; a wave instruction reads
+    // 8 rows x 128 B
+    const int sr = tid >> 3, sc = 4 * (tid & 7);
+    const long long rows_left = Md - m0;
+    const int rows = rows_left < BM ? (int)rows_left : BM;
+    __amdgpu_buffer_rsrc_t ars[NSEG];
+    unsigned arow[NSEG], astep[NSEG];
+    int ast[NSEG], alim[NSEG];
+#pragma unroll
+    for (int sg = 0; sg < NSEG; ++sg) {
+        const long long ld = g.a[sg].ld;
+        ars[sg] = __builtin_amdgcn_make_buffer_rsrc((void*)(g.a[sg].p + m0 * ld), 0, (int)(rows * ld * 4), 0x00020000);
+        arow[sg] = (unsigned)(sr * ld * 4);
+        astep[sg] = (unsigned)(32 * ld * 4);
+        ast[sg] = g.a[sg].start;
+        alim[sg] = g.a[sg].start + (g.a[sg].cols + 3) / 4 * 4;
+    }
+    // this wave's B fragments: column block (n0 + 32 w) / 32 (the planes are zero padded to whole
+    // 256-row tiles, so no block index needs a clamp)
     const long long bstride = (long long)ksteps * NPL * 512;  // elements per 32-column block
-    const unsigned short* bl = bbase + nb0 * bstride + lane * 8;
+    const unsigned short* const bl = g.b + ((n0 + 32 * wave) / 32) * bstride + lane * 8;
 
-    f32x16 acc[4][2];
+    f32x16 acc[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{0};
+    for (int i = 0; i < 4; ++i) acc[i] = f32x16{0};
 
-    auto fetch_b = [&](int kt, BFrag<NPL>& f) {
+    struct BF {
+        u32x4 v[NPL];
+    };
+    auto fetch_b = [&](int kt, BF& f) {
         kt = kt < nk ? kt : nk - 1;
         const unsigned short* bk = bl + (long long)kt * NPL * 512;
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int p = 0; p < NPL; ++p) f.v[p][j] = *reinterpret_cast<const u32x4*>(bk + j * bstride + p * 512);
+        for (int p = 0; p < NPL; ++p) f.v[p] = *reinterpret_cast<const u32x4*>(bk + p * 512);
     };
-    // the stage's 8 float4 of this thread: unconditional loads (clamped row / column, zeroed when
-    // staged), so the compiler's counted vmcnt waits stay exact
-    f32x4 R[8];
-    auto fetch_a = [&](int st) {
-        st = st < nst ? st : nst - 1;
-        int kc = st * SK + sc;
-        kc = kc < kmax4 ? kc : kmax4;
-        const int si = kc >= st2 ? 2 : (kc >= st1 ? 1 : 0);
-        const float* base = tab->p[si];
-        const long long ld = tab->ld[si];
-        const int col = kc - (si == 2 ? st2 : (si == 1 ? st1 : 0));
+    struct RA {
+        f32x4 v[4][NSEG];
+    };
+    // (steps past K read nothing: every column is outside every segment)
+    auto fetch_a = [&](int st, RA& R) {
+        const int col = st * SK + sc;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            long long m = m0 + sr + 16 * i;
-            m = m < mlast ? m : mlast;
-            R[i] = *(gf32x4*)(base + m * ld + col);
+        for (int sg = 0; sg < NSEG; ++sg) {
+            const unsigned vo = col >= ast[sg] && col < alim[sg] ? arow[sg] + (unsigned)(col - ast[sg]) * 4u : NOOB;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                R.v[i][sg] = __builtin_bit_cast(
+                    f32x4, __builtin_amdgcn_raw_buffer_load_b128(ars[sg], vo + (unsigned)i * astep[sg], 0, 0));
         }
     };
-    auto stage_a = [&](int buf, int st) {
-        unsigned short* P = lds + buf * G::STAGE;
-        const bool live = st * SK + sc < Kd;  // (the last group of a ragged K is finite, B is 0 there)
+    auto stage_a = [&](int buf, const RA& R) {
+        unsigned short* const P = lds + buf * G::STAGE + sr * SLDP + sc;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            float r[4];
+        for (int i = 0; i < 4; ++i) {
+            float v[4];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) r[e] = live ? R[i][e] : 0.0f;
+            for (int e = 0; e < 4; ++e) {
+                // (through float rvalues: clang's bit_cast of a vector-element lvalue reads element 0)
+                const float x0 = R.v[i][0][e];
+                unsigned b = __builtin_bit_cast(unsigned, x0);
+#pragma unroll
+                for (int sg = 1; sg < NSEG; ++sg) {  // (one segment is live per lane, the others read 0)
+                    const float xs = R.v[i][sg][e];
+                    b |= __builtin_bit_cast(unsigned, xs);
+                }
+                v[e] = __builtin_bit_cast(float, b);
+            }
 #pragma unroll
             for (int p = 0; p < NPL; ++p) {
-                bf16x4 h;
+                unsigned w[2];
 #pragma unroll
-                for (int e = 0; e < 4; ++e) h[e] = (__bf16)r[e];
-                if (p + 1 < NPL) {
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) r[e] -= (float)h[e];
+                for (int q = 0; q < 2; ++q) {
+                    const bf16x2 h = __builtin_convertvector((f32x2){v[2 * q], v[2 * q + 1]}, bf16x2);
+                    w[q] = __builtin_bit_cast(unsigned, h);
+                    if (p + 1 < NPL) {
+                        v[2 * q] -= (float)h[0];
+                        v[2 * q + 1] -= (float)h[1];
+                    }
                 }
-                *reinterpret_cast<bf16x4*>(P + p * G::PLANE + (sr + 16 * i) * SLDP + sc) = h;
+                typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+                *reinterpret_cast<u32x2*>(P + p * G::PLANE + 32 * i * SLDP) = u32x2{w[0], w[1]};
             }
         }
     };
-    auto step = [&](int buf, int ks, const BFrag<NPL>& f) {
+    auto step = [&](int buf, int kk, const BF& f) {
         const unsigned short* A = lds + buf * G::STAGE;
-        const int r = lane & 31, kh = 16 * ks + 8 * (lane >> 5);
-        bf16x8 a[NPL][4];
+        const int r = lane & 31, kh = 16 * kk + 8 * (lane >> 5);
+        bf16x8 a[NPL][4], b[NPL];
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int p = 0; p < NPL; ++p)
                 a[p][i] = *reinterpret_cast<const bf16x8*>(A + p * G::PLANE + (32 * i + r) * SLDP + kh);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            bf16x8 b[NPL];
+        for (int p = 0; p < NPL; ++p) b[p] = __builtin_bit_cast(bf16x8, f.v[p]);
 #pragma unroll
-            for (int p = 0; p < NPL; ++p) b[p] = __builtin_bit_cast(bf16x8, f.v[p][j]);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                f32x16 c = acc[i][j];
-                if constexpr (NPL == 3) {
-                    c = mfma(a[2][i], b[0], c);
-                    c = mfma(a[1][i], b[1], c);
-                    c = mfma(a[0][i], b[2], c);
-                }
-                c = mfma(a[1][i], b[0], c);
-                c = mfma(a[0][i], b[1], c);
-                acc[i][j] = mfma(a[0][i], b[0], c);
+        for (int i = 0; i < 4; ++i) {
+            f32x16 c = acc[i];
+            if constexpr (NPL == 3) {
+                c = mfma(a[2][i], b[0], c);
+                c = mfma(a[1][i], b[1], c);
+                c = mfma(a[0][i], b[2], c);
             }
+            c = mfma(a[1][i], b[0], c);
+            c = mfma(a[0][i], b[1], c);
+            acc[i] = mfma(a[0][i], b[0], c);
         }
     };
-    BFrag<NPL> f0, f1;
-    __syncthreads();  // (the segment tables)
-    fetch_a(0);
+    RA R0, R1;
+    BF f0, f1;
+    fetch_a(0, R0);
+    fetch_a(1, R1);
     fetch_b(0, f0);
-    stage_a(0, 0);
-    TL(1);
-    fetch_a(1);
+    __builtin_amdgcn_sched_barrier(0);
+    stage_a(0, R0);
     __syncthreads();
-    TL(2);
     // (sched_barrier after every fetch: without it the scheduler sinks the loads to their first use
-    // to save registers, and each fragment then waits out its full L2 round trip)
-    for (int st = 0; st < nst; ++st) {
-        const int buf = st & 1, k0 = 4 * st;
-        // four k16 steps; B fragments one step ahead in the other register set
-        fetch_b(k0 + 1, f1);
+    // to save registers, and each then waits out its full round trip)
+    for (int st = 0; st < nst; st += 2) {
+        fetch_a(st + 2, R0);
         __builtin_amdgcn_sched_barrier(0);
-        step(buf, 0, f0);
+        fetch_b(2 * st + 1, f1);
         __builtin_amdgcn_sched_barrier(0);
-        TL(3 + 8 * st);
-        fetch_b(k0 + 2, f0);
+        step(0, 0, f0);
         __builtin_amdgcn_sched_barrier(0);
-        step(buf, 1, f1);
+        fetch_b(2 * st + 2, f0);
         __builtin_amdgcn_sched_barrier(0);
-        TL(4 + 8 * st);
-        fetch_b(k0 + 3, f1);
+        step(0, 1, f1);
         __builtin_amdgcn_sched_barrier(0);
-        step(buf, 2, f0);
-        __builtin_amdgcn_sched_barrier(0);
-        TL(5 + 8 * st);
-        fetch_b(k0 + 4, f0);
-        __builtin_amdgcn_sched_barrier(0);
-        step(buf, 3, f1);
-        __builtin_amdgcn_sched_barrier(0);
-        TL(6 + 8 * st);
-        if (st + 1 < nst) {
-            stage_a(buf ^ 1, st + 1);  // (its loads were issued a stage ago)
-            TL(7 + 8 * st);
-            fetch_a(st + 2);
-            __builtin_amdgcn_sched_barrier(0);
-        }
+        if (st + 1 < nst) stage_a(1, R1);
         __syncthreads();
-        TL(8 + 8 * st);
+        if (st + 1 >= nst) break;
+        fetch_a(st + 3, R1);
+        __builtin_amdgcn_sched_barrier(0);
+        fetch_b(2 * st + 3, f1);
+        __builtin_amdgcn_sched_barrier(0);
+        step(1, 0, f0);
+        __builtin_amdgcn_sched_barrier(0);
+        fetch_b(2 * st + 4, f0);
+        __builtin_amdgcn_sched_barrier(0);
+        step(1, 1, f1);
+        __builtin_amdgcn_sched_barrier(0);
+        if (st + 2 < nst) stage_a(0, R0);
+        __syncthreads();
     }
-    TL(60);
-    // epilogue through LDS, 64 rows at a time: the waves write their accumulators (lane = column
-    // (lane & 31), registers = rows (r & 3) + 8 (r >> 2) + 4 (lane >> 5)) into a [64][260] fp32
-    // tile, then every wave instruction handles one whole 1 KB output row with 16 B per lane
-    // (bias, relu, relu' mask, accumulate, segment split).  Writing the accumulators straight out
-    // scatters 128 B pieces over 64 rows per instruction and ran at a third of HBM speed.
-    constexpr int TP = 260;  // tile pitch (floats)
+    // epilogue through LDS: the waves write their accumulators (lane = column (lane & 31), registers
+    // = rows (r & 3) + 8 (r >> 2) + 4 (lane >> 5)) into a [128][132] fp32 tile, then every wave
+    // instruction handles two whole 512 B output rows with 16 B per lane (bias, relu, relu' mask,
+    // accumulate, segment split).
+    constexpr int TP = 132;  // tile pitch (floats)
     float* const tile = reinterpret_cast<float*>(lds);
-    const int cs1 = g.nc > 1 ? g.c[1].start : g.N, cs2 = g.nc > 2 ? g.c[2].start : g.N;
-    const bool need_mask = g.c[0].mask || (g.nc > 1 && g.c[1].mask) || (g.nc > 2 && g.c[2].mask);
-    const float* const bias = g.bias;
-    const int relu = g.relu;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int row = 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+            tile[row * TP + 32 * wave + (lane & 31)] = acc[i][r];
+        }
+    __syncthreads();
+    // thread t: rows 8 q + (t >> 5) (q = 0..15), columns 4 (t & 31) .. + 3
+    const int c4 = 4 * (tid & 31), rb = tid >> 5;
+    const int n = n0 + c4;
     const int Nd = g.N;
-    const long long Md = g.M;
+    if (n < Nd) {
+        const int cs1 = g.nc > 1 ? g.c[1].start : Nd, cs2 = g.nc > 2 ? g.c[2].start : Nd;
+        const float* const bias = g.bias;
+        const int relu = g.relu;
+        const int si = n >= cs2 ? 2 : (n >= cs1 ? 1 : 0);
+        float* const op = tab->op[si];
+        const long long old = tab->old[si];
+        const float* const mp = tab->mask[si];
+        const long long ldm = tab->ldm[si];
+        const bool need_acc = tab->accum[si] != 0;
+        const int start = si == 2 ? cs2 : (si == 1 ? cs1 : 0);
+        const int col = n - start;
+        const int send = si == 2 ? Nd : (si == 1 ? cs2 : cs1);  // end of this segment
+        // the whole float4 inside one segment and 16 B aligned: vector path, else per element
+        const bool vec = n + 4 <= send && ((((uintptr_t)(op + col)) | (old * 4)) & 15) == 0 &&
+                         (!mp || ((((uintptr_t)(mp + col)) | (ldm * 4)) & 15) == 0);
+        f32x4 bv = {0.0f, 0.0f, 0.0f, 0.0f};
+        if (bias) {
 #pragma unroll
-    for (int hlf = 0; hlf < 2; ++hlf) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int row = 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-                    tile[row * TP + 64 * wave + 32 * j + (lane & 31)] = acc[2 * hlf + i][j][r];
-                }
-        __syncthreads();
-        // thread t: rows q * 4 + (t >> 6) (q = 0..15), columns 4 (t & 63) .. + 3
-        const int c4 = 4 * lane;
-        const int n = n0 + c4;
-        if (n < Nd) {
-            const int si = n >= cs2 ? 2 : (n >= cs1 ? 1 : 0);
-            float* const op = tab->op[si];
-            const long long old = tab->old[si];
-            const float* const mp = tab->mask[si];
-            const long long ldm = tab->ldm[si];
-            const int acc_out = si == 2 ? g.c[2].accum : (si == 1 ? g.c[1].accum : g.c[0].accum);
-            const int start = si == 2 ? cs2 : (si == 1 ? cs1 : 0);
-            const int col = n - start;
-            const int send = si == 2 ? Nd : (si == 1 ? cs2 : cs1);  // end of this segment
-            // the whole float4 inside one segment and 16 B aligned: vector path, else per element
-            const bool vec = n + 4 <= send && ((((uintptr_t)(op + col)) | (old * 4)) & 15) == 0 &&
-                             (!mp || ((((uintptr_t)(mp + col)) | (ldm * 4)) & 15) == 0);
-            f32x4 bv = {0.0f, 0.0f, 0.0f, 0.0f};
-            if (bias) {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) bv[e] = n + e < Nd ? bias[n + e] : 0.0f;
-            }
-            // mask / accumulate operands of all 16 rows first (clamped rows: no load waits on a branch)
-            const bool need_acc = acc_out != 0;
-            f32x4 mk[16], ov[16];
-            if (vec && op && need_mask && mp) {
-#pragma unroll
-                for (int q = 0; q < 16; ++q) {
-                    long long m = m0 + 64 * hlf + 4 * q + wave;
-                    m = m < Md ? m : Md - 1;
-                    mk[q] = *(gf32x4*)(mp + m * ldm + col);
-                }
-            }
-            if (vec && op && need_acc) {
-#pragma unroll
-                for (int q = 0; q < 16; ++q) {
-                    long long m = m0 + 64 * hlf + 4 * q + wave;
-                    m = m < Md ? m : Md - 1;
-                    ov[q] = *(gf32x4*)(op + m * old + col);
-                }
-            }
+            for (int e = 0; e < 4; ++e) bv[e] = n + e < Nd ? bias[n + e] : 0.0f;
+        }
+        // mask / accumulate operands of all 16 rows first (clamped rows: no load waits on a branch)
+        f32x4 mk[16], ov[16];
+        if (vec && op && mp) {
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
-                const int row = 4 * q + wave;
-                const long long m = m0 + 64 * hlf + row;
+                long long m = m0 + 8 * q + rb;
+                m = m < Md ? m : Md - 1;
+                mk[q] = *(gf32x4*)(mp + m * ldm + col);
+            }
+        }
+        if (vec && op && need_acc) {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                long long m = m0 + 8 * q + rb;
+                m = m < Md ? m : Md - 1;
+                ov[q] = *(gf32x4*)(op + m * old + col);
+            }
+        }
+        if (vec) {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int row = 8 * q + rb;
+                const long long m = m0 + row;
                 f32x4 v = *reinterpret_cast<const f32x4*>(tile + row * TP + c4);
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     v[e] += bv[e];
                     if (relu) v[e] = fmaxf(v[e], 0.0f);
                 }
-                if (vec) {
-                    if (op && m < Md) {
-                        if (need_mask && mp) {
+                if (op && m < Md) {
+                    if (mp) {
 #pragma unroll
-                            for (int e = 0; e < 4; ++e) v[e] = mk[q][e] > 0.0f ? v[e] : 0.0f;
-                        }
-                        if (need_acc) {
-#pragma unroll
-                            for (int e = 0; e < 4; ++e) v[e] += ov[q][e];
-                        }
-                        *reinterpret_cast<f32x4*>(op + m * old + col) = v;
+                        for (int e = 0; e < 4; ++e) v[e] = mk[q][e] > 0.0f ? v[e] : 0.0f;
                     }
-                } else if (m < Md) {
+                    if (need_acc) {
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const int ne = n + e;
-                        if (ne >= Nd) break;
-                        const int se = ne >= cs2 ? 2 : (ne >= cs1 ? 1 : 0);
-                        float* const ope = tab->op[se];
-                        if (!ope) continue;
-                        const int ce = ne - (se == 2 ? cs2 : (se == 1 ? cs1 : 0));
-                        const float* const mpe = tab->mask[se];
-                        float x = v[e];
-                        if (mpe && !(mpe[m * tab->ldm[se] + ce] > 0.0f)) x = 0.0f;
-                        float* de = ope + m * tab->old[se] + ce;
-                        if (se == 2 ? g.c[2].accum : (se == 1 ? g.c[1].accum : g.c[0].accum)) x += *de;
-                        *de = x;
+                        for (int e = 0; e < 4; ++e) v[e] += ov[q][e];
                     }
+                    *reinterpret_cast<f32x4*>(op + m * old + col) = v;
+                }
+            }
+        } else {  // (segment boundaries inside the float4, ragged last columns, unaligned outputs)
+#pragma unroll 1
+            for (int q = 0; q < 16; ++q) {
+                const int row = 8 * q + rb;
+                const long long m = m0 + row;
+                if (m >= Md) break;
+#pragma unroll 1
+                for (int e = 0; e < 4; ++e) {
+                    const int ne = n + e;
+                    if (ne >= Nd) break;
+                    const int se = ne >= cs2 ? 2 : (ne >= cs1 ? 1 : 0);
+                    float* const ope = tab->op[se];
+                    if (!ope) continue;
+                    float x = tile[row * TP + c4 + e] + bv[e];
+                    if (relu) x = fmaxf(x, 0.0f);
+                    const int ce = ne - (se == 2 ? cs2 : (se == 1 ? cs1 : 0));
+                    const float* const mpe = tab->mask[se];
+                    if (mpe && !(mpe[m * tab->ldm[se] + ce] > 0.0f)) x = 0.0f;
+                    float* de = ope + m * tab->old[se] + ce;
+                    if (tab->accum[se]) x += *de;
+                    *de = x;
                 }
             }
         }
-        __syncthreads();
     }
-    TL(61);
 }
 
 // ---------------------------------------------------------------- weight gradient
@@ -608,8 +444,6 @@ struct TNGeo {
 };
 
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const float* p, long long ld, long long mb, long long mhi) {
     long long rows = mhi - mb;
@@ -879,26 +713,12 @@ __global__ void split_weights_kernel(const float* __restrict__ w, int n, int k, 
 
 inline int rup(long long x, int a) { return (int)((x + a - 1) / a * a); }
 
-constexpr int KPAD = 32;  // k padding of split weights (a multiple of both BKs)
-
-// diagnostic timeline buffer (ANERF_GEMM_STAMPS=1): [64 workgroups][4 waves][64 points]
-unsigned long long* diag_stamps() {
-    static unsigned long long* const p = [] {
-        const char* e = std::getenv("ANERF_GEMM_STAMPS");
-        unsigned long long* q = nullptr;
-        if (e && e[0] == '1' && hipMalloc(&q, 64 * 4 * 64 * 8) != hipSuccess) q = nullptr;
-        if (q) (void)hipMemset(q, 0, 64 * 4 * 64 * 8);
-        return q;
-    }();
-    return p;
-}
-
 int planes_of(int precision) { return precision == ANERF_MLP_BF16X6 ? 3 : (precision == ANERF_MLP_BF16X3 ? 2 : 0); }
 
-// the dynamic LDS (80 / 72 KB) is above the default limit: raised once per kernel instance
-template <int NPL>
+// the dynamic LDS (up to 67 KB) is above the default limit: raised once per kernel instance
+template <int NPL, int NSEG>
 hipError_t nt_attr() {
-    static const hipError_t e = hipFuncSetAttribute((const void*)mlp_nt_kernel<NPL>,
+    static const hipError_t e = hipFuncSetAttribute((const void*)mlp_nt_kernel<NPL, NSEG>,
                                                     hipFuncAttributeMaxDynamicSharedMemorySize, NTGeo<NPL>::LDS_BYTES);
     return e;
 }
@@ -951,9 +771,6 @@ int wgrad_plan(int64_t m, int32_t n, int32_t k, int* splits, long long* rows) {
 
 extern "C" {
 
-// diagnostic: copy the last timeline of anerf_mlp_gemm (ANERF_GEMM_STAMPS=1) to host memory
-int anerf_mlp_diag_stamps(unsigned long long* host, size_t n);
-
 size_t anerf_mlp_split_bytes(int32_t rows, int32_t cols, int32_t precision) {
     return (size_t)2 * planes_of(precision) * rup(rows, BNW) * rup(cols, 16);
 }
@@ -985,6 +802,8 @@ int anerf_mlp_gemm(int64_t m, int32_t n, int32_t k, const anerf_seg* a, int32_t 
     g.K = k;
     int rc = set_segs(a, n_a, k, g.a);
     if (rc) return rc;
+    for (int i = 0; i < n_a; ++i)  // (a 128-row tile's byte range fits a buffer descriptor)
+        if (a[i].ld >= (1 << 22)) return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_gemm: operand ld >= 2^22");
     g.na = n_a;
     g.b = static_cast<const unsigned short*>(b_split);
     g.ksteps = (k + 15) / 16;
@@ -999,18 +818,25 @@ int anerf_mlp_gemm(int64_t m, int32_t n, int32_t k, const anerf_seg* a, int32_t 
     }
     if (start != n) return anerf_internal_fail(ANERF_EINVAL, "output segments do not add up to n");
     g.nc = n_c;
-    g.tiles_n = (n + BNW - 1) / BNW;
-    g.stamps = diag_stamps();
+    g.tiles_n = (n + NBN - 1) / NBN;
     const long long tiles = (long long)((m + BM - 1) / BM) * g.tiles_n;
     if (tiles > 0x7fffffff) return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_gemm: too many tiles");
     g.total = (int)tiles;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    hipError_t e = npl == 3 ? nt_attr<3>() : nt_attr<2>();
-    if (e != hipSuccess) return anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));
-    if (npl == 3)
-        hipLaunchKernelGGL(mlp_nt_kernel<3>, dim3((unsigned)tiles), dim3(NTHR), NTGeo<3>::LDS_BYTES, st, g);
-    else
-        hipLaunchKernelGGL(mlp_nt_kernel<2>, dim3((unsigned)tiles), dim3(NTHR), NTGeo<2>::LDS_BYTES, st, g);
+    hipError_t e = hipSuccess;
+#define ANERF_NT_LAUNCH(P, S)                                                                         \
+    if (npl == P && n_a == S) {                                                                       \
+        e = nt_attr<P, S>();                                                                          \
+        if (e != hipSuccess) return anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));            \
+        hipLaunchKernelGGL((mlp_nt_kernel<P, S>), dim3((unsigned)tiles), dim3(NTHR), NTGeo<P>::LDS_BYTES, st, g); \
+    }
+    ANERF_NT_LAUNCH(3, 1)
+    ANERF_NT_LAUNCH(3, 2)
+    ANERF_NT_LAUNCH(3, 3)
+    ANERF_NT_LAUNCH(2, 1)
+    ANERF_NT_LAUNCH(2, 2)
+    ANERF_NT_LAUNCH(2, 3)
+#undef ANERF_NT_LAUNCH
     e = hipGetLastError();
     return e == hipSuccess ? ANERF_OK : anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));
 }
@@ -1085,13 +911,6 @@ int anerf_mlp_wgrad(int64_t m, int32_t n, int32_t k, const float* dy, int64_t ld
                            (long long)g.npad, 0ll, n, db, 0ll, accumulate != 0);
     e = hipGetLastError();
     return e == hipSuccess ? ANERF_OK : anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));
-}
-
-int anerf_mlp_diag_stamps(unsigned long long* host, size_t n) {
-    unsigned long long* p = diag_stamps();
-    if (!p || !host) return ANERF_EINVAL;
-    if (n > 64 * 4 * 64) n = 64 * 4 * 64;
-    return hipMemcpy(host, p, n * 8, hipMemcpyDeviceToHost) == hipSuccess ? ANERF_OK : ANERF_EHIP;
 }
 
 }  // extern "C"

@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--prec", type=int, default=6)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--m", type=int, default=163840)
+    ap.add_argument("--cases", default="forward,input_grad,weight_grad,torch_fp32_mm,copy")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     M, W = a.m, 256
@@ -53,7 +54,8 @@ def main():
         "torch_fp32_mm": (lambda: torch.mm(x, w.t(), out=out), 2 * M * W * 4),
         "copy": (lambda: out.copy_(x), 2 * M * W * 4),
     }
-    for name, (fn, by) in cases.items():
+    for name in a.cases.split(","):
+        fn, by = cases[name]
         us = timeit(fn, a.reps)
         print(json.dumps({"case": name, "M": M, "N": W, "K": W, "prec": a.prec, "us": round(us, 1),
                           "GBps": round(by / us / 1e3, 1),
