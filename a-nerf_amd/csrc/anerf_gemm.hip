@@ -112,8 +112,8 @@ __device__ __forceinline__ f32x16 mfma(const bf16x8& a, const bf16x8& b, const f
 // fp32 in HBM, up to three column segments) is staged 32 columns per step: buffer loads through
 // per-tile segment descriptors whose range ends at the last row (rows past M and columns outside a
 // segment read zero, so no clamp, no select, no zero fill), issued two steps ahead into two register
-// sets, split with v_cvt_pk_bf16_f32 into NPL bf16 planes ([row][k], 80 B pitch: conflict-free
-// ds_read_b128 fragment reads); two LDS stages, one barrier per step.  B (the split weights, a few
+// sets, split with v_cvt_pk_bf16_f32 into NPL bf16 planes ([row][k], swizzled 64 B rows: conflict-free
+// ds_read_b128 fragment reads and staging writes); two LDS stages, one barrier per step.  B (the split weights, a few
 // hundred KB shared by every workgroup) is read straight from L2 as MFMA fragments, stored
 // fragment-major (1 KB per 32-column block, k16 step and plane, in lane order), one k16 step ahead.
 // The epilogue goes through LDS in whole 512 B output rows (bias, relu, relu' mask, accumulate,
@@ -121,12 +121,15 @@ __device__ __forceinline__ f32x16 mfma(const bf16x8& a, const bf16x8& b, const f
 constexpr int BNW = 256;      // row padding of the split weights (whole 256-row tiles)
 constexpr int NBN = 128;      // output columns per workgroup
 constexpr int SK = 32;        // k columns per step
-constexpr int SLDP = SK + 8;  // LDS row pitch (bf16): 80 B, an odd number of 16 B chunks
+// LDS planes [row][32 k] bf16, 64 B rows, the four 16 B chunks of a row XOR-swizzled by bits 2-3 of
+// the row: fragment reads (ds_read_b128, 16 rows x one chunk per lane group) and staging writes
+// (ds_write_b64, two rows per 16-lane group) are both conflict-free
+__device__ __forceinline__ int nt_off(int row, int k) { return row * SK + ((((k >> 3) ^ (row >> 2)) & 3) << 3) + (k & 7); }
 constexpr unsigned NOOB = 0x80000000u;  // a lane offset past every descriptor's range
 
 template <int NPL>
 struct NTGeo {
-    static constexpr int PLANE = BM * SLDP;           // bf16 elements
+    static constexpr int PLANE = BM * SK;             // bf16 elements
     static constexpr int STAGE = NPL * PLANE;
     static constexpr int STAGES_BYTES = 2 * STAGE * 2;
     static constexpr int TILE_BYTES = BM * 132 * 4;  // epilogue tile [128][132] fp32
@@ -219,7 +222,7 @@ __global__ __launch_bounds__(NTHR, 2) void mlp_nt_kernel(NTArgs g) {
         }
     };
     auto stage_a = [&](int buf, const RA& R) {
-        unsigned short* const P = lds + buf * G::STAGE + sr * SLDP + sc;
+        unsigned short* const P = lds + buf * G::STAGE + nt_off(sr, sc);  // (row sr + 32 i: same swizzle)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             float v[4];
@@ -248,7 +251,7 @@ __global__ __launch_bounds__(NTHR, 2) void mlp_nt_kernel(NTArgs g) {
                     }
                 }
                 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-                *reinterpret_cast<u32x2*>(P + p * G::PLANE + 32 * i * SLDP) = u32x2{w[0], w[1]};
+                *reinterpret_cast<u32x2*>(P + p * G::PLANE + 32 * i * SK) = u32x2{w[0], w[1]};
             }
         }
     };
@@ -260,7 +263,7 @@ __global__ __launch_bounds__(NTHR, 2) void mlp_nt_kernel(NTArgs g) {
         for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int p = 0; p < NPL; ++p)
-                a[p][i] = *reinterpret_cast<const bf16x8*>(A + p * G::PLANE + (32 * i + r) * SLDP + kh);
+                a[p][i] = *reinterpret_cast<const bf16x8*>(A + p * G::PLANE + nt_off(32 * i + r, kh));
 #pragma unroll
         for (int p = 0; p < NPL; ++p) b[p] = __builtin_bit_cast(bf16x8, f.v[p]);
 #pragma unroll

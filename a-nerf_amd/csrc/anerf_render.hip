@@ -478,11 +478,15 @@ int anerf_train_encode_backward(const anerf_model* m, const float* ray_batch, in
     if (rc) return rc;
     if (!grad_feat || !grad_skts) return fail(ANERF_EINVAL, "anerf_train_encode_backward: NULL gradient");
     if (n_rays == 0) return ANERF_OK;
-    const int64_t nb = n_rays * ((m->desc.n_joints + 3) / 4);
-    if (nb > 0x7fffffff) return fail(ANERF_EINVAL, "too many rays for one launch");
+    if (n_rays > 0x7fffffff) return fail(ANERF_EINVAL, "too many rays for one launch");
+    const int nj = m->desc.n_joints;
+    if (nj > 256) return fail(ANERF_EINVAL, "anerf_train_encode_backward: more than 256 joints");
+    const int spb = 256 / nj;                      // sample slots per block
+    const int threads = (spb * nj + 63) / 64 * 64;  // (whole waves)
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    hipLaunchKernelGGL(train_encode_backward_kernel, dim3((unsigned)nb), dim3(256), 0, st, m->md, ray_batch,
-                       ray_stride, n_rays, z, n_samples, skts, ray_pose, n_poses, pts_noise, grad_feat, grad_skts);
+    hipLaunchKernelGGL(train_encode_backward_kernel, dim3((unsigned)n_rays), dim3(threads),
+                       (size_t)spb * nj * 12 * sizeof(float), st, m->md, ray_batch, ray_stride, n_rays, z, n_samples,
+                       skts, ray_pose, n_poses, pts_noise, grad_feat, grad_skts, spb);
     HIP_TRY(hipGetLastError());
     return ANERF_OK;
 }

@@ -201,11 +201,12 @@ __device__ __forceinline__ void encode_row_grad_joint(const ModelDev& M, const f
     }
 }
 
-// Encoder backward: dL/dskts from dL/dfeat.  Block = (ray, 4 joints); lane = (sample, joint):
-// 16 samples x the group's 4 joints per wave, so the lanes of one sample read the 4 joints'
-// adjacent feature columns (16-48 B runs) instead of one 4-byte element per lane from 64 rows.
-// Per joint, the 12 sums are reduced over the wave's lanes of that joint (xor shuffles 4..32),
-// then over the 4 waves in LDS, and accumulated into grad_skts[pose] (atomic: rays may share a
+// Encoder backward: dL/dskts from dL/dfeat.  Block = one ray, thread = (sample slot, joint) with the
+// joint fastest (spb sample slots x nj joints, spb = 256 / nj), so each thread keeps one joint's 12
+// sums over the samples s = slot, slot + spb, ... and the lanes of a wave read each feature of a
+// sample as one nj-float run (the feature rows are joint-minor): every 4.3 KB feature row is read
+// once, by one wave, in whole runs.  The slots' sums are added through LDS in slot order
+// (deterministic within the ray) and accumulated into grad_skts[pose] (atomic: rays may share a
 // pose).  Rows 3 (the [0 0 0 1] row) get no gradient, as in the reference.
 __global__ __launch_bounds__(256) void train_encode_backward_kernel(ModelDev M, const float* __restrict__ rb,
                                                                     int stride, int64_t n, const float* __restrict__ z,
@@ -213,25 +214,22 @@ __global__ __launch_bounds__(256) void train_encode_backward_kernel(ModelDev M, 
                                                                     const int32_t* __restrict__ ray_pose, int n_poses,
                                                                     const float* __restrict__ pts_noise,
                                                                     const float* __restrict__ gfeat,
-                                                                    float* __restrict__ gskts) {
-    __shared__ float red[4][4][12];
-    const int ngrp = (M.nj + 3) / 4;
-    const int64_t i = blockIdx.x / ngrp;
-    const int j0 = (int)(blockIdx.x % ngrp) * 4;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int jj = lane & 3, j = j0 + jj;
+                                                                    float* __restrict__ gskts, int spb) {
+    extern __shared__ float red[];  // [spb][nj][12]
+    const int nj = M.nj;
+    const int64_t i = blockIdx.x;
+    const int t = threadIdx.x, slot = t / nj, j = t % nj;
     // (an out-of-range pose index contributes no gradient and is never dereferenced)
-    const int64_t pose = i < n ? (ray_pose ? ray_pose[i] : i) : 0;
+    const int64_t pose = ray_pose ? ray_pose[i] : i;
     const bool pose_ok = pose >= 0 && pose < n_poses;
-    const bool live = i < n && j < M.nj && pose_ok;
     float gS[12] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-    if (live) {
+    if (pose_ok && slot < spb) {
         const float* ray = rb + i * stride;
-        const int F = M.nj * (1 + 2 * M.mr) + 3 * M.nj + 3 * M.nj * (1 + 2 * M.mrv);
-        const f32x4* sp = reinterpret_cast<const f32x4*>(skts + (pose * M.nj + j) * 16);
+        const int F = nj * (1 + 2 * M.mr) + 3 * nj + 3 * nj * (1 + 2 * M.mrv);
+        const f32x4* sp = reinterpret_cast<const f32x4*>(skts + (pose * nj + j) * 16);
         const f32x4 r0 = sp[0], r1 = sp[1], r2 = sp[2];
         const float S[12] = {r0[0], r0[1], r0[2], r0[3], r1[0], r1[1], r1[2], r1[3], r2[0], r2[1], r2[2], r2[3]};
-        for (int s = wave * 16 + (lane >> 2); s < ns; s += 64) {
+        for (int s = slot; s < ns; s += spb) {
             const float zz = z[i * ns + s];
             float px = ray[0] + ray[3] * zz, py = ray[1] + ray[4] * zz, pz = ray[2] + ray[5] * zz;
             if (pts_noise) {
@@ -240,23 +238,17 @@ __global__ __launch_bounds__(256) void train_encode_backward_kernel(ModelDev M, 
             }
             encode_row_grad_joint(M, S, j, px, py, pz, ray[3], ray[4], ray[5], gfeat + (i * ns + s) * F, gS);
         }
-    }
+        float* const rr = red + (slot * nj + j) * 12;
 #pragma unroll
-    for (int k = 0; k < 12; ++k) {
-        float v = gS[k];
-        v += __shfl_xor(v, 4);
-        v += __shfl_xor(v, 8);
-        v += __shfl_xor(v, 16);
-        v += __shfl_xor(v, 32);
-        if (lane < 4) red[wave][lane][k] = v;
+        for (int k = 0; k < 12; ++k) rr[k] = gS[k];
     }
     __syncthreads();
-    if (threadIdx.x < 48) {
-        const int jq = threadIdx.x / 12, k = threadIdx.x % 12;
-        if (i < n && j0 + jq < M.nj && pose_ok) {
-            const float v = (red[0][jq][k] + red[1][jq][k]) + (red[2][jq][k] + red[3][jq][k]);
-            if (v != 0.0f) atomicAdd(gskts + (pose * M.nj + j0 + jq) * 16 + k, v);
-        }
+    if (!pose_ok) return;
+    for (int q = t; q < nj * 12; q += blockDim.x) {
+        float v = red[q];
+        for (int sl = 1; sl < spb; ++sl) v += red[sl * nj * 12 + q];
+        const int jq = q / 12, k = q % 12;
+        if (v != 0.0f) atomicAdd(gskts + (pose * nj + jq) * 16 + k, v);
     }
 }
 
