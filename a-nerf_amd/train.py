@@ -585,17 +585,58 @@ class TrainRayCaster(nn.Module):
         return out
 
 
-def nerf_loss(preds, target, bgs=None, use_background=False, coarse_weight=1.0):
-    """Trainer._compute_nerf_loss with loss_fn MSE (core/trainer.py:350-381): the rgb loss of the fine
-    and (weighted) coarse outputs, background composited with (1 - acc) when use_background."""
-    def one(rgb, acc):
+def _img_loss(name, x, y, reduction="mean", beta=0.1):
+    """get_loss_fn / get_reg_fn (core/trainer.py:10-58, 147-170): MSE (img2mse), L1 (img2l1),
+    Huber (F.smooth_l1_loss with beta), BCE (acc2bce, eps 1e-8; reduction 'off' = the mean over
+    y < 1)."""
+    if name == "MSE":
+        d = (x - y) ** 2
+    elif name == "L1":
+        d = (x - y).abs()
+    elif name == "Huber":
+        return F.smooth_l1_loss(x, y, reduction=reduction, beta=beta)
+    elif name == "BCE":
+        d = -(y * torch.log(x + 1e-8) + (1.0 - y) * torch.log(1 - x + 1e-8))
+        if reduction == "off":
+            return torch.mean(d[y < 1.0])
+    else:
+        raise NotImplementedError(f"loss {name!r}")
+    if reduction == "mean":
+        return torch.mean(d)
+    if reduction == "sum":
+        return torch.sum(d)
+    return d
+
+
+def nerf_loss(preds, target, bgs=None, use_background=False, coarse_weight=1.0, loss_fn="MSE", loss_beta=0.1,
+              reg_fn=None, reg_coef=0.1, fgs=None, return_dict=False):
+    """Trainer._compute_nerf_loss (core/trainer.py:350-381) for the fine and the coarse outputs, summed
+    as Trainer.compute_loss sums them (:325-345): the rgb loss (`loss_fn` MSE / L1 / Huber with
+    `loss_beta`) of the prediction composited over the background with (1 - acc) when
+    use_background, the coarse one times `coarse_weight`; with `reg_fn` (BCE / L1 / MSE) the
+    regulariser reg_fn(acc, fgs[..., 0], reduction='off') * reg_coef per pass (not coarse-weighted).
+    Returns the total, or (total, {name: loss}) with return_dict (the reference's loss_dict keys)."""
+    if reg_fn is not None and fgs is None:
+        raise ValueError("reg_fn needs the batch's fgs")
+
+    def one(rgb, acc, coarse, out):
         if use_background:
             rgb = rgb + (1.0 - acc)[..., None] * (1.0 if bgs is None else bgs)
-        return F.mse_loss(rgb, target, reduction="mean")
-    loss = one(preds["rgb_map"], preds["acc_map"])
+        loss = _img_loss(loss_fn, rgb, target, "mean", loss_beta)
+        if coarse:
+            loss = loss * coarse_weight
+        out["rgb_loss0" if coarse else "rgb_loss"] = loss
+        if reg_fn is not None:
+            out["reg_loss0" if coarse else "reg_loss"] = _img_loss(reg_fn, acc, fgs[..., 0], "off") * reg_coef
+
+    parts = {}
+    one(preds["rgb_map"], preds["acc_map"], False, parts)
     if "rgb0" in preds:
-        loss = loss + one(preds["rgb0"], preds["acc0"]) * coarse_weight
-    return loss
+        one(preds["rgb0"], preds["acc0"], True, parts)
+    total = 0.0
+    for v in parts.values():
+        total = total + v
+    return (total, parts) if return_dict else total
 
 
 __all__ = ["TrainRayCaster", "NeRF", "nerf_loss", "RenderConfig"]

@@ -104,3 +104,35 @@ def test_single_net_shares_one_module_and_fine_keys_win():
     assert set(ck["network_fn_state_dict"]) == set(ck["network_fine_state_dict"])
     for k, v in ck["network_fn_state_dict"].items():
         assert torch.equal(v, torch.as_tensor(g.ckpt["network_fine_state_dict"][k])), k
+
+
+def test_nerf_loss_functions_follow_trainer():
+    """loss_fn MSE / L1 / Huber (the shipped h36m / mixamo / perfcap configs use L1) and the BCE
+    regulariser, restated from core/trainer.py:10-58 (img2mse, img2l1, acc2bce, img2huber) and
+    _compute_nerf_loss / compute_loss (:325-381): background composite, coarse weight on the rgb
+    term only, reg over fgs < 1, everything summed."""
+    g = torch.Generator().manual_seed(0)
+    n = 257
+    preds = {"rgb_map": torch.rand(n, 3, generator=g), "acc_map": torch.rand(n, generator=g) * 0.98 + 0.01,
+             "rgb0": torch.rand(n, 3, generator=g), "acc0": torch.rand(n, generator=g) * 0.98 + 0.01}
+    tgt = torch.rand(n, 3, generator=g)
+    fgs = (torch.rand(n, 1, generator=g) > 0.5).float()
+    bgs = torch.rand(n, 3, generator=g)
+    for fn, ref in (("MSE", lambda x, y: ((x - y) ** 2).mean()), ("L1", lambda x, y: (x - y).abs().mean()),
+                    ("Huber", lambda x, y: F.smooth_l1_loss(x, y, beta=0.05))):
+        total, parts = train.nerf_loss(preds, tgt, bgs=bgs, use_background=True, coarse_weight=0.5, loss_fn=fn,
+                                       loss_beta=0.05, reg_fn="BCE", reg_coef=0.3, fgs=fgs, return_dict=True)
+        want = {}
+        for c, (rk, ak) in enumerate((("rgb_map", "acc_map"), ("rgb0", "acc0"))):
+            rgb = preds[rk] + (1.0 - preds[ak])[..., None] * bgs
+            acc, y = preds[ak], fgs[..., 0]
+            bce = -(y * torch.log(acc + 1e-8) + (1.0 - y) * torch.log(1 - acc + 1e-8))
+            want["rgb_loss" + ("0" if c else "")] = ref(rgb, tgt) * (0.5 if c else 1.0)
+            want["reg_loss" + ("0" if c else "")] = bce[y < 1.0].mean() * 0.3
+        assert set(parts) == set(want)
+        for k in want:
+            assert torch.allclose(parts[k], want[k], rtol=1e-6, atol=0), (fn, k)
+        assert torch.allclose(total, sum(want.values()), rtol=1e-6)
+    # the default stays the round-1 MSE form
+    plain = train.nerf_loss(preds, tgt)
+    assert torch.allclose(plain, ((preds["rgb_map"] - tgt) ** 2).mean() + ((preds["rgb0"] - tgt) ** 2).mean())
