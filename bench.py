@@ -71,6 +71,8 @@ def parse():
     ap.add_argument("--cpu-rays", type=int, default=20000, help="rays in the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline (and its parity check)")
     ap.add_argument("--no-tau20", action="store_true", help="skip the tau = 20 kernel timing")
+    ap.add_argument("--no-train", action="store_true",
+                    help="skip the training-step leg (SURVEY §8(f) row 2: tools/train_bench.py, N = 1 only)")
     ap.add_argument("--shard", default=None, choices=["frames", "pixels"],
                     help="frames: one frame per rank (weak scaling, no collective); pixels: ONE frame per step "
                          "split into whole 4096-ray chunks across the ranks + an RCCL all-gather of the ray "
@@ -289,6 +291,14 @@ def main():
                      "frac_executed": round(tflop / (tms * 1e-3) / 1e12 / tpeak, 4)}
             del rc20
 
+    # N = 1: the training step of the same path at the reference's training configuration (§8(f) row 2)
+    training = None
+    if rank == 0 and world == 1 and not a.no_train:
+        sys.path.insert(0, os.path.join(REPO, "tools"))
+        import train_bench
+        training = train_bench.measure(train_bench.parser().parse_args(["--steps", "10", "--warmup", "2"]), dev=dev)
+        training.pop("data", None)
+
     cpu, parity = None, None
     if rank == 0 and world == 1 and not a.no_cpu:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -349,6 +359,7 @@ def main():
             "tau20": tau20,
             "cpu_baseline": cpu,
             "other_precisions": others or None,
+            "training": training,
         }
         print(json.dumps(line), flush=True)
     if dist:

@@ -23,7 +23,7 @@ sys.path.insert(0, REPO)
 FP32_MFMA_PEAK_TFLOPS = 157.3
 
 
-def main():
+def parser():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
@@ -33,18 +33,22 @@ def main():
     ap.add_argument("--importance", type=int, default=16)
     ap.add_argument("--mlp", default="mixed", choices=["mixed", "bf16x6", "bf16x3", "fp32"],
                     help="training MLP arithmetic (train.TrainRayCaster mlp=)")
-    a = ap.parse_args()
+    return ap
+
+
+def measure(a, dev=None):
+    """One training-step measurement (the dict main() prints); also bench.py's `training` leg."""
     anerf = importlib.import_module("a-nerf_amd")
     syn = importlib.import_module("a-nerf_amd.synthetic")
     train = importlib.import_module("a-nerf_amd.train")
-    dev = torch.device("cuda:0")
+    dev = dev or torch.device("cuda:0")
     S, I, n = a.samples, a.importance, a.rays
     cfg = anerf.RenderConfig(N_samples=S, N_importance=I).validate()
     ck = syn.make_checkpoint(13, n_joints=24, D=8, W=256, fine=True, tau=20.0)
     sc = syn.make_scene(n_joints=24, H=512, W=512, seed=13, n_frames=a.images, yaw_step=2 * np.pi / a.images)
     idx, cyls, _ = anerf.rays.valid_pixels(sc["c2ws"], 512, 512, sc["focal"], kps=sc["kps"], ext_scale=0.001)
     rng = np.random.default_rng(0)
-    tr = train.TrainRayCaster(cfg, ck, mlp=a.mlp).train()
+    tr = train.TrainRayCaster(cfg, ck, device=dev, mlp=a.mlp).train()
     skts = torch.from_numpy(sc["skts"]).to(dev)
     delta = torch.zeros_like(skts, requires_grad=True)  # pose optimisation variable per image
     opt = torch.optim.Adam(list(tr.parameters()) + [delta], lr=5e-4)
@@ -86,14 +90,18 @@ def main():
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.steps
     flop = 3 * anerf.flops_per_sample(cfg) * n * anerf.samples_per_ray(cfg)
-    print(json.dumps({
+    return {
         "metric": "training rays/s (render_rays fwd + loss + bwd + Adam; N_rand 2048, 64+16 samples, 8x256, "
                   "128 images with pose optimisation)",
         "value": round(n / dt, 1), "unit": "rays/s", "ms_per_step": round(1e3 * dt, 3), "steps": a.steps,
         "dtype": "fp32" if a.mlp == "fp32" else f"fp32 in/out, MLP GEMMs as split bf16 ({a.mlp})", "mlp": a.mlp,
         "mlp_gemm_flop_per_step": flop, "mlp_tflops": round(flop / dt / 1e12, 2),
         "frac_of_fp32_mfma_peak": round(flop / dt / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4),
-        "data": "synthetic (seeded SMPL-24 poses, 128 cameras on a circle, seeded weights)"}), flush=True)
+        "data": "synthetic (seeded SMPL-24 poses, 128 cameras on a circle, seeded weights)"}
+
+
+def main():
+    print(json.dumps(measure(parser().parse_args())), flush=True)
 
 
 if __name__ == "__main__":
