@@ -426,37 +426,48 @@ __global__ __launch_bounds__(NTHR, 2) void mlp_nt_kernel(NTArgs g) {
 // ---------------------------------------------------------------- weight gradient
 // dW tile 128 (n) x 128 (k) per workgroup over a slab of rows (4 waves, 2 x 2: 64 x 64 each).  Both
 // operands are activations read along their rows: a step stages 16 rows of dY (columns n0..) and of
-// X (columns k0..), a thread 8 consecutive columns of one row (a wave instruction reads four whole
-// 512 B row pieces), split into NPL bf16 planes kept row-major ([row][128] at a 320 B pitch, one
-// ds_write_b128 per plane).  The MFMA fragments (8 rows of one column) come back through the
-// hardware transpose read ds_read_b64_tr_b16, two per fragment, conflict-free at that pitch.
+// X (columns k0..) (32 rows for bf16x3 with one X segment), a thread 8 consecutive columns of a row
+// (a wave instruction reads four whole 512 B row pieces), split into NPL bf16 planes kept row-major
+// ([row][128], swizzled 256 B rows, one ds_write_b128 per plane and row).  The MFMA fragments (8
+// rows of one column) come back through the hardware transpose read ds_read_b64_tr_b16, two per
+// fragment, conflict-free with the swizzle.
 // Loads are buffer loads through per-step descriptors whose range ends at the slab's last row, so
 // rows past the slab and columns outside the operand read zero without a clamp or a select; a
 // thread's offsets are constant over the whole slab.  Two LDS stages, two register sets in flight;
 // the partial tile leaves through LDS in full rows.  The bias gradient (k-tile 0) sums the staged
 // dY per column in a fixed order.
-constexpr int TSK = 16;                // rows per step
-constexpr int TPB = 320;               // plane row pitch, bytes (128 bf16 + 64: rows q*80 dwords apart)
+constexpr int TSK = 32;                 // rows per step, at most (slabs are whole pairs of steps)
 constexpr unsigned TOOB = 0x40000000u;  // a lane offset past every descriptor's range (ld < 2^24)
 
-template <int NPL>
+// plane [row][128 bf16]: 256 B rows whose 16 B chunks are XOR-swizzled by 4 (row & 3), so the four
+// rows of a transposed read's lane group (64 B each) land on disjoint banks and a staging write (8
+// lanes x one chunk of a row) stays conflict-free
+__device__ __forceinline__ int tn_off(int row, int chunk) { return row * 256 + ((chunk ^ (4 * (row & 3))) << 4); }
+
+template <int NPL, int NSEG>
 struct TNGeo {
-    static constexpr int PLANE = TSK * TPB;        // bytes
+    // rows per step: 32 where two register sets of them fit in 256 VGPRs (bf16x3, one X segment),
+    // else 16
+    static constexpr int SK = NPL == 2 && NSEG == 1 ? 32 : 16;
+    static constexpr int PR = SK / 16;             // rows per staging thread
+    static constexpr int PLANE = SK * 256;         // bytes
     static constexpr int STAGE = 2 * NPL * PLANE;  // dY planes, then X planes
     static constexpr int LDS_BYTES = 2 * STAGE > 128 * 132 * 4 ? 2 * STAGE : 128 * 132 * 4;
 };
 
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
+template <int SK>
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const float* p, long long ld, long long mb, long long mhi) {
     long long rows = mhi - mb;
-    rows = rows < 0 ? 0 : (rows > TSK ? TSK : rows);
+    rows = rows < 0 ? 0 : (rows > SK ? SK : rows);
     return __builtin_amdgcn_make_buffer_rsrc((void*)(p + mb * ld), 0, (int)(rows * ld * 4), 0x00020000);
 }
 
 template <int NPL, int NSEG>
 __global__ __launch_bounds__(NTHR, 2) void mlp_tn_kernel(TNArgs g) {
-    using G = TNGeo<NPL>;
+    using G = TNGeo<NPL, NSEG>;
+    constexpr int SK = G::SK, PR = G::PR;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds8[];
     const int logical = xcd_logical(blockIdx.x, g.total);
     const int split = logical / g.tiles, tile = logical % g.tiles;
@@ -467,8 +478,9 @@ __global__ __launch_bounds__(NTHR, 2) void mlp_tn_kernel(TNArgs g) {
     if (mhi > g.M) mhi = g.M;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wr = wave >> 1, wc = wave & 1;
-    // staging unit: row r of the step, columns c8 .. c8 + 7 of the tile
+    // staging unit: rows r + 16 u (u < PR) of the step, columns c8 .. c8 + 7 of the tile
     const int r = tid >> 4, c8 = 8 * (tid & 15);
+    const unsigned ystep = (unsigned)(16 * g.lddy * 4);
     const float* const dyp = g.dy;
     const long long lddy = g.lddy;
     const int nlim = (g.N + 3) / 4 * 4;
@@ -480,11 +492,12 @@ __global__ __launch_bounds__(NTHR, 2) void mlp_tn_kernel(TNArgs g) {
     }
     const float* xp[NSEG];
     long long xld[NSEG];
-    unsigned vox[2][NSEG];
+    unsigned vox[2][NSEG], xstep[NSEG];
 #pragma unroll
     for (int sg = 0; sg < NSEG; ++sg) {
         xp[sg] = g.x[sg].p;
         xld[sg] = g.x[sg].ld;
+        xstep[sg] = (unsigned)(16 * xld[sg] * 4);
         const int st0 = g.x[sg].start, lim = st0 + (g.x[sg].cols + 3) / 4 * 4;
 #pragma unroll
         for (int f = 0; f < 2; ++f) {
@@ -504,19 +517,26 @@ __global__ __launch_bounds__(NTHR, 2) void mlp_tn_kernel(TNArgs g) {
         for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{0};
 
     struct Regs {
-        f32x4 y[2], x[2][NSEG];
+        f32x4 y[PR][2], x[PR][2][NSEG];
     };
+    // (a TOOB lane offset plus 16 rows stays past the range: ld < 2^24)
     auto fetch = [&](long long mb, Regs& R) {
-        const __amdgpu_buffer_rsrc_t ry = rows_rsrc(dyp, lddy, mb, mhi);
+        const __amdgpu_buffer_rsrc_t ry = rows_rsrc<SK>(dyp, lddy, mb, mhi);
 #pragma unroll
-        for (int f = 0; f < 2; ++f)
-            R.y[f] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ry, voy[f], 0, 0));
-#pragma unroll
-        for (int sg = 0; sg < NSEG; ++sg) {
-            const __amdgpu_buffer_rsrc_t rx = rows_rsrc(xp[sg], xld[sg], mb, mhi);
+        for (int u = 0; u < PR; ++u)
 #pragma unroll
             for (int f = 0; f < 2; ++f)
-                R.x[f][sg] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, vox[f][sg], 0, 0));
+                R.y[u][f] = __builtin_bit_cast(
+                    f32x4, __builtin_amdgcn_raw_buffer_load_b128(ry, voy[f] + (unsigned)u * ystep, 0, 0));
+#pragma unroll
+        for (int sg = 0; sg < NSEG; ++sg) {
+            const __amdgpu_buffer_rsrc_t rx = rows_rsrc<SK>(xp[sg], xld[sg], mb, mhi);
+#pragma unroll
+            for (int u = 0; u < PR; ++u)
+#pragma unroll
+                for (int f = 0; f < 2; ++f)
+                    R.x[u][f][sg] = __builtin_bit_cast(
+                        f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, vox[f][sg] + (unsigned)u * xstep[sg], 0, 0));
         }
     };
     // 8 values -> NPL planes of packed bf16 pairs (round to nearest even of the running remainder)
@@ -537,84 +557,92 @@ __global__ __launch_bounds__(NTHR, 2) void mlp_tn_kernel(TNArgs g) {
         }
     };
     auto stage = [&](int buf, const Regs& R) {
-        unsigned char* const P = lds8 + buf * G::STAGE + r * TPB + 2 * c8;
-        float y[8], x[8];
 #pragma unroll
-        for (int f = 0; f < 2; ++f)
+        for (int u = 0; u < PR; ++u) {
+            // (rows r + 16 u share r's swizzle)
+            unsigned char* const P = lds8 + buf * G::STAGE + tn_off(r + 16 * u, c8 >> 3);
+            float y[8], x[8];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                y[4 * f + e] = R.y[f][e];
-                // (through float rvalues: clang's bit_cast of a vector-element lvalue reads element 0)
-                const float x0 = R.x[f][0][e];
-                unsigned b = __builtin_bit_cast(unsigned, x0);
+            for (int f = 0; f < 2; ++f)
 #pragma unroll
-                for (int sg = 1; sg < NSEG; ++sg) {  // (one segment is live per lane, the others read 0)
-                    const float xs = R.x[f][sg][e];
-                    b |= __builtin_bit_cast(unsigned, xs);
+                for (int e = 0; e < 4; ++e) {
+                    y[4 * f + e] = R.y[u][f][e];
+                    // (through float rvalues: clang's bit_cast of a vector-element lvalue reads element 0)
+                    const float x0 = R.x[u][f][0][e];
+                    unsigned b = __builtin_bit_cast(unsigned, x0);
+#pragma unroll
+                    for (int sg = 1; sg < NSEG; ++sg) {  // (one segment is live per lane, the others read 0)
+                        const float xs = R.x[u][f][sg][e];
+                        b |= __builtin_bit_cast(unsigned, xs);
+                    }
+                    x[4 * f + e] = __builtin_bit_cast(float, b);
                 }
-                x[4 * f + e] = __builtin_bit_cast(float, b);
-            }
-        if (do_bias) {
+            if (do_bias) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) bsum[e] += y[e];
+                for (int e = 0; e < 8; ++e) bsum[e] += y[e];
+            }
+            split_store(y, P);
+            split_store(x, P + NPL * G::PLANE);
         }
-        split_store(y, P);
-        split_store(x, P + NPL * G::PLANE);
     };
-    // fragment = rows 8h .. 8h + 7 of columns cb .. cb + 31: lane 4q + p of each 16-lane group
-    // addresses row q (+4) at column 4p of its half
+    // fragment = rows 16 kk + 8h .. + 7 of columns cb .. cb + 31: lane 4q + p of each 16-lane group
+    // addresses row q (+4) at column 4p of its half (8 B = half of chunk cb / 8 + 2 g1 + p / 2)
     const int h = lane >> 5, q = (lane >> 2) & 3, p4 = lane & 3, g1 = (lane >> 4) & 1;
-    const int frag_off = (8 * h + q) * TPB + 2 * (16 * g1 + 4 * p4);
-    auto frag = [&](const unsigned char* plane, int cb) {
-        const unsigned char* a = plane + frag_off + 2 * cb;
+    auto frag = [&](const unsigned char* plane, int kk, int cb) {
+        const int row = 16 * kk + 8 * h + q, chunk = (cb >> 3) + 2 * g1 + (p4 >> 1);
+        const unsigned char* a = plane + tn_off(row, chunk) + 8 * (p4 & 1);
+        const unsigned char* a4 = plane + tn_off(row + 4, chunk) + 8 * (p4 & 1);  // (same swizzle)
         const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)a);
-        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a + 4 * TPB));
+        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)a4);
         return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
     };
     auto step = [&](int buf) {
         const unsigned char* const P = lds8 + buf * G::STAGE;
-        bf16x8 a[NPL][2], b[NPL][2];
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int kk = 0; kk < PR; ++kk) {
+            bf16x8 a[NPL][2], b[NPL][2];
 #pragma unroll
-            for (int p = 0; p < NPL; ++p) {
-                a[p][i] = frag(P + p * G::PLANE, 64 * wr + 32 * i);
-                b[p][i] = frag(P + (NPL + p) * G::PLANE, 64 * wc + 32 * i);
-            }
+            for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                f32x16 c = acc[i][j];
-                if constexpr (NPL == 3) {
-                    c = mfma(a[2][i], b[0][j], c);
-                    c = mfma(a[1][i], b[1][j], c);
-                    c = mfma(a[0][i], b[2][j], c);
+                for (int p = 0; p < NPL; ++p) {
+                    a[p][i] = frag(P + p * G::PLANE, kk, 64 * wr + 32 * i);
+                    b[p][i] = frag(P + (NPL + p) * G::PLANE, kk, 64 * wc + 32 * i);
                 }
-                c = mfma(a[1][i], b[0][j], c);
-                c = mfma(a[0][i], b[1][j], c);
-                acc[i][j] = mfma(a[0][i], b[0][j], c);
-            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    f32x16 c = acc[i][j];
+                    if constexpr (NPL == 3) {
+                        c = mfma(a[2][i], b[0][j], c);
+                        c = mfma(a[1][i], b[1][j], c);
+                        c = mfma(a[0][i], b[2][j], c);
+                    }
+                    c = mfma(a[1][i], b[0][j], c);
+                    c = mfma(a[0][i], b[1][j], c);
+                    acc[i][j] = mfma(a[0][i], b[0][j], c);
+                }
+        }
     };
     // two LDS stages, two register sets: the loads of step s + 2 fly during steps s and s + 1
-    const int nsteps = mhi > mlo ? (int)((mhi - mlo + TSK - 1) / TSK) : 0;
+    const int nsteps = mhi > mlo ? (int)((mhi - mlo + SK - 1) / SK) : 0;
     Regs R0, R1;
     if (nsteps > 0) {
         fetch(mlo, R0);
-        fetch(mlo + TSK, R1);
+        fetch(mlo + SK, R1);
         __builtin_amdgcn_sched_barrier(0);
         stage(0, R0);
     }
     __syncthreads();
     for (int st = 0; st < nsteps; st += 2) {
-        fetch(mlo + (long long)(st + 2) * TSK, R0);
+        fetch(mlo + (long long)(st + 2) * SK, R0);
         __builtin_amdgcn_sched_barrier(0);  // (keep the loads ahead of the MFMAs)
         step(0);
         __builtin_amdgcn_sched_barrier(0);
         if (st + 1 < nsteps) stage(1, R1);
         __syncthreads();
         if (st + 1 >= nsteps) break;
-        fetch(mlo + (long long)(st + 3) * TSK, R1);
+        fetch(mlo + (long long)(st + 3) * SK, R1);
         __builtin_amdgcn_sched_barrier(0);
         step(1);
         __builtin_amdgcn_sched_barrier(0);
@@ -728,7 +756,7 @@ hipError_t nt_attr() {
 template <int NPL, int NSEG>
 hipError_t tn_attr() {
     static const hipError_t e = hipFuncSetAttribute((const void*)mlp_tn_kernel<NPL, NSEG>,
-                                                    hipFuncAttributeMaxDynamicSharedMemorySize, TNGeo<NPL>::LDS_BYTES);
+                                                    hipFuncAttributeMaxDynamicSharedMemorySize, TNGeo<NPL, NSEG>::LDS_BYTES);
     return e;
 }
 
@@ -897,7 +925,8 @@ int anerf_mlp_wgrad(int64_t m, int32_t n, int32_t k, const float* dy, int64_t ld
     if (npl == P && n_x == S) {                                                                       \
         e = tn_attr<P, S>();                                                                          \
         if (e != hipSuccess) return anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));            \
-        hipLaunchKernelGGL((mlp_tn_kernel<P, S>), dim3((unsigned)g.total), dim3(NTHR), TNGeo<P>::LDS_BYTES, st, g); \
+        constexpr int lds_ = TNGeo<P, S>::LDS_BYTES;                                                  \
+        hipLaunchKernelGGL((mlp_tn_kernel<P, S>), dim3((unsigned)g.total), dim3(NTHR), lds_, st, g);  \
     }
     ANERF_TN_LAUNCH(3, 1)
     ANERF_TN_LAUNCH(3, 2)
