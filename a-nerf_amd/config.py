@@ -31,6 +31,12 @@ class RenderConfig:
     N_importance: int = 0
     single_net: bool = False
     lindisp: bool = False  # --lindisp: sample in inverse depth (render_kwargs['lindisp'], ray_utils.py:223-226)
+    # --freq_schedule: the cutoff embedders weight frequency k's sin/cos by 0.5 (1 - cos(pi clamp(alpha - k,
+    # 0, 1))), alpha = the checkpoint's sched_alpha buffer, moved by update_embed_fns from --init_freq
+    # over --freq_schedule_step k-steps (core/cutoff_embedder.py:89-99, 185-197; raycasters.py:731-748)
+    freq_schedule: bool = False
+    init_freq: float = 0.0
+    freq_schedule_step: int = 5
     chunk: int = 4096
     ext_scale: float = 0.001
     # MLP arithmetic: "fp32" (fp32 MFMA everywhere, the parity default), "bf16x6" (hidden layers as
@@ -65,7 +71,7 @@ class RenderConfig:
             raise ValueError(f"precision={self.precision!r}: 'fp32', 'bf16x6', 'fp16x3' or 'bf16x3'")
         if self.n_joints < 1 or self.n_joints > 128:
             raise NotImplementedError(f"n_joints={self.n_joints} outside [1, 128]")
-        for k in ("normalize_cutoff", "cut_to_dist", "cutoff_shift", "freq_schedule", "cutoff_bones"):
+        for k in ("normalize_cutoff", "cut_to_dist", "cutoff_shift", "cutoff_bones"):
             if self.extra.get(k):
                 raise NotImplementedError(f"--{k} is not implemented")
         for k, allowed in (("kp_dist_type", "reldist"), ("bone_type", "reldir"), ("view_type", "relray"),
@@ -99,7 +105,7 @@ class RenderConfig:
     def from_args(cls, args, n_joints):
         """Build from a run_nerf.config_parser() namespace (or anything with those attributes)."""
         g = lambda k, d=None: getattr(args, k, d)  # noqa: E731
-        extra = {k: g(k) for k in ("normalize_cutoff", "cut_to_dist", "cutoff_shift", "freq_schedule",
+        extra = {k: g(k) for k in ("normalize_cutoff", "cut_to_dist", "cutoff_shift",
                                    "cutoff_bones", "kp_dist_type", "bone_type", "view_type", "pts_tr_type",
                                    "cutoff_mm") if g(k) is not None}
         cfg = cls(n_joints=n_joints, netdepth=g("netdepth", 8), netwidth=g("netwidth", 256),
@@ -111,9 +117,44 @@ class RenderConfig:
                   density_type=g("density_type", "relu"), softplus_shift=g("softplus_shift", 1.0),
                   density_scale=g("density_scale", 1.0), N_samples=g("N_samples", 64),
                   N_importance=g("N_importance", 0), single_net=bool(g("single_net", False)),
-                  lindisp=bool(g("lindisp", False)),
+                  lindisp=bool(g("lindisp", False)), freq_schedule=bool(g("freq_schedule", False)),
+                  init_freq=float(g("init_freq", 0.0) or 0.0), freq_schedule_step=int(g("freq_schedule_step", 5) or 5),
                   chunk=g("chunk", 4096), ext_scale=g("ext_scale", 0.001), extra=extra)
         return cfg.validate()
+
+
+def schedule_weights(alpha, n_freqs):
+    """CutoffEmbedder.get_schedule_w (core/cutoff_embedder.py:192-197) in float32: the weight of
+    frequency k (its sin and its cos), 0.5 (1 - cos(pi clamp(alpha - k, 0, 1)))."""
+    import numpy as np
+    import torch
+    freq_k = torch.log2(2.0 ** torch.linspace(0.0, n_freqs - 1, steps=n_freqs))
+    diff = torch.clamp(torch.as_tensor(np.float32(alpha)) - freq_k, 0, 1)
+    return (0.5 * (1.0 - torch.cos(np.pi * diff))).numpy().astype(np.float32)
+
+
+def feature_scales(cfg, alpha_pts, alpha_views):
+    """Per-column factor of the MLP input [x (input_ch) | bones | views] under --freq_schedule: the
+    schedule weight of the column's frequency for the windowed sin/cos features of the cutoff
+    embedders (pts: column f * NJ + j, views: input_ch + input_ch_bones + f * 3 NJ + 3 j + c, with
+    f = 1 + 2k / 2 + 2k the sin / cos of frequency k), 1 elsewhere; None without a schedule."""
+    import numpy as np
+    if not cfg.freq_schedule:
+        return None
+    nj = cfg.n_joints
+    dnet = cfg.input_ch + cfg.input_ch_bones
+    s = np.ones(dnet + cfg.input_ch_views, np.float32)
+    if cfg.use_cutoff:  # (the pts embedder is a CutoffEmbedder only then)
+        w = schedule_weights(alpha_pts, cfg.multires)
+        for k in range(cfg.multires):
+            for f in (1 + 2 * k, 2 + 2 * k):
+                s[f * nj:(f + 1) * nj] = w[k]
+    if cfg.use_viewdirs and cfg.cutoff_viewdir and cfg.multires_views > 0:
+        w = schedule_weights(alpha_views, cfg.multires_views)
+        for k in range(cfg.multires_views):
+            for f in (1 + 2 * k, 2 + 2 * k):
+                s[dnet + f * 3 * nj:dnet + (f + 1) * 3 * nj] = w[k]
+    return s
 
 
 def flops_per_sample(cfg):

@@ -13,6 +13,7 @@ import numpy as np
 import torch
 
 from . import _lib
+from .config import feature_scales
 
 
 def _np(x):
@@ -54,9 +55,18 @@ class DeviceModel:
         d.single_net = int(cfg.single_net)
         d.has_fine = int(fine_sd is not None and cfg.N_importance > 0)
         self.has_fine = bool(d.has_fine)
+        e, ev = ckpt["embed_state_dict"], ckpt["embeddirs_state_dict"]
+        # --freq_schedule: the embedders' per-frequency weights are folded into the weight columns
+        # that consume those features (layer 0, the skip layer's x part, the view layer's direction
+        # part) -- the same products up to one rounding of w * s (config.feature_scales)
+        self._fs = None
+        if cfg.freq_schedule:
+            if "sched_alpha" not in e or "sched_alpha" not in ev:
+                raise ValueError("freq_schedule: the checkpoint's embed state has no sched_alpha buffer")
+            self._fs = feature_scales(cfg, float(_np(e["sched_alpha"]).reshape(-1)[0]),
+                                      float(_np(ev["sched_alpha"]).reshape(-1)[0]))
         coarse = self._net(coarse_sd)
         fine = self._net(fine_sd) if d.has_fine else None
-        e, ev = ckpt["embed_state_dict"], ckpt["embeddirs_state_dict"]
         emb = _lib.EmbedParams()
         emb.cutoff_dist, emb.tau = self._p(e["cutoff_dist"]), float(_np(e["tau"]).reshape(-1)[0])
         emb.cutoff_dist_v, emb.tau_v = self._p(ev["cutoff_dist"]), float(_np(ev["tau"]).reshape(-1)[0])
@@ -75,13 +85,23 @@ class DeviceModel:
 
     def _net(self, sd):
         cfg = self.cfg
+        fs = self._fs
+        dnet = cfg.input_ch + cfg.input_ch_bones
         w = _lib.NetWeights()
         for i in range(cfg.netdepth):
-            w.pts_w[i] = self._p(sd[f"pts_linears.{i}.weight"])
+            wi = sd[f"pts_linears.{i}.weight"]
+            if fs is not None and (i == 0 or i == cfg.skips[0] + 1):  # (inputs [x] / [x | h])
+                wi = _np(wi).copy()
+                wi[:, :dnet] *= fs[None, :dnet]
+            w.pts_w[i] = self._p(wi)
             w.pts_b[i] = self._p(sd[f"pts_linears.{i}.bias"])
         w.alpha_w, w.alpha_b = self._p(sd["alpha_linear.weight"]), self._p(sd["alpha_linear.bias"])
         w.feature_w, w.feature_b = self._p(sd["feature_linear.weight"]), self._p(sd["feature_linear.bias"])
-        w.views_w, w.views_b = self._p(sd["views_linears.0.weight"]), self._p(sd["views_linears.0.bias"])
+        wv = sd["views_linears.0.weight"]
+        if fs is not None:  # (inputs [feature | views | framecode])
+            wv = _np(wv).copy()
+            wv[:, cfg.netwidth:cfg.netwidth + cfg.input_ch_views] *= fs[None, dnet:]
+        w.views_w, w.views_b = self._p(wv), self._p(sd["views_linears.0.bias"])
         w.rgb_w, w.rgb_b = self._p(sd["rgb_linear.weight"]), self._p(sd["rgb_linear.bias"])
         w.codes = self._p(sd["framecodes.codes.weight"]) if cfg.opt_framecode else None
         return w

@@ -20,7 +20,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _lib
-from .config import RenderConfig
+from .config import RenderConfig, feature_scales
 from .model import DeviceModel
 
 
@@ -317,17 +317,31 @@ class _Embed(nn.Module):
 
     init_tau = 20.0
 
-    def __init__(self, n_joints, cutoff_dist):
+    def __init__(self, n_joints, cutoff_dist, init_alpha=None):
+        """init_alpha: --freq_schedule's --init_freq (a `sched_alpha` buffer, :97-99), None without."""
         super().__init__()
         self.cutoff_dist = nn.Parameter(torch.full((n_joints,), float(cutoff_dist)), requires_grad=False)
         self.register_buffer("tau", torch.tensor(self.init_tau))
+        self.freq_schedule = init_alpha is not None
+        if self.freq_schedule:
+            self.init_alpha = float(init_alpha)
+            self.register_buffer("sched_alpha", torch.tensor(self.init_alpha))
 
     def get_tau(self):
         return self.tau.item()
 
     def update_threshold(self, global_step, tau_step, tau_rate, alpha_step=None, alpha_target=None):
         self.update_tau(global_step, tau_step, tau_rate)
-        # update_alpha is a no-op without freq_schedule (RenderConfig rejects freq_schedule)
+        self.update_alpha(global_step, alpha_step, alpha_target)
+
+    def update_alpha(self, global_step, step, target=None):
+        """sched_alpha = init + (target - init) * global_step / (step * 1000) (cutoff_embedder.py:185-190;
+        the reference's target is multires - 1 for every embedder, raycasters.py:737), in place."""
+        if not self.freq_schedule:
+            return
+        with torch.no_grad():
+            self.sched_alpha.copy_(torch.tensor(self.init_alpha + (target - self.init_alpha) * global_step
+                                                / float(step * 1000)))
 
     def update_tau(self, global_step, step, rate):
         """tau = (20 * rate ** (global_step / (step * 1000))).clamp(max=2000), the reference's own
@@ -366,8 +380,9 @@ class TrainRayCaster(nn.Module):
             self.network_fine = None
         # fresh models: cutoff_mm (default 500, run_nerf.py:416) x ext_scale (raycasters.py:33), tau 20
         cut = float(cfg.extra.get("cutoff_mm", 500.0)) * cfg.ext_scale
-        self.embed_fn = _Embed(cfg.n_joints, cut)
-        self.embeddirs_fn = _Embed(cfg.n_joints, cut)
+        alpha0 = cfg.init_freq if cfg.freq_schedule else None
+        self.embed_fn = _Embed(cfg.n_joints, cut, alpha0)
+        self.embeddirs_fn = _Embed(cfg.n_joints, cut, alpha0)
         for net in (self.network_fn, self.network_fine):
             if net is not None:
                 net.mlp = mlp
@@ -389,9 +404,9 @@ class TrainRayCaster(nn.Module):
 
     def update_embed_fns(self, global_step, args):
         """core/raycasters.py:731-748: the tau schedule of both embedders (args.cutoff_step,
-        args.cutoff_rate); the kernels pick the new tau up at the next launch."""
-        if getattr(args, "freq_schedule", False):
-            raise NotImplementedError("--freq_schedule is not implemented")
+        args.cutoff_rate) and, with --freq_schedule, their sched_alpha (args.freq_schedule_step,
+        target multires - 1); the kernels pick the new tau up at the next launch, the new schedule
+        weights at the next feature product."""
         for e in (self.embed_fn, self.embeddirs_fn):
             e.update_threshold(global_step, args.cutoff_step, args.cutoff_rate,
                                getattr(args, "freq_schedule_step", 5), getattr(args, "multires", 7) - 1)
@@ -422,9 +437,20 @@ class TrainRayCaster(nn.Module):
 
     def _version(self):
         """Identity + version of every network tensor (a tensor replaced by assignment changes the
-        identity, an in-place update the version)."""
+        identity, an in-place update the version) and of the schedule buffers (folded into the eval
+        caster's packed weights)."""
         nets = [self.network_fn] + ([self.network_fine] if self.network_fine is not None else [])
-        return tuple((p.data_ptr(), p._version) for n in nets for p in n.parameters())
+        sched = [e.sched_alpha for e in (self.embed_fn, self.embeddirs_fn) if e.freq_schedule]
+        return tuple((p.data_ptr(), p._version) for n in nets for p in n.parameters()) + tuple(
+            (t.data_ptr(), t._version) for t in sched)
+
+    def _feature_scale(self):
+        """--freq_schedule: the per-column schedule weights of the MLP input (config.feature_scales at
+        the current sched_alpha), on the device; None without a schedule."""
+        if not self.cfg.freq_schedule:
+            return None
+        s = feature_scales(self.cfg, float(self.embed_fn.sched_alpha), float(self.embeddirs_fn.sched_alpha))
+        return torch.from_numpy(s).to(self._dev)
 
     def _embed_version(self):
         return tuple((t.data_ptr(), t._version) for e in (self.embed_fn, self.embeddirs_fn)
@@ -539,9 +565,13 @@ class TrainRayCaster(nn.Module):
             g = torch.randn(n, ns, 3, device=dev) if g is None else g.to(dev, torch.float32)
             return (g * ray_noise_std).contiguous()
 
+        fscale = self._feature_scale()
+
         def raw_of(net, zz, pn=None):
             ns = zz.shape[1]
             feat = _Encode.apply(sk, model, rb, zz, None, pn)
+            if fscale is not None:  # (embedded * get_schedule_w(), cutoff_embedder.py:150; autograd scales dL/dfeat)
+                feat = feat * fscale
             return net(feat, None if cam_t is None else cam_t.repeat_interleave(ns)).reshape(n, ns, 4)
 
         def composite(raw, zz, noise):

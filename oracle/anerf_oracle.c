@@ -53,6 +53,11 @@ typedef struct {
     int has_fine;
     int single_net; /* network_fine IS network_fn; fine pass on the I new samples only (raycasters.py:462-468) */
     int lindisp;    /* sample_from_lineseg in inverse depth (ray_utils.py:223-226) */
+    /* --freq_schedule: weight of frequency k (its sin and cos) in the pts / view cutoff embedders,
+     * CutoffEmbedder.get_schedule_w (cutoff_embedder.py:192-197), applied before the cutoff window
+     * as `embedded * get_schedule_w()` then `* w` (:150-154); NULL = no schedule */
+    const float* sched_w;
+    const float* sched_wv;
     oracle_net coarse, fine;
 } oracle_model;
 
@@ -291,8 +296,13 @@ static void encode_point(const oracle_model* m, const float* skts, const float p
         fv[j] = (m->use_cutoff && m->cutoff_inputs) ? dist * w : dist;
         for (int f = 0; f < nfk; ++f) {
             float a = dist * (float)(1 << f);
-            fv[(1 + 2 * f) * nj + j] = sinf(a) * w;
-            fv[(2 + 2 * f) * nj + j] = cosf(a) * w;
+            if (m->sched_w && m->use_cutoff) {
+                fv[(1 + 2 * f) * nj + j] = (sinf(a) * m->sched_w[f]) * w;
+                fv[(2 + 2 * f) * nj + j] = (cosf(a) * m->sched_w[f]) * w;
+            } else {
+                fv[(1 + 2 * f) * nj + j] = sinf(a) * w;
+                fv[(2 + 2 * f) * nj + j] = cosf(a) * w;
+            }
         }
         /* view block: rays rotated into the joint frame, normalised (encoders.py:25-37, 181-193) */
         float e[3];
@@ -306,8 +316,13 @@ static void encode_point(const oracle_model* m, const float* skts, const float p
             fd[3 * j + c] = (m->cutoff_viewdir && m->cutoff_inputs) ? x * wv : x;
             for (int f = 0; f < nfv; ++f) {
                 float a = x * (float)(1 << f);
-                fd[(1 + 2 * f) * 3 * nj + 3 * j + c] = sinf(a) * wv;
-                fd[(2 + 2 * f) * 3 * nj + 3 * j + c] = cosf(a) * wv;
+                if (m->sched_wv && m->cutoff_viewdir) {
+                    fd[(1 + 2 * f) * 3 * nj + 3 * j + c] = (sinf(a) * m->sched_wv[f]) * wv;
+                    fd[(2 + 2 * f) * 3 * nj + 3 * j + c] = (cosf(a) * m->sched_wv[f]) * wv;
+                } else {
+                    fd[(1 + 2 * f) * 3 * nj + 3 * j + c] = sinf(a) * wv;
+                    fd[(2 + 2 * f) * 3 * nj + 3 * j + c] = cosf(a) * wv;
+                }
             }
         }
     }

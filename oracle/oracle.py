@@ -29,7 +29,7 @@ class _Model(ctypes.Structure):
                 ("density_softplus", ctypes.c_int), ("softplus_shift", ctypes.c_float),
                 ("density_scale", ctypes.c_float), ("tau", ctypes.c_float), ("tau_v", ctypes.c_float),
                 ("cutoff", _f), ("cutoff_v", _f), ("has_fine", ctypes.c_int), ("single_net", ctypes.c_int),
-                ("lindisp", ctypes.c_int),
+                ("lindisp", ctypes.c_int), ("sched_w", _f), ("sched_wv", _f),
                 ("coarse", _Net), ("fine", _Net)]
 
 
@@ -63,6 +63,14 @@ def _f32(a):
     return np.ascontiguousarray(np.asarray(a, dtype=np.float32))
 
 
+def schedule_w(alpha, n_freqs):
+    """CutoffEmbedder.get_schedule_w (core/cutoff_embedder.py:192-197) in float32: frequency k's
+    weight 0.5 (1 - cos(pi clamp(alpha - k, 0, 1))) (freq_k = log2(freq_bands) = k exactly)."""
+    diff = np.clip(np.float32(np.asarray(alpha, np.float32).reshape(-1)[0]) - np.arange(n_freqs, dtype=np.float32),
+                   np.float32(0), np.float32(1))
+    return (np.float32(0.5) * (np.float32(1.0) - np.cos(np.float32(np.pi) * diff))).astype(np.float32)
+
+
 class OracleModel:
     """Holds contiguous (transposed where the C side wants [in][out]) weight copies."""
 
@@ -86,6 +94,9 @@ class OracleModel:
             coarse, fine = (fine if fine is not None else coarse), None
         m.single_net = int(cfg.single_net)
         m.lindisp = int(cfg.lindisp)
+        if getattr(cfg, "freq_schedule", False):
+            m.sched_w = self._k(schedule_w(e["sched_alpha"], cfg.multires))
+            m.sched_wv = self._k(schedule_w(ev["sched_alpha"], cfg.multires_views))
         self._net(m.coarse, coarse)
         m.has_fine = int(fine is not None)
         if fine is not None:

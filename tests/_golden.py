@@ -19,8 +19,8 @@ NAMES = ["c1_64_s32_d4w128", "c2_256_s64_d8w256", "c3_512_s64i128_d8w256", "c4_5
          "v1_mr10_w64_d4", "v2_softplus_nocutview", "v3_nocutinputs", "v4_nocutoff",
          # configs/surreal/surreal_single.txt (single_net, multires_views 0, 96 + 48); tau at its ceiling
          "s1_single_s96i48_mrv0", "t2000_512_s64i128",
-         # --lindisp (inverse-depth samples)
-         "l1_lindisp_s32i16_d4w128"]
+         # --lindisp (inverse-depth samples); --freq_schedule at sched_alpha 2.3 (D = 8: skip layer)
+         "l1_lindisp_s32i16_d4w128", "fs1_freqsched_s32i16_d8w128"]
 
 
 class Golden:
@@ -45,10 +45,13 @@ class Golden:
                                        cutoff_viewdir="--cutoff_viewdir" not in drop,
                                        multires_views=m.get("mrv", 4), single_net=m.get("single", False),
                                        lindisp="--lindisp" in flags or bool(m.get("lindisp", False)),
+                                       freq_schedule="--freq_schedule" in flags,
+                                       init_freq=float(flags[flags.index("--init_freq") + 1])
+                                       if "--init_freq" in flags else 0.0,
                                        **kw).validate()
         self.ckpt = syn.make_checkpoint(m["seed"], n_joints=m["NJ"], D=m["D"], W=m["W"], fine=m["I"] > 0,
                                         tau=m["tau"], use_framecode=fc, n_framecodes=5, multires=m.get("mr", 7),
-                                        multires_views=m.get("mrv", 4))
+                                        multires_views=m.get("mrv", 4), sched_alpha=m.get("sched"))
         assert syn.checkpoint_sha256(self.ckpt) == m["sha256"], "synthetic weights drifted from the fixture"
 
     def __getitem__(self, k):

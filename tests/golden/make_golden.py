@@ -116,6 +116,10 @@ CONFIGS = {
     # --lindisp: samples linear in inverse depth (sample_from_lineseg, ray_utils.py:223-226)
     "l1_lindisp_s32i16_d4w128": dict(H=128, NJ=24, S=32, I=16, D=4, W=128, tau=20.0, kind="rays", n_rays=128,
                                      seed=25, flags=["--lindisp"]),
+    # --freq_schedule at sched_alpha 2.3 (frequencies 0-1 full, 2 at 0.206, 3+ off) in both cutoff
+    # embedders (core/cutoff_embedder.py:150, 192-197); D = 8 so the skip layer's x part is covered
+    "fs1_freqsched_s32i16_d8w128": dict(H=128, NJ=24, S=32, I=16, D=8, W=128, tau=20.0, kind="rays", n_rays=128,
+                                        seed=26, flags=["--freq_schedule", "--init_freq", "2.3"], sched=2.3),
 }
 
 
@@ -148,7 +152,7 @@ def build_reference(mods, cfg, tmp):
     _, render_kwargs, _, _, _, _ = raycasters.create_raycaster(args, data_attrs)
     ck = anerf_syn.make_checkpoint(cfg["seed"], n_joints=NJ, D=cfg["D"], W=cfg["W"], fine=cfg["I"] > 0,
                                    tau=cfg["tau"], use_framecode=use_fc, n_framecodes=5, multires=cfg.get("mr", 7),
-                                   multires_views=cfg.get("mrv", 4))
+                                   multires_views=cfg.get("mrv", 4), sched_alpha=cfg.get("sched"))
     ck_t = {k: {n: torch.from_numpy(np.array(v)) for n, v in d.items()} for k, d in ck.items()}
     rc = render_kwargs["ray_caster"]
     rc.load_state_dict(ck_t, strict=True)
@@ -269,7 +273,8 @@ def make(name, cfg, mods, tmp):
     meta = dict(seed=cfg["seed"], sha256=sha, NJ=cfg["NJ"], S=cfg["S"], I=cfg["I"], D=cfg["D"], W=cfg["W"],
                 tau=cfg["tau"], H=sc["H"], focal=sc["focal"], ext_scale=0.001, chunk=4096,
                 framecode=int(cfg["kind"] == "framecode"), mr=cfg.get("mr", 7), flags=cfg.get("flags", []),
-                drop=cfg.get("drop", []), mrv=cfg.get("mrv", 4), single=bool(cfg.get("single", False)))
+                drop=cfg.get("drop", []), mrv=cfg.get("mrv", 4), single=bool(cfg.get("single", False)),
+                sched=cfg.get("sched"))
     data = {"c2ws": sc["c2ws"], "kps": sc["kps"], "skts": sc["skts"], "bones": sc["bones"]}
     (o, d), vidx, cyls, (tl, br) = rays_for(mods, sc)
     sc["cyls"] = cyls

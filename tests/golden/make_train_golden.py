@@ -42,6 +42,11 @@ CONFIGS = {
                                 n_poses=2, lindisp=True, ray_noise_std=0.01),
     "t7_single_raynoise": dict(H=128, NJ=24, S=32, I=16, D=4, W=128, tau=20.0, kind="rays", seed=37, n_rays=64,
                                n_poses=2, single=True, ray_noise_std=0.02),
+    # --freq_schedule: checkpoint at sched_alpha 1.0 (--init_freq 1), update_embed_fns at step 1,700
+    # (freq_schedule_step 5: alpha = 1 + 5 * 1700 / 5000 = 2.7; tau 20 -> 20.3) before the step; D = 8
+    "t8_freqsched": dict(H=128, NJ=24, S=32, I=16, D=8, W=128, tau=20.0, kind="rays", seed=38, n_rays=64,
+                         n_poses=2, flags=["--freq_schedule", "--init_freq", "1.0"], sched=1.0,
+                         global_step=1700, cutoff_step=250, cutoff_rate=10.0),
 }
 FULL_LIMIT = 20000   # parameters with more entries are sampled
 SAMPLE = 4096
@@ -139,7 +144,9 @@ def make(name, cfg, mods, tmp):
                 raw_noise_std=1.0, n_poses=P, mrv=cfg.get("mrv", 4), single=bool(cfg.get("single", False)),
                 global_step=cfg.get("global_step"), cutoff_step=cfg.get("cutoff_step"),
                 cutoff_rate=cfg.get("cutoff_rate"), tau_step=taus, lindisp=bool(cfg.get("lindisp", False)),
-                ray_noise_std=rns)
+                ray_noise_std=rns, sched=cfg.get("sched"),
+                sched_step=(float(rc.embed_fn.sched_alpha), float(rc.embeddirs_fn.sched_alpha))
+                if cfg.get("sched") is not None else None)
     data = dict(rays=rb, pose=pose, skts=sc["skts"][pose], kps=sc["kps"][pose], bones=sc["bones"][pose], cyls=cyl,
                 target=target, bg=bg, loss=np.float32(loss.item()), grad_skts=skts_t.grad.numpy(),
                 **{"rand_" + k: v for k, v in draws.items()},

@@ -24,7 +24,7 @@ anerf = importlib.import_module("a-nerf_amd")
 train = importlib.import_module("a-nerf_amd.train")
 
 TRAIN = ["t1_s32i16_d4w128", "t2_s64i16_d8w256", "t3_softplus_fc", "t4_tau200", "t5_single_mrv0",
-         "t6_lindisp_raynoise", "t7_single_raynoise"]
+         "t6_lindisp_raynoise", "t7_single_raynoise", "t8_freqsched"]
 TOL = 1e-4
 TOL_ALPHA = 2e-3
 GRAD_REL = 2e-3
@@ -52,6 +52,8 @@ def _run(name, mlp="mixed"):
         tr.module.update_embed_fns(m["global_step"], argparse.Namespace(
             cutoff_step=m["cutoff_step"], cutoff_rate=m["cutoff_rate"], freq_schedule_step=5, multires=7))
         assert (tr.module.embed_fn.get_tau(), tr.module.embeddirs_fn.get_tau()) == tuple(m["tau_step"])
+        if m.get("sched_step") is not None:  # --freq_schedule: sched_alpha moved as update_alpha moves it
+            assert (float(tr.embed_fn.sched_alpha), float(tr.embeddirs_fn.sched_alpha)) == tuple(m["sched_step"])
     c = lambda k: torch.from_numpy(g[k]).to(dev)  # noqa: E731
     sk = c("skts").clone().requires_grad_(True)
     rand = {k: c("rand_" + k) for k in ("t_rand", "noise0", "u", "noise1", "pts_noise0", "pts_noise1")
