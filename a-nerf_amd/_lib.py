@@ -28,6 +28,9 @@ PRECISIONS = {"fp32": ANERF_PREC_FP32, "bf16x3": ANERF_PREC_BF16X3, "bf16x6": AN
               "fp16x3": ANERF_PREC_FP16X3}
 
 
+ANERF_ENC_CUT_TO_DIST, ANERF_ENC_CUTOFF_SHIFT = 1, 2  # anerf_model_desc.encoder_flags
+
+
 class ModelDesc(ctypes.Structure):
     _fields_ = [("n_joints", ctypes.c_int32), ("net_depth", ctypes.c_int32), ("net_width", ctypes.c_int32),
                 ("skip", ctypes.c_int32), ("multires", ctypes.c_int32), ("multires_views", ctypes.c_int32),
@@ -35,7 +38,7 @@ class ModelDesc(ctypes.Structure):
                 ("cutoff_viewdir", ctypes.c_int32), ("framecode_ch", ctypes.c_int32),
                 ("n_framecodes", ctypes.c_int32), ("density_softplus", ctypes.c_int32),
                 ("softplus_shift", ctypes.c_float), ("density_scale", ctypes.c_float),
-                ("has_fine", ctypes.c_int32), ("single_net", ctypes.c_int32)]
+                ("has_fine", ctypes.c_int32), ("single_net", ctypes.c_int32), ("encoder_flags", ctypes.c_int32)]
 
 
 class NetWeights(ctypes.Structure):

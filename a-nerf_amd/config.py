@@ -37,6 +37,13 @@ class RenderConfig:
     freq_schedule: bool = False
     init_freq: float = 0.0
     freq_schedule_step: int = 5
+    # --cut_to_dist / --cutoff_shift: the kp cutoff embedder encodes c_j - dist (raw input and
+    # frequencies) / feeds (input * 2 / c_j - 1) to the frequencies (core/cutoff_embedder.py:125-134)
+    cut_to_dist: bool = False
+    cutoff_shift: bool = False
+    # --normalize_cutoff reaches CutoffEmbedder only as an unused keyword ("normalize_cutoff", not
+    # "normalize": core/raycasters.py:32 vs cutoff_embedder.py:64): a no-op in the reference, and here
+    normalize_cutoff: bool = False
     chunk: int = 4096
     ext_scale: float = 0.001
     # MLP arithmetic: "fp32" (fp32 MFMA everywhere, the parity default), "bf16x6" (hidden layers as
@@ -71,7 +78,7 @@ class RenderConfig:
             raise ValueError(f"precision={self.precision!r}: 'fp32', 'bf16x6', 'fp16x3' or 'bf16x3'")
         if self.n_joints < 1 or self.n_joints > 128:
             raise NotImplementedError(f"n_joints={self.n_joints} outside [1, 128]")
-        for k in ("normalize_cutoff", "cut_to_dist", "cutoff_shift", "cutoff_bones"):
+        for k in ("cutoff_bones",):
             if self.extra.get(k):
                 raise NotImplementedError(f"--{k} is not implemented")
         for k, allowed in (("kp_dist_type", "reldist"), ("bone_type", "reldir"), ("view_type", "relray"),
@@ -105,8 +112,7 @@ class RenderConfig:
     def from_args(cls, args, n_joints):
         """Build from a run_nerf.config_parser() namespace (or anything with those attributes)."""
         g = lambda k, d=None: getattr(args, k, d)  # noqa: E731
-        extra = {k: g(k) for k in ("normalize_cutoff", "cut_to_dist", "cutoff_shift",
-                                   "cutoff_bones", "kp_dist_type", "bone_type", "view_type", "pts_tr_type",
+        extra = {k: g(k) for k in ("cutoff_bones", "kp_dist_type", "bone_type", "view_type", "pts_tr_type",
                                    "cutoff_mm") if g(k) is not None}
         cfg = cls(n_joints=n_joints, netdepth=g("netdepth", 8), netwidth=g("netwidth", 256),
                   multires=g("multires", 7), multires_views=g("multires_views", 4),
@@ -119,6 +125,8 @@ class RenderConfig:
                   N_importance=g("N_importance", 0), single_net=bool(g("single_net", False)),
                   lindisp=bool(g("lindisp", False)), freq_schedule=bool(g("freq_schedule", False)),
                   init_freq=float(g("init_freq", 0.0) or 0.0), freq_schedule_step=int(g("freq_schedule_step", 5) or 5),
+                  cut_to_dist=bool(g("cut_to_dist", False)), cutoff_shift=bool(g("cutoff_shift", False)),
+                  normalize_cutoff=bool(g("normalize_cutoff", False)),
                   chunk=g("chunk", 4096), ext_scale=g("ext_scale", 0.001), extra=extra)
         return cfg.validate()
 

@@ -376,10 +376,12 @@ __device__ void encode_row(const ModelDev& M, const float* __restrict__ skts, fl
         const float dist = norm3(qx, qy, qz);
         const float dn = fmaxf(dist, 1e-12f);
         const float w = M.use_cutoff ? cutoff_w(M.tau, dist, M.cutoff[j]) : 1.0f;
-        f[j] = (M.use_cutoff && M.cutoff_inputs) ? dist * w : dist;
+        float u, uf;
+        kp_inputs(M.cut_to, M.shift_in, dist, M.cutoff[j], u, uf);
+        f[j] = (M.use_cutoff && M.cutoff_inputs) ? u * w : u;
         for (int fi = 0; fi < M.mr; ++fi) {
             float s, c;
-            sincosf(dist * (float)(1 << fi), &s, &c);
+            sincosf(uf * (float)(1 << fi), &s, &c);
             f[(1 + 2 * fi) * nj + j] = s * w;
             f[(2 + 2 * fi) * nj + j] = c * w;
         }

@@ -943,23 +943,24 @@ __device__ __forceinline__ void v_part(f32x16 (&acc)[RB], const ModelDev& M, con
         for (int rb = 0; rb < RB; ++rb) ring[g][rb] = bload2(rs, voff, ((j * GB + g) * RB + rb) * 512);
     float f[KB];
     {
-        float dist, w;
+        float dist, w, u, uf;
         v_geom(M, sk, cut, j, px, py, pz, dist, w);
         w *= xs;  // (a power of two: the products equal the unscaled ones times xs exactly)
+        kp_inputs(M.cut_to, M.shift_in, dist, cut[j], u, uf);  // (u = uf = dist without the flags)
 #pragma unroll
         for (int t = 0; t < MR; ++t) {
             float sn, cs;
-            sincos_rr(dist * (float)(1 << t), sn, cs);
+            sincos_rr(uf * (float)(1 << t), sn, cs);
             f[t] = (hh ? cs : sn) * w;
         }
-        f[MR] = hh ? 0.0f : (dist_in ? dist * w : dist * xs);
+        f[MR] = hh ? 0.0f : (dist_in ? u * w : u * xs);
 #pragma unroll
         for (int t = MR + 1; t < KB; ++t) f[t] = 0.0f;
     }
     STAMP(st, 15);
     while (j >= 0) {
         float fn[KB];
-        float dn = 0.0f, wn = 0.0f;
+        float dn = 0.0f, dfn = 0.0f, wn = 0.0f;  // next joint: raw input, frequency input, window
         const int jg = jn >= 0 ? jn : j;  // geometry of the next joint (harmless redo at the end)
 #pragma unroll
         for (int g = 0; g < GB; ++g) {
@@ -982,14 +983,16 @@ __device__ __forceinline__ void v_part(f32x16 (&acc)[RB], const ModelDev& M, con
             }
             // next joint's features under these MFMAs
             if (g == 0) {
-                v_geom(M, sk, cut, jg, px, py, pz, dn, wn);
+                float dd;
+                v_geom(M, sk, cut, jg, px, py, pz, dd, wn);
                 wn *= xs;
-                pin(dn), pin(wn);
+                kp_inputs(M.cut_to, M.shift_in, dd, cut[jg], dn, dfn);
+                pin(dn), pin(dfn), pin(wn);
             } else {
 #pragma unroll
                 for (int t = (g - 1) * PER; t < g * PER && t < MR; ++t) {
                     float sn, cs;
-                    sincos_rr(dn * (float)(1 << t), sn, cs);
+                    sincos_rr(dfn * (float)(1 << t), sn, cs);
                     fn[t] = (hh ? cs : sn) * wn;
                     pin(fn[t]);
                 }

@@ -127,6 +127,9 @@ int anerf_model_create(const anerf_model_desc* desc, const anerf_net_weights* co
         md.ux6 = !(e && e[0] == '0');
     }
     md.single_net = desc->single_net ? 1 : 0;
+    // (both transforms live in the CutoffEmbedder: without use_cutoff the kp embedder is plain)
+    md.cut_to = desc->use_cutoff && (desc->encoder_flags & ANERF_ENC_CUT_TO_DIST) ? 1 : 0;
+    md.shift_in = desc->use_cutoff && (desc->encoder_flags & ANERF_ENC_CUTOFF_SHIFT) ? 1 : 0;
     md.h3_top = 127 + h3_target();
     md.shift = desc->softplus_shift;
     md.B = desc->density_scale;

@@ -42,10 +42,12 @@ __device__ __forceinline__ void encode_joint(const ModelDev& M, const float* __r
     const float dist = norm3(qx, qy, qz);
     const float dn = fmaxf(dist, 1e-12f);
     const float w = M.use_cutoff ? cutoff_w(M.tau, dist, M.cutoff[j]) : 1.0f;
-    f[j] = (M.use_cutoff && M.cutoff_inputs) ? dist * w : dist;
+    float u, uf;
+    kp_inputs(M.cut_to, M.shift_in, dist, M.cutoff[j], u, uf);
+    f[j] = (M.use_cutoff && M.cutoff_inputs) ? u * w : u;
     for (int fi = 0; fi < M.mr; ++fi) {
         float s, c;
-        sincos_rr(dist * (float)(1 << fi), s, c);
+        sincos_rr(uf * (float)(1 << fi), s, c);
         f[(1 + 2 * fi) * nj + j] = s * w;
         f[(2 + 2 * fi) * nj + j] = c * w;
     }
@@ -113,21 +115,26 @@ __device__ __forceinline__ void encode_row_grad_joint(const ModelDev& M, const f
     // ---- distance block
     const bool cut = M.use_cutoff != 0, cut_in = M.use_cutoff && M.cutoff_inputs;
     const float w = cut ? cutoff_w(M.tau, dist, M.cutoff[j]) : 1.0f;
+    // the encoder's inputs u (raw) and uf (frequencies) and their slopes in dist (kp_inputs)
+    float u, uf;
+    kp_inputs(M.cut_to, M.shift_in, dist, M.cutoff[j], u, uf);
+    const float du = M.cut_to ? -1.0f : 1.0f;
+    const float duf = M.shift_in ? du * (2.0f / M.cutoff[j]) : du;
     float g_dist = 0.0f, g_w = 0.0f;
     const float g0 = g[j];
     if (cut_in) {
-        g_dist += g0 * w;
-        g_w += g0 * dist;
+        g_dist += g0 * w * du;
+        g_w += g0 * u;
     } else {
-        g_dist += g0;
+        g_dist += g0 * du;
     }
     for (int fi = 0; fi < M.mr; ++fi) {
         const float fr = (float)(1 << fi);
         float s, c;
-        sincos_rr(dist * fr, s, c);
+        sincos_rr(uf * fr, s, c);
         const float gs = g[(1 + 2 * fi) * nj + j], gc = g[(2 + 2 * fi) * nj + j];
         g_w += gs * s + gc * c;
-        g_dist += (gs * c - gc * s) * w * fr;
+        g_dist += (gs * c - gc * s) * w * fr * duf;
     }
     if (cut) g_dist += g_w * (-M.tau * w * (1.0f - w));
     // ---- bone direction u = q / max(|q|, eps)

@@ -70,6 +70,7 @@ struct ModelDev {
     int sparse;  // windowed features are exactly 0 where w == 0 (use_cutoff && cutoff_inputs)
     int ux6;     // bf16x6: bone-direction parts as x6 from the LDS feature store (u_part_x6)
     int single_net;  // one network for both passes; the fine pass evaluates only the I new samples
+    int cut_to, shift_in;  // kp encoder input transforms (ANERF_ENC_CUT_TO_DIST / _CUTOFF_SHIFT)
     int h3_top;      // fp16x3: biased exponent the largest scaled activation of a sample gets (127 + 10)
     float shift, B, tau, tau_v;
     const float* cutoff;
@@ -104,6 +105,14 @@ struct LdsPlan {
 };
 
 __host__ __device__ inline int pad32(int x) { return (x + 31) & ~31; }
+
+// The kp CutoffEmbedder's inputs for distance `dist` to a joint with cutoff c
+// (core/cutoff_embedder.py:125-134): the raw input u = c - dist under --cut_to_dist (else dist), the
+// frequencies' input u * (2 / c) - 1 under --cutoff_shift (else u); two roundings each, as torch.
+__device__ __forceinline__ void kp_inputs(int cut_to, int shift_in, float dist, float c, float& u, float& uf) {
+    u = cut_to ? c - dist : dist;
+    uf = shift_in ? u * (2.0f / c) - 1.0f : u;
+}
 
 __host__ __device__ inline LdsPlan make_plan(int R, int nj, int W, int S, int T, int mrv, int ngh, int D, int njh2,
                                              bool with_uf) {

@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define ANERF_ABI_VERSION 6
+#define ANERF_ABI_VERSION 7
 
 enum {
     ANERF_OK = 0,
@@ -109,7 +109,15 @@ typedef struct {
                                 pass evaluates only the I new samples and merges raws (:462-468), the
                                 importance weights are 0.5 (max(w_l,w_k) + max(w_k,w_u)) + 0.01
                                 (ray_utils.py:270-277); requires has_fine == 0 */
+    int32_t encoder_flags;   /* ANERF_ENC_* (kp embedder options of the cutoff embedder; 0 = none) */
 } anerf_model_desc;
+
+/* anerf_model_desc.encoder_flags: the kp (distance) CutoffEmbedder's input transforms
+ * (core/cutoff_embedder.py:125-134, only with use_cutoff): CUT_TO_DIST (--cut_to_dist) feeds
+ * c_j - dist to the encoding (the raw input and the frequencies); CUTOFF_SHIFT (--cutoff_shift)
+ * feeds (input * (2 / c_j) - 1) to the frequencies only.  The cutoff window keeps the distance. */
+#define ANERF_ENC_CUT_TO_DIST 1
+#define ANERF_ENC_CUTOFF_SHIFT 2
 
 /* HOST pointers to one NeRF's weights, torch nn.Linear layout [out][in] (core/networks/nerf.py:57-88). */
 typedef struct {

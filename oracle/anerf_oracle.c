@@ -58,6 +58,9 @@ typedef struct {
      * as `embedded * get_schedule_w()` then `* w` (:150-154); NULL = no schedule */
     const float* sched_w;
     const float* sched_wv;
+    /* --cut_to_dist / --cutoff_shift (kp CutoffEmbedder only, cutoff_embedder.py:125-134): the raw
+     * input is c_j - dist, the frequencies take (input * (2 / c_j) - 1); the window keeps dist */
+    int cut_to, shift_in;
     oracle_net coarse, fine;
 } oracle_model;
 
@@ -293,9 +296,16 @@ static void encode_point(const oracle_model* m, const float* skts, const float p
         /* kp block: CutoffEmbedder(dist_inputs=False) (cutoff_embedder.py:125-158) */
         float w = 1.0f;
         if (m->use_cutoff) w = 1.0f - sigmoidf_(m->tau * (dist - m->cutoff[j]));
-        fv[j] = (m->use_cutoff && m->cutoff_inputs) ? dist * w : dist;
+        float u = dist, uf = dist;
+        if (m->use_cutoff && m->cut_to) u = m->cutoff[j] - dist; /* inputs = cutoff - inputs */
+        uf = u;
+        if (m->use_cutoff && m->shift_in) {                       /* shifted = inputs * (2 / c) - 1 */
+            const float k2 = 2.0f / m->cutoff[j];
+            uf = u * k2 - 1.0f;
+        }
+        fv[j] = (m->use_cutoff && m->cutoff_inputs) ? u * w : u;
         for (int f = 0; f < nfk; ++f) {
-            float a = dist * (float)(1 << f);
+            float a = uf * (float)(1 << f);
             if (m->sched_w && m->use_cutoff) {
                 fv[(1 + 2 * f) * nj + j] = (sinf(a) * m->sched_w[f]) * w;
                 fv[(2 + 2 * f) * nj + j] = (cosf(a) * m->sched_w[f]) * w;

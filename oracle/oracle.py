@@ -29,7 +29,8 @@ class _Model(ctypes.Structure):
                 ("density_softplus", ctypes.c_int), ("softplus_shift", ctypes.c_float),
                 ("density_scale", ctypes.c_float), ("tau", ctypes.c_float), ("tau_v", ctypes.c_float),
                 ("cutoff", _f), ("cutoff_v", _f), ("has_fine", ctypes.c_int), ("single_net", ctypes.c_int),
-                ("lindisp", ctypes.c_int), ("sched_w", _f), ("sched_wv", _f),
+                ("lindisp", ctypes.c_int), ("sched_w", _f), ("sched_wv", _f), ("cut_to", ctypes.c_int),
+                ("shift_in", ctypes.c_int),
                 ("coarse", _Net), ("fine", _Net)]
 
 
@@ -94,6 +95,7 @@ class OracleModel:
             coarse, fine = (fine if fine is not None else coarse), None
         m.single_net = int(cfg.single_net)
         m.lindisp = int(cfg.lindisp)
+        m.cut_to, m.shift_in = int(getattr(cfg, "cut_to_dist", False)), int(getattr(cfg, "cutoff_shift", False))
         if getattr(cfg, "freq_schedule", False):
             m.sched_w = self._k(schedule_w(e["sched_alpha"], cfg.multires))
             m.sched_wv = self._k(schedule_w(ev["sched_alpha"], cfg.multires_views))

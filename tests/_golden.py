@@ -20,7 +20,9 @@ NAMES = ["c1_64_s32_d4w128", "c2_256_s64_d8w256", "c3_512_s64i128_d8w256", "c4_5
          # configs/surreal/surreal_single.txt (single_net, multires_views 0, 96 + 48); tau at its ceiling
          "s1_single_s96i48_mrv0", "t2000_512_s64i128",
          # --lindisp (inverse-depth samples); --freq_schedule at sched_alpha 2.3 (D = 8: skip layer)
-         "l1_lindisp_s32i16_d4w128", "fs1_freqsched_s32i16_d8w128"]
+         "l1_lindisp_s32i16_d4w128", "fs1_freqsched_s32i16_d8w128",
+         # --cut_to_dist, --cutoff_shift (the kp cutoff embedder's input transforms)
+         "cd1_cuttodist_s32i16_d8w128", "cs1_cutoffshift_s32i16_d4w128"]
 
 
 class Golden:
@@ -46,6 +48,7 @@ class Golden:
                                        multires_views=m.get("mrv", 4), single_net=m.get("single", False),
                                        lindisp="--lindisp" in flags or bool(m.get("lindisp", False)),
                                        freq_schedule="--freq_schedule" in flags,
+                                       cut_to_dist="--cut_to_dist" in flags, cutoff_shift="--cutoff_shift" in flags,
                                        init_freq=float(flags[flags.index("--init_freq") + 1])
                                        if "--init_freq" in flags else 0.0,
                                        **kw).validate()

@@ -120,6 +120,12 @@ CONFIGS = {
     # embedders (core/cutoff_embedder.py:150, 192-197); D = 8 so the skip layer's x part is covered
     "fs1_freqsched_s32i16_d8w128": dict(H=128, NJ=24, S=32, I=16, D=8, W=128, tau=20.0, kind="rays", n_rays=128,
                                         seed=26, flags=["--freq_schedule", "--init_freq", "2.3"], sched=2.3),
+    # --cut_to_dist (the kp encoding of c_j - dist) and --cutoff_shift (frequencies of dist * 2 / c_j - 1),
+    # core/cutoff_embedder.py:125-134
+    "cd1_cuttodist_s32i16_d8w128": dict(H=128, NJ=24, S=32, I=16, D=8, W=128, tau=20.0, kind="rays", n_rays=128,
+                                        seed=27, flags=["--cut_to_dist"]),
+    "cs1_cutoffshift_s32i16_d4w128": dict(H=128, NJ=24, S=32, I=16, D=4, W=128, tau=20.0, kind="rays",
+                                          n_rays=128, seed=25, flags=["--cutoff_shift"]),
 }
 
 

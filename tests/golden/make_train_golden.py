@@ -47,6 +47,9 @@ CONFIGS = {
     "t8_freqsched": dict(H=128, NJ=24, S=32, I=16, D=8, W=128, tau=20.0, kind="rays", seed=38, n_rays=64,
                          n_poses=2, flags=["--freq_schedule", "--init_freq", "1.0"], sched=1.0,
                          global_step=1700, cutoff_step=250, cutoff_rate=10.0),
+    # --cut_to_dist with --cutoff_shift: the training encoder and its gradient to the poses
+    "t9_cutto_shift": dict(H=128, NJ=24, S=32, I=16, D=4, W=128, tau=20.0, kind="rays", seed=39, n_rays=64,
+                           n_poses=2, flags=["--cut_to_dist", "--cutoff_shift"]),
 }
 FULL_LIMIT = 20000   # parameters with more entries are sampled
 SAMPLE = 4096

@@ -20,22 +20,32 @@ import make_golden as mg  # noqa: E402
 
 
 def probe_no_viewdirs(mods, tmp):
+    return probe(mods, tmp, [])
+
+
+def probe(mods, tmp, flags):
+    """render_rays of 16 rays under the given flags: None, or the reference's own exception."""
     run_nerf, _, raycasters, _, sk = mods
     argv = ["--N_samples", "32", "--N_importance", "16", "--netdepth", "4", "--netwidth", "128", "--use_cutoff",
             "--cutoff_inputs", "--ext_scale", "0.001", "--chunk", "4096", "--no_reload", "--basedir", tmp,
-            "--expname", "x"]
+            "--expname", "x"] + flags
     args = run_nerf.config_parser().parse_args(argv)
     os.makedirs(os.path.join(tmp, "x"), exist_ok=True)
     data_attrs = {"skel_type": sk.SMPLSkeleton, "near": 0.0, "far": 1.0, "n_views": 5,
                   "joint_coords": np.zeros((24, 3, 3), np.float32)}
     _, rk, _, _, _, _ = raycasters.create_raycaster(args, data_attrs)
     rk["ray_caster"].eval()
+    rc = rk["ray_caster"]
+    attrs = {f"{e}.{a}": bool(getattr(getattr(rc, e), a)) for e in ("embed_fn", "embeddirs_fn")
+             for a in ("normalize", "cut_to_cutoff", "shift_inputs") if hasattr(getattr(rc, e), a)}
     sc = mg.scene_for(dict(H=64, NJ=24, seed=41))
     (o, d), _, cyls, _ = mg.rays_for(mods, sc)
     sc["cyls"] = cyls
     try:
+        import torch
+        torch.manual_seed(0)
         mg.render_subset(mods, rk, o[:16], d[:16], sc)
-        return {"raises": None}
+        return {"raises": None, "embedder_attributes": attrs}
     except Exception as e:  # the reference's own failure, recorded
         tb = traceback.extract_tb(e.__traceback__)
         ref = [f"{os.path.relpath(f.filename, mg.REF)}:{f.lineno}" for f in tb if f.filename.startswith(mg.REF)]
@@ -46,6 +56,13 @@ def main():
     mods = mg.import_reference()
     with tempfile.TemporaryDirectory() as tmp:
         out = {"use_viewdirs=False": probe_no_viewdirs(mods, tmp)}
+        # the remaining refused embedder flags, with the view branch on as in every shipped config
+        vd = ["--use_viewdirs", "--cutoff_viewdir"]
+        for name, flags in (("normalize_cutoff", ["--normalize_cutoff"]), ("cut_to_dist", ["--cut_to_dist"]),
+                            ("cutoff_shift", ["--cutoff_shift"]),
+                            ("cutoff_bones", ["--cutoff_bones"]),
+                            ("cutoff_bones+multires_bones=2", ["--cutoff_bones", "--multires_bones", "2"])):
+            out[name] = probe(mods, tmp, vd + flags)
     path = os.path.join(HERE, "reference_flags.json")
     with open(path, "w") as f:
         json.dump(out, f, indent=1)

@@ -44,7 +44,7 @@ def test_config_rejects_unsupported_flags():
     with pytest.raises(NotImplementedError):
         cfg(multires_bones=2).validate()
     with pytest.raises(NotImplementedError):
-        cfg(extra={"cutoff_shift": True}).validate()
+        cfg(extra={"cutoff_bones": True}).validate()
     with pytest.raises(NotImplementedError):
         cfg(extra={"kp_dist_type": "relpos"}).validate()
     with pytest.raises(NotImplementedError):
@@ -170,3 +170,20 @@ def test_random_boxes_bit_exact_vs_reference():
         np.testing.assert_array_equal(cyls[0], z["cyl"][i])
         np.testing.assert_array_equal(boxes[0][0], z["tl"][i])
         np.testing.assert_array_equal(boxes[0][1], z["br"][i])
+
+
+def test_normalize_cutoff_is_a_noop_like_the_reference():
+    """--normalize_cutoff never reaches CutoffEmbedder.normalize in the reference (the kwarg is named
+    normalize_cutoff, core/raycasters.py:32 vs core/cutoff_embedder.py:64); recorded from the reference
+    by tests/golden/probe_reference_flags.py.  Accepted here with the same (absent) effect."""
+    import json
+    with open(os.path.join(HERE, "golden", "reference_flags.json")) as f:
+        rec = json.load(f)["normalize_cutoff"]
+    assert rec["raises"] is None
+    assert not rec["embedder_attributes"]["embed_fn.normalize"]
+    assert not rec["embedder_attributes"]["embeddirs_fn.normalize"]
+    args = types.SimpleNamespace(normalize_cutoff=True, cut_to_dist=True, cutoff_shift=True)
+    cfg = config.RenderConfig.from_args(args, 24)
+    assert cfg.normalize_cutoff and cfg.cut_to_dist and cfg.cutoff_shift
+    with pytest.raises(NotImplementedError):
+        config.RenderConfig.from_args(types.SimpleNamespace(cutoff_bones=True), 24)
