@@ -437,7 +437,9 @@ __global__ __launch_bounds__(NTHR, 2) void mlp_nt_kernel(NTArgs g) {
 // the partial tile leaves through LDS in full rows.  The bias gradient (k-tile 0) sums the staged
 // dY per column in a fixed order.
 constexpr int TSK = 32;                 // rows per step, at most (slabs are whole pairs of steps)
-constexpr unsigned TOOB = 0x40000000u;  // a lane offset past every descriptor's range (ld < 2^24)
+// a lane offset past every descriptor's range: a step's range is at most 32 rows x ld x 4 B < 2^29
+// for ld < 2^22 (checked on the host), and TOOB plus 16 rows of offset stays below 2^31
+constexpr unsigned TOOB = 0x40000000u;
 
 // plane [row][128 bf16]: 256 B rows whose 16 B chunks are XOR-swizzled by 4 (row & 3), so the four
 // rows of a transposed read's lane group (64 B each) land on disjoint banks and a staging write (8
@@ -519,7 +521,7 @@ __global__ __launch_bounds__(NTHR, 2) void mlp_tn_kernel(TNArgs g) {
     struct Regs {
         f32x4 y[PR][2], x[PR][2][NSEG];
     };
-    // (a TOOB lane offset plus 16 rows stays past the range: ld < 2^24)
+    // (a TOOB lane offset plus 16 rows stays past the range: ld < 2^22)
     auto fetch = [&](long long mb, Regs& R) {
         const __amdgpu_buffer_rsrc_t ry = rows_rsrc<SK>(dyp, lddy, mb, mhi);
 #pragma unroll
@@ -887,9 +889,9 @@ int anerf_mlp_wgrad(int64_t m, int32_t n, int32_t k, const float* dy, int64_t ld
         return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_wgrad: bad arguments");
     // dY is read as float4 groups of whole rows: 16 B aligned, ld a multiple of 4 and >= n rounded up
     // to 4 (the padding columns only reach the discarded rows n.. of the tile)
-    if (lddy >= (1 << 24)) return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_wgrad: lddy >= 2^24");
+    if (lddy >= (1 << 22)) return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_wgrad: lddy >= 2^22");
     for (int i = 0; i < n_x && x; ++i)
-        if (x[i].ld >= (1 << 24)) return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_wgrad: x ld >= 2^24");
+        if (x[i].ld >= (1 << 22)) return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_wgrad: x ld >= 2^22");
     if ((reinterpret_cast<uintptr_t>(dy) & 15) || (lddy & 3) || lddy < (n + 3) / 4 * 4)
         return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_wgrad: dy must be 16 B aligned with ld % 4 == 0 "
                                                  "and ld >= round_up(n, 4)");
