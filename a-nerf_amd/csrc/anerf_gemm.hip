@@ -688,13 +688,27 @@ __global__ __launch_bounds__(NTHR, 2) void mlp_tn_kernel(TNArgs g) {
 // dst[row][col] (+)= sum over the slabs of src[t][row][col]: a workgroup takes 128 columns of one row,
 // 32 float4 column groups x 8 slab groups (each a contiguous run of slabs, 4 loads in flight), the 8
 // partial sums then added in slab-group order through LDS (deterministic).  src rows hold a multiple
-// of 128 columns (the workspace's padding).
+// of 128 columns (the workspace's padding).  Row `rows` (when bsrc is set) is the bias gradient:
+// the same sum over bsrc[t][col] (slab stride bstride, bcols columns) into bdst, in the same launch.
 __global__ __launch_bounds__(256) void mlp_reduce_kernel(const float* __restrict__ src, int splits,
                                                          long long split_stride, long long row_stride, int cols,
-                                                         float* __restrict__ dst, long long ldd, int accum) {
+                                                         float* __restrict__ dst, long long ldd, int accum, int rows,
+                                                         const float* __restrict__ bsrc, long long bstride,
+                                                         int bcols, float* __restrict__ bdst) {
     __shared__ f32x4 part[8][32];
     const int cg = threadIdx.x & 31, sgi = threadIdx.x >> 5;
-    const int row = blockIdx.y, c0 = blockIdx.x * 128 + 4 * cg;
+    int row = blockIdx.y;
+    const int c0 = blockIdx.x * 128 + 4 * cg;
+    if (row == rows) {  // (uniform per workgroup) the bias row
+        src = bsrc;
+        split_stride = bstride;
+        row_stride = 0;
+        cols = bcols;
+        dst = bdst;
+        ldd = 0;
+        row = 0;
+    }
+    if (blockIdx.x * 128 >= cols) return;  // (a row narrower than the grid; uniform per workgroup)
     const int chunk = (splits + 7) / 8;
     const int t0 = sgi * chunk, t1 = t0 + chunk < splits ? t0 + chunk : splits;
     const float* p = src + row * row_stride + c0;
@@ -937,12 +951,11 @@ int anerf_mlp_wgrad(int64_t m, int32_t n, int32_t k, const float* dy, int64_t ld
     ANERF_TN_LAUNCH(2, 2)
     ANERF_TN_LAUNCH(2, 3)
 #undef ANERF_TN_LAUNCH
-    hipLaunchKernelGGL(mlp_reduce_kernel, dim3((unsigned)(g.kpad / 128), (unsigned)n), dim3(256), 0, st, g.ws,
+    // dW rows 0 .. n - 1 and (with db) the bias row n in one launch
+    const int gx = (db && g.npad > g.kpad ? g.npad : g.kpad) / 128;
+    hipLaunchKernelGGL(mlp_reduce_kernel, dim3((unsigned)gx, (unsigned)(n + (db ? 1 : 0))), dim3(256), 0, st, g.ws,
                        g.splits, (long long)g.npad * g.kpad, (long long)g.kpad, k, dw, (long long)lddw,
-                       accumulate != 0);
-    if (db)
-        hipLaunchKernelGGL(mlp_reduce_kernel, dim3((unsigned)(g.npad / 128), 1u), dim3(256), 0, st, g.wsb, g.splits,
-                           (long long)g.npad, 0ll, n, db, 0ll, accumulate != 0);
+                       accumulate != 0, n, g.wsb, (long long)g.npad, n, db);
     e = hipGetLastError();
     return e == hipSuccess ? ANERF_OK : anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));
 }
