@@ -502,8 +502,10 @@ int anerf_train_composite(const anerf_model* m, const float* raw, const float* z
         return fail(ANERF_EINVAL, "anerf_train_composite: bad arguments");
     if (n_rays == 0) return ANERF_OK;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    hipLaunchKernelGGL(train_composite_kernel, dim3(blocks_of(n_rays, 64)), dim3(64), 0, st, m->md, raw, z, ray_batch,
-                       ray_stride, n_rays, n_samples, noise, rgb, disp, acc, weights, alpha, trans);
+    if (n_rays > 0x7fffffff || n_samples > 1024) return fail(ANERF_EINVAL, "anerf_train_composite: more than 1024 samples per ray");
+    hipLaunchKernelGGL(train_composite_kernel, dim3((unsigned)n_rays), dim3(64), (size_t)7 * n_samples * sizeof(float),
+                       st, m->md, raw, z, ray_batch, ray_stride, n_rays, n_samples, noise, rgb, disp, acc, weights,
+                       alpha, trans);
     HIP_TRY(hipGetLastError());
     return ANERF_OK;
 }
@@ -518,9 +520,11 @@ int anerf_train_composite_backward(const anerf_model* m, const float* raw, const
         return fail(ANERF_EINVAL, "anerf_train_composite_backward: bad arguments");
     if (n_rays == 0) return ANERF_OK;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    hipLaunchKernelGGL(train_composite_backward_kernel, dim3(blocks_of(n_rays, 64)), dim3(64), 0, st, m->md, raw, z,
-                       ray_batch, ray_stride, n_rays, n_samples, noise, weights, alpha, trans, g_rgb, g_disp, g_acc,
-                       g_weights, g_alpha, g_raw);
+    if (n_rays > 0x7fffffff || n_samples > 1024)
+        return fail(ANERF_EINVAL, "anerf_train_composite_backward: more than 1024 samples per ray");
+    hipLaunchKernelGGL(train_composite_backward_kernel, dim3((unsigned)n_rays), dim3(64),
+                       (size_t)9 * n_samples * sizeof(float), st, m->md, raw, z, ray_batch, ray_stride, n_rays,
+                       n_samples, noise, weights, alpha, trans, g_rgb, g_disp, g_acc, g_weights, g_alpha, g_raw);
     HIP_TRY(hipGetLastError());
     return ANERF_OK;
 }

@@ -271,45 +271,69 @@ __device__ __forceinline__ float density_act_grad(const ModelDev& M, float x) {
     return e / (e + 1.0f);
 }
 
-__global__ void train_composite_kernel(ModelDev M, const float* __restrict__ raw, const float* __restrict__ z,
-                                       const float* __restrict__ rb, int stride, int64_t n, int ns,
-                                       const float* __restrict__ noise, float* __restrict__ rgb,
-                                       float* __restrict__ disp, float* __restrict__ acc, float* __restrict__ wts,
-                                       float* __restrict__ alpha, float* __restrict__ trans) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// One wave per ray: the per-sample alpha / colour terms in parallel into LDS, the transmittance
+// product (double, torch's CPU cumprod) and the sums in sample order by lane 0, then the per-sample
+// outputs in parallel -- the same operations in the same order as a thread-per-ray loop.
+__global__ __launch_bounds__(64) void train_composite_kernel(ModelDev M, const float* __restrict__ raw,
+                                                             const float* __restrict__ z, const float* __restrict__ rb,
+                                                             int stride, int64_t n, int ns,
+                                                             const float* __restrict__ noise, float* __restrict__ rgb,
+                                                             float* __restrict__ disp, float* __restrict__ acc,
+                                                             float* __restrict__ wts, float* __restrict__ alpha,
+                                                             float* __restrict__ trans) {
+    extern __shared__ float cl[];  // [7][ns]: alpha, rgb terms (3), z, transmittance, weight
+    const int64_t i = blockIdx.x;
     if (i >= n) return;
+    const int lane = threadIdx.x;
+    float *la = cl, *lc0 = cl + ns, *lc1 = cl + 2 * ns, *lc2 = cl + 3 * ns, *lz = cl + 4 * ns, *lt = cl + 5 * ns,
+          *lw = cl + 6 * ns;
     const float* ray = rb + i * stride;
     const float dn = norm3(ray[3], ray[4], ray[5]);
     const float* zr = z + i * ns;
     const float* rr = raw + i * ns * 4;
-    double T = 1.0;
-    float sa = 0.0f, sd = 0.0f, sr = 0.0f, sg = 0.0f, sb = 0.0f;
-    for (int s = 0; s < ns; ++s) {
+    for (int s = lane; s < ns; s += 64) {
         float dist = (s + 1 < ns) ? (zr[s + 1] - zr[s]) : 1e10f;
         dist = dist * dn;
         const float x = rr[4 * s + 3] / M.B + (noise ? noise[i * ns + s] : 0.0f);
-        const float a = 1.0f - expf(-density_act(M, x) * dist);
-        const float t = (float)T;
-        T *= (double)((1.0f - a) + 1e-10f);
-        const float w = a * t;
-        alpha[i * ns + s] = a;
-        trans[i * ns + s] = t;
-        wts[i * ns + s] = w;
-        sa += w;
-        sd += w * zr[s];
-        sr += w * (sigmoid(rr[4 * s + 0]) * 1.002f - 0.001f);
-        sg += w * (sigmoid(rr[4 * s + 1]) * 1.002f - 0.001f);
-        sb += w * (sigmoid(rr[4 * s + 2]) * 1.002f - 0.001f);
+        la[s] = 1.0f - expf(-density_act(M, x) * dist);
+        lz[s] = zr[s];
+        lc0[s] = sigmoid(rr[4 * s + 0]) * 1.002f - 0.001f;
+        lc1[s] = sigmoid(rr[4 * s + 1]) * 1.002f - 0.001f;
+        lc2[s] = sigmoid(rr[4 * s + 2]) * 1.002f - 0.001f;
     }
-    const float ratio = sd / (sa + 1e-10f);
-    float dsp = 1.0f / fmaxf(ratio, 1e-10f);
-    if (ratio != ratio) dsp = ratio;
-    if (fabsf(sa) <= 1e-8f) dsp = 0.0f;
-    rgb[3 * i] = sr;
-    rgb[3 * i + 1] = sg;
-    rgb[3 * i + 2] = sb;
-    disp[i] = dsp;
-    acc[i] = sa < 1.0f ? sa : 1.0f;
+    __syncthreads();
+    if (lane == 0) {
+        double T = 1.0;
+        float sa = 0.0f, sd = 0.0f, sr = 0.0f, sg = 0.0f, sb = 0.0f;
+        for (int s = 0; s < ns; ++s) {
+            const float a = la[s];
+            const float t = (float)T;
+            T *= (double)((1.0f - a) + 1e-10f);
+            const float w = a * t;
+            lt[s] = t;
+            lw[s] = w;
+            sa += w;
+            sd += w * lz[s];
+            sr += w * lc0[s];
+            sg += w * lc1[s];
+            sb += w * lc2[s];
+        }
+        const float ratio = sd / (sa + 1e-10f);
+        float dsp = 1.0f / fmaxf(ratio, 1e-10f);
+        if (ratio != ratio) dsp = ratio;
+        if (fabsf(sa) <= 1e-8f) dsp = 0.0f;
+        rgb[3 * i] = sr;
+        rgb[3 * i + 1] = sg;
+        rgb[3 * i + 2] = sb;
+        disp[i] = dsp;
+        acc[i] = sa < 1.0f ? sa : 1.0f;
+    }
+    __syncthreads();
+    for (int s = lane; s < ns; s += 64) {
+        alpha[i * ns + s] = la[s];
+        trans[i * ns + s] = lt[s];
+        wts[i * ns + s] = lw[s];
+    }
 }
 
 // Backward of train_composite_kernel: dL/draw (N x ns x 4) from dL/d{rgb, disp, acc, weights, alpha}
@@ -317,46 +341,78 @@ __global__ void train_composite_kernel(ModelDev M, const float* __restrict__ raw
 // and P_s their exclusive product: dL/dalpha_s = G_s P_s + galpha_s - P_s R_s, where
 // R_s = sum_{k>s} G_k alpha_k prod_{s<m<k} f_m runs backwards as R_{s-1} = G_s alpha_s + f_s R_s
 // (no division by f_s); then dalpha/dsigma = exp(-sigma delta) delta, the activation's gradient, 1/B;
-// rgb: w_s g_rgb 1.002 sigmoid'(raw).  One thread per ray.
-__global__ void train_composite_backward_kernel(ModelDev M, const float* __restrict__ raw, const float* __restrict__ z,
-                                                const float* __restrict__ rb, int stride, int64_t n, int ns,
-                                                const float* __restrict__ noise, const float* __restrict__ wts,
-                                                const float* __restrict__ alpha, const float* __restrict__ trans,
-                                                const float* __restrict__ g_rgb, const float* __restrict__ g_disp,
-                                                const float* __restrict__ g_acc, const float* __restrict__ g_w,
-                                                const float* __restrict__ g_alpha, float* __restrict__ g_raw) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// rgb: w_s g_rgb 1.002 sigmoid'(raw).  One wave per ray: the per-sample terms in parallel, the sums
+// and the R recurrence (double) in sample order by lane 0 -- the thread-per-ray loop's operations in
+// its order.
+__global__ __launch_bounds__(64) void train_composite_backward_kernel(
+    ModelDev M, const float* __restrict__ raw, const float* __restrict__ z, const float* __restrict__ rb, int stride,
+    int64_t n, int ns, const float* __restrict__ noise, const float* __restrict__ wts, const float* __restrict__ alpha,
+    const float* __restrict__ trans, const float* __restrict__ g_rgb, const float* __restrict__ g_disp,
+    const float* __restrict__ g_acc, const float* __restrict__ g_w, const float* __restrict__ g_alpha,
+    float* __restrict__ g_raw) {
+    extern __shared__ float cl[];  // [8][ns]: w, z, alpha, P, sigmoid(rgb) (3), G, then P R
+    __shared__ float sc[4];        // r, gd_r, den, ga
+    const int64_t i = blockIdx.x;
     if (i >= n) return;
+    const int lane = threadIdx.x;
+    float *lw = cl, *lz = cl + ns, *la = cl + 2 * ns, *lP = cl + 3 * ns, *lc0 = cl + 4 * ns, *lc1 = cl + 5 * ns,
+          *lc2 = cl + 6 * ns, *lG = cl + 7 * ns, *lPR = cl + 8 * ns;
     const float* ray = rb + i * stride;
     const float dn = norm3(ray[3], ray[4], ray[5]);
     const float* zr = z + i * ns;
     const float* rr = raw + i * ns * 4;
-    const float* wr = wts + i * ns;
-    float sa = 0.0f, sd = 0.0f;
-    for (int s = 0; s < ns; ++s) {
-        sa += wr[s];
-        sd += wr[s] * zr[s];
+    for (int s = lane; s < ns; s += 64) {
+        lw[s] = wts[i * ns + s];
+        lz[s] = zr[s];
+        la[s] = alpha[i * ns + s];
+        lP[s] = trans[i * ns + s];
+        lc0[s] = sigmoid(rr[4 * s + 0]);
+        lc1[s] = sigmoid(rr[4 * s + 1]);
+        lc2[s] = sigmoid(rr[4 * s + 2]);
     }
     const float gr = g_rgb ? g_rgb[3 * i] : 0.0f, gg = g_rgb ? g_rgb[3 * i + 1] : 0.0f,
                 gb = g_rgb ? g_rgb[3 * i + 2] : 0.0f;
-    const float ga = (g_acc && sa < 1.0f) ? g_acc[i] : 0.0f;  // torch.minimum(sum w, 1)
-    // disp = mask / max(1e-10, depth / (W + 1e-10)):  d disp / d w_s = -mask / r^2 (z_s - r) / (W + 1e-10)
-    float gd_r = 0.0f, r = 0.0f;
-    const float den = sa + 1e-10f;
-    if (g_disp) {
-        r = sd / den;
-        if (r > 1e-10f && !(fabsf(sa) <= 1e-8f)) gd_r = -g_disp[i] / (r * r);
+    __syncthreads();
+    if (lane == 0) {  // the sums in sample order
+        float sa = 0.0f, sd = 0.0f;
+        for (int s = 0; s < ns; ++s) {
+            sa += lw[s];
+            sd += lw[s] * lz[s];
+        }
+        const float ga = (g_acc && sa < 1.0f) ? g_acc[i] : 0.0f;  // torch.minimum(sum w, 1)
+        // disp = mask / max(1e-10, depth / (W + 1e-10)):  d disp / d w_s = -mask / r^2 (z_s - r) / (W + 1e-10)
+        float gd_r = 0.0f, r = 0.0f;
+        const float den = sa + 1e-10f;
+        if (g_disp) {
+            r = sd / den;
+            if (r > 1e-10f && !(fabsf(sa) <= 1e-8f)) gd_r = -g_disp[i] / (r * r);
+        }
+        sc[0] = r, sc[1] = gd_r, sc[2] = den, sc[3] = ga;
     }
-    double R = 0.0;
-    for (int s = ns - 1; s >= 0; --s) {
-        const float c0 = sigmoid(rr[4 * s + 0]), c1 = sigmoid(rr[4 * s + 1]), c2 = sigmoid(rr[4 * s + 2]);
-        const float w = wr[s], a = alpha[i * ns + s], P = trans[i * ns + s];
-        float G = gr * (c0 * 1.002f - 0.001f) + gg * (c1 * 1.002f - 0.001f) + gb * (c2 * 1.002f - 0.001f) + ga;
-        if (gd_r != 0.0f) G += gd_r * (zr[s] - r) / den;
+    __syncthreads();
+    const float r = sc[0], gd_r = sc[1], den = sc[2], ga = sc[3];
+    for (int s = lane; s < ns; s += 64) {  // G_s = dL/dw_s
+        float G = gr * (lc0[s] * 1.002f - 0.001f) + gg * (lc1[s] * 1.002f - 0.001f) + gb * (lc2[s] * 1.002f - 0.001f) +
+                  ga;
+        if (gd_r != 0.0f) G += gd_r * (lz[s] - r) / den;
         if (g_w) G += g_w[i * ns + s];
-        const float gal = G * P + (g_alpha ? g_alpha[i * ns + s] : 0.0f) - (float)((double)P * R);
-        R = (double)G * (double)a + (double)((1.0f - a) + 1e-10f) * R;
-        float dist = (s + 1 < ns) ? (zr[s + 1] - zr[s]) : 1e10f;
+        lG[s] = G;
+    }
+    __syncthreads();
+    if (lane == 0) {  // R_s backwards (double), P_s R_s for each sample
+        double R = 0.0;
+        for (int s = ns - 1; s >= 0; --s) {
+            lPR[s] = (float)((double)lP[s] * R);
+            R = (double)lG[s] * (double)la[s] + (double)((1.0f - la[s]) + 1e-10f) * R;
+        }
+    }
+    __syncthreads();
+    for (int s = lane; s < ns; s += 64) {
+        const float G = lG[s], a = la[s], P = lP[s], w = lw[s];
+        const float c0 = lc0[s], c1 = lc1[s], c2 = lc2[s];
+        (void)a;
+        const float gal = G * P + (g_alpha ? g_alpha[i * ns + s] : 0.0f) - lPR[s];
+        float dist = (s + 1 < ns) ? (lz[s + 1] - lz[s]) : 1e10f;
         dist = dist * dn;
         const float x = rr[4 * s + 3] / M.B + (noise ? noise[i * ns + s] : 0.0f);
         const float sig = density_act(M, x);

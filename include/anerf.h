@@ -329,13 +329,14 @@ int anerf_train_encode_backward(const anerf_model* m, const float* ray_batch, in
 
 /* raw2outputs of raw [N][S][4] at z [N][S] with noise [N][S] (= randn * raw_noise_std * B, added to
  * raw_sigma / B; NULL: none): rgb [N][3], disp [N], acc [N], weights, alpha and the exclusive
- * transmittance trans [N][S] (kept for the backward). */
+ * transmittance trans [N][S] (kept for the backward).  S <= 1024 (one wave per ray, LDS-staged). */
 int anerf_train_composite(const anerf_model* m, const float* raw, const float* z, const float* ray_batch,
                           int32_t ray_stride, int64_t n_rays, int32_t n_samples, const float* noise, float* rgb,
                           float* disp, float* acc, float* weights, float* alpha, float* trans, void* stream);
 
 /* g_raw [N][S][4] from the gradients of the outputs of anerf_train_composite (g_rgb [N][3], g_disp,
- * g_acc [N], g_weights, g_alpha [N][S]; any may be NULL = zero) and its saved weights/alpha/trans. */
+ * g_acc [N], g_weights, g_alpha [N][S]; any may be NULL = zero) and its saved weights/alpha/trans;
+ * S <= 1024. */
 int anerf_train_composite_backward(const anerf_model* m, const float* raw, const float* z, const float* ray_batch,
                                    int32_t ray_stride, int64_t n_rays, int32_t n_samples, const float* noise,
                                    const float* weights, const float* alpha, const float* trans, const float* g_rgb,
