@@ -487,9 +487,17 @@ int anerf_train_encode_backward(const anerf_model* m, const float* ray_batch, in
     const int spb = 256 / nj;                      // sample slots per block
     const int threads = (spb * nj + 63) / 64 * 64;  // (whole waves)
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    hipLaunchKernelGGL(train_encode_backward_kernel, dim3((unsigned)n_rays), dim3(threads),
-                       (size_t)spb * nj * 12 * sizeof(float), st, m->md, ray_batch, ray_stride, n_rays, z, n_samples,
-                       skts, ray_pose, n_poses, pts_noise, grad_feat, grad_skts, spb);
+    const int mr = m->md.mr, mrv = m->md.mrv;
+    auto launch = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3((unsigned)n_rays), dim3(threads), (size_t)spb * nj * 12 * sizeof(float), st,
+                           m->md, ray_batch, ray_stride, n_rays, z, n_samples, skts, ray_pose, n_poses, pts_noise,
+                           grad_feat, grad_skts, spb);
+    };
+    if (mr == 7 && mrv == 4) launch(train_encode_backward_kernel<7, 4>);
+    else if (mr == 7 && mrv == 0) launch(train_encode_backward_kernel<7, 0>);
+    else if (mr == 10 && mrv == 4) launch(train_encode_backward_kernel<10, 4>);
+    else if (mr == 10 && mrv == 0) launch(train_encode_backward_kernel<10, 0>);
+    else return fail(ANERF_EINVAL, "anerf_train_encode_backward: multires must be 7 or 10, multires_views 4 or 0");
     HIP_TRY(hipGetLastError());
     return ANERF_OK;
 }

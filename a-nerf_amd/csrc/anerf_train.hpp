@@ -104,11 +104,32 @@ __global__ void train_encode_kernel(ModelDev M, const float* __restrict__ rb, in
 // values, row-major) of joint j given the feature gradients g (one row).  Same flags and forms as
 // encode_row (cutoff windows w = 1 - sigmoid(tau (dist - c)), dw/ddist = -tau w (1 - w);
 // F.normalize x / max(|x|, 1e-12); torch.norm's gradient 0 at 0).
+// MR / MRV: the frequencies (compile-time, so every feature gradient of the joint is loaded up front
+// and the loads overlap instead of waiting one loop iteration each).
+template <int MR, int MRV>
 __device__ __forceinline__ void encode_row_grad_joint(const ModelDev& M, const float* __restrict__ S, int j,
                                                       float px, float py, float pz, float dx, float dy, float dz,
                                                       const float* __restrict__ g, float (&gS)[12]) {
-    const int nj = M.nj, nv = 1 + 2 * M.mr;
+    const int nj = M.nj, nv = 1 + 2 * MR;
     const int cx = nj * nv + 3 * nj;
+    constexpr int MV = MRV > 0 ? MRV : 1;
+    float gs_[MR], gc_[MR], gu_[3], gv0_[3], gvs_[3][MV], gvc_[3][MV];
+    const float g0 = g[j];
+#pragma unroll
+    for (int fi = 0; fi < MR; ++fi) {
+        gs_[fi] = g[(1 + 2 * fi) * nj + j];
+        gc_[fi] = g[(2 + 2 * fi) * nj + j];
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        gu_[c] = g[nj * nv + 3 * j + c];
+        gv0_[c] = g[cx + 3 * j + c];
+#pragma unroll
+        for (int fi = 0; fi < MRV; ++fi) {
+            gvs_[c][fi] = g[cx + (1 + 2 * fi) * 3 * nj + 3 * j + c];
+            gvc_[c][fi] = g[cx + (2 + 2 * fi) * 3 * nj + 3 * j + c];
+        }
+    }
     float qx, qy, qz;
     joint_local(S, px, py, pz, qx, qy, qz);
     const float dist = norm3(qx, qy, qz);
@@ -121,18 +142,18 @@ __device__ __forceinline__ void encode_row_grad_joint(const ModelDev& M, const f
     const float du = M.cut_to ? -1.0f : 1.0f;
     const float duf = M.shift_in ? du * (2.0f / M.cutoff[j]) : du;
     float g_dist = 0.0f, g_w = 0.0f;
-    const float g0 = g[j];
     if (cut_in) {
         g_dist += g0 * w * du;
         g_w += g0 * u;
     } else {
         g_dist += g0 * du;
     }
-    for (int fi = 0; fi < M.mr; ++fi) {
+#pragma unroll
+    for (int fi = 0; fi < MR; ++fi) {
         const float fr = (float)(1 << fi);
         float s, c;
         sincos_rr(uf * fr, s, c);
-        const float gs = g[(1 + 2 * fi) * nj + j], gc = g[(2 + 2 * fi) * nj + j];
+        const float gs = gs_[fi], gc = gc_[fi];
         g_w += gs * s + gc * c;
         g_dist += (gs * c - gc * s) * w * fr * duf;
     }
@@ -140,7 +161,7 @@ __device__ __forceinline__ void encode_row_grad_joint(const ModelDev& M, const f
     // ---- bone direction u = q / max(|q|, eps)
     float gqx, gqy, gqz;
     {
-        const float gux = g[nj * nv + 3 * j], guy = g[nj * nv + 3 * j + 1], guz = g[nj * nv + 3 * j + 2];
+        const float gux = gu_[0], guy = gu_[1], guz = gu_[2];
         if (dist > 1e-12f) {
             const float ux = qx / dist, uy = qy / dist, uz = qz / dist;
             const float dot = ux * gux + uy * guy + uz * guz;
@@ -162,19 +183,21 @@ __device__ __forceinline__ void encode_row_grad_joint(const ModelDev& M, const f
     const bool cutv = M.cutoff_viewdir != 0;
     const float wv = cutv ? cutoff_w(M.tau_v, dist, M.cutoff_v[j]) : 1.0f;
     float ge[3] = {0.0f, 0.0f, 0.0f}, g_wv = 0.0f;
+#pragma unroll
     for (int c = 0; c < 3; ++c) {
-        const float gv0 = g[cx + 3 * j + c];
+        const float gv0 = gv0_[c];
         if (cutv && M.cutoff_inputs) {
             ge[c] += gv0 * wv;
             g_wv += gv0 * e[c];
         } else {
             ge[c] += gv0;
         }
-        for (int fi = 0; fi < M.mrv; ++fi) {
+#pragma unroll
+        for (int fi = 0; fi < MRV; ++fi) {
             const float fr = (float)(1 << fi);
             float s, co;
             sincos_rr(e[c] * fr, s, co);
-            const float gs = g[cx + (1 + 2 * fi) * 3 * nj + 3 * j + c], gc = g[cx + (2 + 2 * fi) * 3 * nj + 3 * j + c];
+            const float gs = gvs_[c][fi], gc = gvc_[c][fi];
             g_wv += gs * s + gc * co;
             ge[c] += (gs * co - gc * s) * wv * fr;
         }
@@ -215,6 +238,7 @@ __device__ __forceinline__ void encode_row_grad_joint(const ModelDev& M, const f
 // once, by one wave, in whole runs.  The slots' sums are added through LDS in slot order
 // (deterministic within the ray) and accumulated into grad_skts[pose] (atomic: rays may share a
 // pose).  Rows 3 (the [0 0 0 1] row) get no gradient, as in the reference.
+template <int MR, int MRV>
 __global__ __launch_bounds__(256) void train_encode_backward_kernel(ModelDev M, const float* __restrict__ rb,
                                                                     int stride, int64_t n, const float* __restrict__ z,
                                                                     int ns, const float* __restrict__ skts,
@@ -243,7 +267,7 @@ __global__ __launch_bounds__(256) void train_encode_backward_kernel(ModelDev M, 
                 const float* q = pts_noise + 3 * (i * ns + s);
                 px += q[0], py += q[1], pz += q[2];
             }
-            encode_row_grad_joint(M, S, j, px, py, pz, ray[3], ray[4], ray[5], gfeat + (i * ns + s) * F, gS);
+            encode_row_grad_joint<MR, MRV>(M, S, j, px, py, pz, ray[3], ray[4], ray[5], gfeat + (i * ns + s) * F, gS);
         }
         float* const rr = red + (slot * nj + j) * 12;
 #pragma unroll
