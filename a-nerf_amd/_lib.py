@@ -61,6 +61,12 @@ class Seg(ctypes.Structure):
     _fields_ = [("p", ctypes.c_void_p), ("ld", ctypes.c_int64), ("cols", ctypes.c_int32)]
 
 
+class SplitJob(ctypes.Structure):
+    """anerf_split_job: one weight of anerf_mlp_split_weights_batch."""
+    _fields_ = [("w", ctypes.c_void_p), ("n", ctypes.c_int32), ("k", ctypes.c_int32), ("ldw", ctypes.c_int64),
+                ("transpose", ctypes.c_int32), ("precision", ctypes.c_int32), ("out", ctypes.c_void_p)]
+
+
 class OSeg(ctypes.Structure):
     """anerf_oseg: a column segment of a GEMM output (+ relu' mask, accumulate)."""
     _fields_ = [("p", ctypes.c_void_p), ("ld", ctypes.c_int64), ("cols", ctypes.c_int32), ("mask", ctypes.c_void_p),
@@ -155,6 +161,7 @@ SIGNATURES = {
     "anerf_mlp_split_bytes": (ctypes.c_size_t, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
     "anerf_mlp_split_weights": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64,
                                                ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]),
+    "anerf_mlp_split_weights_batch": (ctypes.c_int, [ctypes.POINTER(SplitJob), ctypes.c_int32, ctypes.c_void_p]),
     "anerf_mlp_gemm": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(Seg),
                                       ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
                                       ctypes.c_int32, ctypes.POINTER(OSeg), ctypes.c_int32, ctypes.c_void_p]),

@@ -739,9 +739,9 @@ __global__ __launch_bounds__(256) void mlp_reduce_kernel(const float* __restrict
 // 1 KB run of 64 lanes x 8 bf16, lane l = row nb*32 + (l & 31), columns ks*16 + 8 (l >> 5) + 0..7
 // (the B operand lane map of v_mfma_f32_32x32x16_bf16), zero padded.  Rows are w's rows (or, when
 // transposed, w's columns).
-__global__ void split_weights_kernel(const float* __restrict__ w, int n, int k, long long ldw, int transpose,
-                                     int nblocks, int ksteps, int npl, unsigned short* __restrict__ out) {
-    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;  // one (nb, ks, lane, e)
+__device__ __forceinline__ void split_weights_elem(const float* __restrict__ w, int n, int k, long long ldw,
+                                                   int transpose, int nblocks, int ksteps, int npl,
+                                                   unsigned short* __restrict__ out, long long idx) {
     const long long per = (long long)nblocks * ksteps * 512;
     if (idx >= per) return;
     const int e = (int)(idx & 7), l = (int)((idx >> 3) & 63);
@@ -756,6 +756,36 @@ __global__ void split_weights_kernel(const float* __restrict__ w, int n, int k, 
         out[((blk * npl + p) << 9) + (l << 3) + e] = __builtin_bit_cast(unsigned short, xh);
         x -= (float)xh;
     }
+}
+
+__global__ void split_weights_kernel(const float* __restrict__ w, int n, int k, long long ldw, int transpose,
+                                     int nblocks, int ksteps, int npl, unsigned short* __restrict__ out) {
+    split_weights_elem(w, n, k, ldw, transpose, nblocks, ksteps, npl, out,
+                       (long long)blockIdx.x * blockDim.x + threadIdx.x);  // one (nb, ks, lane, e)
+}
+
+constexpr int MAXJOBS = 32;
+struct SplitJob {
+    const float* w;
+    unsigned short* out;
+    long long ldw;
+    int n, k, transpose, nblocks, ksteps, npl;
+    int block0;  // first workgroup of this job
+};
+struct SplitBatch {
+    SplitJob j[MAXJOBS];
+    int n;
+};
+
+// every job's workgroups in one grid: a workgroup finds its job by a uniform scan of the starts
+__global__ void split_weights_batch_kernel(SplitBatch b) {
+    int q = 0;
+    for (int t = 1; t < b.n; ++t)
+        if ((int)blockIdx.x >= b.j[t].block0) q = t;
+    // (fields through locals: a per-job select of the argument struct stays in scalar registers)
+    const SplitJob J = b.j[q];
+    split_weights_elem(J.w, J.n, J.k, J.ldw, J.transpose, J.nblocks, J.ksteps, J.npl, J.out,
+                       (long long)(blockIdx.x - J.block0) * blockDim.x + threadIdx.x);
 }
 
 inline int rup(long long x, int a) { return (int)((x + a - 1) / a * a); }
@@ -833,6 +863,38 @@ int anerf_mlp_split_weights(const float* w, int32_t n, int32_t k, int64_t ldw, i
     hipLaunchKernelGGL(split_weights_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
                        reinterpret_cast<hipStream_t>(stream), w, n, k, (long long)ldw, transpose, nblocks, ksteps, npl,
                        static_cast<unsigned short*>(out));
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? ANERF_OK : anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));
+}
+
+int anerf_mlp_split_weights_batch(const anerf_split_job* jobs, int32_t n_jobs, void* stream) {
+    if (!jobs || n_jobs < 1 || n_jobs > MAXJOBS)
+        return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_split_weights_batch: 1 to 32 jobs");
+    SplitBatch b = {};
+    long long blocks = 0;
+    for (int i = 0; i < n_jobs; ++i) {
+        const anerf_split_job& q = jobs[i];
+        const int npl = planes_of(q.precision);
+        if (!q.w || !q.out || q.n < 1 || q.k < 1 || q.ldw < q.k || !npl)
+            return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_split_weights_batch: bad job");
+        const int rows = q.transpose ? q.k : q.n, cols = q.transpose ? q.n : q.k;
+        SplitJob& J = b.j[i];
+        J.w = q.w;
+        J.out = static_cast<unsigned short*>(q.out);
+        J.ldw = q.ldw;
+        J.n = q.n;
+        J.k = q.k;
+        J.transpose = q.transpose;
+        J.nblocks = (rows + BNW - 1) / BNW * (BNW / 32);
+        J.ksteps = (cols + 15) / 16;
+        J.npl = npl;
+        J.block0 = (int)blocks;
+        blocks += ((long long)J.nblocks * J.ksteps * 512 + 255) / 256;
+    }
+    if (blocks > 0x7fffffff) return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_split_weights_batch: too large");
+    b.n = n_jobs;
+    hipLaunchKernelGGL(split_weights_batch_kernel, dim3((unsigned)blocks), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), b);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? ANERF_OK : anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));
 }

@@ -64,6 +64,26 @@ def split_weight(w, transpose=False, prec=6):
     return out
 
 
+def split_weights(jobs, prec):
+    """[(w [n, k], transpose)] -> their bf16 planes (as split_weight), in one launch per 32 weights
+    (anerf_mlp_split_weights_batch)."""
+    lib = _lib.load()
+    outs = []
+    for c0 in range(0, len(jobs), 32):
+        chunk = jobs[c0:c0 + 32]
+        arr = (_lib.SplitJob * len(chunk))()
+        for i, (w, transpose) in enumerate(chunk):
+            n, k = w.shape
+            rows, cols = (k, n) if transpose else (n, k)
+            out = torch.empty(lib.anerf_mlp_split_bytes(rows, cols, prec), device=w.device, dtype=torch.uint8)
+            arr[i].w, arr[i].n, arr[i].k, arr[i].ldw = w.data_ptr(), n, k, w.stride(0)
+            arr[i].transpose, arr[i].precision, arr[i].out = int(transpose), prec, out.data_ptr()
+            outs.append(out)
+        _lib.check(lib.anerf_mlp_split_weights_batch(arr, len(chunk), _stream(chunk[0][0].device)),
+                   "anerf_mlp_split_weights_batch")
+    return outs
+
+
 def gemm(m, n, k, a, b_split, bias, relu, outs, dev, prec=6):
     sa, na = _segs(a)
     so, no = _osegs(outs)
@@ -89,13 +109,13 @@ class _MLP(torch.autograd.Function):
         M, F = feat.shape
         nl = D
 
-        def sw(w, t=False):
-            return split_weight(w, t, prec)
-
         def mm(*a):
             gemm(*a, prec=prec)
         pw, pb = params[0:2 * nl:2], params[1:2 * nl:2]
         wa, ba, wf, bf, wv, bv, wr, br = params[2 * nl:2 * nl + 8]
+        whead = torch.cat([wf, wa]).contiguous()
+        # every layer's planes in one launch: [trunk..., head, views, rgb]
+        sp = split_weights([(w, False) for w in pw] + [(whead, False), (wv, False), (wr, False)], prec)
         cfc = 0 if codes is None else codes.shape[1]
         f32 = dict(device=dev, dtype=torch.float32)
         segx = _seg(feat, dnet)
@@ -108,21 +128,20 @@ class _MLP(torch.autograd.Function):
             else:
                 a, k = [_seg(H[-1], W)], W
             h = torch.empty(M, W, **f32)
-            mm(M, W, k, a, sw(pw[i]), pb[i], True, [(h, W, W, 0, None, False)], dev)
+            mm(M, W, k, a, sp[i], pb[i], True, [(h, W, W, 0, None, False)], dev)
             H.append(h)
         # feature_linear + alpha_linear as one GEMM (alpha in raw[:, 3]); no activation
         raw = torch.empty(M, 4, **f32)
         hf = torch.empty(M, W, **f32)
-        whead = torch.cat([wf, wa]).contiguous()
         bhead = torch.cat([bf, ba]).contiguous()
-        mm(M, W + 1, W, [_seg(H[-1], W)], sw(whead), bhead, False,
+        mm(M, W + 1, W, [_seg(H[-1], W)], sp[D], bhead, False,
              [(hf, W, W, 0, None, False), (raw, 4, 1, 3, None, False)], dev)
         # views_linears[0] on cat([feature, views(, framecode)]), relu
         av = [_seg(hf, W), _seg(feat, nv, dnet)] + ([_seg(codes, cfc)] if cfc else [])
         g = torch.empty(M, W // 2, **f32)
-        mm(M, W // 2, W + nv + cfc, av, sw(wv), bv, True, [(g, W // 2, W // 2, 0, None, False)], dev)
+        mm(M, W // 2, W + nv + cfc, av, sp[D + 1], bv, True, [(g, W // 2, W // 2, 0, None, False)], dev)
         # rgb_linear into raw[:, :3]
-        mm(M, 3, W // 2, [_seg(g, W // 2)], sw(wr), br, False, [(raw, 4, 3, 0, None, False)], dev)
+        mm(M, 3, W // 2, [_seg(g, W // 2)], sp[D + 2], br, False, [(raw, 4, 3, 0, None, False)], dev)
         ctx.shape = shape
         ctx.has_codes = codes is not None
         ctx.save_for_backward(feat, codes if codes is not None else torch.empty(0), hf, g, whead, *H, *params)
@@ -131,9 +150,6 @@ class _MLP(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g_raw):
         W, D, skip, dnet, nv, _, prec = ctx.shape  # (the backward's own arithmetic)
-
-        def sw(w, t=False):
-            return split_weight(w, t, prec)
 
         def mm(*a):
             gemm(*a, prec=prec)
@@ -150,6 +166,10 @@ class _MLP(torch.autograd.Function):
         cfc = 0 if codes is None else codes.shape[1]
         need_feat = ctx.needs_input_grad[1]
         need_codes = ctx.has_codes and ctx.needs_input_grad[2]
+        # every transposed plane in one launch: [trunk (layer 0 only for the feature gradient)..., head, views, rgb]
+        st = split_weights([(w, True) for w in pw[0 if need_feat else 1:]] + [(whead, True), (wv, True), (wr, True)],
+                           prec)
+        st = ([None] if not need_feat else []) + st
         f32 = dict(device=dev, dtype=torch.float32)
         g_raw = g_raw.contiguous()
         lib = _lib.load()
@@ -167,7 +187,7 @@ class _MLP(torch.autograd.Function):
 
         # rgb_linear: input gradient masked by relu(view layer) > 0
         gzv = torch.empty(M, W // 2, **f32)
-        mm(M, W // 2, 3, [_seg(g_raw, 3)], sw(wr, True), None, False,
+        mm(M, W // 2, 3, [_seg(g_raw, 3)], st[D + 2], None, False,
              [(gzv, W // 2, W // 2, 0, g, False)], dev)
         grads[2 * nl + 6], grads[2 * nl + 7] = wg(3, W // 2, g_raw, [_seg(g, W // 2)])
         # views_linears[0]: gradients of feature (into gha[:, :W]), view columns of feat, framecodes
@@ -180,13 +200,13 @@ class _MLP(torch.autograd.Function):
         if cfc:
             outs.append((gcodes, cfc, cfc, 0, None, False))
         nvo = W + (nv + cfc if (need_feat or need_codes) else 0)
-        mm(M, nvo, W // 2, [_seg(gzv, W // 2)], sw(wv, True), None, False,
+        mm(M, nvo, W // 2, [_seg(gzv, W // 2)], st[D + 1], None, False,
              outs if nvo > W else outs[:1], dev)
         av = [_seg(hf, W), _seg(feat, nv, dnet)] + ([_seg(codes, cfc)] if cfc else [])
         grads[2 * nl + 4], grads[2 * nl + 5] = wg(W // 2, W + nv + cfc, gzv, av)
         # feature_linear + alpha_linear: one input gradient, masked by relu(last hidden) > 0
         gz = torch.empty(M, W, **f32)
-        mm(M, W, W + 1, [_seg(gha, W + 1)], sw(whead, True), None, False,
+        mm(M, W, W + 1, [_seg(gha, W + 1)], st[D], None, False,
              [(gz, W, W, 0, H[-1], False)], dev)
         dwh, dbh = wg(W + 1, W, gha, [_seg(H[-1], W)])
         grads[2 * nl + 2], grads[2 * nl + 3] = dwh[:W], dbh[:W]  # feature_linear
@@ -204,17 +224,17 @@ class _MLP(torch.autograd.Function):
             grads[2 * i], grads[2 * i + 1] = wg(W, k, gz, a)
             if i == 0:
                 if need_feat:
-                    mm(M, dnet, W, [_seg(gz, W)], sw(pw[0], True), None, False,
+                    mm(M, dnet, W, [_seg(gz, W)], st[0], None, False,
                          [(gfeat, F, dnet, 0, None, wrote_x)], dev)
                 break
             gprev = torch.empty(M, W, **f32)
             if i - 1 == skip:  # [x | h] input: the x part into the feature gradient, the h part masked
-                mm(M, k, W, [_seg(gz, W)], sw(pw[i], True), None, False,
+                mm(M, k, W, [_seg(gz, W)], st[i], None, False,
                      [(gfeat if need_feat else None, F, dnet, 0, None, False), (gprev, W, W, 0, H[i - 1], False)],
                      dev)
                 wrote_x = need_feat
             else:
-                mm(M, W, W, [_seg(gz, W)], sw(pw[i], True), None, False,
+                mm(M, W, W, [_seg(gz, W)], st[i], None, False,
                      [(gprev, W, W, 0, H[i - 1], False)], dev)
             gz = gprev
         return (None, gfeat, gcodes, *grads)
@@ -246,4 +266,4 @@ def nerf_forward(net, feat, codes=None):
     return _MLP.apply(shape, feat, codes, *params)
 
 
-__all__ = ["nerf_forward", "split_weight", "gemm", "wgrad"]
+__all__ = ["nerf_forward", "split_weight", "split_weights", "gemm", "wgrad"]

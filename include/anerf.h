@@ -39,6 +39,7 @@
  * The training MLP's linears (NeRF.forward / autograd, core/networks/nerf.py:94-148; the reference runs
  * them as torch addmm over cat()-ed inputs, core/raycasters.py:557-577):
  *   anerf_mlp_split_weights a weight (or its transpose) as bf16 hi / lo planes, once per step
+ *   anerf_mlp_split_weights_batch   the same for up to 32 weights in one launch
  *   anerf_mlp_gemm          forward (bias, relu) and input-gradient (relu' mask, accumulate) products
  *   anerf_mlp_wgrad         weight + bias gradients
  */
@@ -52,7 +53,7 @@
 extern "C" {
 #endif
 
-#define ANERF_ABI_VERSION 7
+#define ANERF_ABI_VERSION 8
 
 enum {
     ANERF_OK = 0,
@@ -382,6 +383,16 @@ size_t anerf_mlp_split_bytes(int32_t rows, int32_t cols, int32_t precision);
  * ([k][n], the B operand of an input gradient).  out: anerf_mlp_split_bytes(rows, cols) bytes. */
 int anerf_mlp_split_weights(const float* w, int32_t n, int32_t k, int64_t ldw, int32_t transpose,
                             int32_t precision, void* out, void* stream);
+/* One anerf_mlp_split_weights call of a batch. */
+typedef struct {
+    const float* w;
+    int32_t n, k;
+    int64_t ldw;
+    int32_t transpose, precision;
+    void* out;
+} anerf_split_job;
+/* Up to 32 anerf_mlp_split_weights in one launch (a network's layers: forward or transposed). */
+int anerf_mlp_split_weights_batch(const anerf_split_job* jobs, int32_t n_jobs, void* stream);
 /* C[m][n] = act(sum_k A[m][k] B[n][k] + bias[n]); A: n_a segments adding up to k columns; B: split
  * [n][k] (the forward's weight, or the transposed weight of an input gradient); bias NULL or [n];
  * relu != 0 applies max(., 0); C: n_c segments adding up to n columns. */

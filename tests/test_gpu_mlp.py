@@ -37,6 +37,22 @@ def _bound(a, b, prec=3):
 
 
 @pytest.mark.parametrize("prec", [3, 6])
+def test_split_weights_batch_matches_single(prec):
+    """anerf_mlp_split_weights_batch writes byte-identical planes to one anerf_mlp_split_weights per job
+    (ragged shapes, strided rows, both orientations, more than one 32-job launch)."""
+    torch.manual_seed(prec)
+    shapes = [(256, 432), (3, 128), (257, 256), (1, 1), (128, 904), (33, 17)] * 6
+    jobs = []
+    for i, (n, k) in enumerate(shapes):
+        w = torch.randn(n, k + 3, device=DEV)[:, :k]  # ldw = k + 3
+        jobs.append((w, bool(i % 2)))
+    outs = mlp.split_weights(jobs, prec)
+    assert len(outs) == len(jobs)
+    for (w, t), o in zip(jobs, outs):
+        assert torch.equal(o, mlp.split_weight(w, t, prec))
+
+
+@pytest.mark.parametrize("prec", [3, 6])
 @pytest.mark.parametrize("m,n,ks", [(1000, 257, (256, 648, 16)), (4096, 256, (432, 256)), (77, 3, (128,)),
                                     (130, 128, (904,)), (0, 64, (32,))])
 def test_gemm_forward_segments_bias_relu(m, n, ks, prec):

@@ -33,6 +33,8 @@ def parser():
     ap.add_argument("--importance", type=int, default=16)
     ap.add_argument("--mlp", default="mixed", choices=["mixed", "bf16x6", "bf16x3", "fp32"],
                     help="training MLP arithmetic (train.TrainRayCaster mlp=)")
+    ap.add_argument("--split-single", action="store_true",
+                    help="ablation: one split launch per weight instead of the batched split")
     return ap
 
 
@@ -42,6 +44,9 @@ def measure(a, dev=None):
     syn = importlib.import_module("a-nerf_amd.synthetic")
     train = importlib.import_module("a-nerf_amd.train")
     dev = dev or torch.device("cuda:0")
+    if getattr(a, "split_single", False):
+        mlp = importlib.import_module("a-nerf_amd.mlp")
+        mlp.split_weights = lambda jobs, prec: [mlp.split_weight(w, t, prec) for w, t in jobs]
     S, I, n = a.samples, a.importance, a.rays
     cfg = anerf.RenderConfig(N_samples=S, N_importance=I).validate()
     ck = syn.make_checkpoint(13, n_joints=24, D=8, W=256, fine=True, tau=20.0)
