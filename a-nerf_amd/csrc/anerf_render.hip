@@ -94,9 +94,9 @@ int anerf_model_create(const anerf_model_desc* desc, const anerf_net_weights* co
     const size_t bytes = pk.buf.size() * sizeof(float);
     hipError_t e = hipMalloc(&dbuf, bytes);
     if (e == hipSuccess) e = hipMemcpy(dbuf, pk.buf.data(), bytes, hipMemcpyHostToDevice);
-    hipSetDevice(prev);
+    (void)hipSetDevice(prev);  // restoring the caller's device; the upload's own error is the one reported
     if (e != hipSuccess) {
-        if (dbuf) hipFree(dbuf);
+        if (dbuf) (void)hipFree(dbuf);
         return fail(ANERF_EHIP, std::string("weight upload: ") + hipGetErrorString(e));
     }
     anerf_model* m = new anerf_model();
@@ -146,8 +146,9 @@ int anerf_model_create(const anerf_model_desc* desc, const anerf_net_weights* co
 
 int anerf_model_destroy(anerf_model* m) {
     if (!m) return ANERF_OK;
-    if (m->dev_buf) hipFree(m->dev_buf);
+    const hipError_t e = m->dev_buf ? hipFree(m->dev_buf) : hipSuccess;
     delete m;
+    if (e != hipSuccess) return fail(ANERF_EHIP, std::string("anerf_model_destroy: ") + hipGetErrorString(e));
     return ANERF_OK;
 }
 
@@ -165,7 +166,7 @@ int anerf_model_set_embed(anerf_model* m, const anerf_embed_params* embed) {
             e = hipMemcpy(const_cast<float*>(m->md.cutoff), embed->cutoff_dist, nb, hipMemcpyHostToDevice);
         if (e == hipSuccess && embed->cutoff_dist_v)
             e = hipMemcpy(const_cast<float*>(m->md.cutoff_v), embed->cutoff_dist_v, nb, hipMemcpyHostToDevice);
-        hipSetDevice(prev);
+        (void)hipSetDevice(prev);
         if (e != hipSuccess) return fail(ANERF_EHIP, std::string("anerf_model_set_embed: ") + hipGetErrorString(e));
     }
     m->md.tau = embed->tau;
