@@ -151,7 +151,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = world > 1
+    # an explicit --shard pixels under torch.distributed.run also takes the RCCL path at one rank, so a
+    # one-GPU box rehearses the N > 1 data path (ray ids, all-gather, compose) the driver's scaling run uses
+    dist = world > 1 or (a.shard == "pixels" and "MASTER_ADDR" in os.environ)
     shard = a.shard or ("pixels" if dist else "frames")
     pixels = shard == "pixels"
     if a.res is None:
