@@ -325,9 +325,10 @@ def main():
         # disp = 1 / max(1e-10, depth / acc) is a ratio of two sums of alpha = 1 - exp(-sigma delta), which
         # fp32 quantises to multiples of 2^-24 on a near-empty ray: there ulp-level raw differences decide
         # which samples carry the 2^-24 and move disp by up to 1e-3 in any two fp32 implementations of the
-        # reference (tools/diag_disp.py). Such rays (acc < 2^-20) are counted and their disp
-        # error reported, not held to 1e-4; every other output of every ray is.
-        empty = ref["acc_map"] < 2.0 ** -20
+        # reference (tools/diag_disp.py). Such rays (0 < acc < 2^-20) are counted and their disp
+        # error reported, not held to 1e-4; every other output of every ray is
+        # (rays that miss the body, acc = 0, stay in the strict check)
+        empty = (ref["acc_map"] > 0) & (ref["acc_map"] < 2.0 ** -20)
         errs = {k: float(v[~empty].max() if k == "disp_map" and empty.any() and (~empty).any() else v.max()) for k, v in diff.items()}
         parity = {"rays": int(len(sel)), "max_abs_err": {k: float(f"{v:.3e}") for k, v in errs.items()},
                   "near_empty_rays": int(empty.sum()),
