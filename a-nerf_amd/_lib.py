@@ -23,6 +23,7 @@ ANERF_PREC_BF16X3 = 1
 ANERF_PREC_BF16X6 = 2
 ANERF_PREC_FP16X3 = 3
 ANERF_FLAG_LINDISP = 0x100  # OR-ed into the precision argument (include/anerf.h)
+ANERF_FLAG_NEAR_FAR = 0x200  # ray_batch columns 6, 7 hold the filled near / far (anerf_render_rays)
 MLP_PRECISIONS = {"bf16x3": 3, "bf16x6": 6}  # ANERF_MLP_BF16X3 / _BF16X6 (training MLP GEMMs)
 PRECISIONS = {"fp32": ANERF_PREC_FP32, "bf16x3": ANERF_PREC_BF16X3, "bf16x6": ANERF_PREC_BF16X6,
               "fp16x3": ANERF_PREC_FP16X3}

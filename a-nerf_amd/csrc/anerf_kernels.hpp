@@ -221,6 +221,15 @@ __global__ __launch_bounds__(256, 1) void density_kernel(ModelDev M, DensityArgs
 }
 
 // ======================================================================= small kernels
+// ANERF_FLAG_NEAR_FAR: the caller's filled near / far (ray_batch columns 6, 7) into the workspace
+__global__ void near_far_given_kernel(const float* __restrict__ rb, int stride, int64_t n, float* __restrict__ near_out,
+                                      float* __restrict__ far_out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    near_out[i] = rb[i * stride + 6];
+    far_out[i] = rb[i * stride + 7];
+}
+
 __global__ void near_far_kernel(const float* __restrict__ rb, int stride, int64_t n, const float* __restrict__ cyls,
                                 const int32_t* __restrict__ ray_pose, int n_poses, float* __restrict__ near_out,
                                 float* __restrict__ far_out, uint8_t* __restrict__ qnan) {

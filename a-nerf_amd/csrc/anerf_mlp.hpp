@@ -412,13 +412,15 @@ __device__ __forceinline__ float pow2f(int e) { return __builtin_bit_cast(float,
 
 // values a, b (relu'd, in the input's units) times t -> dword q of the two fp16 components: the high
 // part rounds x to 11 significant bits in the f32 encoding (exact in fp16), the low part is the
-// exact remainder rounded toward zero to fp16
+// exact remainder rounded to nearest even (v_cvt_pk_f16_f32), so x0 + x1 is within 2^-23 |x| of x
+// (a quarter of the values are not exact: the remainder can need 12 bits)
 __device__ __forceinline__ void split2_pair(float a, float b, float t, H3T& T, int q) {
+    typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
     const float xa = a * t, xb = b * t;
     const float ha = __builtin_bit_cast(float, (__builtin_bit_cast(unsigned, xa) + 0x1000u) & 0xffffe000u);
     const float hb = __builtin_bit_cast(float, (__builtin_bit_cast(unsigned, xb) + 0x1000u) & 0xffffe000u);
     T.d[0][q] = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_pkrtz(ha, hb));
-    T.d[1][q] = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_pkrtz(xa - ha, xb - hb));
+    T.d[1][q] = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2{xa - ha, xb - hb}), f16x2));
 }
 
 __device__ __forceinline__ void split2_block_pair(const f32x16& hb, float t, H3T (&T)[2], int p) {

@@ -247,7 +247,8 @@ int anerf_render_rays(const anerf_model* m, const float* ray_batch, int32_t ray_
     if (n_rays == 0) return ANERF_OK;
     const int flags = precision & ~0xff;  // ANERF_FLAG_* bits above the precision mode
     precision &= 0xff;
-    if (flags & ~ANERF_FLAG_LINDISP) return fail(ANERF_EINVAL, "unknown flags in the precision argument");
+    if (flags & ~(ANERF_FLAG_LINDISP | ANERF_FLAG_NEAR_FAR))
+        return fail(ANERF_EINVAL, "unknown flags in the precision argument");
     if (precision < ANERF_PREC_FP32 || precision > ANERF_PREC_FP16X3) return fail(ANERF_EINVAL, "unsupported precision");
     if (!ray_batch || ray_stride < 8 || !skts || !cyls || n_poses < 1 || !rgb || !disp || !acc)
         return fail(ANERF_EINVAL, "anerf_render_rays: bad arguments");
@@ -266,9 +267,18 @@ int anerf_render_rays(const anerf_model* m, const float* ray_batch, int32_t ray_
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
 
     float *nearp, *farp;
-    int rc = launch_near_far(ray_batch, ray_stride, n_rays, cyls, ray_pose, n_poses, chunk, (char*)workspace, &nearp,
-                             &farp, st);
-    if (rc) return rc;
+    if (flags & ANERF_FLAG_NEAR_FAR) {  // near / far given in columns 6, 7: into the workspace as they are
+        auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+        nearp = reinterpret_cast<float*>(workspace);
+        farp = reinterpret_cast<float*>((char*)workspace + al(sizeof(float) * n_rays));
+        hipLaunchKernelGGL(near_far_given_kernel, dim3((unsigned)((n_rays + 255) / 256)), dim3(256), 0, st, ray_batch,
+                           ray_stride, n_rays, nearp, farp);
+        HIP_TRY(hipGetLastError());
+    } else {
+        int rc = launch_near_far(ray_batch, ray_stride, n_rays, cyls, ray_pose, n_poses, chunk, (char*)workspace,
+                                 &nearp, &farp, st);
+        if (rc) return rc;
+    }
     if (debug && debug->near) HIP_TRY(hipMemcpyAsync(debug->near, nearp, 4 * n_rays, hipMemcpyDeviceToDevice, st));
     if (debug && debug->far) HIP_TRY(hipMemcpyAsync(debug->far, farp, 4 * n_rays, hipMemcpyDeviceToDevice, st));
 

@@ -9,10 +9,13 @@ the outputs on GPU 0 — and its chunk-coupled NaN fill then depends on the GPU 
   frames r, r+N, ... with no collective in the data path; `gather_frames` optionally
   all-gathers finished frames afterwards;
 * `pixels` mode (one frame's latency): the frame's bounding-box ray list is cut into
-  contiguous ranges of whole `chunk`-ray chunks (so the per-chunk NaN fill is exactly the
-  single-GPU one), each rank renders its range, and one all-gather of (rgb, disp, acc)
-  assembles the ray outputs on every rank before composition.  Results are bit-identical to
-  the single-GPU render.
+  contiguous ranges, each rank renders its range, and one all-gather of (rgb, disp, acc)
+  assembles the ray outputs on every rank before composition.  Two balancings:
+  `chunks` — ranges of whole `chunk`-ray chunks (chunk_ranges), so each rank's own NaN fill is
+  the single-GPU one; `rays` — equal ray counts (ray_ranges; 209 chunks over 8 ranks are 27 vs
+  26.1 on average, a 3.4 % imbalance), each rank computing near / far over the whole chunks
+  that cover its range (chunk_cover) and rendering its rays with those (ANERF_FLAG_NEAR_FAR).
+  Results are bit-identical to the single-GPU render either way.
 The render function is injectable (default: the HIP RayCaster) so the sharding and collective
 logic is tested with gloo on CPU.
 """
@@ -29,6 +32,18 @@ def chunk_ranges(n_rays, chunk, world):
         c1 = ((r + 1) * n_chunks) // world
         out.append((min(c0 * chunk, n_rays), min(c1 * chunk, n_rays)))
     return out
+
+
+def ray_ranges(n_rays, world):
+    """Contiguous [start, stop) ray ranges balanced by ray count."""
+    return [((r * n_rays) // world, ((r + 1) * n_rays) // world) for r in range(world)]
+
+
+def chunk_cover(s0, s1, chunk, n_rays):
+    """The whole-chunk range [c0, c1) that contains rays [s0, s1) (the rays whose NaN fill they share)."""
+    if s1 <= s0:
+        return s0, s0
+    return (s0 // chunk) * chunk, min(((s1 + chunk - 1) // chunk) * chunk, n_rays)
 
 
 def frame_ids(n_frames, rank, world):
@@ -50,14 +65,25 @@ def all_gather_rows(t, group=None):
     return torch.cat([b[:s] for b, s in zip(bufs, sizes)], 0)
 
 
-def render_rays_sharded(render_fn, ray_batch, chunk, group=None):
-    """Pixel sharding of one ray list: rank r renders its whole-chunk range, then one all-gather
-    of [rgb(3), disp, acc] per ray.  render_fn(ray_slice) -> dict(rgb_map, disp_map, acc_map)."""
+def render_rays_sharded(render_fn, ray_batch, chunk, group=None, near_far_fn=None):
+    """Pixel sharding of one ray list, then one all-gather of [rgb(3), disp, acc] per ray.
+    Without near_far_fn: rank r renders its whole-chunk range, render_fn(ray_slice) ->
+    dict(rgb_map, disp_map, acc_map).  With near_far_fn(rays) -> (near, far) (the chunk NaN fill over
+    the given rays, e.g. raycaster.near_far): ray-balanced ranges; the rank fills near / far over
+    the whole chunks covering its range and calls render_fn(ray_slice, near, far)."""
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     n = ray_batch.shape[0]
-    s0, s1 = chunk_ranges(n, chunk, world)[rank]
+    if near_far_fn is None:
+        s0, s1 = chunk_ranges(n, chunk, world)[rank]
+    else:
+        s0, s1 = ray_ranges(n, world)[rank]
     if s1 > s0:
-        out = render_fn(ray_batch[s0:s1])
+        if near_far_fn is None:
+            out = render_fn(ray_batch[s0:s1])
+        else:
+            c0, c1 = chunk_cover(s0, s1, chunk, n)
+            near, far = near_far_fn(ray_batch[c0:c1])
+            out = render_fn(ray_batch[s0:s1], near[s0 - c0:s1 - c0], far[s0 - c0:s1 - c0])
         local = torch.cat([out["rgb_map"].reshape(-1, 3), out["disp_map"].reshape(-1, 1),
                            out["acc_map"].reshape(-1, 1)], -1).contiguous()
     else:
@@ -70,10 +96,11 @@ class ShardGather:
     """The all-gather of render_rays_sharded with its sizes fixed up front (chunk_ranges is known on
     every rank): per call ONE all_gather_into_tensor of a [world * m, 5] buffer (m = the largest
     range) and one row gather that drops the padding — no size exchange, no host sync.
+    `ranges`: the ranks' [start, stop) (default chunk_ranges; ray_ranges for ray-balanced sharding).
     __call__(out) -> dict(rgb_map, disp_map, acc_map) of the whole ray list, ray order."""
 
-    def __init__(self, n_rays, chunk, world, device, group=None):
-        self.ranges = chunk_ranges(n_rays, chunk, world)
+    def __init__(self, n_rays, chunk, world, device, group=None, ranges=None):
+        self.ranges = ranges if ranges is not None else chunk_ranges(n_rays, chunk, world)
         self.m = max(max(s1 - s0 for s0, s1 in self.ranges), 1)
         self.group = group
         rows = [torch.arange(r * self.m, r * self.m + (s1 - s0)) for r, (s0, s1) in enumerate(self.ranges)]

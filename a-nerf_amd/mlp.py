@@ -257,13 +257,45 @@ def nerf_forward(net, feat, codes=None):
     W, D = cfg.netwidth, cfg.netdepth
     skip = cfg.skips[0] if cfg.skips[0] < D - 1 else -1
     fwd, bwd = MODES[net.mlp]
-    shape = (W, D, skip, net.dnet, cfg.input_ch_views, fwd, bwd)
+    dnet, nv = net.dnet, cfg.input_ch_views
     params = []
     for lin in net.pts_linears:
         params += [lin.weight, lin.bias]
     params += [net.alpha_linear.weight, net.alpha_linear.bias, net.feature_linear.weight, net.feature_linear.bias,
                net.views_linears[0].weight, net.views_linears[0].bias, net.rgb_linear.weight, net.rgb_linear.bias]
+    if dnet % 4 or nv % 4 or feat.shape[1] % 4:
+        feat, params, dnet, nv = _pad_to_segments(feat, params, W, D, skip, dnet, nv)
+    shape = (W, D, skip, dnet, nv, fwd, bwd)
     return _MLP.apply(shape, feat, codes, *params)
+
+
+def _ceil4(x):
+    return (x + 3) // 4 * 4
+
+
+def _pad_to_segments(feat, params, W, D, skip, dnet, nv):
+    """The GEMMs read operand segments as 16-byte float4 groups (anerf_gemm.hip set_segs): every
+    segment starts 16-byte aligned, rows have ld % 4 == 0 and a segment followed by another has
+    cols % 4 == 0.  The encoder's rows [x (18 NJ) | views (27 NJ)] meet that only for NJ % 4 == 0, so
+    other joint counts (17, 65, ...) run on a copy whose x and view blocks are zero-padded to
+    multiples of 4 columns, with zero weight columns inserted where the padding enters (layer 0, the
+    skip layer's x part, the view layer's view part).  The padded products are the same sums plus
+    exact zeros; torch autograd carries the gradients back through the pads to feat and the
+    unpadded parameters."""
+    d4, v4 = _ceil4(dnet), _ceil4(nv)
+    M = feat.shape[0]
+    z = lambda c: feat.new_zeros(M, c)  # noqa: E731
+    featp = torch.cat([feat[:, :dnet], z(d4 - dnet), feat[:, dnet:dnet + nv], z(v4 - nv)], 1).contiguous()
+
+    def pad_cols(w, at, n):
+        return torch.cat([w[:, :at], w.new_zeros(w.shape[0], n), w[:, at:]], 1).contiguous() if n else w
+    params = list(params)
+    params[0] = pad_cols(params[0], dnet, d4 - dnet)  # layer 0: [W][dnet]
+    if skip >= 0:
+        params[2 * (skip + 1)] = pad_cols(params[2 * (skip + 1)], dnet, d4 - dnet)  # [x | h]
+    iv = 2 * D + 4  # views_linears.0: [feature (W) | views (nv) | framecode]
+    params[iv] = pad_cols(params[iv], W + nv, v4 - nv)
+    return featp, params, d4, v4
 
 
 __all__ = ["nerf_forward", "split_weight", "split_weights", "gemm", "wgrad"]

@@ -139,11 +139,14 @@ class RayCaster:
                     subject_idxs=None, retraw=False, lindisp=False, perturb=0., N_importance=0, network_fine=None,
                     raw_noise_std=0., ray_noise_std=0., verbose=False, ext_scale=0.001, pytest=False,
                     preproc_kwargs=None, nerf_type="nerf", chunk=None, debug=False, ret_alpha=True,
-                    count_mfma=False):
+                    count_mfma=False, near_far_given=False):
         """Same arguments and output dict as core/raycasters.py:361-474.
 
         `chunk` (extension): NaN-fill granularity; the reference fills per render_rays call,
-        i.e. per batchify chunk, so the default is the whole batch."""
+        i.e. per batchify chunk, so the default is the whole batch.
+        `near_far_given` (extension): ray_batch[:, 6:8] already hold the rays' near / far after the
+        cylinder intersection and the chunk NaN fill (near_far() over the chunks that contain them),
+        so any sub-range of a chunked ray list renders as in the whole list (ANERF_FLAG_NEAR_FAR)."""
         if perturb or raw_noise_std or ray_noise_std:
             raise NotImplementedError("stochastic sampling / noise (training mode) is not implemented")
         if subject_idxs is not None:
@@ -205,7 +208,8 @@ class RayCaster:
         rc = _lib.load().anerf_render_rays(
             self.model.handle, _lib.ptr(rb), rb.shape[1], n, _lib.ptr(skt_tab), _lib.ptr(cyl_tab),
             skt_tab.shape[0], _lib.ptr(pose), _lib.ptr(cam_t), S, I, int(chunk or max(n, 1)),
-            _lib.PRECISIONS[self.cfg.precision] | (_lib.ANERF_FLAG_LINDISP if lindisp else 0),
+            _lib.PRECISIONS[self.cfg.precision] | (_lib.ANERF_FLAG_LINDISP if lindisp else 0)
+            | (_lib.ANERF_FLAG_NEAR_FAR if near_far_given else 0),
             _lib.ptr(out["rgb_map"]), _lib.ptr(out["disp_map"]), _lib.ptr(out["acc_map"]),
             _lib.ptr(out.get("rgb0")), _lib.ptr(out.get("disp0")), _lib.ptr(out.get("acc0")),
             _lib.ptr(out["alpha"]), _lib.ptr(out.get("alpha0")), ctypes.byref(dbg) if dbg else None,
@@ -215,6 +219,31 @@ class RayCaster:
             out.pop("alpha")
             out.pop("alpha0", None)
         return out
+
+
+def near_far(ray_batch, cyls, chunk=None, out=None):
+    """get_near_far_in_cylinder + the chunk NaN fill (core/utils/ray_utils.py:292-344) of a ray list on
+    the device (anerf_near_far): near / far [n] of every ray, the fill over consecutive `chunk`-ray
+    chunks (default: the whole list).  cyls: [5], [1, 5] (one pose) or [n, 5] per ray.  `out` =
+    (near, far) tensors to fill, e.g. strided views of a ray batch's columns 6 and 7."""
+    rb = ray_batch
+    dev = rb.device
+    if rb.dtype != torch.float32 or rb.stride(-1) != 1 or rb.stride(0) != rb.shape[1]:
+        rb = rb.to(torch.float32).contiguous()
+    n = rb.shape[0]
+    cyl_tab, pose = _pose_table(cyls.to(dev), n, (5,))
+    nearv = torch.empty(n, device=dev, dtype=torch.float32)
+    farv = torch.empty(n, device=dev, dtype=torch.float32)
+    if n:
+        ws = torch.empty(13 * n + 1024, device=dev, dtype=torch.uint8)  # (ws_near_far_bytes, anerf_render.hip)
+        _lib.check(_lib.load().anerf_near_far(_lib.ptr(rb), rb.shape[1], n, _lib.ptr(cyl_tab), cyl_tab.shape[0],
+                                              _lib.ptr(pose), int(chunk or max(n, 1)), _lib.ptr(nearv),
+                                              _lib.ptr(farv), _lib.ptr(ws), ws.numel(), _lib.stream_handle(dev)),
+                   "anerf_near_far")
+    if out is not None:
+        out[0].copy_(nearv)
+        out[1].copy_(farv)
+    return nearv, farv
 
 
 def load_checkpoint(path):

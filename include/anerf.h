@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define ANERF_ABI_VERSION 8
+#define ANERF_ABI_VERSION 9
 
 enum {
     ANERF_OK = 0,
@@ -84,8 +84,14 @@ enum {
 enum { ANERF_PREC_FP32 = 0, ANERF_PREC_BF16X3 = 1, ANERF_PREC_BF16X6 = 2, ANERF_PREC_FP16X3 = 3 };
 /* Flags OR-ed into anerf_render_rays' precision argument (and anerf_train_samples' flags):
  *   ANERF_FLAG_LINDISP  sample linearly in inverse depth, z = 1 / (1/near (1 - t) + 1/far t)
- *                       (render_rays(lindisp=True), core/utils/ray_utils.py:223-226) */
-enum { ANERF_FLAG_LINDISP = 0x100 };
+ *                       (render_rays(lindisp=True), core/utils/ray_utils.py:223-226)
+ *   ANERF_FLAG_NEAR_FAR (anerf_render_rays only) ray_batch columns 6 and 7 already hold every ray's
+ *                       near / far AFTER get_near_far_in_cylinder and its chunk NaN fill
+ *                       (core/utils/ray_utils.py:292-344), e.g. anerf_near_far's outputs over the
+ *                       whole chunks that contain the rays: the kernel uses them as they are (cyls
+ *                       and chunk are then not read).  Lets a rank render any sub-range of a chunked
+ *                       ray list with the single-GPU NaN fill (ray-balanced sharding). */
+enum { ANERF_FLAG_LINDISP = 0x100, ANERF_FLAG_NEAR_FAR = 0x200 };
 
 typedef struct anerf_model anerf_model;
 
@@ -154,7 +160,9 @@ typedef struct {
     float* raw_fine;  /* [N][S+I][4] */
     unsigned long long* mfma_count; /* [2] += MFMA instructions issued, a kernel-side tally of the
                                        work (agrees with PMC SQ_INSTS_MFMA): [0] v_mfma_f32_32x32x2_f32,
-                                       [1] v_mfma_f32_32x32x16_bf16 (bf16x3 / bf16x6 modes) */
+                                       [1] the 16-bit MFMAs, v_mfma_f32_32x32x16_bf16 (bf16x3 / bf16x6
+                                       modes, and the bf16x6 bone-direction parts of fp16x3) and
+                                       v_mfma_f32_32x32x16_f16 (fp16x3), the same FLOPs and cycles each */
 } anerf_debug;
 
 int anerf_abi_version(void);

@@ -52,6 +52,24 @@ def _worker(rank, world, port, q):
         sg = D.ShardGather(rb.shape[0], 4096, world, torch.device("cpu"))(render_fn(rb[s0:s1]))
         for k in out:
             assert torch.equal(sg[k], out[k]), k
+
+        # ray-balanced ranges (rank 1 starts mid-chunk): near / far filled over the covering chunks
+        def near_far_fn(rays):
+            near, far, _, _ = om.near_far(rays.numpy(), g["cyls"][0:1], chunk=4096)
+            return torch.from_numpy(near), torch.from_numpy(far)
+
+        def render_nf(sl, near, far):
+            o = om.render_rays(sl.numpy(), g["skts"][0], g["cyls"][0:1], chunk=4096, near=near.numpy(),
+                               far=far.numpy())
+            return {k: torch.from_numpy(v) for k, v in o.items()}
+        outb = D.render_rays_sharded(render_nf, rb, chunk=4096, near_far_fn=near_far_fn)
+        r0, r1 = D.ray_ranges(rb.shape[0], world)[rank]
+        c0, c1 = D.chunk_cover(r0, r1, 4096, rb.shape[0])
+        nf = near_far_fn(rb[c0:c1])
+        sgb = D.ShardGather(rb.shape[0], 4096, world, torch.device("cpu"), ranges=D.ray_ranges(rb.shape[0], world))(
+            render_nf(rb[r0:r1], nf[0][r0 - c0:r1 - c0], nf[1][r0 - c0:r1 - c0]))
+        for k in out:
+            assert torch.equal(outb[k], out[k]) and torch.equal(sgb[k], out[k]), k
         frames = torch.arange(5 * 4 * 4 * 3, dtype=torch.float32).reshape(5, 4, 4, 3)
         mine = frames[D.frame_ids(5, rank, world)]
         full = D.gather_frames(mine, 5)
@@ -70,6 +88,15 @@ def test_chunk_ranges_are_whole_chunks_and_cover():
             for (a, b), (c, _) in zip(rs, rs[1:]):
                 assert b == c and a % 4096 == 0
     assert D.frame_ids(5, 1, 2) == [1, 3]
+    for n in (0, 1, 9000, 853182):
+        for w in (1, 2, 3, 8):
+            rs = D.ray_ranges(n, w)
+            assert rs[0][0] == 0 and rs[-1][1] == n and max(b - a for a, b in rs) - min(b - a for a, b in rs) <= 1
+            for (a, b), (c, _) in zip(rs, rs[1:]):
+                assert b == c
+            for a, b in rs:
+                c0, c1 = D.chunk_cover(a, b, 4096, n)
+                assert c0 % 4096 == 0 and (c1 % 4096 == 0 or c1 == n) and c0 <= a and b <= c1
 
 
 @pytest.mark.timeout(600)

@@ -5,8 +5,9 @@
   gets the frame's own near / far, i.e. the chunk NaN fill of the whole frame, hazard H1).
 * Config 5 (1024^2): the north star's multi-GPU split — the ray list cut into
   distributed.chunk_ranges(n, 4096, 8) shards rendered separately and concatenated — is bit-identical
-  to the whole-frame render, in the default and the fp32 precision; 4,096 evenly spaced rays match the
-  oracle at 1e-4.  (The RCCL all-gather itself is covered by tests/test_distributed.py over gloo.)
+  to the whole-frame render in the bf16x6, fp16x3 and fp32 precisions, and 20,000 evenly spaced rays
+  (the bench's parity sample) match the oracle at 1e-4 (near-empty rays' disparity, H12: counted and
+  bounded, see _oracle_check).  (The RCCL all-gather itself is covered by tests/test_distributed.py over gloo.)
 The oracle is pinned to the reference's golden fixtures (tests/test_oracle_golden.py).
 """
 import importlib
@@ -58,16 +59,29 @@ def _render(rc, rb, sc, cyls):
 
 
 def _oracle_check(cfg, ck, sc, cyls, rb, out, n_sample):
+    """n_sample evenly spaced rays of the frame against the oracle at 1e-4, every output of every ray
+    except the disparity of near-empty rays (0 < acc < 2^-20, hazard H12): their count and disp error
+    are reported and bounded (1e-3, at most 0.1 % of the sample) — tests/golden/h12_nearempty_c5.npz
+    shows the reference and the oracle themselves differ there by that much."""
     import oracle
     om = oracle.OracleModel(cfg, ck)
     rb_h = rb.cpu().numpy()
     near, far, _, _ = om.near_far(rb_h, cyls[0:1], chunk=4096)
     sel = np.linspace(0, rb_h.shape[0] - 1, n_sample).astype(np.int64)
     ref = om.render_rays(rb_h[sel], sc["skts"][0], cyls[0:1], chunk=4096, near=near[sel], far=far[sel])
+    report = {}
     for k in ("rgb_map", "disp_map", "acc_map", "rgb0", "disp0", "acc0"):
         got = out[k].cpu().numpy()[sel]
-        d = float(np.abs(got.astype(np.float64) - ref[k]).max())
-        assert d <= TOL, f"{k}: max |gpu - oracle| = {d:.3e} over {n_sample} rays"
+        d = np.abs(got.astype(np.float64) - ref[k]).reshape(n_sample, -1).max(-1)
+        acc_k = ref["acc_map" if k in ("rgb_map", "disp_map", "acc_map") else "acc0"]
+        empty = (acc_k > 0) & (acc_k < 2.0 ** -20) if k.startswith("disp") else np.zeros(n_sample, bool)
+        strict = float(d[~empty].max())
+        assert strict <= TOL, f"{k}: max |gpu - oracle| = {strict:.3e} over {n_sample} rays"
+        if empty.any():
+            ne = float(d[empty].max())
+            report[k] = (int(empty.sum()), ne)
+            assert ne <= 1e-3 and empty.sum() <= max(1, n_sample // 1000), (k, int(empty.sum()), ne)
+    print(f"near-empty rays (count, max disp error): {report}")
 
 
 @pytest.mark.parametrize("nj,precision", [(24, "bf16x6"), (24, "fp16x3"), (24, "fp32"), (65, "fp16x3")])
@@ -81,7 +95,7 @@ def test_full_frame_matches_oracle_on_8192_rays(nj, precision):
     _oracle_check(cfg, ck, sc, cyls, rb, out, 8192)
 
 
-@pytest.mark.parametrize("precision", ["fp16x3", "fp32"])
+@pytest.mark.parametrize("precision", ["bf16x6", "fp16x3", "fp32"])
 def test_config5_pixel_shards_are_bit_identical(precision):
     sc, ck, cyls, rb = _frame(1024, 24, 13, 79.6)
     n = rb.shape[0]
@@ -93,5 +107,4 @@ def test_config5_pixel_shards_are_bit_identical(precision):
     torch.cuda.synchronize()
     for k in ("rgb_map", "disp_map", "acc_map", "rgb0", "disp0", "acc0"):
         assert torch.equal(torch.cat([p[k] for p in parts], 0), whole[k]), k
-    if precision != "fp32":
-        _oracle_check(cfg, ck, sc, cyls, rb, whole, 4096)
+    _oracle_check(cfg, ck, sc, cyls, rb, whole, 20000)

@@ -157,12 +157,16 @@ def test_wgrad_is_deterministic():
 
 
 @pytest.mark.parametrize("impl", ["bf16x6", "mixed", "bf16x3"])
-@pytest.mark.parametrize("D,W,fc", [(8, 256, False), (4, 128, True)])
-def test_nerf_forward_backward_matches_fp32_module(D, W, fc, impl):
+@pytest.mark.parametrize("D,W,fc,nj", [(8, 256, False, 24), (4, 128, True, 24),
+                                       # joint counts whose feature blocks are not multiples of 4 columns
+                                       # (mlp._pad_to_segments): 17 (odd), 26 (even, not % 4), 65 (config 4)
+                                       (8, 256, False, 17), (4, 128, True, 26), (8, 128, False, 65)])
+def test_nerf_forward_backward_matches_fp32_module(D, W, fc, nj, impl):
     """The whole network (skip layer, heads, view layer, framecodes) and its autograd vs the same
     module on torch's fp32 GEMMs."""
-    cfg = anerf.RenderConfig(netdepth=D, netwidth=W, opt_framecode=fc, n_framecodes=5 if fc else 0).validate()
-    ck = syn.make_checkpoint(5, n_joints=24, D=D, W=W, fine=False, use_framecode=fc, n_framecodes=5)
+    cfg = anerf.RenderConfig(n_joints=nj, netdepth=D, netwidth=W, opt_framecode=fc,
+                             n_framecodes=5 if fc else 0).validate()
+    ck = syn.make_checkpoint(5, n_joints=nj, D=D, W=W, fine=False, use_framecode=fc, n_framecodes=5)
     torch.manual_seed(0)
     M = 3000
     feat = (torch.rand(M, cfg.feature_dim, device=DEV) * 2 - 1)

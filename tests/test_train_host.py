@@ -136,3 +136,38 @@ def test_nerf_loss_functions_follow_trainer():
     # the default stays the round-1 MSE form
     plain = train.nerf_loss(preds, tgt)
     assert torch.allclose(plain, ((preds["rgb_map"] - tgt) ** 2).mean() + ((preds["rgb0"] - tgt) ** 2).mean())
+
+
+def test_segment_padding_is_exact_for_any_joint_count():
+    """mlp._pad_to_segments (joint counts whose feature blocks are not multiples of 4 columns):
+    the padded layer-0, skip and view products equal the unpadded ones (zeros added), and
+    autograd through the pads gives the unpadded gradients."""
+    mlp = importlib.import_module("a-nerf_amd.mlp")
+    anerf = importlib.import_module("a-nerf_amd")
+    for nj, fc in ((17, False), (26, True), (65, False)):
+        cfg = anerf.RenderConfig(n_joints=nj, netdepth=8, netwidth=64, opt_framecode=fc,
+                                 n_framecodes=5 if fc else 0).validate()
+        net = train.NeRF(cfg).double()
+        D, W, skip, dnet, nv = 8, 64, cfg.skips[0], net.dnet, cfg.input_ch_views
+        params = []
+        for lin in net.pts_linears:
+            params += [lin.weight, lin.bias]
+        params += [net.alpha_linear.weight, net.alpha_linear.bias, net.feature_linear.weight,
+                   net.feature_linear.bias, net.views_linears[0].weight, net.views_linears[0].bias,
+                   net.rgb_linear.weight, net.rgb_linear.bias]
+        feat = torch.randn(9, cfg.feature_dim, dtype=torch.float64, requires_grad=True)
+        fp, pp, d4, v4 = mlp._pad_to_segments(feat, params, W, D, skip, dnet, nv)
+        assert d4 % 4 == 0 and v4 % 4 == 0 and fp.shape[1] == d4 + v4
+        h = torch.randn(9, W, dtype=torch.float64)
+        code = torch.randn(9, cfg.framecode_ch, dtype=torch.float64)
+        ref = (feat[:, :dnet] @ params[0].t(), torch.cat([feat[:, :dnet], h], 1) @ params[2 * (skip + 1)].t(),
+               torch.cat([h, feat[:, dnet:dnet + nv], code], 1) @ params[2 * D + 4].t())
+        got = (fp[:, :d4] @ pp[0].t(), torch.cat([fp[:, :d4], h], 1) @ pp[2 * (skip + 1)].t(),
+               torch.cat([h, fp[:, d4:d4 + v4], code], 1) @ pp[2 * D + 4].t())
+        for r, g in zip(ref, got):  # (BLAS blocks a longer k differently: equal up to double rounding)
+            assert torch.allclose(r, g, rtol=1e-12, atol=1e-12)
+        sum(g.sum() for g in got).backward()
+        gf = feat.grad.clone()
+        feat.grad = None
+        sum(r.sum() for r in ref).backward()
+        assert torch.allclose(gf, feat.grad, rtol=1e-12, atol=1e-12)

@@ -5,7 +5,9 @@ optimisation on): one step = render_rays forward + the MSE/background loss + bac
 the per-image skeleton deltas) + Adam.  Synthetic scene and seeded weights.
 
 Prints one JSON line: training rays/s, steps/s, the MLP's GEMM FLOPs (3 x forward: the input
-gradient is needed for the pose gradient) and their rate against the FP32 matrix peak.
+gradient is needed for the pose gradient) and their rate against the peak of the MFMA pipe the
+GEMMs run on: BF16 dense for the split-bf16 modes ("mixed": bf16x6 forward, bf16x3 backward), FP32
+matrix for "fp32".
 Usage: python tools/train_bench.py [--steps K] [--warmup W] [--rays N]
 """
 import argparse
@@ -20,7 +22,8 @@ import torch
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
-FP32_MFMA_PEAK_TFLOPS = 157.3
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md, FP32 matrix
+BF16_MFMA_PEAK_TFLOPS = 2516.6  # MI355X_MICROARCH.md, BF16 dense
 
 
 def parser():
@@ -101,7 +104,14 @@ def measure(a, dev=None):
         "value": round(n / dt, 1), "unit": "rays/s", "ms_per_step": round(1e3 * dt, 3), "steps": a.steps,
         "dtype": "fp32" if a.mlp == "fp32" else f"fp32 in/out, MLP GEMMs as split bf16 ({a.mlp})", "mlp": a.mlp,
         "mlp_gemm_flop_per_step": flop, "mlp_tflops": round(flop / dt / 1e12, 2),
-        "frac_of_fp32_mfma_peak": round(flop / dt / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4),
+        "peak_tflops": FP32_MFMA_PEAK_TFLOPS if a.mlp == "fp32" else BF16_MFMA_PEAK_TFLOPS,
+        "frac_of_pipe_peak": round(flop / dt / 1e12 / (FP32_MFMA_PEAK_TFLOPS if a.mlp == "fp32"
+                                                       else BF16_MFMA_PEAK_TFLOPS), 4),
+        "pipe": "FP32 matrix" if a.mlp == "fp32" else "BF16 dense (the split-bf16 GEMMs' v_mfma_f32_32x32x16_bf16)",
+        "precision_note": {"mixed": "forward bf16x6 (fp32-accurate), gradients bf16x3 (~16-bit operands, relative "
+                                    "error ~1e-5; pinned at 2e-3 of max |ref| per gradient tensor)",
+                           "bf16x6": "fp32-accurate forward and gradients", "bf16x3": "~16-bit operands",
+                           "fp32": "torch fp32 GEMMs"}[a.mlp],
         "data": "synthetic (seeded SMPL-24 poses, 128 cameras on a circle, seeded weights)"}
 
 
