@@ -82,6 +82,11 @@ __device__ __forceinline__ void sincos_rr(float x, float& s, float& c) {
 }
 
 __device__ __forceinline__ float sigmoid(float x) { return 1.0f / (1.0f + expf(-x)); }
+// alpha = 1 - exp(-x) of raw2outputs (nerf.py:186-187) for x = act(sigma) * delta in float32, with exp
+// rounded to nearest like the CPU reference's: OCML's expf (<= 1 ulp) returned 1.0 for exp(-4.09e-8),
+// whose nearest float is 1 - 2^-24, and on a near-empty ray that one quantum IS the ray's alpha and
+// its disp (hazard H12, tests/golden/h12_nearempty_c5.npz).  exp in double, rounded once to float.
+__device__ __forceinline__ float alpha_of(float x) { return 1.0f - (float)exp(-(double)x); }
 // torch.relu keeps NaN
 __device__ __forceinline__ float relu(float x) { return x < 0.0f ? 0.0f : x; }
 // MLP activation relu in one VALU op: signed-integer max of the bit pattern maps every float with

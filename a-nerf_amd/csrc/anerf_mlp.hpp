@@ -14,6 +14,23 @@ __device__ __forceinline__ f32x2 bload2(__amdgpu_buffer_rsrc_t rs, int voff, int
 __device__ __forceinline__ f32x4 bload4(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
     return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
 }
+// Non-temporal (nt, cache-policy bit 2 on gfx950) forms for the weight streams an XCD's L2 should not
+// keep: the per-joint windowed parts (touched only for the block's live joints) and the view-direction
+// rows of G (once per ray and pass).  Cached like the hidden layers' streams, these push one net's
+// touched set (4.3 MB in bf16x6) past the 4 MB L2, and the cyclic hidden-layer stream then misses
+// (tools/probe/layer_probe_x6: 90 % of the MFMA rate up to a 3.8 MB footprint, 84 % at 4.2 MB).
+#ifndef ANERF_NT_V
+#define ANERF_NT_V 0
+#endif
+#ifndef ANERF_NT_G
+#define ANERF_NT_G 0
+#endif
+__device__ __forceinline__ f32x2 bload2_v(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+    return __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, ANERF_NT_V ? 2 : 0));
+}
+__device__ __forceinline__ f32x4 bload4_g(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, ANERF_NT_G ? 2 : 0));
+}
 
 template <int RB>
 __device__ __forceinline__ void load_bias(f32x16 (&acc)[RB], const float* __restrict__ bp_lds, int hh) {
@@ -583,6 +600,16 @@ struct JointMask {
     uint64_t m0, m1;
 };
 
+// The mask is wave-uniform (built from ballots), but the compiler loses that through the struct and
+// then keeps it -- and every joint index popped from it -- in VGPRs: each per-joint weight load's
+// scalar offset became a waterfall loop (readfirstlane / compare / exec loop around every
+// buffer_load).  Read it back into SGPRs once.
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
 __device__ __forceinline__ int mask_pop(uint64_t& a0, uint64_t& a1) {
     if (a0) {
         const int j = __builtin_ctzll(a0);
@@ -934,7 +961,7 @@ __device__ __forceinline__ void v_part(f32x16 (&acc)[RB], const ModelDev& M, con
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(wp);
     const int voff = lane * 8;
     const bool dist_in = M.use_cutoff && M.cutoff_inputs;
-    uint64_t r0 = mask.m0, r1 = mask.m1;
+    uint64_t r0 = uniform64(mask.m0), r1 = uniform64(mask.m1);
     int j = mask_pop(r0, r1);
     if (j < 0) return;
     int jn = mask_pop(r0, r1);
@@ -942,7 +969,7 @@ __device__ __forceinline__ void v_part(f32x16 (&acc)[RB], const ModelDev& M, con
 #pragma unroll
     for (int g = 0; g < 2; ++g)
 #pragma unroll
-        for (int rb = 0; rb < RB; ++rb) ring[g][rb] = bload2(rs, voff, ((j * GB + g) * RB + rb) * 512);
+        for (int rb = 0; rb < RB; ++rb) ring[g][rb] = bload2_v(rs, voff, ((j * GB + g) * RB + rb) * 512);
     float f[KB];
     {
         float dist, w, u, uf;
@@ -971,11 +998,11 @@ __device__ __forceinline__ void v_part(f32x16 (&acc)[RB], const ModelDev& M, con
             if (g + PD < GB) {
 #pragma unroll
                 for (int rb = 0; rb < RB; ++rb)
-                    ring[(g + PD) % GB][rb] = bload2(rs, voff, ((j * GB + g + PD) * RB + rb) * 512);
+                    ring[(g + PD) % GB][rb] = bload2_v(rs, voff, ((j * GB + g + PD) * RB + rb) * 512);
             } else {  // the next joint's first groups (this joint's again after the last: harmless)
 #pragma unroll
                 for (int rb = 0; rb < RB; ++rb)
-                    ring[(g + PD) % GB][rb] = bload2(rs, voff, ((jg * GB + g + PD - GB) * RB + rb) * 512);
+                    ring[(g + PD) % GB][rb] = bload2_v(rs, voff, ((jg * GB + g + PD - GB) * RB + rb) * 512);
             }
 #pragma unroll
             for (int t = 0; t < 2; ++t) {

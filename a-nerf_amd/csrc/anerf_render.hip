@@ -355,11 +355,13 @@ int anerf_render_rays(const anerf_model* m, const float* ray_batch, int32_t ray_
         }                                                                                           \
     } while (0)
     if (W == 256 && mr == 7) ANERF_LAUNCH(256, 7);
+#ifndef ANERF_AB_FAST  // (tools/build_ab.sh: experiment builds with the config-3 instance only)
     else if (W == 128 && mr == 7) ANERF_LAUNCH(128, 7);
     else if (W == 64 && mr == 7) ANERF_LAUNCH(64, 7);
     else if (W == 256 && mr == 10) ANERF_LAUNCH(256, 10);
     else if (W == 128 && mr == 10) ANERF_LAUNCH(128, 10);
     else if (W == 64 && mr == 10) ANERF_LAUNCH(64, 10);
+#endif
     else return fail(ANERF_EINVAL, "no kernel instance for this width / multires");
 #undef ANERF_LAUNCH
     HIP_TRY(hipGetLastError());
@@ -594,11 +596,13 @@ static int launch_density(const anerf_model* m, DensityArgs a, int32_t precision
         hipLaunchKernelGGL(kfn, dim3(grid), dim3(256), lds_bytes, st, m->md, a, P);                \
     } while (0)
     if (W == 256 && mr == 7) ANERF_LAUNCH(256, 7);
+#ifndef ANERF_AB_FAST
     else if (W == 128 && mr == 7) ANERF_LAUNCH(128, 7);
     else if (W == 64 && mr == 7) ANERF_LAUNCH(64, 7);
     else if (W == 256 && mr == 10) ANERF_LAUNCH(256, 10);
     else if (W == 128 && mr == 10) ANERF_LAUNCH(128, 10);
     else if (W == 64 && mr == 10) ANERF_LAUNCH(64, 10);
+#endif
     else return fail(ANERF_EINVAL, "no kernel instance for this width / multires");
 #undef ANERF_LAUNCH
     HIP_TRY(hipGetLastError());

@@ -53,7 +53,7 @@ __device__ void compute_view_factor(const ModelDev& M, const NetDev& net, float*
         auto load_col = [&](float (&dst)[TP], int col) {
 #pragma unroll
             for (int q = 0; q < TP / 4; ++q) {
-                const f32x4 x = bload4(rs, (col * WH + nn) * TP * 4 + q * 16, 0);
+                const f32x4 x = bload4_g(rs, (col * WH + nn) * TP * 4 + q * 16, 0);
                 dst[4 * q] = x[0], dst[4 * q + 1] = x[1], dst[4 * q + 2] = x[2], dst[4 * q + 3] = x[3];
             }
         };
@@ -159,7 +159,7 @@ __device__ void composite(const ModelDev& M, const float* ray, const float* z, c
         for (int i = lane; i < n; i += 64) {
             float dist = (i + 1 < n) ? (z[i + 1] - z[i]) : 1e10f;
             dist = dist * dn;
-            const float a = 1.0f - expf(-density_act(M, raw[4 * i + 3] / M.B) * dist);
+            const float a = alpha_of(density_act(M, raw[4 * i + 3] / M.B) * dist);
             al[i] = a;
             fac[i] = (1.0f - a) + 1e-10f;
             if (o_alpha) o_alpha[i] = a;

@@ -319,7 +319,7 @@ __global__ __launch_bounds__(64) void train_composite_kernel(ModelDev M, const f
         float dist = (s + 1 < ns) ? (zr[s + 1] - zr[s]) : 1e10f;
         dist = dist * dn;
         const float x = rr[4 * s + 3] / M.B + (noise ? noise[i * ns + s] : 0.0f);
-        la[s] = 1.0f - expf(-density_act(M, x) * dist);
+        la[s] = alpha_of(density_act(M, x) * dist);
         lz[s] = zr[s];
         lc0[s] = sigmoid(rr[4 * s + 0]) * 1.002f - 0.001f;
         lc1[s] = sigmoid(rr[4 * s + 1]) * 1.002f - 0.001f;

@@ -189,18 +189,18 @@ def parity_leg(a, cfg, ck, sc, cyls, idx, c2w_np, H, W, out, n, dev, want_cpu):
     diff = {k: np.abs(out[k].index_select(0, sel_d).cpu().numpy().astype(np.float64) - ref[k].astype(np.float64))
             for k in ("rgb_map", "disp_map", "acc_map")}
     # H12: on a near-empty ray (0 < acc < 2^-20) disp = 1 / max(1e-10, depth / acc) is a ratio
-    # of a few 2^-24 alpha quanta; which sample carries them follows ulp-level raw differences, so two
-    # fp32 implementations (the reference and the oracle included, tests/golden/h12_nearempty_c5.npz)
-    # differ there by up to ~1e-3.  Such rays are counted and their disp error reported and bounded
-    # (1e-3, and at most 0.1 % of the sample); every other output of every ray is held to 1e-4
+    # of a few 2^-24 alpha quanta, and a raw-sigma ulp at a rounding threshold moves a quantum (1 of
+    # config 5's 169 such rays differs from the reference by 1.7e-4 in fp32 / bf16x6,
+    # tests/golden/h12_nearempty_c5.npz).  Such rays are counted and their disp error reported and
+    # bounded (5e-4, and at most 0.1 % of the sample); every other output of every ray is held to 1e-4
     empty = (ref["acc_map"] > 0) & (ref["acc_map"] < 2.0 ** -20)
     errs = {k: float(v[~empty].max() if k == "disp_map" and empty.any() and (~empty).any() else v.max())
             for k, v in diff.items()}
     ne_err = float(diff["disp_map"][empty].max()) if empty.any() else 0.0
-    ok = max(errs.values()) <= 1e-4 and ne_err <= 1e-3 and int(empty.sum()) <= max(1, len(sel) // 1000)
+    ok = max(errs.values()) <= 1e-4 and ne_err <= 5e-4 and int(empty.sum()) <= max(1, len(sel) // 1000)
     parity = {"rays": int(len(sel)), "max_abs_err": {k: float(f"{v:.3e}") for k, v in errs.items()},
               "near_empty_rays": int(empty.sum()), "near_empty_disp_max_abs_err": float(f"{ne_err:.3e}"),
-              "tol": 1e-4, "near_empty_tol": {"disp": 1e-3, "max_rays": max(1, len(sel) // 1000)}, "ok": bool(ok),
+              "tol": 1e-4, "near_empty_tol": {"disp": 5e-4, "max_rays": max(1, len(sel) // 1000)}, "ok": bool(ok),
               "against": "C oracle (pinned to the reference's golden fixtures) on the same rays, near/far "
                          "from the whole frame's 4096-ray chunks"}
     return parity, cpu
@@ -233,6 +233,7 @@ def main():
     syn = importlib.import_module("a-nerf_amd.synthetic")
     _lib = importlib.import_module("a-nerf_amd._lib")
     dmod = importlib.import_module("a-nerf_amd.distributed")
+    near_far = importlib.import_module("a-nerf_amd.raycaster").near_far
     lib = _lib.load()
 
     H = W = a.res
@@ -254,21 +255,26 @@ def main():
     st = _lib.stream_handle(dev)
     ev = []
     sharded = pixels and dist
-    # this rank's rays: pixels mode = its whole-chunk range of the frame's ray list (generated from the
-    # resident pixel indices, nothing else); otherwise the whole box
-    s0, s1 = dmod.chunk_ranges(n, 4096, world)[rank] if sharded else (0, n)
-    n_mine = s1 - s0
-    rb = torch.empty(max(n_mine, 1), 11, device=dev)[:n_mine]
+    # this rank's rays: pixels mode = an equal share of the frame's ray list (distributed.ray_ranges),
+    # generated from the resident pixel indices of the whole 4096-ray chunks that cover it, whose near /
+    # far (cylinder + chunk NaN fill) the rank computes so its rays render exactly as in the whole frame
+    # (ANERF_FLAG_NEAR_FAR); otherwise the whole box
+    ranges = dmod.ray_ranges(n, world) if sharded else [(0, n)]
+    s0, s1 = ranges[rank if sharded else 0]
+    c0, c1 = dmod.chunk_cover(s0, s1, 4096, n) if sharded else (s0, s1)
+    n_mine, n_cover = s1 - s0, c1 - c0
+    rb_cover = torch.empty(max(n_cover, 1), 11, device=dev)[:n_cover]
+    rb = rb_cover[s0 - c0:s1 - c0]
     idx_all = torch.from_numpy(np.ascontiguousarray(idxs[0], np.int64)).to(dev)
     if sharded:
-        idx_mine = idx_all[s0:s1].contiguous()
-        gather = dmod.ShardGather(n, 4096, world, dev)
+        idx_cover = idx_all[c0:c1].contiguous()
+        gather = dmod.ShardGather(n, 4096, world, dev, ranges=ranges)
     last = {}
 
     def render(r):
         m = r.shape[0]
         return rc.render_rays(r, S, skts=skts.expand(m, -1, -1, -1), cyls=cyl.expand(m, -1), N_importance=I,
-                              chunk=4096, ret_alpha=False)
+                              chunk=4096, ret_alpha=False, near_far_given=sharded)
 
     def event():
         e = torch.cuda.Event(enable_timing=True)
@@ -279,7 +285,9 @@ def main():
         if sharded:
             if n_mine:
                 _lib.check(lib.anerf_gen_rays(_lib.ptr(c2w), H, W, sc["focal"], sc["focal"], 0.0, 0.0, 0,
-                                              _lib.ptr(idx_mine), n_mine, 0.0, 1.0, _lib.ptr(rb), st), "gen_rays")
+                                              _lib.ptr(idx_cover), n_cover, 0.0, 1.0, _lib.ptr(rb_cover), st),
+                           "gen_rays")
+                near_far(rb_cover, cyl, chunk=4096, out=(rb_cover[:, 6], rb_cover[:, 7]))
         else:
             _lib.check(lib.anerf_gen_rays_box(_lib.ptr(c2w), H, W, sc["focal"], sc["focal"], 0.0, 0.0, 0, x0, y0, x1,
                                               y1, 0.0, 1.0, _lib.ptr(rb), st), "gen_rays_box")
@@ -336,7 +344,7 @@ def main():
     # the work an exact fp32 implementation must do after exact-zero window skipping: the fp32 mode's
     # tally of the same rays (v_mfma_f32_32x32x2_f32, FLOP_F32_MFMA each)
     rc.render_rays(rb, S, skts=skts.expand(n_mine, -1, -1, -1), cyls=cyl.expand(n_mine, -1), N_importance=I,
-                   chunk=4096, ret_alpha=False, count_mfma=True)
+                   chunk=4096, ret_alpha=False, count_mfma=True, near_far_given=sharded)
     torch.cuda.synchronize()
     n_f32, n_bf16 = (int(v) for v in rc.last_mfma.tolist())
     if a.precision == "fp32":
@@ -345,7 +353,7 @@ def main():
         rc32 = anerf.RayCaster(anerf.RenderConfig(n_joints=a.joints, N_samples=S, N_importance=I,
                                                   precision="fp32").validate(), ck, device=local)
         rc32.render_rays(rb, S, skts=skts.expand(n_mine, -1, -1, -1), cyls=cyl.expand(n_mine, -1), N_importance=I,
-                         chunk=4096, ret_alpha=False, count_mfma=True)
+                         chunk=4096, ret_alpha=False, count_mfma=True, near_far_given=sharded)
         torch.cuda.synchronize()
         req_f32 = int(rc32.last_mfma[0].item())
         del rc32

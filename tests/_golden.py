@@ -22,7 +22,13 @@ NAMES = ["c1_64_s32_d4w128", "c2_256_s64_d8w256", "c3_512_s64i128_d8w256", "c4_5
          # --lindisp (inverse-depth samples); --freq_schedule at sched_alpha 2.3 (D = 8: skip layer)
          "l1_lindisp_s32i16_d4w128", "fs1_freqsched_s32i16_d8w128",
          # --cut_to_dist, --cutoff_shift (the kp cutoff embedder's input transforms)
-         "cd1_cuttodist_s32i16_d8w128", "cs1_cutoffshift_s32i16_d4w128"]
+         "cd1_cuttodist_s32i16_d8w128", "cs1_cutoffshift_s32i16_d4w128",
+         # the shipped configs' shape: mixamo / h36m / perfcap (8x256, 64 + 16, framecodes incl. the eval-mode
+         # mean code), surreal (8x256, 64 + 16)
+         "mx1_mixamo_s64i16_d8w256_fc", "su1_surreal_s64i16_d8w256",
+         # render_path frames with white_bkgd / resized background images (two frames each)
+         "pw_64_white_d4w128", "pb_64_bgimg_d4w128"]
+FRAMES = ["c1_64_s32_d4w128", "pw_64_white_d4w128", "pb_64_bgimg_d4w128"]
 
 
 class Golden:

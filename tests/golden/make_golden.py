@@ -126,6 +126,20 @@ CONFIGS = {
                                         seed=27, flags=["--cut_to_dist"]),
     "cs1_cutoffshift_s32i16_d4w128": dict(H=128, NJ=24, S=32, I=16, D=4, W=128, tau=20.0, kind="rays",
                                           n_rays=128, seed=25, flags=["--cutoff_shift"]),
+    # the shipped configs' render shape (configs/{mixamo,h36m,perfcap}/*.txt: 8x256, multires 7 / 4,
+    # N_samples 64, N_importance 16, opt_framecode; configs/surreal/surreal.txt the same without
+    # framecodes): the view layer's framecode column at W = 256 and the 64 + 16 importance pass
+    "mx1_mixamo_s64i16_d8w256_fc": dict(H=256, NJ=24, S=64, I=16, D=8, W=256, tau=200.0, kind="framecode",
+                                        n_rays=160, seed=41),
+    "su1_surreal_s64i16_d8w256": dict(H=512, NJ=24, S=64, I=16, D=8, W=256, tau=20.0, kind="rays", n_rays=192,
+                                      seed=42),
+    # render_path's background compose (run_nerf.py:100-131): white_bkgd (bg = 1), and bg_imgs resized
+    # with F.interpolate(bilinear, align_corners=False) and picked per frame by bg_indices; two frames
+    # (reuse_input of the pose tensors, run_nerf.py:63-74)
+    "pw_64_white_d4w128": dict(H=64, NJ=24, S=32, I=16, D=4, W=128, tau=20.0, kind="frame", seed=43, n_frames=2,
+                               white_bkgd=True),
+    "pb_64_bgimg_d4w128": dict(H=64, NJ=24, S=32, I=16, D=4, W=128, tau=20.0, kind="frame", seed=44, n_frames=2,
+                               bg_imgs=(3, 48, 40), bg_indices=[2, 0]),
 }
 
 
@@ -167,8 +181,18 @@ def build_reference(mods, cfg, tmp):
 
 
 def scene_for(cfg):
-    sc = anerf_syn.make_scene(n_joints=cfg["NJ"], H=cfg["H"], W=cfg["H"], seed=cfg["seed"])
-    return sc
+    if cfg.get("n_frames", 1) > 1:
+        return anerf_syn.make_scene(n_joints=cfg["NJ"], H=cfg["H"], W=cfg["H"], seed=cfg["seed"],
+                                    n_frames=cfg["n_frames"], yaw_step=0.7)
+    return anerf_syn.make_scene(n_joints=cfg["NJ"], H=cfg["H"], W=cfg["H"], seed=cfg["seed"])
+
+
+def bg_for(cfg):
+    """(bg_imgs float32 [B, h, w, 3] in [0, 1], bg_indices) of a background-compose fixture, or Nones."""
+    if "bg_imgs" not in cfg:
+        return None, None
+    bg = np.random.default_rng(cfg["seed"] + 300).random(cfg["bg_imgs"] + (3,)).astype(np.float32)
+    return bg, np.asarray(cfg["bg_indices"], np.int64)
 
 
 def rays_for(mods, sc):
@@ -280,18 +304,24 @@ def make(name, cfg, mods, tmp):
                 tau=cfg["tau"], H=sc["H"], focal=sc["focal"], ext_scale=0.001, chunk=4096,
                 framecode=int(cfg["kind"] == "framecode"), mr=cfg.get("mr", 7), flags=cfg.get("flags", []),
                 drop=cfg.get("drop", []), mrv=cfg.get("mrv", 4), single=bool(cfg.get("single", False)),
-                sched=cfg.get("sched"))
+                sched=cfg.get("sched"), white_bkgd=bool(cfg.get("white_bkgd", False)),
+                n_frames=int(cfg.get("n_frames", 1)))
     data = {"c2ws": sc["c2ws"], "kps": sc["kps"], "skts": sc["skts"], "bones": sc["bones"]}
     (o, d), vidx, cyls, (tl, br) = rays_for(mods, sc)
     sc["cyls"] = cyls
     data.update(cyls=cyls, valid_idx=vidx, tl=np.asarray(tl), br=np.asarray(br))
     if cfg["kind"] == "frame":
+        bg_imgs, bg_indices = bg_for(cfg)
         with torch.no_grad():
             rgbs, disps, accs, vids, bbs = run_nerf.render_path(
                 torch.from_numpy(sc["c2ws"]), (sc["H"], sc["W"], sc["focal"]), 4096, render_kwargs,
                 kp=torch.from_numpy(sc["kps"]), skts=torch.from_numpy(sc["skts"]),
-                bones=torch.from_numpy(sc["bones"]), ret_acc=True, ext_scale=0.001)
+                bones=torch.from_numpy(sc["bones"]), ret_acc=True, ext_scale=0.001,
+                white_bkgd=bool(cfg.get("white_bkgd", False)), bg_imgs=bg_imgs, bg_indices=bg_indices)
         data.update(frame_rgb=rgbs, frame_disp=disps, frame_acc=accs)
+        if bg_imgs is not None:
+            data.update(bg_imgs=bg_imgs, bg_indices=bg_indices)
+        data.update(**{f"frame_valid_idx_{f}": v.numpy() for f, v in enumerate(vids)})
         sel = np.arange(min(64, len(vidx)))
     elif cfg["kind"] == "nanfill":
         # contiguous 4096-ray chunk starting at the top of the box: its corner rays miss the cylinder

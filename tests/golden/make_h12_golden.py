@@ -38,7 +38,7 @@ syn = importlib.import_module("a-nerf_amd.synthetic")
 SCAN = "/tmp/h12_scan.npz"
 H, NJ, SEED, TAU = 1024, 24, 13, 79.6
 N_ORDINARY = 64
-MAX_EMPTY = 96
+MAX_EMPTY = 256
 
 
 def frame():

@@ -19,7 +19,7 @@ import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
 
-from _golden import Golden, NAMES  # noqa: E402
+from _golden import FRAMES, Golden, NAMES  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -96,7 +96,8 @@ def test_framecode_mean_code_matches_golden():
         assert _maxdiff(out[k], g["outneg_" + k]) <= TOL
 
 
-@pytest.mark.parametrize("name", [n for n in NAMES if n.startswith(("c2", "c3", "c4", "fc", "v", "s1", "t2000"))])
+@pytest.mark.parametrize("name", [n for n in NAMES if n.startswith(("c2", "c3", "c4", "fc", "v", "s1", "t2000", "mx1",
+                                                                    "su1"))])
 def test_stages_match_reference(name):
     """near/far and coarse z bit-exact; raw / weights / fine z against the reference's stage dumps."""
     g = Golden(name)
@@ -230,22 +231,81 @@ def test_encode_points_matches_reference_features():
     assert _maxdiff(feat.cpu().numpy(), ref) <= 2e-6
 
 
-def test_render_path_frame_matches_reference():
-    """Full render_path of config 1 (64x64, 4x128): pixel set exact, image within 1e-4."""
-    g = Golden("c1_64_s32_d4w128")
+@pytest.mark.parametrize("name", FRAMES)
+def test_render_path_frame_matches_reference(name):
+    """Full render_path frames (64x64, 4x128): config 1; two frames with white_bkgd; two frames on
+    background images resized by bilinear F.interpolate and picked by bg_indices (run_nerf.py:100-131).
+    Pixel sets exact, images within 1e-4."""
+    g = Golden(name)
     rc = _caster(g)
-    kw = {"ray_caster": rc, "N_samples": g.cfg.N_samples, "N_importance": 0, "perturb": False,
+    kw = {"ray_caster": rc, "N_samples": g.cfg.N_samples, "N_importance": g.cfg.N_importance, "perturb": False,
           "raw_noise_std": 0., "ray_noise_std": 0., "use_viewdirs": True, "preproc_kwargs": {"density_scale": 1.0},
           "lindisp": False}
     H = g.meta["H"]
-    rgbs, disps, accs, vids, bbs = anerf.render_path(torch.from_numpy(g["c2ws"]), (H, H, g.meta["focal"]), 4096, kw,
-                                                     kp=torch.from_numpy(g["kps"]),
-                                                     skts=torch.from_numpy(g["skts"]), ret_acc=True, ext_scale=0.001)
+    rgbs, disps, accs, vids, bbs = anerf.render_path(
+        torch.from_numpy(g["c2ws"]), (H, H, g.meta["focal"]), 4096, kw, kp=torch.from_numpy(g["kps"]),
+        skts=torch.from_numpy(g["skts"]), ret_acc=True, ext_scale=0.001, white_bkgd=g.meta.get("white_bkgd", False),
+        bg_imgs=g["bg_imgs"] if g.has("bg_imgs") else None, bg_indices=g["bg_indices"] if g.has("bg_indices") else None)
     np.testing.assert_array_equal(vids[0].numpy(), g["valid_idx"])
+    for f in range(len(vids)):
+        if g.has(f"frame_valid_idx_{f}"):
+            np.testing.assert_array_equal(vids[f].numpy(), g[f"frame_valid_idx_{f}"])
     assert tuple(bbs[0][0]) == tuple(g["tl"]) and tuple(bbs[0][1]) == tuple(g["br"])
+    assert rgbs.shape == g["frame_rgb"].shape
     assert _maxdiff(rgbs, g["frame_rgb"]) <= TOL
     assert _maxdiff(disps, g["frame_disp"]) <= TOL
     assert _maxdiff(accs, g["frame_acc"]) <= TOL
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_gen_rays_bit_exact_vs_reference_rays(name):
+    """anerf_gen_rays on the fixture's pixel indices equals the reference's get_rays rays
+    (core/utils/ray_utils.py:6-28, gathered by valid_idx) bit for bit, and anerf_gen_rays_box over the
+    whole box equals the index path."""
+    g = Golden(name)
+    lib = _lib.load()
+    H = g.meta["H"]
+    f = float(g.meta["focal"])
+    c2w = torch.from_numpy(np.ascontiguousarray(g["c2ws"][0][:3, :4])).cuda()
+    idx = torch.from_numpy(np.ascontiguousarray(g["valid_idx"][g["sel"]], np.int64)).cuda()
+    n = idx.shape[0]
+    rb = torch.empty(n, 11, device="cuda")
+    _lib.check(lib.anerf_gen_rays(_lib.ptr(c2w), H, H, f, f, 0.0, 0.0, 0, _lib.ptr(idx), n, 0.0, 1.0, _lib.ptr(rb),
+                                  _lib.stream_handle()), "gen_rays")
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(rb[:, 0:3].cpu().numpy(), g["rays_o"])
+    np.testing.assert_array_equal(rb[:, 3:6].cpu().numpy(), g["rays_d"])
+    tl, br = g["tl"], g["br"]
+    nb = int((br[0] - tl[0]) * (br[1] - tl[1]))
+    box = torch.empty(nb, 11, device="cuda")
+    _lib.check(lib.anerf_gen_rays_box(_lib.ptr(c2w), H, H, f, f, 0.0, 0.0, 0, int(tl[0]), int(tl[1]), int(br[0]),
+                                      int(br[1]), 0.0, 1.0, _lib.ptr(box), _lib.stream_handle()), "gen_rays_box")
+    torch.cuda.synchronize()
+    sel = torch.from_numpy(np.ascontiguousarray(g["sel"], np.int64)).cuda()
+    assert torch.equal(box.index_select(0, sel), rb)
+
+
+def test_gen_rays_box_bit_exact_vs_reference_full_frames():
+    """The first and last 8 rays of the reference's kp_to_valid_rays for configs 2-5 (1024^2 included,
+    3 frames each, tests/golden/bboxes.npz) from anerf_gen_rays_box."""
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "bboxes.npz"))
+    lib = _lib.load()
+    for name in ("c2", "c3", "c4", "c5", "c3_f3"):
+        H, nj, seed = (int(v) for v in z[name + "_meta"])
+        sc = syn.make_scene(n_joints=nj, H=H, W=H, seed=seed, n_frames=3, yaw_step=0.4)
+        for fr in range(3):
+            (x0, y0), (x1, y1) = z[name + "_tl"][fr], z[name + "_br"][fr]
+            n = int((x1 - x0) * (y1 - y0))
+            c2w = torch.from_numpy(np.ascontiguousarray(sc["c2ws"][fr][:3, :4])).cuda()
+            rb = torch.empty(n, 11, device="cuda")
+            _lib.check(lib.anerf_gen_rays_box(_lib.ptr(c2w), H, H, float(sc["focal"]), float(sc["focal"]), 0.0, 0.0, 0,
+                                              int(x0), int(y0), int(x1), int(y1), 0.0, 1.0, _lib.ptr(rb),
+                                              _lib.stream_handle()), "gen_rays_box")
+            torch.cuda.synchronize()
+            d = rb[:, 3:6].cpu().numpy()
+            np.testing.assert_array_equal(d[:8], z[name + "_rays_d_first"][fr], err_msg=f"{name} frame {fr}")
+            np.testing.assert_array_equal(d[-8:], z[name + "_rays_d_last"][fr], err_msg=f"{name} frame {fr}")
+            np.testing.assert_array_equal(rb[0, 0:3].cpu().numpy(), z[name + "_rays_o"][fr])
 
 
 def test_edge_cases_empty_and_ragged():
