@@ -208,6 +208,10 @@ def parity_leg(a, cfg, ck, sc, cyls, idx, c2w_np, H, W, out, n, dev, want_cpu):
 
 def main():
     a = parse()
+    # stdout carries exactly one line, the result: everything else the process or its libraries
+    # print (RCCL's version banner at communicator set-up goes to fd 1) is sent to stderr
+    out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -427,6 +431,12 @@ def main():
                          "unit": "TFLOP/s", "frac": round(achieved_alg / peak, 4),
                          "traffic": traffic, "traffic_source": traffic_src,
                          "traffic_measured_in_this_run": False,
+                         "traffic_note": "2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md, HBM / rocprofv3): L2 "
+                                         "fabric-side bytes, which count Infinity-Cache (L3) hits. bf16x6's per-net "
+                                         "streamed weight set (~4.2 MB) exceeds an XCD's 4 MB L2, so the weights are "
+                                         "re-read from the 256 MB L3 (fp16x3's ~3 MB set fits: ~0.56 GB); the bytes "
+                                         "a render call must move are unique_bytes_per_step + ~8.6 MB of weights",
+                         "unique_bytes_per_step": int(n_mine * (4 * 11 + 4 * 10) + (n_mine * (S + I) * 4 * 2 if I > 0 else 0)),
                          "kernel_ms": round(kern_ms, 3),
                          "launches_per_step": 2 if I > 0 else 1,
                          "flop": "algorithmic: the reference's MLP FLOPs (SURVEY §8(d), reference_flop_per_ray x "
@@ -454,7 +464,7 @@ def main():
             "other_precisions": others or None,
             "training": training,
         }
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=out, flush=True)
     if dist:
         tdist.destroy_process_group()
     if parity is not None and not parity["ok"]:

@@ -74,12 +74,14 @@ enum {
  *                     w = w0 + w1 + w2 (bf16 RNE of the running remainder), computed as the six products
  *                     with i + j <= 2 of x_i w_j on v_mfma_f32_32x32x16_bf16, fp32 accumulation: the
  *                     dropped terms are below 2^-23 of each product (fp32 rounds a product to 2^-24),
- *                     so the contraction is fp32-accurate; encoder, layer 0 and heads fp32;
+ *                     so the contraction is fp32-accurate; layer 0's and the skip layer's bone-direction
+ *                     parts the same way; encoder, the windowed layer-0 part and heads fp32;
  *   ANERF_PREC_FP16X3 the dense hidden layers and the fused view layer in fp16 after exact power-of-two
  *                     scaling (weights per layer, activations per sample, both to a maximum in
  *                     [2^10, 2^11)): x = x0 + x1, w = w0 + w1 (22 significant bits each), computed as
  *                     x0 w0 + x0 w1 + x1 w0 on v_mfma_f32_32x32x16_f16 (exact products, fp32 accumulation,
- *                     the dropped x1 w1 ~2^-22 of |x w|): half of bf16x6's MFMAs at comparable accuracy;
+ *                     the dropped x1 w1 ~2^-22 of |x w|): half of bf16x6's MFMAs, 22-bit instead of
+ *                     24-bit operands;
  *                     bone-direction parts as in bf16x6; encoder, layer 0's windowed part and heads fp32. */
 enum { ANERF_PREC_FP32 = 0, ANERF_PREC_BF16X3 = 1, ANERF_PREC_BF16X6 = 2, ANERF_PREC_FP16X3 = 3 };
 /* Flags OR-ed into anerf_render_rays' precision argument (and anerf_train_samples' flags):

@@ -54,7 +54,8 @@ def test_split_weights_batch_matches_single(prec):
 
 @pytest.mark.parametrize("prec", [3, 6])
 @pytest.mark.parametrize("m,n,ks", [(1000, 257, (256, 648, 16)), (4096, 256, (432, 256)), (77, 3, (128,)),
-                                    (130, 128, (904,)), (0, 64, (32,))])
+                                    (130, 128, (904,)), (0, 64, (32,)), (20011, 920, (128,)),
+                                    (163857, 256, (256,)), (9000, 432, (256,)), (33, 200, (12, 20))])
 def test_gemm_forward_segments_bias_relu(m, n, ks, prec):
     torch.manual_seed(m + n)
     k = sum(ks)
