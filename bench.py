@@ -82,8 +82,9 @@ def parse():
                     help="skip the training-step leg (SURVEY §8(f) row 2: tools/train_bench.py, N = 1 only)")
     ap.add_argument("--shard", default=None, choices=["frames", "pixels"],
                     help="frames: one frame per rank (weak scaling, no collective); pixels: ONE frame per step "
-                         "split into whole 4096-ray chunks across the ranks + an RCCL all-gather of the ray "
-                         "outputs (strong scaling, BASELINE config 5's layout; the default at N > 1)")
+                         "split into ray-balanced ranges across the ranks (near / far from the whole frame's "
+                         "4096-ray chunks) + an RCCL all-gather of the ray outputs (strong scaling, BASELINE "
+                         "config 5's layout; the default under torch.distributed.run)")
     ap.add_argument("--also", default="fp16x3,fp32,bf16x3",
                     help="other precision modes timed on the same frame afterwards (rank 0, N=1; '' = none)")
     ap.add_argument("--precision", default="bf16x6", choices=["fp32", "bf16x6", "fp16x3", "bf16x3"],
@@ -413,7 +414,7 @@ def main():
     if rank == 0:
         value = rays_job / elapsed
         workload = (f"{_config_name(H, S, I, a.joints)}: {H}x{W} frame, {S}+{I} samples, {a.joints}-joint, 8x256 MLP, "
-                    + (f"one frame per step split over {world} GPU(s) in whole 4096-ray chunks + RCCL all-gather"
+                    + (f"one frame per step split over {world} GPU(s) in ray-balanced ranges (near/far from the whole frame's 4096-ray chunks) + RCCL all-gather"
                        if sharded else "one frame per GPU per step"))
         ranks = [{"rank": r, "rays": int(p[3]), "render_ms": round(p[0], 3), "all_gather_ms": round(p[1], 3),
                   "compose_ms": round(p[2], 3)} for r, p in enumerate(per_rank)]
