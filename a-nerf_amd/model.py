@@ -113,8 +113,10 @@ class DeviceModel:
         (anerf_model_set_embed): the training tau schedule."""
         emb = _lib.EmbedParams()
         keep = []
-        emb.tau = float(_np(embed_sd["tau"]).reshape(-1)[0])
-        emb.tau_v = float(_np(embeddirs_sd["tau"]).reshape(-1)[0])
+        def scalar(v):  # (a host float passes as is: no device read)
+            return v if isinstance(v, float) else float(_np(v).reshape(-1)[0])
+        emb.tau = scalar(embed_sd["tau"])
+        emb.tau_v = scalar(embeddirs_sd["tau"])
         if cutoffs:
             a, b = _np(embed_sd["cutoff_dist"]), _np(embeddirs_sd["cutoff_dist"])
             keep += [a, b]

@@ -326,9 +326,30 @@ class _Embed(nn.Module):
         if self.freq_schedule:
             self.init_alpha = float(init_alpha)
             self.register_buffer("sched_alpha", torch.tensor(self.init_alpha))
+        self._hc = {}  # host copies of the scalar buffers: name -> ((data_ptr, version), value)
+
+    def host(self, name):
+        """The float value of scalar buffer `name`.  The schedule updates below write the host copy
+        with the buffer, so a training step reads nothing back from the device; a write they did
+        not make (load_state_dict, .to(), a caller's in-place edit) changes the buffer's identity or
+        version, and the value is read from the device once."""
+        t = getattr(self, name)
+        key = (t.data_ptr(), t._version)
+        c = self._hc.get(name)
+        if c is None or c[0] != key:
+            c = (key, float(t))
+            self._hc[name] = c
+        return c[1]
+
+    def _set(self, name, value):
+        """buffer `name` <- value (a 0-d float32 CPU tensor), host copy included."""
+        t = getattr(self, name)
+        with torch.no_grad():
+            t.copy_(value)
+        self._hc[name] = ((t.data_ptr(), t._version), float(value))
 
     def get_tau(self):
-        return self.tau.item()
+        return self.host("tau")
 
     def update_threshold(self, global_step, tau_step, tau_rate, alpha_step=None, alpha_target=None):
         self.update_tau(global_step, tau_step, tau_rate)
@@ -339,17 +360,16 @@ class _Embed(nn.Module):
         the reference's target is multires - 1 for every embedder, raycasters.py:737), in place."""
         if not self.freq_schedule:
             return
-        with torch.no_grad():
-            self.sched_alpha.copy_(torch.tensor(self.init_alpha + (target - self.init_alpha) * global_step
-                                                / float(step * 1000)))
+        self._set("sched_alpha", torch.tensor(self.init_alpha + (target - self.init_alpha) * global_step
+                                              / float(step * 1000)))
 
     def update_tau(self, global_step, step, rate):
         """tau = (20 * rate ** (global_step / (step * 1000))).clamp(max=2000), the reference's own
-        expression and dtype flow (cutoff_embedder.py:181-183), written into the buffer in place."""
-        with torch.no_grad():
-            new = (self.init_tau * torch.ones_like(self.tau) * rate ** (global_step / float(step * 1000))).clamp(
-                max=2000.)
-            self.tau.copy_(new)
+        expression and dtype flow (cutoff_embedder.py:181-183: float32 tensor times a Python float,
+        the same float32 arithmetic on the host as on the device), written into the buffer in place."""
+        new = (self.init_tau * torch.ones((), dtype=self.tau.dtype) * rate ** (global_step / float(step * 1000))).clamp(
+            max=2000.)
+        self._set("tau", new)
 
 
 class TrainRayCaster(nn.Module):
@@ -395,6 +415,7 @@ class TrainRayCaster(nn.Module):
         self._eval = None
         self._eval_version = None
         self._eval_embed = None
+        self._fs_cache = None  # (sched_alpha values, device feature scales)
 
     @property
     def module(self):
@@ -449,24 +470,36 @@ class TrainRayCaster(nn.Module):
         the current sched_alpha), on the device; None without a schedule."""
         if not self.cfg.freq_schedule:
             return None
-        s = feature_scales(self.cfg, float(self.embed_fn.sched_alpha), float(self.embeddirs_fn.sched_alpha))
-        return torch.from_numpy(s).to(self._dev)
+        a = (self.embed_fn.host("sched_alpha"), self.embeddirs_fn.host("sched_alpha"))
+        if self._fs_cache is None or self._fs_cache[0] != a or self._fs_cache[1].device != self._dev:
+            self._fs_cache = (a, torch.from_numpy(feature_scales(self.cfg, *a)).to(self._dev))
+        return self._fs_cache[1]
 
     def _embed_version(self):
-        return tuple((t.data_ptr(), t._version) for e in (self.embed_fn, self.embeddirs_fn)
-                     for t in (e.tau, e.cutoff_dist))
+        """(tau versions, cutoff_dist versions) of both embedders: the tau schedule moves the first
+        every step, the second only changes on a load or a caller's edit."""
+        es = (self.embed_fn, self.embeddirs_fn)
+        return (tuple((e.tau.data_ptr(), e.tau._version) for e in es),
+                tuple((e.cutoff_dist.data_ptr(), e.cutoff_dist._version) for e in es))
 
     def _embed_state(self):
-        return ({"tau": self.embed_fn.tau, "cutoff_dist": self.embed_fn.cutoff_dist},
-                {"tau": self.embeddirs_fn.tau, "cutoff_dist": self.embeddirs_fn.cutoff_dist})
+        return ({"tau": self.embed_fn.host("tau"), "cutoff_dist": self.embed_fn.cutoff_dist},
+                {"tau": self.embeddirs_fn.host("tau"), "cutoff_dist": self.embeddirs_fn.cutoff_dist})
+
+    def _sync_embed(self, model, seen):
+        """New tau / cutoff_dist into a DeviceModel without a repack; a tau-only change (the schedule,
+        every step) is a host-side field write, no device synchronisation or copy."""
+        v = self._embed_version()
+        if v != seen:
+            model.set_embed(*self._embed_state(), cutoffs=v[1] != seen[1])
+        return v
 
     def _constants(self):
         if self._consts is None:
             self._consts = DeviceModel(self.cfg, self.checkpoint(), device=self._dev.index)
             self._consts_embed = self._embed_version()
-        elif self._embed_version() != self._consts_embed:  # tau schedule: no repack
-            self._consts.set_embed(*self._embed_state())
-            self._consts_embed = self._embed_version()
+        else:
+            self._consts_embed = self._sync_embed(self._consts, self._consts_embed)
         return self._consts
 
     @property
@@ -483,9 +516,8 @@ class TrainRayCaster(nn.Module):
             self._eval = RayCaster(self.cfg, self.checkpoint(), device=self._dev.index)
             self._eval_version = v
             self._eval_embed = self._embed_version()
-        elif self._embed_version() != self._eval_embed:
-            self._eval.model.set_embed(*self._embed_state())
-            self._eval_embed = self._embed_version()
+        else:
+            self._eval_embed = self._sync_embed(self._eval.model, self._eval_embed)
         return self._eval
 
     def forward(self, *args, fwd_type="", **kwargs):

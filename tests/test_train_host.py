@@ -74,6 +74,47 @@ def test_tau_schedule_follows_update_tau():
     assert tr.module is tr
 
 
+def test_schedule_host_copies_and_tau_only_embed_updates():
+    """The tau / sched_alpha schedule keeps host copies (no device read per step), a write it did not
+    make is picked up (load_state_dict, in-place edits), and a tau-only change reaches a DeviceModel
+    as set_embed(cutoffs=False): no device synchronisation or copy."""
+    import argparse
+    g = Golden("t1_s32i16_d4w128")
+    tr = train.TrainRayCaster(g.cfg, g.ckpt, device="cpu")
+    args = argparse.Namespace(cutoff_step=250, cutoff_rate=10.0, freq_schedule_step=5, multires=7)
+    tr.update_embed_fns(123457, args)
+    assert tr.embed_fn.host("tau") == float(tr.embed_fn.tau)  # the host copy is the buffer's value
+    # the device expression of the reference (ones_like on the buffer) gives the same float32
+    ref = (20.0 * torch.ones_like(tr.embed_fn.tau) * 10.0 ** (123457 / 250000.0)).clamp(max=2000.)
+    assert float(ref) == tr.embed_fn.get_tau()
+    with torch.no_grad():
+        tr.embed_fn.tau.fill_(77.0)  # a write the schedule did not make
+    assert tr.embed_fn.get_tau() == 77.0
+    sd = tr.embeddirs_fn.state_dict()
+    sd["tau"] = torch.tensor(33.0)
+    tr.embeddirs_fn.load_state_dict(sd)
+    assert tr.embeddirs_fn.get_tau() == 33.0
+
+    class Rec:
+        def __init__(self):
+            self.calls = []
+
+        def set_embed(self, e, ev, cutoffs=True):
+            self.calls.append((e["tau"], ev["tau"], cutoffs))
+    m = Rec()
+    seen = tr._embed_version()
+    assert tr._sync_embed(m, seen) == seen and m.calls == []  # nothing changed
+    tr.update_embed_fns(250000, args)
+    seen = tr._sync_embed(m, seen)
+    assert len(m.calls) == 1 and m.calls[-1][2] is False  # tau only
+    assert m.calls[-1][:2] == (tr.embed_fn.get_tau(), tr.embeddirs_fn.get_tau())
+    assert isinstance(m.calls[-1][0], float)
+    with torch.no_grad():
+        tr.embed_fn.cutoff_dist.mul_(1.5)
+    seen = tr._sync_embed(m, seen)
+    assert m.calls[-1][2] is True and len(m.calls) == 2
+
+
 def test_checkpoint_is_tensors_and_round_trips(tmp_path):
     """checkpoint() holds CPU tensors in the reference's layout: torch.save -> torch.load(weights_only)
     -> nn.Module.load_state_dict on a fresh module (the reference's loader) and back."""
