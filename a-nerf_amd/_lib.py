@@ -29,7 +29,7 @@ PRECISIONS = {"fp32": ANERF_PREC_FP32, "bf16x3": ANERF_PREC_BF16X3, "bf16x6": AN
               "fp16x3": ANERF_PREC_FP16X3}
 
 
-ANERF_ENC_CUT_TO_DIST, ANERF_ENC_CUTOFF_SHIFT = 1, 2  # anerf_model_desc.encoder_flags
+ANERF_ENC_CUT_TO_DIST, ANERF_ENC_CUTOFF_SHIFT, ANERF_ENC_CUTOFF_BONES = 1, 2, 4  # anerf_model_desc.encoder_flags
 
 
 class ModelDesc(ctypes.Structure):
@@ -49,7 +49,8 @@ class NetWeights(ctypes.Structure):
 
 
 class EmbedParams(ctypes.Structure):
-    _fields_ = [("cutoff_dist", c_f), ("tau", ctypes.c_float), ("cutoff_dist_v", c_f), ("tau_v", ctypes.c_float)]
+    _fields_ = [("cutoff_dist", c_f), ("tau", ctypes.c_float), ("cutoff_dist_v", c_f), ("tau_v", ctypes.c_float),
+                ("cutoff_dist_b", c_f), ("tau_b", ctypes.c_float)]
 
 
 class Debug(ctypes.Structure):

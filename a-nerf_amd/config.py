@@ -44,6 +44,11 @@ class RenderConfig:
     # --normalize_cutoff reaches CutoffEmbedder only as an unused keyword ("normalize_cutoff", not
     # "normalize": core/raycasters.py:32 vs cutoff_embedder.py:64): a no-op in the reference, and here
     normalize_cutoff: bool = False
+    # --cutoff_bones: the bone embedder is a CutoffEmbedder with its own tau / cutoff_dist
+    # (core/raycasters.py:52-64, embedbones_state_dict); with multires_bones 0 it multiplies each
+    # bone direction by w_b = 1 - sigmoid(tau_b (dist - c_b)) when use_cutoff and cutoff_inputs
+    # (cutoff_embedder.py:156-166) and passes it through otherwise
+    cutoff_bones: bool = False
     chunk: int = 4096
     ext_scale: float = 0.001
     # MLP arithmetic: "fp32" (fp32 MFMA everywhere, the parity default), "bf16x6" (hidden layers as
@@ -78,15 +83,17 @@ class RenderConfig:
             raise ValueError(f"precision={self.precision!r}: 'fp32', 'bf16x6', 'fp16x3' or 'bf16x3'")
         if self.n_joints < 1 or self.n_joints > 128:
             raise NotImplementedError(f"n_joints={self.n_joints} outside [1, 128]")
-        for k in ("cutoff_bones",):
-            if self.extra.get(k):
-                raise NotImplementedError(f"--{k} is not implemented")
         for k, allowed in (("kp_dist_type", "reldist"), ("bone_type", "reldir"), ("view_type", "relray"),
                            ("pts_tr_type", "local")):
             v = self.extra.get(k, allowed)
             if v != allowed:
                 raise NotImplementedError(f"--{k}={v}: only {allowed} is implemented")
         return self
+
+    @property
+    def bone_window(self):
+        """--cutoff_bones makes the bone embedder a CutoffEmbedder (its state is in the checkpoint)."""
+        return bool(self.cutoff_bones and self.use_cutoff)
 
     @property
     def framecode_ch(self):
@@ -112,7 +119,7 @@ class RenderConfig:
     def from_args(cls, args, n_joints):
         """Build from a run_nerf.config_parser() namespace (or anything with those attributes)."""
         g = lambda k, d=None: getattr(args, k, d)  # noqa: E731
-        extra = {k: g(k) for k in ("cutoff_bones", "kp_dist_type", "bone_type", "view_type", "pts_tr_type",
+        extra = {k: g(k) for k in ("kp_dist_type", "bone_type", "view_type", "pts_tr_type",
                                    "cutoff_mm") if g(k) is not None}
         cfg = cls(n_joints=n_joints, netdepth=g("netdepth", 8), netwidth=g("netwidth", 256),
                   multires=g("multires", 7), multires_views=g("multires_views", 4),
@@ -126,7 +133,7 @@ class RenderConfig:
                   lindisp=bool(g("lindisp", False)), freq_schedule=bool(g("freq_schedule", False)),
                   init_freq=float(g("init_freq", 0.0) or 0.0), freq_schedule_step=int(g("freq_schedule_step", 5) or 5),
                   cut_to_dist=bool(g("cut_to_dist", False)), cutoff_shift=bool(g("cutoff_shift", False)),
-                  normalize_cutoff=bool(g("normalize_cutoff", False)),
+                  normalize_cutoff=bool(g("normalize_cutoff", False)), cutoff_bones=bool(g("cutoff_bones", False)),
                   chunk=g("chunk", 4096), ext_scale=g("ext_scale", 0.001), extra=extra)
         return cfg.validate()
 

@@ -163,12 +163,12 @@ struct DensityArgs {
     float* out;  // N raw densities
 };
 
-__host__ __device__ inline LdsPlan make_density_plan(int nj, int W, int D, int njh2) {
+__host__ __device__ inline LdsPlan make_density_plan(int nj, int W, int D, int njh2, bool bone_cut) {
     LdsPlan p;
     std::memset(&p, 0, sizeof(p));
     int o = 0;
     p.sk = o; o += 12 * nj;
-    p.cut = o; o += 3 * nj;
+    p.cut = o; o += (bone_cut ? 4 : 3) * nj;
     o = (o + 3) & ~3;
     p.bias = o; o += (D + 2) * W;
     p.uf_stride = 64 * 3 * njh2;
@@ -394,9 +394,11 @@ __device__ void encode_row(const ModelDev& M, const float* __restrict__ skts, fl
             f[(1 + 2 * fi) * nj + j] = s * w;
             f[(2 + 2 * fi) * nj + j] = c * w;
         }
-        f[nj * nv + 3 * j + 0] = qx / dn;
-        f[nj * nv + 3 * j + 1] = qy / dn;
-        f[nj * nv + 3 * j + 2] = qz / dn;
+        // bone directions, times w_b under --cutoff_bones (bone CutoffEmbedder, multires_bones 0)
+        const float wb = M.bone_cut ? cutoff_w(M.tau_b, dist, M.cutoff_b[j]) : 1.0f;
+        f[nj * nv + 3 * j + 0] = M.bone_cut ? (qx / dn) * wb : qx / dn;
+        f[nj * nv + 3 * j + 1] = M.bone_cut ? (qy / dn) * wb : qy / dn;
+        f[nj * nv + 3 * j + 2] = M.bone_cut ? (qz / dn) * wb : qz / dn;
         float ex, ey, ez;
         joint_rot(S, dx, dy, dz, ex, ey, ez);
         const float en = fmaxf(norm3(ex, ey, ez), 1e-12f);

@@ -659,6 +659,7 @@ __device__ __forceinline__ void ring_take(f32x2 (&slot)[RB], const float (&v)[16
 }
 
 // Window tables in LDS: cut[j] = c_j, cut[NJ + j] = c'_j (view directions), cut[2NJ + j] = thr2_j,
+// (with --cutoff_bones) cut[3NJ + j] = c^b_j (bone directions);
 // a conservative squared-distance bound of the window's support: w_j = 1 - 1/(1 + e),
 // e = expf(-tau (d - c_j)), is exactly 0 iff 1 + e rounds to 1, i.e. e <= 2^-24, i.e.
 // tau (d - c_j) >= 24 ln 2 = 16.6355 (up to expf's rounding).  With a 0.05 margin on that
@@ -671,9 +672,12 @@ __device__ __forceinline__ float live_thr2(float tau, float c) {
 }
 
 __device__ __forceinline__ void stage_cut(const ModelDev& M, float* __restrict__ cut, int tid) {
-    for (int j = tid; j < 3 * M.nj; j += blockDim.x) {
+    for (int j = tid; j < (M.bone_cut ? 4 : 3) * M.nj; j += blockDim.x) {
         const int k = j % M.nj;
-        cut[j] = j < M.nj ? M.cutoff[k] : (j < 2 * M.nj ? M.cutoff_v[k] : live_thr2(M.tau, M.cutoff[k]));
+        cut[j] = j < M.nj       ? M.cutoff[k]
+                 : j < 2 * M.nj ? M.cutoff_v[k]
+                 : j < 3 * M.nj ? live_thr2(M.tau, M.cutoff[k])
+                                : M.cutoff_b[k];
     }
 }
 
@@ -681,13 +685,14 @@ __device__ __forceinline__ void stage_cut(const ModelDev& M, float* __restrict__
 // LDS into registers two MFMA groups before use, so the encoder math never waits on LDS.
 struct JRow {
     f32x4 a, b, c;
-    float thr2, cv;
+    float thr2, cv, cb;
 };
 
-__device__ __forceinline__ JRow load_row(const float* __restrict__ sk, const float* __restrict__ cut, int j, int nj) {
+__device__ __forceinline__ JRow load_row(const float* __restrict__ sk, const float* __restrict__ cut, int j, int nj,
+                                         bool bone_cut) {
     const int jc = j < nj ? j : 0;
     const f32x4* p = reinterpret_cast<const f32x4*>(sk + 12 * jc);
-    return JRow{p[0], p[1], p[2], cut[2 * nj + jc], cut[nj + jc]};
+    return JRow{p[0], p[1], p[2], cut[2 * nj + jc], cut[nj + jc], bone_cut ? cut[3 * nj + jc] : 0.0f};
 }
 
 // bone direction u_j = q / max(|q|, 1e-12) of this lane's sample (q * rsq(max(|q|^2, 1e-24)),
@@ -713,6 +718,14 @@ __device__ __forceinline__ void u_joint(const ModelDev& M, const JRow& r, bool v
     u0 = qx * inv;
     u1 = qy * inv;
     u2 = qz * inv;
+    if (M.bone_cut) {  // --cutoff_bones: u_j w_b (uniform branch), w_b = 1 - sigmoid(tau_b (|q| - c^b_j))
+        const float wb = 1.0f - __builtin_amdgcn_rcpf(
+                                    1.0f + __builtin_amdgcn_exp2f(-(M.tau_b * (__builtin_amdgcn_sqrtf(d2) - r.cb)) *
+                                                                  1.44269504f));
+        u0 *= wb;
+        u1 *= wb;
+        u2 *= wb;
+    }
     live = valid & (!M.sparse | !(d2 >= r.thr2));  // (no short-circuit: no branch; NaN -> live)
     if constexpr (WV) {
         const float d = __builtin_amdgcn_sqrtf(d2);
@@ -744,7 +757,7 @@ __device__ __forceinline__ void u_part(f32x16 (&acc)[RB], const ModelDev& M, con
     float f[6];
     bool lv0, lv1;
     const int nj = M.nj, j0 = hh * njh2;
-    JRow ra = load_row(sk, cut, j0, nj), rb2 = load_row(sk, cut, j0 + 1, nj);
+    JRow ra = load_row(sk, cut, j0, nj, M.bone_cut != 0), rb2 = load_row(sk, cut, j0 + 1, nj, M.bone_cut != 0);
     float wv0, wv1;
     u_joint<WV>(M, ra, j0 < nj, px, py, pz, f[0], f[1], f[2], lv0, wv0);
     u_joint<WV>(M, rb2, j0 + 1 < nj, px, py, pz, f[3], f[4], f[5], lv1, wv1);
@@ -752,8 +765,8 @@ __device__ __forceinline__ void u_part(f32x16 (&acc)[RB], const ModelDev& M, con
         wvo[lane] = wv0;
         wvo[64 + lane] = wv1;
     }
-    ra = load_row(sk, cut, j0 + 2, nj);
-    rb2 = load_row(sk, cut, j0 + 3, nj);
+    ra = load_row(sk, cut, j0 + 2, nj, M.bone_cut != 0);
+    rb2 = load_row(sk, cut, j0 + 3, nj, M.bone_cut != 0);
     STAMP(st, 14);
     for (int pp = 0; pp < npp; ++pp) {
         if (mask) {
@@ -792,14 +805,14 @@ __device__ __forceinline__ void u_part(f32x16 (&acc)[RB], const ModelDev& M, con
                 u_joint<WV>(M, ra, j0 + 2 * pp + 2 < nj, px, py, pz, fn[0], fn[1], fn[2], ln0, wv);
                 pin(fn[0]), pin(fn[1]), pin(fn[2]), pin(ln0);
                 if constexpr (WV) wvo[min(2 * pp + 2, njh2) * 64 + lane] = wv;  // (row njh2: discard)
-                ra = load_row(sk, cut, j0 + 2 * pp + 4, nj);
+                ra = load_row(sk, cut, j0 + 2 * pp + 4, nj, M.bone_cut != 0);
             }
             if (g == 1) {
                 float wv;
                 u_joint<WV>(M, rb2, j0 + 2 * pp + 3 < nj, px, py, pz, fn[3], fn[4], fn[5], ln1, wv);
                 pin(fn[3]), pin(fn[4]), pin(fn[5]), pin(ln1);
                 if constexpr (WV) wvo[min(2 * pp + 3, njh2) * 64 + lane] = wv;
-                rb2 = load_row(sk, cut, j0 + 2 * pp + 5, nj);
+                rb2 = load_row(sk, cut, j0 + 2 * pp + 5, nj, M.bone_cut != 0);
             }
             interleave_mfma_valu<2 * RB, 8>();
         }
@@ -857,9 +870,9 @@ __device__ __forceinline__ void u_features_lds(const ModelDev& M, const float* _
                                                JointMask* mask, float* __restrict__ uf, float* __restrict__ wvo) {
     const int hh = lane >> 5, njh2 = M.njh2, nj = M.nj, j0 = hh * njh2;
     uint64_t m0 = 0, m1 = 0;
-    JRow r = load_row(sk, cut, j0, nj);
+    JRow r = load_row(sk, cut, j0, nj, M.bone_cut != 0);
     for (int p = 0; p < njh2; ++p) {
-        const JRow rn = load_row(sk, cut, j0 + min(p + 1, njh2 - 1), nj);
+        const JRow rn = load_row(sk, cut, j0 + min(p + 1, njh2 - 1), nj, M.bone_cut != 0);
         float u0, u1, u2, wv;
         bool live;
         u_joint<WV>(M, r, j0 + p < nj, px, py, pz, u0, u1, u2, live, wv);
@@ -1042,31 +1055,46 @@ __device__ __forceinline__ void v_part(f32x16 (&acc)[RB], const ModelDev& M, con
 // joint p (lane half 0) with joint p + NJH2 (half 1), exactly the u part's pairing, so w'_j comes
 // from the u part (wvp, stored per lane); k-step NJH2 adds the bias / framecode column NJ.  The G
 // values of the next k-step are read under the current k-step's MFMAs.
+// k-steps whose two joints have w'_j == 0 at every sample of the ray (bits of `live`, from
+// compute_view_factor) add exact zeros and are skipped; returns the k-steps run (MFMA tally).
 template <int RBV>
-__device__ __forceinline__ void view_dir_part(f32x16 (&acc)[RBV], const ModelDev& M, const float* __restrict__ G,
-                                              const float* __restrict__ wvp, int lane, float bs = 1.0f) {
+__device__ __forceinline__ int view_dir_part(f32x16 (&acc)[RBV], const ModelDev& M, const float* __restrict__ G,
+                                             const float* __restrict__ wvp, const unsigned* __restrict__ live,
+                                             int lane, float bs = 1.0f) {
     constexpr int WH = RBV * 32;
     const int hh = lane >> 5, sl = lane & 31;
     const int njh2 = M.njh2;
+    const uint64_t L0 = uniform64((uint64_t)live[0] | ((uint64_t)live[1] << 32));
+    const uint64_t L1 = uniform64((uint64_t)live[2] | ((uint64_t)live[3] << 32));
+    auto bit = [&](int j) { return ((j < 64 ? L0 >> j : L1 >> (j - 64)) & 1ull) != 0; };
+    auto next_p = [&](int p) {  // the next k-step with a live joint (njh2: the bias / code step)
+        while (p < njh2 && !bit(p) && !bit(p + njh2)) ++p;
+        return p;
+    };
     auto col = [&](int p) { return p < njh2 ? p + hh * njh2 : M.nj + hh; };
+    int p = next_p(0), steps = 0;
     float gv[RBV];
 #pragma unroll
-    for (int rb = 0; rb < RBV; ++rb) gv[rb] = G[col(0) * WH + sl + 32 * rb];
+    for (int rb = 0; rb < RBV; ++rb) gv[rb] = G[col(p) * WH + sl + 32 * rb];
     // (bs: the units of acc, 2^es for the fp16x3 view layer: the B operands carry it)
-    float b = wvp[lane] * bs;
-    for (int p = 0; p <= njh2; ++p) {
+    float b = p < njh2 ? wvp[p * 64 + lane] * bs : (hh ? 0.0f : bs);
+    while (true) {
         __builtin_amdgcn_sched_barrier(0);
-        const int pn = min(p + 1, njh2);
+        const int pn = p < njh2 ? next_p(p + 1) : njh2;
         float gn[RBV];
 #pragma unroll
         for (int rb = 0; rb < RBV; ++rb) gn[rb] = G[col(pn) * WH + sl + 32 * rb];
         const float bn = pn < njh2 ? wvp[pn * 64 + lane] * bs : (hh ? 0.0f : bs);
 #pragma unroll
         for (int rb = 0; rb < RBV; ++rb) acc[rb] = mfma_f32_32x32x2(gv[rb], b, acc[rb]);
+        ++steps;
+        if (p == njh2) break;
 #pragma unroll
         for (int rb = 0; rb < RBV; ++rb) gv[rb] = gn[rb];
         b = bn;
+        p = pn;
     }
+    return steps;
 }
 
 // Encoder + density trunk of one 32-sample block: L0 (u and v parts), the hidden layers with the
@@ -1201,7 +1229,8 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
     STAMP(st, 16);
     sig += __shfl_xor(sig, 32);
     sig += net.balpha;
-    view_dir_part<RBV>(av, M, G, wvp, lane, P == 3 ? pow2f(es) : 1.0f);
+    const int vsteps = view_dir_part<RBV>(av, M, G, wvp, reinterpret_cast<const unsigned*>(ray) + 12, lane,
+                                          P == 3 ? pow2f(es) : 1.0f);
     STAMP(st, 17);
     float rgb[3];
 #pragma unroll
@@ -1221,7 +1250,7 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
         const int act = __builtin_popcountll(mask.m0) + __builtin_popcountll(mask.m1);
         const bool ux6 = (P >= 2) && (RB % 4 == 0) && uf != nullptr && M.ux6;  // as in mlp_trunk
         const int xk = (ux6 ? 0 : 3 * M.njh2) + act * VPart<MR>::KB;   // f32 k-steps of one x part
-        long long k = (long long)xk * RB + (long long)(M.njh2 + 1) * RBV;
+        long long k = (long long)xk * RB + (long long)vsteps * RBV;
         if (ux6) {
             const int nx = (M.skip + 1 < M.D) ? 2 : 1;
             atomicAdd(mfma_count + 1, (unsigned long long)(nx * ((3 * M.njh2 + 7) / 8) * RB * 6));

@@ -73,6 +73,11 @@ int anerf_model_create(const anerf_model_desc* desc, const anerf_net_weights* co
     if (!coarse || !embed) return fail(ANERF_EINVAL, "coarse weights / embed params are NULL");
     if (desc->has_fine && !fine) return fail(ANERF_EINVAL, "has_fine but fine weights are NULL");
     if (!embed->cutoff_dist || !embed->cutoff_dist_v) return fail(ANERF_EINVAL, "cutoff_dist is NULL");
+    // --cutoff_bones windows the bone directions only through a CutoffEmbedder that weights its input
+    // (use_cutoff, cutoff_inputs; multires_bones 0), as in core/cutoff_embedder.py:156-166
+    const bool bone_cut = (desc->encoder_flags & ANERF_ENC_CUTOFF_BONES) && desc->use_cutoff && desc->cutoff_inputs;
+    if (bone_cut && !embed->cutoff_dist_b)
+        return fail(ANERF_EINVAL, "ANERF_ENC_CUTOFF_BONES: embed->cutoff_dist_b (embedbones_fn.cutoff_dist) is NULL");
     const int nj = desc->n_joints;
     const int njh2 = (((nj + 1) / 2) + 1) & ~1;  // joint pairs of the u part, even
     const int ngh = std::max(2 * njh2, nj + 2) / 2;  // G columns / 2: joint p + h*NJH2 at k-step p, bias at NJ
@@ -86,6 +91,8 @@ int anerf_model_create(const anerf_model_desc* desc, const anerf_net_weights* co
     }
     const size_t off_cut = pk.add(std::vector<float>(embed->cutoff_dist, embed->cutoff_dist + nj));
     const size_t off_cutv = pk.add(std::vector<float>(embed->cutoff_dist_v, embed->cutoff_dist_v + nj));
+    const size_t off_cutb = pk.add(bone_cut ? std::vector<float>(embed->cutoff_dist_b, embed->cutoff_dist_b + nj)
+                                            : std::vector<float>(nj, 0.0f));
 
     int prev = 0;
     HIP_TRY(hipGetDevice(&prev));
@@ -133,10 +140,13 @@ int anerf_model_create(const anerf_model_desc* desc, const anerf_net_weights* co
     md.h3_top = 127 + h3_target();
     md.shift = desc->softplus_shift;
     md.B = desc->density_scale;
+    md.bone_cut = bone_cut ? 1 : 0;
     md.tau = embed->tau;
     md.tau_v = embed->tau_v;
+    md.tau_b = bone_cut ? embed->tau_b : 0.0f;
     md.cutoff = dbuf + off_cut;
     md.cutoff_v = dbuf + off_cutv;
+    md.cutoff_b = dbuf + off_cutb;
     bind_net(desc, dbuf, oc, coarse->alpha_b[0], md.net[0]);
     if (desc->has_fine) bind_net(desc, dbuf, of, fine->alpha_b[0], md.net[1]);
     else md.net[1] = md.net[0];
@@ -156,7 +166,8 @@ size_t anerf_model_bytes(const anerf_model* m) { return m ? m->dev_bytes : 0; }
 
 int anerf_model_set_embed(anerf_model* m, const anerf_embed_params* embed) {
     if (!m || !embed) return fail(ANERF_EINVAL, "anerf_model_set_embed: NULL argument");
-    if (embed->cutoff_dist || embed->cutoff_dist_v) {
+    const bool cb = m->md.bone_cut && embed->cutoff_dist_b;
+    if (embed->cutoff_dist || embed->cutoff_dist_v || cb) {
         const size_t nb = sizeof(float) * (size_t)m->desc.n_joints;
         int prev = 0;
         HIP_TRY(hipGetDevice(&prev));
@@ -166,11 +177,14 @@ int anerf_model_set_embed(anerf_model* m, const anerf_embed_params* embed) {
             e = hipMemcpy(const_cast<float*>(m->md.cutoff), embed->cutoff_dist, nb, hipMemcpyHostToDevice);
         if (e == hipSuccess && embed->cutoff_dist_v)
             e = hipMemcpy(const_cast<float*>(m->md.cutoff_v), embed->cutoff_dist_v, nb, hipMemcpyHostToDevice);
+        if (e == hipSuccess && cb)
+            e = hipMemcpy(const_cast<float*>(m->md.cutoff_b), embed->cutoff_dist_b, nb, hipMemcpyHostToDevice);
         (void)hipSetDevice(prev);
         if (e != hipSuccess) return fail(ANERF_EHIP, std::string("anerf_model_set_embed: ") + hipGetErrorString(e));
     }
     m->md.tau = embed->tau;
     m->md.tau_v = embed->tau_v;
+    if (m->md.bone_cut) m->md.tau_b = embed->tau_b;
     return ANERF_OK;
 }
 
@@ -290,11 +304,11 @@ int anerf_render_rays(const anerf_model* m, const float* ray_batch, int32_t ray_
     R = std::min(R, 8);
     const int W = m->desc.net_width;
     const int nj = m->desc.n_joints, mrv = m->desc.multires_views, D = m->desc.net_depth;
-    LdsPlan P = make_plan(R, nj, W, S, T, mrv, m->ngh, D, m->njh2, true);
-    if (P.total * 4 > 160 * 1024) P = make_plan(R, nj, W, S, T, mrv, m->ngh, D, m->njh2, false);
+    LdsPlan P = make_plan(R, nj, W, S, T, mrv, m->ngh, D, m->njh2, true, m->md.bone_cut != 0);
+    if (P.total * 4 > 160 * 1024) P = make_plan(R, nj, W, S, T, mrv, m->ngh, D, m->njh2, false, m->md.bone_cut != 0);
     while (R > 1 && P.total * 4 > 160 * 1024) {
         R /= 2;
-        P = make_plan(R, nj, W, S, T, mrv, m->ngh, D, m->njh2, false);
+        P = make_plan(R, nj, W, S, T, mrv, m->ngh, D, m->njh2, false, m->md.bone_cut != 0);
     }
     if (P.total * 4 > 160 * 1024) return fail(ANERF_EINVAL, "configuration exceeds the 160 KiB LDS budget");
 
@@ -580,7 +594,7 @@ static int launch_density(const anerf_model* m, DensityArgs a, int32_t precision
     if (a.net == 1 && m->desc.single_net) a.net = 0;  // network_fine is network_fn
     if (a.net > 1 || (a.net == 1 && !m->desc.has_fine)) return fail(ANERF_EINVAL, "no such network");
     const int W = m->desc.net_width, mr = m->desc.multires;
-    const LdsPlan P = make_density_plan(m->desc.n_joints, W, m->desc.net_depth, m->njh2);
+    const LdsPlan P = make_density_plan(m->desc.n_joints, W, m->desc.net_depth, m->njh2, m->md.bone_cut != 0);
     if (P.total * 4 > 160 * 1024) return fail(ANERF_EINVAL, "configuration exceeds the 160 KiB LDS budget");
     const int64_t nb = (a.n + 31) / 32;
     const unsigned grid = (unsigned)std::min<int64_t>((nb + 3) / 4, 256 * 32);

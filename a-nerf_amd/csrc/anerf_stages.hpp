@@ -14,11 +14,54 @@ __device__ void compute_view_factor(const ModelDev& M, const NetDev& net, float*
     constexpr int KC = 3 * NK;
     constexpr int NPART = 256 / WH;
     const int nj = M.nj;
+    const int kfw0 = M.cutoff_inputs ? 0 : 1;
+    // Per-ray live view windows (ray slot words 12..15, a bit per joint).  w'_j = 1 - sigmoid(tau'
+    // (d - c'_j)) is exactly 0 at a sample with d^2 >= live_thr2(tau', c'_j) (the margins of
+    // live_thr2); the samples of a ray lie on the segment o + z d, z in [near, far], so a joint whose
+    // closest approach to the segment is beyond that bound (+0.1 % for the rounding of the samples'
+    // points and transforms) has w'_j == 0 at every sample: its G column and its k-step of the view
+    // layer's direction part only ever add exact zeros and are skipped (bit-identical results).
+    // Only when every direction term is windowed (the usual flags); otherwise every joint is live.
+    const bool cull = M.cutoff_viewdir && kfw0 == 0;
+    for (int i = tid; i < nr * 4; i += blockDim.x)
+        reinterpret_cast<unsigned*>(lds + P.ray + 16 * (i >> 2))[12 + (i & 3)] = cull ? 0u : 0xffffffffu;
+    __syncthreads();
+    if (cull)
+        for (int idx = tid; idx < nr * nj; idx += blockDim.x) {
+            const int r = idx / nj, j = idx % nj;
+            const float* ray = lds + P.ray + 16 * r;
+            const float* S = lds + P.sk + P.sk_stride * r + 12 * j;
+            float ax, ay, az, bx, by, bz;
+            joint_local(S, ray[0], ray[1], ray[2], ax, ay, az);
+            joint_rot(S, ray[3], ray[4], ray[5], bx, by, bz);
+            const float nearv = ray[7], farv = ray[8];
+            const float bb = fmaf(bz, bz, fmaf(by, by, bx * bx));
+            float t = bb > 0.0f ? -fmaf(az, bz, fmaf(ay, by, ax * bx)) / bb : nearv;
+            t = fminf(fmaxf(t, nearv), farv);
+            const float qx = fmaf(t, bx, ax), qy = fmaf(t, by, ay), qz = fmaf(t, bz, az);
+            const float d2 = fmaf(qz, qz, fmaf(qy, qy, qx * qx));
+            const float thr = live_thr2(M.tau_v, lds[P.cut + nj + j]);
+            // (NaN near / far / transforms: live)
+            const bool live = !(nearv <= farv) || !(d2 >= thr * 1.001f);
+            if (live) atomicOr(reinterpret_cast<unsigned*>(lds + P.ray + 16 * r) + 12 + (j >> 5), 1u << (j & 31));
+        }
+    __syncthreads();
+    // the union over the workgroup's rays: G columns are computed (and trig rows filled) for it
+    uint64_t U0 = 0, U1 = 0;
+    for (int r = 0; r < nr; ++r) {
+        const unsigned* w = reinterpret_cast<const unsigned*>(lds + P.ray + 16 * r) + 12;
+        U0 |= (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+        U1 |= (uint64_t)w[2] | ((uint64_t)w[3] << 32);
+    }
+    U0 = uniform64(U0);
+    U1 = uniform64(U1);
+    auto live_col = [&](int c) { return ((c < 64 ? U0 >> c : U1 >> (c - 64)) & 1ull) != 0; };
     // trig table Tt[j][k*3 + c] (27 values, padded to 28) of the normalised joint-frame ray
     // directions, one (ray, joint, coordinate) per thread
     constexpr int TP = (KC + 3) & ~3;
     for (int idx = tid; idx < nr * nj * 3; idx += blockDim.x) {
         const int r = idx / (nj * 3), j = (idx / 3) % nj, c = idx % 3;
+        if (!live_col(j)) continue;
         const float* ray = lds + P.ray + 16 * r;
         const float* S = lds + P.sk + P.sk_stride * r + 12 * j;
         float ex, ey, ez;
@@ -57,10 +100,19 @@ __device__ void compute_view_factor(const ModelDev& M, const NetDev& net, float*
                 dst[4 * q] = x[0], dst[4 * q + 1] = x[1], dst[4 * q + 2] = x[2], dst[4 * q + 3] = x[3];
             }
         };
-        int c = part;
+        // this thread's columns c = part (mod NPART): dead ones (for every ray) are zeroed, live
+        // ones computed, the next live column's weights loaded under the current one
+        for (int cz = part; cz < nj; cz += NPART)
+            if (!live_col(cz))
+                for (int r = 0; r < nr; ++r) lds[P.g + P.g_stride * r + cz * WH + nn] = 0.0f;
+        auto next_col = [&](int c) {
+            while (c < nj && !live_col(c)) c += NPART;
+            return c;
+        };
+        int c = next_col(part);
         if (c < nj) load_col(wc, c);
-        for (; c < nj; c += NPART) {
-            const int cn = c + NPART;
+        for (; c < nj;) {
+            const int cn = next_col(c + NPART);
             if (cn < nj) load_col(wn, cn);
             for (int r0 = 0; r0 < nr; r0 += 4) {
                 float v[4] = {0.0f, 0.0f, 0.0f, 0.0f}, u[4] = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -102,6 +154,7 @@ __device__ void compute_view_factor(const ModelDev& M, const NetDev& net, float*
             }
 #pragma unroll
             for (int kc = 0; kc < TP; ++kc) wc[kc] = wn[kc];
+            c = cn;
         }
     }
     __syncthreads();

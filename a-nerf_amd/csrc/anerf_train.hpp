@@ -51,9 +51,11 @@ __device__ __forceinline__ void encode_joint(const ModelDev& M, const float* __r
         f[(1 + 2 * fi) * nj + j] = s * w;
         f[(2 + 2 * fi) * nj + j] = c * w;
     }
-    f[nj * nv + 3 * j + 0] = qx / dn;
-    f[nj * nv + 3 * j + 1] = qy / dn;
-    f[nj * nv + 3 * j + 2] = qz / dn;
+    // bone directions, times w_b under --cutoff_bones (bone CutoffEmbedder, multires_bones 0)
+    const float wb = M.bone_cut ? cutoff_w(M.tau_b, dist, M.cutoff_b[j]) : 1.0f;
+    f[nj * nv + 3 * j + 0] = M.bone_cut ? (qx / dn) * wb : qx / dn;
+    f[nj * nv + 3 * j + 1] = M.bone_cut ? (qy / dn) * wb : qy / dn;
+    f[nj * nv + 3 * j + 2] = M.bone_cut ? (qz / dn) * wb : qz / dn;
     float ex, ey, ez;
     joint_rot(S, dx, dy, dz, ex, ey, ez);
     const float en = fmaxf(norm3(ex, ey, ez), 1e-12f);
@@ -158,10 +160,19 @@ __device__ __forceinline__ void encode_row_grad_joint(const ModelDev& M, const f
         g_dist += (gs * c - gc * s) * w * fr * duf;
     }
     if (cut) g_dist += g_w * (-M.tau * w * (1.0f - w));
-    // ---- bone direction u = q / max(|q|, eps)
+    // ---- bone direction u = q / max(|q|, eps) (times w_b under --cutoff_bones)
     float gqx, gqy, gqz;
     {
-        const float gux = gu_[0], guy = gu_[1], guz = gu_[2];
+        float gux = gu_[0], guy = gu_[1], guz = gu_[2];
+        if (M.bone_cut) {  // f = u w_b: dL/du = g w_b, dL/dw_b = g . u
+            const float wb = cutoff_w(M.tau_b, dist, M.cutoff_b[j]);
+            const float dn = fmaxf(dist, 1e-12f);
+            const float g_wb = gux * (qx / dn) + guy * (qy / dn) + guz * (qz / dn);
+            g_dist += g_wb * (-M.tau_b * wb * (1.0f - wb));
+            gux *= wb;
+            guy *= wb;
+            guz *= wb;
+        }
         if (dist > 1e-12f) {
             const float ux = qx / dist, uy = qy / dist, uz = qz / dist;
             const float dot = ux * gux + uy * guy + uz * guz;

@@ -72,9 +72,11 @@ struct ModelDev {
     int single_net;  // one network for both passes; the fine pass evaluates only the I new samples
     int cut_to, shift_in;  // kp encoder input transforms (ANERF_ENC_CUT_TO_DIST / _CUTOFF_SHIFT)
     int h3_top;      // fp16x3: biased exponent the largest scaled activation of a sample gets (127 + 10)
-    float shift, B, tau, tau_v;
+    int bone_cut;    // --cutoff_bones (+ use_cutoff, cutoff_inputs): bone directions times w_b
+    float shift, B, tau, tau_v, tau_b;
     const float* cutoff;
     const float* cutoff_v;
+    const float* cutoff_b;
     NetDev net[2];
 };
 
@@ -115,7 +117,7 @@ __device__ __forceinline__ void kp_inputs(int cut_to, int shift_in, float dist, 
 }
 
 __host__ __device__ inline LdsPlan make_plan(int R, int nj, int W, int S, int T, int mrv, int ngh, int D, int njh2,
-                                             bool with_uf) {
+                                             bool with_uf, bool bone_cut) {
     LdsPlan p;
     const int wh = W / 2;
     const int nk = 1 + 2 * mrv;
@@ -136,7 +138,8 @@ __host__ __device__ inline LdsPlan make_plan(int R, int nj, int W, int S, int T,
     p.scr = o; o += p.scr_stride * R;
     o = (o + 3) & ~3;
     p.bias = o; o += (D + 2) * W;  // the current net's hidden + feature biases, accumulator order; w_alpha
-    p.cut = o; o += 3 * nj;        // window: cutoff distances (points, view directions), live thresholds
+    p.cut = o; o += (bone_cut ? 4 : 3) * nj;  // windows: cutoffs (points, view directions), live thresholds
+                                               // (, bone cutoffs)
     o = (o + 3) & ~3;
     p.uf_stride = 64 * 3 * njh2;   // per wave: the L0 bone directions, re-read by the skip layer
     p.uf = with_uf ? o : -1;

@@ -54,7 +54,8 @@ class DeviceModel:
             fine_sd = None
         d.single_net = int(cfg.single_net)
         d.encoder_flags = ((_lib.ANERF_ENC_CUT_TO_DIST if cfg.cut_to_dist else 0) |
-                           (_lib.ANERF_ENC_CUTOFF_SHIFT if cfg.cutoff_shift else 0))
+                           (_lib.ANERF_ENC_CUTOFF_SHIFT if cfg.cutoff_shift else 0) |
+                           (_lib.ANERF_ENC_CUTOFF_BONES if cfg.cutoff_bones else 0))
         d.has_fine = int(fine_sd is not None and cfg.N_importance > 0)
         self.has_fine = bool(d.has_fine)
         e, ev = ckpt["embed_state_dict"], ckpt["embeddirs_state_dict"]
@@ -72,6 +73,11 @@ class DeviceModel:
         emb = _lib.EmbedParams()
         emb.cutoff_dist, emb.tau = self._p(e["cutoff_dist"]), float(_np(e["tau"]).reshape(-1)[0])
         emb.cutoff_dist_v, emb.tau_v = self._p(ev["cutoff_dist"]), float(_np(ev["tau"]).reshape(-1)[0])
+        if cfg.bone_window:  # --cutoff_bones: the bone CutoffEmbedder's state (embedbones_state_dict)
+            eb = ckpt.get("embedbones_state_dict") or {}
+            if "cutoff_dist" not in eb or "tau" not in eb:
+                raise ValueError("cutoff_bones: the checkpoint's embedbones_state_dict has no cutoff_dist / tau")
+            emb.cutoff_dist_b, emb.tau_b = self._p(eb["cutoff_dist"]), float(_np(eb["tau"]).reshape(-1)[0])
         h = ctypes.c_void_p()
         rc = lib.anerf_model_create(ctypes.byref(d), ctypes.byref(coarse), ctypes.byref(fine) if fine else None,
                                     ctypes.byref(emb), self.device, ctypes.byref(h))
@@ -108,9 +114,9 @@ class DeviceModel:
         w.codes = self._p(sd["framecodes.codes.weight"]) if cfg.opt_framecode else None
         return w
 
-    def set_embed(self, embed_sd, embeddirs_sd, cutoffs=True):
-        """New tau (and cutoff_dist) of the two embedders without repacking the weights
-        (anerf_model_set_embed): the training tau schedule."""
+    def set_embed(self, embed_sd, embeddirs_sd, cutoffs=True, embedbones_sd=None):
+        """New tau (and cutoff_dist) of the embedders (the bone one with --cutoff_bones) without
+        repacking the weights (anerf_model_set_embed): the training tau schedule."""
         emb = _lib.EmbedParams()
         keep = []
         def scalar(v):  # (a host float passes as is: no device read)
@@ -121,6 +127,12 @@ class DeviceModel:
             a, b = _np(embed_sd["cutoff_dist"]), _np(embeddirs_sd["cutoff_dist"])
             keep += [a, b]
             emb.cutoff_dist, emb.cutoff_dist_v = a.ctypes.data_as(_lib.c_f), b.ctypes.data_as(_lib.c_f)
+        if embedbones_sd is not None:
+            emb.tau_b = scalar(embedbones_sd["tau"])
+            if cutoffs:
+                c = _np(embedbones_sd["cutoff_dist"])
+                keep.append(c)
+                emb.cutoff_dist_b = c.ctypes.data_as(_lib.c_f)
         _lib.check(_lib.load().anerf_model_set_embed(self.handle, ctypes.byref(emb)), "anerf_model_set_embed")
 
     @property

@@ -199,10 +199,12 @@ def make_embed_state(n_joints, cutoff=0.5, tau=20.0, jitter=0.0, seed=0):
 
 def make_checkpoint(seed, n_joints=24, D=8, W=256, fine=True, tau=20.0, tau_views=None,
                     cutoff_jitter=0.05, alpha_bias=0.5, alpha_gain=30.0, rgb_gain=8.0,
-                    use_framecode=False, n_framecodes=0, multires=7, multires_views=4, sched_alpha=None):
+                    use_framecode=False, n_framecodes=0, multires=7, multires_views=4, sched_alpha=None,
+                    cutoff_bones=False, tau_bones=None):
     """A full RayCaster checkpoint dict with the key layout of RayCaster.state_dict()
-    (core/raycasters.py:752-766); sched_alpha: the --freq_schedule buffer of both cutoff embedders
-    (core/cutoff_embedder.py:97-99), absent when None."""
+    (core/raycasters.py:752-766); sched_alpha: the --freq_schedule buffer of the cutoff embedders
+    (core/cutoff_embedder.py:97-99), absent when None; cutoff_bones: the bone embedder is a
+    CutoffEmbedder (--cutoff_bones, raycasters.py:52-64) with its own state."""
     ck = {
         "network_fn_state_dict": make_nerf_state(seed, n_joints, D, W, multires, multires_views,
                                                  use_framecode=use_framecode,
@@ -213,8 +215,11 @@ def make_checkpoint(seed, n_joints=24, D=8, W=256, fine=True, tau=20.0, tau_view
         "embeddirs_state_dict": make_embed_state(n_joints, tau=tau if tau_views is None else tau_views,
                                                  jitter=cutoff_jitter, seed=seed + 202),
     }
+    if cutoff_bones:
+        ck["embedbones_state_dict"] = make_embed_state(n_joints, tau=tau if tau_bones is None else tau_bones,
+                                                       jitter=cutoff_jitter, seed=seed + 303)
     if sched_alpha is not None:
-        for k in ("embed_state_dict", "embeddirs_state_dict"):
+        for k in ("embed_state_dict", "embeddirs_state_dict") + (("embedbones_state_dict",) if cutoff_bones else ()):
             ck[k]["sched_alpha"] = np.array(sched_alpha, dtype=np.float32)
     if fine:
         ck["network_fine_state_dict"] = make_nerf_state(seed + 1, n_joints, D, W, multires, multires_views,

@@ -403,6 +403,9 @@ class TrainRayCaster(nn.Module):
         alpha0 = cfg.init_freq if cfg.freq_schedule else None
         self.embed_fn = _Embed(cfg.n_joints, cut, alpha0)
         self.embeddirs_fn = _Embed(cfg.n_joints, cut, alpha0)
+        # --cutoff_bones: the bone embedder is a CutoffEmbedder too (raycasters.py:52-64), with its own
+        # tau schedule (update_embed_fns, :745-747); otherwise it has no state
+        self.embedbones_fn = _Embed(cfg.n_joints, cut, alpha0) if cfg.bone_window else None
         for net in (self.network_fn, self.network_fine):
             if net is not None:
                 net.mlp = mlp
@@ -428,9 +431,12 @@ class TrainRayCaster(nn.Module):
         args.cutoff_rate) and, with --freq_schedule, their sched_alpha (args.freq_schedule_step,
         target multires - 1); the kernels pick the new tau up at the next launch, the new schedule
         weights at the next feature product."""
-        for e in (self.embed_fn, self.embeddirs_fn):
+        for e in self._embedders():
             e.update_threshold(global_step, args.cutoff_step, args.cutoff_rate,
                                getattr(args, "freq_schedule_step", 5), getattr(args, "multires", 7) - 1)
+
+    def _embedders(self):
+        return (self.embed_fn, self.embeddirs_fn) + ((self.embedbones_fn,) if self.embedbones_fn is not None else ())
 
     # -- checkpoints in the reference's key layout (raycasters.py:752-788)
     def load_checkpoint(self, ck):
@@ -440,7 +446,10 @@ class TrainRayCaster(nn.Module):
         # (single_net: the same module again; the fine keys load last and win, as in raycasters.py:768-788)
         if self.network_fine is not None and "network_fine_state_dict" in ck:
             self.network_fine.load_state_dict({k: t(v) for k, v in ck["network_fine_state_dict"].items()})
-        for mod, key in ((self.embed_fn, "embed_state_dict"), (self.embeddirs_fn, "embeddirs_state_dict")):
+        mods = [(self.embed_fn, "embed_state_dict"), (self.embeddirs_fn, "embeddirs_state_dict")]
+        if self.embedbones_fn is not None:
+            mods.append((self.embedbones_fn, "embedbones_state_dict"))
+        for mod, key in mods:
             mod.load_state_dict({k: t(v) for k, v in ck[key].items()})
         self._consts = None
         self._eval = None
@@ -451,7 +460,8 @@ class TrainRayCaster(nn.Module):
         def sd(m):
             return {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
         ck = {"network_fn_state_dict": sd(self.network_fn), "embed_state_dict": sd(self.embed_fn),
-              "embedbones_state_dict": {}, "embeddirs_state_dict": sd(self.embeddirs_fn)}
+              "embedbones_state_dict": sd(self.embedbones_fn) if self.embedbones_fn is not None else {},
+              "embeddirs_state_dict": sd(self.embeddirs_fn)}
         if self.network_fine is not None:
             ck["network_fine_state_dict"] = sd(self.network_fine)
         return ck
@@ -478,20 +488,22 @@ class TrainRayCaster(nn.Module):
     def _embed_version(self):
         """(tau versions, cutoff_dist versions) of both embedders: the tau schedule moves the first
         every step, the second only changes on a load or a caller's edit."""
-        es = (self.embed_fn, self.embeddirs_fn)
+        es = self._embedders()
         return (tuple((e.tau.data_ptr(), e.tau._version) for e in es),
                 tuple((e.cutoff_dist.data_ptr(), e.cutoff_dist._version) for e in es))
 
     def _embed_state(self):
-        return ({"tau": self.embed_fn.host("tau"), "cutoff_dist": self.embed_fn.cutoff_dist},
-                {"tau": self.embeddirs_fn.host("tau"), "cutoff_dist": self.embeddirs_fn.cutoff_dist})
+        """(embed_fn, embeddirs_fn, embedbones_fn or None) states for DeviceModel.set_embed."""
+        return tuple(None if e is None else {"tau": e.host("tau"), "cutoff_dist": e.cutoff_dist}
+                     for e in (self.embed_fn, self.embeddirs_fn, self.embedbones_fn))
 
     def _sync_embed(self, model, seen):
         """New tau / cutoff_dist into a DeviceModel without a repack; a tau-only change (the schedule,
         every step) is a host-side field write, no device synchronisation or copy."""
         v = self._embed_version()
         if v != seen:
-            model.set_embed(*self._embed_state(), cutoffs=v[1] != seen[1])
+            e, ev, eb = self._embed_state()
+            model.set_embed(e, ev, cutoffs=v[1] != seen[1], embedbones_sd=eb)
         return v
 
     def _constants(self):

@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define ANERF_ABI_VERSION 9
+#define ANERF_ABI_VERSION 10
 
 enum {
     ANERF_OK = 0,
@@ -127,6 +127,11 @@ typedef struct {
  * feeds (input * (2 / c_j) - 1) to the frequencies only.  The cutoff window keeps the distance. */
 #define ANERF_ENC_CUT_TO_DIST 1
 #define ANERF_ENC_CUTOFF_SHIFT 2
+/* --cutoff_bones (core/raycasters.py:52-64): the bone embedder is a CutoffEmbedder (dist_inputs, its
+ * own tau and cutoff_dist: anerf_embed_params tau_b / cutoff_dist_b); with --multires_bones 0 its
+ * output is the bone direction times w_b = 1 - sigmoid(tau_b (dist - c_b)) when use_cutoff and
+ * cutoff_inputs (core/cutoff_embedder.py:111-166), the bare direction otherwise. */
+#define ANERF_ENC_CUTOFF_BONES 4
 
 /* HOST pointers to one NeRF's weights, torch nn.Linear layout [out][in] (core/networks/nerf.py:57-88). */
 typedef struct {
@@ -149,6 +154,8 @@ typedef struct {
     float tau;                   /* embed_fn.tau                  */
     const float* cutoff_dist_v;  /* embeddirs_fn.cutoff_dist [NJ] */
     float tau_v;                 /* embeddirs_fn.tau              */
+    const float* cutoff_dist_b;  /* embedbones_fn.cutoff_dist [NJ] (ANERF_ENC_CUTOFF_BONES), else NULL */
+    float tau_b;                 /* embedbones_fn.tau             */
 } anerf_embed_params;
 
 /* Optional per-stage outputs of anerf_render_rays (any member may be NULL). */
@@ -175,8 +182,9 @@ int anerf_model_create(const anerf_model_desc* desc, const anerf_net_weights* co
                        const anerf_net_weights* fine, const anerf_embed_params* embed, int device,
                        anerf_model** out);
 int anerf_model_destroy(anerf_model* m);
-/* Replace the embedders' state of a model without repacking its weights: tau / tau_v always,
- * cutoff_dist / cutoff_dist_v when not NULL (then synchronously, after the device has drained).
+/* Replace the embedders' state of a model without repacking its weights: tau / tau_v / tau_b always,
+ * cutoff_dist / cutoff_dist_v / cutoff_dist_b when not NULL (then synchronously, after the device has
+ * drained).
  * Launches issued afterwards use the new values: the tau schedule of training
  * (RayCaster.update_embed_fns -> CutoffEmbedder.update_tau, core/raycasters.py:731-748,
  * core/cutoff_embedder.py:176-183).  Not thread-safe against concurrent launches on the model. */

@@ -62,6 +62,12 @@ typedef struct {
      * input is c_j - dist, the frequencies take (input * (2 / c_j) - 1); the window keeps dist */
     int cut_to, shift_in;
     oracle_net coarse, fine;
+    /* --cutoff_bones (raycasters.py:52-64): the bone embedder is a CutoffEmbedder(dist_inputs=True);
+     * with multires_bones 0 and cutoff_inputs its output is the bone direction times
+     * w_b = 1 - sigmoid(tau_b (dist - c_b)) (cutoff_embedder.py:108-121, 143-158) */
+    int bone_cut;
+    float tau_b;
+    const float* cutoff_b; /* embedbones_fn.cutoff_dist (NJ) */
 } oracle_model;
 
 /* ---------------------------------------------------------------- small helpers */
@@ -293,6 +299,10 @@ static void encode_point(const oracle_model* m, const float* skts, const float p
         fr[3 * j + 0] = q[0] / dn;
         fr[3 * j + 1] = q[1] / dn;
         fr[3 * j + 2] = q[2] / dn;
+        if (m->bone_cut) { /* cat([inputs], embedded) * w, w on the dist expanded per coordinate */
+            const float wb = 1.0f - sigmoidf_(m->tau_b * (dist - m->cutoff_b[j]));
+            for (int c = 0; c < 3; ++c) fr[3 * j + c] *= wb;
+        }
         /* kp block: CutoffEmbedder(dist_inputs=False) (cutoff_embedder.py:125-158) */
         float w = 1.0f;
         if (m->use_cutoff) w = 1.0f - sigmoidf_(m->tau * (dist - m->cutoff[j]));

@@ -31,7 +31,8 @@ class _Model(ctypes.Structure):
                 ("cutoff", _f), ("cutoff_v", _f), ("has_fine", ctypes.c_int), ("single_net", ctypes.c_int),
                 ("lindisp", ctypes.c_int), ("sched_w", _f), ("sched_wv", _f), ("cut_to", ctypes.c_int),
                 ("shift_in", ctypes.c_int),
-                ("coarse", _Net), ("fine", _Net)]
+                ("coarse", _Net), ("fine", _Net),
+                ("bone_cut", ctypes.c_int), ("tau_b", ctypes.c_float), ("cutoff_b", _f)]
 
 
 def build():
@@ -96,6 +97,9 @@ class OracleModel:
         m.single_net = int(cfg.single_net)
         m.lindisp = int(cfg.lindisp)
         m.cut_to, m.shift_in = int(getattr(cfg, "cut_to_dist", False)), int(getattr(cfg, "cutoff_shift", False))
+        if getattr(cfg, "cutoff_bones", False) and cfg.use_cutoff and cfg.cutoff_inputs:
+            eb = ckpt["embedbones_state_dict"]
+            m.bone_cut, m.tau_b, m.cutoff_b = 1, float(np.asarray(eb["tau"])), self._k(eb["cutoff_dist"])
         if getattr(cfg, "freq_schedule", False):
             m.sched_w = self._k(schedule_w(e["sched_alpha"], cfg.multires))
             m.sched_wv = self._k(schedule_w(ev["sched_alpha"], cfg.multires_views))

@@ -23,6 +23,8 @@ NAMES = ["c1_64_s32_d4w128", "c2_256_s64_d8w256", "c3_512_s64i128_d8w256", "c4_5
          "l1_lindisp_s32i16_d4w128", "fs1_freqsched_s32i16_d8w128",
          # --cut_to_dist, --cutoff_shift (the kp cutoff embedder's input transforms)
          "cd1_cuttodist_s32i16_d8w128", "cs1_cutoffshift_s32i16_d4w128",
+         # --cutoff_bones (bone directions windowed by the bone embedder's own tau / cutoffs)
+         "cb1_cutoffbones_s32i16_d8w128",
          # the shipped configs' shape: mixamo / h36m / perfcap (8x256, 64 + 16, framecodes incl. the eval-mode
          # mean code), surreal (8x256, 64 + 16)
          "mx1_mixamo_s64i16_d8w256_fc", "su1_surreal_s64i16_d8w256",
@@ -55,12 +57,14 @@ class Golden:
                                        lindisp="--lindisp" in flags or bool(m.get("lindisp", False)),
                                        freq_schedule="--freq_schedule" in flags,
                                        cut_to_dist="--cut_to_dist" in flags, cutoff_shift="--cutoff_shift" in flags,
+                                       cutoff_bones="--cutoff_bones" in flags,
                                        init_freq=float(flags[flags.index("--init_freq") + 1])
                                        if "--init_freq" in flags else 0.0,
                                        **kw).validate()
         self.ckpt = syn.make_checkpoint(m["seed"], n_joints=m["NJ"], D=m["D"], W=m["W"], fine=m["I"] > 0,
                                         tau=m["tau"], use_framecode=fc, n_framecodes=5, multires=m.get("mr", 7),
-                                        multires_views=m.get("mrv", 4), sched_alpha=m.get("sched"))
+                                        multires_views=m.get("mrv", 4), sched_alpha=m.get("sched"),
+                                        cutoff_bones=bool(m.get("cb", False)), tau_bones=m.get("tau_b"))
         assert syn.checkpoint_sha256(self.ckpt) == m["sha256"], "synthetic weights drifted from the fixture"
 
     def __getitem__(self, k):

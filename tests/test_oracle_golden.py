@@ -23,7 +23,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(HERE), "oracle"))
 import oracle  # noqa: E402
 from _golden import FRAMES, Golden, NAMES  # noqa: E402
 
-STAGED = [n for n in NAMES if n.startswith(("c2", "c3", "c4", "fc", "v", "s1", "t2000", "fs", "cd1", "cs1", "mx1",
+STAGED = [n for n in NAMES if n.startswith(("c2", "c3", "c4", "fc", "v", "s1", "t2000", "fs", "cd1", "cs1", "cb1", "mx1",
                                             "su1"))]
 
 

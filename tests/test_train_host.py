@@ -99,7 +99,7 @@ def test_schedule_host_copies_and_tau_only_embed_updates():
         def __init__(self):
             self.calls = []
 
-        def set_embed(self, e, ev, cutoffs=True):
+        def set_embed(self, e, ev, cutoffs=True, embedbones_sd=None):
             self.calls.append((e["tau"], ev["tau"], cutoffs))
     m = Rec()
     seen = tr._embed_version()
