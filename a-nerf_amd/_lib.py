@@ -69,6 +69,27 @@ class SplitJob(ctypes.Structure):
                 ("transpose", ctypes.c_int32), ("precision", ctypes.c_int32), ("out", ctypes.c_void_p)]
 
 
+class MlpShape(ctypes.Structure):
+    """anerf_mlp_shape (the fused training forward)."""
+    _fields_ = [("depth", ctypes.c_int32), ("width", ctypes.c_int32), ("skip", ctypes.c_int32),
+                ("dnet", ctypes.c_int32), ("nv", ctypes.c_int32), ("cfc", ctypes.c_int32)]
+
+
+class MlpFwdWeights(ctypes.Structure):
+    """anerf_mlp_fwd_weights."""
+    _fields_ = [("pts_w", ctypes.c_void_p * 16), ("pts_ld", ctypes.c_int64 * 16), ("feature_w", ctypes.c_void_p),
+                ("views_w", ctypes.c_void_p), ("views_ld", ctypes.c_int64)]
+
+
+class MlpFwdIO(ctypes.Structure):
+    """anerf_mlp_fwd_io."""
+    _fields_ = [("m", ctypes.c_int64), ("feat", ctypes.c_void_p), ("ld_feat", ctypes.c_int64),
+                ("codes", ctypes.c_void_p), ("ld_codes", ctypes.c_int64), ("pts_b", ctypes.c_void_p * 16),
+                ("feature_b", ctypes.c_void_p), ("alpha_w", ctypes.c_void_p), ("alpha_b", ctypes.c_void_p),
+                ("views_b", ctypes.c_void_p), ("rgb_w", ctypes.c_void_p), ("rgb_b", ctypes.c_void_p),
+                ("h", ctypes.c_void_p * 16), ("hf", ctypes.c_void_p), ("g", ctypes.c_void_p), ("raw", ctypes.c_void_p)]
+
+
 class OSeg(ctypes.Structure):
     """anerf_oseg: a column segment of a GEMM output (+ relu' mask, accumulate)."""
     _fields_ = [("p", ctypes.c_void_p), ("ld", ctypes.c_int64), ("cols", ctypes.c_int32), ("mask", ctypes.c_void_p),
@@ -161,6 +182,11 @@ SIGNATURES = {
                                               ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
                                               ctypes.c_void_p, ctypes.c_void_p]),
     "anerf_mlp_split_bytes": (ctypes.c_size_t, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
+    "anerf_mlp_forward_pack_bytes": (ctypes.c_size_t, [ctypes.POINTER(MlpShape)]),
+    "anerf_mlp_forward_pack": (ctypes.c_int, [ctypes.POINTER(MlpShape), ctypes.POINTER(MlpFwdWeights),
+                                              ctypes.c_void_p, ctypes.c_void_p]),
+    "anerf_mlp_forward": (ctypes.c_int, [ctypes.POINTER(MlpShape), ctypes.POINTER(MlpFwdIO), ctypes.c_void_p,
+                                         ctypes.c_void_p]),
     "anerf_mlp_split_weights": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64,
                                                ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]),
     "anerf_mlp_split_weights_batch": (ctypes.c_int, [ctypes.POINTER(SplitJob), ctypes.c_int32, ctypes.c_void_p]),

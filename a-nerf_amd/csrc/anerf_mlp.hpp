@@ -296,11 +296,16 @@ __device__ __forceinline__ f32x16 mfma_x6(const float (&w)[16], const X6T& x, f3
 
 // OUT_SAME: out aliases ain (hidden layers: out[rb] = bias once ain[rb] is consumed); otherwise out
 // starts at zero (the view layer).  ALPHA folds sig += w_alpha . h in the fp32 path's k order.
-template <int RBO, int RBI, bool OUT_SAME, bool ALPHA>
+// RELU_IN = false takes ain as it is (the training forward's feature -> view edge, no activation).
+// side(g) runs after group g's prefetch (the training forward drains its stores there; NoSide: nothing).
+struct NoSide {
+    __device__ __forceinline__ void operator()(int) const {}
+};
+template <int RBO, int RBI, bool OUT_SAME, bool ALPHA, bool RELU_IN = true, class Side = NoSide>
 __device__ __forceinline__ void mlp_layer_x6(f32x16 (&out)[RBO], f32x16 (&ain)[RBI], f32x16 (&h)[RBI],
                                              const float* __restrict__ bias, const float* __restrict__ wp, int lane,
                                              Ring& ring, bool preloaded, const float* __restrict__ next,
-                                             const float* __restrict__ wa, float& sig) {
+                                             const float* __restrict__ wa, float& sig, Side* side = nullptr) {
     static_assert(RBO <= RBI, "x6 layer shape");
     constexpr int NG = 2 * RBO * RBI;
     constexpr int PD = 3;  // prefetch distance (groups)
@@ -310,7 +315,7 @@ __device__ __forceinline__ void mlp_layer_x6(f32x16 (&out)[RBO], f32x16 (&ain)[R
     const __amdgpu_buffer_rsrc_t rn = make_rsrc(next ? next : wp);
     auto convert_half = [&](int rb, int half) {  // relu of 8 inputs (+ their 8 bias outputs)
 #pragma unroll
-        for (int i = 8 * half; i < 8 * half + 8; ++i) h[rb][i] = relu_act(ain[rb][i]);
+        for (int i = 8 * half; i < 8 * half + 8; ++i) h[rb][i] = RELU_IN ? relu_act(ain[rb][i]) : ain[rb][i];
         if (OUT_SAME && rb < RBO) {
             const f32x4* p = reinterpret_cast<const f32x4*>(bias + (rb * 2 + hh) * 16 + 8 * half);
             const f32x4 v0 = p[0], v1 = p[1];
@@ -367,6 +372,7 @@ __device__ __forceinline__ void mlp_layer_x6(f32x16 (&out)[RBO], f32x16 (&ain)[R
     for (int g = 0; g < NQ; ++g) {
         __builtin_amdgcn_sched_barrier(0);
         prefetch(g);
+        if constexpr (!std::is_same<Side, NoSide>::value) (*side)(g);
         const int ob = g >> 1, s = g & 1;
         out[ob] = mfma_x6(ring.v[g % 4], T[s], out[ob]);
         if (ob == 0) alpha(0, s);
@@ -391,6 +397,7 @@ __device__ __forceinline__ void mlp_layer_x6(f32x16 (&out)[RBO], f32x16 (&ain)[R
             const int g = NQ + (ib - 1) * NQ + q;
             __builtin_amdgcn_sched_barrier(0);
             prefetch(g);
+            if constexpr (!std::is_same<Side, NoSide>::value) (*side)(g);
             out[ob] = mfma_x6(ring.v[g % 4], T[s], out[ob]);
             if (ob == RBO - 1) alpha(ib, s);
             if (ib + 1 < RBI) {

@@ -34,6 +34,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/anerf.h"
@@ -46,6 +47,7 @@ using namespace anerf;
 #include "anerf_stages.hpp"
 #include "anerf_kernels.hpp"
 #include "anerf_train.hpp"
+#include "anerf_trainfwd.hpp"
 #include "anerf_pose.hpp"
 #include "anerf_boxes.hpp"
 #include "anerf_batch.hpp"
@@ -57,6 +59,56 @@ int anerf_internal_fail(int code, const char* msg) { return fail(code, msg); }  
 static unsigned long long* g_stamps = nullptr;
 extern "C" void anerf_diag_set_stamps(unsigned long long* p) { g_stamps = p; }  // diagnostic build only
 #endif
+
+// ---- the training MLP's fused forward (anerf_trainfwd.hpp)
+namespace {
+struct TfLayout {  // offsets (floats) of the packed parts, and the total
+    size_t wx0, wl[MAXL], wskipx, wf, wvf, wvv, wvc, total;
+};
+size_t tf_regs_floats(int n_out, int n_in) { return (size_t)2 * (n_out / 32) * (n_in / 32) * 768; }
+size_t tf_mem_floats(int n_out, int K) { return (size_t)tf_xsteps(K) * (n_out / 32) * 768; }
+int tf_check(const anerf_mlp_shape* s) {
+    if (!s) return fail(ANERF_EINVAL, "anerf_mlp_forward: NULL shape");
+    if (s->width != 128 && s->width != 256)
+        return fail(ANERF_EINVAL, "anerf_mlp_forward: width 128 or 256");
+    if (s->depth < 1 || s->depth > MAXL) return fail(ANERF_EINVAL, "anerf_mlp_forward: depth 1..16");
+    if (s->dnet < 1 || s->dnet % 4 || s->nv < 1 || s->nv % 4 || s->cfc < 0 || s->cfc % 4)
+        return fail(ANERF_EINVAL, "anerf_mlp_forward: dnet, nv, cfc must be multiples of 4");
+    return ANERF_OK;
+}
+TfLayout tf_layout(const anerf_mlp_shape* s) {
+    const int W = s->width, D = s->depth;
+    TfLayout L = {};
+    size_t o = 0;
+    L.wx0 = o; o += tf_mem_floats(W, s->dnet);
+    for (int i = 1; i < D; ++i) { L.wl[i] = o; o += tf_regs_floats(W, W); }
+    const bool has_skip = s->skip >= 0 && s->skip + 1 < D;
+    L.wskipx = o; if (has_skip) o += tf_mem_floats(W, s->dnet);
+    L.wf = o; o += tf_regs_floats(W, W);
+    L.wvf = o; o += tf_regs_floats(W / 2, W);
+    L.wvv = o; o += tf_mem_floats(W / 2, s->nv);
+    L.wvc = o; if (s->cfc > 0) o += tf_mem_floats(W / 2, s->cfc);
+    L.total = o;
+    return L;
+}
+template <int W>
+hipError_t tf_launch(const TfArgs& a, long long m, hipStream_t st) {
+    constexpr int RB = W / 32;
+    const size_t lds = sizeof(float) * ((size_t)(a.D + 1) * W + W / 2 + 2 * RB * 16 + 3 * 2 * (RB / 2) * 16 +
+                                        (size_t)4 * 32 * (W + 4));
+    static const hipError_t attr = hipFuncSetAttribute((const void*)train_mlp_fwd_kernel<W>,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (attr != hipSuccess) return attr;
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const long long nblk = (m + 31) / 32;
+    const long long want = (nblk + 3) / 4;
+    const unsigned grid = (unsigned)(want < ncu ? want : ncu);
+    hipLaunchKernelGGL(train_mlp_fwd_kernel<W>, dim3(grid), dim3(256), lds, st, a);
+    return hipGetLastError();
+}
+}  // namespace
 
 extern "C" {
 
@@ -782,6 +834,109 @@ int anerf_ray_batch(const uint8_t* imgs, const uint8_t* masks, const uint8_t* bg
     hipLaunchKernelGGL(ray_batch_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a);
     HIP_TRY(hipGetLastError());
     return ANERF_OK;
+}
+
+
+
+size_t anerf_mlp_forward_pack_bytes(const anerf_mlp_shape* s) {
+    if (tf_check(s)) return 0;
+    return tf_layout(s).total * sizeof(float);
+}
+
+int anerf_mlp_forward_pack(const anerf_mlp_shape* s, const anerf_mlp_fwd_weights* w, void* packed, void* stream) {
+    int rc = tf_check(s);
+    if (rc) return rc;
+    if (!w || !packed) return fail(ANERF_EINVAL, "anerf_mlp_forward_pack: NULL argument");
+    const int W = s->width, D = s->depth;
+    const TfLayout L = tf_layout(s);
+    float* out = static_cast<float*>(packed);
+    TfPackBatch b = {};
+    long long dw = 0;
+    auto job = [&](const float* wp, int64_t ld, int n_out, int col_off, int n_in, int kind, size_t off) {
+        TfPackJob& J = b.j[b.n++];
+        J.w = wp;
+        J.out = out + off;
+        J.ld = (int)ld;
+        J.n_out = n_out;
+        J.col_off = col_off;
+        J.n_in = n_in;
+        J.kind = kind;
+        J.ngroups = kind == 0 ? 2 * (n_out / 32) * (n_in / 32) : tf_xsteps(n_in) * (n_out / 32);
+        J.dw0 = dw;
+        dw += (long long)J.ngroups * 768;
+    };
+    for (int i = 0; i < D; ++i)
+        if (!w->pts_w[i]) return fail(ANERF_EINVAL, "anerf_mlp_forward_pack: NULL pts_w");
+    if (!w->feature_w || !w->views_w) return fail(ANERF_EINVAL, "anerf_mlp_forward_pack: NULL head weights");
+    const bool has_skip = s->skip >= 0 && s->skip + 1 < D;
+    job(w->pts_w[0], w->pts_ld[0], W, 0, s->dnet, 1, L.wx0);
+    for (int i = 1; i < D; ++i) {
+        const bool sk = has_skip && i == s->skip + 1;  // [x | h]: the h part from column dnet
+        job(w->pts_w[i], w->pts_ld[i], W, sk ? s->dnet : 0, W, 0, L.wl[i]);
+        if (sk) job(w->pts_w[i], w->pts_ld[i], W, 0, s->dnet, 1, L.wskipx);
+    }
+    job(w->feature_w, W, W, 0, W, 0, L.wf);
+    job(w->views_w, w->views_ld, W / 2, 0, W, 0, L.wvf);
+    job(w->views_w, w->views_ld, W / 2, W, s->nv, 1, L.wvv);
+    if (s->cfc > 0) job(w->views_w, w->views_ld, W / 2, W + s->nv, s->cfc, 1, L.wvc);
+    hipLaunchKernelGGL(tf_pack_kernel, dim3((unsigned)((dw + 255) / 256)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), b);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? ANERF_OK : fail(ANERF_EHIP, std::string("anerf_mlp_forward_pack: ") + hipGetErrorString(e));
+}
+
+int anerf_mlp_forward(const anerf_mlp_shape* s, const anerf_mlp_fwd_io* io, const void* packed, void* stream) {
+    int rc = tf_check(s);
+    if (rc) return rc;
+    if (!io || !packed || !io->feat || !io->hf || !io->g || !io->raw || !io->feature_b || !io->alpha_w ||
+        !io->alpha_b || !io->views_b || !io->rgb_w || !io->rgb_b)
+        return fail(ANERF_EINVAL, "anerf_mlp_forward: NULL argument");
+    if (io->m <= 0) return ANERF_OK;
+    const int W = s->width, D = s->depth;
+    if (io->ld_feat < s->dnet + s->nv || io->ld_feat % 4 || (reinterpret_cast<uintptr_t>(io->feat) & 15))
+        return fail(ANERF_EINVAL, "anerf_mlp_forward: feat rows must be 16 B aligned with ld % 4 == 0");
+    if (s->cfc > 0 && (!io->codes || io->ld_codes < s->cfc || io->ld_codes % 4 ||
+                       (reinterpret_cast<uintptr_t>(io->codes) & 15)))
+        return fail(ANERF_EINVAL, "anerf_mlp_forward: framecode rows must be 16 B aligned with ld % 4 == 0");
+    if ((long long)32 * io->ld_feat * 4 >= (1ll << 31) || (s->cfc > 0 && (long long)32 * io->ld_codes * 4 >= (1ll << 31)))
+        return fail(ANERF_EINVAL, "anerf_mlp_forward: row stride too large");
+    const TfLayout L = tf_layout(s);
+    const float* pk = static_cast<const float*>(packed);
+    TfArgs a = {};
+    a.D = D;
+    a.skip = (s->skip >= 0 && s->skip + 1 < D) ? s->skip : -2;
+    a.dnet = s->dnet;
+    a.nv = s->nv;
+    a.cfc = s->cfc;
+    a.M = io->m;
+    a.feat = io->feat;
+    a.ldf = io->ld_feat;
+    a.codes = io->codes;
+    a.ldc = s->cfc > 0 ? io->ld_codes : 0;
+    a.wx0 = pk + L.wx0;
+    for (int i = 1; i < D; ++i) a.wl[i] = pk + L.wl[i];
+    a.wskipx = pk + L.wskipx;
+    a.wf = pk + L.wf;
+    a.wvf = pk + L.wvf;
+    a.wvv = pk + L.wvv;
+    a.wvc = pk + L.wvc;
+    for (int i = 0; i < D; ++i) {
+        if (!io->pts_b[i] || !io->h[i]) return fail(ANERF_EINVAL, "anerf_mlp_forward: NULL pts_b / h");
+        a.b[i] = io->pts_b[i];
+        a.h[i] = io->h[i];
+    }
+    a.bf = io->feature_b;
+    a.wa = io->alpha_w;
+    a.ba = io->alpha_b;
+    a.bv = io->views_b;
+    a.wrgb = io->rgb_w;
+    a.brgb = io->rgb_b;
+    a.hf = io->hf;
+    a.g = io->g;
+    a.raw = io->raw;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const hipError_t e = W == 256 ? tf_launch<256>(a, io->m, st) : tf_launch<128>(a, io->m, st);
+    return e == hipSuccess ? ANERF_OK : fail(ANERF_EHIP, std::string("anerf_mlp_forward: ") + hipGetErrorString(e));
 }
 
 }  // extern "C"

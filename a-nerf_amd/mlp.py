@@ -18,10 +18,17 @@ bf16x6 and the backward in bf16x3; fp32 accumulation in all (`anerf_gemm.hip`). 
 built and a GPU present.
 """
 import ctypes
+import os
 
 import torch
 
 from . import _lib
+
+# ANERF_TRAIN_FWD=fused: the whole bf16x6 forward (width 128 / 256) in one kernel (anerf_mlp_forward)
+# instead of the layer-by-layer GEMMs.  Measured equal on MI355X (1.96 vs 1.95 ms at M = 163840,
+# DESIGN.md §10): its 1.6 GB of saved activations cost as much as the GEMMs' re-reads, so the GEMMs
+# stay the default
+_FUSED = os.environ.get("ANERF_TRAIN_FWD", "gemm") == "fused"
 
 
 def _stream(dev):
@@ -114,10 +121,17 @@ class _MLP(torch.autograd.Function):
         pw, pb = params[0:2 * nl:2], params[1:2 * nl:2]
         wa, ba, wf, bf, wv, bv, wr, br = params[2 * nl:2 * nl + 8]
         whead = torch.cat([wf, wa]).contiguous()
-        # every layer's planes in one launch: [trunk..., head, views, rgb]
-        sp = split_weights([(w, False) for w in pw] + [(whead, False), (wv, False), (wr, False)], prec)
         cfc = 0 if codes is None else codes.shape[1]
         f32 = dict(device=dev, dtype=torch.float32)
+        if _FUSED and prec == 6 and W in (128, 256) and dnet % 4 == 0 and nv % 4 == 0 and cfc % 4 == 0:
+            H, hf, g, raw = _fused_forward(feat, codes, pw, pb, wa, ba, wf, bf, wv, bv, wr, br, W, D, skip, dnet, nv,
+                                           cfc, dev)
+            ctx.shape = shape
+            ctx.has_codes = codes is not None
+            ctx.save_for_backward(feat, codes if codes is not None else torch.empty(0), hf, g, whead, *H, *params)
+            return raw
+        # every layer's planes in one launch: [trunk..., head, views, rgb]
+        sp = split_weights([(w, False) for w in pw] + [(whead, False), (wv, False), (wr, False)], prec)
         segx = _seg(feat, dnet)
         H = []
         for i in range(D):
@@ -238,6 +252,37 @@ class _MLP(torch.autograd.Function):
                      [(gprev, W, W, 0, H[i - 1], False)], dev)
             gz = gprev
         return (None, gfeat, gcodes, *grads)
+
+
+def _fused_forward(feat, codes, pw, pb, wa, ba, wf, bf, wv, bv, wr, br, W, D, skip, dnet, nv, cfc, dev):
+    """The whole forward in one kernel (anerf_mlp_forward, bf16x6): h_0..h_{D-1}, hf, g, raw."""
+    lib = _lib.load()
+    M = feat.shape[0]
+    st = _stream(dev)
+    shp = _lib.MlpShape(D, W, skip if skip >= 0 else -1, dnet, nv, cfc)
+    wts = _lib.MlpFwdWeights()
+    for i in range(D):
+        wts.pts_w[i], wts.pts_ld[i] = pw[i].data_ptr(), pw[i].stride(0)
+    wts.feature_w, wts.views_w, wts.views_ld = wf.data_ptr(), wv.data_ptr(), wv.stride(0)
+    packed = torch.empty(lib.anerf_mlp_forward_pack_bytes(ctypes.byref(shp)), device=dev, dtype=torch.uint8)
+    _lib.check(lib.anerf_mlp_forward_pack(ctypes.byref(shp), ctypes.byref(wts), _lib.ptr(packed), st),
+               "anerf_mlp_forward_pack")
+    f32 = dict(device=dev, dtype=torch.float32)
+    H = [torch.empty(M, W, **f32) for _ in range(D)]
+    hf = torch.empty(M, W, **f32)
+    g = torch.empty(M, W // 2, **f32)
+    raw = torch.empty(M, 4, **f32)
+    io = _lib.MlpFwdIO()
+    io.m, io.feat, io.ld_feat = M, feat.data_ptr(), feat.stride(0)
+    if cfc:
+        io.codes, io.ld_codes = codes.data_ptr(), codes.stride(0)
+    for i in range(D):
+        io.pts_b[i], io.h[i] = pb[i].data_ptr(), H[i].data_ptr()
+    io.feature_b, io.alpha_w, io.alpha_b = bf.data_ptr(), wa.data_ptr(), ba.data_ptr()
+    io.views_b, io.rgb_w, io.rgb_b = bv.data_ptr(), wr.data_ptr(), br.data_ptr()
+    io.hf, io.g, io.raw = hf.data_ptr(), g.data_ptr(), raw.data_ptr()
+    _lib.check(lib.anerf_mlp_forward(ctypes.byref(shp), ctypes.byref(io), _lib.ptr(packed), st), "anerf_mlp_forward")
+    return H, hf, g, raw
 
 
 # mode -> (forward, backward) arithmetic (ANERF_MLP_BF16X6 = 6, _BF16X3 = 3).  "mixed": the forward

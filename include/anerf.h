@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define ANERF_ABI_VERSION 10
+#define ANERF_ABI_VERSION 11
 
 enum {
     ANERF_OK = 0,
@@ -394,6 +394,47 @@ typedef struct {
     int64_t ldm;
     int32_t accumulate;
 } anerf_oseg;
+
+/* The training MLP's forward as ONE fused kernel (mlp.py, default for widths 128 / 256 when the
+ * forward runs bf16x6): NeRF.forward (core/networks/nerf.py:94-148) over M rows of encoder features,
+ * every layer's output written once for the backward.  feat [m][ld_feat]: x = columns [0, dnet),
+ * views = [dnet, dnet + nv); codes [m][ld_codes] (cfc columns) or NULL.  Outputs: h[i] [m][W] =
+ * relu(pts_linears[i](.)), hf [m][W] = feature_linear(h[D-1]), g [m][W/2] = relu(views_linears.0(
+ * [hf | views | codes])), raw [m][4] = [rgb_linear(g), alpha_linear(h[D-1])].  Arithmetic as
+ * ANERF_MLP_BF16X6.  The weights are packed once per step (anerf_mlp_forward_pack, one launch). */
+typedef struct {
+    int32_t depth, width;  /* width 128 or 256 */
+    int32_t skip;          /* pts_linears[skip + 1] takes [x | h]; -1 (or >= depth - 1): none */
+    int32_t dnet, nv, cfc; /* multiples of 4; cfc 0: no framecodes */
+} anerf_mlp_shape;
+typedef struct {
+    const float* pts_w[16]; /* pts_linears[i].weight [W][in] */
+    int64_t pts_ld[16];
+    const float* feature_w; /* [W][W] */
+    const float* views_w;   /* views_linears.0.weight [W/2][W + nv + cfc] */
+    int64_t views_ld;
+} anerf_mlp_fwd_weights;
+typedef struct {
+    int64_t m;
+    const float* feat;
+    int64_t ld_feat;
+    const float* codes;
+    int64_t ld_codes;
+    const float* pts_b[16];
+    const float* feature_b;
+    const float* alpha_w; /* [W] */
+    const float* alpha_b; /* [1] (device) */
+    const float* views_b; /* [W/2] */
+    const float* rgb_w;   /* [3][W/2] */
+    const float* rgb_b;   /* [3] */
+    float* h[16];
+    float* hf;
+    float* g;
+    float* raw;
+} anerf_mlp_fwd_io;
+size_t anerf_mlp_forward_pack_bytes(const anerf_mlp_shape* s);
+int anerf_mlp_forward_pack(const anerf_mlp_shape* s, const anerf_mlp_fwd_weights* w, void* packed, void* stream);
+int anerf_mlp_forward(const anerf_mlp_shape* s, const anerf_mlp_fwd_io* io, const void* packed, void* stream);
 
 /* Bytes of one split operand of `rows` x `cols` (anerf_mlp_split_weights' output). */
 size_t anerf_mlp_split_bytes(int32_t rows, int32_t cols, int32_t precision);

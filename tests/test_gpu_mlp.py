@@ -195,3 +195,38 @@ def test_nerf_forward_backward_matches_fp32_module(D, W, fc, nj, impl):
     assert q99 <= 1e-3 and rel(gf_b, gf_f) <= 5e-3, (q99, rel(gf_b, gf_f))
     for k in gp_f:
         assert rel(gp_b[k], gp_f[k]) <= 5e-3, (k, rel(gp_b[k], gp_f[k]))
+
+
+@pytest.mark.parametrize("D,W,fc,nj,M", [(8, 256, False, 24, 5000), (4, 128, True, 24, 3001), (8, 256, True, 17, 77),
+                                         (8, 128, False, 65, 1000), (2, 256, False, 24, 40)])
+def test_fused_forward_matches_layer_by_layer_gemms(D, W, fc, nj, M, monkeypatch):
+    """anerf_mlp_forward (one kernel, bf16x6) against the layer-by-layer bf16x6 GEMMs on the same
+    weights and features: raw and every saved activation (h_i, feature, view hidden) within fp32
+    accuracy (2e-6 of each tensor's max |.| + 1e-6: both are fp32-accurate, in other summation
+    orders); ragged M (77, 3001) and framecodes included."""
+    cfg = anerf.RenderConfig(n_joints=nj, netdepth=D, netwidth=W, opt_framecode=fc,
+                             n_framecodes=5 if fc else 0).validate()
+    ck = syn.make_checkpoint(7, n_joints=nj, D=D, W=W, fine=False, use_framecode=fc, n_framecodes=5)
+    torch.manual_seed(1)
+    feat = torch.rand(M, cfg.feature_dim, device=DEV) * 2 - 1
+    cams = torch.randint(0, 5, (M,), device=DEV) if fc else None
+    saved = {}
+    for fused in (True, False):
+        monkeypatch.setattr(mlp, "_FUSED", fused)
+        tr = train.TrainRayCaster(cfg, ck, mlp="bf16x6").train()
+        f = feat.clone().requires_grad_(True)
+        raw = tr.network_fn(f, cams)
+        node = raw.grad_fn
+        saved[fused] = (raw.detach(), [t.detach().clone() for t in node.saved_tensors])
+    (ra, sa), (rb, sb) = saved[True], saved[False]
+    assert torch.all(torch.isfinite(ra))
+
+    def close(a, b, what):
+        d = float((a.double() - b.double()).abs().max()) if a.numel() else 0.0
+        scale = float(b.abs().max()) if b.numel() else 0.0
+        assert d <= 2e-6 * scale + 1e-6, f"{what}: max diff {d:.3e} (max |ref| {scale:.3e})"
+    close(ra, rb, "raw")
+    assert len(sa) == len(sb)
+    for i, (a, b) in enumerate(zip(sa, sb)):  # feat, codes, hf, g, whead, h_0 .. h_{D-1}, params
+        assert a.shape == b.shape
+        close(a, b, f"saved tensor {i}")
