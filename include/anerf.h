@@ -42,6 +42,7 @@
  *   anerf_mlp_split_weights_batch   the same for up to 32 weights in one launch
  *   anerf_mlp_gemm          forward (bias, relu) and input-gradient (relu' mask, accumulate) products
  *   anerf_mlp_wgrad         weight + bias gradients
+ *   anerf_mlp_forward(_pack)  the whole forward in one kernel (opt-in alternative to the GEMMs)
  */
 #ifndef ANERF_H
 #define ANERF_H
@@ -395,9 +396,10 @@ typedef struct {
     int32_t accumulate;
 } anerf_oseg;
 
-/* The training MLP's forward as ONE fused kernel (mlp.py, default for widths 128 / 256 when the
- * forward runs bf16x6): NeRF.forward (core/networks/nerf.py:94-148) over M rows of encoder features,
- * every layer's output written once for the backward.  feat [m][ld_feat]: x = columns [0, dnet),
+/* The training MLP's forward as ONE fused kernel (mlp.py with ANERF_TRAIN_FWD=fused, widths 128 /
+ * 256, bf16x6 forward; measured equal to the layer GEMMs): NeRF.forward
+ * (core/networks/nerf.py:94-148) over M rows of encoder features, every layer's output written once
+ * for the backward.  feat [m][ld_feat]: x = columns [0, dnet),
  * views = [dnet, dnet + nv); codes [m][ld_codes] (cfc columns) or NULL.  Outputs: h[i] [m][W] =
  * relu(pts_linears[i](.)), hf [m][W] = feature_linear(h[D-1]), g [m][W/2] = relu(views_linears.0(
  * [hf | views | codes])), raw [m][4] = [rgb_linear(g), alpha_linear(h[D-1])].  Arithmetic as
