@@ -71,10 +71,10 @@ class RayCaster:
         if fwd_type == "mesh":
             return self.render_mesh_density(*args, **kwargs)
         if fwd_type == "density_color":
-            raise NotImplementedError("fwd_type='density_color' needs texture layers the NeRF model does not have")
-        if fwd_type:
-            raise ValueError(f"unknown fwd_type {fwd_type!r}")
-        return self.render_rays(*args, **kwargs)
+            # (the reference asserts the network has texture layers, _get_density_fwd_fn :623-624; its
+            # NeRF has none, so the call fails the same way there)
+            raise AssertionError("need to have texture layer!")
+        return self.render_rays(*args, **kwargs)  # (any other fwd_type renders rays, as :357-359)
 
     # ------------------------------------------------------------------ density-only queries
     def _net_index(self, network):

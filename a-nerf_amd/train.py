@@ -533,7 +533,7 @@ class TrainRayCaster(nn.Module):
         return self._eval
 
     def forward(self, *args, fwd_type="", **kwargs):
-        if fwd_type:
+        if fwd_type in ("density", "mesh", "density_color"):  # (core/raycasters.py:349-359)
             return self.eval_caster()(*args, fwd_type=fwd_type, **kwargs)
         if not self.training:
             with torch.no_grad():

@@ -190,3 +190,18 @@ def test_normalize_cutoff_is_a_noop_like_the_reference():
     assert config.RenderConfig.from_args(types.SimpleNamespace(cutoff_bones=True), 24).cutoff_bones
     with pytest.raises(NotImplementedError):  # (bone frequencies stay refused)
         config.RenderConfig.from_args(types.SimpleNamespace(cutoff_bones=True, multires_bones=4), 24)
+
+
+def test_forward_dispatch_matches_the_reference():
+    """RayCaster.forward's fwd_type dispatch (core/raycasters.py:349-359): 'density' / 'mesh' to the
+    density queries, 'density_color' fails the reference's texture-layer assertion (:623-624, NeRF
+    has no texture_linears), anything else renders rays."""
+    rc_mod = importlib.import_module("a-nerf_amd.raycaster")
+    rc = object.__new__(rc_mod.RayCaster)  # (dispatch only: no device model)
+    rc.render_pts_density = lambda *a, **k: "density"
+    rc.render_mesh_density = lambda *a, **k: "mesh"
+    rc.render_rays = lambda *a, **k: "rays"
+    assert rc(fwd_type="density") == "density" and rc(fwd_type="mesh") == "mesh"
+    assert rc() == "rays" and rc(fwd_type="something") == "rays"
+    with pytest.raises(AssertionError, match="texture layer"):
+        rc(fwd_type="density_color")
