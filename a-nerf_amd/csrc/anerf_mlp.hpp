@@ -1058,6 +1058,106 @@ __device__ __forceinline__ void v_part(f32x16 (&acc)[RB], const ModelDev& M, con
     }
 }
 
+// The windowed part as bf16x6 (precision modes 2 and 3, RB % 4 == 0): per live joint, lane half h
+// holds features 8 s + i of k16-step s — i < MR: sin_i (h = 0) / cos_i (h = 1) of the frequency
+// input times the window, i == MR: the distance input (h = 0), zero otherwise: v_part's f[] — split
+// by truncation (exact), against weight groups (joint, s, rb) of 12 floats (pack_vpart_x6) in the
+// 4-slot ring, three groups ahead (the last three groups of a joint load the next live joint's
+// first).  Six bf16 MFMAs (32 cycles) per 16 k instead of eight f32 ones (64 cycles).  The next
+// live joint's geometry (group 0), sincos terms (one per group) and splits (as soon as a pair is
+// complete) run under this joint's MFMAs.
+template <int MR, int NG>
+struct VPartX6 {
+    static constexpr int KS = (MR + 1 + 7) / 8;        // k16-steps per joint
+    static constexpr int NF = 8 * KS;                  // features per lane half
+    static constexpr int PER = (MR + NG - 2) / (NG - 1);  // sincos terms per group 1 .. NG - 1
+    // the group in which feature q of the next joint is complete (sincos t in group t / PER + 1;
+    // the distance input and the zero padding in group 1)
+    static constexpr int ready(int q) { return q < MR ? q / PER + 1 : 1; }
+    static constexpr int pair_ready(int e) { return ready(2 * e) > ready(2 * e + 1) ? ready(2 * e) : ready(2 * e + 1); }
+};
+
+template <int RB, int MR>
+__device__ __forceinline__ void v_part_x6(f32x16 (&acc)[RB], const ModelDev& M, const float* __restrict__ wp,
+                                          const float* __restrict__ sk, const float* __restrict__ cut, float px,
+                                          float py, float pz, int lane, JointMask mask, Ring& ring,
+                                          float xs = 1.0f) {
+    static_assert(RB % 4 == 0, "v_part_x6 keeps ring slots static: groups per joint % 4 == 0");
+    constexpr int NG = VPartX6<MR, 1>::KS * RB, PD = 3;  // groups per joint
+    using V = VPartX6<MR, NG>;
+    constexpr int KS = V::KS, NF = V::NF, PER = V::PER;
+    const int hh = lane >> 5;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(wp);
+    const bool dist_in = M.use_cutoff && M.cutoff_inputs;
+    uint64_t r0 = uniform64(mask.m0), r1 = uniform64(mask.m1);
+    int j = mask_pop(r0, r1);
+    if (j < 0) return;
+    int jn = mask_pop(r0, r1);
+#pragma unroll
+    for (int d = 0; d < PD; ++d) load_group<12>(ring.v[d], rs, lane, j * NG + d);
+    X6T cur[KS];
+    {
+        float f[NF];
+        float dist, w, u, uf;
+        v_geom(M, sk, cut, j, px, py, pz, dist, w);
+        w *= xs;  // (a power of two: the products equal the unscaled ones times xs exactly)
+        kp_inputs(M.cut_to, M.shift_in, dist, cut[j], u, uf);
+#pragma unroll
+        for (int t = 0; t < MR; ++t) {
+            float sn, cs;
+            sincos_rr(uf * (float)(1 << t), sn, cs);
+            f[t] = (hh ? cs : sn) * w;
+        }
+        f[MR] = hh ? 0.0f : (dist_in ? u * w : u * xs);
+#pragma unroll
+        for (int t = MR + 1; t < NF; ++t) f[t] = 0.0f;
+#pragma unroll
+        for (int e = 0; e < NF / 2; ++e) split3_pair(f[2 * e], f[2 * e + 1], cur[e / 4], e % 4);
+    }
+    while (j >= 0) {
+        X6T nxt[KS];
+        float fn[NF];
+        float dn = 0.0f, dfn = 0.0f, wn = 0.0f;  // next joint: raw input, frequency input, window
+        const int jg = jn >= 0 ? jn : j;          // (a harmless redo of this joint after the last)
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            const int s = g / RB, rb = g % RB;
+            __builtin_amdgcn_sched_barrier(0);
+            const int gp = g + PD;
+            load_group<12>(ring.v[gp % 4], rs, lane, gp < NG ? j * NG + gp : jg * NG + gp - NG);
+            acc[rb] = mfma_x6(ring.v[g % 4], cur[s], acc[rb]);
+            if (g == 0) {
+                float dd;
+                v_geom(M, sk, cut, jg, px, py, pz, dd, wn);
+                wn *= xs;
+                kp_inputs(M.cut_to, M.shift_in, dd, cut[jg], dn, dfn);
+                pin(dn), pin(dfn), pin(wn);
+            } else {
+#pragma unroll
+                for (int t = (g - 1) * PER; t < g * PER && t < MR; ++t) {
+                    float sn, cs;
+                    sincos_rr(dfn * (float)(1 << t), sn, cs);
+                    fn[t] = (hh ? cs : sn) * wn;
+                    pin(fn[t]);
+                }
+            }
+            if (g == 1) {
+                fn[MR] = hh ? 0.0f : (dist_in ? dn * wn : dn * xs);
+#pragma unroll
+                for (int t = MR + 1; t < NF; ++t) fn[t] = 0.0f;
+            }
+#pragma unroll
+            for (int e = 0; e < NF / 2; ++e)
+                if (V::pair_ready(e) == g) split3_pair(fn[2 * e], fn[2 * e + 1], nxt[e / 4], e % 4);
+            interleave_mfma_valu<6, 6>();
+        }
+#pragma unroll
+        for (int k = 0; k < KS; ++k) cur[k] = nxt[k];
+        j = jn;
+        jn = mask_pop(r0, r1);
+    }
+}
+
 // View layer, per-ray direction part: acc[RBV] += G^T * [w'_j, 1]  (G in LDS).  k-step p pairs
 // joint p (lane half 0) with joint p + NJH2 (half 1), exactly the u part's pairing, so w'_j comes
 // from the u part (wvp, stored per lane); k-step NJH2 adds the bias / framecode column NJ.  The G
@@ -1137,7 +1237,12 @@ __device__ __forceinline__ bool mlp_trunk(const ModelDev& M, const NetDev& net, 
                        M.D > 1 ? (P >= 2 ? nullptr : wl[1]) : after_last, st);
     }
     STAMP(st, 8);
-    v_part<RB, MR>(acc, M, net.wl0v, sk, cut, px, py, pz, lane, mask, st);
+    // (precision modes 2 / 3: the windowed parts as bf16x6; the u part's ring groups are consumed)
+    constexpr bool VX6 = (P >= 2) && (RB % 4 == 0);
+    if constexpr (VX6)
+        v_part_x6<RB, MR>(acc, M, net.wv6, sk, cut, px, py, pz, lane, mask, ring);
+    else
+        v_part<RB, MR>(acc, M, net.wl0v, sk, cut, px, py, pz, lane, mask, st);
     STAMP(st, 9);
     bool pre6 = false;
     for (int L = 1; L < M.D; ++L) {
@@ -1185,7 +1290,10 @@ __device__ __forceinline__ bool mlp_trunk(const ModelDev& M, const NetDev& net, 
             else
                 u_part<RB, false>(acc, M, net.wskipu, sk, cut, px, py, pz, lane, nullptr, nullptr, nullptr, ring, after,
                                   st, xs);
-            v_part<RB, MR>(acc, M, net.wskipv, sk, cut, px, py, pz, lane, mask, st, xs);
+            if constexpr (VX6)
+                v_part_x6<RB, MR>(acc, M, net.wskipv6, sk, cut, px, py, pz, lane, mask, ring, xs);
+            else
+                v_part<RB, MR>(acc, M, net.wskipv, sk, cut, px, py, pz, lane, mask, st, xs);
             STAMP(st, 12);
         }
     }
@@ -1256,12 +1364,12 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
     if (mfma_count && lane == 0) {  // exact MFMA work of this block (wave-uniform quantities)
         const int act = __builtin_popcountll(mask.m0) + __builtin_popcountll(mask.m1);
         const bool ux6 = (P >= 2) && (RB % 4 == 0) && uf != nullptr && M.ux6;  // as in mlp_trunk
-        const int xk = (ux6 ? 0 : 3 * M.njh2) + act * VPart<MR>::KB;   // f32 k-steps of one x part
+        constexpr bool vx6 = (P >= 2) && (RB % 4 == 0);
+        const int xk = (ux6 ? 0 : 3 * M.njh2) + (vx6 ? 0 : act * VPart<MR>::KB);  // f32 k-steps of one x part
         long long k = (long long)xk * RB + (long long)vsteps * RBV;
-        if (ux6) {
-            const int nx = (M.skip + 1 < M.D) ? 2 : 1;
-            atomicAdd(mfma_count + 1, (unsigned long long)(nx * ((3 * M.njh2 + 7) / 8) * RB * 6));
-        }
+        const int nx = (M.skip + 1 < M.D) ? 2 : 1;
+        if (ux6) atomicAdd(mfma_count + 1, (unsigned long long)(nx * ((3 * M.njh2 + 7) / 8) * RB * 6));
+        if (vx6) atomicAdd(mfma_count + 1, (unsigned long long)(nx * act * VPartX6<MR, 1>::KS * RB * 6));
         if (P >= 2)  // view layer, bf16x6 / fp16x3
             atomicAdd(mfma_count + 1, (unsigned long long)(RBV * RB * 2 * (P == 2 ? 6 : 3)));
         else

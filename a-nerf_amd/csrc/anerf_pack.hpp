@@ -297,6 +297,33 @@ std::vector<float> pack_vpart(const float* Wt, int n_out, int ld, int nj, int mr
     return out;
 }
 
+// windowed part as bf16x6 groups for v_part_x6: joint j, k16-step s, lane half h, element i ->
+// feature q = 8 s + i of that half: q < mr -> sin_q (h = 0) / cos_q (h = 1) = column
+// (1 + 2q + h) nj + j, q == mr and h == 0 -> the distance input (column j), else zero; groups
+// (j, s, rb) of 12 floats = fragments w0, w1, w2 (as pack_layer_x6).
+std::vector<float> pack_vpart_x6(const float* Wt, int n_out, int ld, int nj, int mr) {
+    const int RB = n_out / 32, ks = (mr + 1 + 7) / 8;
+    return pack_groups(nj * ks * RB, 12, [&](int g, int sl, int l) {
+        const int j = g / (ks * RB), s = (g / RB) % ks, rb = g % RB, f = sl >> 2, e = sl & 3;
+        const int h = l >> 5, row = 32 * rb + (l & 31);
+        uint32_t bits = 0;
+        for (int jj = 0; jj < 2; ++jj) {
+            const int q = 8 * s + 2 * e + jj;
+            const int col = q < mr ? (1 + 2 * q + h) * nj + j : (q == mr && h == 0 ? j : -1);
+            float r = col >= 0 ? Wt[(size_t)row * ld + col] : 0.0f;
+            uint16_t v = 0;
+            for (int p = 0; p <= f; ++p) {
+                v = bf16_rne(r);
+                r -= bf16_to_f(v);
+            }
+            bits |= (uint32_t)v << (16 * jj);
+        }
+        float out;
+        std::memcpy(&out, &bits, 4);
+        return out;
+    });
+}
+
 // per-lane-half vectors [rb][h][16] of a length-n vector in accumulator row order
 std::vector<float> pack_rowvec(const float* v, int n, bool half_major) {
     const int RB = n / 32;
@@ -491,6 +518,11 @@ static int pack_net(const anerf_model_desc* d, int njh2, const anerf_net_weights
         offs.push_back((size_t)(int64_t)ew);
         offs.push_back(pk.add(pack_layer_h3(wfused.data(), WH, W, 0, W, ew)));     // wviewh
     }
+    offs.push_back(pk.add(pack_vpart_x6(w->pts_w[0], W, cin, nj, mr)));               // wv6 (layer 0)
+    if (skl < d->net_depth)                                                           // wskipv6
+        offs.push_back(pk.add(pack_vpart_x6(w->pts_w[skl], W, cin + W, nj, mr)));
+    else
+        offs.push_back((size_t)-1);
     return ANERF_OK;
 }
 
@@ -529,6 +561,9 @@ static void bind_net(const anerf_model_desc* d, const float* base, const std::ve
     }
     nd.ew_view = (int)(int64_t)o[k++];
     nd.wviewh = base + o[k++];
+    nd.wv6 = base + o[k++];
+    nd.wskipv6 = o[k] == (size_t)-1 ? nullptr : base + o[k];
+    ++k;
     nd.balpha = balpha;
 }
 

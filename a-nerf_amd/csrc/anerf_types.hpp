@@ -59,6 +59,8 @@ struct NetDev {
     const float* wview6;     // wview as bf16x6 fragments
     const float* wu6;        // layer 0 bone-direction part as bf16x6 fragments (pack_upart_x6)
     const float* wskipu6;    // the skip layer's, or null
+    const float* wv6;        // layer 0 windowed part as bf16x6 groups (pack_vpart_x6)
+    const float* wskipv6;    // the skip layer's, or null
     const float* wlh[MAXL];  // [i>0] activation parts as fp16x3 fragments (pack_layer_h3), scaled by 2^ewl[i]
     const float* wviewh;     // wview as fp16x3 fragments, scaled by 2^ew_view
     int ewl[MAXL], ew_view;

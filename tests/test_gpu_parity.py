@@ -523,9 +523,18 @@ def test_split_modes_execute_16bit_mfmas(precision, per_block):
     #   hidden 32x32 blocks: 16 f32 MFMAs (k = 2) -> 2 k16-steps x 6 (bf16x6) or x 3 (fp16x3)
     #   fused view layer (128 x 256): 64 x 4 f32 -> 4 x 8 x per_block
     #   two bone-direction x parts (36 features, bf16x6 in both modes): 36 x 8 f32 -> ceil(36 / 8) x 8 x 6
+    # and per live joint of a block, two windowed x parts (16 features, bf16x6 in both modes):
+    #   8 k-steps x 8 f32 each -> one k16-step x 8 x 6
     f32_removed = 7 * 64 * 16 + 128 * 4 + 2 * 36 * 8
     bf16_added = 7 * 64 * per_block + 4 * 8 * per_block + 2 * 5 * 8 * 6
-    assert n_bf16 > 0 and (f32_only - n_f32) * bf16_added == n_bf16 * f32_removed
+    f32_joint, bf16_joint = 2 * 8 * 8, 2 * 8 * 6
+    # two equations in the block count and the live-joint count: both must come out as the 64 rays'
+    # 2 + 6 blocks and a whole number of live joints
+    diff = f32_only - n_f32
+    nb, rem = divmod(n_bf16 * f32_joint - diff * bf16_joint, bf16_added * f32_joint - f32_removed * bf16_joint)
+    assert rem == 0 and nb == 64 * (64 // 32 + (64 + 128) // 32), (nb, rem)
+    act, rem = divmod(n_bf16 - nb * bf16_added, bf16_joint)
+    assert rem == 0 and 0 < act <= nb * 24 and diff == nb * f32_removed + act * f32_joint
 
 
 def test_bf16x3_executes_bf16_mfmas():
