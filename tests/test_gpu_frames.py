@@ -95,6 +95,30 @@ def test_full_frame_matches_oracle_on_8192_rays(nj, precision):
     _oracle_check(cfg, ck, sc, cyls, rb, out, 8192)
 
 
+@pytest.mark.parametrize("W,precision", [(256, "bf16x6"), (128, "bf16x6"), (256, "fp16x3"), (128, "fp16x3")])
+def test_multires10_split_modes_match_oracle(W, precision):
+    """--multires 10 at widths 128 / 256 in the split modes: the windowed k-streams run as bf16x6 with
+    two k16-steps per joint (10 sin / cos terms + the distance input per lane half; v_part_x6), and
+    at W = 128 four groups per joint (three sincos terms per group).  The reference's fixture with
+    multires 10 (v1_mr10_w64_d4) is at width 64, which stays on f32 MFMAs; this pins the split path
+    against the oracle (itself pinned to v1) on 2,048 rays of a 512^2 frame at tau 20."""
+    seed = 17
+    sc = syn.make_scene(n_joints=24, H=512, W=512, seed=seed)
+    ck = syn.make_checkpoint(seed, n_joints=24, D=8, W=W, fine=True, tau=20.0, multires=10)
+    idx, cyls, boxes = anerf.rays.valid_pixels(sc["c2ws"], 512, 512, sc["focal"], kps=sc["kps"], ext_scale=0.001)
+    (x0, y0), (x1, y1) = (int(v) for v in boxes[0][0]), (int(v) for v in boxes[0][1])
+    n = (x1 - x0) * (y1 - y0)
+    c2w = torch.from_numpy(np.ascontiguousarray(sc["c2ws"][0][:3, :4])).cuda()
+    rb = torch.empty(n, 11, device="cuda")
+    _lib.check(_lib.load().anerf_gen_rays_box(_lib.ptr(c2w), 512, 512, sc["focal"], sc["focal"], 0.0, 0.0, 0, x0, y0,
+                                              x1, y1, 0.0, 1.0, _lib.ptr(rb), _lib.stream_handle()), "gen_rays_box")
+    cfg = anerf.RenderConfig(n_joints=24, netwidth=W, multires=10, N_samples=64, N_importance=128,
+                             precision=precision).validate()
+    out = _render(anerf.RayCaster(cfg, ck), rb, sc, cyls)
+    torch.cuda.synchronize()
+    _oracle_check(cfg, ck, sc, cyls, rb, out, 2048)
+
+
 @pytest.mark.parametrize("precision", ["bf16x6", "fp16x3", "fp32"])
 def test_config5_pixel_shards_are_bit_identical(precision):
     sc, ck, cyls, rb = _frame(1024, 24, 13, 79.6)
