@@ -434,9 +434,10 @@ def main():
                          "traffic_measured_in_this_run": False,
                          "traffic_note": "2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md, HBM / rocprofv3): L2 "
                                          "fabric-side bytes, which count Infinity-Cache (L3) hits. bf16x6's per-net "
-                                         "streamed weight set (~4.2 MB) exceeds an XCD's 4 MB L2, so the weights are "
-                                         "re-read from the 256 MB L3 (fp16x3's ~3 MB set fits: ~0.56 GB); the bytes "
-                                         "a render call must move are unique_bytes_per_step + ~8.6 MB of weights",
+                                         "streamed weight set (hidden layers 2.75 MB + the view, bone-direction and "
+                                         "live joints' windowed parts) is just over an XCD's 4 MB L2, so weight groups "
+                                         "are re-read from the 256 MB L3 (fp16x3's smaller set fits: ~0.7 GB); the "
+                                         "bytes a render call must move are unique_bytes_per_step + ~8 MB of weights",
                          "unique_bytes_per_step": int(n_mine * (4 * 11 + 4 * 10) + (n_mine * (S + I) * 4 * 2 if I > 0 else 0)),
                          "kernel_ms": round(kern_ms, 3),
                          "launches_per_step": 2 if I > 0 else 1,
