@@ -25,7 +25,9 @@ Extra JSON fields:
                 instructions the launches actually issue (kernel-side tally, agrees with PMC
                 SQ_INSTS_MFMA) against the instruction-mix-weighted peak — it differs because the
                 kernel skips exact-zero cutoff-window k-steps and fuses feature_linear (fewer FLOPs)
-                and splits operands for fp32 accuracy (more FLOPs)
+                and splits operands for fp32 accuracy (more FLOPs); the peaks assume 2.4 GHz, and
+                `mfma_busy_at_profile_clock` rescales frac_executed to the effective clock of the
+                committed PMC summary (GRBM_GUI_ACTIVE / kernel time; the chip is power-limited here)
   parity        every N: the oracle's outputs for an evenly spaced sample of the frame's rays (near /
                 far from the whole frame's chunks) against the GPU's (at N > 1 the all-gathered frame);
                 exits non-zero above 1e-4
@@ -93,7 +95,7 @@ def parse():
 
 
 def traffic_from_profiles(precision):
-    """(HBM bytes per render call, file) of render_kernel from the newest committed rocprofv3 --pmc
+    """(HBM bytes per render call, file, effective clock GHz) of render_kernel from the newest committed rocprofv3 --pmc
     summary of this precision mode (profiles/*pmc*.json, field "precision"; untagged files are fp32).
     Copied from that profile, not measured by this run (PMC passes need their own rocprofv3 runs)."""
     for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")), reverse=True):
@@ -102,8 +104,8 @@ def traffic_from_profiles(precision):
         except Exception:
             continue
         if d.get("precision", "fp32") == precision and "render_kernel_hbm_bytes_per_launch" in d:
-            return d["render_kernel_hbm_bytes_per_launch"], os.path.relpath(f, REPO)
-    return None, None
+            return d["render_kernel_hbm_bytes_per_launch"], os.path.relpath(f, REPO), d.get("effective_clock_GHz")
+    return None, None, None
 
 
 def _config_name(H, S, I, nj):
@@ -369,8 +371,8 @@ def main():
     achieved_req = req_f32 * FLOP_F32_MFMA / (kern_ms * 1e-3) / 1e12
     peak = pipe_peak(a.precision)
     # the committed PMC summaries are of config 3's frame; other shapes report null
-    traffic, traffic_src = (traffic_from_profiles(a.precision) if _config_name(H, S, I, a.joints) == "config3"
-                            else (None, None))
+    traffic, traffic_src, prof_clock = (traffic_from_profiles(a.precision)
+                                        if _config_name(H, S, I, a.joints) == "config3" else (None, None, None))
 
     # N = 1 extras on the same frame: the other precision modes, and this mode at tau = 20 (the untrained
     # value: wider cutoff windows, more live joints per block than tau = 79.6)
@@ -451,6 +453,11 @@ def main():
                                    "average x launches_per_step agrees (profiles/)",
                          "achieved_executed": round(achieved_exec, 2), "peak_executed_mix": round(peak_exec, 1),
                          "frac_executed": round(achieved_exec / peak_exec, 4),
+                         # the peaks assume 2.4 GHz; the chip runs this load power-limited below that
+                         # (GRBM_GUI_ACTIVE / kernel time in the same committed PMC summary as traffic)
+                         "profile_clock_GHz": prof_clock,
+                         "mfma_busy_at_profile_clock": (round(achieved_exec / peak_exec * 2.4 / prof_clock, 4)
+                                                        if prof_clock else None),
                          "achieved_required": round(achieved_req, 2),
                          "frac_required": round(achieved_req / peak, 4),
                          "required": "the FLOPs an exact fp32 implementation must do after exact-zero cutoff-window "
