@@ -284,6 +284,34 @@ __device__ __forceinline__ void split3_block_pair(const f32x16& hb, X6T (&t)[2],
     split3_pair(hb[8 * s + 2 * q], hb[8 * s + 2 * q + 1], t[s], q);
 }
 
+// Issue-order pins of the split layers' groups (round 3, A/B on the box, tools/gpu_ab3.sh): the
+// scheduler otherwise packs a group's split / relu work into one or two MFMA gaps.  bf16x6 +1.25 %,
+// fp16x3 +0.4 % with at most three VALU per gap (two: +1.1 %); the same pin on u_part_x6: -0.1 %.
+#ifndef ANERF_X6_IL
+#define ANERF_X6_IL 3
+#endif
+#ifndef ANERF_H3_IL
+#define ANERF_H3_IL 3
+#endif
+// One x6 group's issue order: each of the six MFMAs followed by at most one weight load and three
+// VALU instructions (the split / relu / bias work of the group), so no MFMA gap carries more than
+// the ~5 single-issue instructions an MFMA of this shape hides (MI355X_MICROARCH.md).
+// (NM MFMAs; the first NLG each followed by NL vector-memory reads; then up to NV VALU instructions)
+template <int NM, int NLG, int NL, int NV>
+__device__ __forceinline__ void group_schedule() {
+#pragma unroll
+    for (int i = 0; i < NM; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if (i < NLG) __builtin_amdgcn_sched_group_barrier(0x020, NL, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);
+    }
+}
+__device__ __forceinline__ void x6_group_schedule() {
+#if ANERF_X6_IL
+    group_schedule<6, 3, 1, ANERF_X6_IL>();
+#endif
+}
+
 __device__ __forceinline__ f32x16 mfma_x6(const float (&w)[16], const X6T& x, f32x16 c) {
     const bf16x8 w0 = frag_of(w, 0), w1 = frag_of(w, 1), w2 = frag_of(w, 2);
     c = mfma_bf16_32x32x16(w2, x.frag(0), c);  // small terms first
@@ -383,6 +411,7 @@ __device__ __forceinline__ void mlp_layer_x6(f32x16 (&out)[RBO], f32x16 (&ain)[R
                 if (pair_group(p, QL) == (g < QL ? -1 : g) || (g == NQ - 1 && pair_group(p, QL) > g))
                     split3_block_pair(h[1], Tn, p);
         }
+        x6_group_schedule();
     }
 #pragma clang loop unroll(full)
     for (int ib = 1; ib < RBI; ++ib) {
@@ -407,6 +436,7 @@ __device__ __forceinline__ void mlp_layer_x6(f32x16 (&out)[RBO], f32x16 (&ain)[R
                     if (pair_group(p, q0) == q || (q == NQ - 1 && pair_group(p, q0) > q))
                         split3_block_pair(h[ib + 1], Tn, p);
             }
+            x6_group_schedule();
         }
     }
 }
@@ -450,6 +480,13 @@ __device__ __forceinline__ void split2_pair(float a, float b, float t, H3T& T, i
 __device__ __forceinline__ void split2_block_pair(const f32x16& hb, float t, H3T (&T)[2], int p) {
     const int s = p >> 2, q = p & 3;
     split2_pair(hb[8 * s + 2 * q], hb[8 * s + 2 * q + 1], t, T[s], q);
+}
+
+// mlp_layer_h3's group: three MFMAs, the ring slot's four loads (even groups) after the first two
+__device__ __forceinline__ void h3_group_schedule() {
+#if ANERF_H3_IL
+    group_schedule<3, 2, 2, ANERF_H3_IL>();
+#endif
 }
 
 __device__ __forceinline__ f32x16 mfma_f16_32x32x16(f16x8 a, f16x8 b, f32x16 c) {
@@ -570,6 +607,7 @@ __device__ __forceinline__ void mlp_layer_h3(f32x16 (&out)[RBO], f32x16 (&ain)[R
                 if (pair_group(p, QL) == (g < QL ? -1 : g) || (g == NQ - 1 && pair_group(p, QL) > g))
                     split2_block_pair(h[1], t, Tn, p);
         }
+        h3_group_schedule();
     }
 #pragma clang loop unroll(full)
     for (int ib = 1; ib < RBI; ++ib) {
@@ -592,6 +630,7 @@ __device__ __forceinline__ void mlp_layer_h3(f32x16 (&out)[RBO], f32x16 (&ain)[R
                     if (pair_group(p, q0) == q || (q == NQ - 1 && pair_group(p, q0) > q))
                         split2_block_pair(h[ib + 1], t, Tn, p);
             }
+            h3_group_schedule();
         }
     }
 }
