@@ -69,14 +69,18 @@ __global__ __launch_bounds__(256, 1) void render_kernel(ModelDev M, RenderArgs A
         // ---- MLP over 32-sample blocks, round-robin over the 4 waves
         const int nm = only_new ? I : n;
         const int nb = (nm + 31) / 32;
-        for (int b = wave; b < nr * nb; b += 4) {
+        // (the same trip count on every wave: bf16x6's mlp_trunk has a workgroup barrier per hidden
+        // layer; a wave past the last block redoes that block without storing or counting it)
+        for (int it = 0; it < (nr * nb + 3) / 4; ++it) {
+            const bool own = it * 4 + wave < nr * nb;
+            const int b = own ? it * 4 + wave : nr * nb - 1;
             const int r = b / nb, s0 = (b % nb) * 32;
             const float* zr = only_new ? lds + P.scr + P.scr_stride * r + 6 * P.z_stride : lds + zoff + P.z_stride * r;
             float* rawr = lds + P.raw + P.raw_stride * r + (only_new ? 4 * S : 0);
             mlp_block<W, MR, PREC>(M, net, lds + P.ray + 16 * r, lds + P.sk + P.sk_stride * r, lds + P.cut,
-                             zr, nm, s0, lds + P.g + P.g_stride * r, rawr, lane, A.mfma_count, lds + P.bias,
-                             (P.uf >= 0 && M.skip + 1 < M.D) ? lds + P.uf + wave * P.uf_stride : nullptr,
-                             lds + P.wv + wave * P.wv_stride, st);
+                             zr, nm, s0, lds + P.g + P.g_stride * r, rawr, lane, own ? A.mfma_count : nullptr,
+                             lds + P.bias, (P.uf >= 0 && M.skip + 1 < M.D) ? lds + P.uf + wave * P.uf_stride : nullptr,
+                             lds + P.wv + wave * P.wv_stride, st, own);
         }
         STAMP(st, 2 + 2 * pass);
         __syncthreads();

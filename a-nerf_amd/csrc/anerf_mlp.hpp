@@ -1287,6 +1287,13 @@ __device__ __forceinline__ bool mlp_trunk(const ModelDev& M, const NetDev& net, 
     for (int L = 1; L < M.D; ++L) {
         const float* after = L + 1 < M.D ? wl[L + 1] : after_last;
         const bool skl = (L == M.skip + 1);
+        // bf16x6 render: the workgroup's four waves enter every hidden layer together (s_barrier, no
+        // memory fence: the ring's loads stay in flight), so each 3 KiB weight group is read from L2
+        // about once per CU and the other waves hit the CU's L1 — the hidden layers stream 12 KiB per
+        // CU per group otherwise, and the waves drift apart over the windowed parts' live joints.
+        // +2.1 % (A/B, profiles/r03_ab_experiments.txt); the render kernel's block loop has the same
+        // trip count on every wave (the density kernel's grid-stride loop does not: WV = false there).
+        if constexpr (WV && P == 2) __builtin_amdgcn_s_barrier();
         if constexpr (P == 3) {
             // the next h3 phase (the next hidden layer or the view layer) is prefetched; not across the
             // skip layer's x parts, which load themselves and scale their B operands by 2^es (the
@@ -1346,7 +1353,7 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
                           int n, int s0,
                           const float* __restrict__ G, float* __restrict__ raw_out, int lane,
                           unsigned long long* mfma_count, const float* __restrict__ bias, float* __restrict__ uf,
-                          float* __restrict__ wvp, Stamps& st) {
+                          float* __restrict__ wvp, Stamps& st, bool store = true) {
     constexpr int RB = W / 32;
     constexpr int RBV = (W / 2) / 32;
     const int sl = lane & 31, hh = lane >> 5;
@@ -1422,7 +1429,7 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
         }
         atomicAdd(mfma_count, (unsigned long long)k);
     }
-    if (hh == 0 && s0 + sl < n) {
+    if (store && hh == 0 && s0 + sl < n) {
         float* o = raw_out + 4 * (s0 + sl);
         o[0] = rgb[0];
         o[1] = rgb[1];
