@@ -837,6 +837,24 @@ int anerf_ray_batch(const uint8_t* imgs, const uint8_t* masks, const uint8_t* bg
 }
 
 
+int anerf_gather_rows(const float* src, int64_t width, int64_t n_rows, const int64_t* rows, int64_t n_img,
+                      int64_t n_per, float* dst, int32_t* bad_out, void* stream) {
+    if (width < 0 || n_rows < 1 || n_img < 0 || n_per < 0) return fail(ANERF_EINVAL, "anerf_gather_rows: bad sizes");
+    const int64_t n = n_img * n_per;
+    if (n == 0 || width == 0) return ANERF_OK;
+    if (!src || !rows || !dst) return fail(ANERF_EINVAL, "anerf_gather_rows: missing buffer");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const bool v4 = width % 4 == 0 && reinterpret_cast<uintptr_t>(src) % 16 == 0 &&
+                    reinterpret_cast<uintptr_t>(dst) % 16 == 0;
+    const int64_t items = n * (v4 ? width / 4 : width);
+    const dim3 grid((unsigned)((items + 255) / 256));
+    if (v4)
+        hipLaunchKernelGGL(gather_rows_kernel<4>, grid, dim3(256), 0, st, src, width, n_rows, rows, n_per, n, dst, bad_out);
+    else
+        hipLaunchKernelGGL(gather_rows_kernel<1>, grid, dim3(256), 0, st, src, width, n_rows, rows, n_per, n, dst, bad_out);
+    HIP_TRY(hipGetLastError());
+    return ANERF_OK;
+}
 
 size_t anerf_mlp_forward_pack_bytes(const anerf_mlp_shape* s) {
     if (tf_check(s)) return 0;

@@ -180,8 +180,15 @@ class RayImageDataset:
         rep = rows_d.repeat_interleave(n_per)
         out = {"rays_o": rays[0], "rays_d": rays[1], "target_s": target, "fgs": fg, "bgs": bg,
                "kp_idx": rep, "cam_idxs": rep.clone(), "rays": rays}
-        for k, v in self._pose.items():
-            out[k] = v.index_select(0, rep)
+        # every ray carries its image's pose rows (core/dataset.py:96-104): one anerf_gather_rows each
+        with torch.cuda.device(dev):
+            for k, v in self._pose.items():
+                dst = torch.empty((n,) + tuple(v.shape[1:]), dtype=torch.float32, device=dev)
+                width = int(v[0].numel()) if v.shape[0] else 0
+                rc = lib.anerf_gather_rows(_lib.ptr(v), width, int(v.shape[0]), _lib.ptr(rows_d), n_img, n_per,
+                                           _lib.ptr(dst), None, _lib.stream_handle(dev))
+                _lib.check(rc, "anerf_gather_rows")
+                out[k] = dst
         return out
 
 

@@ -28,6 +28,7 @@
  *   anerf_kp_boxes          kp_to_valid_rays' cylinder + pixel box             core/utils/ray_utils.py:83-136
  *   anerf_ray_batch         BaseH5Dataset.__getitem__ + ray_collate_fn (the    core/dataset.py:57-105, 259-275,
  *                           training ray sampler) over HBM-resident images     346-364, 796-802
+ *   anerf_gather_rows       ray_collate_fn's per-ray pose rows                 core/dataset.py:96-104, 796-802
  * Training stages of render_rays (perturb, raw noise, stochastic importance sampling, gradients):
  *   anerf_train_samples     sample_from_lineseg (perturb > 0)                  core/utils/ray_utils.py:204-251
  *   anerf_train_encode      sample_pts + encode_inputs (+ embedders)           core/raycasters.py:476-555, 650-663
@@ -54,7 +55,7 @@
 extern "C" {
 #endif
 
-#define ANERF_ABI_VERSION 11
+#define ANERF_ABI_VERSION 12
 
 enum {
     ANERF_OK = 0,
@@ -320,6 +321,13 @@ int anerf_ray_batch(const uint8_t* imgs, const uint8_t* masks, const uint8_t* bg
                     int32_t H, int32_t W, const int64_t* rows, int64_t n_img, const int64_t* pixels, int64_t n_per,
                     int32_t mask_img, float* rays_out, float* target_out, float* fg_out, float* bg_out,
                     int32_t* bad_out, void* stream);
+
+/* Per-ray copies of per-image rows (ray_collate_fn's kp3d / bones / skts / cyls, core/dataset.py:
+ * 96-104, 796-802: every ray of batch image i carries image i's pose rows): dst [n_img * n_per][width]
+ * = src [rows[t / n_per]][width] float32, one launch per array (ABI 12; before, torch index_select).
+ * A row outside [0, n_rows) gives NaN rows and sets *bad_out = 1 (device int32, may be NULL). */
+int anerf_gather_rows(const float* src, int64_t width, int64_t n_rows, const int64_t* rows, int64_t n_img,
+                      int64_t n_per, float* dst, int32_t* bad_out, void* stream);
 
 /* ---- Training stages.  All pointers are device pointers; random numbers are
  * inputs (torch.rand / torch.randn draws of the caller), so a run can reproduce the reference's. */

@@ -26,7 +26,7 @@ def test_header_declares_expected_entry_points():
               "anerf_density_points", "anerf_density_grid", "anerf_gen_rays_box", "anerf_compose_box",
               "anerf_pose_kinematics", "anerf_kp_boxes", "anerf_train_samples", "anerf_train_encode",
               "anerf_train_encode_backward", "anerf_train_composite", "anerf_train_composite_backward",
-              "anerf_train_importance", "anerf_pose_kinematics_backward", "anerf_ray_batch",
+              "anerf_train_importance", "anerf_pose_kinematics_backward", "anerf_ray_batch", "anerf_gather_rows",
               "anerf_mlp_split_bytes", "anerf_mlp_split_weights", "anerf_mlp_split_weights_batch", "anerf_mlp_gemm", "anerf_mlp_wgrad_workspace",
               "anerf_mlp_wgrad"):
         assert f in fns

@@ -47,6 +47,9 @@ def test_ray_batch_vs_reference(name):
         np.testing.assert_array_equal(_np(out[k]), G[f"{name}/out/{k}"], err_msg=k)
     np.testing.assert_array_equal(_np(out["rays"][0]), _np(out["rays_o"]))
     assert out["skts"].shape == (len(q) * pix.shape[1], 24, 4, 4)
+    rep = np.repeat(np.asarray(q), pix.shape[1])
+    for k in ("kp3d", "bones", "skts", "cyls"):  # anerf_gather_rows: each ray carries its image's rows
+        np.testing.assert_array_equal(_np(out[k]), np.asarray(data[k], np.float32)[rep], err_msg=k)
 
 
 def test_ray_batch_full_size_vs_oracle():
@@ -77,6 +80,9 @@ def test_ray_batch_full_size_vs_oracle():
     ref = odata.ray_batch(data, q, pix, mask_img=True)
     for k in ("rays_o", "rays_d", "target_s", "fgs", "bgs"):
         np.testing.assert_array_equal(_np(out[k]), ref[k], err_msg=k)
+    rep = np.repeat(q, 3072)
+    for k in ("kp3d", "bones", "skts", "cyls"):  # float4 rows (kp3d, bones, skts) and 5-float rows (cyls)
+        np.testing.assert_array_equal(_np(out[k]), data[k][rep], err_msg=k)
 
 
 def test_ray_batch_rejects_out_of_range():
@@ -99,3 +105,21 @@ def test_ray_batch_empty():
     ds = dmod.RayImageDataset(data, **kw)
     out = ds.get_batch([])
     assert out["rays_o"].shape == (0, 3) and out["target_s"].shape == (0, 3)
+
+
+def test_gather_rows_out_of_range_rows_are_nan_and_flagged():
+    lib = importlib.import_module("a-nerf_amd._lib")
+    L = lib.load()
+    src = torch.arange(3 * 8, dtype=torch.float32, device="cuda").reshape(3, 8)
+    for width, s in ((8, src), (5, src[:, :5].contiguous())):
+        rows = torch.tensor([2, 3, 0], dtype=torch.int64, device="cuda")
+        dst = torch.empty(6, width, device="cuda")
+        bad = torch.zeros(1, dtype=torch.int32, device="cuda")
+        rc = L.anerf_gather_rows(lib.ptr(s), width, 3, lib.ptr(rows), 3, 2, lib.ptr(dst), lib.ptr(bad),
+                                 lib.stream_handle(torch.device("cuda", 0)))
+        lib.check(rc, "anerf_gather_rows")
+        torch.cuda.synchronize()
+        assert int(bad.item()) == 1
+        assert torch.isnan(dst[2:4]).all()
+        torch.testing.assert_close(dst[0:2], s[2].expand(2, -1), rtol=0, atol=0)
+        torch.testing.assert_close(dst[4:6], s[0].expand(2, -1), rtol=0, atol=0)
