@@ -549,3 +549,27 @@ def test_bf16x3_executes_bf16_mfmas():
     assert int(rc32.last_mfma[1].item()) == 0
     # each 32x32 block of a hidden layer: 16 f32 MFMAs (k = 2 each) -> 6 bf16 MFMAs (k = 16, x3)
     assert (f32_only - n_f32) * 6 == n_bf16 * 16
+
+
+@pytest.mark.parametrize("precision", ["bf16x6", "fp16x3"])
+def test_ragged_workgroups_split_modes(precision):
+    """bf16x6's block loop runs the same trip count on every wave (a workgroup barrier per hidden
+    layer); a wave past its workgroup's last block redoes it without storing or counting.  Ragged
+    batches (workgroups of 1-3 rays, block counts not a multiple of 4) must give each ray the outputs
+    it gets alone, and the MFMA tally must add up over rays (no duplicate block counted)."""
+    g = Golden("c3_512_s64i128_d8w256")
+    rc = _caster_prec(g, precision)
+    # near / far of the 37 rays fixed once (their chunk's NaN fill), so any subset renders as in the batch
+    rbt = torch.from_numpy(np.ascontiguousarray(g.ray_batch()[:37])).cuda()
+    anerf.raycaster.near_far(rbt, torch.from_numpy(g["cyls"][0:1]).cuda(), out=(rbt[:, 6], rbt[:, 7]))
+    rb = rbt.cpu().numpy()
+    full = _render(rc, g, rb, count_mfma=True, near_far_given=True)
+    t37 = rc.last_mfma.clone()
+    for i in (0, 5, 36):
+        one = _render(rc, g, rb[i:i + 1], near_far_given=True)
+        for k in ("rgb_map", "disp_map", "acc_map", "rgb0"):
+            np.testing.assert_array_equal(one[k][0], full[k][i], err_msg=f"ray {i} {k}")
+    _render(rc, g, rb[:34], count_mfma=True, near_far_given=True)
+    t34 = rc.last_mfma.clone()
+    _render(rc, g, rb[34:37], count_mfma=True, near_far_given=True)
+    assert torch.equal(t37, t34 + rc.last_mfma), (t37, t34, rc.last_mfma)
