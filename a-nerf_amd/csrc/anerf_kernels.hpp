@@ -195,7 +195,11 @@ __global__ __launch_bounds__(256, 1) void density_kernel(ModelDev M, DensityArgs
     float* uf = (M.skip + 1 < M.D) ? lds + P.uf + wave * P.uf_stride : nullptr;
     const float* wa = lds + P.bias + (M.D + 1) * W + hh * (W / 2);
     const int64_t nb = (A.n + 31) / 32;
-    for (int64_t b = (int64_t)blockIdx.x * 4 + wave; b < nb; b += (int64_t)gridDim.x * 4) {
+    // (the same trip count on every wave: bf16x6's mlp_trunk has a workgroup barrier per hidden layer;
+    // a wave past the last block redoes it without storing)
+    for (int64_t base = (int64_t)blockIdx.x * 4; base < nb; base += (int64_t)gridDim.x * 4) {
+        const bool own = base + wave < nb;
+        const int64_t b = own ? base + wave : nb - 1;
         const int64_t s_out = b * 32 + (lane & 31);
         const int64_t s = s_out < A.n ? s_out : A.n - 1;
         float px, py, pz;
@@ -211,7 +215,7 @@ __global__ __launch_bounds__(256, 1) void density_kernel(ModelDev M, DensityArgs
         JointMask mask;
         Ring ring;
         int es = 0;
-        mlp_trunk<W, MR, false, PREC>(M, net, lds + P.sk, lds + P.cut, px, py, pz, lane, lds + P.bias, uf, nullptr, acc, h, ring,
+        mlp_trunk<W, MR, false, PREC, true>(M, net, lds + P.sk, lds + P.cut, px, py, pz, lane, lds + P.bias, uf, nullptr, acc, h, ring,
                          mask, nullptr, st, es);
         // alpha_linear on relu(h_last), in the k-step order of the render path's fused alpha head
         float sig = 0.0f;
@@ -220,7 +224,7 @@ __global__ __launch_bounds__(256, 1) void density_kernel(ModelDev M, DensityArgs
         if constexpr (PREC == 3) sig *= pow2f(-es);  // (fp16x3: the last layer's units)
         sig += __shfl_xor(sig, 32);
         sig += net.balpha;
-        if (hh == 0 && s_out < A.n) A.out[s_out] = sig;
+        if (own && hh == 0 && s_out < A.n) A.out[s_out] = sig;
     }
 }
 

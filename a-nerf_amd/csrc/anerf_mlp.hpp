@@ -1246,7 +1246,7 @@ __device__ __forceinline__ int view_dir_part(f32x16 (&acc)[RBV], const ModelDev&
 // Encoder + density trunk of one 32-sample block: L0 (u and v parts), the hidden layers with the
 // skip; acc ends as the pre-activation of the last hidden layer.  `after_last` is the weight stream
 // that follows (the feature layer, or nothing for density-only queries).
-template <int W, int MR, bool WV, int P>
+template <int W, int MR, bool WV, int P, bool SYNC = WV>
 __device__ __forceinline__ bool mlp_trunk(const ModelDev& M, const NetDev& net, const float* __restrict__ sk,
                                           const float* __restrict__ cut, float px, float py, float pz, int lane,
                                           const float* __restrict__ bias, float* __restrict__ uf,
@@ -1291,9 +1291,9 @@ __device__ __forceinline__ bool mlp_trunk(const ModelDev& M, const NetDev& net, 
         // memory fence: the ring's loads stay in flight), so each 3 KiB weight group is read from L2
         // about once per CU and the other waves hit the CU's L1 — the hidden layers stream 12 KiB per
         // CU per group otherwise, and the waves drift apart over the windowed parts' live joints.
-        // +2.1 % (A/B, profiles/r03_ab_experiments.txt); the render kernel's block loop has the same
-        // trip count on every wave (the density kernel's grid-stride loop does not: WV = false there).
-        if constexpr (WV && P == 2) __builtin_amdgcn_s_barrier();
+        // +2.1 % (A/B, profiles/r03_ab_experiments.txt); the calling block loop must have the same
+        // trip count on every wave (SYNC: the render and density kernels' block loops).
+        if constexpr (SYNC && P == 2) __builtin_amdgcn_s_barrier();
         if constexpr (P == 3) {
             // the next h3 phase (the next hidden layer or the view layer) is prefetched; not across the
             // skip layer's x parts, which load themselves and scale their B operands by 2^es (the
