@@ -73,6 +73,8 @@ __global__ __launch_bounds__(256, 1) void render_kernel(ModelDev M, RenderArgs A
         // layer; a wave past the last block redoes that block without storing or counting it)
         for (int it = 0; it < (nr * nb + 3) / 4; ++it) {
             const bool own = it * 4 + wave < nr * nb;
+            if constexpr (PREC != 2)  // (no workgroup barrier inside: a wave without a block is done)
+                if (!own) break;
             const int b = own ? it * 4 + wave : nr * nb - 1;
             const int r = b / nb, s0 = (b % nb) * 32;
             const float* zr = only_new ? lds + P.scr + P.scr_stride * r + 6 * P.z_stride : lds + zoff + P.z_stride * r;
@@ -199,6 +201,8 @@ __global__ __launch_bounds__(256, 1) void density_kernel(ModelDev M, DensityArgs
     // a wave past the last block redoes it without storing)
     for (int64_t base = (int64_t)blockIdx.x * 4; base < nb; base += (int64_t)gridDim.x * 4) {
         const bool own = base + wave < nb;
+        if constexpr (PREC != 2)
+            if (!own) break;
         const int64_t b = own ? base + wave : nb - 1;
         const int64_t s_out = b * 32 + (lane & 31);
         const int64_t s = s_out < A.n ? s_out : A.n - 1;

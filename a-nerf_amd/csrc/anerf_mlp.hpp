@@ -1293,7 +1293,10 @@ __device__ __forceinline__ bool mlp_trunk(const ModelDev& M, const NetDev& net, 
         // CU per group otherwise, and the waves drift apart over the windowed parts' live joints.
         // +2.1 % (A/B, profiles/r03_ab_experiments.txt); the calling block loop must have the same
         // trip count on every wave (SYNC: the render and density kernels' block loops).
-        if constexpr (SYNC && P == 2) __builtin_amdgcn_s_barrier();
+        if constexpr (SYNC && P == 2) {
+            __builtin_amdgcn_s_barrier();
+            STAMP(st, 18);  // (stamps build: the wait at this barrier)
+        }
         if constexpr (P == 3) {
             // the next h3 phase (the next hidden layer or the view layer) is prefetched; not across the
             // skip layer's x parts, which load themselves and scale their B operands by 2^es (the

@@ -96,8 +96,9 @@ hipError_t tf_launch(const TfArgs& a, long long m, hipStream_t st) {
     constexpr int RB = W / 32;
     const size_t lds = sizeof(float) * ((size_t)(a.D + 1) * W + W / 2 + 2 * RB * 16 + 3 * 2 * (RB / 2) * 16 +
                                         (size_t)4 * 32 * (W + 4));
-    static const hipError_t attr = hipFuncSetAttribute((const void*)train_mlp_fwd_kernel<W>,
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    // (per call: the attribute belongs to the current device, and a cached failure would stick)
+    const hipError_t attr = hipFuncSetAttribute((const void*)train_mlp_fwd_kernel<W>,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (attr != hipSuccess) return attr;
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     int dev = 0, ncu = 256;

@@ -1,7 +1,7 @@
 // anerf_train.hpp — training-mode stages of RayCaster.render_rays: stratified
 // samples, the encoder forward and backward (gradient to the skeleton transforms, i.e. to the pose
 // optimisation), raw2outputs forward and backward, and stochastic importance sampling.  The MLP
-// between them runs as plain fp32 GEMMs (hipBLASLt through torch autograd, a-nerf_amd/train.py).
+// between them runs on the hand-written split-bf16 GEMMs of anerf_gemm.hip (a-nerf_amd/mlp.py).
 // Random numbers are inputs (t_rand, noise, u), so a caller can feed the reference's draws.
 // Part of the single translation unit anerf_render.hip (included there, in order).
 #pragma once

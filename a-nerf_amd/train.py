@@ -6,9 +6,11 @@ Mirrors `core/raycasters.py:361-474` (training branch of `RayCaster.forward`, :3
 loss of `Trainer._compute_nerf_loss` (`core/trainer.py:350-381`).  The per-sample stages run as
 HIP kernels through the C ABI (include/anerf.h, `anerf_train_*`): sample placement, the skeleton-
 relative encoding and its backward (dL/dskts), raw2outputs and its backward, importance sampling.
-The MLP between them is plain fp32 GEMMs under torch autograd (hipBLASLt), with the reference's
-concatenations (`cat([x, h])` at the skip, `cat([feature, views(, code)])` at the view layer)
-replaced by split weight blocks, so no concatenated activation is ever materialised.
+The MLP between them is one autograd Function on the hand-written split-bf16 GEMMs of
+`anerf_gemm.hip` (`mlp.py`; default `mlp="mixed"`: bf16x6 forward, bf16x3 gradients; `mlp="fp32"`
+keeps torch's fp32 GEMMs), with the reference's concatenations (`cat([x, h])` at the skip,
+`cat([feature, views(, code)])` at the view layer) replaced by operand segments / split weight
+blocks, so no concatenated activation is ever materialised.
 
 Random numbers: torch's generator on the device by default; pass `rand={"t_rand": (N,S),
 "noise0": (N,S), "u": (N,I), "noise1": (N,S+I)}` (standard-uniform / standard-normal draws; with
@@ -342,11 +344,14 @@ class _Embed(nn.Module):
         return c[1]
 
     def _set(self, name, value):
-        """buffer `name` <- value (a 0-d float32 CPU tensor), host copy included."""
+        """buffer `name` <- value (a 0-d float32 CPU tensor), host copy included.  fill_ with the
+        Python float (exact: a float32 value) launches a fill kernel and never waits on the stream, where
+        a host-to-device copy_ of a pageable 0-d tensor would."""
         t = getattr(self, name)
+        v = float(value)
         with torch.no_grad():
-            t.copy_(value)
-        self._hc[name] = ((t.data_ptr(), t._version), float(value))
+            t.fill_(v)
+        self._hc[name] = ((t.data_ptr(), t._version), v)
 
     def get_tau(self):
         return self.host("tau")

@@ -57,14 +57,16 @@ DTYPE = {
               "W = W0+W1+W2, the six bf16 MFMA products with i + j <= 2 (each dropped term below 2^-23 of |x W|), fp32 "
               "accumulate; encoder, windowed layer-0 part, heads, compositing fp32",
     "fp16x3": "22-bit operands: split fp16 after exact power-of-two scaling (x = x0+x1 within 2^-23 |x|, W = W0+W1), "
-              "three fp16 MFMA products (x1 W1, ~2^-22 of |x W|, dropped), fp32 accumulate; bone-direction parts bf16x6; "
-              "encoder, windowed layer-0 part, heads, compositing fp32",
+              "three fp16 MFMA products (x1 W1, ~2^-22 of |x W|, dropped), fp32 accumulate; bone-direction parts and "
+              "the windowed layer-0 / skip-layer parts bf16x6 at widths 128/256 (fp32 at 64); encoder, heads, "
+              "compositing fp32",
     "bf16x3": "16-bit operands: split bf16 (x = hi+lo, W = hi+lo, three bf16 MFMA products), fp32 accumulate; "
               "fp32 elsewhere",
 }
 PRODUCTS = {"fp32": 1, "bf16x6": 6, "fp16x3": 3, "bf16x3": 3}
 FLOP_F32_MFMA = 32 * 32 * 2 * 2     # v_mfma_f32_32x32x2_f32
 FLOP_BF16_MFMA = 32 * 32 * 16 * 2   # v_mfma_f32_32x32x16_bf16
+TILE = 256  # pixels mode: rays per tile of the round-robin split (distributed.tile_rows)
 
 
 def parse():
@@ -80,6 +82,9 @@ def parse():
     ap.add_argument("--cpu-rays", type=int, default=20000, help="rays in the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline (and its parity check)")
     ap.add_argument("--no-tau20", action="store_true", help="skip the tau = 20 kernel timing")
+    ap.add_argument("--no-balance", action="store_true", help="skip the 8-shard balance projection (N = 1)")
+    ap.add_argument("--other-configs", default=",".join(OTHER_CONFIGS),
+                    help="N = 1: the other 1-GPU configurations measured in the same run ('' = none)")
     ap.add_argument("--no-train", action="store_true",
                     help="skip the training-step leg (SURVEY §8(f) row 2: tools/train_bench.py, N = 1 only)")
     ap.add_argument("--shard", default=None, choices=["frames", "pixels"],
@@ -145,6 +150,124 @@ def kernel_time(rc, rb, S, I, skts, cyl, reps=4):
     return float(np.mean(ts)), tuple(int(v) for v in rc.last_mfma.tolist())
 
 
+def shard_projection(rc, rb_nf, S, I, skts, cyl, world=8, reps=2):
+    """The pixel-sharded step's balance projected on this one GPU: the frame's rays (near / far already
+    filled over the whole frame) cut into `world` shards by the tiled split bench.py runs under the
+    launcher (distributed.tile_rows) and by contiguous equal-ray ranges, each shard rendered alone
+    (best of `reps` HIP-event timings).  An N-rank step waits for its slowest shard: max / mean."""
+    dmod = importlib.import_module("a-nerf_amd.distributed")
+    n = rb_nf.shape[0]
+    splits = {"tiles": [dmod.tile_rows(n, world, r, TILE) for r in range(world)],
+              "ranges": [torch.arange(s0, s1) for s0, s1 in dmod.ray_ranges(n, world)]}
+    res = {}
+    for name, parts in splits.items():
+        ms = []
+        for rows in parts:
+            sub = rb_nf.index_select(0, rows.to(rb_nf.device))
+            m = sub.shape[0]
+            best = None
+            for _ in range(reps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                rc.render_rays(sub, S, skts=skts.expand(m, -1, -1, -1), cyls=cyl.expand(m, -1), N_importance=I,
+                               chunk=4096, ret_alpha=False, near_far_given=True)
+                e1.record()
+                torch.cuda.synchronize()
+                t = e0.elapsed_time(e1)
+                best = t if best is None else min(best, t)
+            ms.append(best)
+        res[name] = {"shard_ms": [round(x, 3) for x in ms], "max_over_mean": round(max(ms) * len(ms) / sum(ms), 4)}
+    return {"world": world, "tile": TILE, "frame_rays": n, "split_run_under_the_launcher": "tiles", **res}
+
+
+# Every other 1-GPU configuration of BASELINE.json, and the reference's shipped render configuration
+# (configs/mixamo/mixamo.txt:28-38,55: 8x256, 64 + 16 samples, opt_framecode), measured in the headline
+# precision on its own frame: kernel rays/s, frac, frac_executed and a 2,000-ray oracle parity check.
+OTHER_CONFIGS = {
+    "config2": dict(res=256, S=64, I=0, joints=24, seed=13, desc="256x256, 64 coarse samples, 24-joint, 8x256"),
+    "config4": dict(res=512, S=64, I=128, joints=65, seed=14,
+                    desc="512x512, 64+128 samples, 65-joint synthetic skeleton (LDS-pressure case), 8x256"),
+    "mixamo_shipped": dict(res=512, S=64, I=16, joints=24, seed=15, framecode=True, cam=2,
+                           desc="configs/mixamo/mixamo.txt: 512x512, 64+16 samples, 24-joint, 8x256, "
+                                "opt_framecode (5 codes, camera 2)"),
+}
+
+
+def other_config_leg(a, name, spec, dev, n_parity=2000):
+    """One OTHER_CONFIGS entry: its own synthetic scene and seeded checkpoint, the whole bounding box's rays,
+    render kernel time (kernel_time), the MFMA tally's executed fraction, and the C oracle on n_parity
+    evenly spaced rays (near / far of the whole frame's chunks) at 1e-4 (near-empty disp: + the
+    reference's measured spread, oracle.h12_spread)."""
+    anerf = importlib.import_module("a-nerf_amd")
+    syn = importlib.import_module("a-nerf_amd.synthetic")
+    _lib = importlib.import_module("a-nerf_amd._lib")
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+    H, S, I, nj = spec["res"], spec["S"], spec["I"], spec["joints"]
+    fc = bool(spec.get("framecode"))
+    cfg = anerf.RenderConfig(n_joints=nj, N_samples=S, N_importance=I, precision=a.precision, opt_framecode=fc,
+                             n_framecodes=5 if fc else 0).validate()
+    ck = syn.make_checkpoint(spec["seed"], n_joints=nj, D=8, W=256, fine=I > 0, tau=a.tau, use_framecode=fc,
+                             n_framecodes=5 if fc else 0)
+    sc = syn.make_scene(n_joints=nj, H=H, W=H, seed=spec["seed"])
+    rc = anerf.RayCaster(cfg, ck, device=dev.index or 0)
+    idxs, cyls, boxes = anerf.rays.valid_pixels(sc["c2ws"], H, H, sc["focal"], kps=sc["kps"], ext_scale=0.001)
+    (x0, y0), (x1, y1) = (int(v) for v in boxes[0][0]), (int(v) for v in boxes[0][1])
+    n = (x1 - x0) * (y1 - y0)
+    c2w_np = np.ascontiguousarray(sc["c2ws"][0][:3, :4])
+    c2w = torch.from_numpy(c2w_np).to(dev)
+    rb = torch.empty(n, 11, device=dev)
+    _lib.check(_lib.load().anerf_gen_rays_box(_lib.ptr(c2w), H, H, sc["focal"], sc["focal"], 0.0, 0.0, 0, x0, y0, x1,
+                                              y1, 0.0, 1.0, _lib.ptr(rb), _lib.stream_handle(dev)), "gen_rays_box")
+    skts = torch.from_numpy(sc["skts"][0:1]).to(dev)
+    cyl = torch.from_numpy(cyls[0:1]).to(dev)
+    cams = torch.full((n,), float(spec.get("cam", 0)), device=dev) if fc else None
+    ts = []
+    for it in range(4):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        out = rc.render_rays(rb, S, skts=skts.expand(n, -1, -1, -1), cyls=cyl.expand(n, -1), cams=cams,
+                             N_importance=I, chunk=4096, ret_alpha=False)
+        e1.record()
+        torch.cuda.synchronize()
+        if it:
+            ts.append(e0.elapsed_time(e1))
+    ms = float(np.mean(ts))
+    rc.render_rays(rb, S, skts=skts.expand(n, -1, -1, -1), cyls=cyl.expand(n, -1), cams=cams, N_importance=I,
+                   chunk=4096, ret_alpha=False, count_mfma=True)
+    torch.cuda.synchronize()
+    nf, nb = (int(v) for v in rc.last_mfma.tolist())
+    ppeak, pflop = mix_peak(nf, nb)
+    flop_ray = anerf.flops_per_sample(cfg) * anerf.samples_per_ray(cfg)
+    # parity: the oracle on evenly spaced rays of this frame
+    om = oracle.OracleModel(cfg, ck)
+    rb_h = oracle.gen_rays(sc["c2ws"][0][:3, :4], H, H, sc["focal"], idxs[0])
+    near_f, far_f, _, _ = om.near_far(rb_h, cyls[0:1], chunk=4096)
+    sel = np.linspace(0, n - 1, min(n_parity, n)).astype(np.int64)
+    ref = om.render_rays(rb_h[sel], sc["skts"][0], cyls[0:1], chunk=4096, nthreads=cpu_threads(), near=near_f[sel],
+                         far=far_f[sel], cams=np.full(len(sel), float(spec.get("cam", 0)), np.float32) if fc else None)
+    sel_d = torch.from_numpy(sel).to(dev)
+    keys = ["rgb_map", "disp_map", "acc_map"] + (["rgb0", "disp0", "acc0"] if I > 0 else [])
+    errs, ne_n, ne_err = {}, 0, 0.0
+    for k in keys:
+        d = np.abs(out[k].index_select(0, sel_d).cpu().numpy().astype(np.float64) - ref[k]).reshape(len(sel), -1).max(-1)
+        acc_k = ref["acc0" if k.endswith("0") else "acc_map"]
+        empty = ((acc_k > 0) & (acc_k < 2.0 ** -20)) if k.startswith("disp") else np.zeros(len(sel), bool)
+        errs[k] = float(f"{d[~empty].max():.3e}")
+        if empty.any():
+            ne_n, ne_err = max(ne_n, int(empty.sum())), max(ne_err, float(d[empty].max()))
+    ne_tol = 1e-4 + oracle.h12_spread()["float64"]
+    ok = max(errs.values()) <= 1e-4 and ne_err <= ne_tol
+    return {"workload": spec["desc"], "rays_per_frame": n, "tau": a.tau, "precision": a.precision,
+            "kernel_ms": round(ms, 3), "rays_per_s_kernel": round(n / (ms * 1e-3), 1),
+            "reference_flop_per_ray": flop_ray,
+            "frac": round(flop_ray * n / (ms * 1e-3) / 1e12 / pipe_peak(a.precision), 4),
+            "frac_executed": round(pflop / (ms * 1e-3) / 1e12 / ppeak, 4),
+            "parity": {"rays": int(len(sel)), "max_abs_err": errs, "near_empty_rays": ne_n,
+                       "near_empty_disp_max_abs_err": float(f"{ne_err:.3e}"), "ok": bool(ok),
+                       "against": "C oracle, near/far from the whole frame's 4096-ray chunks"}}
+
+
 def mix_peak(n_f32, n_bf16):
     """Instruction-mix-weighted MFMA peak (TFLOP/s) and the executed FLOPs of a tally."""
     flop = n_f32 * FLOP_F32_MFMA + n_bf16 * FLOP_BF16_MFMA
@@ -192,18 +315,21 @@ def parity_leg(a, cfg, ck, sc, cyls, idx, c2w_np, H, W, out, n, dev, want_cpu):
     diff = {k: np.abs(out[k].index_select(0, sel_d).cpu().numpy().astype(np.float64) - ref[k].astype(np.float64))
             for k in ("rgb_map", "disp_map", "acc_map")}
     # H12: on a near-empty ray (0 < acc < 2^-20) disp = 1 / max(1e-10, depth / acc) is a ratio
-    # of a few 2^-24 alpha quanta, and a raw-sigma ulp at a rounding threshold moves a quantum (1 of
-    # config 5's 169 such rays differs from the reference by 1.7e-4 in fp32 / bf16x6,
-    # tests/golden/h12_nearempty_c5.npz).  Such rays are counted and their disp error reported and
-    # bounded (5e-4, and at most 0.1 % of the sample); every other output of every ray is held to 1e-4
+    # of a few 2^-24 alpha quanta; the reference's own float32 disp on such rays sits up to 1.92e-4 from
+    # its float64 value (tests/golden/h12_spread_c5.npz, oracle.h12_spread).  Such rays are counted and
+    # their disp held to 1e-4 + that measured spread; every other output of every ray to 1e-4
     empty = (ref["acc_map"] > 0) & (ref["acc_map"] < 2.0 ** -20)
     errs = {k: float(v[~empty].max() if k == "disp_map" and empty.any() and (~empty).any() else v.max())
             for k, v in diff.items()}
     ne_err = float(diff["disp_map"][empty].max()) if empty.any() else 0.0
-    ok = max(errs.values()) <= 1e-4 and ne_err <= 5e-4 and int(empty.sum()) <= max(1, len(sel) // 1000)
+    ne_tol = 1e-4 + oracle.h12_spread()["float64"]
+    ok = max(errs.values()) <= 1e-4 and ne_err <= ne_tol
     parity = {"rays": int(len(sel)), "max_abs_err": {k: float(f"{v:.3e}") for k, v in errs.items()},
               "near_empty_rays": int(empty.sum()), "near_empty_disp_max_abs_err": float(f"{ne_err:.3e}"),
-              "tol": 1e-4, "near_empty_tol": {"disp": 5e-4, "max_rays": max(1, len(sel) // 1000)}, "ok": bool(ok),
+              "tol": 1e-4, "near_empty_tol": {"disp": float(f"{ne_tol:.3e}"),
+                                             "source": "1e-4 + the reference's own float32-vs-float64 disp spread on "
+                                                       "near-empty rays (tests/golden/h12_spread_c5.npz)"},
+              "ok": bool(ok),
               "against": "C oracle (pinned to the reference's golden fixtures) on the same rays, near/far "
                          "from the whole frame's 4096-ray chunks"}
     return parity, cpu
@@ -262,20 +388,22 @@ def main():
     st = _lib.stream_handle(dev)
     ev = []
     sharded = pixels and dist
-    # this rank's rays: pixels mode = an equal share of the frame's ray list (distributed.ray_ranges),
-    # generated from the resident pixel indices of the whole 4096-ray chunks that cover it, whose near /
-    # far (cylinder + chunk NaN fill) the rank computes so its rays render exactly as in the whole frame
-    # (ANERF_FLAG_NEAR_FAR); otherwise the whole box
-    ranges = dmod.ray_ranges(n, world) if sharded else [(0, n)]
-    s0, s1 = ranges[rank if sharded else 0]
-    c0, c1 = dmod.chunk_cover(s0, s1, 4096, n) if sharded else (s0, s1)
-    n_mine, n_cover = s1 - s0, c1 - c0
-    rb_cover = torch.empty(max(n_cover, 1), 11, device=dev)[:n_cover]
-    rb = rb_cover[s0 - c0:s1 - c0]
-    idx_all = torch.from_numpy(np.ascontiguousarray(idxs[0], np.int64)).to(dev)
+    # this rank's rays: pixels mode = the frame's ray list cut into 256-ray tiles dealt round-robin over
+    # the ranks (distributed.tile_rows: per-ray cost follows the live joints, and contiguous ranges put
+    # the torso's rays on a few ranks, 1.05x max/mean vs 1.002x, tools/shard_balance.py); every rank
+    # generates the whole box's rays and fills near / far (cylinder + chunk NaN fill) over the whole
+    # frame's chunks (0.1 ms), so its rays render exactly as in the whole frame (ANERF_FLAG_NEAR_FAR),
+    # and renders its own tiles; otherwise the whole box
+    rb_all = torch.empty(n, 11, device=dev)
     if sharded:
-        idx_cover = idx_all[c0:c1].contiguous()
-        gather = dmod.ShardGather(n, 4096, world, dev, ranges=ranges)
+        rank_rows = [dmod.tile_rows(n, world, r, TILE) for r in range(world)]
+        rows_mine = rank_rows[rank].to(dev)
+        n_mine = int(rows_mine.shape[0])
+        rb = torch.empty(max(n_mine, 1), 11, device=dev)[:n_mine]
+        gather = dmod.ShardGather(n, 4096, world, dev, rank_rows=rank_rows)
+    else:
+        n_mine, rb = n, rb_all
+    idx_all = torch.from_numpy(np.ascontiguousarray(idxs[0], np.int64)).to(dev)
     last = {}
 
     def render(r):
@@ -289,15 +417,11 @@ def main():
         return e
 
     def step(record):
-        if sharded:
-            if n_mine:
-                _lib.check(lib.anerf_gen_rays(_lib.ptr(c2w), H, W, sc["focal"], sc["focal"], 0.0, 0.0, 0,
-                                              _lib.ptr(idx_cover), n_cover, 0.0, 1.0, _lib.ptr(rb_cover), st),
-                           "gen_rays")
-                near_far(rb_cover, cyl, chunk=4096, out=(rb_cover[:, 6], rb_cover[:, 7]))
-        else:
-            _lib.check(lib.anerf_gen_rays_box(_lib.ptr(c2w), H, W, sc["focal"], sc["focal"], 0.0, 0.0, 0, x0, y0, x1,
-                                              y1, 0.0, 1.0, _lib.ptr(rb), st), "gen_rays_box")
+        _lib.check(lib.anerf_gen_rays_box(_lib.ptr(c2w), H, W, sc["focal"], sc["focal"], 0.0, 0.0, 0, x0, y0, x1,
+                                          y1, 0.0, 1.0, _lib.ptr(rb_all), st), "gen_rays_box")
+        if sharded and n_mine:
+            near_far(rb_all, cyl, chunk=4096, out=(rb_all[:, 6], rb_all[:, 7]))
+            torch.index_select(rb_all, 0, rows_mine, out=rb)
         e0 = event()
         out = render(rb) if n_mine else None
         e1 = event()
@@ -399,6 +523,21 @@ def main():
                      "frac_executed": round(tflop / (tms * 1e-3) / 1e12 / tpeak, 4)}
             del rc20
 
+    # N = 1: the 8-rank pixel split's balance, projected on this GPU (each shard of this frame alone)
+    balance = None
+    if rank == 0 and world == 1 and not a.no_balance:
+        rb_nf = rb_all.clone()
+        near_far(rb_nf, cyl, chunk=4096, out=(rb_nf[:, 6], rb_nf[:, 7]))
+        balance = shard_projection(rc, rb_nf, S, I, skts, cyl)
+        del rb_nf
+
+    # N = 1: every other 1-GPU BASELINE configuration and the shipped mixamo configuration, same precision
+    other_cfgs = {}
+    if rank == 0 and world == 1:
+        for name in [x for x in a.other_configs.split(",") if x]:
+            other_cfgs[name] = other_config_leg(a, name, OTHER_CONFIGS[name], dev)
+            torch.cuda.empty_cache()
+
     # N = 1: the training step of the same path at the reference's training configuration (§8(f) row 2)
     training = None
     if rank == 0 and world == 1 and not a.no_train:
@@ -416,7 +555,7 @@ def main():
     if rank == 0:
         value = rays_job / elapsed
         workload = (f"{_config_name(H, S, I, a.joints)}: {H}x{W} frame, {S}+{I} samples, {a.joints}-joint, 8x256 MLP, "
-                    + (f"one frame per step split over {world} GPU(s) in ray-balanced ranges (near/far from the whole frame's 4096-ray chunks) + RCCL all-gather"
+                    + (f"one frame per step split over {world} GPU(s) in {TILE}-ray tiles dealt round-robin (near/far from the whole frame's 4096-ray chunks) + RCCL all-gather"
                        if sharded else "one frame per GPU per step"))
         ranks = [{"rank": r, "rays": int(p[3]), "render_ms": round(p[0], 3), "all_gather_ms": round(p[1], 3),
                   "compose_ms": round(p[2], 3)} for r, p in enumerate(per_rank)]
@@ -469,6 +608,8 @@ def main():
                          "reference_flop_per_ray": flop_ray},
             "parity": parity,
             "tau20": tau20,
+            "shard_balance_projection": balance,
+            "other_configs": other_cfgs or None,
             "cpu_baseline": cpu,
             "other_precisions": others or None,
             "training": training,
@@ -478,6 +619,9 @@ def main():
         tdist.destroy_process_group()
     if parity is not None and not parity["ok"]:
         sys.exit(f"parity check failed: {parity}")
+    bad = {k: v["parity"] for k, v in (other_cfgs or {}).items() if not v["parity"]["ok"]} if rank == 0 else {}
+    if bad:
+        sys.exit(f"parity check failed on other configs: {bad}")
 
 
 if __name__ == "__main__":

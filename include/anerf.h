@@ -77,14 +77,16 @@ enum {
  *                     with i + j <= 2 of x_i w_j on v_mfma_f32_32x32x16_bf16, fp32 accumulation: the
  *                     dropped terms are below 2^-23 of each product (fp32 rounds a product to 2^-24),
  *                     so the contraction is fp32-accurate; layer 0's and the skip layer's bone-direction
- *                     parts the same way; encoder, the windowed layer-0 part and heads fp32;
+ *                     parts the same way, and their windowed (per-joint sin/cos) parts too at widths
+ *                     128 / 256 (fp32 at width 64); encoder and heads fp32;
  *   ANERF_PREC_FP16X3 the dense hidden layers and the fused view layer in fp16 after exact power-of-two
  *                     scaling (weights per layer, activations per sample, both to a maximum in
  *                     [2^10, 2^11)): x = x0 + x1, w = w0 + w1 (22 significant bits each), computed as
  *                     x0 w0 + x0 w1 + x1 w0 on v_mfma_f32_32x32x16_f16 (exact products, fp32 accumulation,
  *                     the dropped x1 w1 ~2^-22 of |x w|): half of bf16x6's MFMAs, 22-bit instead of
  *                     24-bit operands;
- *                     bone-direction parts as in bf16x6; encoder, layer 0's windowed part and heads fp32. */
+ *                     bone-direction parts and (widths 128 / 256) the windowed parts of layer 0 and the
+ *                     skip layer as in bf16x6 (fp32 at width 64); encoder and heads fp32. */
 enum { ANERF_PREC_FP32 = 0, ANERF_PREC_BF16X3 = 1, ANERF_PREC_BF16X6 = 2, ANERF_PREC_FP16X3 = 3 };
 /* Flags OR-ed into anerf_render_rays' precision argument (and anerf_train_samples' flags):
  *   ANERF_FLAG_LINDISP  sample linearly in inverse depth, z = 1 / (1/near (1 - t) + 1/far t)
@@ -132,7 +134,8 @@ typedef struct {
 /* --cutoff_bones (core/raycasters.py:52-64): the bone embedder is a CutoffEmbedder (dist_inputs, its
  * own tau and cutoff_dist: anerf_embed_params tau_b / cutoff_dist_b); with --multires_bones 0 its
  * output is the bone direction times w_b = 1 - sigmoid(tau_b (dist - c_b)) when use_cutoff and
- * cutoff_inputs (core/cutoff_embedder.py:111-166), the bare direction otherwise. */
+ * cutoff_inputs (core/cutoff_embedder.py:111-166), the bare direction otherwise.  The flag is ignored
+ * (and tau_b / cutoff_dist_b unused) unless desc->use_cutoff and desc->cutoff_inputs are both set. */
 #define ANERF_ENC_CUTOFF_BONES 4
 
 /* HOST pointers to one NeRF's weights, torch nn.Linear layout [out][in] (core/networks/nerf.py:57-88). */

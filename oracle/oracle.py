@@ -248,3 +248,22 @@ def linspace(n):
     out = np.empty(n, np.float32)
     lib().oracle_linspace(n, _p(out))
     return out
+
+
+
+H12_SPREAD = os.path.join(os.path.dirname(HERE), "tests", "golden", "h12_spread_c5.npz")
+
+
+def h12_spread(path=H12_SPREAD):
+    """The reference's own disparity spread on near-empty rays (hazard H12), measured by
+    tests/golden/make_h12_golden.py spread: the reference's render_rays on config 5's 169 near-empty
+    rays (0 < acc < 2^-20) rendered with 8 threads (= the fixture), 1 thread, and in float64.  Returns
+    dict(threads=max |t8 - t1|, float64=max |t8 - f64|, per_ray=|t8 - f64| [169]) over those rays:
+    a near-empty ray's disp = (acc + 1e-10) / depth is a ratio of a few 2^-24 alpha quanta, and the
+    reference's float32 value sits up to that far from its own exact value."""
+    z = np.load(path)
+    ne = z["near_empty"]
+    t8 = z["t8_disp_map"].astype(np.float64)
+    d81 = np.abs(t8 - z["t1_disp_map"])[ne]
+    d8f = np.abs(t8 - z["f64_disp_map"])[ne]
+    return {"threads": float(d81.max()), "float64": float(d8f.max()), "per_ray": d8f}

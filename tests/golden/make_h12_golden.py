@@ -113,5 +113,91 @@ def fixture():
           f"near-empty max {dd[ne].max():.3e} ({int((dd[ne] > 1e-4).sum())} > 1e-4), ordinary max {dd[~ne].max():.3e}")
 
 
+def _reference_runs(mods, render_kwargs, sc, o, d):
+    """The reference's render_rays on rays (o, d) three ways: torch.set_num_threads(8) (the fixture's
+    own setting), (1), and with the networks, embedders and every input in float64
+    (torch.set_default_dtype(float64): linspace, the 1e10 / ones constants of raw2outputs follow).  The
+    fine pass's raw sigma, alpha, weights and z are captured by wrapping network_fine.raw2outputs."""
+    import torch
+    _, trainer, _, _, _ = mods
+    rc = render_kwargs["ray_caster"]
+    net = rc.network_fine
+    orig = net.raw2outputs
+    cap = {}
+
+    def hook(raw, z_vals, rays_d, *a, **k):
+        ret = orig(raw, z_vals, rays_d, *a, **k)
+        cap.setdefault("sigma", []).append(raw[..., 3].detach().to(torch.float64).numpy())
+        cap.setdefault("alpha", []).append(ret["alpha"].detach().to(torch.float64).numpy())
+        cap.setdefault("weights", []).append(ret["weights"].detach().to(torch.float64).numpy())
+        cap.setdefault("z", []).append(z_vals.detach().to(torch.float64).numpy())
+        return ret
+
+    net.raw2outputs = hook
+    runs = {}
+    try:
+        for name, threads, f64 in (("t8", 8, False), ("t1", 1, False), ("f64", 8, True)):
+            cap.clear()
+            torch.set_num_threads(threads)
+            dt = torch.float64 if f64 else torch.float32
+            torch.set_default_dtype(dt)
+            rc.to(dt)
+            n = o.shape[0]
+            oo, dd = torch.as_tensor(o).to(dt), torch.as_tensor(d).to(dt)
+            vd = dd / torch.norm(dd, dim=-1, keepdim=True)
+            rays = torch.cat([oo, dd, torch.zeros(n, 1, dtype=dt), torch.ones(n, 1, dtype=dt), vd], -1)
+            kw = {k: v for k, v in render_kwargs.items() if k not in ("use_viewdirs", "near", "far", "center", "c2w_staticcam")}
+            with torch.no_grad():
+                ret = trainer.batchify_rays(rays, 4096, kp_batch=torch.from_numpy(sc["kps"][0:1]).to(dt).expand(n, -1, -1),
+                                            skts=torch.from_numpy(sc["skts"][0:1]).to(dt).expand(n, -1, -1, -1),
+                                            cyls=torch.from_numpy(sc["cyls"][0:1]).to(dt).expand(n, -1),
+                                            bones=torch.from_numpy(sc["bones"][0:1]).to(dt).expand(n, -1, -1),
+                                            cams=None, subject_idxs=None, **kw)
+            runs[name] = {k: v.to(torch.float64).numpy() for k, v in ret.items() if not k.startswith("alpha")}
+            runs[name].update({k: np.concatenate(v, 0) for k, v in cap.items()})
+            print(f"reference run {name}: {n} rays", flush=True)
+    finally:
+        net.raw2outputs = orig
+        torch.set_default_dtype(torch.float32)
+        rc.to(torch.float32)
+        torch.set_num_threads(8)
+    return runs
+
+
+def spread():
+    """H12 evidence: how far the REFERENCE's own disp moves on the fixture's rays
+    when only its summation order (thread count) or its precision (float64) changes.  Writes
+    tests/golden/h12_spread_c5.npz: per ray and run disp / acc / rgb, and for the near-empty rays the
+    fine pass's per-sample raw sigma, alpha, weights and z of every run."""
+    import make_golden as mg
+    z = np.load(os.path.join(HERE, "h12_nearempty_c5.npz"))
+    sc, ck, cfg, idx, cyls = frame()
+    sel, ne = z["sel"], z["near_empty"]
+    mods = mg.import_reference()
+    gcfg = dict(H=H, NJ=NJ, S=64, I=128, D=8, W=256, tau=TAU, kind="rays", seed=SEED)
+    with tempfile.TemporaryDirectory() as tmp:
+        args, render_kwargs, ck_ref = mg.build_reference(mods, gcfg, tmp)
+        assert syn.checkpoint_sha256(ck_ref) == syn.checkpoint_sha256(ck)
+        (o, d), vidx, rcyls, _ = mg.rays_for(mods, sc)
+        sc["cyls"] = rcyls
+        runs = _reference_runs(mods, render_kwargs, sc, o[sel], d[sel])
+    assert np.array_equal(runs["t8"]["disp_map"].astype(np.float32), z["out_disp_map"]), "t8 run != the fixture"
+    data = {"sel": sel, "near_empty": ne}
+    for name, r in runs.items():
+        for k in ("rgb_map", "disp_map", "acc_map"):
+            data[f"{name}_{k}"] = r[k].astype(np.float64 if name == "f64" else np.float32)
+        for k in ("sigma", "alpha", "weights", "z"):
+            data[f"{name}_{k}"] = r[k][ne].astype(np.float64 if name == "f64" else np.float32)
+    path = os.path.join(HERE, "h12_spread_c5.npz")
+    np.savez_compressed(path, meta=np.array(repr(dict(seed=SEED, tau=TAU, H=H, runs="t8: 8 threads (= the fixture), "
+                                                              "t1: 1 thread, f64: float64 networks/inputs"))), **data)
+    d81 = np.abs(data["t8_disp_map"].astype(np.float64) - data["t1_disp_map"])
+    d8f = np.abs(data["t8_disp_map"].astype(np.float64) - data["f64_disp_map"])
+    print(f"wrote {path}")
+    print(f"near-empty ({int(ne.sum())}): |t8 - t1| disp max {d81[ne].max():.3e} ({int((d81[ne] > 1e-4).sum())} > 1e-4); "
+          f"|t8 - f64| disp max {d8f[ne].max():.3e} ({int((d8f[ne] > 1e-4).sum())} > 1e-4)")
+    print(f"ordinary ({int((~ne).sum())}): |t8 - t1| disp max {d81[~ne].max():.3e}; |t8 - f64| disp max {d8f[~ne].max():.3e}")
+
+
 if __name__ == "__main__":
-    {"scan": scan, "fixture": fixture}[sys.argv[1]]()
+    {"scan": scan, "fixture": fixture, "spread": spread}[sys.argv[1]]()

@@ -70,6 +70,15 @@ def _worker(rank, world, port, q):
             render_nf(rb[r0:r1], nf[0][r0 - c0:r1 - c0], nf[1][r0 - c0:r1 - c0]))
         for k in out:
             assert torch.equal(outb[k], out[k]) and torch.equal(sgb[k], out[k]), k
+        # tiles dealt round-robin (what bench.py runs): near / far over the whole list, this rank's tiles
+        outt = D.render_rays_sharded(render_nf, rb, chunk=4096, near_far_fn=near_far_fn, split="tiles", tile=1000)
+        rows = [D.tile_rows(rb.shape[0], world, r, 1000) for r in range(world)]
+        nfa = near_far_fn(rb)
+        mine_r = rows[rank]
+        sgt = D.ShardGather(rb.shape[0], 4096, world, torch.device("cpu"), rank_rows=rows)(
+            render_nf(rb[mine_r], nfa[0][mine_r], nfa[1][mine_r]))
+        for k in out:
+            assert torch.equal(outt[k], out[k]) and torch.equal(sgt[k], out[k]), k
         frames = torch.arange(5 * 4 * 4 * 3, dtype=torch.float32).reshape(5, 4, 4, 3)
         mine = frames[D.frame_ids(5, rank, world)]
         full = D.gather_frames(mine, 5)
@@ -97,6 +106,12 @@ def test_chunk_ranges_are_whole_chunks_and_cover():
             for a, b in rs:
                 c0, c1 = D.chunk_cover(a, b, 4096, n)
                 assert c0 % 4096 == 0 and (c1 % 4096 == 0 or c1 == n) and c0 <= a and b <= c1
+            for tile in (1, 256, 1000):
+                rows = [D.tile_rows(n, w, r, tile) for r in range(w)]
+                allr = torch.cat(rows)
+                assert allr.shape[0] == n and torch.equal(torch.sort(allr).values, torch.arange(n))
+                sizes = [int(r.shape[0]) for r in rows]
+                assert max(sizes) - min(sizes) <= tile
 
 
 @pytest.mark.timeout(600)

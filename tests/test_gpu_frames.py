@@ -60,10 +60,12 @@ def _render(rc, rb, sc, cyls):
 
 def _oracle_check(cfg, ck, sc, cyls, rb, out, n_sample):
     """n_sample evenly spaced rays of the frame against the oracle at 1e-4, every output of every ray
-    except the disparity of near-empty rays (0 < acc < 2^-20, hazard H12): their count and disp error
-    are reported and bounded (5e-4, at most 0.1 % of the sample; test_near_empty_rays_against_the_reference
-    pins all 169 of config 5's against the reference itself)."""
+    except the disparity of near-empty rays (0 < acc < 2^-20, hazard H12): those are held to 1e-4 plus
+    the reference's own measured spread on such rays (oracle.h12_spread: the reference's float32 disp vs
+    its float64 disp on config 5's 169 near-empty rays, 1.92e-4), and reported;
+    test_near_empty_rays_against_the_reference pins all 169 against the reference itself, ray by ray."""
     import oracle
+    ne_tol = TOL + oracle.h12_spread()["float64"]
     om = oracle.OracleModel(cfg, ck)
     rb_h = rb.cpu().numpy()
     near, far, _, _ = om.near_far(rb_h, cyls[0:1], chunk=4096)
@@ -80,11 +82,11 @@ def _oracle_check(cfg, ck, sc, cyls, rb, out, n_sample):
         if empty.any():
             ne = float(d[empty].max())
             report[k] = (int(empty.sum()), ne)
-            assert ne <= 5e-4 and empty.sum() <= max(1, n_sample // 1000), (k, int(empty.sum()), ne)
+            assert ne <= ne_tol, (k, int(empty.sum()), ne, ne_tol)
     print(f"near-empty rays (count, max disp error): {report}")
 
 
-@pytest.mark.parametrize("nj,precision", [(24, "bf16x6"), (24, "fp16x3"), (24, "fp32"), (65, "fp16x3")])
+@pytest.mark.parametrize("nj,precision", [(24, "bf16x6"), (24, "fp16x3"), (24, "fp32"), (65, "fp16x3"), (65, "bf16x6")])
 def test_full_frame_matches_oracle_on_8192_rays(nj, precision):
     seed = 13 if nj == 24 else 14
     sc, ck, cyls, rb = _frame(512, nj, seed, 79.6 if nj == 24 else 20.0)
@@ -166,11 +168,14 @@ def test_near_empty_rays_against_the_reference(precision):
     """Hazard H12 against the REFERENCE (tests/golden/h12_nearempty_c5.npz: config 5's near-empty rays,
     0 < acc < 2^-20, and 64 ordinary rays, rendered by core.raycasters.render_rays with the frame's
     own near / far): every output of the ordinary rays and rgb / acc / the coarse outputs of the
-    near-empty rays within 1e-4.  Their disp is a ratio of a few 2^-24 alpha quanta: with alpha's exp
-    rounded to nearest (anerf_device.hpp alpha_of; OCML's expf moved a quantum on 2 of these rays, disp
-    off by 0.195) the GPU matches the reference on all 169 near-empty rays at 1e-4 in fp16x3 and on 168
-    in fp32 / bf16x6 -- one ray takes one more quantum (raw sigma ulps at the rounding threshold) and is
-    off by 1.7e-4.  Reported (count above 1e-4, max), bounded: at most 2 rays, 5e-4."""
+    near-empty rays within 1e-4.  Their disp = (acc + 1e-10) / depth is a ratio of a few 2^-24 alpha
+    quanta.  tests/golden/h12_spread_c5.npz holds the reference's own spread on these rays:
+    its disp does not move with the thread count, but its float64 run differs from its float32 one by
+    up to 1.92e-4 (2 rays above 1e-4) -- every quantum is rounded from a sigma * delta that the
+    float32 MLP only knows to ~1e-6 relative, and torch's CPU exp rounds exp(-x) for tiny x up from
+    k + 29/64 quanta, where alpha_of rounds to nearest.  Asserted per ray: the GPU is within 1e-4 of the
+    reference's float64 value widened by the reference's own distance from it,
+    |gpu - f64| <= 1e-4 + |ref - f64|; and within 1e-4 + the largest such spread of the reference."""
     import ast
     z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "h12_nearempty_c5.npz"))
     meta = ast.literal_eval(str(z["meta"]))
@@ -192,9 +197,17 @@ def test_near_empty_rays_against_the_reference(precision):
     for k in ("rgb_map", "acc_map", "rgb0", "disp0", "acc0"):
         d = np.abs(out[k].cpu().numpy().astype(np.float64) - z["out_" + k]).reshape(n, -1).max(-1)
         assert d.max() <= TOL, (k, float(d.max()))
-    dd = np.abs(out["disp_map"].cpu().numpy().astype(np.float64) - z["out_disp_map"])
+    got = out["disp_map"].cpu().numpy().astype(np.float64)
+    dd = np.abs(got - z["out_disp_map"])
     assert dd[~ne].max() <= TOL, float(dd[~ne].max())
-    print(f"{precision} H12: {int(ne.sum())} near-empty rays, |gpu - reference| disp max {dd[ne].max():.3e}, "
-          f"{int((dd[ne] > TOL).sum())} above 1e-4")
-    assert dd[ne].max() <= 5e-4 and int((dd[ne] > TOL).sum()) <= 2
+    sp = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "h12_spread_c5.npz"))
+    assert np.array_equal(sp["sel"], z["sel"]) and np.array_equal(sp["t8_disp_map"], z["out_disp_map"])
+    f64 = sp["f64_disp_map"]
+    own = np.abs(z["out_disp_map"].astype(np.float64) - f64)  # the reference's distance from its float64 value
+    margin = np.abs(got - f64) - (TOL + own)
+    print(f"{precision} H12: {int(ne.sum())} near-empty rays, |gpu - reference| disp max {dd[ne].max():.3e} "
+          f"({int((dd[ne] > TOL).sum())} above 1e-4); |gpu - f64| - |ref - f64| max {(margin[ne] + TOL).max():.3e}; "
+          f"reference spread max {own[ne].max():.3e}")
+    assert margin[ne].max() <= 0.0, (int(np.argmax(np.where(ne, margin, -1))), float(margin[ne].max()))
+    assert dd[ne].max() <= TOL + own[ne].max()
 

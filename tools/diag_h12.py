@@ -39,9 +39,23 @@ def main():
         np.savez_compressed(os.path.join(REPO, "gpurun_out", f"h12_diag_{prec}.npz"), **save)
         dd = np.abs(save["disp_map"].astype(np.float64) - z["out_disp_map"])
         worst = np.argsort(-dd)[:6]
+        sp = np.load(os.path.join(REPO, "tests", "golden", "h12_spread_c5.npz"))
+        nei = np.flatnonzero(sp["near_empty"])
         for i in worst:
-            print(f"{prec} ray {int(z['sel'][i])}: disp gpu {save['disp_map'][i]:.6f} ref {z['out_disp_map'][i]:.6f} "
-                  f"oracle {z['oracle_disp_map'][i]:.6f}; acc gpu {save['acc_map'][i]:.3e} ref {z['out_acc_map'][i]:.3e}")
+            print(f"{prec} ray {int(z['sel'][i])} (#{i}): disp gpu {save['disp_map'][i]:.6f} ref {z['out_disp_map'][i]:.6f} "
+                  f"ref-f64 {sp['f64_disp_map'][i]:.6f} oracle {z['oracle_disp_map'][i]:.6f}; acc gpu {save['acc_map'][i]:.3e} "
+                  f"ref {z['out_acc_map'][i]:.3e} ref-f64 {sp['f64_acc_map'][i]:.3e}")
+            if i in nei:  # per-sample: alpha in 2^-24 quanta, raw sigma, z (GPU fine pass vs the reference's)
+                k = int(np.flatnonzero(nei == i)[0])
+                ga = save["alpha"][i].astype(np.float64)
+                gs = save["dbg_raw_fine"][i][..., 3] if "dbg_raw_fine" in save else None
+                gz = save["dbg_z_fine"][i] if "dbg_z_fine" in save else None
+                live = np.flatnonzero((ga > 0) | (sp["t8_alpha"][k] > 0) | (sp["f64_alpha"][k] > 2.0 ** -26))
+                for s in live[:12]:
+                    print(f"    sample {s}: alpha quanta gpu {ga[s] * 2**24:.3f} ref {sp['t8_alpha'][k][s] * 2**24:.3f} "
+                          f"f64 {sp['f64_alpha'][k][s] * 2**24:.3f}; sigma gpu {gs[s] if gs is not None else float('nan'):.9g} "
+                          f"ref {sp['t8_sigma'][k][s]:.9g} f64 {sp['f64_sigma'][k][s]:.9g}; z gpu "
+                          f"{gz[s] if gz is not None else float('nan'):.9g} ref {sp['t8_z'][k][s]:.9g}")
 
 
 if __name__ == "__main__":

@@ -19,7 +19,8 @@ NAMES = {0: "prologue", 1: "view factor G (G + bias column)", 7: "  view factor:
          5: "composite fine", 6: "barrier wait after MLP", 8: "  L0 u-part", 9: "  L0 v-part",
          10: "  bias/relu boundaries", 11: "  hidden h-parts", 12: "  skip u+v", 13: "  heads (alpha/feat/view/rgb)",
          14: "  L0 u-part prologue", 15: "  v-part prologues (L0 + skip)",
-         16: "  heads: view layer (+ alpha)", 17: "  heads: view-direction part", 13: "  heads: rgb head + stores"}
+         16: "  heads: view layer (+ alpha)", 17: "  heads: view-direction part", 13: "  heads: rgb head + stores",
+         18: "  barrier wait before hidden layers (bf16x6)"}
 
 
 def main():
