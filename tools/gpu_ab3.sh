@@ -5,7 +5,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 for r in 1 2 3; do
   for l in ${LIBS:-base}; do
-    v=$(ANERF_LIB_PATH=$PWD/tools/ab/lib_$l.so timeout -k 10 300 python bench.py --no-cpu --no-tau20 --no-train --also "" --precision ${PREC:-bf16x6} 2>/dev/null | python -c "import json,sys;d=json.load(sys.stdin);print(d['value'], d['roofline']['kernel_ms'])") || exit 1
+    v=$(ANERF_LIB_PATH=$PWD/tools/ab/lib_$l.so timeout -k 10 300 python bench.py --no-cpu --no-tau20 --no-train --no-balance --other-configs "" --also "" --precision ${PREC:-bf16x6} 2>/dev/null | python -c "import json,sys;d=json.load(sys.stdin);print(d['value'], d['roofline']['kernel_ms'])") || exit 1
     echo "$l $v"
   done
 done

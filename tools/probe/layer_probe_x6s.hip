@@ -219,7 +219,7 @@ __device__ __forceinline__ float hash01(unsigned x) {
 
 template <bool S, bool SYNC = false>
 __global__ __launch_bounds__(256, 1) void layer_speed(const float* w, int nl, int foot, float* out,
-                                                      unsigned long long* cyc) {
+                                                      unsigned long long* cyc, int copies = 1) {
     __shared__ __attribute__((aligned(16))) float bias[256];
     const int lane = threadIdx.x & 63;
     for (int i = threadIdx.x; i < 256; i += 256) bias[i] = 0.05f * hash01(i * 7 + 3) - 0.02f;
@@ -232,8 +232,10 @@ __global__ __launch_bounds__(256, 1) void layer_speed(const float* w, int nl, in
     bool pre = false;
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
     for (int L = 0; L < nl; ++L) {
-        const float* wl = w + (size_t)(L % foot) * LAYER_FLOATS;
-        const float* wn = w + (size_t)((L + 1) % foot) * LAYER_FLOATS;
+        // (copies > 1: wave w streams its own copy of the weights, so the CU's four waves share no L1 line)
+        const int cw = ((int)threadIdx.x >> 6) % copies;
+        const float* wl = w + (size_t)(L % foot + cw * foot) * LAYER_FLOATS;
+        const float* wn = w + (size_t)((L + 1) % foot + cw * foot) * LAYER_FLOATS;
         if (SYNC) __builtin_amdgcn_s_barrier();
         if (S)
             mlp_layer_x6s<8, 8, true>(acc, acc, h, bias, wl, lane, ring, pre, wn);
@@ -303,6 +305,8 @@ static int g_nl, g_foot, g_iters;
 static void L6() { hipLaunchKernelGGL(layer_speed<false>, dim3(256), dim3(256), 0, 0, g_w6, g_nl, g_foot, g_out, g_cyc); }
 static void L6s() { hipLaunchKernelGGL(layer_speed<true>, dim3(256), dim3(256), 0, 0, g_w6s, g_nl, g_foot, g_out, g_cyc); }
 static void L6sync() { hipLaunchKernelGGL((layer_speed<false, true>), dim3(256), dim3(256), 0, 0, g_w6, g_nl, g_foot, g_out, g_cyc); }
+static int g_copies = 1;
+static void L6c() { hipLaunchKernelGGL((layer_speed<false, true>), dim3(256), dim3(256), 0, 0, g_w6, g_nl, g_foot, g_out, g_cyc, g_copies); }
 static void B32() { hipLaunchKernelGGL(bare<false>, dim3(256), dim3(256), 0, 0, g_iters, g_out, g_cyc); }
 static void B16() { hipLaunchKernelGGL(bare<true>, dim3(256), dim3(256), 0, 0, g_iters, g_out, g_cyc); }
 
@@ -389,5 +393,20 @@ int main() {
             }
         }
     }
+    // L1 sharing: the four waves of a CU on one weight stream (copies 1) or on four (copies 4), in step
+    for (int rnd = 0; rnd < 2; ++rnd)
+        for (int cp : {1, 4}) {
+            g_foot = 2;
+            g_copies = cp;
+            g_nl = 440;
+            double cyc;
+            const int reps = 10;
+            const float ms = time_launches(L6c, g_cyc, &cyc, reps);
+            const double flop = 256.0 * 4 * reps * g_nl * 768.0 * 32768.0;
+            const double cyc_layer = cyc / (256.0 * 4 * reps) / g_nl;
+            printf("layer x6 sync, 2 layers x %d copies (%s): %.1f TFLOP/s, %.0f cyc/layer (%.1f %%), clock %.2f GHz\n", cp,
+                   cp == 1 ? "L1-shared" : "no L1 sharing", flop / (ms * 1e-3) / 1e12, cyc_layer, 100.0 * 24576 / cyc_layer,
+                   cyc / (256.0 * 4 * reps) / (ms * 1e-3 / reps) / 1e9);
+        }
     return 0;
 }
