@@ -73,8 +73,10 @@ class RenderConfig:
             raise NotImplementedError(f"netwidth={self.netwidth}: multiples of 64 up to 256 are supported")
         if self.netdepth < 2 or self.netdepth > 16:
             raise NotImplementedError(f"netdepth={self.netdepth} outside [2, 16]")
-        if self.multires not in (7, 10) or self.multires_views not in (0, 4):
-            raise NotImplementedError("kernel instances exist for multires in {7, 10} and multires_views in {0, 4}")
+        if not 1 <= self.multires <= 10 or not 0 <= self.multires_views <= 4:
+            # (kernel instances for multires 7 / 10 and multires_views 0 / 4; smaller counts run on them with
+            # the missing frequencies' weights zero, anerf_pack.hpp layout_multires)
+            raise NotImplementedError("multires must be in [1, 10] and multires_views in [0, 4]")
         if self.density_type not in ("relu", "softplus"):
             raise NotImplementedError(f"density activation {self.density_type} is undefined")
         if self.opt_framecode and self.n_framecodes <= 0:

@@ -48,6 +48,9 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int BM = 128, BN = 128, NTHR = 256;
+#ifndef ANERF_GEMM_IL
+#define ANERF_GEMM_IL 1
+#endif
 constexpr int MAXSEG = 3;
 
 struct SegD {
@@ -279,6 +282,21 @@ __global__ __launch_bounds__(NTHR, 2) void mlp_nt_kernel(NTArgs g) {
             acc[i] = mfma(a[0][i], b[0], c);
         }
     };
+    // step kk = 1 of a buffer with the staging of the next step's A tile interleaved into its MFMAs
+    // (one MFMA, then up to VS VALU and one LDS write): the split and the ds_writes run in the MFMA
+    // gaps instead of after the last MFMA (ANERF_GEMM_IL; 0 = the two one after the other)
+    auto step_stage = [&](int buf, const BF& f, int sbuf, const RA& R) {
+        step(buf, 1, f);
+        stage_a(sbuf, R);
+        constexpr int NM = 4 * (NPL == 3 ? 6 : 3), VS = NPL == 3 ? 3 : 4;
+        __builtin_amdgcn_sched_group_barrier(0x100, 4 * NPL, 0);  // the fragment reads first
+#pragma unroll
+        for (int i = 0; i < NM; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, VS, 0);
+            __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+        }
+    };
     RA R0, R1;
     BF f0, f1;
     fetch_a(0, R0);
@@ -298,9 +316,13 @@ __global__ __launch_bounds__(NTHR, 2) void mlp_nt_kernel(NTArgs g) {
         __builtin_amdgcn_sched_barrier(0);
         fetch_b(2 * st + 2, f0);
         __builtin_amdgcn_sched_barrier(0);
-        step(0, 1, f1);
-        __builtin_amdgcn_sched_barrier(0);
-        if (st + 1 < nst) stage_a(1, R1);
+        if (ANERF_GEMM_IL && st + 1 < nst) {
+            step_stage(0, f1, 1, R1);
+        } else {
+            step(0, 1, f1);
+            __builtin_amdgcn_sched_barrier(0);
+            if (st + 1 < nst) stage_a(1, R1);
+        }
         __syncthreads();
         if (st + 1 >= nst) break;
         fetch_a(st + 3, R1);
@@ -311,9 +333,13 @@ __global__ __launch_bounds__(NTHR, 2) void mlp_nt_kernel(NTArgs g) {
         __builtin_amdgcn_sched_barrier(0);
         fetch_b(2 * st + 4, f0);
         __builtin_amdgcn_sched_barrier(0);
-        step(1, 1, f1);
-        __builtin_amdgcn_sched_barrier(0);
-        if (st + 2 < nst) stage_a(0, R0);
+        if (ANERF_GEMM_IL && st + 2 < nst) {
+            step_stage(1, f1, 0, R0);
+        } else {
+            step(1, 1, f1);
+            __builtin_amdgcn_sched_barrier(0);
+            if (st + 2 < nst) stage_a(0, R0);
+        }
         __syncthreads();
     }
     // epilogue through LDS: the waves write their accumulators (lane = column (lane & 31), registers
@@ -793,17 +819,16 @@ inline int rup(long long x, int a) { return (int)((x + a - 1) / a * a); }
 int planes_of(int precision) { return precision == ANERF_MLP_BF16X6 ? 3 : (precision == ANERF_MLP_BF16X3 ? 2 : 0); }
 
 // the dynamic LDS (up to 67 KB) is above the default limit: raised once per kernel instance
+// (set on every call: the attribute belongs to the current device, and a cached failure would stick)
 template <int NPL, int NSEG>
 hipError_t nt_attr() {
-    static const hipError_t e = hipFuncSetAttribute((const void*)mlp_nt_kernel<NPL, NSEG>,
-                                                    hipFuncAttributeMaxDynamicSharedMemorySize, NTGeo<NPL>::LDS_BYTES);
-    return e;
+    return hipFuncSetAttribute((const void*)mlp_nt_kernel<NPL, NSEG>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               NTGeo<NPL>::LDS_BYTES);
 }
 template <int NPL, int NSEG>
 hipError_t tn_attr() {
-    static const hipError_t e = hipFuncSetAttribute((const void*)mlp_tn_kernel<NPL, NSEG>,
-                                                    hipFuncAttributeMaxDynamicSharedMemorySize, TNGeo<NPL, NSEG>::LDS_BYTES);
-    return e;
+    return hipFuncSetAttribute((const void*)mlp_tn_kernel<NPL, NSEG>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               TNGeo<NPL, NSEG>::LDS_BYTES);
 }
 
 // Operand segments: every segment but the last a multiple of 4 columns, all 16-byte aligned with

@@ -3,6 +3,9 @@
 #pragma once
 
 // ======================================================================= fused render kernel
+#ifndef ANERF_BLOCK_SORT
+#define ANERF_BLOCK_SORT 1  // (0: blocks in ray order; tools/build_ab.sh experiments)
+#endif
 template <int W, int MR, int PREC>
 __global__ __launch_bounds__(256, 1) void render_kernel(ModelDev M, RenderArgs A, LdsPlan P) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -66,18 +69,49 @@ __global__ __launch_bounds__(256, 1) void render_kernel(ModelDev M, RenderArgs A
             else compute_view_factor<WH, 4>(M, net, lds, P, nr, tid, st);
         }
         STAMP(st, 1);
-        // ---- MLP over 32-sample blocks, round-robin over the 4 waves
+        // ---- MLP over 32-sample blocks, four at a time (one per wave)
         const int nm = only_new ? I : n;
-        const int nb = (nm + 31) / 32;
+        const int nb = (nm + 31) / 32, nbt = nr * nb;
+        auto block_z = [&](int r) {
+            return only_new ? lds + P.scr + P.scr_stride * r + 6 * P.z_stride : lds + zoff + P.z_stride * r;
+        };
+        int* const bcnt = reinterpret_cast<int*>(lds + P.bord);
+        int* const bord = bcnt + P.bord_n;
+        if constexpr (PREC == 2 && ANERF_BLOCK_SORT) {
+            // bf16x6: the four waves meet at a workgroup barrier before every hidden layer (L1 sharing of
+            // the weight stream), where a wave whose block has fewer live joints waits for the others
+            // (5.8 % of the wave-cycles, profiles/r04c_stamps_bf16x6.txt).  The blocks of the workgroup
+            // run in ascending order of their live-joint counts, so the four blocks of an iteration have
+            // about equal windowed work.  (Outputs are unchanged: a block's arithmetic does not depend on
+            // the wave that runs it.)
+            for (int b = wave; b < nbt; b += 4) {
+                const int r = b / nb;
+                const int c = block_live_count(M, lds + P.ray + 16 * r, lds + P.sk + P.sk_stride * r, lds + P.cut,
+                                               block_z(r), nm, (b % nb) * 32, lane);
+                if (lane == 0) bcnt[b] = c;
+            }
+            __syncthreads();
+            for (int i = tid; i < nbt; i += blockDim.x) {
+                const int ci = bcnt[i];
+                int rank = 0;
+                for (int j = 0; j < nbt; ++j) {
+                    const int cj = bcnt[j];
+                    rank += (cj < ci) | ((cj == ci) & (j < i));
+                }
+                bord[rank] = i;
+            }
+            __syncthreads();
+        }
         // (the same trip count on every wave: bf16x6's mlp_trunk has a workgroup barrier per hidden
         // layer; a wave past the last block redoes that block without storing or counting it)
-        for (int it = 0; it < (nr * nb + 3) / 4; ++it) {
-            const bool own = it * 4 + wave < nr * nb;
+        for (int it = 0; it < (nbt + 3) / 4; ++it) {
+            const bool own = it * 4 + wave < nbt;
             if constexpr (PREC != 2)  // (no workgroup barrier inside: a wave without a block is done)
                 if (!own) break;
-            const int b = own ? it * 4 + wave : nr * nb - 1;
+            const int bi = own ? it * 4 + wave : nbt - 1;
+            const int b = (PREC == 2 && ANERF_BLOCK_SORT) ? bord[bi] : bi;
             const int r = b / nb, s0 = (b % nb) * 32;
-            const float* zr = only_new ? lds + P.scr + P.scr_stride * r + 6 * P.z_stride : lds + zoff + P.z_stride * r;
+            const float* zr = block_z(r);
             float* rawr = lds + P.raw + P.raw_stride * r + (only_new ? 4 * S : 0);
             mlp_block<W, MR, PREC>(M, net, lds + P.ray + 16 * r, lds + P.sk + P.sk_stride * r, lds + P.cut,
                              zr, nm, s0, lds + P.g + P.g_stride * r, rawr, lane, own ? A.mfma_count : nullptr,

@@ -915,32 +915,82 @@ __device__ __forceinline__ void u_features_lds(const ModelDev& M, const float* _
                                                const float* __restrict__ cut, float px, float py, float pz, int lane,
                                                JointMask* mask, float* __restrict__ uf, float* __restrict__ wvo) {
     const int hh = lane >> 5, njh2 = M.njh2, nj = M.nj, j0 = hh * njh2;
+    // (njh2 <= 64: joint p of half 0 is mask bit p, joint p + njh2 of half 1 bit p + njh2 < 128.  The
+    // bits are set branch-free with scalar selects; two joints per iteration for instruction-level
+    // parallelism in the dependent transcendental chains of u_joint)
     uint64_t m0 = 0, m1 = 0;
-    JRow r = load_row(sk, cut, j0, nj, M.bone_cut != 0);
-    for (int p = 0; p < njh2; ++p) {
-        const JRow rn = load_row(sk, cut, j0 + min(p + 1, njh2 - 1), nj, M.bone_cut != 0);
-        float u0, u1, u2, wv;
-        bool live;
-        u_joint<WV>(M, r, j0 + p < nj, px, py, pz, u0, u1, u2, live, wv);
+    auto set_bits = [&](int p, uint64_t b) {
+        const uint64_t lo = (b & 0xffffffffull) ? 1ull : 0ull, hi = (b >> 32) ? 1ull : 0ull;
+        const int jb = p + njh2;
+        m0 |= lo << p;
+        m0 |= (jb < 64 ? hi : 0ull) << (jb & 63);
+        m1 |= (jb >= 64 ? hi : 0ull) << (jb & 63);
+    };
+    JRow ra = load_row(sk, cut, j0, nj, M.bone_cut != 0);
+    JRow rb = load_row(sk, cut, j0 + min(1, njh2 - 1), nj, M.bone_cut != 0);
+    for (int p = 0; p < njh2; p += 2) {
+        const bool two = p + 1 < njh2;  // (uniform)
+        const JRow na = load_row(sk, cut, j0 + min(p + 2, njh2 - 1), nj, M.bone_cut != 0);
+        const JRow nb = load_row(sk, cut, j0 + min(p + 3, njh2 - 1), nj, M.bone_cut != 0);
+        float u0, u1, u2, wv, v0, v1, v2, wv2;
+        bool live, live2;
+        u_joint<WV>(M, ra, j0 + p < nj, px, py, pz, u0, u1, u2, live, wv);
+        u_joint<WV>(M, rb, two && (j0 + p + 1 < nj), px, py, pz, v0, v1, v2, live2, wv2);
         uf[(3 * p + 0) * 64 + lane] = u0;
         uf[(3 * p + 1) * 64 + lane] = u1;
         uf[(3 * p + 2) * 64 + lane] = u2;
         if constexpr (WV) wvo[p * 64 + lane] = wv;
-        const uint64_t b = __ballot(live);
-        const int jb = p + njh2;
-        if (b & 0xffffffffull) {
-            if (p < 64) m0 |= 1ull << p; else m1 |= 1ull << (p - 64);
+        set_bits(p, __ballot(live));
+        if (two) {
+            uf[(3 * p + 3) * 64 + lane] = v0;
+            uf[(3 * p + 4) * 64 + lane] = v1;
+            uf[(3 * p + 5) * 64 + lane] = v2;
+            if constexpr (WV) wvo[(p + 1) * 64 + lane] = wv2;
+            set_bits(p + 1, __ballot(live2));
         }
-        if (b >> 32) {
-            if (jb < 64) m0 |= 1ull << jb; else m1 |= 1ull << (jb - 64);
-        }
-        r = rn;
+        ra = na;
+        rb = nb;
     }
     if (mask) {
         mask->m0 = m0;
         mask->m1 = m1;
     }
 }
+
+// Live-joint count of one 32-sample block: the union over its samples of the cutoff-window test that
+// u_features_lds ballots (lane half h: joints h NJH2 + p), without the features.  The render kernel
+// orders a workgroup's blocks by it (bf16x6): the four waves pass a workgroup barrier at every hidden
+// layer, so a wave whose block has fewer live joints (fewer windowed MFMAs) waits there for the others.
+__device__ __forceinline__ int block_live_count(const ModelDev& M, const float* __restrict__ ray,
+                                                const float* __restrict__ sk, const float* __restrict__ cut,
+                                                const float* __restrict__ z, int n, int s0, int lane) {
+    if (!M.sparse) return M.nj;
+    int s = s0 + (lane & 31);
+    if (s >= n) s = n - 1;
+    const float zs = z[s];
+    const float px = ray[0] + ray[3] * zs, py = ray[1] + ray[4] * zs, pz = ray[2] + ray[5] * zs;
+    const int hh = lane >> 5, njh2 = M.njh2, nj = M.nj, j0 = hh * njh2;
+    int cnt = 0;
+    for (int p0 = 0; p0 < njh2; p0 += 4) {  // (four joints' rows loaded together: one LDS latency per four)
+        JRow r[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) r[k] = load_row(sk, cut, j0 + min(p0 + k, njh2 - 1), nj, false);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float qx = fmaf(r[k].a[3], 1.0f, fmaf(r[k].a[2], pz, fmaf(r[k].a[1], py, r[k].a[0] * px)));
+            const float qy = fmaf(r[k].b[3], 1.0f, fmaf(r[k].b[2], pz, fmaf(r[k].b[1], py, r[k].b[0] * px)));
+            const float qz = fmaf(r[k].c[3], 1.0f, fmaf(r[k].c[2], pz, fmaf(r[k].c[1], py, r[k].c[0] * px)));
+            const float d2 = fmaf(qz, qz, fmaf(qy, qy, qx * qx));
+            const uint64_t b = __ballot((p0 + k < njh2) & (j0 + p0 + k < nj) & !(d2 >= r[k].thr2));
+            cnt += ((b & 0xffffffffull) != 0) + ((b >> 32) != 0);
+        }
+    }
+    return cnt;
+}
+
+#ifndef ANERF_X6_BARRIERS
+#define ANERF_X6_BARRIERS 3
+#endif
 
 // One x part's bone-direction contraction from the LDS features as bf16x6: k16-step s takes
 // features 8 s .. 8 s + 7 of each lane half (zero past 3 NJH2), split by truncation (split3_pair);
@@ -1293,9 +1343,14 @@ __device__ __forceinline__ bool mlp_trunk(const ModelDev& M, const NetDev& net, 
         // CU per group otherwise, and the waves drift apart over the windowed parts' live joints.
         // +2.1 % (A/B, profiles/r03_ab_experiments.txt); the calling block loop must have the same
         // trip count on every wave (SYNC: the render and density kernels' block loops).
-        if constexpr (SYNC && P == 2) {
-            __builtin_amdgcn_s_barrier();
-            STAMP(st, 18);  // (stamps build: the wait at this barrier)
+        // (ANERF_X6_BARRIERS, experiments: 3 before every hidden layer, 2 before layer 1 and the layer
+        // after the skip layer, 1 before layer 1 only, 0 none)
+        constexpr int XB = ANERF_X6_BARRIERS;
+        if constexpr (SYNC && P == 2 && XB > 0) {
+            if (XB == 3 || L == 1 || (XB == 2 && L == M.skip + 2)) {
+                __builtin_amdgcn_s_barrier();
+                STAMP(st, 18);  // (stamps build: the wait at this barrier)
+            }
         }
         if constexpr (P == 3) {
             // the next h3 phase (the next hidden layer or the view layer) is prefetched; not across the

@@ -281,15 +281,22 @@ std::vector<float> pack_upart_x6(const float* Wt, int n_out, int ld, int nj, int
     });
 }
 
+// The windowed parts are laid out for the kernel instance's frequency count mrl (layout_multires:
+// 7 or 10) and filled from the model's mr <= mrl: the k-slots of frequencies mr .. mrl - 1 carry
+// zero weights (their features are computed and add exact zeros), so every multires up to 10 runs on
+// the two instances.
+int layout_multires(int mr) { return mr <= 7 ? 7 : 10; }
+int layout_multires_views(int mrv) { return mrv == 0 ? 0 : 4; }
+
 // windowed part, per joint j: k-step t < mr -> (sin_t, cos_t) = columns ((1+2t)NJ + j, (2+2t)NJ + j);
-// t == mr -> (dist, pad); padded to an even count.  Layout [joint][group][RB][64][2].
-std::vector<float> pack_vpart(const float* Wt, int n_out, int ld, int nj, int mr) {
-    const int kb = ((mr + 1) + 1) & ~1;
+// mr <= t < mrl -> zero; t == mrl -> (dist, pad); padded to an even count.  Layout [joint][group][RB][64][2].
+std::vector<float> pack_vpart(const float* Wt, int n_out, int ld, int nj, int mr, int mrl) {
+    const int kb = ((mrl + 1) + 1) & ~1;
     std::vector<float> out;
     for (int j = 0; j < nj; ++j) {
         std::vector<float> pj = pack_kmajor(Wt, n_out, ld, kb, [&](int t, int h) {
             if (t < mr) return (1 + 2 * t + h) * nj + j;
-            if (t == mr && h == 0) return j;
+            if (t == mrl && h == 0) return j;
             return -1;
         });
         out.insert(out.end(), pj.begin(), pj.end());
@@ -299,17 +306,17 @@ std::vector<float> pack_vpart(const float* Wt, int n_out, int ld, int nj, int mr
 
 // windowed part as bf16x6 groups for v_part_x6: joint j, k16-step s, lane half h, element i ->
 // feature q = 8 s + i of that half: q < mr -> sin_q (h = 0) / cos_q (h = 1) = column
-// (1 + 2q + h) nj + j, q == mr and h == 0 -> the distance input (column j), else zero; groups
+// (1 + 2q + h) nj + j, q == mrl and h == 0 -> the distance input (column j), else zero; groups
 // (j, s, rb) of 12 floats = fragments w0, w1, w2 (as pack_layer_x6).
-std::vector<float> pack_vpart_x6(const float* Wt, int n_out, int ld, int nj, int mr) {
-    const int RB = n_out / 32, ks = (mr + 1 + 7) / 8;
+std::vector<float> pack_vpart_x6(const float* Wt, int n_out, int ld, int nj, int mr, int mrl) {
+    const int RB = n_out / 32, ks = (mrl + 1 + 7) / 8;
     return pack_groups(nj * ks * RB, 12, [&](int g, int sl, int l) {
         const int j = g / (ks * RB), s = (g / RB) % ks, rb = g % RB, f = sl >> 2, e = sl & 3;
         const int h = l >> 5, row = 32 * rb + (l & 31);
         uint32_t bits = 0;
         for (int jj = 0; jj < 2; ++jj) {
             const int q = 8 * s + 2 * e + jj;
-            const int col = q < mr ? (1 + 2 * q + h) * nj + j : (q == mr && h == 0 ? j : -1);
+            const int col = q < mr ? (1 + 2 * q + h) * nj + j : (q == mrl && h == 0 ? j : -1);
             float r = col >= 0 ? Wt[(size_t)row * ld + col] : 0.0f;
             uint16_t v = 0;
             for (int p = 0; p <= f; ++p) {
@@ -390,9 +397,10 @@ static int validate_desc(const anerf_model_desc* d) {
     if (d->net_width != 64 && d->net_width != 128 && d->net_width != 256)
         return fail(ANERF_EINVAL, "net_width must be 64, 128 or 256");
     if (d->net_depth < 2 || d->net_depth > MAXL) return fail(ANERF_EINVAL, "net_depth outside [2, 16]");
-    if (d->multires != 7 && d->multires != 10) return fail(ANERF_EINVAL, "multires must be 7 or 10");
-    if (d->multires_views != 4 && d->multires_views != 0)
-        return fail(ANERF_EINVAL, "multires_views must be 4 (the reference default) or 0 (surreal_single.txt)");
+    if (d->multires < 1 || d->multires > 10)
+        return fail(ANERF_EINVAL, "multires outside [1, 10] (kernel instances: 7 and 10, smaller counts zero-padded)");
+    if (d->multires_views < 0 || d->multires_views > 4)
+        return fail(ANERF_EINVAL, "multires_views outside [0, 4] (kernel instances: 0 and 4, 1-3 zero-padded)");
     if (d->single_net && d->has_fine) return fail(ANERF_EINVAL, "single_net models have no separate fine network");
     if (d->n_joints < 1 || d->n_joints > 128) return fail(ANERF_EINVAL, "n_joints outside [1, 128]");
     if (d->skip < 0) return fail(ANERF_EINVAL, "skip must be >= 0");
@@ -405,6 +413,7 @@ static int validate_desc(const anerf_model_desc* d) {
 static int pack_net(const anerf_model_desc* d, int njh2, const anerf_net_weights* w, Packer& pk,
                     std::vector<size_t>& offs) {
     const int W = d->net_width, WH = W / 2, nj = d->n_joints, mr = d->multires, mrv = d->multires_views;
+    const int mrl = layout_multires(mr), nkl = 1 + 2 * layout_multires_views(mrv);  // kernel layouts
     const int cin = nj * (1 + 2 * mr) + 3 * nj;
     const int nk = 1 + 2 * mrv;
     const int cv = 3 * nj * nk, cfc = d->framecode_ch;
@@ -423,11 +432,11 @@ static int pack_net(const anerf_model_desc* d, int njh2, const anerf_net_weights
         const bool sk = (i == d->skip + 1);
         offs.push_back(pk.add(pack_layer(w->pts_w[i], W, sk ? cin + W : W, sk ? cin : 0, W)));
     }
-    offs.push_back(pk.add(pack_vpart(w->pts_w[0], W, cin, nj, mr)));
+    offs.push_back(pk.add(pack_vpart(w->pts_w[0], W, cin, nj, mr, mrl)));
     const int skl = d->skip + 1;
     if (skl < d->net_depth) {
         offs.push_back(pk.add(pack_upart(w->pts_w[skl], W, cin + W, nj, njh2, mr)));
-        offs.push_back(pk.add(pack_vpart(w->pts_w[skl], W, cin + W, nj, mr)));
+        offs.push_back(pk.add(pack_vpart(w->pts_w[skl], W, cin + W, nj, mr, mrl)));
     } else {
         offs.push_back((size_t)-1);
         offs.push_back((size_t)-1);
@@ -454,7 +463,9 @@ static int pack_net(const anerf_model_desc* d, int njh2, const anerf_net_weights
     offs.push_back(pk.add(pack_rowvec(w->feature_b, W, false)));                      // bfeat (unused)
     offs.push_back(pk.add(pack_layer(wfused.data(), WH, W, 0, W)));                   // wview = Wv_f Wf
     {
-        const int tp = (3 * nk + 3) & ~3;
+        // [joint][WH][tp] rows of the view-direction weights in the instance's trig-table layout (nkl
+        // terms per component); the model's nk <= nkl terms filled, the rest zero
+        const int tp = (3 * nkl + 3) & ~3;
         std::vector<float> t((size_t)nj * WH * tp, 0.0f);
         for (int j = 0; j < nj; ++j)
             for (int k = 0; k < nk; ++k)
@@ -518,9 +529,9 @@ static int pack_net(const anerf_model_desc* d, int njh2, const anerf_net_weights
         offs.push_back((size_t)(int64_t)ew);
         offs.push_back(pk.add(pack_layer_h3(wfused.data(), WH, W, 0, W, ew)));     // wviewh
     }
-    offs.push_back(pk.add(pack_vpart_x6(w->pts_w[0], W, cin, nj, mr)));               // wv6 (layer 0)
+    offs.push_back(pk.add(pack_vpart_x6(w->pts_w[0], W, cin, nj, mr, mrl)));               // wv6 (layer 0)
     if (skl < d->net_depth)                                                           // wskipv6
-        offs.push_back(pk.add(pack_vpart_x6(w->pts_w[skl], W, cin + W, nj, mr)));
+        offs.push_back(pk.add(pack_vpart_x6(w->pts_w[skl], W, cin + W, nj, mr, mrl)));
     else
         offs.push_back((size_t)-1);
     return ANERF_OK;

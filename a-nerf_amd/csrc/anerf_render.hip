@@ -356,7 +356,7 @@ int anerf_render_rays(const anerf_model* m, const float* ray_batch, int32_t ray_
     int R = std::max(4, 8 / nbc);
     R = std::min(R, 8);
     const int W = m->desc.net_width;
-    const int nj = m->desc.n_joints, mrv = m->desc.multires_views, D = m->desc.net_depth;
+    const int nj = m->desc.n_joints, mrv = layout_multires_views(m->desc.multires_views), D = m->desc.net_depth;
     LdsPlan P = make_plan(R, nj, W, S, T, mrv, m->ngh, D, m->njh2, true, m->md.bone_cut != 0);
     if (P.total * 4 > 160 * 1024) P = make_plan(R, nj, W, S, T, mrv, m->ngh, D, m->njh2, false, m->md.bone_cut != 0);
     while (R > 1 && P.total * 4 > 160 * 1024) {
@@ -407,7 +407,7 @@ int anerf_render_rays(const anerf_model* m, const float* ray_batch, int32_t ray_
     a.zf_ws = I > 0 ? reinterpret_cast<float*>((char*)workspace + ws_near_far_bytes(n_rays)) : nullptr;
     const unsigned grid = (unsigned)((n_rays + R - 1) / R);
     const size_t lds_bytes = (size_t)P.total * 4;
-    const int mr = m->desc.multires;
+    const int mr = layout_multires(m->desc.multires);  // (the instance; smaller counts zero-padded, anerf_pack.hpp)
 #define ANERF_LAUNCH(WW, MM)                                                                         \
     do {                                                                                            \
         auto kfn = precision == ANERF_PREC_BF16X3 ? render_kernel<WW, MM, 1>                       \
@@ -577,7 +577,8 @@ int anerf_train_encode_backward(const anerf_model* m, const float* ray_batch, in
     else if (mr == 7 && mrv == 0) launch(train_encode_backward_kernel<7, 0>);
     else if (mr == 10 && mrv == 4) launch(train_encode_backward_kernel<10, 4>);
     else if (mr == 10 && mrv == 0) launch(train_encode_backward_kernel<10, 0>);
-    else return fail(ANERF_EINVAL, "anerf_train_encode_backward: multires must be 7 or 10, multires_views 4 or 0");
+    else return fail(ANERF_EINVAL, "anerf_train_encode_backward: training instances exist for multires 7 or 10 and "
+                                   "multires_views 4 or 0 (rendering takes multires 1-10, multires_views 0-4)");
     HIP_TRY(hipGetLastError());
     return ANERF_OK;
 }
@@ -646,7 +647,7 @@ static int launch_density(const anerf_model* m, DensityArgs a, int32_t precision
     if (a.net < 0) a.net = m->desc.has_fine ? 1 : 0;  // the reference's default network (raycasters.py:616-620)
     if (a.net == 1 && m->desc.single_net) a.net = 0;  // network_fine is network_fn
     if (a.net > 1 || (a.net == 1 && !m->desc.has_fine)) return fail(ANERF_EINVAL, "no such network");
-    const int W = m->desc.net_width, mr = m->desc.multires;
+    const int W = m->desc.net_width, mr = layout_multires(m->desc.multires);
     const LdsPlan P = make_density_plan(m->desc.n_joints, W, m->desc.net_depth, m->njh2, m->md.bone_cut != 0);
     if (P.total * 4 > 160 * 1024) return fail(ANERF_EINVAL, "configuration exceeds the 160 KiB LDS budget");
     const int64_t nb = (a.n + 31) / 32;

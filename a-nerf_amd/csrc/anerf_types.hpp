@@ -104,6 +104,7 @@ struct RenderArgs {
 // ======================================================================= LDS plan
 struct LdsPlan {
     int ray, sk, zc, zf, raw, g, scr, bias, cut, uf, wv;  // float offsets (uf < 0: no u-feature store)
+    int bord, bord_n;                   // block order (bf16x6): live-joint counts [bord_n], then the order
     int total;                          // floats
     int sk_stride, z_stride, raw_stride, g_stride, scr_stride, uf_stride, wv_stride;
 };
@@ -148,6 +149,8 @@ __host__ __device__ inline LdsPlan make_plan(int R, int nj, int W, int S, int T,
     if (with_uf) o += 4 * p.uf_stride;
     p.wv_stride = 64 * (njh2 + 1);  // per wave: view-direction windows w'_j of the block (+ a discard row)
     p.wv = o; o += 4 * p.wv_stride;
+    p.bord_n = (R * (((T > S ? T : S) + 31) / 32) + 3) & ~3;  // 32-sample blocks of the workgroup
+    p.bord = o; o += 2 * p.bord_n;
     p.total = (o + 3) & ~3;
     return p;
 }

@@ -390,6 +390,11 @@ class TrainRayCaster(nn.Module):
         uses cfg.precision."""
         super().__init__()
         self.cfg = cfg.validate()
+        if cfg.multires not in (7, 10) or cfg.multires_views not in (0, 4):
+            # (rendering takes any multires 1-10 / multires_views 0-4 on zero-padded instances; the encoder
+            # backward is instantiated per frequency count)
+            raise NotImplementedError("training: the encoder backward has instances for multires 7 / 10 and "
+                                      "multires_views 0 / 4")
         if mlp not in ("mixed", "bf16x6", "bf16x3", "fp32"):
             raise ValueError(f"mlp={mlp!r}: 'mixed', 'bf16x6', 'bf16x3' or 'fp32'")
         if isinstance(device, (str, torch.device)):

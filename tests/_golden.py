@@ -29,7 +29,10 @@ NAMES = ["c1_64_s32_d4w128", "c2_256_s64_d8w256", "c3_512_s64i128_d8w256", "c4_5
          # mean code), surreal (8x256, 64 + 16)
          "mx1_mixamo_s64i16_d8w256_fc", "su1_surreal_s64i16_d8w256",
          # render_path frames with white_bkgd / resized background images (two frames each)
-         "pw_64_white_d4w128", "pb_64_bgimg_d4w128"]
+         "pw_64_white_d4w128", "pb_64_bgimg_d4w128",
+         # multires / multires_views other than 7 / 4 and 10 (zero-padded on the 7 / 10, 4 instances) at
+         # widths 256 (bf16x6 windowed part), 128 and 64 (f32 windowed part)
+         "mr5_mrv2_s32i16_d8w256", "mr9_mrv3_s32i16_d8w128", "mr3_mrv1_s32i16_d4w64"]
 FRAMES = ["c1_64_s32_d4w128", "pw_64_white_d4w128", "pb_64_bgimg_d4w128"]
 
 
@@ -79,3 +82,50 @@ class Golden:
         vd = d / np.linalg.norm(d, axis=-1, keepdims=True)
         return np.concatenate([o, d, np.zeros((n, 1), np.float32), np.ones((n, 1), np.float32), vd],
                               axis=-1).astype(np.float32)
+
+
+def sqrt_tie_rays(rb, cyl, tol_ulp=0.02):
+    """Rays whose get_near_far_in_cylinder Q = (r^2 - dist^2)^0.5 (core/utils/ray_utils.py:318) is a
+    near-tie for float32 rounding: the exact square root of the float32 argument lies within tol_ulp of
+    the midpoint between two floats (hazard H13).  torch's CPU sqrt / pow(0.5) is faithful,
+    not correctly rounded (MKL VML), and can round such a Q the other way from the correctly rounded
+    sqrtf of the oracle and the GPU: near / far then differ by one float32 ulp.  The argument is
+    recomputed in the oracle's float32 operation order (oracle/anerf_oracle.c oracle_near_far)."""
+    f = np.float32
+    rb = np.asarray(rb, np.float32)
+    cy = np.asarray(cyl, np.float32).reshape(-1)
+    out = np.zeros(rb.shape[0], bool)
+    for i, r in enumerate(rb):
+        near, far = r[6], r[7]
+        rn0, rn1 = f(r[0] + f(r[3] * near)), f(r[2] + f(r[5] * near))
+        rf0, rf1 = f(r[0] + f(r[3] * far)), f(r[2] + f(r[5] * far))
+        nc0, nc1 = f(cy[0] - rn0), f(cy[1] - rn1)
+        nf0, nf1 = f(rf0 - rn0), f(rf1 - rn1)
+        nfn = f(np.sqrt(np.float32(np.float64(nf1) * nf1 + np.float64(f(nf0 * nf0)))))
+        dist = f(abs(f(f(nc0 * nf1) - f(nc1 * nf0))) / nfn)
+        c = f(f(cy[2] * cy[2]) - f(dist * dist))
+        if not c > 0:
+            continue
+        e = float(np.sqrt(np.float64(c)))
+        lo = np.float32(e)
+        lo = lo if float(lo) <= e else np.nextafter(lo, f(0))
+        ulp = float(np.nextafter(lo, f(np.inf))) - float(lo)
+        out[i] = abs((e - float(lo)) / ulp - 0.5) < tol_ulp
+    return out
+
+
+def assert_near_far_z(near, far, z, g, rb, what=""):
+    """near / far / coarse z against the reference's stage dumps: bit-exact, except on rays with a
+    sqrt near-tie (sqrt_tie_rays, hazard H13), where near / far may differ by one float32 ulp and z by
+    what that moves (1e-6 relative)."""
+    tie = sqrt_tie_rays(rb, g["cyls"][0])
+    for got, ref in ((near, g["stage_near"][:, 0]), (far, g["stage_far"][:, 0])):
+        np.testing.assert_array_equal(got[~tie], ref[~tie], err_msg=what)
+        if tie.any():
+            ulps = np.abs(got[tie].view(np.int32).astype(np.int64) - ref[tie].view(np.int32).astype(np.int64))
+            assert ulps.max() <= 1, (what, ulps)
+    np.testing.assert_array_equal(z[~tie], g["stage_z"][~tie], err_msg=what)
+    if tie.any():
+        zr = g["stage_z"][tie]
+        assert np.abs(z[tie] - zr).max() <= 1e-6 * np.abs(zr).max(), what
+    return int(tie.sum())

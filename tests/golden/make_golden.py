@@ -137,6 +137,15 @@ CONFIGS = {
                                         n_rays=160, seed=41),
     "su1_surreal_s64i16_d8w256": dict(H=512, NJ=24, S=64, I=16, D=8, W=256, tau=20.0, kind="rays", n_rays=192,
                                       seed=42),
+    # --multires / --multires_views other than the shipped 7 / 4 and the default 10 (run_nerf.py:275-280):
+    # the kernels' instances for 7 / 10 and 0 / 4 run them with the missing frequencies' weights zero
+    # (anerf_pack.hpp layout_multires); bf16x6 windowed part at W = 256 and 128, the f32 one at W = 64
+    "mr5_mrv2_s32i16_d8w256": dict(H=128, NJ=24, S=32, I=16, D=8, W=256, tau=20.0, kind="rays", n_rays=128, seed=51,
+                                   mr=5, mrv=2),
+    "mr9_mrv3_s32i16_d8w128": dict(H=128, NJ=24, S=32, I=16, D=8, W=128, tau=20.0, kind="rays", n_rays=128, seed=52,
+                                   mr=9, mrv=3),
+    "mr3_mrv1_s32i16_d4w64": dict(H=128, NJ=24, S=32, I=16, D=4, W=64, tau=20.0, kind="rays", n_rays=128, seed=53,
+                                  mr=3, mrv=1),
     # render_path's background compose (run_nerf.py:100-131): white_bkgd (bg = 1), and bg_imgs resized
     # with F.interpolate(bilinear, align_corners=False) and picked per frame by bg_indices; two frames
     # (reuse_input of the pose tensors, run_nerf.py:63-74)

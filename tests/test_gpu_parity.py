@@ -19,7 +19,7 @@ import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
 
-from _golden import FRAMES, Golden, NAMES  # noqa: E402
+from _golden import FRAMES, Golden, NAMES, assert_near_far_z  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -97,7 +97,7 @@ def test_framecode_mean_code_matches_golden():
 
 
 @pytest.mark.parametrize("name", [n for n in NAMES if n.startswith(("c2", "c3", "c4", "fc", "v", "s1", "t2000", "mx1",
-                                                                    "su1"))])
+                                                                    "su1", "mr"))])
 def test_stages_match_reference(name):
     """near/far and coarse z bit-exact; raw / weights / fine z against the reference's stage dumps."""
     g = Golden(name)
@@ -105,9 +105,8 @@ def test_stages_match_reference(name):
     rb = g.ray_batch()[:4]
     out = _render(rc, g, rb, cams=g["cams"][:4] if g.has("cams") else None, debug=True)
     dbg = {k: v.cpu().numpy() for k, v in rc.last_debug.items()}
-    np.testing.assert_array_equal(dbg["near"], g["stage_near"][:, 0])
-    np.testing.assert_array_equal(dbg["far"], g["stage_far"][:, 0])
-    np.testing.assert_array_equal(dbg["z_coarse"], g["stage_z"])
+    # bit-exact, but for a ray whose cylinder Q is a float32 rounding near-tie (hazard H13)
+    assert_near_far_z(dbg["near"], dbg["far"], dbg["z_coarse"], g, rb, name)
     _raw_close(dbg["raw_coarse"], g["stage_raw"], f"{name} raw_coarse")
     if g.cfg.N_importance > 0:
         assert _maxdiff(dbg["weights0"], g["stage_weights"]) <= 1e-5
