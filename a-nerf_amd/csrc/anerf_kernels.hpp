@@ -6,13 +6,16 @@
 #ifndef ANERF_BLOCK_SORT
 #define ANERF_BLOCK_SORT 1  // (0: blocks in ray order; tools/build_ab.sh experiments)
 #endif
+#ifndef ANERF_PERSIST
+#define ANERF_PERSIST 0  // (1: persistent workgroups over XCD-banded queues; tools/build_ab.sh experiments)
+#endif
+// The rays [ray0, ray0 + R) of one workgroup: both passes (or the launch's one) end to end.
 template <int W, int MR, int PREC>
-__global__ __launch_bounds__(256, 1) void render_kernel(ModelDev M, RenderArgs A, LdsPlan P) {
-    extern __shared__ __attribute__((aligned(16))) float lds[];
+__device__ __forceinline__ void render_item(const ModelDev& M, const RenderArgs& A, const LdsPlan& P,
+                                            float* __restrict__ lds, int64_t ray0) {
     constexpr int WH = W / 2;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int R = A.R, S = A.S, I = A.I, T = S + I;
-    const int64_t ray0 = (int64_t)blockIdx.x * R;
     const int nr = (int)min((int64_t)R, A.n - ray0);
 
     // ---- rays, poses, skeleton transforms into LDS
@@ -186,6 +189,41 @@ __global__ __launch_bounds__(256, 1) void render_kernel(ModelDev M, RenderArgs A
             __builtin_nontemporal_store(lds[P.zf + P.z_stride * r + s], A.zf_ws + (ray0 + r) * T + s);
         }
     STAMP_FLUSH(st, A.stamps);
+}
+
+// One launch of the render pass(es).  Default: workgroup b renders rays [b R, b R + R).  ANERF_PERSIST:
+// one workgroup per CU that takes R-ray items from eight queues, queue g = the g-th contiguous band of
+// the ray list, starting with its own (blockIdx & 7: workgroups b and b + 8 share an XCD under the
+// round-robin dispatch — a locality choice only, correctness does not depend on it) and stealing from
+// the others when it is empty, so each XCD's L2 sees the live joints of one band of the frame.
+template <int W, int MR, int PREC>
+__global__ __launch_bounds__(256, 1) void render_kernel(ModelDev M, RenderArgs A, LdsPlan P) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    if constexpr (!ANERF_PERSIST) {
+        render_item<W, MR, PREC>(M, A, P, lds, (int64_t)blockIdx.x * A.R);
+    } else {
+        const int64_t items = (A.n + A.R - 1) / A.R;
+        int* const slot = reinterpret_cast<int*>(lds + P.bord) + 2 * P.bord_n;
+        const int g0 = blockIdx.x & 7;
+        for (;;) {
+            if (threadIdx.x == 0) {
+                int64_t item = -1;
+                for (int k = 0; k < 8 && item < 0; ++k) {
+                    const int g = (g0 + k) & 7;
+                    const int64_t b0 = items * g / 8, b1 = items * (g + 1) / 8;
+                    if (b1 <= b0) continue;
+                    const unsigned t = atomicAdd(A.queue + g, 1u);
+                    if ((int64_t)t < b1 - b0) item = b0 + t;
+                }
+                slot[0] = (int)item;
+            }
+            __syncthreads();
+            const int item = slot[0];
+            if (item < 0) break;
+            render_item<W, MR, PREC>(M, A, P, lds, (int64_t)item * A.R);
+            __syncthreads();
+        }
+    }
 }
 
 // ======================================================================= density-only queries

@@ -483,9 +483,12 @@ __device__ __forceinline__ void split2_block_pair(const f32x16& hb, float t, H3T
 }
 
 // mlp_layer_h3's group: three MFMAs, the ring slot's four loads (even groups) after the first two
+#ifndef ANERF_H4
+#define ANERF_H4 0  // (experiment: + x1 w1, four fp16 products)
+#endif
 __device__ __forceinline__ void h3_group_schedule() {
 #if ANERF_H3_IL
-    group_schedule<3, 2, 2, ANERF_H3_IL>();
+    group_schedule<3 + ANERF_H4, 2, 2, ANERF_H3_IL>();
 #endif
 }
 
@@ -498,6 +501,7 @@ __device__ __forceinline__ f32x16 mfma_h3(const float (&w)[16], int half, const 
     const int o = 8 * half;
     const f16x8 w0 = __builtin_bit_cast(f16x8, f32x4{w[o], w[o + 1], w[o + 2], w[o + 3]});
     const f16x8 w1 = __builtin_bit_cast(f16x8, f32x4{w[o + 4], w[o + 5], w[o + 6], w[o + 7]});
+    if (ANERF_H4) c = mfma_f16_32x32x16(w1, x.frag(1), c);
     c = mfma_f16_32x32x16(w1, x.frag(0), c);  // small terms first
     c = mfma_f16_32x32x16(w0, x.frag(1), c);
     return mfma_f16_32x32x16(w0, x.frag(0), c);

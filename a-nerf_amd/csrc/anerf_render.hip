@@ -255,7 +255,7 @@ static size_t ws_zf_bytes(int64_t n, int32_t n_samples, int32_t n_importance) {
 size_t anerf_workspace_size(const anerf_model* m, int64_t n_rays, int32_t n_samples, int32_t n_importance) {
     (void)m;
     const int64_t n = n_rays > 0 ? n_rays : 1;
-    return ws_near_far_bytes(n) + ws_zf_bytes(n, n_samples, n_importance);
+    return ws_near_far_bytes(n) + ws_zf_bytes(n, n_samples, n_importance) + 256;  // (+ 2 x 8 queue counters)
 }
 
 static int launch_near_far(const float* rb, int stride, int64_t n, const float* cyls, const int32_t* ray_pose,
@@ -405,7 +405,15 @@ int anerf_render_rays(const anerf_model* m, const float* ray_batch, int32_t ray_
     // (single_net: one network, so one launch; the fine pass reuses the coarse raws, biases and G in LDS)
     const int pstep = (I > 0 && !fused_passes() && !m->desc.single_net) ? 1 : 2;
     a.zf_ws = I > 0 ? reinterpret_cast<float*>((char*)workspace + ws_near_far_bytes(n_rays)) : nullptr;
-    const unsigned grid = (unsigned)((n_rays + R - 1) / R);
+    unsigned grid = (unsigned)((n_rays + R - 1) / R);
+    unsigned* queues = reinterpret_cast<unsigned*>((char*)workspace + ws_near_far_bytes(n_rays) +
+                                                   ws_zf_bytes(n_rays, S, I));
+    if (ANERF_PERSIST) {  // one workgroup per CU, the items from the band queues (render_kernel)
+        int dev = 0, ncu = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        grid = std::min<unsigned>(grid, (unsigned)ncu);
+        HIP_TRY(hipMemsetAsync(queues, 0, 2 * 8 * sizeof(unsigned), st));
+    }
     const size_t lds_bytes = (size_t)P.total * 4;
     const int mr = layout_multires(m->desc.multires);  // (the instance; smaller counts zero-padded, anerf_pack.hpp)
 #define ANERF_LAUNCH(WW, MM)                                                                         \
@@ -418,6 +426,7 @@ int anerf_render_rays(const anerf_model* m, const float* ray_batch, int32_t ray_
         for (int p0 = 0; p0 < 2; p0 += pstep) {                                                     \
             a.pass0 = p0;                                                                           \
             a.pass1 = p0 + pstep;                                                                   \
+            a.queue = queues + 8 * p0;                                                              \
             hipLaunchKernelGGL(kfn, dim3(grid), dim3(256), lds_bytes, st, m->md, a, P);            \
         }                                                                                           \
     } while (0)

@@ -99,6 +99,7 @@ struct RenderArgs {
     int pass0, pass1;  // passes [pass0, pass1) of this launch (0 coarse, 1 fine)
     float* zf_ws;      // n x T: the fine pass's sorted z, handed from the coarse launch to the fine one
     int lindisp;       // sample_from_lineseg in inverse depth (ANERF_FLAG_LINDISP)
+    unsigned* queue;   // ANERF_PERSIST: this launch's 8 band counters (workspace, zeroed before the launch)
 };
 
 // ======================================================================= LDS plan
@@ -150,7 +151,7 @@ __host__ __device__ inline LdsPlan make_plan(int R, int nj, int W, int S, int T,
     p.wv_stride = 64 * (njh2 + 1);  // per wave: view-direction windows w'_j of the block (+ a discard row)
     p.wv = o; o += 4 * p.wv_stride;
     p.bord_n = (R * (((T > S ? T : S) + 31) / 32) + 3) & ~3;  // 32-sample blocks of the workgroup
-    p.bord = o; o += 2 * p.bord_n;
+    p.bord = o; o += 2 * p.bord_n + 4;  // (+ the persistent launch's item slot)
     p.total = (o + 3) & ~3;
     return p;
 }
