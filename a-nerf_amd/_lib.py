@@ -22,11 +22,12 @@ ANERF_PREC_FP32 = 0
 ANERF_PREC_BF16X3 = 1
 ANERF_PREC_BF16X6 = 2
 ANERF_PREC_FP16X3 = 3
+ANERF_PREC_FP16X4 = 4
 ANERF_FLAG_LINDISP = 0x100  # OR-ed into the precision argument (include/anerf.h)
 ANERF_FLAG_NEAR_FAR = 0x200  # ray_batch columns 6, 7 hold the filled near / far (anerf_render_rays)
 MLP_PRECISIONS = {"bf16x3": 3, "bf16x6": 6}  # ANERF_MLP_BF16X3 / _BF16X6 (training MLP GEMMs)
 PRECISIONS = {"fp32": ANERF_PREC_FP32, "bf16x3": ANERF_PREC_BF16X3, "bf16x6": ANERF_PREC_BF16X6,
-              "fp16x3": ANERF_PREC_FP16X3}
+              "fp16x3": ANERF_PREC_FP16X3, "fp16x4": ANERF_PREC_FP16X4}
 
 
 ANERF_ENC_CUT_TO_DIST, ANERF_ENC_CUTOFF_SHIFT, ANERF_ENC_CUTOFF_BONES = 1, 2, 4  # anerf_model_desc.encoder_flags

@@ -81,8 +81,8 @@ class RenderConfig:
             raise NotImplementedError(f"density activation {self.density_type} is undefined")
         if self.opt_framecode and self.n_framecodes <= 0:
             raise ValueError("opt_framecode needs n_framecodes > 0")
-        if self.precision not in ("fp32", "bf16x6", "bf16x3", "fp16x3"):
-            raise ValueError(f"precision={self.precision!r}: 'fp32', 'bf16x6', 'fp16x3' or 'bf16x3'")
+        if self.precision not in ("fp32", "bf16x6", "bf16x3", "fp16x3", "fp16x4"):
+            raise ValueError(f"precision={self.precision!r}: 'fp32', 'bf16x6', 'fp16x4', 'fp16x3' or 'bf16x3'")
         if self.n_joints < 1 or self.n_joints > 128:
             raise NotImplementedError(f"n_joints={self.n_joints} outside [1, 128]")
         for k, allowed in (("kp_dist_type", "reldist"), ("bone_type", "reldir"), ("view_type", "relray"),

@@ -49,7 +49,13 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int BM = 128, BN = 128, NTHR = 256;
 #ifndef ANERF_GEMM_IL
-#define ANERF_GEMM_IL 1
+#define ANERF_GEMM_IL 0  // (measured neutral: profiles/r04i_gemm_interleave_ab.txt)
+#endif
+// forward / input gradient row-tile height (experiment switch): 128 rows, two workgroups per CU; or 64
+// rows, four per CU (half the accumulators, LDS and epilogue per workgroup: more tiles in flight to
+// cover the per-tile load and store latency at K = 256)
+#ifndef ANERF_GEMM_BM
+#define ANERF_GEMM_BM 128
 #endif
 constexpr int MAXSEG = 3;
 
@@ -130,12 +136,13 @@ constexpr int SK = 32;        // k columns per step
 __device__ __forceinline__ int nt_off(int row, int k) { return row * SK + ((((k >> 3) ^ (row >> 2)) & 3) << 3) + (k & 7); }
 constexpr unsigned NOOB = 0x80000000u;  // a lane offset past every descriptor's range
 
-template <int NPL>
+template <int NPL, int TBM>
 struct NTGeo {
-    static constexpr int PLANE = BM * SK;             // bf16 elements
+    static constexpr int RBM = TBM / 32;               // 32-row blocks per tile
+    static constexpr int PLANE = TBM * SK;             // bf16 elements
     static constexpr int STAGE = NPL * PLANE;
     static constexpr int STAGES_BYTES = 2 * STAGE * 2;
-    static constexpr int TILE_BYTES = BM * 132 * 4;  // epilogue tile [128][132] fp32
+    static constexpr int TILE_BYTES = TBM * 132 * 4;  // epilogue tile [TBM][132] fp32
     static constexpr int TAB = STAGES_BYTES > TILE_BYTES ? STAGES_BYTES : TILE_BYTES;  // segment tables
     static constexpr int LDS_BYTES = TAB + 256;
 };
@@ -150,13 +157,14 @@ struct SegTab {
     int accum[MAXSEG];
 };
 
-template <int NPL, int NSEG>
-__global__ __launch_bounds__(NTHR, 2) void mlp_nt_kernel(NTArgs g) {
-    using G = NTGeo<NPL>;
+template <int NPL, int NSEG, int TBM>
+__global__ __launch_bounds__(NTHR, 256 / TBM) void mlp_nt_kernel(NTArgs g) {
+    using G = NTGeo<NPL, TBM>;
+    constexpr int RBM = G::RBM;
     extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
     const int logical = xcd_logical(blockIdx.x, g.total);
     const int mt = logical / g.tiles_n, nt = logical % g.tiles_n;
-    const long long m0 = (long long)mt * BM;
+    const long long m0 = (long long)mt * TBM;
     const int n0 = nt * NBN;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     // (kernel-argument fields as locals: referencing `g` inside the lambdas makes clang copy the
@@ -178,7 +186,7 @@ __global__ __launch_bounds__(NTHR, 2) void mlp_nt_kernel(NTArgs g) {
     // 8 rows x 128 B
     const int sr = tid >> 3, sc = 4 * (tid & 7);
     const long long rows_left = Md - m0;
-    const int rows = rows_left < BM ? (int)rows_left : BM;
+    const int rows = rows_left < TBM ? (int)rows_left : TBM;
     __amdgpu_buffer_rsrc_t ars[NSEG];
     unsigned arow[NSEG], astep[NSEG];
     int ast[NSEG], alim[NSEG];
@@ -196,9 +204,9 @@ __global__ __launch_bounds__(NTHR, 2) void mlp_nt_kernel(NTArgs g) {
     const long long bstride = (long long)ksteps * NPL * 512;  // elements per 32-column block
     const unsigned short* const bl = g.b + ((n0 + 32 * wave) / 32) * bstride + lane * 8;
 
-    f32x16 acc[4];
+    f32x16 acc[RBM];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) acc[i] = f32x16{0};
+    for (int i = 0; i < RBM; ++i) acc[i] = f32x16{0};
 
     struct BF {
         u32x4 v[NPL];
@@ -210,7 +218,7 @@ __global__ __launch_bounds__(NTHR, 2) void mlp_nt_kernel(NTArgs g) {
         for (int p = 0; p < NPL; ++p) f.v[p] = *reinterpret_cast<const u32x4*>(bk + p * 512);
     };
     struct RA {
-        f32x4 v[4][NSEG];
+        f32x4 v[RBM][NSEG];
     };
     // (steps past K read nothing: every column is outside every segment)
     auto fetch_a = [&](int st, RA& R) {
@@ -219,7 +227,7 @@ __global__ __launch_bounds__(NTHR, 2) void mlp_nt_kernel(NTArgs g) {
         for (int sg = 0; sg < NSEG; ++sg) {
             const unsigned vo = col >= ast[sg] && col < alim[sg] ? arow[sg] + (unsigned)(col - ast[sg]) * 4u : NOOB;
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+            for (int i = 0; i < RBM; ++i)
                 R.v[i][sg] = __builtin_bit_cast(
                     f32x4, __builtin_amdgcn_raw_buffer_load_b128(ars[sg], vo + (unsigned)i * astep[sg], 0, 0));
         }
@@ -227,7 +235,7 @@ __global__ __launch_bounds__(NTHR, 2) void mlp_nt_kernel(NTArgs g) {
     auto stage_a = [&](int buf, const RA& R) {
         unsigned short* const P = lds + buf * G::STAGE + nt_off(sr, sc);  // (row sr + 32 i: same swizzle)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < RBM; ++i) {
             float v[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -261,16 +269,16 @@ __global__ __launch_bounds__(NTHR, 2) void mlp_nt_kernel(NTArgs g) {
     auto step = [&](int buf, int kk, const BF& f) {
         const unsigned short* A = lds + buf * G::STAGE;
         const int r = lane & 31, kh = 16 * kk + 8 * (lane >> 5);
-        bf16x8 a[NPL][4], b[NPL];
+        bf16x8 a[NPL][RBM], b[NPL];
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < RBM; ++i)
 #pragma unroll
             for (int p = 0; p < NPL; ++p)
                 a[p][i] = *reinterpret_cast<const bf16x8*>(A + p * G::PLANE + nt_off(32 * i + r, kh));
 #pragma unroll
         for (int p = 0; p < NPL; ++p) b[p] = __builtin_bit_cast(bf16x8, f.v[p]);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < RBM; ++i) {
             f32x16 c = acc[i];
             if constexpr (NPL == 3) {
                 c = mfma(a[2][i], b[0], c);
@@ -288,8 +296,8 @@ __global__ __launch_bounds__(NTHR, 2) void mlp_nt_kernel(NTArgs g) {
     auto step_stage = [&](int buf, const BF& f, int sbuf, const RA& R) {
         step(buf, 1, f);
         stage_a(sbuf, R);
-        constexpr int NM = 4 * (NPL == 3 ? 6 : 3), VS = NPL == 3 ? 3 : 4;
-        __builtin_amdgcn_sched_group_barrier(0x100, 4 * NPL, 0);  // the fragment reads first
+        constexpr int NM = RBM * (NPL == 3 ? 6 : 3), VS = NPL == 3 ? 3 : 4;
+        __builtin_amdgcn_sched_group_barrier(0x100, RBM * NPL, 0);  // the fragment reads first
 #pragma unroll
         for (int i = 0; i < NM; ++i) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -349,14 +357,14 @@ __global__ __launch_bounds__(NTHR, 2) void mlp_nt_kernel(NTArgs g) {
     constexpr int TP = 132;  // tile pitch (floats)
     float* const tile = reinterpret_cast<float*>(lds);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < RBM; ++i)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int row = 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
             tile[row * TP + 32 * wave + (lane & 31)] = acc[i][r];
         }
     __syncthreads();
-    // thread t: rows 8 q + (t >> 5) (q = 0..15), columns 4 (t & 31) .. + 3
+    // thread t: rows 8 q + (t >> 5) (q < TBM / 8), columns 4 (t & 31) .. + 3
     const int c4 = 4 * (tid & 31), rb = tid >> 5;
     const int n = n0 + c4;
     const int Nd = g.N;
@@ -382,10 +390,10 @@ __global__ __launch_bounds__(NTHR, 2) void mlp_nt_kernel(NTArgs g) {
             for (int e = 0; e < 4; ++e) bv[e] = n + e < Nd ? bias[n + e] : 0.0f;
         }
         // mask / accumulate operands of all 16 rows first (clamped rows: no load waits on a branch)
-        f32x4 mk[16], ov[16];
+        f32x4 mk[TBM / 8], ov[TBM / 8];
         if (vec && op && mp) {
 #pragma unroll
-            for (int q = 0; q < 16; ++q) {
+            for (int q = 0; q < TBM / 8; ++q) {
                 long long m = m0 + 8 * q + rb;
                 m = m < Md ? m : Md - 1;
                 mk[q] = *(gf32x4*)(mp + m * ldm + col);
@@ -393,7 +401,7 @@ __global__ __launch_bounds__(NTHR, 2) void mlp_nt_kernel(NTArgs g) {
         }
         if (vec && op && need_acc) {
 #pragma unroll
-            for (int q = 0; q < 16; ++q) {
+            for (int q = 0; q < TBM / 8; ++q) {
                 long long m = m0 + 8 * q + rb;
                 m = m < Md ? m : Md - 1;
                 ov[q] = *(gf32x4*)(op + m * old + col);
@@ -401,7 +409,7 @@ __global__ __launch_bounds__(NTHR, 2) void mlp_nt_kernel(NTArgs g) {
         }
         if (vec) {
 #pragma unroll
-            for (int q = 0; q < 16; ++q) {
+            for (int q = 0; q < TBM / 8; ++q) {
                 const int row = 8 * q + rb;
                 const long long m = m0 + row;
                 f32x4 v = *reinterpret_cast<const f32x4*>(tile + row * TP + c4);
@@ -424,7 +432,7 @@ __global__ __launch_bounds__(NTHR, 2) void mlp_nt_kernel(NTArgs g) {
             }
         } else {  // (segment boundaries inside the float4, ragged last columns, unaligned outputs)
 #pragma unroll 1
-            for (int q = 0; q < 16; ++q) {
+            for (int q = 0; q < TBM / 8; ++q) {
                 const int row = 8 * q + rb;
                 const long long m = m0 + row;
                 if (m >= Md) break;
@@ -820,10 +828,10 @@ int planes_of(int precision) { return precision == ANERF_MLP_BF16X6 ? 3 : (preci
 
 // the dynamic LDS (up to 67 KB) is above the default limit: raised once per kernel instance
 // (set on every call: the attribute belongs to the current device, and a cached failure would stick)
-template <int NPL, int NSEG>
+template <int NPL, int NSEG, int TBM>
 hipError_t nt_attr() {
-    return hipFuncSetAttribute((const void*)mlp_nt_kernel<NPL, NSEG>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               NTGeo<NPL>::LDS_BYTES);
+    return hipFuncSetAttribute((const void*)mlp_nt_kernel<NPL, NSEG, TBM>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               NTGeo<NPL, TBM>::LDS_BYTES);
 }
 template <int NPL, int NSEG>
 hipError_t tn_attr() {
@@ -953,16 +961,20 @@ int anerf_mlp_gemm(int64_t m, int32_t n, int32_t k, const anerf_seg* a, int32_t 
     if (start != n) return anerf_internal_fail(ANERF_EINVAL, "output segments do not add up to n");
     g.nc = n_c;
     g.tiles_n = (n + NBN - 1) / NBN;
-    const long long tiles = (long long)((m + BM - 1) / BM) * g.tiles_n;
+    // row-tile height: 128, or (ANERF_GEMM_BM 64) 64 for the single-segment instances
+    const int tbm = (ANERF_GEMM_BM == 64 && n_a == 1) ? 64 : 128;
+    const long long tiles = (long long)((m + tbm - 1) / tbm) * g.tiles_n;
     if (tiles > 0x7fffffff) return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_gemm: too many tiles");
     g.total = (int)tiles;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     hipError_t e = hipSuccess;
 #define ANERF_NT_LAUNCH(P, S)                                                                         \
     if (npl == P && n_a == S) {                                                                       \
-        e = nt_attr<P, S>();                                                                          \
+        constexpr int TB = (ANERF_GEMM_BM == 64 && S == 1) ? 64 : 128;                                \
+        e = nt_attr<P, S, TB>();                                                                      \
         if (e != hipSuccess) return anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));            \
-        hipLaunchKernelGGL((mlp_nt_kernel<P, S>), dim3((unsigned)tiles), dim3(NTHR), NTGeo<P>::LDS_BYTES, st, g); \
+        constexpr int LB = NTGeo<P, TB>::LDS_BYTES;                                                   \
+        hipLaunchKernelGGL((mlp_nt_kernel<P, S, TB>), dim3((unsigned)tiles), dim3(NTHR), LB, st, g);  \
     }
     ANERF_NT_LAUNCH(3, 1)
     ANERF_NT_LAUNCH(3, 2)

@@ -80,7 +80,7 @@ __device__ __forceinline__ void render_item(const ModelDev& M, const RenderArgs&
         };
         int* const bcnt = reinterpret_cast<int*>(lds + P.bord);
         int* const bord = bcnt + P.bord_n;
-        if constexpr (PREC == 2 && ANERF_BLOCK_SORT) {
+        if constexpr (lockstep_mode<PREC>() && ANERF_BLOCK_SORT) {
             // bf16x6: the four waves meet at a workgroup barrier before every hidden layer (L1 sharing of
             // the weight stream), where a wave whose block has fewer live joints waits for the others
             // (5.8 % of the wave-cycles, profiles/r04c_stamps_bf16x6.txt).  The blocks of the workgroup
@@ -109,10 +109,10 @@ __device__ __forceinline__ void render_item(const ModelDev& M, const RenderArgs&
         // layer; a wave past the last block redoes that block without storing or counting it)
         for (int it = 0; it < (nbt + 3) / 4; ++it) {
             const bool own = it * 4 + wave < nbt;
-            if constexpr (PREC != 2)  // (no workgroup barrier inside: a wave without a block is done)
+            if constexpr (!lockstep_mode<PREC>())  // (no workgroup barrier inside: a wave without a block is done)
                 if (!own) break;
             const int bi = own ? it * 4 + wave : nbt - 1;
-            const int b = (PREC == 2 && ANERF_BLOCK_SORT) ? bord[bi] : bi;
+            const int b = (lockstep_mode<PREC>() && ANERF_BLOCK_SORT) ? bord[bi] : bi;
             const int r = b / nb, s0 = (b % nb) * 32;
             const float* zr = block_z(r);
             float* rawr = lds + P.raw + P.raw_stride * r + (only_new ? 4 * S : 0);
@@ -273,7 +273,7 @@ __global__ __launch_bounds__(256, 1) void density_kernel(ModelDev M, DensityArgs
     // a wave past the last block redoes it without storing)
     for (int64_t base = (int64_t)blockIdx.x * 4; base < nb; base += (int64_t)gridDim.x * 4) {
         const bool own = base + wave < nb;
-        if constexpr (PREC != 2)
+        if constexpr (!lockstep_mode<PREC>())
             if (!own) break;
         const int64_t b = own ? base + wave : nb - 1;
         const int64_t s_out = b * 32 + (lane & 31);
@@ -297,7 +297,7 @@ __global__ __launch_bounds__(256, 1) void density_kernel(ModelDev M, DensityArgs
         float sig = 0.0f;
 #pragma unroll
         for (int q = 0; q < W / 2; ++q) sig = fmaf(wa[q], relu_act(acc[q >> 4][q & 15]), sig);
-        if constexpr (PREC == 3) sig *= pow2f(-es);  // (fp16x3: the last layer's units)
+        if constexpr (PREC >= 3) sig *= pow2f(-es);  // (fp16x3 / fp16x4: the last layer's units)
         sig += __shfl_xor(sig, 32);
         sig += net.balpha;
         if (own && hh == 0 && s_out < A.n) A.out[s_out] = sig;

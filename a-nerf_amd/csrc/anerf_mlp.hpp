@@ -483,12 +483,11 @@ __device__ __forceinline__ void split2_block_pair(const f32x16& hb, float t, H3T
 }
 
 // mlp_layer_h3's group: three MFMAs, the ring slot's four loads (even groups) after the first two
-#ifndef ANERF_H4
-#define ANERF_H4 0  // (experiment: + x1 w1, four fp16 products)
-#endif
+// (NP = 3: fp16x3, NP = 4: fp16x4)
+template <int NP>
 __device__ __forceinline__ void h3_group_schedule() {
 #if ANERF_H3_IL
-    group_schedule<3 + ANERF_H4, 2, 2, ANERF_H3_IL>();
+    group_schedule<NP, 2, 2, ANERF_H3_IL>();
 #endif
 }
 
@@ -496,12 +495,16 @@ __device__ __forceinline__ f32x16 mfma_f16_32x32x16(f16x8 a, f16x8 b, f32x16 c) 
     return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 
-// group `half` (0 / 1) of a 16-float ring slot: fragments w0 (floats 8 half .. +3), w1 (+4 .. +7)
+// group `half` (0 / 1) of a 16-float ring slot: fragments w0 (floats 8 half .. +3), w1 (+4 .. +7).
+// NP = 4 (ANERF_PREC_FP16X4) adds x1 w1: the product is then (x - r_x)(w - r_w) with |r_x| <= 2^-23 |x|
+// and |r_w| <= 2^-23 |w| (the split remainders), i.e. within ~2^-22 of |x w| — the same bound as
+// bf16x6's dropped x1 w2 + x2 w1 + x2 w2 + r_w terms — with four products instead of six.
+template <int NP>
 __device__ __forceinline__ f32x16 mfma_h3(const float (&w)[16], int half, const H3T& x, f32x16 c) {
     const int o = 8 * half;
     const f16x8 w0 = __builtin_bit_cast(f16x8, f32x4{w[o], w[o + 1], w[o + 2], w[o + 3]});
     const f16x8 w1 = __builtin_bit_cast(f16x8, f32x4{w[o + 4], w[o + 5], w[o + 6], w[o + 7]});
-    if (ANERF_H4) c = mfma_f16_32x32x16(w1, x.frag(1), c);
+    if constexpr (NP == 4) c = mfma_f16_32x32x16(w1, x.frag(1), c);
     c = mfma_f16_32x32x16(w1, x.frag(0), c);  // small terms first
     c = mfma_f16_32x32x16(w0, x.frag(1), c);
     return mfma_f16_32x32x16(w0, x.frag(0), c);
@@ -535,7 +538,7 @@ __device__ __forceinline__ float h3_scale(const f32x16 (&a)[RBI], int& es, int e
 // mlp_layer_x6's schedule with 8-float groups (3 MFMAs each), two groups per ring slot (slot
 // (g / 2) % 4, prefetched 3 slots = 6 groups ahead).  OUT_SAME layers alias out and ain; bias * 2^es
 // initialises the outputs.  ALPHA folds sig += w_alpha . h with h in the INPUT's units.
-template <int RBO, int RBI, bool OUT_SAME, bool ALPHA>
+template <int RBO, int RBI, bool OUT_SAME, bool ALPHA, int NP = 3>
 __device__ __forceinline__ void mlp_layer_h3(f32x16 (&out)[RBO], f32x16 (&ain)[RBI], f32x16 (&h)[RBI],
                                              const float* __restrict__ bias, const float* __restrict__ wp, int lane,
                                              Ring& ring, bool preloaded, const float* __restrict__ next,
@@ -602,7 +605,7 @@ __device__ __forceinline__ void mlp_layer_h3(f32x16 (&out)[RBO], f32x16 (&ain)[R
         __builtin_amdgcn_sched_barrier(0);
         prefetch(g);
         const int ob = g >> 1, s = g & 1;
-        out[ob] = mfma_h3(ring.v[(g >> 1) % 4], g & 1, T[s], out[ob]);
+        out[ob] = mfma_h3<NP>(ring.v[(g >> 1) % 4], g & 1, T[s], out[ob]);
         if (ob == 0) alpha(0, s);
         if (ob + 1 < RBI && (ob + 1 < RBO || ob == 0)) convert_half(ob + 1, s);
         if (RBI > 1) {
@@ -611,7 +614,7 @@ __device__ __forceinline__ void mlp_layer_h3(f32x16 (&out)[RBO], f32x16 (&ain)[R
                 if (pair_group(p, QL) == (g < QL ? -1 : g) || (g == NQ - 1 && pair_group(p, QL) > g))
                     split2_block_pair(h[1], t, Tn, p);
         }
-        h3_group_schedule();
+        h3_group_schedule<NP>();
     }
 #pragma clang loop unroll(full)
     for (int ib = 1; ib < RBI; ++ib) {
@@ -625,7 +628,7 @@ __device__ __forceinline__ void mlp_layer_h3(f32x16 (&out)[RBO], f32x16 (&ain)[R
             const int g = NQ + (ib - 1) * NQ + q;
             __builtin_amdgcn_sched_barrier(0);
             prefetch(g);
-            out[ob] = mfma_h3(ring.v[(g >> 1) % 4], g & 1, T[s], out[ob]);
+            out[ob] = mfma_h3<NP>(ring.v[(g >> 1) % 4], g & 1, T[s], out[ob]);
             if (ob == RBO - 1) alpha(ib, s);
             if (ib + 1 < RBI) {
                 if (conv_next && q < 2) convert_half(ib + 1, q);
@@ -634,7 +637,7 @@ __device__ __forceinline__ void mlp_layer_h3(f32x16 (&out)[RBO], f32x16 (&ain)[R
                     if (pair_group(p, q0) == q || (q == NQ - 1 && pair_group(p, q0) > q))
                         split2_block_pair(h[ib + 1], t, Tn, p);
             }
-            h3_group_schedule();
+            h3_group_schedule<NP>();
         }
     }
 }
@@ -995,6 +998,11 @@ __device__ __forceinline__ int block_live_count(const ModelDev& M, const float* 
 #ifndef ANERF_X6_BARRIERS
 #define ANERF_X6_BARRIERS 3
 #endif
+// Precision modes whose four waves run the hidden layers in lock step (a workgroup barrier before
+// each, blocks in live-joint order): bf16x6 and fp16x4 (+2.6 % on fp16x4, bit-identical outputs,
+// profiles/r04i_ab_fp16x4.txt); fp16x3 runs free (neutral in round 3)
+template <int P>
+constexpr bool lockstep_mode() { return P == 2 || P == 4; }
 
 // One x part's bone-direction contraction from the LDS features as bf16x6: k16-step s takes
 // features 8 s .. 8 s + 7 of each lane half (zero past 3 NJH2), split by truncation (split3_pair);
@@ -1318,7 +1326,7 @@ __device__ __forceinline__ bool mlp_trunk(const ModelDev& M, const NetDev& net, 
     if (!ux6) ring_preload<2 * RB>(ring, net.wl[0], lane);  // the u part's first groups, early
     load_bias<RB>(acc, bias, hh);
     STAMP(st, 10);
-    const float* const* wl = P == 3 ? net.wlh : (P == 2 ? net.wl6 : (P ? net.wl3 : net.wl));  // hidden-layer streams
+    const float* const* wl = P >= 3 ? net.wlh : (P == 2 ? net.wl6 : (P ? net.wl3 : net.wl));  // hidden-layer streams
     if (ux6) {
         if constexpr (UX6) u_part_x6_preload<RB>(net.wu6, lane, ring);  // (latency under the VALU pass)
         u_features_lds<WV>(M, sk, cut, px, py, pz, lane, &mask, uf, wvo);
@@ -1350,18 +1358,18 @@ __device__ __forceinline__ bool mlp_trunk(const ModelDev& M, const NetDev& net, 
         // (ANERF_X6_BARRIERS, experiments: 3 before every hidden layer, 2 before layer 1 and the layer
         // after the skip layer, 1 before layer 1 only, 0 none)
         constexpr int XB = ANERF_X6_BARRIERS;
-        if constexpr (SYNC && P == 2 && XB > 0) {
+        if constexpr (SYNC && lockstep_mode<P>() && XB > 0) {
             if (XB == 3 || L == 1 || (XB == 2 && L == M.skip + 2)) {
                 __builtin_amdgcn_s_barrier();
                 STAMP(st, 18);  // (stamps build: the wait at this barrier)
             }
         }
-        if constexpr (P == 3) {
+        if constexpr (P >= 3) {
             // the next h3 phase (the next hidden layer or the view layer) is prefetched; not across the
             // skip layer's x parts, which load themselves and scale their B operands by 2^es (the
             // units the h part left in the accumulators)
             const float* nxth = skl ? nullptr : after;
-            mlp_layer_h3<RB, RB, true, false>(acc, acc, h, bias + L * W, wl[L], lane, ring, pre6, nxth, nullptr,
+            mlp_layer_h3<RB, RB, true, false, P == 4 ? 4 : 3>(acc, acc, h, bias + L * W, wl[L], lane, ring, pre6, nxth, nullptr,
                                               nosig, es, net.ewl[L], M.h3_top);
             pre6 = nxth != nullptr;
             if (skl) {  // the f32 skip x parts take their first groups from the ring (the x6 one loads itself)
@@ -1390,7 +1398,7 @@ __device__ __forceinline__ bool mlp_trunk(const ModelDev& M, const NetDev& net, 
         }
         STAMP(st, 11);
         if (skl) {  // x part after the h part (in the h part's units: B operands times xs)
-            const float xs = P == 3 ? pow2f(es) : 1.0f;
+            const float xs = P >= 3 ? pow2f(es) : 1.0f;
             if (ux6) {
                 if constexpr (UX6) u_part_x6<RB>(acc, M, net.wskipu6, uf, lane, ring, P == 2, xs);
             } else if (uf)
@@ -1432,15 +1440,15 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
     Ring ring;
     int es = 0;
     const bool pre = mlp_trunk<W, MR, true, P>(M, net, sk, cut, px, py, pz, lane, bias, uf, wvp, acc, h, ring, mask,
-                                               P == 3 ? net.wviewh : (P == 2 ? net.wview6 : net.wview), st, es);
+                                               P >= 3 ? net.wviewh : (P == 2 ? net.wview6 : net.wview), st, es);
     // views_linears.0 with feature_linear fused in (W' = Wv_f Wf, see pack_net) on relu(h_last),
     // alpha_linear folded into its groups (same relu'd B operands), + the factorised
     // direction / code / bias part from G, then relu
     float sig = 0.0f;
     f32x16 av[RBV];
-    if constexpr (P == 3) {
+    if constexpr (P >= 3) {
         const int es_h = es;  // the alpha head sums the last hidden layer's activations, in its units
-        mlp_layer_h3<RBV, RB, false, true>(av, acc, h, nullptr, net.wviewh, lane, ring, pre, nullptr,
+        mlp_layer_h3<RBV, RB, false, true, P == 4 ? 4 : 3>(av, acc, h, nullptr, net.wviewh, lane, ring, pre, nullptr,
                                            bias + (M.D + 1) * W, sig, es, net.ew_view, M.h3_top);
         sig *= pow2f(-es_h);
     } else if constexpr (P == 2)
@@ -1453,7 +1461,7 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
     sig += __shfl_xor(sig, 32);
     sig += net.balpha;
     const int vsteps = view_dir_part<RBV>(av, M, G, wvp, reinterpret_cast<const unsigned*>(ray) + 12, lane,
-                                          P == 3 ? pow2f(es) : 1.0f);
+                                          P >= 3 ? pow2f(es) : 1.0f);
     STAMP(st, 17);
     float rgb[3];
 #pragma unroll
@@ -1465,7 +1473,7 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
 #pragma unroll
             for (int i = 0; i < 16; ++i) a += wr[rb * 16 + i] * relu_act(av[rb][i]);
         a += __shfl_xor(a, 32);
-        if constexpr (P == 3) a *= pow2f(-es);  // (the view layer's units)
+        if constexpr (P >= 3) a *= pow2f(-es);  // (the view layer's units)
         rgb[c] = a + net.brgb[c];
     }
     STAMP(st, 13);
@@ -1478,14 +1486,15 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
         const int nx = (M.skip + 1 < M.D) ? 2 : 1;
         if (ux6) atomicAdd(mfma_count + 1, (unsigned long long)(nx * ((3 * M.njh2 + 7) / 8) * RB * 6));
         if (vx6) atomicAdd(mfma_count + 1, (unsigned long long)(nx * act * VPartX6<MR, 1>::KS * RB * 6));
-        if (P >= 2)  // view layer, bf16x6 / fp16x3
-            atomicAdd(mfma_count + 1, (unsigned long long)(RBV * RB * 2 * (P == 2 ? 6 : 3)));
+        constexpr int NPR = P == 2 ? 6 : (P == 4 ? 4 : 3);  // products per k16-step
+        if (P >= 2)  // view layer, bf16x6 / fp16x3 / fp16x4
+            atomicAdd(mfma_count + 1, (unsigned long long)(RBV * RB * 2 * NPR));
         else
             k += (long long)(W / 2) * RBV;
         if (M.skip + 1 < M.D) k += (long long)xk * RB;
         const long long hid = (long long)(M.D - 1) * RB * RB;  // 32x32 blocks of the hidden layers
         if (P != 0) {
-            atomicAdd(mfma_count + 1, (unsigned long long)(hid * 2 * (P == 2 ? 6 : 3)));  // 2 k16-steps x products
+            atomicAdd(mfma_count + 1, (unsigned long long)(hid * 2 * NPR));  // 2 k16-steps x products
         } else {
             k += hid * 16;
         }

@@ -316,7 +316,7 @@ int anerf_render_rays(const anerf_model* m, const float* ray_batch, int32_t ray_
     precision &= 0xff;
     if (flags & ~(ANERF_FLAG_LINDISP | ANERF_FLAG_NEAR_FAR))
         return fail(ANERF_EINVAL, "unknown flags in the precision argument");
-    if (precision < ANERF_PREC_FP32 || precision > ANERF_PREC_FP16X3) return fail(ANERF_EINVAL, "unsupported precision");
+    if (precision < ANERF_PREC_FP32 || precision > ANERF_PREC_FP16X4) return fail(ANERF_EINVAL, "unsupported precision");
     if (!ray_batch || ray_stride < 8 || !skts || !cyls || n_poses < 1 || !rgb || !disp || !acc)
         return fail(ANERF_EINVAL, "anerf_render_rays: bad arguments");
     if (n_samples < 2 || n_samples > 1024 || n_importance < 0 || n_importance > 2048)
@@ -420,7 +420,8 @@ int anerf_render_rays(const anerf_model* m, const float* ray_batch, int32_t ray_
     do {                                                                                            \
         auto kfn = precision == ANERF_PREC_BF16X3 ? render_kernel<WW, MM, 1>                       \
                  : precision == ANERF_PREC_BF16X6 ? render_kernel<WW, MM, 2>                       \
-                 : precision == ANERF_PREC_FP16X3 ? render_kernel<WW, MM, 3> : render_kernel<WW, MM, 0>; \
+                 : precision == ANERF_PREC_FP16X3 ? render_kernel<WW, MM, 3>                       \
+                 : precision == ANERF_PREC_FP16X4 ? render_kernel<WW, MM, 4> : render_kernel<WW, MM, 0>; \
         HIP_TRY(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,  \
                                     (int)lds_bytes));                                               \
         for (int p0 = 0; p0 < 2; p0 += pstep) {                                                     \
@@ -648,7 +649,7 @@ int anerf_train_importance(const float* z, const float* weights, int64_t n_rays,
 }
 
 static int launch_density(const anerf_model* m, DensityArgs a, int32_t precision, void* stream) {
-    if (precision < ANERF_PREC_FP32 || precision > ANERF_PREC_FP16X3) return fail(ANERF_EINVAL, "unsupported precision");
+    if (precision < ANERF_PREC_FP32 || precision > ANERF_PREC_FP16X4) return fail(ANERF_EINVAL, "unsupported precision");
     if (a.n == 0) return ANERF_OK;
     int dev = -1;
     HIP_TRY(hipGetDevice(&dev));
@@ -667,7 +668,8 @@ static int launch_density(const anerf_model* m, DensityArgs a, int32_t precision
     do {                                                                                            \
         auto kfn = precision == ANERF_PREC_BF16X3 ? density_kernel<WW, MM, 1>                      \
                  : precision == ANERF_PREC_BF16X6 ? density_kernel<WW, MM, 2>                      \
-                 : precision == ANERF_PREC_FP16X3 ? density_kernel<WW, MM, 3> : density_kernel<WW, MM, 0>; \
+                 : precision == ANERF_PREC_FP16X3 ? density_kernel<WW, MM, 3>                      \
+                 : precision == ANERF_PREC_FP16X4 ? density_kernel<WW, MM, 4> : density_kernel<WW, MM, 0>; \
         HIP_TRY(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,  \
                                     (int)lds_bytes));                                               \
         hipLaunchKernelGGL(kfn, dim3(grid), dim3(256), lds_bytes, st, m->md, a, P);                \

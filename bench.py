@@ -14,8 +14,11 @@ kp_to_valid_rays is computed on the host before the timed region).
   layout (one independent frame per rank, no collective).
 Rank 0 reports the job's rays / max-over-ranks time, and per-rank render / all-gather / compose ms.
 
-Headline precision: bf16x6 (operands split exactly into 3 x 8 bits, the six products with i + j <= 2,
-fp32 accumulation: fp32-accurate).  The other modes are timed on the same frame (`other_precisions`).
+Headline precision: fp16x4 (operands scaled by exact powers of two and split into two fp16 parts each,
+x = x0 + x1 and W = W0 + W1 within 2^-23 of |x|, |W|; all four products, fp32 accumulation: each product
+within ~2^-22 of |x W|, the bound of bf16x6's dropped terms, so fp32-accurate like bf16x6 with four
+16-bit MFMAs per 16 k instead of six).  The other modes — bf16x6 (the round-3 headline), fp16x3, fp32,
+bf16x3 — are timed on the same frame (`other_precisions`).
 
 Extra JSON fields:
   roofline      dominant kernel (render_kernel, coarse + fine launch) against the peak of the MFMA
@@ -60,10 +63,14 @@ DTYPE = {
               "three fp16 MFMA products (x1 W1, ~2^-22 of |x W|, dropped), fp32 accumulate; bone-direction parts and "
               "the windowed layer-0 / skip-layer parts bf16x6 at widths 128/256 (fp32 at 64); encoder, heads, "
               "compositing fp32",
+    "fp16x4": "fp32-accurate split fp16: hidden and view layers after exact power-of-two scaling, x = x0+x1 and "
+              "W = W0+W1 (remainders within 2^-23 of |x|, |W|), the four fp16 MFMA products x_i W_j (dropped: the "
+              "remainders' ~2^-22 of |x W|, the bound of bf16x6's dropped terms), fp32 accumulate; bone-direction and "
+              "windowed layer-0 / skip-layer parts bf16x6 at widths 128/256; encoder, heads, compositing fp32",
     "bf16x3": "16-bit operands: split bf16 (x = hi+lo, W = hi+lo, three bf16 MFMA products), fp32 accumulate; "
               "fp32 elsewhere",
 }
-PRODUCTS = {"fp32": 1, "bf16x6": 6, "fp16x3": 3, "bf16x3": 3}
+PRODUCTS = {"fp32": 1, "bf16x6": 6, "fp16x4": 4, "fp16x3": 3, "bf16x3": 3}
 FLOP_F32_MFMA = 32 * 32 * 2 * 2     # v_mfma_f32_32x32x2_f32
 FLOP_BF16_MFMA = 32 * 32 * 16 * 2   # v_mfma_f32_32x32x16_bf16
 TILE = 256  # pixels mode: rays per tile of the round-robin split (distributed.tile_rows)
@@ -92,9 +99,9 @@ def parse():
                          "split into ray-balanced ranges across the ranks (near / far from the whole frame's "
                          "4096-ray chunks) + an RCCL all-gather of the ray outputs (strong scaling, BASELINE "
                          "config 5's layout; the default under torch.distributed.run)")
-    ap.add_argument("--also", default="fp16x3,fp32,bf16x3",
+    ap.add_argument("--also", default="bf16x6,fp16x3,fp32,bf16x3",
                     help="other precision modes timed on the same frame afterwards (rank 0, N=1; '' = none)")
-    ap.add_argument("--precision", default="bf16x6", choices=["fp32", "bf16x6", "fp16x3", "bf16x3"],
+    ap.add_argument("--precision", default="fp16x4", choices=["fp32", "bf16x6", "fp16x4", "fp16x3", "bf16x3"],
                     help="MLP arithmetic (include/anerf.h ANERF_PREC_*)")
     return ap.parse_args()
 
@@ -574,10 +581,11 @@ def main():
                          "traffic": traffic, "traffic_source": traffic_src,
                          "traffic_measured_in_this_run": False,
                          "traffic_note": "2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md, HBM / rocprofv3): L2 "
-                                         "fabric-side bytes, which count Infinity-Cache (L3) hits. bf16x6's per-net "
-                                         "streamed weight set (hidden layers 2.75 MB + the view, bone-direction and "
-                                         "live joints' windowed parts) is just over an XCD's 4 MB L2, so weight groups "
-                                         "are re-read from the 256 MB L3 (fp16x3's smaller set fits: ~0.7 GB); the "
+                                         "fabric-side bytes, which count Infinity-Cache (L3) hits. The fp16 modes' "
+                                         "per-net streamed weight set (two fp16 planes, 4 B per weight: hidden layers "
+                                         "1.8 MB + the view and encoder-fed parts) fits an XCD's 4 MB L2; bf16x6's "
+                                         "(three bf16 planes, 6 B per weight: 2.75 MB + the rest) is just over it, so "
+                                         "its weight groups are re-read from the 256 MB L3 (5-5.6 GB per frame); the "
                                          "bytes a render call must move are unique_bytes_per_step + ~8 MB of weights",
                          "unique_bytes_per_step": int(n_mine * (4 * 11 + 4 * 10) + (n_mine * (S + I) * 4 * 2 if I > 0 else 0)),
                          "kernel_ms": round(kern_ms, 3),
@@ -602,7 +610,8 @@ def main():
                          "required": "the FLOPs an exact fp32 implementation must do after exact-zero cutoff-window "
                                      "skipping and the feature_linear fusion (the fp32 mode's MFMA tally of the same "
                                      "rays x 4096 FLOP) / kernel_ms / peak: why fp32's algorithmic frac exceeds 1",
-                         "mfma_tally": "kernel-side tally of issued MFMA instructions (agrees with PMC SQ_INSTS_MFMA)",
+                         "mfma_tally": "kernel-side tally of issued MFMA instructions (agrees with PMC SQ_INSTS_MFMA); "
+                                       "mfma_bf16_per_step counts the 32x32x16 16-bit MFMAs (bf16 or f16, same rate)",
                          "mfma_f32_per_step": n_f32, "mfma_bf16_per_step": n_bf16,
                          "mfma_f32_required_per_step": req_f32,
                          "reference_flop_per_ray": flop_ray},

@@ -86,8 +86,14 @@ enum {
  *                     the dropped x1 w1 ~2^-22 of |x w|): half of bf16x6's MFMAs, 22-bit instead of
  *                     24-bit operands;
  *                     bone-direction parts and (widths 128 / 256) the windowed parts of layer 0 and the
- *                     skip layer as in bf16x6 (fp32 at width 64); encoder and heads fp32. */
-enum { ANERF_PREC_FP32 = 0, ANERF_PREC_BF16X3 = 1, ANERF_PREC_BF16X6 = 2, ANERF_PREC_FP16X3 = 3 };
+ *                     skip layer as in bf16x6 (fp32 at width 64); encoder and heads fp32;
+ *   ANERF_PREC_FP16X4 fp16x3 plus the fourth product x1 w1: the contraction is then (x - r_x)(w - r_w)
+ *                     with the split remainders |r_x| <= 2^-23 |x|, |r_w| <= 2^-23 |w|, within ~2^-22 of
+ *                     |x w| per product — the bound of bf16x6's dropped terms (x1 w2 + x2 w1 + x2 w2 and
+ *                     the weights' third remainder, ~2^-22.2), so fp32-accurate like bf16x6, with four
+ *                     MFMAs per 16 k instead of six and two weight planes (4 B per weight) instead of
+ *                     three; everything else as fp16x3. */
+enum { ANERF_PREC_FP32 = 0, ANERF_PREC_BF16X3 = 1, ANERF_PREC_BF16X6 = 2, ANERF_PREC_FP16X3 = 3, ANERF_PREC_FP16X4 = 4 };
 /* Flags OR-ed into anerf_render_rays' precision argument (and anerf_train_samples' flags):
  *   ANERF_FLAG_LINDISP  sample linearly in inverse depth, z = 1 / (1/near (1 - t) + 1/far t)
  *                       (render_rays(lindisp=True), core/utils/ray_utils.py:223-226)

@@ -5,7 +5,8 @@
   gets the frame's own near / far, i.e. the chunk NaN fill of the whole frame, hazard H1).
 * Config 5 (1024^2): the north star's multi-GPU split — the ray list cut into
   distributed.chunk_ranges(n, 4096, 8) shards rendered separately and concatenated — is bit-identical
-  to the whole-frame render in the bf16x6, fp16x3 and fp32 precisions, and 20,000 evenly spaced rays
+  to the whole-frame render in the bf16x6, fp16x4, fp16x3 and fp32 precisions (and so is bench.py's
+  N > 1 split, 256-ray tiles dealt round-robin with near / far from the whole frame), and 20,000 evenly spaced rays
   (the bench's parity sample) match the oracle at 1e-4 (near-empty rays' disparity, H12: counted and
   bounded, see _oracle_check).  (The RCCL all-gather itself is covered by tests/test_distributed.py over gloo.)
 The oracle is pinned to the reference's golden fixtures (tests/test_oracle_golden.py).
@@ -86,7 +87,8 @@ def _oracle_check(cfg, ck, sc, cyls, rb, out, n_sample):
     print(f"near-empty rays (count, max disp error): {report}")
 
 
-@pytest.mark.parametrize("nj,precision", [(24, "bf16x6"), (24, "fp16x3"), (24, "fp32"), (65, "fp16x3"), (65, "bf16x6")])
+@pytest.mark.parametrize("nj,precision", [(24, "bf16x6"), (24, "fp16x4"), (24, "fp16x3"), (24, "fp32"), (65, "fp16x3"),
+                                          (65, "bf16x6"), (65, "fp16x4")])
 def test_full_frame_matches_oracle_on_8192_rays(nj, precision):
     seed = 13 if nj == 24 else 14
     sc, ck, cyls, rb = _frame(512, nj, seed, 79.6 if nj == 24 else 20.0)
@@ -97,7 +99,7 @@ def test_full_frame_matches_oracle_on_8192_rays(nj, precision):
     _oracle_check(cfg, ck, sc, cyls, rb, out, 8192)
 
 
-@pytest.mark.parametrize("W,precision", [(256, "bf16x6"), (128, "bf16x6"), (256, "fp16x3"), (128, "fp16x3")])
+@pytest.mark.parametrize("W,precision", [(256, "bf16x6"), (128, "bf16x6"), (256, "fp16x4"), (256, "fp16x3"), (128, "fp16x3")])
 def test_multires10_split_modes_match_oracle(W, precision):
     """--multires 10 at widths 128 / 256 in the split modes: the windowed k-streams run as bf16x6 with
     two k16-steps per joint (10 sin / cos terms + the distance input per lane half; v_part_x6), and
@@ -121,7 +123,7 @@ def test_multires10_split_modes_match_oracle(W, precision):
     _oracle_check(cfg, ck, sc, cyls, rb, out, 2048)
 
 
-@pytest.mark.parametrize("precision", ["bf16x6", "fp16x3", "fp32"])
+@pytest.mark.parametrize("precision", ["bf16x6", "fp16x4", "fp16x3", "fp32"])
 def test_config5_pixel_shards_are_bit_identical(precision):
     sc, ck, cyls, rb = _frame(1024, 24, 13, 79.6)
     n = rb.shape[0]
@@ -163,7 +165,39 @@ def test_config5_ray_balanced_shards_are_bit_identical():
         assert torch.equal(torch.cat([p[k] for p in parts], 0), whole[k]), k
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16x6", "fp16x3"])
+@pytest.mark.parametrize("precision", ["fp16x4", "bf16x6"])
+def test_config5_tile_shards_are_bit_identical(precision):
+    """The split bench.py runs at N > 1 (distributed.tile_rows: 256-ray tiles dealt round-robin over 8
+    ranks, near / far from the whole frame's 4096-ray chunks, ANERF_FLAG_NEAR_FAR): every rank's rays
+    rendered on their own and put back in frame order equal the whole-frame render bit for bit."""
+    near_far = importlib.import_module("a-nerf_amd.raycaster").near_far
+    sc, ck, cyls, rb = _frame(1024, 24, 13, 79.6)
+    n = rb.shape[0]
+    cfg = anerf.RenderConfig(N_samples=64, N_importance=128, precision=precision).validate()
+    rc = anerf.RayCaster(cfg, ck)
+    whole = _render(rc, rb, sc, cyls)
+    cy = torch.from_numpy(cyls[0:1]).cuda()
+    sk = torch.from_numpy(sc["skts"][0:1]).cuda()
+    rbn = rb.clone()
+    near_far(rbn, cy, chunk=4096, out=(rbn[:, 6], rbn[:, 7]))
+    got = {k: torch.full_like(v, float("nan")) for k, v in whole.items()}
+    seen = torch.zeros(n, dtype=torch.int32)
+    for r in range(8):
+        rows = dmod.tile_rows(n, 8, r, 256)
+        seen[rows] += 1
+        mine = rbn[rows.cuda()]
+        m = mine.shape[0]
+        out = rc.render_rays(mine, 64, skts=sk.expand(m, -1, -1, -1), cyls=cy.expand(m, -1), N_importance=128,
+                             chunk=4096, ret_alpha=False, near_far_given=True)
+        for k in got:
+            got[k][rows.cuda()] = out[k]
+    torch.cuda.synchronize()
+    assert bool((seen == 1).all())
+    for k in ("rgb_map", "disp_map", "acc_map", "rgb0", "disp0", "acc0"):
+        assert torch.equal(got[k].nan_to_num(7.0), whole[k].nan_to_num(7.0)), k
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16x6", "fp16x4", "fp16x3"])
 def test_near_empty_rays_against_the_reference(precision):
     """Hazard H12 against the REFERENCE (tests/golden/h12_nearempty_c5.npz: config 5's near-empty rays,
     0 < acc < 2^-20, and 64 ordinary rays, rendered by core.raycasters.render_rays with the frame's

@@ -394,7 +394,7 @@ def test_density_matches_oracle_both_nets_and_ragged():
     assert empty.shape == (0, 1)
 
 
-@pytest.mark.parametrize("precision", ["bf16x6", "fp16x3", "bf16x3"])
+@pytest.mark.parametrize("precision", ["bf16x6", "fp16x4", "fp16x3", "bf16x3"])
 def test_density_split_precisions(precision):
     """Density queries in the split modes: the reference goldens within 1e-4 and the fp32 path
     within 2e-6 (bf16x6, fp32-accurate products; fp16x3, 22-bit operands) / 5e-5 (bf16x3) on the
@@ -489,7 +489,7 @@ def test_render_rays_bf16x3_matches_reference_golden(name):
             assert np.quantile(dd, 0.999) <= 2e-5, f"{name} {k}: bf16x3 vs fp32"
 
 
-@pytest.mark.parametrize("precision", ["bf16x6", "fp16x3"])
+@pytest.mark.parametrize("precision", ["bf16x6", "fp16x4", "fp16x3"])
 @pytest.mark.parametrize("name", NAMES)
 def test_render_rays_split_matches_reference_golden(name, precision):
     """ANERF_PREC_BF16X6 (three-way split-bf16 hidden layers, fp32-accurate products) and
@@ -509,7 +509,7 @@ def test_render_rays_split_matches_reference_golden(name, precision):
             assert np.quantile(dd, 0.999) <= 1e-5, f"{name} {k}: {precision} vs fp32 {np.quantile(dd, 0.999):.3e}"
 
 
-@pytest.mark.parametrize("precision,per_block", [("bf16x6", 12), ("fp16x3", 6)])
+@pytest.mark.parametrize("precision,per_block", [("bf16x6", 12), ("fp16x4", 8), ("fp16x3", 6)])
 def test_split_modes_execute_16bit_mfmas(precision, per_block):
     g = Golden("c3_512_s64i128_d8w256")
     rc = _caster_prec(g, precision)
@@ -519,7 +519,7 @@ def test_split_modes_execute_16bit_mfmas(precision, per_block):
     _render(rc32, g, g.ray_batch()[:64], count_mfma=True)
     f32_only = int(rc32.last_mfma[0].item())
     # per 32-sample block (W 256: RB 8, RBV 4, 7 hidden layers, NJH2 12, skip layer present):
-    #   hidden 32x32 blocks: 16 f32 MFMAs (k = 2) -> 2 k16-steps x 6 (bf16x6) or x 3 (fp16x3)
+    #   hidden 32x32 blocks: 16 f32 MFMAs (k = 2) -> 2 k16-steps x 6 (bf16x6), x 4 (fp16x4) or x 3 (fp16x3)
     #   fused view layer (128 x 256): 64 x 4 f32 -> 4 x 8 x per_block
     #   two bone-direction x parts (36 features, bf16x6 in both modes): 36 x 8 f32 -> ceil(36 / 8) x 8 x 6
     # and per live joint of a block, two windowed x parts (16 features, bf16x6 in both modes):
@@ -550,7 +550,7 @@ def test_bf16x3_executes_bf16_mfmas():
     assert (f32_only - n_f32) * 6 == n_bf16 * 16
 
 
-@pytest.mark.parametrize("precision", ["bf16x6", "fp16x3"])
+@pytest.mark.parametrize("precision", ["bf16x6", "fp16x4", "fp16x3"])
 def test_ragged_workgroups_split_modes(precision):
     """bf16x6's block loop runs the same trip count on every wave (a workgroup barrier per hidden
     layer); a wave past its workgroup's last block redoes it without storing or counting.  Ragged

@@ -8,7 +8,7 @@ import os
 import sys
 
 
-PREC_TEMPLATE = {"fp32": 0, "bf16x3": 1, "bf16x6": 2, "fp16x3": 3}
+PREC_TEMPLATE = {"fp32": 0, "bf16x3": 1, "bf16x6": 2, "fp16x3": 3, "fp16x4": 4}
 
 
 def rows(path, kernel="render_kernel"):
