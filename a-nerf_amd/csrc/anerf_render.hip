@@ -408,10 +408,10 @@ int anerf_render_rays(const anerf_model* m, const float* ray_batch, int32_t ray_
     unsigned grid = (unsigned)((n_rays + R - 1) / R);
     unsigned* queues = reinterpret_cast<unsigned*>((char*)workspace + ws_near_far_bytes(n_rays) +
                                                    ws_zf_bytes(n_rays, S, I));
-    if (ANERF_PERSIST) {  // one workgroup per CU, the items from the band queues (render_kernel)
-        int dev = 0, ncu = 256;
+    int ncu = 256;  // ANERF_PERSIST: as many workgroups as fit on the chip at once, items from the band queues
+    if (ANERF_PERSIST) {
+        int dev = 0;
         if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-        grid = std::min<unsigned>(grid, (unsigned)ncu);
         HIP_TRY(hipMemsetAsync(queues, 0, 2 * 8 * sizeof(unsigned), st));
     }
     const size_t lds_bytes = (size_t)P.total * 4;
@@ -424,11 +424,18 @@ int anerf_render_rays(const anerf_model* m, const float* ray_batch, int32_t ray_
                  : precision == ANERF_PREC_FP16X4 ? render_kernel<WW, MM, 4> : render_kernel<WW, MM, 0>; \
         HIP_TRY(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,  \
                                     (int)lds_bytes));                                               \
+        unsigned g = grid;                                                                          \
+        if (ANERF_PERSIST) {                                                                        \
+            int nb = 1;                                                                             \
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kfn, 256, lds_bytes) != hipSuccess || nb < 1) \
+                nb = 1;                                                                             \
+            g = std::min<unsigned>(grid, (unsigned)(ncu * nb));                                     \
+        }                                                                                           \
         for (int p0 = 0; p0 < 2; p0 += pstep) {                                                     \
             a.pass0 = p0;                                                                           \
             a.pass1 = p0 + pstep;                                                                   \
             a.queue = queues + 8 * p0;                                                              \
-            hipLaunchKernelGGL(kfn, dim3(grid), dim3(256), lds_bytes, st, m->md, a, P);            \
+            hipLaunchKernelGGL(kfn, dim3(g), dim3(256), lds_bytes, st, m->md, a, P);               \
         }                                                                                           \
     } while (0)
     if (W == 256 && mr == 7) ANERF_LAUNCH(256, 7);
