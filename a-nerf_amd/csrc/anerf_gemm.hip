@@ -57,6 +57,10 @@ constexpr int BM = 128, BN = 128, NTHR = 256;
 #ifndef ANERF_GEMM_BM
 #define ANERF_GEMM_BM 128
 #endif
+// B-fragment ring depth of the single-segment forward / input-gradient instances (2 or 4)
+#ifndef ANERF_GEMM_BD
+#define ANERF_GEMM_BD 4
+#endif
 constexpr int MAXSEG = 3;
 
 struct SegD {
@@ -305,29 +309,38 @@ __global__ __launch_bounds__(NTHR, 256 / TBM) void mlp_nt_kernel(NTArgs g) {
             __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
         }
     };
+    // B fragments (the split weights, L2-resident) in a ring of BD k16-steps, prefetched BD - 1 steps
+    // ahead: the waves' SQ counters showed them parked at s_waitcnt 45 % of the time with the B loads
+    // one k16-step (12 MFMAs) ahead of their use (profiles/r04l_pmc_waves.txt); two more register sets
+    // fit the single-segment instances (ANERF_GEMM_BD; the multi-segment ones keep the 2-ring)
+    constexpr int BD = (NSEG == 1 && ANERF_GEMM_BD == 4) ? 4 : 2;
     RA R0, R1;
-    BF f0, f1;
+    BF f[BD];
     fetch_a(0, R0);
     fetch_a(1, R1);
-    fetch_b(0, f0);
+#pragma unroll
+    for (int j = 0; j < BD - 1; ++j) fetch_b(j, f[j]);
     __builtin_amdgcn_sched_barrier(0);
     stage_a(0, R0);
     __syncthreads();
     // (sched_barrier after every fetch: without it the scheduler sinks the loads to their first use
     // to save registers, and each then waits out its full round trip)
+    // k16-step q0 + j of this iteration (j = 0..3: buffer j >> 1, half j & 1) uses f[j % BD] and first
+    // fetches step q0 + j + BD - 1 into the slot the previous step freed
     for (int st = 0; st < nst; st += 2) {
+        const int q0 = 2 * st;
         fetch_a(st + 2, R0);
         __builtin_amdgcn_sched_barrier(0);
-        fetch_b(2 * st + 1, f1);
+        fetch_b(q0 + BD - 1, f[(BD - 1) % BD]);
         __builtin_amdgcn_sched_barrier(0);
-        step(0, 0, f0);
+        step(0, 0, f[0]);
         __builtin_amdgcn_sched_barrier(0);
-        fetch_b(2 * st + 2, f0);
+        fetch_b(q0 + BD, f[BD % BD]);
         __builtin_amdgcn_sched_barrier(0);
         if (ANERF_GEMM_IL && st + 1 < nst) {
-            step_stage(0, f1, 1, R1);
+            step_stage(0, f[1 % BD], 1, R1);
         } else {
-            step(0, 1, f1);
+            step(0, 1, f[1 % BD]);
             __builtin_amdgcn_sched_barrier(0);
             if (st + 1 < nst) stage_a(1, R1);
         }
@@ -335,16 +348,16 @@ __global__ __launch_bounds__(NTHR, 256 / TBM) void mlp_nt_kernel(NTArgs g) {
         if (st + 1 >= nst) break;
         fetch_a(st + 3, R1);
         __builtin_amdgcn_sched_barrier(0);
-        fetch_b(2 * st + 3, f1);
+        fetch_b(q0 + BD + 1, f[(BD + 1) % BD]);
         __builtin_amdgcn_sched_barrier(0);
-        step(1, 0, f0);
+        step(1, 0, f[2 % BD]);
         __builtin_amdgcn_sched_barrier(0);
-        fetch_b(2 * st + 4, f0);
+        fetch_b(q0 + BD + 2, f[(BD + 2) % BD]);
         __builtin_amdgcn_sched_barrier(0);
         if (ANERF_GEMM_IL && st + 2 < nst) {
-            step_stage(1, f1, 0, R0);
+            step_stage(1, f[3 % BD], 0, R0);
         } else {
-            step(1, 1, f1);
+            step(1, 1, f[3 % BD]);
             __builtin_amdgcn_sched_barrier(0);
             if (st + 2 < nst) stage_a(0, R0);
         }

@@ -5,6 +5,7 @@ GRBM_GUI_ACTIVE x 4 SIMDs per CU, MI355X_MICROARCH.md units: SQ_WAVE_CYCLES / SQ
 quad-cycles, SQ_VALU_MFMA_BUSY_CYCLES in cycles, summed over the chip's 256 CUs; GRBM_GUI_ACTIVE per
 XCD).  Usage: python tools/pmc_waves.py DIR ..."""
 import csv
+import re
 import glob
 import os
 import sys
@@ -14,7 +15,8 @@ def kernels(d):
     f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     out = {}
     for r in csv.DictReader(open(f[0])):
-        k = r["Kernel_Name"].split("(")[0][:60]
+        k = re.sub(r"\(anonymous namespace\)::", "", r["Kernel_Name"])
+        k = re.sub(r"^void ", "", k).split("(")[0][:60]
         e = out.setdefault(k, {"n": set(), "ns": 0})
         if r["Dispatch_Id"] not in e["n"]:
             e["n"].add(r["Dispatch_Id"])
