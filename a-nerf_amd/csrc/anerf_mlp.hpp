@@ -479,6 +479,10 @@ __device__ __forceinline__ void split2_pair(float a, float b, float t, H3T& T, i
 
 __device__ __forceinline__ void split2_block_pair(const f32x16& hb, float t, H3T (&T)[2], int p) {
     const int s = p >> 2, q = p & 3;
+#if ANERF_X6_PROBE == 2  // (diagnostic builds of tools/probe only: no split arithmetic)
+    T[s].d[0][q] = T[s].d[1][q] = __builtin_bit_cast(unsigned, hb[8 * s + 2 * q]);
+    return;
+#endif
     split2_pair(hb[8 * s + 2 * q], hb[8 * s + 2 * q + 1], t, T[s], q);
 }
 
@@ -551,7 +555,11 @@ __device__ __forceinline__ void mlp_layer_h3(f32x16 (&out)[RBO], f32x16 (&ain)[R
     const int hh = lane >> 5;
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(wp);
     const __amdgpu_buffer_rsrc_t rn = make_rsrc(next ? next : wp);
+#if ANERF_X6_PROBE == 4  // (diagnostic builds of tools/probe only: no per-sample scale)
+    const float t = 1.0f;
+#else
     const float t = h3_scale<RBI>(ain, es, ew, top);
+#endif
     const float S = pow2f(es);
     auto convert_half = [&](int rb, int half) {  // relu of 8 inputs (+ their 8 scaled bias outputs)
 #pragma unroll
@@ -582,6 +590,9 @@ __device__ __forceinline__ void mlp_layer_h3(f32x16 (&out)[RBO], f32x16 (&ain)[R
     // last slot again without one: harmless; unconditional loads keep the counted vmcnt waits exact)
     const bool has_next = next != nullptr;
     auto prefetch = [&](int g) {
+#if ANERF_X6_PROBE == 1  // (diagnostic builds of tools/probe only: no weight loads)
+        return;
+#endif
         if (g & 1) return;
         const int G = g >> 1;
         if (G + PS < NS)
