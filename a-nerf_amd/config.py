@@ -136,7 +136,8 @@ class RenderConfig:
                   init_freq=float(g("init_freq", 0.0) or 0.0), freq_schedule_step=int(g("freq_schedule_step", 5) or 5),
                   cut_to_dist=bool(g("cut_to_dist", False)), cutoff_shift=bool(g("cutoff_shift", False)),
                   normalize_cutoff=bool(g("normalize_cutoff", False)), cutoff_bones=bool(g("cutoff_bones", False)),
-                  chunk=g("chunk", 4096), ext_scale=g("ext_scale", 0.001), extra=extra)
+                  chunk=g("chunk", 4096), ext_scale=g("ext_scale", 0.001), extra=extra,
+                  precision=g("anerf_precision", "fp32") or "fp32")  # (not a reference flag: opt-in mode)
         return cfg.validate()
 
 

@@ -113,6 +113,23 @@ def test_config_lindisp_from_args():
     assert not config.RenderConfig.from_args(types.SimpleNamespace(), 24).lindisp
 
 
+def test_precision_modes_plumbing():
+    """Every precision mode the C header declares is selectable from Python (RenderConfig, the
+    `anerf_precision` attribute of a run_nerf namespace) and maps to the header's enum value."""
+    import re
+    lib = importlib.import_module("a-nerf_amd._lib")
+    hdr = open(os.path.join(os.path.dirname(HERE), "include", "anerf.h")).read()
+    enum = dict((k.lower(), int(v)) for k, v in re.findall(r"ANERF_PREC_(\w+) = (\d+)", hdr))
+    assert enum == {"fp32": 0, "bf16x3": 1, "bf16x6": 2, "fp16x3": 3, "fp16x4": 4}
+    assert lib.PRECISIONS == enum
+    for p in enum:
+        assert config.RenderConfig(precision=p).validate().precision == p
+        assert config.RenderConfig.from_args(types.SimpleNamespace(anerf_precision=p), 24).precision == p
+    assert config.RenderConfig.from_args(types.SimpleNamespace(), 24).precision == "fp32"
+    with pytest.raises(ValueError, match="precision"):
+        config.RenderConfig(precision="fp16x5").validate()
+
+
 def test_config_from_args_matches_surreal_config():
     args = types.SimpleNamespace(netdepth=8, netwidth=256, multires=7, multires_views=4, use_cutoff=True,
                                  cutoff_inputs=True, cutoff_viewdir=True, use_viewdirs=True, N_samples=64,
