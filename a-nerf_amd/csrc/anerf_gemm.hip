@@ -197,7 +197,11 @@ __global__ __launch_bounds__(NTHR, 256 / TBM) void mlp_nt_kernel(NTArgs g) {
 #pragma unroll
     for (int sg = 0; sg < NSEG; ++sg) {
         const long long ld = g.a[sg].ld;
+#ifdef ANERF_GEMM_PROBE_A  // (timing diagnostic only, wrong results: every tile reads rows 0..127, L2-hot)
+        ars[sg] = __builtin_amdgcn_make_buffer_rsrc((void*)(g.a[sg].p), 0, (int)(rows * ld * 4), 0x00020000);
+#else
         ars[sg] = __builtin_amdgcn_make_buffer_rsrc((void*)(g.a[sg].p + m0 * ld), 0, (int)(rows * ld * 4), 0x00020000);
+#endif
         arow[sg] = (unsigned)(sr * ld * 4);
         astep[sg] = (unsigned)(32 * ld * 4);
         ast[sg] = g.a[sg].start;
