@@ -245,3 +245,39 @@ def test_near_empty_rays_against_the_reference(precision):
     assert margin[ne].max() <= 0.0, (int(np.argmax(np.where(ne, margin, -1))), float(margin[ne].max()))
     assert dd[ne].max() <= TOL + own[ne].max()
 
+
+
+@pytest.mark.parametrize("precision", ["fp16x4", "fp16x3", "bf16x6", "fp32"])
+def test_power_of_two_rescaled_hidden_layers_render_identically(precision):
+    """relu is positively homogeneous, so scaling hidden layer i's outputs by s_i (its weights' h columns
+    by s_i / s_(i-1), the skip layer's x columns and every bias by s_i, the heads by 1 / s_7) leaves the
+    network's function unchanged; with powers of two (2^-14 .. 2^15 here) every fp32 product and sum is
+    the same up to the exponent.  The fp16 modes scale each sample's activations into [2^10, 2^11) and
+    each layer's weights by a power of two, so they must absorb the factors exactly too: all modes render
+    the rescaled checkpoint bit-identically to the original (this pins the fp16 range handling at
+    activations far outside fp16's own range)."""
+    sc, ck, cyls, rb = _frame(512, 24, 13, 79.6)
+    rb = rb[::97].contiguous()
+    s = [1.0, 2.0 ** 12, 2.0 ** -9, 2.0 ** 15, 2.0 ** -14, 2.0 ** 10, 2.0 ** -6, 2.0 ** 13]
+    skip = 4
+    ck2 = {k: (dict(v) if isinstance(v, dict) else v) for k, v in ck.items()}
+    for net in ("network_fn_state_dict", "network_fine_state_dict"):
+        sd = {k: np.array(v, copy=True) for k, v in ck[net].items()}
+        for i in range(1, 8):
+            w, b = sd[f"pts_linears.{i}.weight"], sd[f"pts_linears.{i}.bias"]
+            if i == skip + 1:  # [x | h] input (core/networks/nerf.py: cat([input_pts, h]))
+                nx = w.shape[1] - 256
+                w[:, :nx] *= np.float32(s[i])
+                w[:, nx:] *= np.float32(s[i] / s[i - 1])
+            else:
+                w *= np.float32(s[i] / s[i - 1])
+            b *= np.float32(s[i])
+        for k in ("alpha_linear.weight", "feature_linear.weight"):
+            sd[k] *= np.float32(1.0 / s[7])
+        ck2[net] = {k: torch.from_numpy(v) if isinstance(ck[net][k], torch.Tensor) else v for k, v in sd.items()}
+    cfg = anerf.RenderConfig(N_samples=64, N_importance=128, precision=precision).validate()
+    a = _render(anerf.RayCaster(cfg, ck), rb, sc, cyls)
+    b2 = _render(anerf.RayCaster(cfg, ck2), rb, sc, cyls)
+    torch.cuda.synchronize()
+    for k in ("rgb_map", "disp_map", "acc_map", "rgb0", "disp0", "acc0"):
+        assert torch.equal(a[k].nan_to_num(7.0), b2[k].nan_to_num(7.0)), (k, float((a[k] - b2[k]).abs().max()))
