@@ -48,8 +48,10 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int BM = 128, BN = 128, NTHR = 256;
-#ifndef ANERF_GEMM_IL
-#define ANERF_GEMM_IL 0  // (measured neutral: profiles/r04i_gemm_interleave_ab.txt)
+// k columns per step of the bf16x3 single-segment forward / input-gradient instances: 32, or 64
+// (half the barriers, twice the A bytes in flight; experiment switch)
+#ifndef ANERF_GEMM_SK64
+#define ANERF_GEMM_SK64 0
 #endif
 // forward / input gradient row-tile height (experiment switch): 128 rows, two workgroups per CU; or 64
 // rows, four per CU (half the accumulators, LDS and epilogue per workgroup: more tiles in flight to
@@ -133,17 +135,23 @@ __device__ __forceinline__ f32x16 mfma(const bf16x8& a, const bf16x8& b, const f
 // output segments); with two workgroups per CU one's epilogue and prologue overlap the other's MFMAs.
 constexpr int BNW = 256;      // row padding of the split weights (whole 256-row tiles)
 constexpr int NBN = 128;      // output columns per workgroup
-constexpr int SK = 32;        // k columns per step
-// LDS planes [row][32 k] bf16, 64 B rows, the four 16 B chunks of a row XOR-swizzled by bits 2-3 of
-// the row: fragment reads (ds_read_b128, 16 rows x one chunk per lane group) and staging writes
-// (ds_write_b64, two rows per 16-lane group) are both conflict-free
-__device__ __forceinline__ int nt_off(int row, int k) { return row * SK + ((((k >> 3) ^ (row >> 2)) & 3) << 3) + (k & 7); }
+// LDS planes [row][SKT k] bf16.  SKT 32: 64 B rows, the four 16 B chunks of a row XOR-swizzled by bits
+// 2-3 of the row; SKT 64: 128 B rows, the eight chunks swizzled by bits 1-3.  Fragment reads
+// (ds_read_b128, 16 rows x one chunk per lane group) and staging writes (ds_write_b64, whole rows per
+// 16-lane group) are both conflict-free
+template <int SKT>
+__device__ __forceinline__ int nt_off(int row, int k) {
+    if constexpr (SKT == 32) return row * 32 + ((((k >> 3) ^ (row >> 2)) & 3) << 3) + (k & 7);
+    return row * 64 + ((((k >> 3) ^ (row >> 1)) & 7) << 3) + (k & 7);
+}
 constexpr unsigned NOOB = 0x80000000u;  // a lane offset past every descriptor's range
 
-template <int NPL, int TBM>
+template <int NPL, int TBM, int SKT = 32>
 struct NTGeo {
     static constexpr int RBM = TBM / 32;               // 32-row blocks per tile
-    static constexpr int PLANE = TBM * SK;             // bf16 elements
+    static constexpr int RPS = 1024 / SKT;             // rows per staging pass (256 threads x 4 columns)
+    static constexpr int NRS = TBM / RPS;              // staging passes per step
+    static constexpr int PLANE = TBM * SKT;            // bf16 elements
     static constexpr int STAGE = NPL * PLANE;
     static constexpr int STAGES_BYTES = 2 * STAGE * 2;
     static constexpr int TILE_BYTES = TBM * 132 * 4;  // epilogue tile [TBM][132] fp32
@@ -161,10 +169,10 @@ struct SegTab {
     int accum[MAXSEG];
 };
 
-template <int NPL, int NSEG, int TBM>
+template <int NPL, int NSEG, int TBM, int SKT = 32>
 __global__ __launch_bounds__(NTHR, 256 / TBM) void mlp_nt_kernel(NTArgs g) {
-    using G = NTGeo<NPL, TBM>;
-    constexpr int RBM = G::RBM;
+    using G = NTGeo<NPL, TBM, SKT>;
+    constexpr int RBM = G::RBM, NRS = G::NRS, SK = SKT, KK = SKT / 16;
     extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
     const int logical = xcd_logical(blockIdx.x, g.total);
     const int mt = logical / g.tiles_n, nt = logical % g.tiles_n;
@@ -186,9 +194,10 @@ __global__ __launch_bounds__(NTHR, 256 / TBM) void mlp_nt_kernel(NTArgs g) {
         tab->ldm[tid] = g.c[u].ldm;
         tab->accum[tid] = g.c[u].accum;
     }
-    // staging: rows sr + 32 i (i = 0..3), columns sc .. sc + 3 of the step; a wave instruction reads
-    // 8 rows x 128 B
-    const int sr = tid >> 3, sc = 4 * (tid & 7);
+    // staging: rows sr + RPS i (i < NRS), columns sc .. sc + 3 of the step; a wave instruction reads
+    // 8 rows x 128 B (SKT 32) or 4 rows x 256 B (SKT 64)
+    constexpr int RPS = G::RPS;
+    const int sr = tid / (SKT / 4), sc = 4 * (tid % (SKT / 4));
     const long long rows_left = Md - m0;
     const int rows = rows_left < TBM ? (int)rows_left : TBM;
     __amdgpu_buffer_rsrc_t ars[NSEG];
@@ -203,7 +212,7 @@ __global__ __launch_bounds__(NTHR, 256 / TBM) void mlp_nt_kernel(NTArgs g) {
         ars[sg] = __builtin_amdgcn_make_buffer_rsrc((void*)(g.a[sg].p + m0 * ld), 0, (int)(rows * ld * 4), 0x00020000);
 #endif
         arow[sg] = (unsigned)(sr * ld * 4);
-        astep[sg] = (unsigned)(32 * ld * 4);
+        astep[sg] = (unsigned)(RPS * ld * 4);
         ast[sg] = g.a[sg].start;
         alim[sg] = g.a[sg].start + (g.a[sg].cols + 3) / 4 * 4;
     }
@@ -226,7 +235,7 @@ __global__ __launch_bounds__(NTHR, 256 / TBM) void mlp_nt_kernel(NTArgs g) {
         for (int p = 0; p < NPL; ++p) f.v[p] = *reinterpret_cast<const u32x4*>(bk + p * 512);
     };
     struct RA {
-        f32x4 v[RBM][NSEG];
+        f32x4 v[NRS][NSEG];
     };
     // (steps past K read nothing: every column is outside every segment)
     auto fetch_a = [&](int st, RA& R) {
@@ -235,15 +244,15 @@ __global__ __launch_bounds__(NTHR, 256 / TBM) void mlp_nt_kernel(NTArgs g) {
         for (int sg = 0; sg < NSEG; ++sg) {
             const unsigned vo = col >= ast[sg] && col < alim[sg] ? arow[sg] + (unsigned)(col - ast[sg]) * 4u : NOOB;
 #pragma unroll
-            for (int i = 0; i < RBM; ++i)
+            for (int i = 0; i < NRS; ++i)
                 R.v[i][sg] = __builtin_bit_cast(
                     f32x4, __builtin_amdgcn_raw_buffer_load_b128(ars[sg], vo + (unsigned)i * astep[sg], 0, 0));
         }
     };
     auto stage_a = [&](int buf, const RA& R) {
-        unsigned short* const P = lds + buf * G::STAGE + nt_off(sr, sc);  // (row sr + 32 i: same swizzle)
+        unsigned short* const P = lds + buf * G::STAGE + nt_off<SKT>(sr, sc);  // (row sr + RPS i: same swizzle)
 #pragma unroll
-        for (int i = 0; i < RBM; ++i) {
+        for (int i = 0; i < NRS; ++i) {
             float v[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -270,7 +279,7 @@ __global__ __launch_bounds__(NTHR, 256 / TBM) void mlp_nt_kernel(NTArgs g) {
                     }
                 }
                 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-                *reinterpret_cast<u32x2*>(P + p * G::PLANE + 32 * i * SK) = u32x2{w[0], w[1]};
+                *reinterpret_cast<u32x2*>(P + p * G::PLANE + RPS * i * SK) = u32x2{w[0], w[1]};
             }
         }
     };
@@ -282,7 +291,7 @@ __global__ __launch_bounds__(NTHR, 256 / TBM) void mlp_nt_kernel(NTArgs g) {
         for (int i = 0; i < RBM; ++i)
 #pragma unroll
             for (int p = 0; p < NPL; ++p)
-                a[p][i] = *reinterpret_cast<const bf16x8*>(A + p * G::PLANE + nt_off(32 * i + r, kh));
+                a[p][i] = *reinterpret_cast<const bf16x8*>(A + p * G::PLANE + nt_off<SKT>(32 * i + r, kh));
 #pragma unroll
         for (int p = 0; p < NPL; ++p) b[p] = __builtin_bit_cast(bf16x8, f.v[p]);
 #pragma unroll
@@ -296,21 +305,6 @@ __global__ __launch_bounds__(NTHR, 256 / TBM) void mlp_nt_kernel(NTArgs g) {
             c = mfma(a[1][i], b[0], c);
             c = mfma(a[0][i], b[1], c);
             acc[i] = mfma(a[0][i], b[0], c);
-        }
-    };
-    // step kk = 1 of a buffer with the staging of the next step's A tile interleaved into its MFMAs
-    // (one MFMA, then up to VS VALU and one LDS write): the split and the ds_writes run in the MFMA
-    // gaps instead of after the last MFMA (ANERF_GEMM_IL; 0 = the two one after the other)
-    auto step_stage = [&](int buf, const BF& f, int sbuf, const RA& R) {
-        step(buf, 1, f);
-        stage_a(sbuf, R);
-        constexpr int NM = RBM * (NPL == 3 ? 6 : 3), VS = NPL == 3 ? 3 : 4;
-        __builtin_amdgcn_sched_group_barrier(0x100, RBM * NPL, 0);  // the fragment reads first
-#pragma unroll
-        for (int i = 0; i < NM; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, VS, 0);
-            __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
         }
     };
     // B fragments (the split weights, L2-resident) in a ring of BD k16-steps, prefetched BD - 1 steps
@@ -329,42 +323,32 @@ __global__ __launch_bounds__(NTHR, 256 / TBM) void mlp_nt_kernel(NTArgs g) {
     __syncthreads();
     // (sched_barrier after every fetch: without it the scheduler sinks the loads to their first use
     // to save registers, and each then waits out its full round trip)
-    // k16-step q0 + j of this iteration (j = 0..3: buffer j >> 1, half j & 1) uses f[j % BD] and first
-    // fetches step q0 + j + BD - 1 into the slot the previous step freed
+    // k16-step q0 + j of an iteration (j < 2 KK: buffer j / KK, half j % KK) uses f[j % BD] (BD divides
+    // 2 KK) and first fetches step q0 + j + BD - 1 into the slot the previous step freed
     for (int st = 0; st < nst; st += 2) {
-        const int q0 = 2 * st;
+        const int q0 = KK * st;
         fetch_a(st + 2, R0);
         __builtin_amdgcn_sched_barrier(0);
-        fetch_b(q0 + BD - 1, f[(BD - 1) % BD]);
-        __builtin_amdgcn_sched_barrier(0);
-        step(0, 0, f[0]);
-        __builtin_amdgcn_sched_barrier(0);
-        fetch_b(q0 + BD, f[BD % BD]);
-        __builtin_amdgcn_sched_barrier(0);
-        if (ANERF_GEMM_IL && st + 1 < nst) {
-            step_stage(0, f[1 % BD], 1, R1);
-        } else {
-            step(0, 1, f[1 % BD]);
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk) {
+            fetch_b(q0 + kk + BD - 1, f[(kk + BD - 1) % BD]);
             __builtin_amdgcn_sched_barrier(0);
-            if (st + 1 < nst) stage_a(1, R1);
+            step(0, kk, f[kk % BD]);
+            __builtin_amdgcn_sched_barrier(0);
         }
+        if (st + 1 < nst) stage_a(1, R1);
         __syncthreads();
         if (st + 1 >= nst) break;
         fetch_a(st + 3, R1);
         __builtin_amdgcn_sched_barrier(0);
-        fetch_b(q0 + BD + 1, f[(BD + 1) % BD]);
-        __builtin_amdgcn_sched_barrier(0);
-        step(1, 0, f[2 % BD]);
-        __builtin_amdgcn_sched_barrier(0);
-        fetch_b(q0 + BD + 2, f[(BD + 2) % BD]);
-        __builtin_amdgcn_sched_barrier(0);
-        if (ANERF_GEMM_IL && st + 2 < nst) {
-            step_stage(1, f[3 % BD], 0, R0);
-        } else {
-            step(1, 1, f[3 % BD]);
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk) {
+            fetch_b(q0 + KK + kk + BD - 1, f[(KK + kk + BD - 1) % BD]);
             __builtin_amdgcn_sched_barrier(0);
-            if (st + 2 < nst) stage_a(0, R0);
+            step(1, kk, f[(KK + kk) % BD]);
+            __builtin_amdgcn_sched_barrier(0);
         }
+        if (st + 2 < nst) stage_a(0, R0);
         __syncthreads();
     }
     // epilogue through LDS: the waves write their accumulators (lane = column (lane & 31), registers
@@ -845,10 +829,10 @@ int planes_of(int precision) { return precision == ANERF_MLP_BF16X6 ? 3 : (preci
 
 // the dynamic LDS (up to 67 KB) is above the default limit: raised once per kernel instance
 // (set on every call: the attribute belongs to the current device, and a cached failure would stick)
-template <int NPL, int NSEG, int TBM>
+template <int NPL, int NSEG, int TBM, int SKT>
 hipError_t nt_attr() {
-    return hipFuncSetAttribute((const void*)mlp_nt_kernel<NPL, NSEG, TBM>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               NTGeo<NPL, TBM>::LDS_BYTES);
+    return hipFuncSetAttribute((const void*)mlp_nt_kernel<NPL, NSEG, TBM, SKT>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, NTGeo<NPL, TBM, SKT>::LDS_BYTES);
 }
 template <int NPL, int NSEG>
 hipError_t tn_attr() {
@@ -988,10 +972,11 @@ int anerf_mlp_gemm(int64_t m, int32_t n, int32_t k, const anerf_seg* a, int32_t 
 #define ANERF_NT_LAUNCH(P, S)                                                                         \
     if (npl == P && n_a == S) {                                                                       \
         constexpr int TB = (ANERF_GEMM_BM == 64 && S == 1) ? 64 : 128;                                \
-        e = nt_attr<P, S, TB>();                                                                      \
+        constexpr int SKT = (ANERF_GEMM_SK64 && P == 2 && S == 1) ? 64 : 32;                          \
+        e = nt_attr<P, S, TB, SKT>();                                                                 \
         if (e != hipSuccess) return anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));            \
-        constexpr int LB = NTGeo<P, TB>::LDS_BYTES;                                                   \
-        hipLaunchKernelGGL((mlp_nt_kernel<P, S, TB>), dim3((unsigned)tiles), dim3(NTHR), LB, st, g);  \
+        constexpr int LB = NTGeo<P, TB, SKT>::LDS_BYTES;                                              \
+        hipLaunchKernelGGL((mlp_nt_kernel<P, S, TB, SKT>), dim3((unsigned)tiles), dim3(NTHR), LB, st, g); \
     }
     ANERF_NT_LAUNCH(3, 1)
     ANERF_NT_LAUNCH(3, 2)
