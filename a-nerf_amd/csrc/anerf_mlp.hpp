@@ -1010,13 +1010,10 @@ __device__ __forceinline__ int block_live_count(const ModelDev& M, const float* 
 #define ANERF_X6_BARRIERS 3
 #endif
 // Precision modes whose four waves run the hidden layers in lock step (a workgroup barrier before
-// each, blocks in live-joint order): bf16x6 and fp16x4 (+2.6 % on fp16x4, bit-identical outputs,
-// profiles/r04i_ab_fp16x4.txt); fp16x3 runs free (neutral in round 3)
-#ifndef ANERF_LOCK_H3
-#define ANERF_LOCK_H3 0  // (experiment: fp16x3 lock-stepped too)
-#endif
+// each, blocks in live-joint order): the split modes bf16x6, fp16x4 and fp16x3 (+2.6 % fp16x4,
+// +0.8 % fp16x3, bit-identical outputs: profiles/r04i_ab_fp16x4.txt, r04y_ab_h3lock.txt)
 template <int P>
-constexpr bool lockstep_mode() { return P == 2 || P == 4 || (P == 3 && ANERF_LOCK_H3); }
+constexpr bool lockstep_mode() { return P >= 2; }
 
 // One x part's bone-direction contraction from the LDS features as bf16x6: k16-step s takes
 // features 8 s .. 8 s + 7 of each lane half (zero past 3 NJH2), split by truncation (split3_pair);
