@@ -25,7 +25,7 @@ ANERF_PREC_FP16X3 = 3
 ANERF_PREC_FP16X4 = 4
 ANERF_FLAG_LINDISP = 0x100  # OR-ed into the precision argument (include/anerf.h)
 ANERF_FLAG_NEAR_FAR = 0x200  # ray_batch columns 6, 7 hold the filled near / far (anerf_render_rays)
-MLP_PRECISIONS = {"bf16x3": 3, "bf16x6": 6}  # ANERF_MLP_BF16X3 / _BF16X6 (training MLP GEMMs)
+MLP_PRECISIONS = {"bf16x3": 3, "fp16x4": 4, "bf16x6": 6}  # ANERF_MLP_* (training MLP GEMMs; fp16x4: forward only)
 PRECISIONS = {"fp32": ANERF_PREC_FP32, "bf16x3": ANERF_PREC_BF16X3, "bf16x6": ANERF_PREC_BF16X6,
               "fp16x3": ANERF_PREC_FP16X3, "fp16x4": ANERF_PREC_FP16X4}
 
@@ -197,6 +197,10 @@ SIGNATURES = {
     "anerf_mlp_gemm": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(Seg),
                                       ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
                                       ctypes.c_int32, ctypes.POINTER(OSeg), ctypes.c_int32, ctypes.c_void_p]),
+    "anerf_mlp_gemm_rows": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(Seg),
+                                           ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+                                           ctypes.c_int32, ctypes.POINTER(OSeg), ctypes.c_int32, ctypes.c_void_p,
+                                           ctypes.c_void_p, ctypes.c_void_p]),
     "anerf_mlp_wgrad_workspace": (ctypes.c_size_t, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]),
     "anerf_mlp_wgrad": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
                                        ctypes.c_int64, ctypes.POINTER(Seg), ctypes.c_int32, ctypes.c_int32,

@@ -92,6 +92,11 @@ struct NTArgs {
     OSegD c[MAXSEG];
     int nc;
     int tiles_n, total;
+    // fp16x4 (F16 instances): per-row maxima of A (non-negative floats' bit patterns, the producing
+    // layer's rout) and the weights' exponent (split buffer tail); rout: this product's row maxima
+    const int* rin;
+    const int* bexp;
+    int* rout;
 };
 
 struct TNArgs {
@@ -119,6 +124,18 @@ typedef __attribute__((address_space(1))) const f32x4 gf32x4;
 
 __device__ __forceinline__ f32x16 mfma(const bf16x8& a, const bf16x8& b, const f32x16& c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x16 mfma16(const bf16x8& a, const bf16x8& b, const f32x16& c) {  // (f16 bits)
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+}
+__device__ __forceinline__ float pow2i(int e) { return __builtin_bit_cast(float, (e + 127) << 23); }  // |e| <= 126
+// fp16x4 row scale: the shift that puts a row's largest |value| (bits m of a non-negative float) in
+// [2^10, 2^11) (anerf_mlp.hpp h3_scale; 0 for an all-zero row)
+__device__ __forceinline__ int f16_row_shift(int m) {
+    int s = m > 0 ? 137 - (m >> 23) : 0;
+    return min(max(s, -100), 100);
 }
 
 // ---------------------------------------------------------------- forward / input gradient
@@ -156,7 +173,7 @@ struct NTGeo {
     static constexpr int STAGES_BYTES = 2 * STAGE * 2;
     static constexpr int TILE_BYTES = TBM * 132 * 4;  // epilogue tile [TBM][132] fp32
     static constexpr int TAB = STAGES_BYTES > TILE_BYTES ? STAGES_BYTES : TILE_BYTES;  // segment tables
-    static constexpr int LDS_BYTES = TAB + 256;
+    static constexpr int LDS_BYTES = TAB + 256 + 4 * TBM;  // (+ segment tables, fp16x4 row shifts)
 };
 
 // output segment tables in LDS: per-lane segment choices read their pointer and stride from here
@@ -169,8 +186,9 @@ struct SegTab {
     int accum[MAXSEG];
 };
 
-template <int NPL, int NSEG, int TBM, int SKT = 32>
+template <int NPL, int NSEG, int TBM, int SKT = 32, bool F16 = false>
 __global__ __launch_bounds__(NTHR, 256 / TBM) void mlp_nt_kernel(NTArgs g) {
+    static_assert(!F16 || (NPL == 2 && NSEG == 1), "fp16x4: two fp16 planes, one A segment");
     using G = NTGeo<NPL, TBM, SKT>;
     constexpr int RBM = G::RBM, NRS = G::NRS, SK = SKT, KK = SKT / 16;
     extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
@@ -186,6 +204,13 @@ __global__ __launch_bounds__(NTHR, 256 / TBM) void mlp_nt_kernel(NTArgs g) {
     const int nst = (Kd + SK - 1) / SK;  // steps
     const int nk = (Kd + 15) / 16;        // k16 steps of the B planes
     SegTab* const tab = reinterpret_cast<SegTab*>(reinterpret_cast<char*>(lds) + G::TAB);
+    int* const rsh = reinterpret_cast<int*>(reinterpret_cast<char*>(lds) + G::TAB + 256);  // F16: row shifts
+    if constexpr (F16) {
+        if (tid < TBM) {
+            const long long m = m0 + tid;
+            rsh[tid] = m < Md ? f16_row_shift(g.rin[m]) : 0;
+        }
+    }
     if (tid < MAXSEG) {
         const int u = tid < g.nc ? tid : 0;
         tab->op[tid] = g.c[u].p;
@@ -224,6 +249,15 @@ __global__ __launch_bounds__(NTHR, 256 / TBM) void mlp_nt_kernel(NTArgs g) {
     f32x16 acc[RBM];
 #pragma unroll
     for (int i = 0; i < RBM; ++i) acc[i] = f32x16{0};
+    float ts[NRS];  // F16: the row scales 2^shift of this thread's staging rows
+#pragma unroll
+    for (int i = 0; i < NRS; ++i) {
+        ts[i] = 1.0f;
+        if constexpr (F16) {
+            const long long m = m0 + sr + RPS * i;
+            ts[i] = m < Md ? pow2i(f16_row_shift(g.rin[m])) : 1.0f;
+        }
+    }
 
     struct BF {
         u32x4 v[NPL];
@@ -266,6 +300,21 @@ __global__ __launch_bounds__(NTHR, 256 / TBM) void mlp_nt_kernel(NTArgs g) {
                 }
                 v[e] = __builtin_bit_cast(float, b);
             }
+            if constexpr (F16) {  // x t = x0 + x1: fp16 round to nearest, then the exact remainder's
+                typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+                unsigned w0[2], w1[2];
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const f32x2 x = (f32x2){v[2 * q] * ts[i], v[2 * q + 1] * ts[i]};
+                    const f16x2 hi = __builtin_convertvector(x, f16x2);
+                    const f32x2 r = x - __builtin_convertvector(hi, f32x2);
+                    w0[q] = __builtin_bit_cast(unsigned, hi);
+                    w1[q] = __builtin_bit_cast(unsigned, __builtin_convertvector(r, f16x2));
+                }
+                *reinterpret_cast<u32x2*>(P + RPS * i * SK) = u32x2{w0[0], w0[1]};
+                *reinterpret_cast<u32x2*>(P + G::PLANE + RPS * i * SK) = u32x2{w1[0], w1[1]};
+                continue;
+            }
 #pragma unroll
             for (int p = 0; p < NPL; ++p) {
                 unsigned w[2];
@@ -297,6 +346,13 @@ __global__ __launch_bounds__(NTHR, 256 / TBM) void mlp_nt_kernel(NTArgs g) {
 #pragma unroll
         for (int i = 0; i < RBM; ++i) {
             f32x16 c = acc[i];
+            if constexpr (F16) {  // the four products, small terms first
+                c = mfma16(a[1][i], b[1], c);
+                c = mfma16(a[1][i], b[0], c);
+                c = mfma16(a[0][i], b[1], c);
+                acc[i] = mfma16(a[0][i], b[0], c);
+                continue;
+            }
             if constexpr (NPL == 3) {
                 c = mfma(a[2][i], b[0], c);
                 c = mfma(a[1][i], b[1], c);
@@ -408,16 +464,29 @@ __global__ __launch_bounds__(NTHR, 256 / TBM) void mlp_nt_kernel(NTArgs g) {
                 ov[q] = *(gf32x4*)(op + m * old + col);
             }
         }
+        int* const rout = g.rout;  // (the host allows it with n % 128 == 0: every lane of a row is here)
+        const float uw = F16 ? pow2i(-g.bexp[0]) : 1.0f;  // fp16x4: undo the weights' and rows' scales
         if (vec) {
 #pragma unroll
             for (int q = 0; q < TBM / 8; ++q) {
                 const int row = 8 * q + rb;
                 const long long m = m0 + row;
                 f32x4 v = *reinterpret_cast<const f32x4*>(tile + row * TP + c4);
+                if constexpr (F16) {
+                    const float ur = pow2i(-rsh[row]);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = v[e] * uw * ur;  // (exact: powers of two)
+                }
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     v[e] += bv[e];
                     if (relu) v[e] = fmaxf(v[e], 0.0f);
+                }
+                if (rout) {  // the row's largest |output| (for the next layer's fp16x4 scale)
+                    float mx = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
+#pragma unroll
+                    for (int o = 16; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+                    if ((lane & 31) == 0 && m < Md) atomicMax(rout + m, __builtin_bit_cast(int, mx));
                 }
                 if (op && m < Md) {
                     if (mp) {
@@ -444,8 +513,11 @@ __global__ __launch_bounds__(NTHR, 256 / TBM) void mlp_nt_kernel(NTArgs g) {
                     const int se = ne >= cs2 ? 2 : (ne >= cs1 ? 1 : 0);
                     float* const ope = tab->op[se];
                     if (!ope) continue;
-                    float x = tile[row * TP + c4 + e] + bv[e];
+                    float x = tile[row * TP + c4 + e];
+                    if constexpr (F16) x = x * uw * pow2i(-rsh[row]);
+                    x += bv[e];
                     if (relu) x = fmaxf(x, 0.0f);
+                    if (rout) atomicMax(rout + m, __builtin_bit_cast(int, fabsf(x)));
                     const int ce = ne - (se == 2 ? cs2 : (se == 1 ? cs1 : 0));
                     const float* const mpe = tab->mask[se];
                     if (mpe && !(mpe[m * tab->ldm[se] + ce] > 0.0f)) x = 0.0f;
@@ -776,7 +848,8 @@ __global__ __launch_bounds__(256) void mlp_reduce_kernel(const float* __restrict
 // transposed, w's columns).
 __device__ __forceinline__ void split_weights_elem(const float* __restrict__ w, int n, int k, long long ldw,
                                                    int transpose, int nblocks, int ksteps, int npl,
-                                                   unsigned short* __restrict__ out, long long idx) {
+                                                   unsigned short* __restrict__ out, long long idx,
+                                                   const int* __restrict__ f16exp = nullptr) {
     const long long per = (long long)nblocks * ksteps * 512;
     if (idx >= per) return;
     const int e = (int)(idx & 7), l = (int)((idx >> 3) & 63);
@@ -786,6 +859,14 @@ __device__ __forceinline__ void split_weights_elem(const float* __restrict__ w, 
     const int rows = transpose ? k : n, cols = transpose ? n : k;
     const int wn = transpose ? col : row, wk = transpose ? row : col;
     float x = (row < rows && col < cols) ? w[(long long)wn * ldw + wk] : 0.0f;
+    if (f16exp) {  // fp16x4: w 2^ew = w0 + w1, fp16 round to nearest of the running remainder
+        x *= pow2i(f16exp[0]);
+        const _Float16 h0 = (_Float16)x;
+        const _Float16 h1 = (_Float16)(x - (float)h0);
+        out[((blk * 2 + 0) << 9) + (l << 3) + e] = __builtin_bit_cast(unsigned short, h0);
+        out[((blk * 2 + 1) << 9) + (l << 3) + e] = __builtin_bit_cast(unsigned short, h1);
+        return;
+    }
     for (int p = 0; p < npl; ++p) {
         const __bf16 xh = (__bf16)x;
         out[((blk * npl + p) << 9) + (l << 3) + e] = __builtin_bit_cast(unsigned short, xh);
@@ -803,6 +884,7 @@ constexpr int MAXJOBS = 32;
 struct SplitJob {
     const float* w;
     unsigned short* out;
+    int* f16exp;  // fp16x4: the weights' exponent (the split buffer's tail), else null
     long long ldw;
     int n, k, transpose, nblocks, ksteps, npl;
     int block0;  // first workgroup of this job
@@ -820,18 +902,45 @@ __global__ void split_weights_batch_kernel(SplitBatch b) {
     // (fields through locals: a per-job select of the argument struct stays in scalar registers)
     const SplitJob J = b.j[q];
     split_weights_elem(J.w, J.n, J.k, J.ldw, J.transpose, J.nblocks, J.ksteps, J.npl, J.out,
-                       (long long)(blockIdx.x - J.block0) * blockDim.x + threadIdx.x);
+                       (long long)(blockIdx.x - J.block0) * blockDim.x + threadIdx.x, J.f16exp);
+}
+
+// fp16x4 weights: the exponent ew that puts max |w| in [2^10, 2^11) (the render path's h3_exponent),
+// one workgroup per job, written to the job's split-buffer tail before the split reads it
+__global__ __launch_bounds__(256) void split_exponent_kernel(SplitBatch b) {
+    const SplitJob J = b.j[blockIdx.x];
+    if (!J.f16exp) return;
+    __shared__ int red[256];
+    int m = 0;
+    for (long long i = threadIdx.x; i < (long long)J.n * J.k; i += 256) {
+        const float v = fabsf(J.w[(i / J.k) * J.ldw + i % J.k]);
+        m = max(m, __builtin_bit_cast(int, v));
+    }
+    red[threadIdx.x] = m;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) red[threadIdx.x] = max(red[threadIdx.x], red[threadIdx.x + o]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const int mm = red[0];
+        J.f16exp[0] = (mm > 0 && mm < 0x7f800000) ? min(max(137 - (mm >> 23), -100), 100) : 0;
+    }
 }
 
 inline int rup(long long x, int a) { return (int)((x + a - 1) / a * a); }
 
-int planes_of(int precision) { return precision == ANERF_MLP_BF16X6 ? 3 : (precision == ANERF_MLP_BF16X3 ? 2 : 0); }
+int planes_of(int precision) {
+    return precision == ANERF_MLP_BF16X6 ? 3 : ((precision == ANERF_MLP_BF16X3 || precision == ANERF_MLP_FP16X4) ? 2 : 0);
+}
+// the fp16x4 exponent sits after the planes (anerf_mlp_split_bytes adds 256 bytes for it)
+size_t split_plane_bytes(int rows, int cols, int npl) { return (size_t)2 * npl * rup(rows, BNW) * rup(cols, 16); }
 
 // the dynamic LDS (up to 67 KB) is above the default limit: raised once per kernel instance
 // (set on every call: the attribute belongs to the current device, and a cached failure would stick)
-template <int NPL, int NSEG, int TBM, int SKT>
+template <int NPL, int NSEG, int TBM, int SKT, bool F16 = false>
 hipError_t nt_attr() {
-    return hipFuncSetAttribute((const void*)mlp_nt_kernel<NPL, NSEG, TBM, SKT>,
+    return hipFuncSetAttribute((const void*)mlp_nt_kernel<NPL, NSEG, TBM, SKT, F16>,
                                hipFuncAttributeMaxDynamicSharedMemorySize, NTGeo<NPL, TBM, SKT>::LDS_BYTES);
 }
 template <int NPL, int NSEG>
@@ -883,7 +992,7 @@ int wgrad_plan(int64_t m, int32_t n, int32_t k, int* splits, long long* rows) {
 extern "C" {
 
 size_t anerf_mlp_split_bytes(int32_t rows, int32_t cols, int32_t precision) {
-    return (size_t)2 * planes_of(precision) * rup(rows, BNW) * rup(cols, 16);
+    return split_plane_bytes(rows, cols, planes_of(precision)) + (precision == ANERF_MLP_FP16X4 ? 256 : 0);
 }
 
 int anerf_mlp_split_weights(const float* w, int32_t n, int32_t k, int64_t ldw, int32_t transpose, int32_t precision,
@@ -891,6 +1000,10 @@ int anerf_mlp_split_weights(const float* w, int32_t n, int32_t k, int64_t ldw, i
     const int npl = planes_of(precision);
     if (!w || !out || n < 1 || k < 1 || ldw < k || !npl)
         return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_split_weights: bad arguments");
+    if (precision == ANERF_MLP_FP16X4) {  // (the exponent pass: through the batch path)
+        anerf_split_job j = {w, n, k, ldw, transpose, precision, out};
+        return anerf_mlp_split_weights_batch(&j, 1, stream);
+    }
     const int rows = transpose ? k : n, cols = transpose ? n : k;
     const int nblocks = (rows + BNW - 1) / BNW * (BNW / 32), ksteps = (cols + 15) / 16;  // whole 256-row tiles
     const long long tot = (long long)nblocks * ksteps * 512;
@@ -922,11 +1035,19 @@ int anerf_mlp_split_weights_batch(const anerf_split_job* jobs, int32_t n_jobs, v
         J.nblocks = (rows + BNW - 1) / BNW * (BNW / 32);
         J.ksteps = (cols + 15) / 16;
         J.npl = npl;
+        J.f16exp = q.precision == ANERF_MLP_FP16X4
+                       ? reinterpret_cast<int*>(static_cast<char*>(q.out) + split_plane_bytes(rows, cols, 2))
+                       : nullptr;
         J.block0 = (int)blocks;
         blocks += ((long long)J.nblocks * J.ksteps * 512 + 255) / 256;
     }
     if (blocks > 0x7fffffff) return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_split_weights_batch: too large");
     b.n = n_jobs;
+    bool any16 = false;
+    for (int i = 0; i < n_jobs; ++i) any16 |= b.j[i].f16exp != nullptr;
+    if (any16)
+        hipLaunchKernelGGL(split_exponent_kernel, dim3((unsigned)n_jobs), dim3(256), 0,
+                           reinterpret_cast<hipStream_t>(stream), b);
     hipLaunchKernelGGL(split_weights_batch_kernel, dim3((unsigned)blocks), dim3(256), 0,
                        reinterpret_cast<hipStream_t>(stream), b);
     hipError_t e = hipGetLastError();
@@ -935,9 +1056,20 @@ int anerf_mlp_split_weights_batch(const anerf_split_job* jobs, int32_t n_jobs, v
 
 int anerf_mlp_gemm(int64_t m, int32_t n, int32_t k, const anerf_seg* a, int32_t n_a, const void* b_split,
                    int32_t precision, const float* bias, int32_t relu, const anerf_oseg* c, int32_t n_c, void* stream) {
+    return anerf_mlp_gemm_rows(m, n, k, a, n_a, b_split, precision, bias, relu, c, n_c, nullptr, nullptr, stream);
+}
+
+int anerf_mlp_gemm_rows(int64_t m, int32_t n, int32_t k, const anerf_seg* a, int32_t n_a, const void* b_split,
+                        int32_t precision, const float* bias, int32_t relu, const anerf_oseg* c, int32_t n_c,
+                        const int32_t* rowmax_in, int32_t* rowmax_out, void* stream) {
     const int npl = planes_of(precision);
     if (m < 0 || n < 1 || k < 1 || !b_split || !c || n_c < 1 || n_c > MAXSEG || !npl)
         return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_gemm: bad arguments");
+    const bool f16 = precision == ANERF_MLP_FP16X4;
+    if (f16 && (n_a != 1 || !rowmax_in))
+        return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_gemm: fp16x4 takes one A segment and its row maxima");
+    if (!f16 && rowmax_in) return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_gemm: row maxima are fp16x4 input");
+    if (rowmax_out && n % NBN) return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_gemm: row maxima need n % 128 == 0");
     if (m == 0) return ANERF_OK;
     NTArgs g = {};
     g.M = m;
@@ -967,8 +1099,20 @@ int anerf_mlp_gemm(int64_t m, int32_t n, int32_t k, const anerf_seg* a, int32_t 
     const long long tiles = (long long)((m + tbm - 1) / tbm) * g.tiles_n;
     if (tiles > 0x7fffffff) return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_gemm: too many tiles");
     g.total = (int)tiles;
+    g.rin = rowmax_in;
+    g.rout = rowmax_out;
+    g.bexp = f16 ? reinterpret_cast<const int*>(static_cast<const char*>(b_split) + split_plane_bytes(n, k, 2))
+                 : nullptr;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     hipError_t e = hipSuccess;
+    if (f16) {
+        e = nt_attr<2, 1, 128, 32, true>();
+        if (e != hipSuccess) return anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));
+        constexpr int LB = NTGeo<2, 128, 32>::LDS_BYTES;
+        hipLaunchKernelGGL((mlp_nt_kernel<2, 1, 128, 32, true>), dim3((unsigned)tiles), dim3(NTHR), LB, st, g);
+        e = hipGetLastError();
+        return e == hipSuccess ? ANERF_OK : anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));
+    }
 #define ANERF_NT_LAUNCH(P, S)                                                                         \
     if (npl == P && n_a == S) {                                                                       \
         constexpr int TB = (ANERF_GEMM_BM == 64 && S == 1) ? 64 : 128;                                \
@@ -1000,7 +1144,7 @@ int anerf_mlp_wgrad(int64_t m, int32_t n, int32_t k, const float* dy, int64_t ld
                     int32_t precision, float* dw, int64_t lddw, float* db, int32_t accumulate, void* workspace,
                     size_t workspace_bytes, void* stream) {
     const int npl = planes_of(precision);
-    if (m < 0 || n < 1 || k < 1 || !dy || lddy < n || !dw || lddw < k || !npl)
+    if (m < 0 || n < 1 || k < 1 || !dy || lddy < n || !dw || lddw < k || !npl || precision == ANERF_MLP_FP16X4)
         return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_wgrad: bad arguments");
     // dY is read as float4 groups of whole rows: 16 B aligned, ld a multiple of 4 and >= n rounded up
     // to 4 (the padding columns only reach the discarded rows n.. of the tile)

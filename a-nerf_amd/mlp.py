@@ -29,6 +29,7 @@ from . import _lib
 # DESIGN.md §10): its 1.6 GB of saved activations cost as much as the GEMMs' re-reads, so the GEMMs
 # stay the default
 _FUSED = os.environ.get("ANERF_TRAIN_FWD", "gemm") == "fused"
+ANERF_MLP_FP16X4 = _lib.MLP_PRECISIONS["fp16x4"]
 
 
 def _stream(dev):
@@ -72,30 +73,33 @@ def split_weight(w, transpose=False, prec=6):
 
 
 def split_weights(jobs, prec):
-    """[(w [n, k], transpose)] -> their bf16 planes (as split_weight), in one launch per 32 weights
-    (anerf_mlp_split_weights_batch)."""
+    """[(w [n, k], transpose[, precision])] -> their split planes (as split_weight), in one launch per
+    32 weights (anerf_mlp_split_weights_batch); a job's own precision overrides `prec`."""
     lib = _lib.load()
     outs = []
     for c0 in range(0, len(jobs), 32):
         chunk = jobs[c0:c0 + 32]
         arr = (_lib.SplitJob * len(chunk))()
-        for i, (w, transpose) in enumerate(chunk):
+        for i, job in enumerate(chunk):
+            w, transpose = job[0], job[1]
+            p = job[2] if len(job) > 2 else prec
             n, k = w.shape
             rows, cols = (k, n) if transpose else (n, k)
-            out = torch.empty(lib.anerf_mlp_split_bytes(rows, cols, prec), device=w.device, dtype=torch.uint8)
+            out = torch.empty(lib.anerf_mlp_split_bytes(rows, cols, p), device=w.device, dtype=torch.uint8)
             arr[i].w, arr[i].n, arr[i].k, arr[i].ldw = w.data_ptr(), n, k, w.stride(0)
-            arr[i].transpose, arr[i].precision, arr[i].out = int(transpose), prec, out.data_ptr()
+            arr[i].transpose, arr[i].precision, arr[i].out = int(transpose), p, out.data_ptr()
             outs.append(out)
         _lib.check(lib.anerf_mlp_split_weights_batch(arr, len(chunk), _stream(chunk[0][0].device)),
                    "anerf_mlp_split_weights_batch")
     return outs
 
 
-def gemm(m, n, k, a, b_split, bias, relu, outs, dev, prec=6):
+def gemm(m, n, k, a, b_split, bias, relu, outs, dev, prec=6, rin=None, rout=None):
+    """anerf_mlp_gemm_rows: rin / rout int32 [m] row maxima (fp16x4 input; any precision's output)."""
     sa, na = _segs(a)
     so, no = _osegs(outs)
-    _lib.check(_lib.load().anerf_mlp_gemm(m, n, k, sa, na, _lib.ptr(b_split), prec, _lib.ptr(bias), int(relu), so,
-                                          no, _stream(dev)), "anerf_mlp_gemm")
+    _lib.check(_lib.load().anerf_mlp_gemm_rows(m, n, k, sa, na, _lib.ptr(b_split), prec, _lib.ptr(bias), int(relu),
+                                               so, no, _lib.ptr(rin), _lib.ptr(rout), _stream(dev)), "anerf_mlp_gemm")
 
 
 def wgrad(m, n, k, dy, x, dw, db, ws, dev, prec=6):
@@ -130,8 +134,17 @@ class _MLP(torch.autograd.Function):
             ctx.has_codes = codes is not None
             ctx.save_for_backward(feat, codes if codes is not None else torch.empty(0), hf, g, whead, *H, *params)
             return raw
+        # fp16x4 forward (prec 4): the GEMMs whose input is one hidden layer's output run as fp16x4
+        # with that layer's row maxima (written by its GEMM's epilogue); layer 0, the skip layer's
+        # [x | h] and the view / rgb layers (encoder columns in their input) stay bf16x6
+        f16 = prec == ANERF_MLP_FP16X4 and W % 128 == 0  # (the row-max epilogue's tile width)
+        prec = 6 if prec == ANERF_MLP_FP16X4 and not f16 else prec
+        lp = [(ANERF_MLP_FP16X4 if (i >= 1 and i - 1 != skip) else 6) if f16 else prec for i in range(D)]
+        hp, op_ = (ANERF_MLP_FP16X4, 6) if f16 else (prec, prec)
         # every layer's planes in one launch: [trunk..., head, views, rgb]
-        sp = split_weights([(w, False) for w in pw] + [(whead, False), (wv, False), (wr, False)], prec)
+        sp = split_weights([(w, False, lp[i]) for i, w in enumerate(pw)] + [(whead, False, hp), (wv, False, op_),
+                                                                            (wr, False, op_)], prec)
+        rm = torch.zeros(D, M, device=dev, dtype=torch.int32) if f16 else [None] * D
         segx = _seg(feat, dnet)
         H = []
         for i in range(D):
@@ -142,14 +155,17 @@ class _MLP(torch.autograd.Function):
             else:
                 a, k = [_seg(H[-1], W)], W
             h = torch.empty(M, W, **f32)
-            mm(M, W, k, a, sp[i], pb[i], True, [(h, W, W, 0, None, False)], dev)
+            gemm(M, W, k, a, sp[i], pb[i], True, [(h, W, W, 0, None, False)], dev, lp[i],
+                 rin=rm[i - 1] if lp[i] == ANERF_MLP_FP16X4 else None, rout=rm[i] if f16 else None)
             H.append(h)
         # feature_linear + alpha_linear as one GEMM (alpha in raw[:, 3]); no activation
         raw = torch.empty(M, 4, **f32)
         hf = torch.empty(M, W, **f32)
         bhead = torch.cat([bf, ba]).contiguous()
-        mm(M, W + 1, W, [_seg(H[-1], W)], sp[D], bhead, False,
-             [(hf, W, W, 0, None, False), (raw, 4, 1, 3, None, False)], dev)
+        gemm(M, W + 1, W, [_seg(H[-1], W)], sp[D], bhead, False,
+             [(hf, W, W, 0, None, False), (raw, 4, 1, 3, None, False)], dev, hp,
+             rin=rm[D - 1] if hp == ANERF_MLP_FP16X4 else None)
+        prec = op_  # (the view and rgb layers)
         # views_linears[0] on cat([feature, views(, framecode)]), relu
         av = [_seg(hf, W), _seg(feat, nv, dnet)] + ([_seg(codes, cfc)] if cfc else [])
         g = torch.empty(M, W // 2, **f32)
@@ -285,10 +301,11 @@ def _fused_forward(feat, codes, pw, pb, wa, ba, wf, bf, wv, bv, wr, br, W, D, sk
     return H, hf, g, raw
 
 
-# mode -> (forward, backward) arithmetic (ANERF_MLP_BF16X6 = 6, _BF16X3 = 3).  "mixed": the forward
-# fp32-accurate (every relu decision as in fp32), the gradients with ~16-bit operands (relative
-# error ~1e-5, no branch decisions downstream of them)
-MODES = {"bf16x6": (6, 6), "bf16x3": (3, 3), "mixed": (6, 3)}
+# mode -> (forward, backward) arithmetic (ANERF_MLP_BF16X6 = 6, _BF16X3 = 3, _FP16X4 = 4).  "mixed": the
+# forward fp32-accurate (every relu decision as in fp32), the gradients with ~16-bit operands (relative
+# error ~1e-5, no branch decisions downstream of them); "mixed16": the forward's hidden-to-hidden
+# products as fp16x4 (the same error bound as bf16x6, four products instead of six), else as "mixed"
+MODES = {"bf16x6": (6, 6), "bf16x3": (3, 3), "mixed": (6, 3), "mixed16": (4, 3)}
 
 
 def nerf_forward(net, feat, codes=None):

@@ -286,12 +286,12 @@ class NeRF(nn.Module):
 
     def forward(self, feat, cams=None):
         """feat [M, F] = [v | r | views] -> raw [M, 4] (rgb, alpha): forward_density + forward_view."""
-        if self.mlp in ("mixed", "bf16x6", "bf16x3"):
+        if self.mlp in ("mixed", "mixed16", "bf16x6", "bf16x3"):
             from . import mlp as _mlp
             codes = self.framecodes(cams) if self.cfg.opt_framecode else None
             return _mlp.nerf_forward(self, feat, codes)
         if self.mlp != "fp32":
-            raise ValueError(f"mlp={self.mlp!r}: 'mixed', 'bf16x6', 'bf16x3' or 'fp32'")
+            raise ValueError(f"mlp={self.mlp!r}: 'mixed', 'mixed16', 'bf16x6', 'bf16x3' or 'fp32'")
         x, x_skip, views = _SplitCols.apply(feat, self.dnet)
         h = x
         for i, lin in enumerate(self.pts_linears):
@@ -395,8 +395,8 @@ class TrainRayCaster(nn.Module):
             # backward is instantiated per frequency count)
             raise NotImplementedError("training: the encoder backward has instances for multires 7 / 10 and "
                                       "multires_views 0 / 4")
-        if mlp not in ("mixed", "bf16x6", "bf16x3", "fp32"):
-            raise ValueError(f"mlp={mlp!r}: 'mixed', 'bf16x6', 'bf16x3' or 'fp32'")
+        if mlp not in ("mixed", "mixed16", "bf16x6", "bf16x3", "fp32"):
+            raise ValueError(f"mlp={mlp!r}: 'mixed', 'mixed16', 'bf16x6', 'bf16x3' or 'fp32'")
         if isinstance(device, (str, torch.device)):
             dev = torch.device(device)  # (a CPU device holds the parameters only: checkpoints, no rendering)
         else:

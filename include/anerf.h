@@ -55,7 +55,7 @@
 extern "C" {
 #endif
 
-#define ANERF_ABI_VERSION 12
+#define ANERF_ABI_VERSION 13
 
 enum {
     ANERF_OK = 0,
@@ -391,8 +391,13 @@ int anerf_train_importance(const float* z, const float* weights, int64_t n_rays,
 /* ---- training MLP linears on the bf16 MFMA pipe, fp32 in / out with split-bf16 operands:
  *   ANERF_MLP_BF16X6  x = x0 + x1 + x2, w likewise, the six products with i + j <= 2 (fp32-accurate:
  *                     the dropped terms are below 2^-23 of |x w|), fp32 accumulation
- *   ANERF_MLP_BF16X3  x = x0 + x1, three products (~16 significant bits per operand) */
-enum { ANERF_MLP_BF16X3 = 3, ANERF_MLP_BF16X6 = 6 };
+ *   ANERF_MLP_BF16X3  x = x0 + x1, three products (~16 significant bits per operand)
+ *   ANERF_MLP_FP16X4  forward products only (anerf_mlp_gemm_rows): each A row scaled by a power of two
+ *                     from its largest |value| (row maxima given), the weights by one from theirs
+ *                     (computed on the device by the split), x = x0 + x1 and w = w0 + w1 in fp16, all
+ *                     four products on v_mfma_f32_32x32x16_f16: within ~2^-22 of |x w| per product, the
+ *                     bound of ANERF_MLP_BF16X6 (the render path's fp16x4) */
+enum { ANERF_MLP_BF16X3 = 3, ANERF_MLP_FP16X4 = 4, ANERF_MLP_BF16X6 = 6 };
 /*
  * An operand is up to 3 column segments (the reference's torch.cat along features, never
  * materialised here): segment i holds columns [sum of earlier cols, + cols) at p[row * ld + c]. */
@@ -477,6 +482,14 @@ int anerf_mlp_split_weights_batch(const anerf_split_job* jobs, int32_t n_jobs, v
 int anerf_mlp_gemm(int64_t m, int32_t n, int32_t k, const anerf_seg* a, int32_t n_a, const void* b_split,
                    int32_t precision, const float* bias, int32_t relu, const anerf_oseg* c, int32_t n_c,
                    void* stream);
+/* anerf_mlp_gemm with row maxima: rowmax_in [m] (ANERF_MLP_FP16X4 only, required there; one A segment):
+ * the bit patterns of max_k |A[row][k]| (as written by rowmax_out); rowmax_out [m] (NULL or any
+ * precision, n % 128 == 0, zeroed by the caller): atomically max'd with the bit patterns of
+ * max_j |C[row][j]| after bias and relu (the next layer's rowmax_in).  The split weights of
+ * ANERF_MLP_FP16X4 carry their exponent (anerf_mlp_split_bytes includes it). */
+int anerf_mlp_gemm_rows(int64_t m, int32_t n, int32_t k, const anerf_seg* a, int32_t n_a, const void* b_split,
+                        int32_t precision, const float* bias, int32_t relu, const anerf_oseg* c, int32_t n_c,
+                        const int32_t* rowmax_in, int32_t* rowmax_out, void* stream);
 /* Workspace bytes of anerf_mlp_wgrad for these sizes. */
 size_t anerf_mlp_wgrad_workspace(int64_t m, int32_t n, int32_t k);
 /* dW[n][k] (+)= sum_m dY[m][n] X[m][k] and db[n] (+)= sum_m dY[m][n] (db may be NULL); X: n_x

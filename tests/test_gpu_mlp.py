@@ -73,6 +73,57 @@ def test_gemm_forward_segments_bias_relu(m, n, ks, prec):
     assert torch.all(err <= _bound(a, w, prec)), float(err.max())
 
 
+def _rowmax_bits(t):
+    """int32 [m]: the bit pattern of each row's largest |value| (what the GEMM epilogue's rout holds)."""
+    return t.abs().amax(1).contiguous().view(torch.int32) if t.shape[1] else torch.zeros(t.shape[0], dtype=torch.int32)
+
+
+@pytest.mark.parametrize("m,n,k", [(1000, 256, 256), (163857, 256, 256), (77, 257, 256), (4096, 128, 128),
+                                   (3001, 3, 128), (9000, 256, 432)])
+def test_gemm_fp16x4_row_scaled(m, n, k):
+    """fp16x4 (anerf_mlp_gemm_rows, precision 4): each A row scaled by a power of two from its row
+    maximum, the weights by one from their maximum, both split into two fp16 planes, four products.
+    Rows spanning 2^-40 .. 2^40 (and all-zero rows) keep the bf16x6 error bound 2e-6 (|a| |w|) per
+    element, and rout holds the exact row maxima of the relu output."""
+    torch.manual_seed(m + k)
+    a = torch.relu(torch.randn(m, k, device=DEV))
+    a *= torch.pow(2.0, torch.randint(-40, 41, (m, 1), device=DEV).float())
+    a[::97] = 0.0
+    w = torch.randn(n, k, device=DEV) / k ** 0.5 * 1e-3
+    b = torch.randn(n, device=DEV) * 1e-3
+    out = torch.full((m, n), 7.0, device=DEV)
+    rin = _rowmax_bits(a)
+    rout = torch.zeros(m, device=DEV, dtype=torch.int32) if n % 128 == 0 else None
+    sp = mlp.split_weights([(w, False, 4)], 6)[0]
+    mlp.gemm(m, n, k, [mlp._seg(a, k)], sp, b, True, [(out, n, n, 0, None, False)], torch.device(DEV), 4,
+             rin=rin, rout=rout)
+    ref = torch.relu(a.double() @ w.double().t() + b.double())
+    err = (out.double() - ref).abs()
+    bound = 2e-6 * (a.double().abs() @ w.double().abs().t()) + 1e-6 * b.double().abs().max() + 1e-30
+    assert torch.all(err <= bound), float((err / bound).max())
+    if rout is not None:
+        assert torch.equal(rout, _rowmax_bits(out))
+
+
+def test_gemm_fp16x4_rejects_bad_arguments():
+    x = torch.rand(64, 128, device=DEV)
+    w = torch.randn(128, 128, device=DEV)
+    sp4 = mlp.split_weights([(w, False, 4)], 6)[0]
+    o = [(torch.empty(64, 128, device=DEV), 128, 128, 0, None, False)]
+    with pytest.raises(mlp._lib.AnerfError, match="row maxima"):
+        mlp.gemm(64, 128, 128, [mlp._seg(x, 128)], sp4, None, False, o, torch.device(DEV), 4)
+    with pytest.raises(mlp._lib.AnerfError, match="row maxima"):
+        mlp.gemm(64, 128, 128, [mlp._seg(x, 64), mlp._seg(x, 64, 64)], sp4, None, False, o, torch.device(DEV), 4,
+                 rin=_rowmax_bits(x))
+    with pytest.raises(mlp._lib.AnerfError, match="row maxima are fp16x4"):
+        mlp.gemm(64, 128, 128, [mlp._seg(x, 128)], mlp.split_weight(w), None, False, o, torch.device(DEV), 6,
+                 rin=_rowmax_bits(x))
+    with pytest.raises(mlp._lib.AnerfError, match="n % 128"):
+        mlp.gemm(64, 64, 128, [mlp._seg(x, 128)], mlp.split_weight(w[:64].contiguous()), None, False,
+                 [(torch.empty(64, 64, device=DEV), 64, 64, 0, None, False)], torch.device(DEV), 6,
+                 rout=torch.zeros(64, device=DEV, dtype=torch.int32))
+
+
 def test_gemm_rejects_misaligned_segments():
     x = torch.randn(64, 35, device=DEV)
     w = torch.randn(16, 34, device=DEV)
@@ -157,7 +208,7 @@ def test_wgrad_is_deterministic():
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
 
 
-@pytest.mark.parametrize("impl", ["bf16x6", "mixed", "bf16x3"])
+@pytest.mark.parametrize("impl", ["bf16x6", "mixed", "mixed16", "bf16x3"])
 @pytest.mark.parametrize("D,W,fc,nj", [(8, 256, False, 24), (4, 128, True, 24),
                                        # joint counts whose feature blocks are not multiples of 4 columns
                                        # (mlp._pad_to_segments): 17 (odd), 26 (even, not % 4), 65 (config 4)

@@ -67,9 +67,9 @@ def _run(name, mlp="mixed"):
     return g, tr, sk, out, loss
 
 
-# the training MLP on the hand-written split-bf16 GEMMs (mixed — the default — and bf16x6) and on torch's
-# fp32 GEMMs
-@pytest.fixture(scope="module", params=[(n, mlp) for n in TRAIN for mlp in ("mixed", "bf16x6", "fp32")],
+# the training MLP on the hand-written split-bf16 GEMMs (mixed — the default —, mixed16 and bf16x6) and on
+# torch's fp32 GEMMs
+@pytest.fixture(scope="module", params=[(n, mlp) for n in TRAIN for mlp in ("mixed", "mixed16", "bf16x6", "fp32")],
                 ids=lambda p: f"{p[0]}-{p[1]}")
 def run(request):
     return _run(*request.param)

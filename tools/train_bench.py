@@ -34,7 +34,7 @@ def parser():
     ap.add_argument("--images", type=int, default=128)
     ap.add_argument("--samples", type=int, default=64)
     ap.add_argument("--importance", type=int, default=16)
-    ap.add_argument("--mlp", default="mixed", choices=["mixed", "bf16x6", "bf16x3", "fp32"],
+    ap.add_argument("--mlp", default="mixed", choices=["mixed", "mixed16", "bf16x6", "bf16x3", "fp32"],
                     help="training MLP arithmetic (train.TrainRayCaster mlp=)")
     ap.add_argument("--split-single", action="store_true",
                     help="ablation: one split launch per weight instead of the batched split")
@@ -49,7 +49,8 @@ def measure(a, dev=None):
     dev = dev or torch.device("cuda:0")
     if getattr(a, "split_single", False):
         mlp = importlib.import_module("a-nerf_amd.mlp")
-        mlp.split_weights = lambda jobs, prec: [mlp.split_weight(w, t, prec) for w, t in jobs]
+        mlp.split_weights = lambda jobs, prec: [mlp.split_weight(j[0], j[1], j[2] if len(j) > 2 else prec)
+                                                   for j in jobs]
     S, I, n = a.samples, a.importance, a.rays
     cfg = anerf.RenderConfig(N_samples=S, N_importance=I).validate()
     ck = syn.make_checkpoint(13, n_joints=24, D=8, W=256, fine=True, tau=20.0)
@@ -110,6 +111,8 @@ def measure(a, dev=None):
         "pipe": "FP32 matrix" if a.mlp == "fp32" else "BF16 dense (the split-bf16 GEMMs' v_mfma_f32_32x32x16_bf16)",
         "precision_note": {"mixed": "forward bf16x6 (fp32-accurate), gradients bf16x3 (~16-bit operands, relative "
                                     "error ~1e-5; pinned at 2e-3 of max |ref| per gradient tensor)",
+                           "mixed16": "as mixed, the forward's hidden-to-hidden layers and head as fp16x4 (row-scaled "
+                                      "two-way fp16 split, the bf16x6 error bound)",
                            "bf16x6": "fp32-accurate forward and gradients", "bf16x3": "~16-bit operands",
                            "fp32": "torch fp32 GEMMs"}[a.mlp],
         "data": "synthetic (seeded SMPL-24 poses, 128 cameras on a circle, seeded weights)"}
