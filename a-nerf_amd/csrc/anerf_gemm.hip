@@ -482,11 +482,15 @@ __global__ __launch_bounds__(NTHR, 256 / TBM) void mlp_nt_kernel(NTArgs g) {
                     v[e] += bv[e];
                     if (relu) v[e] = fmaxf(v[e], 0.0f);
                 }
-                if (rout) {  // the row's largest |output| (for the next layer's fp16x4 scale)
-                    float mx = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
-#pragma unroll
-                    for (int o = 16; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-                    if ((lane & 31) == 0 && m < Md) atomicMax(rout + m, __builtin_bit_cast(int, mx));
+                if (rout) {  // the row's largest |output| (for the next layer's fp16x4 scale): a max over
+                    // each 16-lane DPP row (quad xor 1, xor 2, half-row mirror, row mirror), one atomic per row
+                    int mx = __builtin_bit_cast(
+                        int, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+                    mx = max(mx, __builtin_amdgcn_update_dpp(0, mx, 0xB1, 0xF, 0xF, false));
+                    mx = max(mx, __builtin_amdgcn_update_dpp(0, mx, 0x4E, 0xF, 0xF, false));
+                    mx = max(mx, __builtin_amdgcn_update_dpp(0, mx, 0x141, 0xF, 0xF, false));
+                    mx = max(mx, __builtin_amdgcn_update_dpp(0, mx, 0x140, 0xF, 0xF, false));
+                    if ((lane & 15) == 0 && m < Md) atomicMax(rout + m, mx);
                 }
                 if (op && m < Md) {
                     if (mp) {
@@ -907,23 +911,27 @@ __global__ void split_weights_batch_kernel(SplitBatch b) {
 
 // fp16x4 weights: the exponent ew that puts max |w| in [2^10, 2^11) (the render path's h3_exponent),
 // one workgroup per job, written to the job's split-buffer tail before the split reads it
-__global__ __launch_bounds__(256) void split_exponent_kernel(SplitBatch b) {
+// one 1024-thread workgroup per fp16x4 job: wave w reads rows w, w + 16, ... (coalesced, 4 loads in
+// flight per lane), then a wave and a workgroup max
+__global__ __launch_bounds__(1024) void split_exponent_kernel(SplitBatch b) {
     const SplitJob J = b.j[blockIdx.x];
     if (!J.f16exp) return;
-    __shared__ int red[256];
+    __shared__ int red[16];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     int m = 0;
-    for (long long i = threadIdx.x; i < (long long)J.n * J.k; i += 256) {
-        const float v = fabsf(J.w[(i / J.k) * J.ldw + i % J.k]);
-        m = max(m, __builtin_bit_cast(int, v));
+    for (int r = wave; r < J.n; r += 16) {
+        const float* const row = J.w + (long long)r * J.ldw;
+#pragma unroll 4
+        for (int c = lane; c < J.k; c += 64) m = max(m, __builtin_bit_cast(int, fabsf(row[c])));
     }
-    red[threadIdx.x] = m;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o));
+    if (lane == 0) red[wave] = m;
     __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-        if ((int)threadIdx.x < o) red[threadIdx.x] = max(red[threadIdx.x], red[threadIdx.x + o]);
-        __syncthreads();
-    }
     if (threadIdx.x == 0) {
-        const int mm = red[0];
+        int mm = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) mm = max(mm, red[i]);
         J.f16exp[0] = (mm > 0 && mm < 0x7f800000) ? min(max(137 - (mm >> 23), -100), 100) : 0;
     }
 }
@@ -1046,7 +1054,7 @@ int anerf_mlp_split_weights_batch(const anerf_split_job* jobs, int32_t n_jobs, v
     bool any16 = false;
     for (int i = 0; i < n_jobs; ++i) any16 |= b.j[i].f16exp != nullptr;
     if (any16)
-        hipLaunchKernelGGL(split_exponent_kernel, dim3((unsigned)n_jobs), dim3(256), 0,
+        hipLaunchKernelGGL(split_exponent_kernel, dim3((unsigned)n_jobs), dim3(1024), 0,
                            reinterpret_cast<hipStream_t>(stream), b);
     hipLaunchKernelGGL(split_weights_batch_kernel, dim3((unsigned)blocks), dim3(256), 0,
                        reinterpret_cast<hipStream_t>(stream), b);

@@ -9,7 +9,7 @@ true || timeout -k 10 600 python -u -m pytest tests/test_gpu_mlp.py tests/test_g
     --timeout 120 --timeout-method thread > gpurun_out/${TAG}_pytest.log 2>&1; rc=$?
 rc=0
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || { echo "pytest rc=$rc"; exit $rc; }
-for r in 1 2 3; do
+for r in 1 2; do
   for m in mixed mixed16; do
     timeout -k 10 200 python tools/train_bench.py --mlp $m >> gpurun_out/${TAG}_train_ab.txt 2>> gpurun_out/${TAG}_train_ab.err \
       || { tail -20 gpurun_out/${TAG}_train_ab.err; exit 1; }
