@@ -37,6 +37,16 @@ def _pose_table(x, n, per_ray_shape):
     return table.reshape(-1, *per_ray_shape).contiguous(), inverse.to(torch.int32).contiguous()
 
 
+
+def _check_subject_idxs(subject_idxs):
+    """The density paths take `subject_idxs` as the reference does (an integer index per query; it
+    selects joint_coords rows that no encoder reads)."""
+    if subject_idxs is None:
+        return
+    t = torch.as_tensor(subject_idxs)
+    if t.is_floating_point() or t.is_complex():
+        raise IndexError("subject_idxs: tensors used as indices must be long, int, byte or bool tensors")
+
 class RayCaster:
     """Eval-mode RayCaster over a DeviceModel (the reference class is an nn.Module; this one holds
     no torch parameters: its weights live packed in HBM)."""
@@ -100,11 +110,16 @@ class RayCaster:
     def render_pts_density(self, pts, kps, skts, bones, render_kwargs=None, subject_idxs=None, netchunk=1024 * 64,
                            network=None, color=False, v=None):
         """Raw density (alpha_linear, before the density activation) at points, shape
-        pts.shape[:-1] + (1,)  (core/raycasters.py:597-648; `netchunk` is only a batching hint there)."""
+        pts.shape[:-1] + (1,)  (core/raycasters.py:597-648; `netchunk` is only a batching hint there).
+
+        `subject_idxs` selects the reference's per-subject `joint_coords` rows (raycasters.py:601,
+        726-729), which only reach the bone encoder's unused `coords` argument (no encoder in
+        core/encoders.py reads them): the density does not depend on them, here as there."""
         if color:
             raise NotImplementedError("color=True needs texture layers the NeRF model does not have")
-        if subject_idxs is not None or v is not None:
-            raise NotImplementedError("subject_idxs / precomputed kp inputs are not supported")
+        _check_subject_idxs(subject_idxs)
+        if v is not None:
+            raise NotImplementedError("precomputed kp inputs (v) are not supported")
         dev = torch.device(f"cuda:{self.model.device}")
         p = torch.as_tensor(pts).to(dev, torch.float32)
         shape = p.shape[:-1]
@@ -120,9 +135,11 @@ class RayCaster:
     def render_mesh_density(self, kps, skts, bones, subject_idxs=None, radius=1.0, res=64, render_kwargs=None,
                             netchunk=1024 * 64, v=None, network=None):
         """Raw density on the (res+1)^3 grid around kps[0, 0] (core/raycasters.py:579-595), generated
-        on the device; same grid and element order as the reference's meshgrid."""
-        if subject_idxs is not None or v is not None:
-            raise NotImplementedError("subject_idxs / precomputed kp inputs are not supported")
+        on the device; same grid and element order as the reference's meshgrid (`subject_idxs`: as
+        in render_pts_density)."""
+        _check_subject_idxs(subject_idxs)
+        if v is not None:
+            raise NotImplementedError("precomputed kp inputs (v) are not supported")
         dev = torch.device(f"cuda:{self.model.device}")
         res1 = int(res) + 1
         axis = torch.from_numpy(np.linspace(-radius, radius, res1).astype(np.float32)).to(dev)
@@ -150,7 +167,10 @@ class RayCaster:
         if perturb or raw_noise_std or ray_noise_std:
             raise NotImplementedError("stochastic sampling / noise (training mode) is not implemented")
         if subject_idxs is not None:
-            raise NotImplementedError("multi-subject rendering (subject_idxs) is not implemented")
+            # the reference appends the indices to the view encoding (raycasters.py:545-548) and its
+            # NeRF.forward then cannot split [pts | views | cam] (nerf.py:135-137): the same error
+            raise RuntimeError("subject_idxs: the NeRF input has one column more than "
+                               "input_ch + input_ch_bones + input_ch_views + cam_ch (core/networks/nerf.py:135)")
         if preproc_kwargs:
             B = preproc_kwargs.get("density_scale", self.cfg.density_scale)
             if B != self.cfg.density_scale:

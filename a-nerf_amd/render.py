@@ -87,8 +87,9 @@ def render_frames(render_poses, hwf, chunk, render_kwargs, centers=None, kp=None
         else:
             focal = np.array(focal, copy=True) / render_factor
             centers = None if centers is None else np.array(centers, copy=True) / render_factor
-    if subject_idxs is not None:
-        raise NotImplementedError("subject_idxs is not implemented")
+    if subject_idxs is not None:  # (render_rays raises for them, as the reference's NeRF does)
+        raise RuntimeError("subject_idxs: the NeRF input has one column more than "
+                           "input_ch + input_ch_bones + input_ch_views + cam_ch (core/networks/nerf.py:135)")
     rc = render_kwargs["ray_caster"]
     dev = torch.device(f"cuda:{rc.model.device}")
     poses_np = _to_np(render_poses).astype(np.float32)

@@ -557,8 +557,9 @@ class TrainRayCaster(nn.Module):
                     preproc_kwargs=None, nerf_type="nerf", rand=None, chunk=None):
         """core/raycasters.py:361-474 with autograd: gradients reach the networks' parameters and
         `skts` (when it requires grad).  `rand` overrides the random draws (module docstring)."""
-        if subject_idxs is not None:
-            raise NotImplementedError("multi-subject training (subject_idxs) is not implemented")
+        if subject_idxs is not None:  # (as the reference's NeRF.forward split, core/networks/nerf.py:135-137)
+            raise RuntimeError("subject_idxs: the NeRF input has one column more than "
+                               "input_ch + input_ch_bones + input_ch_views + cam_ch (core/networks/nerf.py:135)")
         if skts is None or cyls is None:
             raise ValueError("skts and cyls are required")
         cfg = self.cfg

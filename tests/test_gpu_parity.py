@@ -392,6 +392,16 @@ def test_density_matches_oracle_both_nets_and_ragged():
     np.testing.assert_array_equal(one.cpu().numpy()[0], full.cpu().numpy()[7])  # points are independent
     empty = rc.render_pts_density(torch.from_numpy(pts[:0]), None, torch.from_numpy(g["skts"]), None)
     assert empty.shape == (0, 1)
+    # subject_idxs select joint_coords rows no encoder reads (core/raycasters.py:601, 726-729): no effect
+    subj = rc.render_pts_density(torch.from_numpy(pts), None, torch.from_numpy(g["skts"]), None,
+                                 subject_idxs=torch.zeros(1, dtype=torch.long))
+    assert torch.equal(subj, full)
+    with pytest.raises(IndexError):
+        rc.render_pts_density(torch.from_numpy(pts), None, torch.from_numpy(g["skts"]), None,
+                              subject_idxs=torch.zeros(1))
+    with pytest.raises(RuntimeError, match="subject_idxs"):  # as the reference's NeRF.forward split
+        rc.render_rays(torch.zeros(4, 8), 8, skts=torch.from_numpy(g["skts"]), cyls=torch.zeros(1, 4),
+                       subject_idxs=torch.zeros(1, dtype=torch.long))
 
 
 @pytest.mark.parametrize("precision", ["bf16x6", "fp16x4", "fp16x3", "bf16x3"])
