@@ -31,6 +31,7 @@ PRECISIONS = {"fp32": ANERF_PREC_FP32, "bf16x3": ANERF_PREC_BF16X3, "bf16x6": AN
 
 
 ANERF_ENC_CUT_TO_DIST, ANERF_ENC_CUTOFF_SHIFT, ANERF_ENC_CUTOFF_BONES = 1, 2, 4  # anerf_model_desc.encoder_flags
+ANERF_ENC_VIEW_RAW = 8  # --view_type world
 
 
 class ModelDesc(ctypes.Structure):

@@ -85,11 +85,21 @@ class RenderConfig:
             raise ValueError(f"precision={self.precision!r}: 'fp32', 'bf16x6', 'fp16x4', 'fp16x3' or 'bf16x3'")
         if self.n_joints < 1 or self.n_joints > 128:
             raise NotImplementedError(f"n_joints={self.n_joints} outside [1, 128]")
-        for k, allowed in (("kp_dist_type", "reldist"), ("bone_type", "reldir"), ("view_type", "relray"),
-                           ("pts_tr_type", "local")):
-            v = self.extra.get(k, allowed)
-            if v != allowed:
-                raise NotImplementedError(f"--{k}={v}: only {allowed} is implemented")
+        # encoder selectors (core/raycasters.py:251-305).  The reference itself raises TypeError for
+        # kp_dist_type 'cat' (KPCatEncoder's expand, encoders.py:168) and bone_type 'axisang'
+        # (IdentityExpandEncoder called without refs, raycasters.py:521), recorded by
+        # tests/golden/probe_reference_flags.py in reference_flags.json: the same error here
+        if self.extra.get("kp_dist_type") == "cat":
+            raise TypeError("--kp_dist_type cat: the reference's KPCatEncoder raises TypeError in expand() "
+                            "(core/encoders.py:168)")
+        if self.extra.get("bone_type") == "axisang":
+            raise TypeError("--bone_type axisang: IdentityExpandEncoder.forward() missing 1 required positional "
+                            "argument: 'refs' (core/raycasters.py:521)")
+        for k, allowed in (("kp_dist_type", ("reldist",)), ("bone_type", ("reldir",)),
+                           ("view_type", ("relray", "world")), ("pts_tr_type", ("local",))):
+            v = self.extra.get(k, allowed[0])
+            if v not in allowed:
+                raise NotImplementedError(f"--{k}={v}: only {' / '.join(allowed)} implemented")
         return self
 
     @property

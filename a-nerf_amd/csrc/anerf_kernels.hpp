@@ -488,7 +488,7 @@ __device__ void encode_row(const ModelDev& M, const float* __restrict__ skts, fl
         f[nj * nv + 3 * j + 2] = M.bone_cut ? (qz / dn) * wb : qz / dn;
         float ex, ey, ez;
         joint_rot(S, dx, dy, dz, ex, ey, ez);
-        const float en = fmaxf(norm3(ex, ey, ez), 1e-12f);
+        const float en = M.view_raw ? 1.0f : fmaxf(norm3(ex, ey, ez), 1e-12f);  // (world: R_j d itself)
         const float e[3] = {ex / en, ey / en, ez / en};
         const float wv = M.cutoff_viewdir ? cutoff_w(M.tau_v, dist, M.cutoff_v[j]) : 1.0f;
         for (int c = 0; c < 3; ++c) {

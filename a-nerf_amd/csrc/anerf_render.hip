@@ -194,6 +194,7 @@ int anerf_model_create(const anerf_model_desc* desc, const anerf_net_weights* co
     md.shift = desc->softplus_shift;
     md.B = desc->density_scale;
     md.bone_cut = bone_cut ? 1 : 0;
+    md.view_raw = (desc->encoder_flags & ANERF_ENC_VIEW_RAW) ? 1 : 0;
     md.tau = embed->tau;
     md.tau_v = embed->tau_v;
     md.tau_b = bone_cut ? embed->tau_b : 0.0f;

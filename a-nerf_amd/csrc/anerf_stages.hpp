@@ -66,7 +66,7 @@ __device__ void compute_view_factor(const ModelDev& M, const NetDev& net, float*
         const float* S = lds + P.sk + P.sk_stride * r + 12 * j;
         float ex, ey, ez;
         joint_rot(S, ray[3], ray[4], ray[5], ex, ey, ez);
-        const float en = fmaxf(norm3(ex, ey, ez), 1e-12f);
+        const float en = M.view_raw ? 1.0f : fmaxf(norm3(ex, ey, ez), 1e-12f);  // (world: R_j d itself)
         const float e = (c == 0 ? ex : (c == 1 ? ey : ez)) / en;
         float* Tt = lds + P.scr + P.scr_stride * r + TP * j;
         Tt[c] = e;

@@ -75,6 +75,7 @@ struct ModelDev {
     int cut_to, shift_in;  // kp encoder input transforms (ANERF_ENC_CUT_TO_DIST / _CUTOFF_SHIFT)
     int h3_top;      // fp16x3: biased exponent the largest scaled activation of a sample gets (127 + 10)
     int bone_cut;    // --cutoff_bones (+ use_cutoff, cutoff_inputs): bone directions times w_b
+    int view_raw;    // --view_type world: the view input is R_j d, not normalised (ANERF_ENC_VIEW_RAW)
     float shift, B, tau, tau_v, tau_b;
     const float* cutoff;
     const float* cutoff_v;

@@ -55,7 +55,8 @@ class DeviceModel:
         d.single_net = int(cfg.single_net)
         d.encoder_flags = ((_lib.ANERF_ENC_CUT_TO_DIST if cfg.cut_to_dist else 0) |
                            (_lib.ANERF_ENC_CUTOFF_SHIFT if cfg.cutoff_shift else 0) |
-                           (_lib.ANERF_ENC_CUTOFF_BONES if cfg.bone_window and cfg.cutoff_inputs else 0))
+                           (_lib.ANERF_ENC_CUTOFF_BONES if cfg.bone_window and cfg.cutoff_inputs else 0) |
+                           (_lib.ANERF_ENC_VIEW_RAW if cfg.extra.get("view_type", "relray") == "world" else 0))
         # (the C side applies the flag under the same condition: anerf.h, ANERF_ENC_CUTOFF_BONES)
         d.has_fine = int(fine_sd is not None and cfg.N_importance > 0)
         self.has_fine = bool(d.has_fine)

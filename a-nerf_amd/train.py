@@ -397,6 +397,9 @@ class TrainRayCaster(nn.Module):
                                       "multires_views 0 / 4")
         if mlp not in ("mixed", "mixed16", "bf16x6", "bf16x3", "fp32"):
             raise ValueError(f"mlp={mlp!r}: 'mixed', 'mixed16', 'bf16x6', 'bf16x3' or 'fp32'")
+        if cfg.extra.get("view_type", "relray") != "relray":
+            raise NotImplementedError("training: --view_type world renders (RayCaster) but the training encoder "
+                                      "and its backward take the normalised relray directions only")
         if isinstance(device, (str, torch.device)):
             dev = torch.device(device)  # (a CPU device holds the parameters only: checkpoints, no rendering)
         else:

@@ -55,7 +55,7 @@
 extern "C" {
 #endif
 
-#define ANERF_ABI_VERSION 13
+#define ANERF_ABI_VERSION 14
 
 enum {
     ANERF_OK = 0,
@@ -143,6 +143,11 @@ typedef struct {
  * cutoff_inputs (core/cutoff_embedder.py:111-166), the bare direction otherwise.  The flag is ignored
  * (and tau_b / cutoff_dist_b unused) unless desc->use_cutoff and desc->cutoff_inputs are both set. */
 #define ANERF_ENC_CUTOFF_BONES 4
+/* --view_type world (core/raycasters.py:279-280, ABI 14): the view input of joint j is R_j d itself
+ * (IdentityExpandEncoder of transform_batch_rays, encoders.py:25-37, 71-79), not the normalised
+ * R_j d / |R_j d| of the default relray (VecNormEncoder, encoders.py:172-193).  Rendering only:
+ * anerf_train_encode / _encode_backward do not read it (train.TrainRayCaster refuses the flag). */
+#define ANERF_ENC_VIEW_RAW 8
 
 /* HOST pointers to one NeRF's weights, torch nn.Linear layout [out][in] (core/networks/nerf.py:57-88). */
 typedef struct {

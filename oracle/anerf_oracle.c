@@ -68,6 +68,9 @@ typedef struct {
     int bone_cut;
     float tau_b;
     const float* cutoff_b; /* embedbones_fn.cutoff_dist (NJ) */
+    /* --view_type world (raycasters.py:279-280): IdentityExpandEncoder of the joint-frame ray
+     * directions, i.e. R_j d without the VecNorm normalisation (encoders.py:71-79) */
+    int view_raw;
 } oracle_model;
 
 /* ---------------------------------------------------------------- small helpers */
@@ -329,6 +332,7 @@ static void encode_point(const oracle_model* m, const float* skts, const float p
         for (int r = 0; r < 3; ++r) e[r] = fmaf(S[4 * r + 2], d[2], fmaf(S[4 * r + 1], d[1], S[4 * r + 0] * d[0]));
         float en = norm3_(e[0], e[1], e[2]);
         en = en > 1e-12f ? en : 1e-12f;
+        if (m->view_raw) en = 1.0f; /* (x = e[c] / 1 = e[c]) */
         float wv = 1.0f;
         if (m->cutoff_viewdir) wv = 1.0f - sigmoidf_(m->tau_v * (dist - m->cutoff_v[j]));
         for (int c = 0; c < 3; ++c) {

@@ -32,7 +32,7 @@ class _Model(ctypes.Structure):
                 ("lindisp", ctypes.c_int), ("sched_w", _f), ("sched_wv", _f), ("cut_to", ctypes.c_int),
                 ("shift_in", ctypes.c_int),
                 ("coarse", _Net), ("fine", _Net),
-                ("bone_cut", ctypes.c_int), ("tau_b", ctypes.c_float), ("cutoff_b", _f)]
+                ("bone_cut", ctypes.c_int), ("tau_b", ctypes.c_float), ("cutoff_b", _f), ("view_raw", ctypes.c_int)]
 
 
 def build():
@@ -97,6 +97,7 @@ class OracleModel:
         m.single_net = int(cfg.single_net)
         m.lindisp = int(cfg.lindisp)
         m.cut_to, m.shift_in = int(getattr(cfg, "cut_to_dist", False)), int(getattr(cfg, "cutoff_shift", False))
+        m.view_raw = int(getattr(cfg, "extra", {}).get("view_type", "relray") == "world")
         if getattr(cfg, "cutoff_bones", False) and cfg.use_cutoff and cfg.cutoff_inputs:
             eb = ckpt["embedbones_state_dict"]
             m.bone_cut, m.tau_b, m.cutoff_b = 1, float(np.asarray(eb["tau"])), self._k(eb["cutoff_dist"])

@@ -32,7 +32,9 @@ NAMES = ["c1_64_s32_d4w128", "c2_256_s64_d8w256", "c3_512_s64i128_d8w256", "c4_5
          "pw_64_white_d4w128", "pb_64_bgimg_d4w128",
          # multires / multires_views other than 7 / 4 and 10 (zero-padded on the 7 / 10, 4 instances) at
          # widths 256 (bf16x6 windowed part), 128 and 64 (f32 windowed part)
-         "mr5_mrv2_s32i16_d8w256", "mr9_mrv3_s32i16_d8w128", "mr3_mrv1_s32i16_d4w64"]
+         "mr5_mrv2_s32i16_d8w256", "mr9_mrv3_s32i16_d8w128", "mr3_mrv1_s32i16_d4w64",
+         # --view_type world (un-normalised joint-frame ray directions into the view embedder)
+         "vw1_viewworld_s32i16_d8w128"]
 FRAMES = ["c1_64_s32_d4w128", "pw_64_white_d4w128", "pb_64_bgimg_d4w128"]
 
 
@@ -48,6 +50,8 @@ class Golden:
         kw = {}
         if "--density_type" in flags:
             kw["density_type"] = flags[flags.index("--density_type") + 1]
+        if "--view_type" in flags:
+            kw["extra"] = {"view_type": flags[flags.index("--view_type") + 1]}
         if "--softplus_shift" in flags:
             kw["softplus_shift"] = float(flags[flags.index("--softplus_shift") + 1])
         self.cfg = config.RenderConfig(n_joints=m["NJ"], netdepth=m["D"], netwidth=m["W"], N_samples=m["S"],

@@ -126,6 +126,9 @@ CONFIGS = {
                                         seed=27, flags=["--cut_to_dist"]),
     "cs1_cutoffshift_s32i16_d4w128": dict(H=128, NJ=24, S=32, I=16, D=4, W=128, tau=20.0, kind="rays",
                                           n_rays=128, seed=25, flags=["--cutoff_shift"]),
+    # --view_type world: IdentityExpandEncoder of the joint-frame ray directions (not normalised)
+    "vw1_viewworld_s32i16_d8w128": dict(H=128, NJ=24, S=32, I=16, D=8, W=128, tau=20.0, kind="rays", n_rays=128,
+                                        seed=29, flags=["--view_type", "world"]),
     # --cutoff_bones (the bone embedder a CutoffEmbedder with its own tau / cutoff_dist: bone directions
     # times w_b, core/raycasters.py:52-64, cutoff_embedder.py:108-166); D = 8 for the skip layer's x part
     "cb1_cutoffbones_s32i16_d8w128": dict(H=128, NJ=24, S=32, I=16, D=8, W=128, tau=20.0, kind="rays", n_rays=128,

@@ -63,6 +63,17 @@ def main():
                             ("cutoff_bones", ["--cutoff_bones"]),
                             ("cutoff_bones+multires_bones=2", ["--cutoff_bones", "--multires_bones", "2"])):
             out[name] = probe(mods, tmp, vd + flags)
+        # the non-default encoder selectors (core/raycasters.py:251-305)
+        for name, flags in (("kp_dist_type=cat", ["--kp_dist_type", "cat"]),
+                            ("kp_dist_type=relpos", ["--kp_dist_type", "relpos"]),
+                            ("kp_dist_type=querypts", ["--kp_dist_type", "querypts"]),
+                            ("view_type=rayangle", ["--view_type", "rayangle"]),
+                            ("view_type=world", ["--view_type", "world"]),
+                            ("bone_type=axisang", ["--bone_type", "axisang"])):
+            try:
+                out[name] = probe(mods, tmp, vd + flags)
+            except Exception as e:  # (raised while building the caster)
+                out[name] = {"raises": type(e).__name__, "message": str(e), "at": "create_raycaster"}
     path = os.path.join(HERE, "reference_flags.json")
     with open(path, "w") as f:
         json.dump(out, f, indent=1)

@@ -107,6 +107,27 @@ def test_no_viewdirs_refusal_matches_the_reference():
         config.RenderConfig(use_viewdirs=False).validate()
 
 
+def test_encoder_selectors_follow_the_reference():
+    """The non-default encoder selectors (core/raycasters.py:251-305) as the reference behaves on them
+    (reference_flags.json, recorded by tests/golden/probe_reference_flags.py): kp_dist_type 'cat' and
+    bone_type 'axisang' raise TypeError there and here; view_type 'world' runs there and renders here
+    (fixture vw1_viewworld_s32i16_d8w128); relpos / querypts / rayangle run there and stay refused."""
+    import json
+    with open(os.path.join(os.path.dirname(__file__), "golden", "reference_flags.json")) as f:
+        rec = json.load(f)
+    cfg = config.RenderConfig
+    for key, val in (("kp_dist_type", "cat"), ("bone_type", "axisang")):
+        assert rec[f"{key}={val}"]["raises"] == "TypeError"
+        with pytest.raises(TypeError):
+            cfg(extra={key: val}).validate()
+    assert rec["view_type=world"]["raises"] is None
+    assert cfg(extra={"view_type": "world"}).validate().extra["view_type"] == "world"
+    for key, val in (("kp_dist_type", "relpos"), ("kp_dist_type", "querypts"), ("view_type", "rayangle")):
+        assert rec[f"{key}={val}"]["raises"] is None
+        with pytest.raises(NotImplementedError):
+            cfg(extra={key: val}).validate()
+
+
 def test_config_lindisp_from_args():
     args = types.SimpleNamespace(lindisp=True, N_samples=32)
     assert config.RenderConfig.from_args(args, 24).lindisp
