@@ -287,11 +287,13 @@ __device__ __forceinline__ void split3_block_pair(const f32x16& hb, X6T (&t)[2],
 // Issue-order pins of the split layers' groups (round 3, A/B on the box, tools/gpu_ab3.sh): the
 // scheduler otherwise packs a group's split / relu work into one or two MFMA gaps.  bf16x6 +1.25 %,
 // fp16x3 +0.4 % with at most three VALU per gap (two: +1.1 %); the same pin on u_part_x6: -0.1 %.
+// The fp16 layers (round 4, with the fp16x4 four-MFMA groups): two VALU per gap +0.85 % fp16x4 over
+// three, fp16x3 neutral; one +0.55 %, four +0.2 %, five -0.8 % (profiles/r04h3il_ab*.txt)
 #ifndef ANERF_X6_IL
 #define ANERF_X6_IL 3
 #endif
 #ifndef ANERF_H3_IL
-#define ANERF_H3_IL 3
+#define ANERF_H3_IL 2
 #endif
 // One x6 group's issue order: each of the six MFMAs followed by at most one weight load and three
 // VALU instructions (the split / relu / bias work of the group), so no MFMA gap carries more than
