@@ -490,10 +490,13 @@ __device__ __forceinline__ void split2_block_pair(const f32x16& hb, float t, H3T
 
 // mlp_layer_h3's group: three MFMAs, the ring slot's four loads (even groups) after the first two
 // (NP = 3: fp16x3, NP = 4: fp16x4)
+#ifndef ANERF_H3_NLG  // (experiments: MFMAs followed by loads, loads after each; NLG x NL = 4)
+#define ANERF_H3_NLG 2
+#endif
 template <int NP>
 __device__ __forceinline__ void h3_group_schedule() {
 #if ANERF_H3_IL
-    group_schedule<NP, 2, 2, ANERF_H3_IL>();
+    group_schedule<NP, ANERF_H3_NLG, 4 / ANERF_H3_NLG, ANERF_H3_IL>();
 #endif
 }
 
