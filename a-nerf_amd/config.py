@@ -51,10 +51,12 @@ class RenderConfig:
     cutoff_bones: bool = False
     chunk: int = 4096
     ext_scale: float = 0.001
-    # MLP arithmetic: "fp32" (fp32 MFMA everywhere, the parity default), "bf16x6" (hidden layers as
-    # three-way split-bf16 products on the bf16 MFMA pipe, fp32-accurate) or "bf16x3" (two-way split,
-    # ~16-bit operands); fp32 accumulation in all (see include/anerf.h)
-    precision: str = "fp32"
+    # MLP arithmetic (include/anerf.h), fp32 accumulation in all: "fp16x4" (the default and bench.py's
+    # headline: power-of-two scaled two-way fp16 splits, all four products on the fp16 MFMA pipe,
+    # fp32-accurate to bf16x6's error bound), "fp32" (fp32 MFMA everywhere), "bf16x6"
+    # (three-way split-bf16, six products, fp32-accurate), "fp16x3" (fp16x4 without x1 w1, 22-bit
+    # operands) or "bf16x3" (two-way split-bf16, ~16-bit operands)
+    precision: str = "fp16x4"
     extra: dict = field(default_factory=dict)
 
     def validate(self):
@@ -147,7 +149,8 @@ class RenderConfig:
                   cut_to_dist=bool(g("cut_to_dist", False)), cutoff_shift=bool(g("cutoff_shift", False)),
                   normalize_cutoff=bool(g("normalize_cutoff", False)), cutoff_bones=bool(g("cutoff_bones", False)),
                   chunk=g("chunk", 4096), ext_scale=g("ext_scale", 0.001), extra=extra,
-                  precision=g("anerf_precision", "fp32") or "fp32")  # (not a reference flag: opt-in mode)
+                  # (not a reference flag: the drop-in renders in the default precision unless the caller sets it)
+                  precision=g("anerf_precision", None) or cls.precision)
         return cfg.validate()
 
 

@@ -133,9 +133,10 @@ __device__ __forceinline__ f32x16 mfma16(const bf16x8& a, const bf16x8& b, const
 __device__ __forceinline__ float pow2i(int e) { return __builtin_bit_cast(float, (e + 127) << 23); }  // |e| <= 126
 // fp16x4 row scale: the shift that puts a row's largest |value| (bits m of a non-negative float) in
 // [2^10, 2^11) (anerf_mlp.hpp h3_scale; 0 for an all-zero row)
+// (clamped to pow2i's exponent range: rows of any finite magnitude from 2^-126 up scale into fp16's range)
 __device__ __forceinline__ int f16_row_shift(int m) {
     int s = m > 0 ? 137 - (m >> 23) : 0;
-    return min(max(s, -100), 100);
+    return min(max(s, -126), 126);
 }
 
 // ---------------------------------------------------------------- forward / input gradient
@@ -932,7 +933,7 @@ __global__ __launch_bounds__(1024) void split_exponent_kernel(SplitBatch b) {
         int mm = 0;
 #pragma unroll
         for (int i = 0; i < 16; ++i) mm = max(mm, red[i]);
-        J.f16exp[0] = (mm > 0 && mm < 0x7f800000) ? min(max(137 - (mm >> 23), -100), 100) : 0;
+        J.f16exp[0] = (mm > 0 && mm < 0x7f800000) ? min(max(137 - (mm >> 23), -126), 126) : 0;
     }
 }
 
@@ -1078,6 +1079,12 @@ int anerf_mlp_gemm_rows(int64_t m, int32_t n, int32_t k, const anerf_seg* a, int
         return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_gemm: fp16x4 takes one A segment and its row maxima");
     if (!f16 && rowmax_in) return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_gemm: row maxima are fp16x4 input");
     if (rowmax_out && n % NBN) return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_gemm: row maxima need n % 128 == 0");
+    // the epilogue's row max is taken on the vector path of one aligned output segment, before any mask or
+    // accumulation: outside that case it would not be the maximum of what is stored
+    if (rowmax_out && (n_c != 1 || c[0].mask || c[0].accumulate || !c[0].p || (reinterpret_cast<uintptr_t>(c[0].p) & 15) ||
+                       (c[0].ld & 3)))
+        return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_gemm: row maxima need one 16-byte aligned output segment "
+                                                 "(ld % 4 == 0) without mask or accumulation");
     if (m == 0) return ANERF_OK;
     NTArgs g = {};
     g.M = m;
@@ -1103,7 +1110,8 @@ int anerf_mlp_gemm_rows(int64_t m, int32_t n, int32_t k, const anerf_seg* a, int
     g.nc = n_c;
     g.tiles_n = (n + NBN - 1) / NBN;
     // row-tile height: 128, or (ANERF_GEMM_BM 64) 64 for the single-segment instances
-    const int tbm = (ANERF_GEMM_BM == 64 && n_a == 1) ? 64 : 128;
+    // (the fp16x4 instance is always 128 rows high)
+    const int tbm = (ANERF_GEMM_BM == 64 && n_a == 1 && !f16) ? 64 : 128;
     const long long tiles = (long long)((m + tbm - 1) / tbm) * g.tiles_n;
     if (tiles > 0x7fffffff) return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_gemm: too many tiles");
     g.total = (int)tiles;

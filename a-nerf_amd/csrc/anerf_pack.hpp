@@ -198,11 +198,18 @@ float f16_to_f(uint16_t b) {
     return f;
 }
 
-// fp16x3 operand range: maxima in [2^T, 2^(T+1)), T = 10 (ANERF_H3_TARGET overrides: A/B studies only)
-int h3_target() {
-    const char* e = std::getenv("ANERF_H3_TARGET");
-    return e ? std::atoi(e) : 10;
-}
+// fp16 operand range of the fp16x3 / fp16x4 layers: maxima in [2^T, 2^(T+1)), T = ANERF_H3_TARGET = 10.
+// A compile-time constant (experiment builds of tools/build_ab.sh may pass -DANERF_H3_TARGET=...; the
+// shipped library never reads it from the environment).  The probe of the f16 MFMA
+// (tools/probe/mfma_f16_numerics.hip) returned wrong sums once both operands' maxima reached 2^13 (products
+// ~2^28), and matched the fp32 path at 2^12 and below: targets above 11 (maxima up to 2^12) are rejected at
+// build time, and so are targets below 6 (the low fp16 parts of ordinary values would turn subnormal).
+#ifndef ANERF_H3_TARGET
+#define ANERF_H3_TARGET 10
+#endif
+static_assert(ANERF_H3_TARGET >= 6 && ANERF_H3_TARGET <= 11,
+              "ANERF_H3_TARGET outside the probed safe range [6, 11] of the f16 MFMA");
+constexpr int h3_target() { return ANERF_H3_TARGET; }
 
 // power-of-two exponent ew with max |W[:, col_off : col_off + n_in]| 2^ew in [2^T, 2^(T+1))
 int h3_exponent(const float* Wt, int n_out, int ld, int col_off, int n_in) {

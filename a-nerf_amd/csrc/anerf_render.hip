@@ -53,6 +53,12 @@ using namespace anerf;
 #include "anerf_batch.hpp"
 #include "anerf_pack.hpp"
 
+// Experiment switches are compile-time only (tools/build_ab.sh -D...): the shipped library reads no
+// environment variable that could change its numerics or schedule.
+#ifndef ANERF_UX6
+#define ANERF_UX6 1  // split-precision bone-direction parts; 0: f32 MFMA (A/B builds only)
+#endif
+
 int anerf_internal_fail(int code, const char* msg) { return fail(code, msg); }  // for anerf_gemm.hip
 
 #ifdef ANERF_STAMPS
@@ -182,10 +188,7 @@ int anerf_model_create(const anerf_model_desc* desc, const anerf_net_weights* co
     md.cfc = desc->framecode_ch;
     md.n_codes = desc->n_framecodes;
     md.softplus = desc->density_softplus;
-    {  // bf16x6 bone-direction parts (u_part_x6); ANERF_UX6=0 keeps them on the f32 MFMA (A/B only)
-        const char* e = std::getenv("ANERF_UX6");
-        md.ux6 = !(e && e[0] == '0');
-    }
+    md.ux6 = ANERF_UX6;  // split bone-direction parts (u_part_x6); 0 only in experiment builds (tools/build_ab.sh)
     md.single_net = desc->single_net ? 1 : 0;
     // (both transforms live in the CutoffEmbedder: without use_cutoff the kp embedder is plain)
     md.cut_to = desc->use_cutoff && (desc->encoder_flags & ANERF_ENC_CUT_TO_DIST) ? 1 : 0;
@@ -295,14 +298,12 @@ int anerf_near_far(const float* ray_batch, int32_t ray_stride, int64_t n_rays, c
     return ANERF_OK;
 }
 
-// ANERF_FUSED_PASSES=1: both passes in one launch (the earlier schedule; A/B measurements only)
-static bool fused_passes() {
-    static const bool v = [] {
-        const char* e = std::getenv("ANERF_FUSED_PASSES");
-        return e && e[0] == '1';
-    }();
-    return v;
-}
+// -DANERF_FUSED_PASSES=1 (experiment builds of tools/build_ab.sh only): both passes in one launch, the
+// round-1 schedule kept for A/B measurements
+#ifndef ANERF_FUSED_PASSES
+#define ANERF_FUSED_PASSES 0
+#endif
+static constexpr bool fused_passes() { return ANERF_FUSED_PASSES != 0; }
 
 int anerf_render_rays(const anerf_model* m, const float* ray_batch, int32_t ray_stride, int64_t n_rays,
                       const float* skts, const float* cyls, int32_t n_poses, const int32_t* ray_pose,

@@ -67,7 +67,7 @@ class Golden:
                                        cutoff_bones="--cutoff_bones" in flags,
                                        init_freq=float(flags[flags.index("--init_freq") + 1])
                                        if "--init_freq" in flags else 0.0,
-                                       **kw).validate()
+                                       precision="fp32", **kw).validate()
         self.ckpt = syn.make_checkpoint(m["seed"], n_joints=m["NJ"], D=m["D"], W=m["W"], fine=m["I"] > 0,
                                         tau=m["tau"], use_framecode=fc, n_framecodes=5, multires=m.get("mr", 7),
                                         multires_views=m.get("mrv", 4), sched_alpha=m.get("sched"),

@@ -62,3 +62,13 @@ def test_null_model_render_is_rejected():
                                None, None, None, None, None, None, None, 0, None)
     assert rc == -1
     assert b"model" in lib.anerf_last_error()
+
+
+def test_library_reads_no_experiment_switches_from_the_environment():
+    """The fp16 operand range, the bone-direction part's precision and the two-launch schedule are
+    compile-time constants of the shipped library (experiment builds pass -D flags, tools/build_ab.sh):
+    none of the switch names is in the binary, so no environment variable can change a render."""
+    with open(_lib.LIB_PATH, "rb") as f:
+        blob = f.read()
+    for name in (b"ANERF_H3_TARGET", b"ANERF_UX6", b"ANERF_FUSED_PASSES"):
+        assert name not in blob, name

@@ -89,6 +89,10 @@ def test_gemm_fp16x4_row_scaled(m, n, k):
     a = torch.relu(torch.randn(m, k, device=DEV))
     a *= torch.pow(2.0, torch.randint(-40, 41, (m, 1), device=DEV).float())
     a[::97] = 0.0
+    # rows at the ends of the exponent range the row shift covers (advisor r4: the shift was clamped to
+    # +-100, so rows past ~2^110 overflowed fp16): ~2^115 and ~2^-118
+    a[1::131] = torch.relu(torch.randn_like(a[1::131])) * 2.0 ** 115
+    a[2::131] = torch.relu(torch.randn_like(a[2::131])) * 2.0 ** -118
     w = torch.randn(n, k, device=DEV) / k ** 0.5 * 1e-3
     b = torch.randn(n, device=DEV) * 1e-3
     out = torch.full((m, n), 7.0, device=DEV)
@@ -118,6 +122,12 @@ def test_gemm_fp16x4_rejects_bad_arguments():
     with pytest.raises(mlp._lib.AnerfError, match="row maxima are fp16x4"):
         mlp.gemm(64, 128, 128, [mlp._seg(x, 128)], mlp.split_weight(w), None, False, o, torch.device(DEV), 6,
                  rin=_rowmax_bits(x))
+    for oseg in ([(torch.empty(64, 128, device=DEV), 128, 128, 0, torch.ones(64, 128, device=DEV), False)],
+                 [(torch.zeros(64, 128, device=DEV), 128, 128, 0, None, True)],
+                 [(torch.empty(64, 64, device=DEV), 64, 64, 0, None, False)] * 2):
+        with pytest.raises(mlp._lib.AnerfError, match="one 16-byte aligned output segment"):
+            mlp.gemm(64, 128, 128, [mlp._seg(x, 128)], sp4, None, False, oseg, torch.device(DEV), 4,
+                     rin=_rowmax_bits(x), rout=torch.zeros(64, device=DEV, dtype=torch.int32))
     with pytest.raises(mlp._lib.AnerfError, match="n % 128"):
         mlp.gemm(64, 64, 128, [mlp._seg(x, 128)], mlp.split_weight(w[:64].contiguous()), None, False,
                  [(torch.empty(64, 64, device=DEV), 64, 64, 0, None, False)], torch.device(DEV), 6,

@@ -582,3 +582,37 @@ def test_ragged_workgroups_split_modes(precision):
     t34 = rc.last_mfma.clone()
     _render(rc, g, rb[34:37], count_mfma=True, near_far_given=True)
     assert torch.equal(t37, t34 + rc.last_mfma), (t37, t34, rc.last_mfma)
+
+
+_CHILD = r"""
+import importlib, os, sys, numpy as np, torch
+sys.path[:0] = [os.environ["ANERF_TEST_REPO"], os.path.join(os.environ["ANERF_TEST_REPO"], "tests")]
+import test_gpu_parity as t
+from _golden import Golden
+g = Golden("c3_512_s64i128_d8w256")
+res = {}
+for p in ("fp16x4", "bf16x6", "fp16x3"):
+    out = t._render(t._caster_prec(g, p), g, g.ray_batch()[:96])
+    res.update({p + "/" + k: v for k, v in out.items()})
+np.savez(os.environ["ANERF_TEST_OUT"], **res)
+"""
+
+
+def test_environment_switches_do_not_change_renders(tmp_path):
+    """a fresh process with the former A/B switches set (an fp16 operand range past
+    the f16 MFMA's safe limit, the f32 bone-direction parts, the one-launch schedule) renders exactly
+    what this process renders without them."""
+    import subprocess
+    g = Golden("c3_512_s64i128_d8w256")
+    here = {}
+    for p in ("fp16x4", "bf16x6", "fp16x3"):
+        out = _render(_caster_prec(g, p), g, g.ray_batch()[:96])
+        here.update({p + "/" + k: v for k, v in out.items()})
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, ANERF_H3_TARGET="14", ANERF_UX6="0", ANERF_FUSED_PASSES="1",
+               ANERF_TEST_REPO=repo, ANERF_TEST_OUT=str(tmp_path / "child.npz"))
+    subprocess.run([sys.executable, "-c", _CHILD], env=env, check=True, timeout=110)
+    child = np.load(tmp_path / "child.npz")
+    assert set(child.files) == set(here)
+    for k in here:
+        np.testing.assert_array_equal(child[k], here[k], err_msg=k)

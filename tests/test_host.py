@@ -146,9 +146,32 @@ def test_precision_modes_plumbing():
     for p in enum:
         assert config.RenderConfig(precision=p).validate().precision == p
         assert config.RenderConfig.from_args(types.SimpleNamespace(anerf_precision=p), 24).precision == p
-    assert config.RenderConfig.from_args(types.SimpleNamespace(), 24).precision == "fp32"
+    assert config.RenderConfig.from_args(types.SimpleNamespace(), 24).precision == "fp16x4"
     with pytest.raises(ValueError, match="precision"):
         config.RenderConfig(precision="fp16x5").validate()
+
+
+def test_drop_in_renders_in_the_benched_precision():
+    """create_raycaster(args) on a run_nerf namespace WITHOUT the non-reference `anerf_precision`
+    attribute builds the precision bench.py's headline measures: the number in
+    the bench line is what the untouched drop-in does.  The eval view of the test kwargs renders
+    through the same config."""
+    import ast
+    anerf = importlib.import_module("a-nerf_amd")
+    src = open(os.path.join(os.path.dirname(HERE), "bench.py")).read()
+    tree = ast.parse(src)
+    bench_default = None
+    for node in ast.walk(tree):
+        if (isinstance(node, ast.Call) and getattr(node.func, "attr", "") == "add_argument" and node.args
+                and isinstance(node.args[0], ast.Constant) and node.args[0].value == "--precision"):
+            bench_default = next(k.value.value for k in node.keywords if k.arg == "default")
+    assert bench_default == "fp16x4"
+    args = types.SimpleNamespace(netdepth=4, netwidth=64, N_samples=8, N_importance=0, lrate=5e-4,
+                                 basedir="/nonexistent", expname="x", no_reload=True, ft_path=None)
+    assert not hasattr(args, "anerf_precision")
+    rk_train, rk_test, *_ = anerf.create_raycaster(args, {"skel_type": 24}, device="cpu")
+    assert rk_train["ray_caster"].cfg.precision == bench_default
+    assert config.RenderConfig().precision == bench_default
 
 
 def test_config_from_args_matches_surreal_config():

@@ -1,5 +1,7 @@
 """fp16x3 bring-up probe: render the fixtures that stress it in fp32 and fp16x3 with the debug stage
-dumps, for several operand-range targets (ANERF_H3_TARGET), and report where they differ."""
+dumps and report where they differ.  The operand-range target is a compile-time constant: probe
+another one with an experiment build, `bash tools/build_ab.sh T9 -DANERF_H3_TARGET=9` and
+`ANERF_LIB_PATH=tools/ab/lib_T9.so python tools/h3_probe.py` (the config-3 shape only)."""
 import dataclasses
 import importlib
 import os
@@ -33,8 +35,7 @@ def run(g, prec):
 for name in sys.argv[1:] or ["v1_mr10_w64_d4", "v4_nocutoff", "c4_512_s64i128_j65", "h1_nanfill_s32i16_d4w128"]:
     g = Golden(name)
     o32, d32 = run(g, "fp32")
-    for T in ("10",):
-        os.environ["ANERF_H3_TARGET"] = T
+    for T in (os.path.basename(os.environ.get("ANERF_LIB_PATH", "default")),):
         o, d = run(g, "fp16x3")
         e = float(np.abs(o["rgb_map"] - o32["rgb_map"]).max())
         r, r32 = d["raw_coarse"], d32["raw_coarse"]
