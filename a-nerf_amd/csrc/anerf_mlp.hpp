@@ -524,7 +524,7 @@ __device__ __forceinline__ f32x16 mfma_h3(const float (&w)[16], int half, const 
 // lane's values, scaled into [2^10, 2^11).  es: exponent of the units the input is in; on return the units of this layer's
 // output, es + shift + ew, kept within [-100, 60] so that bias * 2^es stays finite.
 template <int RBI>
-__device__ __forceinline__ float h3_scale(const f32x16 (&a)[RBI], int& es, int ew, int top) {
+__device__ __forceinline__ float h3_scale(const f32x16 (&a)[RBI], int& es, int ew, int top, int cap = 60) {
     int m = 0;
 #pragma unroll
     for (int rb = 0; rb < RBI; ++rb)
@@ -537,8 +537,10 @@ __device__ __forceinline__ float h3_scale(const f32x16 (&a)[RBI], int& es, int e
         }
     m = max(m, __shfl_xor(m, 32));
     int shift = m > 0 ? top - (m >> 23) : 0;  // (m >> 23: the biased exponent; top = 127 + 10)
-    shift = min(shift, 60 - es - ew);
+    // (cap: the skip layer's h part keeps its output units at most 2^cap, so that the fp16 x parts'
+    // features, scaled into those units, stay in range: enc16_units)
     shift = max(shift, -100 - es - ew);
+    shift = min(shift, cap - es - ew);
     shift = min(max(shift, -126), 126);
     es += shift + ew;
     return pow2f(shift);
@@ -551,7 +553,8 @@ template <int RBO, int RBI, bool OUT_SAME, bool ALPHA, int NP = 3>
 __device__ __forceinline__ void mlp_layer_h3(f32x16 (&out)[RBO], f32x16 (&ain)[RBI], f32x16 (&h)[RBI],
                                              const float* __restrict__ bias, const float* __restrict__ wp, int lane,
                                              Ring& ring, bool preloaded, const float* __restrict__ next,
-                                             const float* __restrict__ wa, float& sig, int& es, int ew, int top) {
+                                             const float* __restrict__ wa, float& sig, int& es, int ew, int top,
+                                             int cap = 60) {
     static_assert(RBO <= RBI, "h3 layer shape");
     constexpr int NG = 2 * RBO * RBI;
     constexpr int NS = NG / 2;  // ring slots of this layer
@@ -563,7 +566,7 @@ __device__ __forceinline__ void mlp_layer_h3(f32x16 (&out)[RBO], f32x16 (&ain)[R
 #if ANERF_X6_PROBE == 4  // (diagnostic builds of tools/probe only: no per-sample scale)
     const float t = 1.0f;
 #else
-    const float t = h3_scale<RBI>(ain, es, ew, top);
+    const float t = h3_scale<RBI>(ain, es, ew, top, cap);
 #endif
     const float S = pow2f(es);
     auto convert_half = [&](int rb, int half) {  // relu of 8 inputs (+ their 8 scaled bias outputs)
@@ -1275,6 +1278,128 @@ __device__ __forceinline__ void v_part_x6(f32x16 (&acc)[RB], const ModelDev& M, 
     }
 }
 
+// ---- fp16 encoder-fed parts (fp16x4 NP = 4, fp16x3 NP = 3; ModelDev::enc16): u_part_x6 / v_part_x6 with
+// the features times a power of two t (the part's units, enc16_units: layer 0 a constant, the skip layer
+// per sample) split into two fp16 parts (split2_pair) against weight groups of 8 floats = fragments
+// [w0, w1] (pack_upart_h / pack_vpart_h), NP products per 16 k instead of bf16x6's six.
+template <int RB>
+__device__ __forceinline__ void u_part_h_preload(const float* __restrict__ wp, int lane, Ring& ring) {
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(wp);
+#pragma unroll
+    for (int g = 0; g < 3; ++g) load_group<8>(ring.v[g], rs, lane, g);
+}
+
+template <int RB, int NP>
+__device__ __forceinline__ void u_part_h(f32x16 (&acc)[RB], const ModelDev& M, const float* __restrict__ wp,
+                                         const float* __restrict__ uf, int lane, Ring& ring, bool preloaded, float t) {
+    static_assert(RB % 4 == 0 && RB >= 4, "u_part_h needs RB % 4 == 0");
+    constexpr int PD = 3;
+    const int nq = 3 * M.njh2, ns = (nq + 7) / 8, ng = ns * RB;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(wp);
+    if (!preloaded) u_part_h_preload<RB>(wp, lane, ring);
+    auto feat = [&](int q) { return mask_f(uf[min(q, nq - 1) * 64 + lane], q < nq); };  // (as u_part_x6)
+    H3T cur, nxt;
+    float fn[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) split2_pair(feat(2 * e), feat(2 * e + 1), t, cur, e);
+    for (int s = 0; s < ns; ++s) {
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) {
+            const int g = s * RB + rb;
+            __builtin_amdgcn_sched_barrier(0);
+            load_group<8>(ring.v[(rb + PD) % 4], rs, lane, min(g + PD, ng - 1));
+            if (rb == 0) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) fn[j] = feat(8 * (s + 1) + j);
+            }
+            acc[rb] = mfma_h3<NP>(ring.v[rb % 4], 0, cur, acc[rb]);
+            if (rb >= RB - 4) {
+                const int e = rb - (RB - 4);
+                split2_pair(fn[2 * e], fn[2 * e + 1], t, nxt, e);
+            }
+        }
+        cur = nxt;
+    }
+}
+
+template <int RB, int MR, int NP>
+__device__ __forceinline__ void v_part_h(f32x16 (&acc)[RB], const ModelDev& M, const float* __restrict__ wp,
+                                         const float* __restrict__ sk, const float* __restrict__ cut, float px,
+                                         float py, float pz, int lane, JointMask mask, Ring& ring, float t) {
+    static_assert(RB % 4 == 0, "v_part_h keeps ring slots static: groups per joint % 4 == 0");
+    constexpr int NG = VPartX6<MR, 1>::KS * RB, PD = 3;  // groups per joint
+    using V = VPartX6<MR, NG>;
+    constexpr int KS = V::KS, NF = V::NF, PER = V::PER;
+    const int hh = lane >> 5;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(wp);
+    const bool dist_in = M.use_cutoff && M.cutoff_inputs;
+    uint64_t r0 = uniform64(mask.m0), r1 = uniform64(mask.m1);
+    int j = mask_pop(r0, r1);
+    if (j < 0) return;
+    int jn = mask_pop(r0, r1);
+#pragma unroll
+    for (int d = 0; d < PD; ++d) load_group<8>(ring.v[d], rs, lane, j * NG + d);
+    H3T cur[KS];
+    {
+        float f[NF];
+        float dist, w, u, uf;
+        v_geom(M, sk, cut, j, px, py, pz, dist, w);
+        kp_inputs(M.cut_to, M.shift_in, dist, cut[j], u, uf);
+#pragma unroll
+        for (int q = 0; q < MR; ++q) {
+            float sn, cs;
+            sincos_rr(uf * (float)(1 << q), sn, cs);
+            f[q] = (hh ? cs : sn) * w;
+        }
+        f[MR] = hh ? 0.0f : (dist_in ? u * w : u);
+#pragma unroll
+        for (int q = MR + 1; q < NF; ++q) f[q] = 0.0f;
+#pragma unroll
+        for (int e = 0; e < NF / 2; ++e) split2_pair(f[2 * e], f[2 * e + 1], t, cur[e / 4], e % 4);
+    }
+    while (j >= 0) {
+        H3T nxt[KS];
+        float fn[NF];
+        float dn = 0.0f, dfn = 0.0f, wn = 0.0f;  // next joint: raw input, frequency input, window
+        const int jg = jn >= 0 ? jn : j;          // (a harmless redo of this joint after the last)
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            const int s = g / RB, rb = g % RB;
+            __builtin_amdgcn_sched_barrier(0);
+            const int gp = g + PD;
+            load_group<8>(ring.v[gp % 4], rs, lane, gp < NG ? j * NG + gp : jg * NG + gp - NG);
+            acc[rb] = mfma_h3<NP>(ring.v[g % 4], 0, cur[s], acc[rb]);
+            if (g == 0) {
+                float dd;
+                v_geom(M, sk, cut, jg, px, py, pz, dd, wn);
+                kp_inputs(M.cut_to, M.shift_in, dd, cut[jg], dn, dfn);
+                pin(dn), pin(dfn), pin(wn);
+            } else {
+#pragma unroll
+                for (int q = (g - 1) * PER; q < g * PER && q < MR; ++q) {
+                    float sn, cs;
+                    sincos_rr(dfn * (float)(1 << q), sn, cs);
+                    fn[q] = (hh ? cs : sn) * wn;
+                    pin(fn[q]);
+                }
+            }
+            if (g == 1) {
+                fn[MR] = hh ? 0.0f : (dist_in ? dn * wn : dn);
+#pragma unroll
+                for (int q = MR + 1; q < NF; ++q) fn[q] = 0.0f;
+            }
+#pragma unroll
+            for (int e = 0; e < NF / 2; ++e)
+                if (V::pair_ready(e) == g) split2_pair(fn[2 * e], fn[2 * e + 1], t, nxt[e / 4], e % 4);
+            interleave_mfma_valu<NP, 6>();
+        }
+#pragma unroll
+        for (int k = 0; k < KS; ++k) cur[k] = nxt[k];
+        j = jn;
+        jn = mask_pop(r0, r1);
+    }
+}
+
 // View layer, per-ray direction part: acc[RBV] += G^T * [w'_j, 1]  (G in LDS).  k-step p pairs
 // joint p (lane half 0) with joint p + NJH2 (half 1), exactly the u part's pairing, so w'_j comes
 // from the u part (wvp, stored per lane); k-step NJH2 adds the bias / framecode column NJ.  The G
@@ -1339,11 +1464,26 @@ __device__ __forceinline__ bool mlp_trunk(const ModelDev& M, const NetDev& net, 
     // bf16x6 / fp16x3 with the LDS feature store: features in a VALU pass, both bone-direction parts as x6
     constexpr bool UX6 = (P >= 2) && (RB % 4 == 0);
     const bool ux6 = UX6 && M.ux6 && uf != nullptr;
+    // fp16x4 / fp16x3 with bounded windowed features: the encoder-fed parts as fp16 splits (NP products),
+    // in units 2^enc_e0 (layer 0) and below 2^enc_cap (the skip layer), enc16_units
+    constexpr bool H16 = (P >= 3) && UX6;
+    constexpr int NPH = P == 4 ? 4 : 3;
+    const bool enc16 = H16 && ux6 && M.enc16;
     if (!ux6) ring_preload<2 * RB>(ring, net.wl[0], lane);  // the u part's first groups, early
     load_bias<RB>(acc, bias, hh);
+    if (enc16) {  // (a power of two: exact)
+        const float s0 = pow2f(net.enc_e0);
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) acc[rb] = acc[rb] * s0;
+    }
     STAMP(st, 10);
     const float* const* wl = P >= 3 ? net.wlh : (P == 2 ? net.wl6 : (P ? net.wl3 : net.wl));  // hidden-layer streams
-    if (ux6) {
+    if (enc16) {
+        if constexpr (H16) u_part_h_preload<RB>(net.wuh[0], lane, ring);  // (latency under the VALU pass)
+        u_features_lds<WV>(M, sk, cut, px, py, pz, lane, &mask, uf, wvo);
+        STAMP(st, 14);
+        if constexpr (H16) u_part_h<RB, NPH>(acc, M, net.wuh[0], uf, lane, ring, true, pow2f(net.enc_e0 - net.ewh_u[0]));
+    } else if (ux6) {
         if constexpr (UX6) u_part_x6_preload<RB>(net.wu6, lane, ring);  // (latency under the VALU pass)
         u_features_lds<WV>(M, sk, cut, px, py, pz, lane, &mask, uf, wvo);
         STAMP(st, 14);
@@ -1356,10 +1496,16 @@ __device__ __forceinline__ bool mlp_trunk(const ModelDev& M, const NetDev& net, 
     STAMP(st, 8);
     // (precision modes 2 / 3: the windowed parts as bf16x6; the u part's ring groups are consumed)
     constexpr bool VX6 = (P >= 2) && (RB % 4 == 0);
-    if constexpr (VX6)
+    if (enc16) {
+        if constexpr (H16)
+            v_part_h<RB, MR, NPH>(acc, M, net.wvh[0], sk, cut, px, py, pz, lane, mask, ring,
+                                  pow2f(net.enc_e0 - net.ewh_v[0]));
+        es = net.enc_e0;
+    } else if constexpr (VX6) {
         v_part_x6<RB, MR>(acc, M, net.wv6, sk, cut, px, py, pz, lane, mask, ring);
-    else
+    } else {
         v_part<RB, MR>(acc, M, net.wl0v, sk, cut, px, py, pz, lane, mask, st);
+    }
     STAMP(st, 9);
     bool pre6 = false;
     for (int L = 1; L < M.D; ++L) {
@@ -1386,7 +1532,7 @@ __device__ __forceinline__ bool mlp_trunk(const ModelDev& M, const NetDev& net, 
             // units the h part left in the accumulators)
             const float* nxth = skl ? nullptr : after;
             mlp_layer_h3<RB, RB, true, false, P == 4 ? 4 : 3>(acc, acc, h, bias + L * W, wl[L], lane, ring, pre6, nxth, nullptr,
-                                              nosig, es, net.ewl[L], M.h3_top);
+                                              nosig, es, net.ewl[L], M.h3_top, (skl && enc16) ? net.enc_cap : 60);
             pre6 = nxth != nullptr;
             if (skl) {  // the f32 skip x parts take their first groups from the ring (the x6 one loads itself)
                 if (!ux6) ring_preload<2 * RB>(ring, net.wskipu, lane);
@@ -1413,7 +1559,14 @@ __device__ __forceinline__ bool mlp_trunk(const ModelDev& M, const NetDev& net, 
             if (skl && !HANDOFF) ring_preload<2 * RB>(ring, net.wskipu, lane);
         }
         STAMP(st, 11);
-        if (skl) {  // x part after the h part (in the h part's units: B operands times xs)
+        if (skl && enc16) {  // fp16 x parts, their features scaled into the h part's per-sample units
+            if constexpr (H16) {
+                u_part_h<RB, NPH>(acc, M, net.wuh[1], uf, lane, ring, false, pow2f(max(es - net.ewh_u[1], -126)));
+                v_part_h<RB, MR, NPH>(acc, M, net.wvh[1], sk, cut, px, py, pz, lane, mask, ring,
+                                      pow2f(max(es - net.ewh_v[1], -126)));
+            }
+            STAMP(st, 12);
+        } else if (skl) {  // x part after the h part (in the h part's units: B operands times xs)
             const float xs = P >= 3 ? pow2f(es) : 1.0f;
             if (ux6) {
                 if constexpr (UX6) u_part_x6<RB>(acc, M, net.wskipu6, uf, lane, ring, P == 2, xs);
@@ -1497,11 +1650,12 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
         const int act = __builtin_popcountll(mask.m0) + __builtin_popcountll(mask.m1);
         const bool ux6 = (P >= 2) && (RB % 4 == 0) && uf != nullptr && M.ux6;  // as in mlp_trunk
         constexpr bool vx6 = (P >= 2) && (RB % 4 == 0);
+        const int npe = (P >= 3 && ux6 && M.enc16) ? (P == 4 ? 4 : 3) : 6;  // products of the encoder-fed parts
         const int xk = (ux6 ? 0 : 3 * M.njh2) + (vx6 ? 0 : act * VPart<MR>::KB);  // f32 k-steps of one x part
         long long k = (long long)xk * RB + (long long)vsteps * RBV;
         const int nx = (M.skip + 1 < M.D) ? 2 : 1;
-        if (ux6) atomicAdd(mfma_count + 1, (unsigned long long)(nx * ((3 * M.njh2 + 7) / 8) * RB * 6));
-        if (vx6) atomicAdd(mfma_count + 1, (unsigned long long)(nx * act * VPartX6<MR, 1>::KS * RB * 6));
+        if (ux6) atomicAdd(mfma_count + 1, (unsigned long long)(nx * ((3 * M.njh2 + 7) / 8) * RB * npe));
+        if (vx6) atomicAdd(mfma_count + 1, (unsigned long long)(nx * act * VPartX6<MR, 1>::KS * RB * npe));
         constexpr int NPR = P == 2 ? 6 : (P == 4 ? 4 : 3);  // products per k16-step
         if (P >= 2)  // view layer, bf16x6 / fp16x3 / fp16x4
             atomicAdd(mfma_count + 1, (unsigned long long)(RBV * RB * 2 * NPR));

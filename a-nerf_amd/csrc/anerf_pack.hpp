@@ -338,6 +338,53 @@ std::vector<float> pack_vpart_x6(const float* Wt, int n_out, int ld, int nj, int
     });
 }
 
+// ---- fp16 split of the encoder-fed parts (fp16x4 / fp16x3 with ModelDev::enc16): the weights of a part
+// scaled by 2^ew (its own h3_exponent), then w = w0 + w1 in fp16 (RNE of the running remainder), groups of
+// 8 floats = fragments [w0, w1] (element j of lane half h as in pack_upart_x6 / pack_vpart_x6), one group
+// per ring slot (u_part_h / v_part_h).
+uint32_t f16_split_bits(float a, float b, int part) {
+    const uint16_t a0 = f16_rne(a), b0 = f16_rne(b);
+    const uint16_t va = part ? f16_rne(a - f16_to_f(a0)) : a0, vb = part ? f16_rne(b - f16_to_f(b0)) : b0;
+    return (uint32_t)va | ((uint32_t)vb << 16);
+}
+
+std::vector<float> pack_upart_h(const float* Wt, int n_out, int ld, int nj, int njh2, int mr, int ew) {
+    const int nv = 1 + 2 * mr, RB = n_out / 32, nq = 3 * njh2, ns = (nq + 7) / 8;
+    const float sc = std::ldexp(1.0f, ew);
+    return pack_groups(ns * RB, 8, [&](int g, int sl, int l) {
+        const int s = g / RB, rb = g % RB, f = sl >> 2, e = sl & 3;
+        const int h = l >> 5, row = 32 * rb + (l & 31);
+        float v[2];
+        for (int jj = 0; jj < 2; ++jj) {
+            const int q = 8 * s + 2 * e + jj, joint = q / 3 + h * njh2, c = q % 3;
+            v[jj] = (q < nq && joint < nj) ? Wt[(size_t)row * ld + nv * nj + 3 * joint + c] * sc : 0.0f;
+        }
+        const uint32_t bits = f16_split_bits(v[0], v[1], f);
+        float out;
+        std::memcpy(&out, &bits, 4);
+        return out;
+    });
+}
+
+std::vector<float> pack_vpart_h(const float* Wt, int n_out, int ld, int nj, int mr, int mrl, int ew) {
+    const int RB = n_out / 32, ks = (mrl + 1 + 7) / 8;
+    const float sc = std::ldexp(1.0f, ew);
+    return pack_groups(nj * ks * RB, 8, [&](int g, int sl, int l) {
+        const int j = g / (ks * RB), s = (g / RB) % ks, rb = g % RB, f = sl >> 2, e = sl & 3;
+        const int h = l >> 5, row = 32 * rb + (l & 31);
+        float v[2];
+        for (int jj = 0; jj < 2; ++jj) {
+            const int q = 8 * s + 2 * e + jj;
+            const int col = q < mr ? (1 + 2 * q + h) * nj + j : (q == mrl && h == 0 ? j : -1);
+            v[jj] = col >= 0 ? Wt[(size_t)row * ld + col] * sc : 0.0f;
+        }
+        const uint32_t bits = f16_split_bits(v[0], v[1], f);
+        float out;
+        std::memcpy(&out, &bits, 4);
+        return out;
+    });
+}
+
 // per-lane-half vectors [rb][h][16] of a length-n vector in accumulator row order
 std::vector<float> pack_rowvec(const float* v, int n, bool half_major) {
     const int RB = n / 32;
@@ -360,7 +407,45 @@ struct anerf_model {
     float* dev_buf;
     size_t dev_bytes;
     ModelDev md;
+    std::vector<float> cut_host;  // the kp embedder's cutoff distances (enc16_units)
 };
+
+// Units of the fp16 encoder-fed parts (fp16x4 / fp16x3).  Their features are bounded: the bone directions
+// |u_j| <= 1 (times w_b <= 1), the windowed sin / cos times w_j in [-1, 1], and -- with sparse windows --
+// the distance input |dist w_j| (|(c_j - dist) w_j| under --cut_to_dist) < max(|c_j|, c_j + 16.69 / tau):
+// w_j is exactly 0 beyond d^2 >= thr2_j = (c_j + 16.69 / tau)^2 (1 + 1e-5) (live_thr2).  So fixed powers of
+// two put them in fp16's range, like the hidden layers' per-sample scales: the bone directions times 2^T,
+// the windowed features times 2^fv with 2^fv x their bound < 2^(T+1).  Layer 0's accumulators hold the
+// output times 2^e0, e0 = min(ew_u + T, ew_v + fv) (ew: the part's weight exponent), so neither feature set
+// passes 2^(T+1) scaled; the skip layer's h part keeps its per-sample units below 2^cap, cap = min(ew_u' + T,
+// ew_v' + fv), for the same reason.  Without bounded windows (no cutoff inputs, tau <= 0) or with extreme
+// weight exponents the parts stay bf16x6 (enc16 = 0).
+static void enc16_units(anerf_model* m) {
+    ModelDev& md = m->md;
+    md.enc16 = 0;
+    for (int i = 0; i < 2; ++i) md.net[i].enc_e0 = 0, md.net[i].enc_cap = 60;
+    if (!md.sparse || !(md.tau > 0.0f) || !std::isfinite(md.tau)) return;
+    double vb = 1.0;
+    for (const float c : m->cut_host) {
+        if (!std::isfinite(c)) return;
+        vb = std::max(vb, std::max(std::fabs((double)c), (double)c + 16.69 / (double)md.tau) * 1.001);
+    }
+    if (!(vb < 1e30)) return;
+    int eb;
+    std::frexp(vb, &eb);  // vb < 2^eb
+    const int T = h3_target(), fv = T + 1 - eb;
+    for (int i = 0; i < 2; ++i) {
+        NetDev& n = md.net[i];
+        const bool skip = n.wuh[1] != nullptr;
+        const int e0 = std::min(n.ewh_u[0] + T, n.ewh_v[0] + fv);
+        const int cap = skip ? std::min(n.ewh_u[1] + T, n.ewh_v[1] + fv) : 60;
+        for (int e : {n.ewh_u[0], n.ewh_v[0], n.ewh_u[1], n.ewh_v[1], e0, cap})
+            if (e < -60 || e > 60) return;
+        n.enc_e0 = e0;
+        n.enc_cap = cap;
+    }
+    md.enc16 = 1;
+}
 
 template <int WIDTH>
 static void host_row_sum(const float* x, int64_t xs, int64_t n, float* out) {
@@ -541,6 +626,20 @@ static int pack_net(const anerf_model_desc* d, int njh2, const anerf_net_weights
         offs.push_back(pk.add(pack_vpart_x6(w->pts_w[skl], W, cin + W, nj, mr, mrl)));
     else
         offs.push_back((size_t)-1);
+    // fp16 encoder-fed parts (u: columns nv nj .. cin, v: columns 0 .. nv nj), each with its own exponent:
+    // layer 0's, then the skip layer's (exponent 0 / no buffer without a skip layer)
+    for (int part = 0; part < 2; ++part) {
+        const bool has = part == 0 || skl < d->net_depth;
+        const float* Wp = part == 0 ? w->pts_w[0] : (has ? w->pts_w[skl] : nullptr);
+        const int ld = part == 0 ? cin : cin + W;
+        const int nv = 1 + 2 * mr;
+        const int ewu = has ? h3_exponent(Wp, W, ld, nv * nj, 3 * nj) : 0;
+        const int ewv = has ? h3_exponent(Wp, W, ld, 0, nv * nj) : 0;
+        offs.push_back((size_t)(int64_t)ewu);
+        offs.push_back(has ? pk.add(pack_upart_h(Wp, W, ld, nj, njh2, mr, ewu)) : (size_t)-1);
+        offs.push_back((size_t)(int64_t)ewv);
+        offs.push_back(has ? pk.add(pack_vpart_h(Wp, W, ld, nj, mr, mrl, ewv)) : (size_t)-1);
+    }
     return ANERF_OK;
 }
 
@@ -582,6 +681,14 @@ static void bind_net(const anerf_model_desc* d, const float* base, const std::ve
     nd.wv6 = base + o[k++];
     nd.wskipv6 = o[k] == (size_t)-1 ? nullptr : base + o[k];
     ++k;
+    for (int part = 0; part < 2; ++part) {
+        nd.ewh_u[part] = (int)(int64_t)o[k++];
+        nd.wuh[part] = o[k] == (size_t)-1 ? nullptr : base + o[k];
+        ++k;
+        nd.ewh_v[part] = (int)(int64_t)o[k++];
+        nd.wvh[part] = o[k] == (size_t)-1 ? nullptr : base + o[k];
+        ++k;
+    }
     nd.balpha = balpha;
 }
 

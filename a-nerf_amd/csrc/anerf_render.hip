@@ -207,6 +207,8 @@ int anerf_model_create(const anerf_model_desc* desc, const anerf_net_weights* co
     bind_net(desc, dbuf, oc, coarse->alpha_b[0], md.net[0]);
     if (desc->has_fine) bind_net(desc, dbuf, of, fine->alpha_b[0], md.net[1]);
     else md.net[1] = md.net[0];
+    m->cut_host.assign(embed->cutoff_dist, embed->cutoff_dist + nj);
+    enc16_units(m);
     *out = m;
     return ANERF_OK;
 }
@@ -242,6 +244,8 @@ int anerf_model_set_embed(anerf_model* m, const anerf_embed_params* embed) {
     m->md.tau = embed->tau;
     m->md.tau_v = embed->tau_v;
     if (m->md.bone_cut) m->md.tau_b = embed->tau_b;
+    if (embed->cutoff_dist) m->cut_host.assign(embed->cutoff_dist, embed->cutoff_dist + m->desc.n_joints);
+    enc16_units(m);  // (the windowed features' bound moves with tau and the cutoffs)
     return ANERF_OK;
 }
 

@@ -64,6 +64,13 @@ struct NetDev {
     const float* wlh[MAXL];  // [i>0] activation parts as fp16x3 fragments (pack_layer_h3), scaled by 2^ewl[i]
     const float* wviewh;     // wview as fp16x3 fragments, scaled by 2^ew_view
     int ewl[MAXL], ew_view;
+    // fp16 encoder-fed parts (ModelDev::enc16): [0] layer 0, [1] the skip layer (null without one); the
+    // bone-direction (u) and windowed (v) weights scaled by 2^ewh_u / 2^ewh_v (pack_upart_h, pack_vpart_h)
+    const float* wuh[2];
+    const float* wvh[2];
+    int ewh_u[2], ewh_v[2];
+    int enc_e0;   // exponent of layer 0's accumulator units (enc16)
+    int enc_cap;  // the largest exponent of the skip layer's accumulator units its x parts' features allow
     float balpha;
 };
 
@@ -76,6 +83,10 @@ struct ModelDev {
     int h3_top;      // fp16x3: biased exponent the largest scaled activation of a sample gets (127 + 10)
     int bone_cut;    // --cutoff_bones (+ use_cutoff, cutoff_inputs): bone directions times w_b
     int view_raw;    // --view_type world: the view input is R_j d, not normalised (ANERF_ENC_VIEW_RAW)
+    // fp16x4 / fp16x3: the encoder-fed parts (bone-direction and windowed x parts of layer 0 and the skip
+    // layer) as fp16 splits too, when every windowed feature is bounded (sparse windows, tau > 0; host:
+    // enc16_units in anerf_pack.hpp); bf16x6 parts otherwise
+    int enc16;
     float shift, B, tau, tau_v, tau_b;
     const float* cutoff;
     const float* cutoff_v;

@@ -200,7 +200,11 @@ def test_create_raycaster_training_drop_in(tmp_path):
     sk = torch.from_numpy(g["skts"]).to(dev)
     cy = torch.from_numpy(g["cyls"]).to(dev)
     te0 = anerf.render(None, None, None, chunk=4096, rays=(rays[:, :3], rays[:, 3:6]), skts=sk, cyls=cy, **te_kw)
-    ref = anerf.RayCaster(g.cfg, g.ckpt).render_rays(rays, m["S"], skts=sk, cyls=cy, N_importance=m["I"])
+    # (the drop-in renders in the default precision, fp16x4: the same kernel as a RayCaster in that mode)
+    import dataclasses
+    assert tr_kw["ray_caster"].cfg.precision == "fp16x4"
+    ref = anerf.RayCaster(dataclasses.replace(g.cfg, precision="fp16x4"), g.ckpt).render_rays(
+        rays, m["S"], skts=sk, cyls=cy, N_importance=m["I"])
     assert torch.equal(te0["rgb_map"], ref["rgb_map"])
     out = anerf.render(None, None, None, chunk=4096, rays=(rays[:, :3], rays[:, 3:6]), skts=sk, cyls=cy, **tr_kw)
     loss = train.nerf_loss(out, torch.from_numpy(g["target"]).to(dev))
