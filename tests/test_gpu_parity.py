@@ -531,12 +531,15 @@ def test_split_modes_execute_16bit_mfmas(precision, per_block):
     # per 32-sample block (W 256: RB 8, RBV 4, 7 hidden layers, NJH2 12, skip layer present):
     #   hidden 32x32 blocks: 16 f32 MFMAs (k = 2) -> 2 k16-steps x 6 (bf16x6), x 4 (fp16x4) or x 3 (fp16x3)
     #   fused view layer (128 x 256): 64 x 4 f32 -> 4 x 8 x per_block
-    #   two bone-direction x parts (36 features, bf16x6 in both modes): 36 x 8 f32 -> ceil(36 / 8) x 8 x 6
-    # and per live joint of a block, two windowed x parts (16 features, bf16x6 in both modes):
-    #   8 k-steps x 8 f32 each -> one k16-step x 8 x 6
+    #   two bone-direction x parts (36 features): 36 x 8 f32 -> ceil(36 / 8) x 8 x enc
+    # and per live joint of a block, two windowed x parts (16 features):
+    #   8 k-steps x 8 f32 each -> one k16-step x 8 x enc
+    # enc: products of the encoder-fed parts, bf16x6's six, or the fp16 modes' own count (ModelDev.enc16:
+    # this fixture's windows are bounded)
+    enc = 6 if precision == "bf16x6" else per_block // 2
     f32_removed = 7 * 64 * 16 + 128 * 4 + 2 * 36 * 8
-    bf16_added = 7 * 64 * per_block + 4 * 8 * per_block + 2 * 5 * 8 * 6
-    f32_joint, bf16_joint = 2 * 8 * 8, 2 * 8 * 6
+    bf16_added = 7 * 64 * per_block + 4 * 8 * per_block + 2 * 5 * 8 * enc
+    f32_joint, bf16_joint = 2 * 8 * 8, 2 * 8 * enc
     # two equations in the block count and the live-joint count: both must come out as the 64 rays'
     # 2 + 6 blocks and a whole number of live joints
     diff = f32_only - n_f32
