@@ -47,11 +47,21 @@ __device__ __forceinline__ void render_item(const ModelDev& M, const RenderArgs&
         const float nearv = lds[P.ray + 16 * r + 7], farv = lds[P.ray + 16 * r + 8];
         lds[P.zc + P.z_stride * r + s] = lineseg_z(nearv, farv, t, A.lindisp != 0);
     }
-    if (A.pass0 == 1)  // fine-only launch: the sorted fine z of the coarse launch
-        for (int idx = tid; idx < nr * T; idx += blockDim.x) {
-            const int r = idx / T, s = idx % T;
-            lds[P.zf + P.z_stride * r + s] = __builtin_nontemporal_load(A.zf_ws + (ray0 + r) * T + s);
+    if (A.pass0 == 1) {  // fine-only launch: the sorted fine z of the coarse launch
+        // (16 B per lane: the item's nr x T floats are one contiguous run, rows 16-B aligned)
+        if (T % 4 == 0 && (reinterpret_cast<uintptr_t>(A.zf_ws) & 15) == 0) {
+            const f32x4* src = reinterpret_cast<const f32x4*>(A.zf_ws + ray0 * T);
+            for (int idx = tid; idx < nr * T / 4; idx += blockDim.x) {
+                const int r = (4 * idx) / T, s = (4 * idx) % T;
+                *reinterpret_cast<f32x4*>(lds + P.zf + P.z_stride * r + s) = __builtin_nontemporal_load(src + idx);
+            }
+        } else {
+            for (int idx = tid; idx < nr * T; idx += blockDim.x) {
+                const int r = idx / T, s = idx % T;
+                lds[P.zf + P.z_stride * r + s] = __builtin_nontemporal_load(A.zf_ws + (ray0 + r) * T + s);
+            }
         }
+    }
     __syncthreads();
 
     Stamps st;
@@ -182,12 +192,22 @@ __device__ __forceinline__ void render_item(const ModelDev& M, const RenderArgs&
         __syncthreads();
         STAMP(st, 3 + 2 * pass);
     }
-    if (I > 0 && A.pass1 == 1)  // coarse-only launch: hand the fine z over
-        for (int idx = tid; idx < nr * T; idx += blockDim.x) {
-            const int r = idx / T, s = idx % T;
-            // (non-temporal: 0.8 KB per ray streams through L2 and would evict weight groups)
-            __builtin_nontemporal_store(lds[P.zf + P.z_stride * r + s], A.zf_ws + (ray0 + r) * T + s);
+    if (I > 0 && A.pass1 == 1) {  // coarse-only launch: hand the fine z over
+        // (non-temporal: 0.8 KB per ray streams through L2 and would evict weight groups; 16 B per lane where
+        // T % 4 == 0 -- whole 64-B lines per quarter wave instead of 4-B pieces)
+        if (T % 4 == 0 && (reinterpret_cast<uintptr_t>(A.zf_ws) & 15) == 0) {
+            f32x4* dst = reinterpret_cast<f32x4*>(A.zf_ws + ray0 * T);
+            for (int idx = tid; idx < nr * T / 4; idx += blockDim.x) {
+                const int r = (4 * idx) / T, s = (4 * idx) % T;
+                __builtin_nontemporal_store(*reinterpret_cast<const f32x4*>(lds + P.zf + P.z_stride * r + s), dst + idx);
+            }
+        } else {
+            for (int idx = tid; idx < nr * T; idx += blockDim.x) {
+                const int r = idx / T, s = idx % T;
+                __builtin_nontemporal_store(lds[P.zf + P.z_stride * r + s], A.zf_ws + (ray0 + r) * T + s);
+            }
         }
+    }
     STAMP_FLUSH(st, A.stamps);
 }
 

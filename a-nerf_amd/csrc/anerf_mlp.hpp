@@ -470,13 +470,40 @@ __device__ __forceinline__ float pow2f(int e) { return __builtin_bit_cast(float,
 // part rounds x to 11 significant bits in the f32 encoding (exact in fp16), the low part is the
 // exact remainder rounded to nearest even (v_cvt_pk_f16_f32), so x0 + x1 is within 2^-23 |x| of x
 // (a quarter of the values are not exact: the remainder can need 12 bits)
+#ifndef ANERF_SPLIT_MIX
+#define ANERF_SPLIT_MIX 1
+#endif
+#ifdef ANERF_H3_STAMPS  // (tools/probe/h4_probe.hip -DPROBE_STAMPS only: per-phase cycles of a layer, summed
+                        // into ANERF_H3_STAMPS[4] = preamble, lead groups, middle blocks, last block)
+#define ANERF_H3_HOOK(b)                                                       \
+    do {                                                                       \
+        const unsigned long long now_ = __builtin_amdgcn_s_memtime();          \
+        ph_acc[ph_cur] += now_ - ph_last;                                      \
+        ph_last = now_;                                                        \
+        ph_cur = (b);                                                          \
+    } while (0)
+#else
+#define ANERF_H3_HOOK(b) do { } while (0)
+#endif
 __device__ __forceinline__ void split2_pair(float a, float b, float t, H3T& T, int q) {
     typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
     const float xa = a * t, xb = b * t;
+#if ANERF_SPLIT_MIX
+    // (round 5) the high parts as one RNE conversion of the pair, the remainders x - x0 read the fp16 high
+    // part straight from the packed pair by v_fma_mix_f32 (exact: x - x0 fits 13 bits), then one RNE
+    // conversion: 4 instructions per pair where the integer rounding took 6
+    const unsigned hi = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2{xa, xb}), f16x2));
+    float la, lb;
+    asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(la) : "v"(hi), "v"(xa));
+    asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(lb) : "v"(hi), "v"(xb));
+    T.d[0][q] = hi;
+    T.d[1][q] = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2{la, lb}), f16x2));
+#else
     const float ha = __builtin_bit_cast(float, (__builtin_bit_cast(unsigned, xa) + 0x1000u) & 0xffffe000u);
     const float hb = __builtin_bit_cast(float, (__builtin_bit_cast(unsigned, xb) + 0x1000u) & 0xffffe000u);
     T.d[0][q] = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_pkrtz(ha, hb));
     T.d[1][q] = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2{xa - ha, xb - hb}), f16x2));
+#endif
 }
 
 __device__ __forceinline__ void split2_block_pair(const f32x16& hb, float t, H3T (&T)[2], int p) {
@@ -493,10 +520,14 @@ __device__ __forceinline__ void split2_block_pair(const f32x16& hb, float t, H3T
 #ifndef ANERF_H3_NLG  // (experiments: MFMAs followed by loads, loads after each; NLG x NL = 4)
 #define ANERF_H3_NLG 2
 #endif
-template <int NP>
+#ifndef ANERF_H3_LEAD_IL  // VALU per MFMA gap in the lead groups (input copies + bias initialisation; round 5
+                          // A/B: 4 +0.2 % over 2, 6 -0.2 %, profiles/r05e_ab.txt)
+#define ANERF_H3_LEAD_IL 4
+#endif
+template <int NP, int NV = ANERF_H3_IL>
 __device__ __forceinline__ void h3_group_schedule() {
 #if ANERF_H3_IL
-    group_schedule<NP, ANERF_H3_NLG, 4 / ANERF_H3_NLG, ANERF_H3_IL>();
+    group_schedule<NP, ANERF_H3_NLG, 4 / ANERF_H3_NLG, NV>();
 #endif
 }
 
@@ -556,6 +587,10 @@ __device__ __forceinline__ void mlp_layer_h3(f32x16 (&out)[RBO], f32x16 (&ain)[R
                                              const float* __restrict__ wa, float& sig, int& es, int ew, int top,
                                              int cap = 60) {
     static_assert(RBO <= RBI, "h3 layer shape");
+#ifdef ANERF_H3_STAMPS
+    unsigned long long ph_last = __builtin_amdgcn_s_memtime(), ph_acc[4] = {0, 0, 0, 0};
+    int ph_cur = 0;
+#endif
     constexpr int NG = 2 * RBO * RBI;
     constexpr int NS = NG / 2;  // ring slots of this layer
     constexpr int PS = 2;       // prefetch distance (slots)
@@ -622,6 +657,7 @@ __device__ __forceinline__ void mlp_layer_h3(f32x16 (&out)[RBO], f32x16 (&ain)[R
 #pragma clang loop unroll(full)
     for (int g = 0; g < NQ; ++g) {
         __builtin_amdgcn_sched_barrier(0);
+        ANERF_H3_HOOK(1);
         prefetch(g);
         const int ob = g >> 1, s = g & 1;
         out[ob] = mfma_h3<NP>(ring.v[(g >> 1) % 4], g & 1, T[s], out[ob]);
@@ -633,7 +669,7 @@ __device__ __forceinline__ void mlp_layer_h3(f32x16 (&out)[RBO], f32x16 (&ain)[R
                 if (pair_group(p, QL) == (g < QL ? -1 : g) || (g == NQ - 1 && pair_group(p, QL) > g))
                     split2_block_pair(h[1], t, Tn, p);
         }
-        h3_group_schedule<NP>();
+        h3_group_schedule<NP, ANERF_H3_LEAD_IL>();
     }
 #pragma clang loop unroll(full)
     for (int ib = 1; ib < RBI; ++ib) {
@@ -646,6 +682,7 @@ __device__ __forceinline__ void mlp_layer_h3(f32x16 (&out)[RBO], f32x16 (&ain)[R
             const int s = q / RBO, ob = q % RBO;
             const int g = NQ + (ib - 1) * NQ + q;
             __builtin_amdgcn_sched_barrier(0);
+            ANERF_H3_HOOK(ib + 1 < RBI ? 2 : 3);
             prefetch(g);
             out[ob] = mfma_h3<NP>(ring.v[(g >> 1) % 4], g & 1, T[s], out[ob]);
             if (ob == RBO - 1) alpha(ib, s);
@@ -659,6 +696,12 @@ __device__ __forceinline__ void mlp_layer_h3(f32x16 (&out)[RBO], f32x16 (&ain)[R
             h3_group_schedule<NP>();
         }
     }
+    __builtin_amdgcn_sched_barrier(0);
+    ANERF_H3_HOOK(0);
+#ifdef ANERF_H3_STAMPS
+    if ((threadIdx.x & 63) == 0)
+        for (int i = 0; i < 4; ++i) atomicAdd(ANERF_H3_STAMPS + i, ph_acc[i]);
+#endif
 }
 
 // The MLP input x = [v (k*NJ + j), r (NJ*NV + 3j + c)] is split into two k-streams:
@@ -932,6 +975,9 @@ __device__ __forceinline__ void u_part_lds(f32x16 (&acc)[RB], const ModelDev& M,
 }
 
 // ---- bf16x6 bone-direction parts (P == 2, layer 0 and the skip layer)
+#ifndef ANERF_UF_UNROLL
+#define ANERF_UF_UNROLL 2
+#endif
 // VALU pass: the 3 NJH2 bone-direction features of this lane (sample l & 31, joints h NJH2 ..
 // h NJH2 + NJH2 - 1) into the wave's LDS store as [q][64 lanes] (q = 3 p + c: conflict-free
 // b32 rows), the per-joint live ballots (JointMask) and the view windows w'_j — what u_part
@@ -952,30 +998,33 @@ __device__ __forceinline__ void u_features_lds(const ModelDev& M, const float* _
         m0 |= (jb < 64 ? hi : 0ull) << (jb & 63);
         m1 |= (jb >= 64 ? hi : 0ull) << (jb & 63);
     };
-    JRow ra = load_row(sk, cut, j0, nj, M.bone_cut != 0);
-    JRow rb = load_row(sk, cut, j0 + min(1, njh2 - 1), nj, M.bone_cut != 0);
-    for (int p = 0; p < njh2; p += 2) {
-        const bool two = p + 1 < njh2;  // (uniform)
-        const JRow na = load_row(sk, cut, j0 + min(p + 2, njh2 - 1), nj, M.bone_cut != 0);
-        const JRow nb = load_row(sk, cut, j0 + min(p + 3, njh2 - 1), nj, M.bone_cut != 0);
-        float u0, u1, u2, wv, v0, v1, v2, wv2;
-        bool live, live2;
-        u_joint<WV>(M, ra, j0 + p < nj, px, py, pz, u0, u1, u2, live, wv);
-        u_joint<WV>(M, rb, two && (j0 + p + 1 < nj), px, py, pz, v0, v1, v2, live2, wv2);
-        uf[(3 * p + 0) * 64 + lane] = u0;
-        uf[(3 * p + 1) * 64 + lane] = u1;
-        uf[(3 * p + 2) * 64 + lane] = u2;
-        if constexpr (WV) wvo[p * 64 + lane] = wv;
-        set_bits(p, __ballot(live));
-        if (two) {
-            uf[(3 * p + 3) * 64 + lane] = v0;
-            uf[(3 * p + 4) * 64 + lane] = v1;
-            uf[(3 * p + 5) * 64 + lane] = v2;
-            if constexpr (WV) wvo[(p + 1) * 64 + lane] = wv2;
-            set_bits(p + 1, __ballot(live2));
+    // (U joints per iteration: the chains of U joints interleave; round 5: U = 4, was 2)
+    constexpr int U = ANERF_UF_UNROLL;
+    JRow r[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) r[k] = load_row(sk, cut, j0 + min(k, njh2 - 1), nj, M.bone_cut != 0);
+    for (int p = 0; p < njh2; p += U) {
+        JRow n[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) n[k] = load_row(sk, cut, j0 + min(p + U + k, njh2 - 1), nj, M.bone_cut != 0);
+        float u[U][3], wv[U];
+        bool live[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k)
+            u_joint<WV>(M, r[k], (p + k < njh2) && (j0 + p + k < nj), px, py, pz, u[k][0], u[k][1], u[k][2], live[k],
+                        wv[k]);
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            if (p + k < njh2) {  // (uniform)
+                uf[(3 * (p + k) + 0) * 64 + lane] = u[k][0];
+                uf[(3 * (p + k) + 1) * 64 + lane] = u[k][1];
+                uf[(3 * (p + k) + 2) * 64 + lane] = u[k][2];
+                if constexpr (WV) wvo[(p + k) * 64 + lane] = wv[k];
+                set_bits(p + k, __ballot(live[k]));
+            }
         }
-        ra = na;
-        rb = nb;
+#pragma unroll
+        for (int k = 0; k < U; ++k) r[k] = n[k];
     }
     if (mask) {
         mask->m0 = m0;

@@ -29,6 +29,10 @@ struct Stamps {
         if ((threadIdx.x & 63) == 0 && (ptr))                             \
             for (int i_ = 0; i_ < 24; ++i_) atomicAdd((ptr) + i_, (st).acc[i_]); \
     } while (0)
+#elif defined(ANERF_ASM_MARKS)  // (diagnostic: phase markers in the device assembly, tools only)
+#define STAMP_INIT(st) do { } while (0)
+#define STAMP(st, i) asm volatile(";@@STAMP " #i)
+#define STAMP_FLUSH(st, ptr) do { } while (0)
 #else
 #define STAMP_INIT(st) do { } while (0)
 #define STAMP(st, i) do { } while (0)

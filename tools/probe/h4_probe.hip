@@ -11,6 +11,10 @@
 #include <random>
 #include <vector>
 
+#ifdef PROBE_STAMPS  // per-phase cycles of the layer: 0 preamble, 1 lead groups, 2 middle blocks, 3 last block
+__device__ unsigned long long g_ph[4];
+#define ANERF_H3_STAMPS g_ph
+#endif
 #include "../../include/anerf.h"
 #include "../../a-nerf_amd/csrc/anerf_device.hpp"
 using namespace anerf;
@@ -76,10 +80,16 @@ int main() {
     hipMalloc(&cyc, 8);
     const int nl = 440, reps = 20;
     const double ideal = 128.0 * PROBE_NP * 32.0;
+#ifdef PROBE_STAMPS
+    unsigned long long zero[4] = {0, 0, 0, 0};
+#endif
     for (int rnd = 0; rnd < 3; ++rnd) {
         hipLaunchKernelGGL(layer_speed, dim3(256), dim3(256), 0, 0, w, nl, foot, out, cyc);
         hipDeviceSynchronize();
         hipMemset(cyc, 0, 8);
+#ifdef PROBE_STAMPS
+        hipMemcpyToSymbol(HIP_SYMBOL(g_ph), zero, sizeof(zero));
+#endif
         hipEvent_t e0, e1;
         hipEventCreate(&e0);
         hipEventCreate(&e1);
@@ -95,6 +105,13 @@ int main() {
         printf("fp16 layer NP=%d: %.1f TFLOP/s (16-bit MFMA), %.0f cyc/layer (%.1f %% of ideal %.0f), clock %.3f GHz\n", PROBE_NP,
                256.0 * 4 * reps * nl * 128.0 * PROBE_NP * 32768.0 / (ms * 1e-3) / 1e12, cyc_layer, 100.0 * ideal / cyc_layer,
                ideal, cyc_wave / (ms * 1e-3 / reps) / 1e9);
+#ifdef PROBE_STAMPS
+        unsigned long long ph[4];
+        hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_ph), sizeof(ph));
+        const double den = 256.0 * 4 * reps * nl;
+        printf("  per layer: preamble %.0f, lead groups %.0f (16 groups), middle blocks %.0f (96), last block %.0f (16) cycles\n",
+               ph[0] / den, ph[1] / den, ph[2] / den, ph[3] / den);
+#endif
     }
     return 0;
 }
