@@ -506,6 +506,34 @@ __device__ __forceinline__ void split2_pair(float a, float b, float t, H3T& T, i
 #endif
 }
 
+// fp16x4 with the x1 w1 product in fp8 (ANERF_F8_X1W1, round 5): the same split, and the low parts x1 also
+// as e4m3 bytes of the x1 w1 MFMA's B operand (x1 scaled by 2^8 into e4m3's range; the MFMA's block scale
+// 2^-8 undoes it): byte 2 (p & 1) .. +1 of dword `d` (two pairs per dword)
+#ifndef ANERF_F8_X1W1
+#define ANERF_F8_X1W1 0
+#endif
+template <bool HI_WORD>
+__device__ __forceinline__ void split2_pair_f8(float a, float b, float t, H3T& T, int q, unsigned& x8) {
+    typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+    const float xa = a * t, xb = b * t;
+    const unsigned hi = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2{xa, xb}), f16x2));
+    float la, lb;
+    asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(la) : "v"(hi), "v"(xa));
+    asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(lb) : "v"(hi), "v"(xb));
+    T.d[0][q] = hi;
+    T.d[1][q] = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2{la, lb}), f16x2));
+    x8 = (unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(la * 256.0f, lb * 256.0f, (int)x8, HI_WORD);
+}
+
+__device__ __forceinline__ void split2_block_pair_f8(const f32x16& hb, float t, H3T (&T)[2], int p,
+                                                     unsigned (&X8)[8], int half) {
+    const int s = p >> 2, q = p & 3;
+    if (p & 1)
+        split2_pair_f8<true>(hb[8 * s + 2 * q], hb[8 * s + 2 * q + 1], t, T[s], q, X8[4 * half + (p >> 1)]);
+    else
+        split2_pair_f8<false>(hb[8 * s + 2 * q], hb[8 * s + 2 * q + 1], t, T[s], q, X8[4 * half + (p >> 1)]);
+}
+
 __device__ __forceinline__ void split2_block_pair(const f32x16& hb, float t, H3T (&T)[2], int p) {
     const int s = p >> 2, q = p & 3;
 #if ANERF_X6_PROBE == 2  // (diagnostic builds of tools/probe only: no split arithmetic)
@@ -585,8 +613,12 @@ __device__ __forceinline__ void mlp_layer_h3(f32x16 (&out)[RBO], f32x16 (&ain)[R
                                              const float* __restrict__ bias, const float* __restrict__ wp, int lane,
                                              Ring& ring, bool preloaded, const float* __restrict__ next,
                                              const float* __restrict__ wa, float& sig, int& es, int ew, int top,
-                                             int cap = 60) {
+                                             int cap = 60, const float* __restrict__ w8 = nullptr) {
     static_assert(RBO <= RBI, "h3 layer shape");
+    // F8: fp16x4 with x1 w1 as one v_mfma_scale_f32_32x32x64_f8f6f4 (e4m3) per output block and pair of
+    // input blocks (64 k) instead of four f16 MFMAs: w8 holds the e4m3 w1 groups (pack_layer_f8)
+    constexpr bool F8 = (NP == 4) && ANERF_F8_X1W1 && (RBI % 2 == 0);
+    constexpr int NPG = F8 ? 3 : NP;  // f16 products per 16 k
 #ifdef ANERF_H3_STAMPS
     unsigned long long ph_last = __builtin_amdgcn_s_memtime(), ph_acc[4] = {0, 0, 0, 0};
     int ph_cur = 0;
@@ -651,25 +683,49 @@ __device__ __forceinline__ void mlp_layer_h3(f32x16 (&out)[RBO], f32x16 (&ain)[R
     convert_half(0, 0);
     convert_half(0, 1);
     H3T T[2], Tn[2];
+    // (F8) e4m3 x1 of input blocks 2c, 2c + 1 in X8[c & 1] (block b: half b & 1); w1 groups in a 2-slot ring
+    unsigned X8[2][8];
+    float W8[2][16];
+    const __amdgpu_buffer_rsrc_t r8 = make_rsrc(w8 ? w8 : wp);
+    auto split_block_pair = [&](int b, int p, H3T (&TT)[2]) {
+        if constexpr (F8) split2_block_pair_f8(h[b], t, TT, p, X8[(b >> 1) & 1], b & 1);
+        else split2_block_pair(h[b], t, TT, p);
+    };
+    auto load8 = [&](int c, int o8) {  // w1 group (c, o8): output block o8, input blocks 2c, 2c + 1
+        if constexpr (F8) load_group<8>(W8[o8 & 1], r8, lane, c * RBO + o8);
+    };
+    auto mfma8 = [&](int c, int o8) {
+        if constexpr (F8) {
+            typedef int i32x8 __attribute__((ext_vector_type(8)));
+            typedef float f32x8 __attribute__((ext_vector_type(8)));
+            const float (&w)[16] = W8[o8 & 1];
+            const unsigned (&x)[8] = X8[c & 1];
+            const i32x8 a = __builtin_bit_cast(i32x8, (f32x8){w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7]});
+            const i32x8 bx = i32x8{(int)x[0], (int)x[1], (int)x[2], (int)x[3], (int)x[4], (int)x[5], (int)x[6], (int)x[7]};
+            // (e4m3 both; block scales 2^-8 (E8M0 119) undo the 2^8 of the packed w1 and of x1)
+            out[o8] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, bx, out[o8], 0, 0, 0, 119, 0, 119);
+        }
+    };
 #pragma unroll
-    for (int p = 0; p < 8; ++p) split2_block_pair(h[0], t, T, p);
+    for (int p = 0; p < 8; ++p) split_block_pair(0, p, T);
     constexpr int QL = NQ > 2 ? 2 : NQ;
 #pragma clang loop unroll(full)
     for (int g = 0; g < NQ; ++g) {
         __builtin_amdgcn_sched_barrier(0);
         ANERF_H3_HOOK(1);
         prefetch(g);
+        if (F8 && g == NQ - 1) load8(0, 0);
         const int ob = g >> 1, s = g & 1;
-        out[ob] = mfma_h3<NP>(ring.v[(g >> 1) % 4], g & 1, T[s], out[ob]);
+        out[ob] = mfma_h3<NPG>(ring.v[(g >> 1) % 4], g & 1, T[s], out[ob]);
         if (ob == 0) alpha(0, s);
         if (ob + 1 < RBI && (ob + 1 < RBO || ob == 0)) convert_half(ob + 1, s);
         if (RBI > 1) {
 #pragma unroll
             for (int p = 0; p < 8; ++p)
                 if (pair_group(p, QL) == (g < QL ? -1 : g) || (g == NQ - 1 && pair_group(p, QL) > g))
-                    split2_block_pair(h[1], t, Tn, p);
+                    split_block_pair(1, p, Tn);
         }
-        h3_group_schedule<NP, ANERF_H3_LEAD_IL>();
+        h3_group_schedule<NPG, ANERF_H3_LEAD_IL>();
     }
 #pragma clang loop unroll(full)
     for (int ib = 1; ib < RBI; ++ib) {
@@ -681,19 +737,30 @@ __device__ __forceinline__ void mlp_layer_h3(f32x16 (&out)[RBO], f32x16 (&ain)[R
         for (int q = 0; q < NQ; ++q) {
             const int s = q / RBO, ob = q % RBO;
             const int g = NQ + (ib - 1) * NQ + q;
+            // (F8) odd input blocks: the x1 w1 MFMA of output block q >> 1 in odd groups, its successor's
+            // w1 group loaded there; even blocks load the next pair's first group in their last group
+            const bool f8mm = F8 && (ib & 1) && (q & 1);
             __builtin_amdgcn_sched_barrier(0);
             ANERF_H3_HOOK(ib + 1 < RBI ? 2 : 3);
             prefetch(g);
-            out[ob] = mfma_h3<NP>(ring.v[(g >> 1) % 4], g & 1, T[s], out[ob]);
+            if (F8 && !(ib & 1) && q == NQ - 1) load8(ib / 2, 0);
+            out[ob] = mfma_h3<NPG>(ring.v[(g >> 1) % 4], g & 1, T[s], out[ob]);
+            if (f8mm) {
+                mfma8(ib / 2, q >> 1);
+                if ((q >> 1) + 1 < RBO) load8(ib / 2, (q >> 1) + 1);
+            }
             if (ob == RBO - 1) alpha(ib, s);
             if (ib + 1 < RBI) {
                 if (conv_next && q < 2) convert_half(ib + 1, q);
 #pragma unroll
                 for (int p = 0; p < 8; ++p)
                     if (pair_group(p, q0) == q || (q == NQ - 1 && pair_group(p, q0) > q))
-                        split2_block_pair(h[ib + 1], t, Tn, p);
+                        split_block_pair(ib + 1, p, Tn);
             }
-            h3_group_schedule<NP>();
+            if (f8mm)
+                h3_group_schedule<NPG + 1>();
+            else
+                h3_group_schedule<NPG>();
         }
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -1581,7 +1648,8 @@ __device__ __forceinline__ bool mlp_trunk(const ModelDev& M, const NetDev& net, 
             // units the h part left in the accumulators)
             const float* nxth = skl ? nullptr : after;
             mlp_layer_h3<RB, RB, true, false, P == 4 ? 4 : 3>(acc, acc, h, bias + L * W, wl[L], lane, ring, pre6, nxth, nullptr,
-                                              nosig, es, net.ewl[L], M.h3_top, (skl && enc16) ? net.enc_cap : 60);
+                                              nosig, es, net.ewl[L], M.h3_top, (skl && enc16) ? net.enc_cap : 60,
+                                              net.wl8[L]);
             pre6 = nxth != nullptr;
             if (skl) {  // the f32 skip x parts take their first groups from the ring (the x6 one loads itself)
                 if (!ux6) ring_preload<2 * RB>(ring, net.wskipu, lane);
@@ -1667,7 +1735,7 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
     if constexpr (P >= 3) {
         const int es_h = es;  // the alpha head sums the last hidden layer's activations, in its units
         mlp_layer_h3<RBV, RB, false, true, P == 4 ? 4 : 3>(av, acc, h, nullptr, net.wviewh, lane, ring, pre, nullptr,
-                                           bias + (M.D + 1) * W, sig, es, net.ew_view, M.h3_top);
+                                           bias + (M.D + 1) * W, sig, es, net.ew_view, M.h3_top, 60, net.wview8);
         sig *= pow2f(-es_h);
     } else if constexpr (P == 2)
         mlp_layer_x6<RBV, RB, false, true>(av, acc, h, nullptr, net.wview6, lane, ring, pre, nullptr,

@@ -251,6 +251,50 @@ std::vector<float> pack_layer_h3(const float* Wt, int n_out, int ld, int col_off
     });
 }
 
+// ---- e4m3 (OCP fp8, the MFMA's "fp8") round to nearest even with saturation at 448: 1 sign, 4 exponent
+// (bias 7), 3 mantissa bits; subnormals below 2^-6 in units of 2^-9
+uint8_t f8e4m3_rne(float f) {
+    if (std::isnan(f)) return 0x7f;
+    const uint8_t sign = std::signbit(f) ? 0x80 : 0;
+    double a = std::fabs((double)f);
+    if (a >= 464.0) return sign | 0x7e;  // (448 is the largest finite; 464 would round past it)
+    int e;
+    std::frexp(a, &e);  // a in [2^(e-1), 2^e)
+    int E = e - 1;      // a = 1.m x 2^E
+    if (E < -6) {       // subnormal: units of 2^-9
+        const double q = std::nearbyint(a * 512.0);
+        return sign | (uint8_t)q;  // (q == 8 is 2^-6, the smallest normal: the encoding carries over)
+    }
+    double m = std::nearbyint((a / std::ldexp(1.0, E) - 1.0) * 8.0);
+    if (m >= 8.0) { m = 0.0; ++E; }
+    if (E > 8) return sign | 0x7e;
+    return sign | (uint8_t)(((E + 7) << 3) | (int)m);
+}
+
+// fp16x4's x1 w1 products on v_mfma_scale_f32_32x32x64_f8f6f4 (ANERF_F8_X1W1): for output block ob and the
+// input block pair (2c, 2c + 1), lane l (row 32 ob + (l & 31), half h = l >> 5) holds 32 bytes: byte t is the
+// e4m3 of w1 x 2^8 -- w1 the low fp16 part of the layer's scaled weight (pack_layer_h3: w x 2^ew = w0 + w1) --
+// for input block 2c + (t >> 4) and its element i = t & 15 in the order the kernel's split packs x1 (k16-step
+// i >> 3, element i & 7: column 32 ib + 16 s + 8 (j >> 2) + 4 h + (j & 3)).  Groups (c, ob), 8 floats each.
+std::vector<float> pack_layer_f8(const float* Wt, int n_out, int ld, int col_off, int n_in, int ew) {
+    const int RBO = n_out / 32, RBI = n_in / 32;
+    const float sc = std::ldexp(1.0f, ew);
+    return pack_groups((RBI / 2) * RBO, 8, [&](int g, int sl, int l) {
+        const int c = g / RBO, ob = g % RBO, h = l >> 5, row = 32 * ob + (l & 31);
+        uint32_t bits = 0;
+        for (int b = 0; b < 4; ++b) {
+            const int t = 4 * sl + b, ib = 2 * c + (t >> 4), i = t & 15, s = i >> 3, j = i & 7;
+            const int col = col_off + 32 * ib + 16 * s + 8 * (j >> 2) + 4 * h + (j & 3);
+            const float w = Wt[(size_t)row * ld + col] * sc;
+            const float w1 = f16_to_f(f16_rne(w - f16_to_f(f16_rne(w))));
+            bits |= (uint32_t)f8e4m3_rne(w1 * 256.0f) << (8 * b);
+        }
+        float out;
+        std::memcpy(&out, &bits, 4);
+        return out;
+    });
+}
+
 // bone-direction part: k-step q = 3p + c, half h -> joint p + h*njh2, column nv*nj + 3j + c;
 // groups of 2 k-steps x RB blocks (slot float 2 rb + t)
 std::vector<float> pack_upart(const float* Wt, int n_out, int ld, int nj, int njh2, int mr) {
@@ -626,6 +670,12 @@ static int pack_net(const anerf_model_desc* d, int njh2, const anerf_net_weights
         offs.push_back(pk.add(pack_vpart_x6(w->pts_w[skl], W, cin + W, nj, mr, mrl)));
     else
         offs.push_back((size_t)-1);
+    for (int i = 1; i < d->net_depth; ++i) {                                          // fp16x4 x1 w1 (e4m3)
+        const bool sk = (i == d->skip + 1);
+        const int ld = sk ? cin + W : W, c0 = sk ? cin : 0;
+        offs.push_back(pk.add(pack_layer_f8(w->pts_w[i], W, ld, c0, W, h3_exponent(w->pts_w[i], W, ld, c0, W))));
+    }
+    offs.push_back(pk.add(pack_layer_f8(wfused.data(), WH, W, 0, W, h3_exponent(wfused.data(), WH, W, 0, W))));
     // fp16 encoder-fed parts (u: columns nv nj .. cin, v: columns 0 .. nv nj), each with its own exponent:
     // layer 0's, then the skip layer's (exponent 0 / no buffer without a skip layer)
     for (int part = 0; part < 2; ++part) {
@@ -681,6 +731,8 @@ static void bind_net(const anerf_model_desc* d, const float* base, const std::ve
     nd.wv6 = base + o[k++];
     nd.wskipv6 = o[k] == (size_t)-1 ? nullptr : base + o[k];
     ++k;
+    for (int i = 1; i < D; ++i) nd.wl8[i] = base + o[k++];
+    nd.wview8 = base + o[k++];
     for (int part = 0; part < 2; ++part) {
         nd.ewh_u[part] = (int)(int64_t)o[k++];
         nd.wuh[part] = o[k] == (size_t)-1 ? nullptr : base + o[k];

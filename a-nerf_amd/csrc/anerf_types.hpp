@@ -73,6 +73,8 @@ struct NetDev {
     const float* wuh[2];
     const float* wvh[2];
     int ewh_u[2], ewh_v[2];
+    const float* wl8[MAXL];  // [i>0] fp16x4's x1 w1 products: the e4m3 w1 of the fp16 planes (pack_layer_f8)
+    const float* wview8;     // the same for wviewh
     int enc_e0;   // exponent of layer 0's accumulator units (enc16)
     int enc_cap;  // the largest exponent of the skip layer's accumulator units its x parts' features allow
     float balpha;

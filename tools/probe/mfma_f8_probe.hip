@@ -45,6 +45,14 @@ __global__ __launch_bounds__(256, 1) void rate(const i32x8* a, const i32x8* b, f
     if (threadIdx.x == 0) atomicAdd(cyc, t1 - t0);
 }
 
+__global__ void cvt(unsigned* o, float s) {
+    typedef short s16x2 __attribute__((ext_vector_type(2)));
+    const s16x2 v = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(__builtin_bit_cast(s16x2, 0u), 1.0f, 0.0078125f, s, false);
+    o[0] = __builtin_bit_cast(unsigned, v);
+    o[1] = __builtin_amdgcn_cvt_pk_fp8_f32(1.0f, 0.0078125f, 0, false);
+    o[2] = __builtin_amdgcn_cvt_pk_fp8_f32(1.0f, 0.0078125f, 0x12345678, true);
+}
+
 static float e4m3(unsigned char v) {
     const int s = v >> 7, e = (v >> 3) & 15, m = v & 7;
     float x = e == 0 ? std::ldexp((float)m / 8.0f, -6) : std::ldexp(1.0f + m / 8.0f, e - 7);
@@ -96,6 +104,17 @@ int main() {
                    "(max |ref| %.3e)\n", sa, map, maxerr, maxref);
             break;
         }
+    }
+    {
+        unsigned* o;
+        hipMalloc(&o, 12);
+        hipLaunchKernelGGL(cvt, dim3(1), dim3(1), 0, 0, o, 256.0f);
+        unsigned h[3];
+        hipMemcpy(h, o, 12, hipMemcpyDeviceToHost);
+        printf("cvt_scalef32_pk_fp8_f32(1.0, 2^-7, scale 256) -> bytes %02x %02x = %g %g (x * 256 would be 256, 2; x / 256: "
+               "2^-8, 2^-15)\n", h[0] & 255, (h[0] >> 8) & 255, e4m3(h[0] & 255), e4m3((h[0] >> 8) & 255));
+        printf("cvt_pk_fp8_f32(1.0, 2^-7) -> %08x (%g %g); word_sel 1 into 0x12345678 -> %08x\n", h[1],
+               e4m3(h[1] & 255), e4m3((h[1] >> 8) & 255), h[2]);
     }
     for (int mode = 0; mode < 2; ++mode) {
         const int n = 2000;
