@@ -63,6 +63,10 @@ constexpr int BM = 128, BN = 128, NTHR = 256;
 #ifndef ANERF_GEMM_BD
 #define ANERF_GEMM_BD 4
 #endif
+// forward / input gradient column-tile width (round 5): 2 = 256 columns per workgroup where N % 256 == 0, 1 = 128
+#ifndef ANERF_GEMM_CB
+#define ANERF_GEMM_CB 2
+#endif
 constexpr int MAXSEG = 3;
 
 struct SegD {
@@ -187,16 +191,20 @@ struct SegTab {
     int accum[MAXSEG];
 };
 
-template <int NPL, int NSEG, int TBM, int SKT = 32, bool F16 = false>
-__global__ __launch_bounds__(NTHR, 256 / TBM) void mlp_nt_kernel(NTArgs g) {
+// CB: 32-column blocks per wave -- 1: a 128-column tile, two workgroups per CU; 2 (round 5): a 256-column
+// tile, one workgroup per CU, so that every A row is staged once for all 256 output columns (the 128-column
+// tiles staged each row twice: with K = 256 the A rows are half the vector-memory bytes of a step)
+template <int NPL, int NSEG, int TBM, int SKT = 32, bool F16 = false, int CB = 1>
+__global__ __launch_bounds__(NTHR, CB == 1 ? 256 / TBM : 1) void mlp_nt_kernel(NTArgs g) {
     static_assert(!F16 || (NPL == 2 && NSEG == 1), "fp16x4: two fp16 planes, one A segment");
+    static_assert(!F16 || CB == 1, "fp16x4's row-max epilogue works on 128-column tiles");
     using G = NTGeo<NPL, TBM, SKT>;
     constexpr int RBM = G::RBM, NRS = G::NRS, SK = SKT, KK = SKT / 16;
     extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
     const int logical = xcd_logical(blockIdx.x, g.total);
     const int mt = logical / g.tiles_n, nt = logical % g.tiles_n;
     const long long m0 = (long long)mt * TBM;
-    const int n0 = nt * NBN;
+    const int n0 = nt * NBN * CB;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     // (kernel-argument fields as locals: referencing `g` inside the lambdas makes clang copy the
     // whole argument struct to scratch and reload fields from there in the loop)
@@ -245,11 +253,13 @@ __global__ __launch_bounds__(NTHR, 256 / TBM) void mlp_nt_kernel(NTArgs g) {
     // this wave's B fragments: column block (n0 + 32 w) / 32 (the planes are zero padded to whole
     // 256-row tiles, so no block index needs a clamp)
     const long long bstride = (long long)ksteps * NPL * 512;  // elements per 32-column block
-    const unsigned short* const bl = g.b + ((n0 + 32 * wave) / 32) * bstride + lane * 8;
+    const unsigned short* const bl = g.b + ((n0 + 32 * CB * wave) / 32) * bstride + lane * 8;
 
-    f32x16 acc[RBM];
+    f32x16 acc[RBM][CB];
 #pragma unroll
-    for (int i = 0; i < RBM; ++i) acc[i] = f32x16{0};
+    for (int i = 0; i < RBM; ++i)
+#pragma unroll
+        for (int cb = 0; cb < CB; ++cb) acc[i][cb] = f32x16{0};
     float ts[NRS];  // F16: the row scales 2^shift of this thread's staging rows
 #pragma unroll
     for (int i = 0; i < NRS; ++i) {
@@ -261,13 +271,15 @@ __global__ __launch_bounds__(NTHR, 256 / TBM) void mlp_nt_kernel(NTArgs g) {
     }
 
     struct BF {
-        u32x4 v[NPL];
+        u32x4 v[NPL][CB];
     };
     auto fetch_b = [&](int kt, BF& f) {
         kt = kt < nk ? kt : nk - 1;
         const unsigned short* bk = bl + (long long)kt * NPL * 512;
 #pragma unroll
-        for (int p = 0; p < NPL; ++p) f.v[p] = *reinterpret_cast<const u32x4*>(bk + p * 512);
+        for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+            for (int p = 0; p < NPL; ++p) f.v[p][cb] = *reinterpret_cast<const u32x4*>(bk + cb * bstride + p * 512);
     };
     struct RA {
         f32x4 v[NRS][NSEG];
@@ -336,39 +348,43 @@ __global__ __launch_bounds__(NTHR, 256 / TBM) void mlp_nt_kernel(NTArgs g) {
     auto step = [&](int buf, int kk, const BF& f) {
         const unsigned short* A = lds + buf * G::STAGE;
         const int r = lane & 31, kh = 16 * kk + 8 * (lane >> 5);
-        bf16x8 a[NPL][RBM], b[NPL];
+        bf16x8 a[NPL][RBM], b[NPL][CB];
 #pragma unroll
         for (int i = 0; i < RBM; ++i)
 #pragma unroll
             for (int p = 0; p < NPL; ++p)
                 a[p][i] = *reinterpret_cast<const bf16x8*>(A + p * G::PLANE + nt_off<SKT>(32 * i + r, kh));
 #pragma unroll
-        for (int p = 0; p < NPL; ++p) b[p] = __builtin_bit_cast(bf16x8, f.v[p]);
+        for (int p = 0; p < NPL; ++p)
 #pragma unroll
-        for (int i = 0; i < RBM; ++i) {
-            f32x16 c = acc[i];
-            if constexpr (F16) {  // the four products, small terms first
-                c = mfma16(a[1][i], b[1], c);
-                c = mfma16(a[1][i], b[0], c);
-                c = mfma16(a[0][i], b[1], c);
-                acc[i] = mfma16(a[0][i], b[0], c);
-                continue;
+            for (int cb = 0; cb < CB; ++cb) b[p][cb] = __builtin_bit_cast(bf16x8, f.v[p][cb]);
+#pragma unroll
+        for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+            for (int i = 0; i < RBM; ++i) {
+                f32x16 c = acc[i][cb];
+                if constexpr (F16) {  // the four products, small terms first
+                    c = mfma16(a[1][i], b[1][cb], c);
+                    c = mfma16(a[1][i], b[0][cb], c);
+                    c = mfma16(a[0][i], b[1][cb], c);
+                    acc[i][cb] = mfma16(a[0][i], b[0][cb], c);
+                    continue;
+                }
+                if constexpr (NPL == 3) {
+                    c = mfma(a[2][i], b[0][cb], c);
+                    c = mfma(a[1][i], b[1][cb], c);
+                    c = mfma(a[0][i], b[2][cb], c);
+                }
+                c = mfma(a[1][i], b[0][cb], c);
+                c = mfma(a[0][i], b[1][cb], c);
+                acc[i][cb] = mfma(a[0][i], b[0][cb], c);
             }
-            if constexpr (NPL == 3) {
-                c = mfma(a[2][i], b[0], c);
-                c = mfma(a[1][i], b[1], c);
-                c = mfma(a[0][i], b[2], c);
-            }
-            c = mfma(a[1][i], b[0], c);
-            c = mfma(a[0][i], b[1], c);
-            acc[i] = mfma(a[0][i], b[0], c);
-        }
     };
     // B fragments (the split weights, L2-resident) in a ring of BD k16-steps, prefetched BD - 1 steps
     // ahead: the waves' SQ counters showed them parked at s_waitcnt 45 % of the time with the B loads
     // one k16-step (12 MFMAs) ahead of their use (profiles/r04l_pmc_waves.txt); two more register sets
     // fit the single-segment instances (ANERF_GEMM_BD; the multi-segment ones keep the 2-ring)
-    constexpr int BD = (NSEG == 1 && ANERF_GEMM_BD == 4) ? 4 : 2;
+    constexpr int BD = (NSEG == 1 && ANERF_GEMM_BD == 4 && CB == 1) ? 4 : 2;
     RA R0, R1;
     BF f[BD];
     fetch_a(0, R0);
@@ -414,17 +430,25 @@ __global__ __launch_bounds__(NTHR, 256 / TBM) void mlp_nt_kernel(NTArgs g) {
     // accumulate, segment split).
     constexpr int TP = 132;  // tile pitch (floats)
     float* const tile = reinterpret_cast<float*>(lds);
+    // (CB 2: two passes over the [128][132] tile, 128 columns each, written by waves 2 hh and 2 hh + 1)
 #pragma unroll
-    for (int i = 0; i < RBM; ++i)
+    for (int hh = 0; hh < CB; ++hh) {
+    if (hh) __syncthreads();
+    if (CB == 1 || (wave >> 1) == hh) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int row = 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-            tile[row * TP + 32 * wave + (lane & 31)] = acc[i][r];
-        }
+        for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+            for (int i = 0; i < RBM; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                    tile[row * TP + 32 * CB * wave + 32 * cb - 128 * hh + (lane & 31)] = acc[i][cb][r];
+                }
+    }
     __syncthreads();
     // thread t: rows 8 q + (t >> 5) (q < TBM / 8), columns 4 (t & 31) .. + 3
     const int c4 = 4 * (tid & 31), rb = tid >> 5;
-    const int n = n0 + c4;
+    const int n = n0 + 128 * hh + c4;
     const int Nd = g.N;
     if (n < Nd) {
         const int cs1 = g.nc > 1 ? g.c[1].start : Nd, cs2 = g.nc > 2 ? g.c[2].start : Nd;
@@ -533,6 +557,7 @@ __global__ __launch_bounds__(NTHR, 256 / TBM) void mlp_nt_kernel(NTArgs g) {
             }
         }
     }
+    }  // (hh: the tile's 128-column halves)
 }
 
 // ---------------------------------------------------------------- weight gradient
@@ -947,9 +972,9 @@ size_t split_plane_bytes(int rows, int cols, int npl) { return (size_t)2 * npl *
 
 // the dynamic LDS (up to 67 KB) is above the default limit: raised once per kernel instance
 // (set on every call: the attribute belongs to the current device, and a cached failure would stick)
-template <int NPL, int NSEG, int TBM, int SKT, bool F16 = false>
+template <int NPL, int NSEG, int TBM, int SKT, bool F16 = false, int CB = 1>
 hipError_t nt_attr() {
-    return hipFuncSetAttribute((const void*)mlp_nt_kernel<NPL, NSEG, TBM, SKT, F16>,
+    return hipFuncSetAttribute((const void*)mlp_nt_kernel<NPL, NSEG, TBM, SKT, F16, CB>,
                                hipFuncAttributeMaxDynamicSharedMemorySize, NTGeo<NPL, TBM, SKT>::LDS_BYTES);
 }
 template <int NPL, int NSEG>
@@ -1108,10 +1133,12 @@ int anerf_mlp_gemm_rows(int64_t m, int32_t n, int32_t k, const anerf_seg* a, int
     }
     if (start != n) return anerf_internal_fail(ANERF_EINVAL, "output segments do not add up to n");
     g.nc = n_c;
-    g.tiles_n = (n + NBN - 1) / NBN;
     // row-tile height: 128, or (ANERF_GEMM_BM 64) 64 for the single-segment instances
     // (the fp16x4 instance is always 128 rows high)
     const int tbm = (ANERF_GEMM_BM == 64 && n_a == 1 && !f16) ? 64 : 128;
+    // 256-column tiles (CB 2) where the columns are whole 256s (the trunk and view-input layers at W 256)
+    const int cb = (ANERF_GEMM_CB == 2 && !f16 && tbm == 128 && n % 256 == 0) ? 2 : 1;
+    g.tiles_n = (n + NBN * cb - 1) / (NBN * cb);
     const long long tiles = (long long)((m + tbm - 1) / tbm) * g.tiles_n;
     if (tiles > 0x7fffffff) return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_gemm: too many tiles");
     g.total = (int)tiles;
@@ -1133,10 +1160,16 @@ int anerf_mlp_gemm_rows(int64_t m, int32_t n, int32_t k, const anerf_seg* a, int
     if (npl == P && n_a == S) {                                                                       \
         constexpr int TB = (ANERF_GEMM_BM == 64 && S == 1) ? 64 : 128;                                \
         constexpr int SKT = (ANERF_GEMM_SK64 && P == 2 && S == 1) ? 64 : 32;                          \
-        e = nt_attr<P, S, TB, SKT>();                                                                 \
-        if (e != hipSuccess) return anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));            \
         constexpr int LB = NTGeo<P, TB, SKT>::LDS_BYTES;                                              \
-        hipLaunchKernelGGL((mlp_nt_kernel<P, S, TB, SKT>), dim3((unsigned)tiles), dim3(NTHR), LB, st, g); \
+        if (TB == 128 && cb == 2) {                                                                   \
+            e = nt_attr<P, S, TB, SKT, false, 2>();                                                   \
+            if (e != hipSuccess) return anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));        \
+            hipLaunchKernelGGL((mlp_nt_kernel<P, S, TB, SKT, false, 2>), dim3((unsigned)tiles), dim3(NTHR), LB, st, g); \
+        } else {                                                                                      \
+            e = nt_attr<P, S, TB, SKT>();                                                             \
+            if (e != hipSuccess) return anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));        \
+            hipLaunchKernelGGL((mlp_nt_kernel<P, S, TB, SKT>), dim3((unsigned)tiles), dim3(NTHR), LB, st, g); \
+        }                                                                                             \
     }
     ANERF_NT_LAUNCH(3, 1)
     ANERF_NT_LAUNCH(3, 2)
