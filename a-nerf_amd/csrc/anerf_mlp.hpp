@@ -883,7 +883,9 @@ __device__ __forceinline__ JRow load_row(const float* __restrict__ sk, const flo
 // scheduled into.
 // With WV, also the joint's view-direction window w'_j = 1 - sigmoid(tau' (|q| - c'_j)) (hardware
 // sqrt/exp2/rcp, a few ulp; 0 for padding joints or without cutoff_viewdir) for the view layer.
-template <bool WV>
+// (BC: -1 reads M.bone_cut in a uniform branch, 0 / 1 fix it at compile time, 2 selects — no branch inside
+// an MFMA region)
+template <bool WV, int BC = -1>
 __device__ __forceinline__ void u_joint(const ModelDev& M, const JRow& r, bool valid, float px, float py, float pz,
                                         float& u0, float& u1, float& u2, bool& live, float& wv) {
 #ifdef ANERF_EXP_UFAST  // timing experiment only (stamps build): encoder VALU removed
@@ -900,7 +902,15 @@ __device__ __forceinline__ void u_joint(const ModelDev& M, const JRow& r, bool v
     u0 = qx * inv;
     u1 = qy * inv;
     u2 = qz * inv;
-    if (M.bone_cut) {  // --cutoff_bones: u_j w_b (uniform branch), w_b = 1 - sigmoid(tau_b (|q| - c^b_j))
+    if constexpr (BC == 2) {  // (the window as a select: both sides computed, no branch)
+        const float wb = 1.0f - __builtin_amdgcn_rcpf(
+                                    1.0f + __builtin_amdgcn_exp2f(-(M.tau_b * (__builtin_amdgcn_sqrtf(d2) - r.cb)) *
+                                                                  1.44269504f));
+        const float f = M.bone_cut ? wb : 1.0f;
+        u0 *= f;
+        u1 *= f;
+        u2 *= f;
+    } else if (BC > 0 || (BC < 0 && M.bone_cut)) {  // --cutoff_bones: u_j w_b (uniform branch), w_b = 1 - sigmoid(tau_b (|q| - c^b_j))
         const float wb = 1.0f - __builtin_amdgcn_rcpf(
                                     1.0f + __builtin_amdgcn_exp2f(-(M.tau_b * (__builtin_amdgcn_sqrtf(d2) - r.cb)) *
                                                                   1.44269504f));
@@ -1438,6 +1448,109 @@ __device__ __forceinline__ void u_part_h(f32x16 (&acc)[RB], const ModelDev& M, c
     }
 }
 
+// (round 5, ANERF_UFUSE) layer 0's fp16 bone-direction part with u_features_lds's VALU pass under its MFMAs:
+// k-step s (8 features) runs while joints 3 s + 3 .. 3 s + 5 are computed, one per two-group scheduling
+// region, and the features of k-step s + 1 (joints <= 3 s + 5) are read back and split in the last two
+// regions.  The features still go through the LDS store (the skip layer reads them again; LDS is in order
+// within a wave).  Joints past NJH2 - 1 recompute the last one (identical stores and ballots: no branch).
+// --cutoff_bones' window is a select (a uniform branch would split the MFMA regions).
+#ifndef ANERF_UFUSE
+#define ANERF_UFUSE 0
+#endif
+#ifndef ANERF_UFUSE_PF  // (the next joint's skeleton row loaded one region ahead)
+#define ANERF_UFUSE_PF 1
+#endif
+#ifndef ANERF_UFUSE_IL
+#define ANERF_UFUSE_IL 1
+#endif
+#ifndef ANERF_UFUSE_BC  // (2: --cutoff_bones' window as a select; 0: the caller takes the unfused path with it)
+#define ANERF_UFUSE_BC 2
+#endif
+template <int RB, int NP, bool WV>
+__device__ __forceinline__ void u_part_h_fused(f32x16 (&acc)[RB], const ModelDev& M, const float* __restrict__ wp,
+                                               const float* __restrict__ sk, const float* __restrict__ cut, float px,
+                                               float py, float pz, int lane, JointMask* mask, float* __restrict__ uf,
+                                               float* __restrict__ wvo, Ring& ring, float t) {
+    static_assert(RB == 8, "u_part_h_fused: eight groups per k-step (three joint regions + the split region)");
+    constexpr int PD = 3, NV = NP == 4 ? 8 : 10;
+    const int hh = lane >> 5, njh2 = M.njh2, nj = M.nj, j0 = hh * njh2;
+    const int nq = 3 * njh2, ns = (nq + 7) / 8, ng = ns * RB;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(wp);
+    uint64_t m0 = 0, m1 = 0;
+    const bool bc = M.bone_cut != 0;
+    auto row = [&](int p) {  // (load_row with the bone window's column selected by address: no branch)
+        const int j = j0 + min(p, njh2 - 1), jc = j < nj ? j : 0;
+        const f32x4* q = reinterpret_cast<const f32x4*>(sk + 12 * jc);
+        return JRow{q[0], q[1], q[2], cut[2 * nj + jc], cut[nj + jc], cut[(bc ? 3 : 2) * nj + jc]};
+    };
+    auto joint = [&](int p, const JRow& r) {
+        const int pc = min(p, njh2 - 1);
+        float u0, u1, u2, wv;
+        bool live;
+        u_joint<WV, ANERF_UFUSE_BC>(M, r, j0 + pc < nj, px, py, pz, u0, u1, u2, live, wv);
+        uf[(3 * pc + 0) * 64 + lane] = u0;
+        uf[(3 * pc + 1) * 64 + lane] = u1;
+        uf[(3 * pc + 2) * 64 + lane] = u2;
+        if constexpr (WV) wvo[pc * 64 + lane] = wv;
+        const uint64_t b = __ballot(live);  // (as u_features_lds: joint pc, half 1 joint pc + njh2)
+        const uint64_t lo = (b & 0xffffffffull) ? 1ull : 0ull, hi = (b >> 32) ? 1ull : 0ull;
+        const int jb = pc + njh2;
+        m0 |= lo << pc;
+        m0 |= (jb < 64 ? hi : 0ull) << (jb & 63);
+        m1 |= (jb >= 64 ? hi : 0ull) << (jb & 63);
+    };
+    auto feat = [&](int q) { return mask_f(uf[min(q, nq - 1) * 64 + lane], q < nq); };
+    {
+        const JRow r0 = row(0), r1 = row(1), r2 = row(2);
+        joint(0, r0);
+        joint(1, r1);
+        joint(2, r2);
+    }
+#if ANERF_UFUSE_PF
+    JRow rn = row(3);
+#endif
+    H3T cur, nxt;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) split2_pair(feat(2 * e), feat(2 * e + 1), t, cur, e);
+    for (int s = 0; s < ns; ++s) {
+        float fn[8];
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) {
+            const int g = s * RB + rb;
+            if (rb % 2 == 0) __builtin_amdgcn_sched_barrier(0);
+            load_group<8>(ring.v[(rb + PD) % 4], rs, lane, min(g + PD, ng - 1));
+            acc[rb] = mfma_h3<NP>(ring.v[rb % 4], 0, cur, acc[rb]);
+            if (rb == 0 || rb == 2 || rb == 4) {
+                const int p = 3 * s + 3 + rb / 2;
+#if ANERF_UFUSE_PF
+                const JRow r = rn;
+                rn = row(p + 1);
+                joint(p, r);
+#else
+                joint(p, row(p));
+#endif
+            }
+            if (rb == 5) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) fn[j] = feat(8 * (s + 1) + j);
+            }
+            if (rb >= 6) {
+                const int e = 2 * (rb - 6);
+                split2_pair(fn[2 * e], fn[2 * e + 1], t, nxt, e);
+                split2_pair(fn[2 * e + 2], fn[2 * e + 3], t, nxt, e + 1);
+            }
+#if ANERF_UFUSE_IL
+            if (rb % 2 == 1) interleave_mfma_valu<2 * NP, NV>();
+#endif
+        }
+        cur = nxt;
+    }
+    if (mask) {
+        mask->m0 = m0;
+        mask->m1 = m1;
+    }
+}
+
 template <int RB, int MR, int NP>
 __device__ __forceinline__ void v_part_h(f32x16 (&acc)[RB], const ModelDev& M, const float* __restrict__ wp,
                                          const float* __restrict__ sk, const float* __restrict__ cut, float px,
@@ -1596,9 +1709,15 @@ __device__ __forceinline__ bool mlp_trunk(const ModelDev& M, const NetDev& net, 
     const float* const* wl = P >= 3 ? net.wlh : (P == 2 ? net.wl6 : (P ? net.wl3 : net.wl));  // hidden-layer streams
     if (enc16) {
         if constexpr (H16) u_part_h_preload<RB>(net.wuh[0], lane, ring);  // (latency under the VALU pass)
-        u_features_lds<WV>(M, sk, cut, px, py, pz, lane, &mask, uf, wvo);
-        STAMP(st, 14);
-        if constexpr (H16) u_part_h<RB, NPH>(acc, M, net.wuh[0], uf, lane, ring, true, pow2f(net.enc_e0 - net.ewh_u[0]));
+        const float t0 = pow2f(net.enc_e0 - net.ewh_u[0]);
+        if (ANERF_UFUSE && RB == 8 && (ANERF_UFUSE_BC == 2 || !M.bone_cut)) {
+            if constexpr (H16 && RB == 8)
+                u_part_h_fused<RB, NPH, WV>(acc, M, net.wuh[0], sk, cut, px, py, pz, lane, &mask, uf, wvo, ring, t0);
+        } else {
+            u_features_lds<WV>(M, sk, cut, px, py, pz, lane, &mask, uf, wvo);
+            STAMP(st, 14);
+            if constexpr (H16) u_part_h<RB, NPH>(acc, M, net.wuh[0], uf, lane, ring, true, t0);
+        }
     } else if (ux6) {
         if constexpr (UX6) u_part_x6_preload<RB>(net.wu6, lane, ring);  // (latency under the VALU pass)
         u_features_lds<WV>(M, sk, cut, px, py, pz, lane, &mask, uf, wvo);

@@ -600,8 +600,8 @@ int anerf_train_encode_backward(const anerf_model* m, const float* ray_batch, in
     else if (mr == 7 && mrv == 0) launch(train_encode_backward_kernel<7, 0>);
     else if (mr == 10 && mrv == 4) launch(train_encode_backward_kernel<10, 4>);
     else if (mr == 10 && mrv == 0) launch(train_encode_backward_kernel<10, 0>);
-    else return fail(ANERF_EINVAL, "anerf_train_encode_backward: training instances exist for multires 7 or 10 and "
-                                   "multires_views 4 or 0 (rendering takes multires 1-10, multires_views 0-4)");
+    else if (mr >= 0 && mr <= 10 && mrv >= 0 && mrv <= 4) launch(train_encode_backward_kernel<-1, -1>);  // (generic)
+    else return fail(ANERF_EINVAL, "anerf_train_encode_backward: multires 0-10 and multires_views 0-4");
     HIP_TRY(hipGetLastError());
     return ANERF_OK;
 }

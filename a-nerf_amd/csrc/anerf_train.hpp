@@ -58,7 +58,7 @@ __device__ __forceinline__ void encode_joint(const ModelDev& M, const float* __r
     f[nj * nv + 3 * j + 2] = M.bone_cut ? (qz / dn) * wb : qz / dn;
     float ex, ey, ez;
     joint_rot(S, dx, dy, dz, ex, ey, ez);
-    const float en = fmaxf(norm3(ex, ey, ez), 1e-12f);
+    const float en = M.view_raw ? 1.0f : fmaxf(norm3(ex, ey, ez), 1e-12f);  // (--view_type world: R_j d itself)
     const float e[3] = {ex / en, ey / en, ez / en};
     const float wv = M.cutoff_viewdir ? cutoff_w(M.tau_v, dist, M.cutoff_v[j]) : 1.0f;
     for (int c = 0; c < 3; ++c) {
@@ -107,29 +107,32 @@ __global__ void train_encode_kernel(ModelDev M, const float* __restrict__ rb, in
 // encode_row (cutoff windows w = 1 - sigmoid(tau (dist - c)), dw/ddist = -tau w (1 - w);
 // F.normalize x / max(|x|, 1e-12); torch.norm's gradient 0 at 0).
 // MR / MRV: the frequencies (compile-time, so every feature gradient of the joint is loaded up front
-// and the loads overlap instead of waiting one loop iteration each).
+// and the loads overlap instead of waiting one loop iteration each); -1: the model's counts at run time
+// (multires up to 10, multires_views up to 4: the other configurations' generic instance).
 template <int MR, int MRV>
 __device__ __forceinline__ void encode_row_grad_joint(const ModelDev& M, const float* __restrict__ S, int j,
                                                       float px, float py, float pz, float dx, float dy, float dz,
                                                       const float* __restrict__ g, float (&gS)[12]) {
-    const int nj = M.nj, nv = 1 + 2 * MR;
+    constexpr int MRX = MR >= 0 ? MR : 10, MVX = MRV >= 0 ? MRV : 4;  // (loop bounds; runtime counts below)
+    const int mr = MR >= 0 ? MR : M.mr, mrv = MRV >= 0 ? MRV : M.mrv;
+    const int nj = M.nj, nv = 1 + 2 * mr;
     const int cx = nj * nv + 3 * nj;
-    constexpr int MV = MRV > 0 ? MRV : 1;
-    float gs_[MR], gc_[MR], gu_[3], gv0_[3], gvs_[3][MV], gvc_[3][MV];
+    constexpr int MV = MVX > 0 ? MVX : 1;
+    float gs_[MRX > 0 ? MRX : 1], gc_[MRX > 0 ? MRX : 1], gu_[3], gv0_[3], gvs_[3][MV], gvc_[3][MV];
     const float g0 = g[j];
 #pragma unroll
-    for (int fi = 0; fi < MR; ++fi) {
-        gs_[fi] = g[(1 + 2 * fi) * nj + j];
-        gc_[fi] = g[(2 + 2 * fi) * nj + j];
+    for (int fi = 0; fi < MRX; ++fi) {
+        gs_[fi] = fi < mr ? g[(1 + 2 * fi) * nj + j] : 0.0f;
+        gc_[fi] = fi < mr ? g[(2 + 2 * fi) * nj + j] : 0.0f;
     }
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         gu_[c] = g[nj * nv + 3 * j + c];
         gv0_[c] = g[cx + 3 * j + c];
 #pragma unroll
-        for (int fi = 0; fi < MRV; ++fi) {
-            gvs_[c][fi] = g[cx + (1 + 2 * fi) * 3 * nj + 3 * j + c];
-            gvc_[c][fi] = g[cx + (2 + 2 * fi) * 3 * nj + 3 * j + c];
+        for (int fi = 0; fi < MVX; ++fi) {
+            gvs_[c][fi] = fi < mrv ? g[cx + (1 + 2 * fi) * 3 * nj + 3 * j + c] : 0.0f;
+            gvc_[c][fi] = fi < mrv ? g[cx + (2 + 2 * fi) * 3 * nj + 3 * j + c] : 0.0f;
         }
     }
     float qx, qy, qz;
@@ -151,7 +154,8 @@ __device__ __forceinline__ void encode_row_grad_joint(const ModelDev& M, const f
         g_dist += g0 * du;
     }
 #pragma unroll
-    for (int fi = 0; fi < MR; ++fi) {
+    for (int fi = 0; fi < MRX; ++fi) {
+        if (fi >= mr) break;
         const float fr = (float)(1 << fi);
         float s, c;
         sincos_rr(uf * fr, s, c);
@@ -189,7 +193,7 @@ __device__ __forceinline__ void encode_row_grad_joint(const ModelDev& M, const f
     float ex, ey, ez;
     joint_rot(S, dx, dy, dz, ex, ey, ez);
     const float enr = norm3(ex, ey, ez);
-    const float en = fmaxf(enr, 1e-12f);
+    const float en = M.view_raw ? 1.0f : fmaxf(enr, 1e-12f);  // (--view_type world: no normalisation)
     const float e[3] = {ex / en, ey / en, ez / en};
     const bool cutv = M.cutoff_viewdir != 0;
     const float wv = cutv ? cutoff_w(M.tau_v, dist, M.cutoff_v[j]) : 1.0f;
@@ -204,7 +208,8 @@ __device__ __forceinline__ void encode_row_grad_joint(const ModelDev& M, const f
             ge[c] += gv0;
         }
 #pragma unroll
-        for (int fi = 0; fi < MRV; ++fi) {
+        for (int fi = 0; fi < MVX; ++fi) {
+            if (fi >= mrv) break;
             const float fr = (float)(1 << fi);
             float s, co;
             sincos_rr(e[c] * fr, s, co);
@@ -215,7 +220,11 @@ __device__ __forceinline__ void encode_row_grad_joint(const ModelDev& M, const f
     }
     if (cutv) g_dist += g_wv * (-M.tau_v * wv * (1.0f - wv));
     float gex, gey, gez;
-    if (enr > 1e-12f) {
+    if (M.view_raw) {  // e = R_j d itself
+        gex = ge[0];
+        gey = ge[1];
+        gez = ge[2];
+    } else if (enr > 1e-12f) {
         const float dot = e[0] * ge[0] + e[1] * ge[1] + e[2] * ge[2];
         gex = (ge[0] - e[0] * dot) / enr;
         gey = (ge[1] - e[1] * dot) / enr;
@@ -267,7 +276,7 @@ __global__ __launch_bounds__(256) void train_encode_backward_kernel(ModelDev M, 
     float gS[12] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
     if (pose_ok && slot < spb) {
         const float* ray = rb + i * stride;
-        const int F = nj * (1 + 2 * M.mr) + 3 * nj + 3 * nj * (1 + 2 * M.mrv);
+        const int F = nj * (1 + 2 * M.mr) + 3 * nj + 3 * nj * (1 + 2 * M.mrv);  // (M.mr == MR when MR >= 0)
         const f32x4* sp = reinterpret_cast<const f32x4*>(skts + (pose * nj + j) * 16);
         const f32x4 r0 = sp[0], r1 = sp[1], r2 = sp[2];
         const float S[12] = {r0[0], r0[1], r0[2], r0[3], r1[0], r1[1], r1[2], r1[3], r2[0], r2[1], r2[2], r2[3]};

@@ -390,16 +390,12 @@ class TrainRayCaster(nn.Module):
         uses cfg.precision."""
         super().__init__()
         self.cfg = cfg.validate()
-        if cfg.multires not in (7, 10) or cfg.multires_views not in (0, 4):
-            # (rendering takes any multires 1-10 / multires_views 0-4 on zero-padded instances; the encoder
-            # backward is instantiated per frequency count)
-            raise NotImplementedError("training: the encoder backward has instances for multires 7 / 10 and "
-                                      "multires_views 0 / 4")
+        if not (1 <= cfg.multires <= 10 and 0 <= cfg.multires_views <= 4):
+            # (the render kernel's zero-padded instances; the encoder backward has tuned instances for
+            # multires 7 / 10 x multires_views 0 / 4 and a generic one for the rest)
+            raise NotImplementedError("training: multires 1-10 and multires_views 0-4")
         if mlp not in ("mixed", "mixed16", "bf16x6", "bf16x3", "fp32"):
             raise ValueError(f"mlp={mlp!r}: 'mixed', 'mixed16', 'bf16x6', 'bf16x3' or 'fp32'")
-        if cfg.extra.get("view_type", "relray") != "relray":
-            raise NotImplementedError("training: --view_type world renders (RayCaster) but the training encoder "
-                                      "and its backward take the normalised relray directions only")
         if isinstance(device, (str, torch.device)):
             dev = torch.device(device)  # (a CPU device holds the parameters only: checkpoints, no rendering)
         else:

@@ -145,8 +145,8 @@ typedef struct {
 #define ANERF_ENC_CUTOFF_BONES 4
 /* --view_type world (core/raycasters.py:279-280, ABI 14): the view input of joint j is R_j d itself
  * (IdentityExpandEncoder of transform_batch_rays, encoders.py:25-37, 71-79), not the normalised
- * R_j d / |R_j d| of the default relray (VecNormEncoder, encoders.py:172-193).  Rendering only:
- * anerf_train_encode / _encode_backward do not read it (train.TrainRayCaster refuses the flag). */
+ * R_j d / |R_j d| of the default relray (VecNormEncoder, encoders.py:172-193).  Rendering, and (round 5)
+ * anerf_train_encode / _encode_backward (the identity's gradient in place of the normalisation's). */
 #define ANERF_ENC_VIEW_RAW 8
 
 /* HOST pointers to one NeRF's weights, torch nn.Linear layout [out][in] (core/networks/nerf.py:57-88). */

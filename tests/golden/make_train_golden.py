@@ -58,6 +58,10 @@ CONFIGS = {
     # with every output, the loss and dL/dskts within their bounds.)
     "t10_cutoffbones": dict(H=128, NJ=24, S=32, I=16, D=8, W=128, tau=20.0, kind="rays", seed=44, n_rays=64,
                             n_poses=2, flags=["--cutoff_bones"], cb=True, tau_b=35.0),
+    # (round 5) multires 5 / multires_views 2 (the training encoder backward's generic instance) with
+    # --view_type world (un-normalised joint-frame ray directions: the identity's gradient to the poses)
+    "t11_mr5_mrv2_world": dict(H=128, NJ=24, S=32, I=16, D=4, W=128, tau=20.0, kind="rays", seed=45, n_rays=64,
+                               n_poses=2, mr=5, mrv=2, flags=["--view_type", "world"]),
 }
 FULL_LIMIT = 20000   # parameters with more entries are sampled
 SAMPLE = 4096
@@ -151,7 +155,7 @@ def make(name, cfg, mods, tmp):
     loss.backward()
     meta = dict(seed=cfg["seed"], sha256=mg.anerf_syn.checkpoint_sha256(ck), NJ=NJ, S=S, I=I, D=cfg["D"],
                 W=cfg["W"], tau=cfg["tau"], H=sc["H"], focal=sc["focal"], ext_scale=0.001, chunk=4096,
-                framecode=int(cfg["kind"] == "framecode"), mr=7, flags=cfg.get("flags", []), drop=[],
+                framecode=int(cfg["kind"] == "framecode"), mr=cfg.get("mr", 7), flags=cfg.get("flags", []), drop=[],
                 raw_noise_std=1.0, n_poses=P, mrv=cfg.get("mrv", 4), single=bool(cfg.get("single", False)),
                 global_step=cfg.get("global_step"), cutoff_step=cfg.get("cutoff_step"),
                 cutoff_rate=cfg.get("cutoff_rate"), tau_step=taus, lindisp=bool(cfg.get("lindisp", False)),

@@ -212,3 +212,18 @@ def test_segment_padding_is_exact_for_any_joint_count():
         feat.grad = None
         sum(r.sum() for r in ref).backward()
         assert torch.allclose(gf, feat.grad, rtol=1e-12, atol=1e-12)
+
+
+def test_training_caster_takes_generic_multires_and_world_views():
+    """Round 5: the training encoder backward has a generic instance (multires 1-10, multires_views 0-4)
+    and takes --view_type world; the GPU parity is tests/test_gpu_train.py's t11 fixture."""
+    import dataclasses
+
+    import pytest
+    g = Golden("t11_mr5_mrv2_world")
+    cfg = g.cfg
+    assert (cfg.multires, cfg.multires_views, cfg.extra.get("view_type")) == (5, 2, "world")
+    tr = train.TrainRayCaster(cfg, g.ckpt, device="cpu")  # (CPU: the parameters only)
+    assert tr.network_fn.pts_linears[0].weight.shape[1] == cfg.input_ch + cfg.input_ch_bones
+    with pytest.raises(NotImplementedError, match="multires"):
+        train.TrainRayCaster(dataclasses.replace(cfg, multires=11), device="cpu")

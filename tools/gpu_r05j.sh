@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 5: (1) GPU tests of the product build (256-column training GEMM tiles, fp8 x1w1 off); (2) fp8 probe and
-# render A/B f8x0 / f8x1 with parity; (3) training GEMM A/B: 128- vs 256-column tiles (gemm_bench, train_bench)
+# render A/B uf0 (product) / f8x1 / uf1 (fused u part) with parity; (3) training GEMM A/B: 128- vs 256-column tiles (gemm_bench, train_bench)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
@@ -18,4 +18,4 @@ done; done 2>&1 | tee gpurun_out/${TAG}_gemm.txt
 for r in 1 2; do for l in gcb1 gcb2; do
   echo "== $l train"; ANERF_LIB_PATH=$PWD/tools/ab/lib_$l.so timeout -k 10 300 python tools/train_bench.py || exit 1
 done; done 2>&1 | tee gpurun_out/${TAG}_train.txt
-LIBS="f8x0 f8x1" PREC=fp16x4 bash tools/gpu_ab3p.sh | tee gpurun_out/${TAG}_ab.txt
+LIBS="uf0 f8x1 uf1 uf1f8" PREC=fp16x4 bash tools/gpu_ab3p.sh | tee gpurun_out/${TAG}_ab.txt
