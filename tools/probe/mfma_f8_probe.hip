@@ -16,7 +16,7 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 __global__ void one(const i32x8* a, const i32x8* b, f32x16* c, int sa, int sb) {
     const int l = threadIdx.x;
-    f32x16 acc = {0};
+    f32x16 acc = c[l];  // (the caller's accumulator: zero, or large values whose low bits must survive)
     acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a[l], b[l], acc, 0, 0, 0, sa, 0, sb);
     c[l] = acc;
 }
@@ -80,7 +80,13 @@ int main() {
         if (map == 1) return 16 * (t / 8) + 8 * h + (t % 8);   // 8-byte runs interleaved by half
         return 32 * (t / 16) + 16 * h + (t % 16);               // 16-byte runs interleaved by half
     };
-    for (int sa : {127, 119}) {
+    for (int sa : {127, 119, 100}) {
+        // sa 100: products ~2^-27 of the accumulator's 1000-ish values (the x1 w1 term's place in fp16x4): is the
+        // accumulator kept to fp32 (the error then ~ulp(1000) = 6e-5) or truncated to the dot product's width?
+        std::vector<float> C0(64 * 16, 0.0f);
+        if (sa == 100)
+            for (int i = 0; i < 64 * 16; ++i) C0[i] = 1000.0f + (float)i * 0.0001220703125f;
+        hipMemcpy(dc, C0.data(), 64 * 64, hipMemcpyHostToDevice);
         hipLaunchKernelGGL(one, dim3(1), dim3(64), 0, 0, da, db, dc, sa, 127);
         std::vector<float> C(64 * 16);
         hipMemcpy(C.data(), dc, 64 * 64, hipMemcpyDeviceToHost);
@@ -97,6 +103,7 @@ int main() {
                             ref += (double)e4m3(A[(row + 32 * h) * 32 + t]) * (double)e4m3(B[(col + 32 * h) * 32 + t]);
                         }
                     ref *= std::ldexp(1.0, sa - 127);
+                    ref += (double)C0[l * 16 + r];
                     maxerr = std::fmax(maxerr, std::fabs(ref - C[l * 16 + r]));
                     maxref = std::fmax(maxref, std::fabs(ref));
                 }
