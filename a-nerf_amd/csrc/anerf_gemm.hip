@@ -64,8 +64,10 @@ constexpr int BM = 128, BN = 128, NTHR = 256;
 #define ANERF_GEMM_BD 4
 #endif
 // forward / input gradient column-tile width (round 5): 2 = 256 columns per workgroup where N % 256 == 0, 1 = 128
+// (A/B, profiles/r05j_gemm.txt: 256 columns 108.6 -> 134-139 us forward at M = 163,840, training 203 k -> 189 k:
+// one workgroup per CU instead of two exposes the staging; not kept)
 #ifndef ANERF_GEMM_CB
-#define ANERF_GEMM_CB 2
+#define ANERF_GEMM_CB 1
 #endif
 constexpr int MAXSEG = 3;
 
