@@ -32,6 +32,8 @@ PRECISIONS = {"fp32": ANERF_PREC_FP32, "bf16x3": ANERF_PREC_BF16X3, "bf16x6": AN
 
 ANERF_ENC_CUT_TO_DIST, ANERF_ENC_CUTOFF_SHIFT, ANERF_ENC_CUTOFF_BONES = 1, 2, 4  # anerf_model_desc.encoder_flags
 ANERF_ENC_VIEW_RAW = 8  # --view_type world
+ANERF_ENC_KP_RELPOS, ANERF_ENC_VIEW_ANGLE = 16, 32  # --kp_dist_type relpos, --view_type rayangle (staged, ABI 15)
+ABI_VERSION = 15  # include/anerf.h ANERF_ABI_VERSION: the structs below
 
 
 class ModelDesc(ctypes.Structure):
@@ -41,7 +43,8 @@ class ModelDesc(ctypes.Structure):
                 ("cutoff_viewdir", ctypes.c_int32), ("framecode_ch", ctypes.c_int32),
                 ("n_framecodes", ctypes.c_int32), ("density_softplus", ctypes.c_int32),
                 ("softplus_shift", ctypes.c_float), ("density_scale", ctypes.c_float),
-                ("has_fine", ctypes.c_int32), ("single_net", ctypes.c_int32), ("encoder_flags", ctypes.c_int32)]
+                ("has_fine", ctypes.c_int32), ("single_net", ctypes.c_int32), ("encoder_flags", ctypes.c_int32),
+                ("multires_bones", ctypes.c_int32)]
 
 
 class NetWeights(ctypes.Structure):
@@ -230,6 +233,8 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.anerf_abi_version() != ABI_VERSION:  # (a stale build would read these structs with another layout)
+        raise AnerfError(f"{LIB_PATH} has ABI {lib.anerf_abi_version()}, this binding {ABI_VERSION}: rebuild it")
     _lib = lib
     return lib
 

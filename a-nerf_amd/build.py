@@ -44,10 +44,18 @@ def build(force=False, verbose=True):
     if not force and stamp_matches():
         return OUT
     digest = source_hash()
-    cmd = [HIPCC] + FLAGS + ["-o", OUT] + SRC
+    tmp = OUT + ".tmp"
+    cmd = [HIPCC] + FLAGS + ["-o", tmp] + SRC
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
+    # hipcc reads the headers once per offload pass: a source edited during the build can give the host and
+    # the device passes different struct layouts (a torn library).  Keep only a build whose sources did not
+    # move, and replace the library in one rename (a copy of the tree never sees a half-written file).
+    if source_hash() != digest:
+        os.remove(tmp)
+        raise RuntimeError("sources changed during the build: the library was discarded, build again")
+    os.replace(tmp, OUT)
     with open(STAMP, "w") as f:
         f.write(digest + "\n")
     return OUT

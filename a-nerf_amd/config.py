@@ -66,8 +66,8 @@ class RenderConfig:
             # tests/golden/probe_reference_flags.py in reference_flags.json)
             raise NotImplementedError("use_viewdirs=False: the reference raises TypeError on this path "
                                       "(core/raycasters.py:67, 538); not implemented")
-        if self.multires_bones != 0:
-            raise NotImplementedError("multires_bones > 0 is not implemented (configs use 0)")
+        if not 0 <= self.multires_bones <= 10:
+            raise NotImplementedError(f"multires_bones={self.multires_bones} outside [0, 10]")
         if len(self.skips) != 1 or self.skips[0] < 0:
             # a skip index >= netdepth-1 is never reached (D=4 configs): no skip layer
             raise NotImplementedError(f"skips={self.skips}: exactly one skip index is supported")
@@ -97,8 +97,8 @@ class RenderConfig:
         if self.extra.get("bone_type") == "axisang":
             raise TypeError("--bone_type axisang: IdentityExpandEncoder.forward() missing 1 required positional "
                             "argument: 'refs' (core/raycasters.py:521)")
-        for k, allowed in (("kp_dist_type", ("reldist",)), ("bone_type", ("reldir",)),
-                           ("view_type", ("relray", "world")), ("pts_tr_type", ("local",))):
+        for k, allowed in (("kp_dist_type", ("reldist", "relpos")), ("bone_type", ("reldir",)),
+                           ("view_type", ("relray", "world", "rayangle")), ("pts_tr_type", ("local",))):
             v = self.extra.get(k, allowed[0])
             if v not in allowed:
                 raise NotImplementedError(f"--{k}={v}: only {' / '.join(allowed)} implemented")
@@ -110,20 +110,36 @@ class RenderConfig:
         return bool(self.cutoff_bones and self.use_cutoff)
 
     @property
+    def kp_relpos(self):
+        """--kp_dist_type relpos (core/encoders.py:124-142): three local coordinates per joint."""
+        return self.extra.get("kp_dist_type", "reldist") == "relpos"
+
+    @property
+    def view_angle(self):
+        """--view_type rayangle (core/encoders.py:195-212): one ray angle per joint."""
+        return self.extra.get("view_type", "relray") == "rayangle"
+
+    @property
+    def staged(self):
+        """An encoder the fused render kernel does not stream (bone frequencies, relpos, ray angles,
+        include/anerf.h "staged encoders"): the training stages render it (train.TrainRayCaster)."""
+        return self.multires_bones > 0 or self.kp_relpos or self.view_angle
+
+    @property
     def framecode_ch(self):
         return self.framecode_size if self.opt_framecode else 0
 
     @property
     def input_ch(self):
-        return self.n_joints * (1 + 2 * self.multires)
+        return self.n_joints * (3 if self.kp_relpos else 1) * (1 + 2 * self.multires)
 
     @property
     def input_ch_bones(self):
-        return 3 * self.n_joints
+        return 3 * self.n_joints * (1 + 2 * self.multires_bones)
 
     @property
     def input_ch_views(self):
-        return 3 * self.n_joints * (1 + 2 * self.multires_views)
+        return self.n_joints * (1 if self.view_angle else 3) * (1 + 2 * self.multires_views)
 
     @property
     def feature_dim(self):
@@ -164,27 +180,34 @@ def schedule_weights(alpha, n_freqs):
     return (0.5 * (1.0 - torch.cos(np.pi * diff))).numpy().astype(np.float32)
 
 
-def feature_scales(cfg, alpha_pts, alpha_views):
+def feature_scales(cfg, alpha_pts, alpha_views, alpha_bones=None):
     """Per-column factor of the MLP input [x (input_ch) | bones | views] under --freq_schedule: the
     schedule weight of the column's frequency for the windowed sin/cos features of the cutoff
-    embedders (pts: column f * NJ + j, views: input_ch + input_ch_bones + f * 3 NJ + 3 j + c, with
-    f = 1 + 2k / 2 + 2k the sin / cos of frequency k), 1 elsewhere; None without a schedule."""
+    embedders (a part's frequency slot f = 1 + 2k / 2 + 2k, the sin / cos of frequency k, is the column
+    block [f B, (f + 1) B) of the part, B its columns per slot: pts NJ (relpos 3 NJ), bones 3 NJ (a
+    CutoffEmbedder with --cutoff_bones, `alpha_bones`), views 3 NJ (rayangle NJ)), 1 elsewhere; None
+    without a schedule."""
     import numpy as np
     if not cfg.freq_schedule:
         return None
     nj = cfg.n_joints
     dnet = cfg.input_ch + cfg.input_ch_bones
     s = np.ones(dnet + cfg.input_ch_views, np.float32)
+
+    def part(o, b, n_freq, alpha):
+        w = schedule_weights(alpha, n_freq)
+        for k in range(n_freq):
+            for f in (1 + 2 * k, 2 + 2 * k):
+                s[o + f * b:o + (f + 1) * b] = w[k]
+
     if cfg.use_cutoff:  # (the pts embedder is a CutoffEmbedder only then)
-        w = schedule_weights(alpha_pts, cfg.multires)
-        for k in range(cfg.multires):
-            for f in (1 + 2 * k, 2 + 2 * k):
-                s[f * nj:(f + 1) * nj] = w[k]
+        part(0, nj * (3 if cfg.kp_relpos else 1), cfg.multires, alpha_pts)
+    if cfg.bone_window and cfg.multires_bones > 0:
+        if alpha_bones is None:
+            raise ValueError("freq_schedule with a windowed bone embedder: its sched_alpha is needed")
+        part(cfg.input_ch, 3 * nj, cfg.multires_bones, alpha_bones)
     if cfg.use_viewdirs and cfg.cutoff_viewdir and cfg.multires_views > 0:
-        w = schedule_weights(alpha_views, cfg.multires_views)
-        for k in range(cfg.multires_views):
-            for f in (1 + 2 * k, 2 + 2 * k):
-                s[dnet + f * 3 * nj:dnet + (f + 1) * 3 * nj] = w[k]
+        part(dnet, nj * (1 if cfg.view_angle else 3), cfg.multires_views, alpha_views)
     return s
 
 

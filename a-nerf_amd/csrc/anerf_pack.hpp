@@ -543,7 +543,18 @@ static int validate_desc(const anerf_model_desc* d) {
     if (d->framecode_ch < 0 || d->framecode_ch > 64) return fail(ANERF_EINVAL, "framecode_ch outside [0, 64]");
     if (d->framecode_ch > 0 && d->n_framecodes <= 0) return fail(ANERF_EINVAL, "n_framecodes must be > 0");
     if (d->density_scale == 0.0f) return fail(ANERF_EINVAL, "density_scale must be non-zero");
+    if (d->multires_bones < 0 || d->multires_bones > 10) return fail(ANERF_EINVAL, "multires_bones outside [0, 10]");
+    if (d->encoder_flags & ~(ANERF_ENC_CUT_TO_DIST | ANERF_ENC_CUTOFF_SHIFT | ANERF_ENC_CUTOFF_BONES | ANERF_ENC_VIEW_RAW |
+                             ANERF_ENC_KP_RELPOS | ANERF_ENC_VIEW_ANGLE))
+        return fail(ANERF_EINVAL, "unknown encoder_flags bits");
+    if ((d->encoder_flags & ANERF_ENC_VIEW_RAW) && (d->encoder_flags & ANERF_ENC_VIEW_ANGLE))
+        return fail(ANERF_EINVAL, "ANERF_ENC_VIEW_RAW and ANERF_ENC_VIEW_ANGLE are two view types");
     return ANERF_OK;
+}
+
+// A staged encoder (anerf.h, ABI 15): the training stages serve the model, the fused kernels do not.
+static bool desc_staged(const anerf_model_desc* d) {
+    return d->multires_bones > 0 || (d->encoder_flags & (ANERF_ENC_KP_RELPOS | ANERF_ENC_VIEW_ANGLE));
 }
 
 static int pack_net(const anerf_model_desc* d, int njh2, const anerf_net_weights* w, Packer& pk,

@@ -129,28 +129,35 @@ int anerf_model_create(const anerf_model_desc* desc, const anerf_net_weights* co
     *out = nullptr;
     int rc = validate_desc(desc);
     if (rc) return rc;
-    if (!coarse || !embed) return fail(ANERF_EINVAL, "coarse weights / embed params are NULL");
-    if (desc->has_fine && !fine) return fail(ANERF_EINVAL, "has_fine but fine weights are NULL");
+    if (!embed) return fail(ANERF_EINVAL, "embed params are NULL");
+    const bool staged = desc_staged(desc);  // (the training stages only: no packed weights, anerf.h)
+    if (!staged && !coarse) return fail(ANERF_EINVAL, "coarse weights are NULL");
+    if (!staged && desc->has_fine && !fine) return fail(ANERF_EINVAL, "has_fine but fine weights are NULL");
     if (!embed->cutoff_dist || !embed->cutoff_dist_v) return fail(ANERF_EINVAL, "cutoff_dist is NULL");
     // --cutoff_bones windows the bone directions only through a CutoffEmbedder that weights its input
-    // (use_cutoff, cutoff_inputs; multires_bones 0), as in core/cutoff_embedder.py:156-166
-    const bool bone_cut = (desc->encoder_flags & ANERF_ENC_CUTOFF_BONES) && desc->use_cutoff && desc->cutoff_inputs;
-    if (bone_cut && !embed->cutoff_dist_b)
+    // (use_cutoff, cutoff_inputs; multires_bones 0), as in core/cutoff_embedder.py:156-166; with bone
+    // frequencies (staged) the CutoffEmbedder windows their sin / cos whatever cutoff_inputs says
+    const bool bone_win = (desc->encoder_flags & ANERF_ENC_CUTOFF_BONES) && desc->use_cutoff;
+    const bool bone_cut = bone_win && desc->cutoff_inputs;
+    if ((bone_cut || (bone_win && desc->multires_bones > 0)) && !embed->cutoff_dist_b)
         return fail(ANERF_EINVAL, "ANERF_ENC_CUTOFF_BONES: embed->cutoff_dist_b (embedbones_fn.cutoff_dist) is NULL");
+    const bool bone_tab = bone_cut || (bone_win && desc->multires_bones > 0);
     const int nj = desc->n_joints;
     const int njh2 = (((nj + 1) / 2) + 1) & ~1;  // joint pairs of the u part, even
     const int ngh = std::max(2 * njh2, nj + 2) / 2;  // G columns / 2: joint p + h*NJH2 at k-step p, bias at NJ
     Packer pk;
     std::vector<size_t> oc, of;
-    rc = pack_net(desc, njh2, coarse, pk, oc);
-    if (rc) return rc;
-    if (desc->has_fine) {
-        rc = pack_net(desc, njh2, fine, pk, of);
+    if (!staged) {
+        rc = pack_net(desc, njh2, coarse, pk, oc);
         if (rc) return rc;
+        if (desc->has_fine) {
+            rc = pack_net(desc, njh2, fine, pk, of);
+            if (rc) return rc;
+        }
     }
     const size_t off_cut = pk.add(std::vector<float>(embed->cutoff_dist, embed->cutoff_dist + nj));
     const size_t off_cutv = pk.add(std::vector<float>(embed->cutoff_dist_v, embed->cutoff_dist_v + nj));
-    const size_t off_cutb = pk.add(bone_cut ? std::vector<float>(embed->cutoff_dist_b, embed->cutoff_dist_b + nj)
+    const size_t off_cutb = pk.add(bone_tab ? std::vector<float>(embed->cutoff_dist_b, embed->cutoff_dist_b + nj)
                                             : std::vector<float>(nj, 0.0f));
 
     int prev = 0;
@@ -198,17 +205,24 @@ int anerf_model_create(const anerf_model_desc* desc, const anerf_net_weights* co
     md.B = desc->density_scale;
     md.bone_cut = bone_cut ? 1 : 0;
     md.view_raw = (desc->encoder_flags & ANERF_ENC_VIEW_RAW) ? 1 : 0;
+    md.mrb = desc->multires_bones;
+    md.kp_relpos = (desc->encoder_flags & ANERF_ENC_KP_RELPOS) ? 1 : 0;
+    md.view_angle = (desc->encoder_flags & ANERF_ENC_VIEW_ANGLE) ? 1 : 0;
+    md.bone_win = bone_win ? 1 : 0;
+    md.staged = staged ? 1 : 0;
     md.tau = embed->tau;
     md.tau_v = embed->tau_v;
-    md.tau_b = bone_cut ? embed->tau_b : 0.0f;
+    md.tau_b = bone_tab ? embed->tau_b : 0.0f;
     md.cutoff = dbuf + off_cut;
     md.cutoff_v = dbuf + off_cutv;
     md.cutoff_b = dbuf + off_cutb;
-    bind_net(desc, dbuf, oc, coarse->alpha_b[0], md.net[0]);
-    if (desc->has_fine) bind_net(desc, dbuf, of, fine->alpha_b[0], md.net[1]);
-    else md.net[1] = md.net[0];
+    if (!staged) {
+        bind_net(desc, dbuf, oc, coarse->alpha_b[0], md.net[0]);
+        if (desc->has_fine) bind_net(desc, dbuf, of, fine->alpha_b[0], md.net[1]);
+        else md.net[1] = md.net[0];
+    }
     m->cut_host.assign(embed->cutoff_dist, embed->cutoff_dist + nj);
-    enc16_units(m);
+    if (!staged) enc16_units(m);
     *out = m;
     return ANERF_OK;
 }
@@ -225,7 +239,8 @@ size_t anerf_model_bytes(const anerf_model* m) { return m ? m->dev_bytes : 0; }
 
 int anerf_model_set_embed(anerf_model* m, const anerf_embed_params* embed) {
     if (!m || !embed) return fail(ANERF_EINVAL, "anerf_model_set_embed: NULL argument");
-    const bool cb = m->md.bone_cut && embed->cutoff_dist_b;
+    const bool btab = m->md.bone_cut || (m->md.bone_win && m->md.mrb > 0);  // (the bone window is read)
+    const bool cb = btab && embed->cutoff_dist_b;
     if (embed->cutoff_dist || embed->cutoff_dist_v || cb) {
         const size_t nb = sizeof(float) * (size_t)m->desc.n_joints;
         int prev = 0;
@@ -243,9 +258,9 @@ int anerf_model_set_embed(anerf_model* m, const anerf_embed_params* embed) {
     }
     m->md.tau = embed->tau;
     m->md.tau_v = embed->tau_v;
-    if (m->md.bone_cut) m->md.tau_b = embed->tau_b;
+    if (btab) m->md.tau_b = embed->tau_b;
     if (embed->cutoff_dist) m->cut_host.assign(embed->cutoff_dist, embed->cutoff_dist + m->desc.n_joints);
-    enc16_units(m);  // (the windowed features' bound moves with tau and the cutoffs)
+    if (!m->md.staged) enc16_units(m);  // (the windowed features' bound moves with tau and the cutoffs)
     return ANERF_OK;
 }
 
@@ -316,6 +331,7 @@ int anerf_render_rays(const anerf_model* m, const float* ray_batch, int32_t ray_
                       float* alpha0, const anerf_debug* debug, void* workspace, size_t workspace_bytes,
                       void* stream) {
     if (!m) return fail(ANERF_EINVAL, "model is NULL");
+    if (m->md.staged) return fail(ANERF_EINVAL, "anerf_render_rays: staged encoder (multires_bones > 0, relpos or rayangle kp / view inputs): the training stages serve this model, anerf.h");
     if (n_rays < 0) return fail(ANERF_EINVAL, "n_rays < 0");
     if (n_rays == 0) return ANERF_OK;
     const int flags = precision & ~0xff;  // ANERF_FLAG_* bits above the precision mode
@@ -526,6 +542,7 @@ int anerf_compose_box(const float* rgb, const float* disp, const float* acc, int
 int anerf_encode_points(const anerf_model* m, const float* skts, const float* pts, const float* dirs, int64_t n_points,
                         float* feat_out, void* stream) {
     if (!m || !skts || !pts || !dirs || !feat_out || n_points < 0) return fail(ANERF_EINVAL, "anerf_encode_points: bad arguments");
+    if (m->md.staged) return fail(ANERF_EINVAL, "anerf_encode_points: staged encoder (multires_bones > 0, relpos or rayangle kp / view inputs): the training stages serve this model, anerf.h");
     if (n_points == 0) return ANERF_OK;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(encode_points_kernel, dim3((unsigned)((n_points + 127) / 128)), dim3(128), 0, st, m->md, skts,
@@ -596,7 +613,8 @@ int anerf_train_encode_backward(const anerf_model* m, const float* ray_batch, in
                            m->md, ray_batch, ray_stride, n_rays, z, n_samples, skts, ray_pose, n_poses, pts_noise,
                            grad_feat, grad_skts, spb);
     };
-    if (mr == 7 && mrv == 4) launch(train_encode_backward_kernel<7, 4>);
+    if (m->md.staged) launch(train_encode_backward_kernel<-1, -1>);  // (the staged encoders: run-time layout)
+    else if (mr == 7 && mrv == 4) launch(train_encode_backward_kernel<7, 4>);
     else if (mr == 7 && mrv == 0) launch(train_encode_backward_kernel<7, 0>);
     else if (mr == 10 && mrv == 4) launch(train_encode_backward_kernel<10, 4>);
     else if (mr == 10 && mrv == 0) launch(train_encode_backward_kernel<10, 0>);
@@ -704,6 +722,7 @@ static int launch_density(const anerf_model* m, DensityArgs a, int32_t precision
 int anerf_density_points(const anerf_model* m, const float* pts, int64_t n_points, const float* skts, int32_t net,
                          int32_t precision, float* raw_out, void* stream) {
     if (!m || n_points < 0) return fail(ANERF_EINVAL, "anerf_density_points: bad arguments");
+    if (m->md.staged) return fail(ANERF_EINVAL, "anerf_density_points: staged encoder (multires_bones > 0, relpos or rayangle kp / view inputs): the training stages serve this model, anerf.h");
     if (n_points == 0) return ANERF_OK;
     if (!pts || !skts || !raw_out) return fail(ANERF_EINVAL, "anerf_density_points: bad arguments");
     DensityArgs a;
@@ -719,6 +738,7 @@ int anerf_density_points(const anerf_model* m, const float* pts, int64_t n_point
 int anerf_density_grid(const anerf_model* m, const float* axis, int32_t res1, const float* kp0, const float* skts,
                        int32_t net, int32_t precision, float* raw_out, void* stream) {
     if (!m || !axis || !kp0 || !skts || !raw_out || res1 < 1) return fail(ANERF_EINVAL, "anerf_density_grid: bad arguments");
+    if (m->md.staged) return fail(ANERF_EINVAL, "anerf_density_grid: staged encoder (multires_bones > 0, relpos or rayangle kp / view inputs): the training stages serve this model, anerf.h");
     DensityArgs a;
     std::memset(&a, 0, sizeof(a));
     a.t = axis;

@@ -29,38 +29,105 @@ __global__ void train_z_kernel(const float* __restrict__ nearp, const float* __r
     z[idx] = zv;
 }
 
+// Feature-row layout of a model (anerf.h, "staged encoders"): per-joint kp dims (1 reldist / 3 relpos), per-joint
+// view dims (3 relray / world, 1 rayangle), the bone and view parts' first columns and the row width.  Column of
+// feature (frequency slot f, joint j, component c) in a part: part + (f NJ + j) dims + c.
+struct FeatLayout {
+    int nkp, nvw, cb, cv, F;
+};
+__host__ __device__ inline FeatLayout feat_layout(const ModelDev& M) {
+    FeatLayout L;
+    L.nkp = M.kp_relpos ? 3 : 1;
+    L.nvw = M.view_angle ? 1 : 3;
+    L.cb = M.nj * L.nkp * (1 + 2 * M.mr);
+    L.cv = L.cb + 3 * M.nj * (1 + 2 * M.mrb);
+    L.F = L.cv + M.nj * L.nvw * (1 + 2 * M.mrv);
+    return L;
+}
+
+// RayAngEncoder's input (core/encoders.py:195-212 -> skeleton_utils.py:594-605): the angle between the local point
+// q and the local ray direction e, acos(clamp(q.e / (|q| |e|), -1 + 1e-6, 1 - 1e-6)) - pi / 2; also the cosine
+__device__ __forceinline__ float ray_angle(float qx, float qy, float qz, float ex, float ey, float ez, float& cs) {
+    const float dot = qx * ex + qy * ey + qz * ez;  // ((a * b).sum(-1): elementwise products, then the sum)
+    cs = dot / (norm3(qx, qy, qz) * norm3(ex, ey, ez));
+    const float cl = fminf(fmaxf(cs, -1.0f + 1e-6f), 1.0f - 1e-6f);
+    return acosf(cl) - 1.5707963267948966f;
+}
+
 // encode_inputs over a ray batch: sample s of ray i at p = o + d z (sample_pts,
 // raycasters.py:650-663), pose ray_pose[i] (or i when per_ray), feature row [v | r | d] of
 // encode_row.  One thread per (sample, joint): consecutive lanes are consecutive joints, so every
-// feature k (layout k NJ + j) is written by contiguous lanes.
+// feature k (layout k NJ + j) is written by contiguous lanes.  Staged encoders (anerf.h): relpos kp
+// inputs, bone frequencies and ray angles in the same row layout (feat_layout).
 __device__ __forceinline__ void encode_joint(const ModelDev& M, const float* __restrict__ S, int j, float px,
                                              float py, float pz, float dx, float dy, float dz, float* __restrict__ f) {
-    const int nj = M.nj, nv = 1 + 2 * M.mr;
-    const int cx = nj * nv + 3 * nj;
+    const int nj = M.nj;
+    const FeatLayout L = feat_layout(M);
     float qx, qy, qz;
     joint_local(S, px, py, pz, qx, qy, qz);
     const float dist = norm3(qx, qy, qz);
     const float dn = fmaxf(dist, 1e-12f);
     const float w = M.use_cutoff ? cutoff_w(M.tau, dist, M.cutoff[j]) : 1.0f;
-    float u, uf;
-    kp_inputs(M.cut_to, M.shift_in, dist, M.cutoff[j], u, uf);
-    f[j] = (M.use_cutoff && M.cutoff_inputs) ? u * w : u;
-    for (int fi = 0; fi < M.mr; ++fi) {
-        float s, c;
-        sincos_rr(uf * (float)(1 << fi), s, c);
-        f[(1 + 2 * fi) * nj + j] = s * w;
-        f[(2 + 2 * fi) * nj + j] = c * w;
+    if (!M.kp_relpos) {
+        float u, uf;
+        kp_inputs(M.cut_to, M.shift_in, dist, M.cutoff[j], u, uf);
+        f[j] = (M.use_cutoff && M.cutoff_inputs) ? u * w : u;
+        for (int fi = 0; fi < M.mr; ++fi) {
+            float s, c;
+            sincos_rr(uf * (float)(1 << fi), s, c);
+            f[(1 + 2 * fi) * nj + j] = s * w;
+            f[(2 + 2 * fi) * nj + j] = c * w;
+        }
+    } else {  // relpos: q itself, the window of all three from the joint distance (dist_inputs)
+        const float q[3] = {qx, qy, qz};
+        for (int c = 0; c < 3; ++c) {
+            f[3 * j + c] = (M.use_cutoff && M.cutoff_inputs) ? q[c] * w : q[c];
+            for (int fi = 0; fi < M.mr; ++fi) {
+                float s, co;
+                sincos_rr(q[c] * (float)(1 << fi), s, co);
+                f[3 * ((1 + 2 * fi) * nj + j) + c] = s * w;
+                f[3 * ((2 + 2 * fi) * nj + j) + c] = co * w;
+            }
+        }
     }
-    // bone directions, times w_b under --cutoff_bones (bone CutoffEmbedder, multires_bones 0)
-    const float wb = M.bone_cut ? cutoff_w(M.tau_b, dist, M.cutoff_b[j]) : 1.0f;
-    f[nj * nv + 3 * j + 0] = M.bone_cut ? (qx / dn) * wb : qx / dn;
-    f[nj * nv + 3 * j + 1] = M.bone_cut ? (qy / dn) * wb : qy / dn;
-    f[nj * nv + 3 * j + 2] = M.bone_cut ? (qz / dn) * wb : qz / dn;
+    // bone directions, times w_b under --cutoff_bones (bone CutoffEmbedder); with bone frequencies the
+    // sin / cos of each direction component, windowed by w_b when the bone embedder is a CutoffEmbedder
+    if (M.mrb == 0) {
+        const float wb = M.bone_cut ? cutoff_w(M.tau_b, dist, M.cutoff_b[j]) : 1.0f;
+        f[L.cb + 3 * j + 0] = M.bone_cut ? (qx / dn) * wb : qx / dn;
+        f[L.cb + 3 * j + 1] = M.bone_cut ? (qy / dn) * wb : qy / dn;
+        f[L.cb + 3 * j + 2] = M.bone_cut ? (qz / dn) * wb : qz / dn;
+    } else {
+        const float wb = M.bone_win ? cutoff_w(M.tau_b, dist, M.cutoff_b[j]) : 1.0f;
+        const float ub[3] = {qx / dn, qy / dn, qz / dn};
+        for (int c = 0; c < 3; ++c) {
+            f[L.cb + 3 * j + c] = M.bone_cut ? ub[c] * wb : ub[c];
+            for (int fi = 0; fi < M.mrb; ++fi) {
+                float s, co;
+                sincos_rr(ub[c] * (float)(1 << fi), s, co);
+                f[L.cb + 3 * ((1 + 2 * fi) * nj + j) + c] = s * wb;
+                f[L.cb + 3 * ((2 + 2 * fi) * nj + j) + c] = co * wb;
+            }
+        }
+    }
     float ex, ey, ez;
     joint_rot(S, dx, dy, dz, ex, ey, ez);
+    const float wv = M.cutoff_viewdir ? cutoff_w(M.tau_v, dist, M.cutoff_v[j]) : 1.0f;
+    if (M.view_angle) {
+        float cs;
+        const float a = ray_angle(qx, qy, qz, ex, ey, ez, cs);
+        f[L.cv + j] = (M.cutoff_viewdir && M.cutoff_inputs) ? a * wv : a;
+        for (int fi = 0; fi < M.mrv; ++fi) {
+            float s, co;
+            sincos_rr(a * (float)(1 << fi), s, co);
+            f[L.cv + (1 + 2 * fi) * nj + j] = s * wv;
+            f[L.cv + (2 + 2 * fi) * nj + j] = co * wv;
+        }
+        return;
+    }
     const float en = M.view_raw ? 1.0f : fmaxf(norm3(ex, ey, ez), 1e-12f);  // (--view_type world: R_j d itself)
     const float e[3] = {ex / en, ey / en, ez / en};
-    const float wv = M.cutoff_viewdir ? cutoff_w(M.tau_v, dist, M.cutoff_v[j]) : 1.0f;
+    const int cx = L.cv;
     for (int c = 0; c < 3; ++c) {
         f[cx + 3 * j + c] = (M.cutoff_viewdir && M.cutoff_inputs) ? e[c] * wv : e[c];
         for (int fi = 0; fi < M.mrv; ++fi) {
@@ -89,7 +156,7 @@ __global__ void train_encode_kernel(ModelDev M, const float* __restrict__ rb, in
     if (pts_noise) {  // sample_pts' ray_noise_std (raycasters.py:660-661): pts + randn * std
         px += pts_noise[3 * idx], py += pts_noise[3 * idx + 1], pz += pts_noise[3 * idx + 2];
     }
-    const int F = nj * (1 + 2 * M.mr) + 3 * nj + 3 * nj * (1 + 2 * M.mrv);
+    const int F = feat_layout(M).F;
     f32x4 r0, r1, r2;
     if (pose >= 0 && pose < n_poses) {
         const f32x4* sp = reinterpret_cast<const f32x4*>(skts + (pose * nj + j) * 16);
@@ -251,6 +318,163 @@ __device__ __forceinline__ void encode_row_grad_joint(const ModelDev& M, const f
     }
 }
 
+// d feature / d inputs for the staged encoders (anerf.h, ABI 15), run-time frequency counts: relpos kp inputs,
+// bone frequencies, ray angles, with every option of encode_joint.  With relpos the reference's window distance
+// is |p - kp_j| (raycasters.py:530-533), not a function of the poses: no window gradient reaches skts then.
+__device__ __noinline__ void encode_row_grad_joint_staged(const ModelDev& M, const float* __restrict__ S, int j,
+                                                          float px, float py, float pz, float dx, float dy, float dz,
+                                                          const float* __restrict__ g, float (&gS)[12]) {
+    const int nj = M.nj;
+    const FeatLayout L = feat_layout(M);
+    const bool dg = !M.kp_relpos;  // (the windows' distance carries a gradient)
+    float qx, qy, qz;
+    joint_local(S, px, py, pz, qx, qy, qz);
+    const float dist = norm3(qx, qy, qz);
+    const float q[3] = {qx, qy, qz};
+    float gq[3] = {0.0f, 0.0f, 0.0f};
+    float g_dist = 0.0f;
+    // ---- kp part
+    const bool cut = M.use_cutoff != 0, cut_in = M.use_cutoff && M.cutoff_inputs;
+    const float w = cut ? cutoff_w(M.tau, dist, M.cutoff[j]) : 1.0f;
+    float g_w = 0.0f;
+    if (!M.kp_relpos) {
+        float u, uf;
+        kp_inputs(M.cut_to, M.shift_in, dist, M.cutoff[j], u, uf);
+        const float du = M.cut_to ? -1.0f : 1.0f;
+        const float duf = M.shift_in ? du * (2.0f / M.cutoff[j]) : du;
+        const float g0 = g[j];
+        if (cut_in) {
+            g_dist += g0 * w * du;
+            g_w += g0 * u;
+        } else {
+            g_dist += g0 * du;
+        }
+        for (int fi = 0; fi < M.mr; ++fi) {
+            const float fr = (float)(1 << fi);
+            float sn, cs;
+            sincos_rr(uf * fr, sn, cs);
+            const float gs = g[(1 + 2 * fi) * nj + j], gc = g[(2 + 2 * fi) * nj + j];
+            g_w += gs * sn + gc * cs;
+            g_dist += (gs * cs - gc * sn) * w * fr * duf;
+        }
+    } else {
+        for (int c = 0; c < 3; ++c) {
+            const float g0 = g[3 * j + c];
+            gq[c] += cut_in ? g0 * w : g0;
+            if (cut_in) g_w += g0 * q[c];
+            for (int fi = 0; fi < M.mr; ++fi) {
+                const float fr = (float)(1 << fi);
+                float sn, cs;
+                sincos_rr(q[c] * fr, sn, cs);
+                const float gs = g[3 * ((1 + 2 * fi) * nj + j) + c], gc = g[3 * ((2 + 2 * fi) * nj + j) + c];
+                g_w += gs * sn + gc * cs;
+                gq[c] += (gs * cs - gc * sn) * w * fr;
+            }
+        }
+    }
+    if (cut && dg) g_dist += g_w * (-M.tau * w * (1.0f - w));
+    // ---- bone part: u = q / max(|q|, eps), its frequencies, the bone window
+    {
+        const float dn = fmaxf(dist, 1e-12f);
+        const float ub[3] = {qx / dn, qy / dn, qz / dn};
+        const bool win = M.mrb > 0 ? M.bone_win != 0 : M.bone_cut != 0;
+        const float wb = win ? cutoff_w(M.tau_b, dist, M.cutoff_b[j]) : 1.0f;
+        float gu[3], g_wb = 0.0f;
+        for (int c = 0; c < 3; ++c) {
+            const float g0 = g[L.cb + 3 * j + c];
+            gu[c] = M.bone_cut ? g0 * wb : g0;
+            if (M.bone_cut) g_wb += g0 * ub[c];
+            for (int fi = 0; fi < M.mrb; ++fi) {
+                const float fr = (float)(1 << fi);
+                float sn, cs;
+                sincos_rr(ub[c] * fr, sn, cs);
+                const float gs = g[L.cb + 3 * ((1 + 2 * fi) * nj + j) + c], gc = g[L.cb + 3 * ((2 + 2 * fi) * nj + j) + c];
+                g_wb += gs * sn + gc * cs;
+                gu[c] += (gs * cs - gc * sn) * wb * fr;
+            }
+        }
+        if (win && dg) g_dist += g_wb * (-M.tau_b * wb * (1.0f - wb));
+        if (dist > 1e-12f) {
+            const float dot = ub[0] * gu[0] + ub[1] * gu[1] + ub[2] * gu[2];
+            for (int c = 0; c < 3; ++c) gq[c] += (gu[c] - ub[c] * dot) / dist;
+        } else {
+            for (int c = 0; c < 3; ++c) gq[c] += gu[c] / 1e-12f;
+        }
+    }
+    // ---- view part
+    float ex, ey, ez;
+    joint_rot(S, dx, dy, dz, ex, ey, ez);
+    const bool cutv = M.cutoff_viewdir != 0;
+    const float wv = cutv ? cutoff_w(M.tau_v, dist, M.cutoff_v[j]) : 1.0f;
+    float gr[3] = {0.0f, 0.0f, 0.0f}, g_wv = 0.0f;
+    if (M.view_angle) {
+        float cs;
+        const float a = ray_angle(qx, qy, qz, ex, ey, ez, cs);
+        const float g0 = g[L.cv + j];
+        float ga = (cutv && M.cutoff_inputs) ? g0 * wv : g0;
+        if (cutv && M.cutoff_inputs) g_wv += g0 * a;
+        for (int fi = 0; fi < M.mrv; ++fi) {
+            const float fr = (float)(1 << fi);
+            float sn, co;
+            sincos_rr(a * fr, sn, co);
+            const float gs = g[L.cv + (1 + 2 * fi) * nj + j], gc = g[L.cv + (2 + 2 * fi) * nj + j];
+            g_wv += gs * sn + gc * co;
+            ga += (gs * co - gc * sn) * wv * fr;
+        }
+        // acos' slope inside the clamp (torch.clamp passes the gradient on [min, max]), then the cosine's
+        const bool inside = cs >= -1.0f + 1e-6f && cs <= 1.0f - 1e-6f;
+        const float gcs = inside ? -ga / sqrtf(fmaxf(1.0f - cs * cs, 1e-30f)) : 0.0f;
+        const float nq = dist, ne = norm3(ex, ey, ez);
+        const float e[3] = {ex, ey, ez};
+        if (nq > 0.0f && ne > 0.0f) {
+            const float inv = 1.0f / (nq * ne);
+            for (int c = 0; c < 3; ++c) {
+                gq[c] += gcs * (e[c] * inv - cs * q[c] / (nq * nq));
+                gr[c] += gcs * (q[c] * inv - cs * e[c] / (ne * ne));
+            }
+        }
+    } else {
+        const float enr = norm3(ex, ey, ez);
+        const float en = M.view_raw ? 1.0f : fmaxf(enr, 1e-12f);
+        const float e[3] = {ex / en, ey / en, ez / en};
+        float ge[3] = {0.0f, 0.0f, 0.0f};
+        for (int c = 0; c < 3; ++c) {
+            const float gv0 = g[L.cv + 3 * j + c];
+            if (cutv && M.cutoff_inputs) {
+                ge[c] += gv0 * wv;
+                g_wv += gv0 * e[c];
+            } else {
+                ge[c] += gv0;
+            }
+            for (int fi = 0; fi < M.mrv; ++fi) {
+                const float fr = (float)(1 << fi);
+                float sn, co;
+                sincos_rr(e[c] * fr, sn, co);
+                const float gs = g[L.cv + (1 + 2 * fi) * 3 * nj + 3 * j + c], gc = g[L.cv + (2 + 2 * fi) * 3 * nj + 3 * j + c];
+                g_wv += gs * sn + gc * co;
+                ge[c] += (gs * co - gc * sn) * wv * fr;
+            }
+        }
+        if (M.view_raw) {
+            for (int c = 0; c < 3; ++c) gr[c] = ge[c];
+        } else if (enr > 1e-12f) {
+            const float dot = e[0] * ge[0] + e[1] * ge[1] + e[2] * ge[2];
+            for (int c = 0; c < 3; ++c) gr[c] = (ge[c] - e[c] * dot) / enr;
+        } else {
+            for (int c = 0; c < 3; ++c) gr[c] = ge[c] / 1e-12f;
+        }
+    }
+    if (cutv && dg) g_dist += g_wv * (-M.tau_v * wv * (1.0f - wv));
+    if (dist > 0.0f)
+        for (int c = 0; c < 3; ++c) gq[c] += g_dist * q[c] / dist;
+    for (int r = 0; r < 3; ++r) {  // q = A p + t, e_raw = A d
+        gS[4 * r + 0] += gq[r] * px + gr[r] * dx;
+        gS[4 * r + 1] += gq[r] * py + gr[r] * dy;
+        gS[4 * r + 2] += gq[r] * pz + gr[r] * dz;
+        gS[4 * r + 3] += gq[r];
+    }
+}
+
 // Encoder backward: dL/dskts from dL/dfeat.  Block = one ray, thread = (sample slot, joint) with the
 // joint fastest (spb sample slots x nj joints, spb = 256 / nj), so each thread keeps one joint's 12
 // sums over the samples s = slot, slot + spb, ... and the lanes of a wave read each feature of a
@@ -276,7 +500,7 @@ __global__ __launch_bounds__(256) void train_encode_backward_kernel(ModelDev M, 
     float gS[12] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
     if (pose_ok && slot < spb) {
         const float* ray = rb + i * stride;
-        const int F = nj * (1 + 2 * M.mr) + 3 * nj + 3 * nj * (1 + 2 * M.mrv);  // (M.mr == MR when MR >= 0)
+        const int F = feat_layout(M).F;
         const f32x4* sp = reinterpret_cast<const f32x4*>(skts + (pose * nj + j) * 16);
         const f32x4 r0 = sp[0], r1 = sp[1], r2 = sp[2];
         const float S[12] = {r0[0], r0[1], r0[2], r0[3], r1[0], r1[1], r1[2], r1[3], r2[0], r2[1], r2[2], r2[3]};
@@ -287,7 +511,10 @@ __global__ __launch_bounds__(256) void train_encode_backward_kernel(ModelDev M, 
                 const float* q = pts_noise + 3 * (i * ns + s);
                 px += q[0], py += q[1], pz += q[2];
             }
-            encode_row_grad_joint<MR, MRV>(M, S, j, px, py, pz, ray[3], ray[4], ray[5], gfeat + (i * ns + s) * F, gS);
+            if (MR < 0 && M.staged)  // (the generic instance serves the staged encoders too)
+                encode_row_grad_joint_staged(M, S, j, px, py, pz, ray[3], ray[4], ray[5], gfeat + (i * ns + s) * F, gS);
+            else
+                encode_row_grad_joint<MR, MRV>(M, S, j, px, py, pz, ray[3], ray[4], ray[5], gfeat + (i * ns + s) * F, gS);
         }
         float* const rr = red + (slot * nj + j) * 12;
 #pragma unroll

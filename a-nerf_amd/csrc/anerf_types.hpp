@@ -89,6 +89,9 @@ struct ModelDev {
     int h3_top;      // fp16x3: biased exponent the largest scaled activation of a sample gets (127 + 10)
     int bone_cut;    // --cutoff_bones (+ use_cutoff, cutoff_inputs): bone directions times w_b
     int view_raw;    // --view_type world: the view input is R_j d, not normalised (ANERF_ENC_VIEW_RAW)
+    // staged encoders (ABI 15, training stages only; anerf.h): bone frequencies, relpos kp inputs, ray angles;
+    // bone_win: the bone embedder is a CutoffEmbedder (--cutoff_bones + use_cutoff: windows its sin / cos)
+    int mrb, kp_relpos, view_angle, bone_win, staged;
     // fp16x4 / fp16x3: the encoder-fed parts (bone-direction and windowed x parts of layer 0 and the skip
     // layer) as fp16 splits too, when every windowed feature is bounded (sparse windows, tau > 0; host:
     // enc16_units in anerf_pack.hpp); bf16x6 parts otherwise

@@ -55,9 +55,14 @@ class DeviceModel:
         d.single_net = int(cfg.single_net)
         d.encoder_flags = ((_lib.ANERF_ENC_CUT_TO_DIST if cfg.cut_to_dist else 0) |
                            (_lib.ANERF_ENC_CUTOFF_SHIFT if cfg.cutoff_shift else 0) |
-                           (_lib.ANERF_ENC_CUTOFF_BONES if cfg.bone_window and cfg.cutoff_inputs else 0) |
-                           (_lib.ANERF_ENC_VIEW_RAW if cfg.extra.get("view_type", "relray") == "world" else 0))
-        # (the C side applies the flag under the same condition: anerf.h, ANERF_ENC_CUTOFF_BONES)
+                           (_lib.ANERF_ENC_CUTOFF_BONES if cfg.bone_window else 0) |
+                           (_lib.ANERF_ENC_VIEW_RAW if cfg.extra.get("view_type", "relray") == "world" else 0) |
+                           (_lib.ANERF_ENC_KP_RELPOS if cfg.kp_relpos else 0) |
+                           (_lib.ANERF_ENC_VIEW_ANGLE if cfg.view_angle else 0))
+        d.multires_bones = cfg.multires_bones
+        # (the C side windows the bare bone directions under the reference's condition, cutoff_inputs too:
+        # anerf.h, ANERF_ENC_CUTOFF_BONES)
+        self.staged = cfg.staged  # (no packed weights: the training stages serve the model, anerf.h)
         d.has_fine = int(fine_sd is not None and cfg.N_importance > 0)
         self.has_fine = bool(d.has_fine)
         e, ev = ckpt["embed_state_dict"], ckpt["embeddirs_state_dict"]
@@ -65,13 +70,13 @@ class DeviceModel:
         # that consume those features (layer 0, the skip layer's x part, the view layer's direction
         # part) -- the same products up to one rounding of w * s (config.feature_scales)
         self._fs = None
-        if cfg.freq_schedule:
+        if cfg.freq_schedule and not cfg.staged:
             if "sched_alpha" not in e or "sched_alpha" not in ev:
                 raise ValueError("freq_schedule: the checkpoint's embed state has no sched_alpha buffer")
             self._fs = feature_scales(cfg, float(_np(e["sched_alpha"]).reshape(-1)[0]),
                                       float(_np(ev["sched_alpha"]).reshape(-1)[0]))
-        coarse = self._net(coarse_sd)
-        fine = self._net(fine_sd) if d.has_fine else None
+        coarse = self._net(coarse_sd) if not cfg.staged else None
+        fine = self._net(fine_sd) if d.has_fine and not cfg.staged else None
         emb = _lib.EmbedParams()
         emb.cutoff_dist, emb.tau = self._p(e["cutoff_dist"]), float(_np(e["tau"]).reshape(-1)[0])
         emb.cutoff_dist_v, emb.tau_v = self._p(ev["cutoff_dist"]), float(_np(ev["tau"]).reshape(-1)[0])
@@ -81,7 +86,8 @@ class DeviceModel:
                 raise ValueError("cutoff_bones: the checkpoint's embedbones_state_dict has no cutoff_dist / tau")
             emb.cutoff_dist_b, emb.tau_b = self._p(eb["cutoff_dist"]), float(_np(eb["tau"]).reshape(-1)[0])
         h = ctypes.c_void_p()
-        rc = lib.anerf_model_create(ctypes.byref(d), ctypes.byref(coarse), ctypes.byref(fine) if fine else None,
+        rc = lib.anerf_model_create(ctypes.byref(d), ctypes.byref(coarse) if coarse else None,
+                                    ctypes.byref(fine) if fine else None,
                                     ctypes.byref(emb), self.device, ctypes.byref(h))
         _lib.check(rc, "anerf_model_create")
         self.handle = h

@@ -5,6 +5,9 @@ dict of `_collect_outputs`, :711-724) and the model factory `create_raycaster`
 (:17-184).  `render_rays` keeps the reference signature; what the reference does in a
 dozen ATen ops per stage happens in one fused launch (`anerf_render_rays`).
 
+Staged encoders (`--multires_bones > 0`, `--kp_dist_type relpos`, `--view_type rayangle`; include/anerf.h)
+render on the training stages instead (`train.StagedCaster`, deterministic).
+
 Supported: eval-mode rendering (`perturb=0`, `raw_noise_std=0`, `ray_noise_std=0`; `lindisp`
 either way), any per-ray poses (`skts`/`cyls` may be expanded views of one pose —
 detected without copying — or genuinely per-ray), framecodes via `cams`; density-only
@@ -53,7 +56,15 @@ class RayCaster:
 
     def __init__(self, cfg, ckpt, device=None):
         self.cfg = cfg.validate()
-        self.model = DeviceModel(cfg, ckpt, device=device)
+        self._staged = None
+        if cfg.staged:
+            # (bone frequencies / relpos / ray angles: the training stages render the model deterministically,
+            # include/anerf.h "staged encoders", train.StagedCaster)
+            from .train import TrainRayCaster
+            self._staged = TrainRayCaster(cfg, ckpt, device=device).eval()
+            self.model = self._staged.model
+        else:
+            self.model = DeviceModel(cfg, ckpt, device=device)
         self.training = False
         self.last_debug = None
 
@@ -68,6 +79,10 @@ class RayCaster:
         return self
 
     def load_state_dict(self, ckpt, strict=True):
+        if self._staged is not None:
+            self._staged.load_checkpoint(ckpt)
+            self.model = self._staged.model
+            return
         self.model.close()
         self.model = DeviceModel(self.cfg, ckpt, device=self.model.device)
 
@@ -76,6 +91,8 @@ class RayCaster:
 
     def forward(self, *args, fwd_type="", **kwargs):
         """core/raycasters.py:349-359."""
+        if self._staged is not None:
+            return self._staged.eval_caster()(*args, fwd_type=fwd_type, **kwargs)
         if fwd_type == "density":
             return self.render_pts_density(*args, **kwargs)
         if fwd_type == "mesh":
@@ -118,6 +135,8 @@ class RayCaster:
         if color:
             raise NotImplementedError("color=True needs texture layers the NeRF model does not have")
         _check_subject_idxs(subject_idxs)
+        if self._staged is not None:
+            return self._staged.eval_caster().render_pts_density(pts, kps, skts, bones, network=network, v=v)
         if v is not None:
             raise NotImplementedError("precomputed kp inputs (v) are not supported")
         dev = torch.device(f"cuda:{self.model.device}")
@@ -138,6 +157,9 @@ class RayCaster:
         on the device; same grid and element order as the reference's meshgrid (`subject_idxs`: as
         in render_pts_density)."""
         _check_subject_idxs(subject_idxs)
+        if self._staged is not None:
+            return self._staged.eval_caster().render_mesh_density(kps, skts, bones, radius=radius, res=res, v=v,
+                                                                  network=network)
         if v is not None:
             raise NotImplementedError("precomputed kp inputs (v) are not supported")
         dev = torch.device(f"cuda:{self.model.device}")
@@ -166,6 +188,12 @@ class RayCaster:
         so any sub-range of a chunked ray list renders as in the whole list (ANERF_FLAG_NEAR_FAR)."""
         if perturb or raw_noise_std or ray_noise_std:
             raise NotImplementedError("stochastic sampling / noise (training mode) is not implemented")
+        if self._staged is not None:
+            if debug or count_mfma or near_far_given:
+                raise NotImplementedError("debug / count_mfma / near_far_given: fused-kernel options (staged encoder)")
+            return self._staged.eval_caster().render_rays(
+                ray_batch, N_samples, skts=skts, cyls=cyls, cams=cams, subject_idxs=subject_idxs, lindisp=lindisp,
+                N_importance=N_importance, preproc_kwargs=preproc_kwargs, chunk=chunk, ret_alpha=ret_alpha)
         if subject_idxs is not None:
             # the reference appends the indices to the view encoding (raycasters.py:545-548) and its
             # NeRF.forward then cannot split [pts | views | cam] (nerf.py:135-137): the same error

@@ -151,21 +151,23 @@ def _linear(rng, n_out, n_in):
     return w, b
 
 
-def nerf_input_dims(n_joints, multires=7, multires_views=4, multires_bones=0):
+def nerf_input_dims(n_joints, multires=7, multires_views=4, multires_bones=0, kp_dims=1, view_dims=3):
     """(input_ch, input_ch_bones, input_ch_views) as create_raycaster derives them
-    (core/raycasters.py:24-79, core/cutoff_embedder.py:15-40)."""
-    input_ch = n_joints * (1 + 2 * multires)
+    (core/raycasters.py:24-79, core/cutoff_embedder.py:15-40); kp_dims 3 for --kp_dist_type relpos,
+    view_dims 1 for --view_type rayangle."""
+    input_ch = n_joints * kp_dims * (1 + 2 * multires)
     input_ch_bones = 3 * n_joints * (1 + 2 * multires_bones)
-    input_ch_views = 3 * n_joints * (1 + 2 * multires_views)
+    input_ch_views = view_dims * n_joints * (1 + 2 * multires_views)
     return input_ch, input_ch_bones, input_ch_views
 
 
 def make_nerf_state(seed, n_joints=24, D=8, W=256, multires=7, multires_views=4,
                     skips=(4,), use_framecode=False, framecode_ch=16, n_framecodes=0,
-                    alpha_bias=2.0, alpha_gain=1.0, rgb_gain=1.0):
+                    alpha_bias=2.0, alpha_gain=1.0, rgb_gain=1.0, multires_bones=0, kp_dims=1, view_dims=3):
     """Seeded NeRF state dict with the key layout of core/networks/nerf.py:57-88."""
     rng = np.random.default_rng(seed)
-    input_ch, input_ch_bones, input_ch_views = nerf_input_dims(n_joints, multires, multires_views)
+    input_ch, input_ch_bones, input_ch_views = nerf_input_dims(n_joints, multires, multires_views, multires_bones,
+                                                               kp_dims, view_dims)
     dnet = input_ch + input_ch_bones
     sd = {}
     w, b = _linear(rng, W, dnet)
@@ -200,7 +202,7 @@ def make_embed_state(n_joints, cutoff=0.5, tau=20.0, jitter=0.0, seed=0):
 def make_checkpoint(seed, n_joints=24, D=8, W=256, fine=True, tau=20.0, tau_views=None,
                     cutoff_jitter=0.05, alpha_bias=0.5, alpha_gain=30.0, rgb_gain=8.0,
                     use_framecode=False, n_framecodes=0, multires=7, multires_views=4, sched_alpha=None,
-                    cutoff_bones=False, tau_bones=None):
+                    cutoff_bones=False, tau_bones=None, multires_bones=0, kp_dims=1, view_dims=3):
     """A full RayCaster checkpoint dict with the key layout of RayCaster.state_dict()
     (core/raycasters.py:752-766); sched_alpha: the --freq_schedule buffer of the cutoff embedders
     (core/cutoff_embedder.py:97-99), absent when None; cutoff_bones: the bone embedder is a
@@ -209,7 +211,8 @@ def make_checkpoint(seed, n_joints=24, D=8, W=256, fine=True, tau=20.0, tau_view
         "network_fn_state_dict": make_nerf_state(seed, n_joints, D, W, multires, multires_views,
                                                  use_framecode=use_framecode,
                                                  n_framecodes=n_framecodes, alpha_bias=alpha_bias,
-                                                 alpha_gain=alpha_gain, rgb_gain=rgb_gain),
+                                                 alpha_gain=alpha_gain, rgb_gain=rgb_gain, multires_bones=multires_bones,
+                                                 kp_dims=kp_dims, view_dims=view_dims),
         "embed_state_dict": make_embed_state(n_joints, tau=tau, jitter=cutoff_jitter, seed=seed + 101),
         "embedbones_state_dict": {},
         "embeddirs_state_dict": make_embed_state(n_joints, tau=tau if tau_views is None else tau_views,
@@ -225,7 +228,9 @@ def make_checkpoint(seed, n_joints=24, D=8, W=256, fine=True, tau=20.0, tau_view
         ck["network_fine_state_dict"] = make_nerf_state(seed + 1, n_joints, D, W, multires, multires_views,
                                                         use_framecode=use_framecode,
                                                         n_framecodes=n_framecodes, alpha_bias=alpha_bias,
-                                                        alpha_gain=alpha_gain, rgb_gain=rgb_gain)
+                                                        alpha_gain=alpha_gain, rgb_gain=rgb_gain,
+                                                        multires_bones=multires_bones, kp_dims=kp_dims,
+                                                        view_dims=view_dims)
     return ck
 
 

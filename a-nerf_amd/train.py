@@ -17,6 +17,7 @@ Random numbers: torch's generator on the device by default; pass `rand={"t_rand"
 ray_noise_std also "pts_noise0": (N,S,3), "pts_noise1": (N,I,3)) to reproduce a given draw — the
 parity tests feed the reference's.
 """
+import numpy as np
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -489,7 +490,9 @@ class TrainRayCaster(nn.Module):
         the current sched_alpha), on the device; None without a schedule."""
         if not self.cfg.freq_schedule:
             return None
-        a = (self.embed_fn.host("sched_alpha"), self.embeddirs_fn.host("sched_alpha"))
+        eb = self.embedbones_fn
+        a = (self.embed_fn.host("sched_alpha"), self.embeddirs_fn.host("sched_alpha"),
+             eb.host("sched_alpha") if eb is not None and eb.freq_schedule else None)
         if self._fs_cache is None or self._fs_cache[0] != a or self._fs_cache[1].device != self._dev:
             self._fs_cache = (a, torch.from_numpy(feature_scales(self.cfg, *a)).to(self._dev))
         return self._fs_cache[1]
@@ -530,7 +533,10 @@ class TrainRayCaster(nn.Module):
 
     def eval_caster(self):
         """The fused eval RayCaster over the current weights (repacked only after they changed; a new
-        tau / cutoff reaches it without a repack)."""
+        tau / cutoff reaches it without a repack); for a staged encoder (cfg.staged) the training stages
+        run deterministically instead (StagedCaster)."""
+        if self.cfg.staged:
+            return StagedCaster(self)
         from .raycaster import RayCaster
         v = self._version()
         if self._eval is None or v != self._eval_version:
@@ -667,6 +673,100 @@ class TrainRayCaster(nn.Module):
             out = {"rgb_map": rgb1, "disp_map": disp1, "acc_map": acc1, "alpha": a1,
                    "rgb0": rgb, "disp0": disp, "acc0": acc, "alpha0": a}
         return out
+
+
+class StagedCaster:
+    """Eval renders of a staged-encoder model (RenderConfig.staged: --multires_bones > 0, --kp_dist_type
+    relpos, --view_type rayangle; include/anerf.h) on the training stages: TrainRayCaster.render_rays with
+    perturb 0 and no noise -- the reference's eval path (core/raycasters.py:361-474, deterministic
+    sample_pdf) -- under no_grad, the MLP on the trainable networks' GEMMs (mlp.py; the default "mixed"
+    forward is the fp32-accurate bf16x6).  Density queries (fwd_type 'density' / 'mesh',
+    raycasters.py:579-648) encode the points the same way and read alpha_linear."""
+
+    def __init__(self, trainable):
+        self._t = trainable
+
+    @property
+    def model(self):
+        return self._t.model
+
+    @property
+    def cfg(self):
+        return self._t.cfg
+
+    def __call__(self, *args, fwd_type="", **kwargs):
+        if fwd_type == "density":
+            return self.render_pts_density(*args, **kwargs)
+        if fwd_type == "mesh":
+            return self.render_mesh_density(*args, **kwargs)
+        if fwd_type == "density_color":
+            raise AssertionError("need to have texture layer!")
+        return self.render_rays(*args, **kwargs)
+
+    @torch.no_grad()
+    def render_rays(self, ray_batch, N_samples, kp_batch=None, skts=None, cyls=None, bones=None, cams=None,
+                    subject_idxs=None, retraw=False, lindisp=False, perturb=0., N_importance=0, network_fine=None,
+                    raw_noise_std=0., ray_noise_std=0., verbose=False, ext_scale=0.001, pytest=False,
+                    preproc_kwargs=None, nerf_type="nerf", chunk=None, ret_alpha=True, **unused):
+        if perturb or raw_noise_std or ray_noise_std:
+            raise NotImplementedError("the eval caster renders deterministically; train() for stochastic renders")
+        out = self._t.render_rays(ray_batch, N_samples, kp_batch=kp_batch, skts=skts, cyls=cyls, bones=bones,
+                                  cams=cams, subject_idxs=subject_idxs, lindisp=lindisp, perturb=0.,
+                                  N_importance=N_importance, preproc_kwargs=preproc_kwargs, chunk=chunk)
+        out = {k: v.detach() for k, v in out.items()}
+        if not ret_alpha:
+            out.pop("alpha", None)
+            out.pop("alpha0", None)
+        return out
+
+    @torch.no_grad()
+    def render_pts_density(self, pts, kps, skts, bones, render_kwargs=None, subject_idxs=None, netchunk=1024 * 64,
+                           network=None, color=False, v=None):
+        """alpha_linear at points (raycasters.py:597-648): the points as zero-length rays through the
+        training encoder (the view part, which the density does not read, from a fixed direction)."""
+        if color:
+            raise NotImplementedError("color=True needs texture layers the NeRF model does not have")
+        if v is not None:
+            raise NotImplementedError("precomputed kp inputs (v) are not supported")
+        t = self._t
+        dev = t._dev
+        nj = self.cfg.n_joints
+        p = torch.as_tensor(pts).to(dev, torch.float32)
+        shape = p.shape[:-1]
+        p = p.reshape(-1, 3)
+        n = p.shape[0]
+        sk = torch.as_tensor(skts).to(dev, torch.float32).reshape(-1, nj, 4, 4)[:1].contiguous()
+        if network in (None, -1):
+            net = t.network_fine if t.network_fine is not None else t.network_fn
+        elif network in ("coarse", 0):
+            net = t.network_fn
+        elif network in ("fine", 1):
+            if t.network_fine is None:
+                raise ValueError("this model has no fine network")
+            net = t.network_fine
+        else:
+            raise ValueError(f"network must be None, 'coarse' or 'fine', got {network!r}")
+        rb = torch.zeros(n, 11, device=dev, dtype=torch.float32)
+        rb[:, :3] = p
+        rb[:, 5] = 1.0
+        z = torch.zeros(n, 1, device=dev, dtype=torch.float32)
+        feat = _Encode.apply(sk, t._constants(), rb, z, torch.zeros(n, device=dev, dtype=torch.int32), None)
+        fs = t._feature_scale()
+        if fs is not None:
+            feat = feat * fs
+        cams = torch.zeros(n, device=dev, dtype=torch.long) if self.cfg.opt_framecode else None
+        return net(feat, cams)[:, 3:4].reshape(*shape, 1)
+
+    @torch.no_grad()
+    def render_mesh_density(self, kps, skts, bones, subject_idxs=None, radius=1.0, res=64, render_kwargs=None,
+                            netchunk=1024 * 64, v=None, network=None):
+        """raycasters.py:579-595: np.meshgrid of linspace(-radius, radius, res + 1) around kps[0, 0]."""
+        t = np.linspace(-radius, radius, int(res) + 1)
+        grid = np.stack(np.meshgrid(t, t, t), axis=-1).astype(np.float32)
+        kp0 = torch.as_tensor(kps).to(torch.float32).reshape(-1, 3)[0].cpu()
+        pts = torch.from_numpy(grid.reshape(-1, 3)) + kp0
+        raw = self.render_pts_density(pts, kps, skts, bones, network=network, v=v)
+        return raw.reshape(*grid.shape[:-1])
 
 
 def _img_loss(name, x, y, reduction="mean", beta=0.1):

@@ -55,7 +55,7 @@
 extern "C" {
 #endif
 
-#define ANERF_ABI_VERSION 14
+#define ANERF_ABI_VERSION 15
 
 enum {
     ANERF_OK = 0,
@@ -129,7 +129,24 @@ typedef struct {
                                 importance weights are 0.5 (max(w_l,w_k) + max(w_k,w_u)) + 0.01
                                 (ray_utils.py:270-277); requires has_fine == 0 */
     int32_t encoder_flags;   /* ANERF_ENC_* (kp embedder options of the cutoff embedder; 0 = none) */
+    int32_t multires_bones;  /* --multires_bones (ABI 15): bone-direction frequencies, 0-10 (0: the bare
+                                directions, the default); > 0 is a staged encoder (below) */
 } anerf_model_desc;
+
+/* Staged encoders (ABI 15): --multires_bones > 0, ANERF_ENC_KP_RELPOS and ANERF_ENC_VIEW_ANGLE change the
+ * MLP's input layout beyond what the fused render kernel streams (its layer-0 parts and the per-ray view
+ * factor G assume one distance per joint, bare bone directions and per-ray view directions).  A model with
+ * any of them ("staged") is served by the training stages -- anerf_train_samples / _encode (+ _backward) /
+ * _composite (+ _backward) / _importance with the MLP on anerf_mlp_gemm -- which the Python RayCaster runs
+ * deterministically (perturb 0, no noise) for eval renders; anerf_render_rays, anerf_density_points /
+ * _grid and anerf_encode_points reject it (ANERF_EINVAL), and anerf_model_create takes no weights for it
+ * (the anerf_net_weights pointers may be NULL).  The feature row of a sample is
+ *   [kp part | bone part | view part], with
+ *   kp part   reldist: NJ (1 + 2 multires) columns, column f NJ + j (f = 0 the input, 2k + 1 / 2k + 2 the sin /
+ *             cos of frequency 2^k);  relpos: 3 NJ (1 + 2 multires), column 3 f NJ + 3 j + c;
+ *   bone part 3 NJ (1 + 2 multires_bones), column 3 f NJ + 3 j + c;
+ *   view part relray / world: 3 NJ (1 + 2 multires_views), column 3 f NJ + 3 j + c;
+ *             rayangle: NJ (1 + 2 multires_views), column f NJ + j. */
 
 /* anerf_model_desc.encoder_flags: the kp (distance) CutoffEmbedder's input transforms
  * (core/cutoff_embedder.py:125-134, only with use_cutoff): CUT_TO_DIST (--cut_to_dist) feeds
@@ -140,14 +157,25 @@ typedef struct {
 /* --cutoff_bones (core/raycasters.py:52-64): the bone embedder is a CutoffEmbedder (dist_inputs, its
  * own tau and cutoff_dist: anerf_embed_params tau_b / cutoff_dist_b); with --multires_bones 0 its
  * output is the bone direction times w_b = 1 - sigmoid(tau_b (dist - c_b)) when use_cutoff and
- * cutoff_inputs (core/cutoff_embedder.py:111-166), the bare direction otherwise.  The flag is ignored
- * (and tau_b / cutoff_dist_b unused) unless desc->use_cutoff and desc->cutoff_inputs are both set. */
+ * cutoff_inputs (core/cutoff_embedder.py:111-166), the bare direction otherwise.  With --multires_bones 0
+ * the flag is ignored (and tau_b / cutoff_dist_b unused) unless desc->use_cutoff and desc->cutoff_inputs are
+ * both set; with --multires_bones > 0 (staged) it needs use_cutoff only: the sin / cos features are windowed
+ * by w_b either way, the bare directions with cutoff_inputs. */
 #define ANERF_ENC_CUTOFF_BONES 4
 /* --view_type world (core/raycasters.py:279-280, ABI 14): the view input of joint j is R_j d itself
  * (IdentityExpandEncoder of transform_batch_rays, encoders.py:25-37, 71-79), not the normalised
  * R_j d / |R_j d| of the default relray (VecNormEncoder, encoders.py:172-193).  Rendering, and (round 5)
  * anerf_train_encode / _encode_backward (the identity's gradient in place of the normalisation's). */
 #define ANERF_ENC_VIEW_RAW 8
+/* --kp_dist_type relpos (core/encoders.py:124-142, raycasters.py:261-262; staged, ABI 15): the kp input of joint
+ * j is its local point q_j (3 values) instead of |q_j|; the kp CutoffEmbedder then has dist_inputs (the window
+ * of all three from the joint distance, no cut_to_dist / cutoff_shift transform, cutoff_embedder.py:115-121)
+ * and the reference's window distance |p - kp_j| is not a function of the poses (raycasters.py:530-533): its
+ * gradient to skts is 0, for every windowed embedder of such a model. */
+#define ANERF_ENC_KP_RELPOS 16
+/* --view_type rayangle (core/encoders.py:195-212, skeleton_utils.py:594-605; staged, ABI 15): the view input
+ * of joint j is one angle, acos(clamp(q_j . R_j d / (|q_j| |R_j d|), -1 + 1e-6, 1 - 1e-6)) - pi / 2. */
+#define ANERF_ENC_VIEW_ANGLE 32
 
 /* HOST pointers to one NeRF's weights, torch nn.Linear layout [out][in] (core/networks/nerf.py:57-88). */
 typedef struct {

@@ -35,6 +35,9 @@ NAMES = ["c1_64_s32_d4w128", "c2_256_s64_d8w256", "c3_512_s64i128_d8w256", "c4_5
          "mr5_mrv2_s32i16_d8w256", "mr9_mrv3_s32i16_d8w128", "mr3_mrv1_s32i16_d4w64",
          # --view_type world (un-normalised joint-frame ray directions into the view embedder)
          "vw1_viewworld_s32i16_d8w128"]
+# (round 5) staged encoders (include/anerf.h): rendered by train.StagedCaster on the training stages; GPU parity
+# in tests/test_gpu_staged.py
+STAGED = ["sg1_relpos_s32i16_d4w128", "sg2_rayangle_mrb2_cb_s32i16_d8w128", "sg3_all_fs_s32i16_d8w256"]
 FRAMES = ["c1_64_s32_d4w128", "pw_64_white_d4w128", "pb_64_bgimg_d4w128"]
 
 
@@ -50,8 +53,13 @@ class Golden:
         kw = {}
         if "--density_type" in flags:
             kw["density_type"] = flags[flags.index("--density_type") + 1]
-        if "--view_type" in flags:
-            kw["extra"] = {"view_type": flags[flags.index("--view_type") + 1]}
+        val = lambda k, d=None: flags[flags.index(k) + 1] if k in flags else d  # noqa: E731
+        extra = {k[2:]: val(k) for k in ("--view_type", "--kp_dist_type") if k in flags}
+        if extra:
+            kw["extra"] = extra
+        # (round 5) the staged encoders' input shapes (tests/golden/make_golden.py staged_dims)
+        dims = dict(multires_bones=int(val("--multires_bones", 0)), kp_dims=3 if val("--kp_dist_type") == "relpos" else 1,
+                    view_dims=1 if val("--view_type") == "rayangle" else 3)
         if "--softplus_shift" in flags:
             kw["softplus_shift"] = float(flags[flags.index("--softplus_shift") + 1])
         self.cfg = config.RenderConfig(n_joints=m["NJ"], netdepth=m["D"], netwidth=m["W"], N_samples=m["S"],
@@ -67,11 +75,11 @@ class Golden:
                                        cutoff_bones="--cutoff_bones" in flags,
                                        init_freq=float(flags[flags.index("--init_freq") + 1])
                                        if "--init_freq" in flags else 0.0,
-                                       precision="fp32", **kw).validate()
+                                       multires_bones=dims["multires_bones"], precision="fp32", **kw).validate()
         self.ckpt = syn.make_checkpoint(m["seed"], n_joints=m["NJ"], D=m["D"], W=m["W"], fine=m["I"] > 0,
                                         tau=m["tau"], use_framecode=fc, n_framecodes=5, multires=m.get("mr", 7),
                                         multires_views=m.get("mrv", 4), sched_alpha=m.get("sched"),
-                                        cutoff_bones=bool(m.get("cb", False)), tau_bones=m.get("tau_b"))
+                                        cutoff_bones=bool(m.get("cb", False)), tau_bones=m.get("tau_b"), **dims)
         assert syn.checkpoint_sha256(self.ckpt) == m["sha256"], "synthetic weights drifted from the fixture"
 
     def __getitem__(self, k):

@@ -133,6 +133,23 @@ CONFIGS = {
     # times w_b, core/raycasters.py:52-64, cutoff_embedder.py:108-166); D = 8 for the skip layer's x part
     "cb1_cutoffbones_s32i16_d8w128": dict(H=128, NJ=24, S=32, I=16, D=8, W=128, tau=20.0, kind="rays", n_rays=128,
                                           seed=28, flags=["--cutoff_bones"], cb=True, tau_b=35.0),
+    # (round 5) staged encoders (include/anerf.h, rendered on the training stages): --kp_dist_type relpos;
+    # --view_type rayangle with --multires_bones 2 and --cutoff_bones; all three at 8 x 256 (the skip layer's
+    # [x | h]) with --multires_bones 3 and --freq_schedule
+    "sgd1_relpos_mrb2_density": dict(H=64, NJ=24, S=32, I=16, D=8, W=128, tau=20.0, kind="density", seed=54, res=10,
+                                     radius=1.0, n_pts=300, cb=True, tau_b=35.0,
+                                     flags=["--kp_dist_type", "relpos", "--multires_bones", "2", "--cutoff_bones"]),
+    "sg1_relpos_s32i16_d4w128": dict(H=128, NJ=24, S=32, I=16, D=4, W=128, tau=20.0, kind="rays", n_rays=128,
+                                     seed=51, flags=["--kp_dist_type", "relpos"]),
+    "sg2_rayangle_mrb2_cb_s32i16_d8w128": dict(H=128, NJ=24, S=32, I=16, D=8, W=128, tau=20.0, kind="rays",
+                                               n_rays=128, seed=52, cb=True, tau_b=35.0,
+                                               flags=["--view_type", "rayangle", "--multires_bones", "2",
+                                                      "--cutoff_bones"]),
+    "sg3_all_fs_s32i16_d8w256": dict(H=128, NJ=24, S=32, I=16, D=8, W=256, tau=20.0, kind="rays", n_rays=96,
+                                     seed=53, sched=2.3, cb=True, tau_b=35.0,
+                                     flags=["--kp_dist_type", "relpos", "--view_type", "rayangle",
+                                            "--multires_bones", "3", "--cutoff_bones", "--freq_schedule",
+                                            "--init_freq", "2.3"]),
     # the shipped configs' render shape (configs/{mixamo,h36m,perfcap}/*.txt: 8x256, multires 7 / 4,
     # N_samples 64, N_importance 16, opt_framecode; configs/surreal/surreal.txt the same without
     # framecodes): the view layer's framecode column at W = 256 and the 64 + 16 importance pass
@@ -157,6 +174,15 @@ CONFIGS = {
     "pb_64_bgimg_d4w128": dict(H=64, NJ=24, S=32, I=16, D=4, W=128, tau=20.0, kind="frame", seed=44, n_frames=2,
                                bg_imgs=(3, 48, 40), bg_indices=[2, 0]),
 }
+
+
+def staged_dims(flags):
+    """make_checkpoint's input-shape arguments for the staged encoders' flags (--multires_bones,
+    --kp_dist_type relpos, --view_type rayangle)."""
+    def val(k, d):
+        return flags[flags.index(k) + 1] if k in flags else d
+    return dict(multires_bones=int(val("--multires_bones", 0)), kp_dims=3 if val("--kp_dist_type", "") == "relpos" else 1,
+                view_dims=1 if val("--view_type", "") == "rayangle" else 3)
 
 
 def build_reference(mods, cfg, tmp):
@@ -189,7 +215,8 @@ def build_reference(mods, cfg, tmp):
     ck = anerf_syn.make_checkpoint(cfg["seed"], n_joints=NJ, D=cfg["D"], W=cfg["W"], fine=cfg["I"] > 0,
                                    tau=cfg["tau"], use_framecode=use_fc, n_framecodes=5, multires=cfg.get("mr", 7),
                                    multires_views=cfg.get("mrv", 4), sched_alpha=cfg.get("sched"),
-                                   cutoff_bones=cfg.get("cb", False), tau_bones=cfg.get("tau_b"))
+                                   cutoff_bones=cfg.get("cb", False), tau_bones=cfg.get("tau_b"),
+                                   **staged_dims(cfg.get("flags", [])))
     ck_t = {k: {n: torch.from_numpy(np.array(v)) for n, v in d.items()} for k, d in ck.items()}
     rc = render_kwargs["ray_caster"]
     rc.load_state_dict(ck_t, strict=True)
@@ -301,7 +328,8 @@ def make_density(name, cfg, mods, tmp):
                   fwd_type="density")
     meta = dict(seed=cfg["seed"], sha256=anerf_syn.checkpoint_sha256(ck), NJ=cfg["NJ"], S=cfg["S"], I=cfg["I"],
                 D=cfg["D"], W=cfg["W"], tau=cfg["tau"], H=sc["H"], focal=sc["focal"], ext_scale=0.001, chunk=4096,
-                framecode=0, res=cfg["res"], radius=cfg["radius"])
+                framecode=0, res=cfg["res"], radius=cfg["radius"], flags=cfg.get("flags", []),
+                cb=bool(cfg.get("cb", False)), tau_b=cfg.get("tau_b"))
     data = {"kps": sc["kps"][0:1], "skts": sc["skts"][0:1], "bones": sc["bones"][0:1], "pts": pts,
             "grid_density": grid.numpy(), "pts_density": dens.numpy()}
     path = os.path.join(HERE, name + ".npz")

@@ -62,6 +62,12 @@ CONFIGS = {
     # --view_type world (un-normalised joint-frame ray directions: the identity's gradient to the poses)
     "t11_mr5_mrv2_world": dict(H=128, NJ=24, S=32, I=16, D=4, W=128, tau=20.0, kind="rays", seed=45, n_rays=64,
                                n_poses=2, mr=5, mrv=2, flags=["--view_type", "world"]),
+    # (round 5) the staged encoders (include/anerf.h): relpos kp inputs, ray angles, bone frequencies windowed
+    # by --cutoff_bones; D = 8 (the skip layer's [x | h])
+    "t12_staged_relpos_rayangle_mrb2": dict(H=128, NJ=24, S=32, I=16, D=8, W=128, tau=20.0, kind="rays", seed=46,
+                                            n_rays=64, n_poses=2, cb=True, tau_b=35.0,
+                                            flags=["--kp_dist_type", "relpos", "--view_type", "rayangle",
+                                                   "--multires_bones", "2", "--cutoff_bones"]),
 }
 FULL_LIMIT = 20000   # parameters with more entries are sampled
 SAMPLE = 4096

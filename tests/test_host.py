@@ -1,4 +1,5 @@
 """CPU: host-side logic of the drop-in (integer pixel sets, configuration, synthetic inputs)."""
+import dataclasses
 import importlib
 import os
 import types
@@ -41,14 +42,16 @@ def test_config_rejects_unsupported_flags():
     cfg = config.RenderConfig
     with pytest.raises(NotImplementedError):
         cfg(use_viewdirs=False).validate()
-    with pytest.raises(NotImplementedError):
-        cfg(multires_bones=2).validate()
-    with pytest.raises(NotImplementedError):  # (--cutoff_bones is implemented, with multires_bones 0)
-        cfg(multires_bones=2, cutoff_bones=True).validate()
+    with pytest.raises(NotImplementedError):  # (bone frequencies 1-10: staged encoders, round 5)
+        cfg(multires_bones=11).validate()
+    assert cfg(multires_bones=2, cutoff_bones=True).validate().staged
     assert cfg(cutoff_bones=True).validate().bone_window
     assert not cfg(cutoff_bones=True, use_cutoff=False).validate().bone_window
     with pytest.raises(NotImplementedError):
-        cfg(extra={"kp_dist_type": "relpos"}).validate()
+        cfg(extra={"kp_dist_type": "querypts"}).validate()
+    assert cfg(extra={"kp_dist_type": "relpos"}).validate().staged
+    assert cfg(extra={"view_type": "rayangle"}).validate().staged
+    assert not cfg(extra={"view_type": "world"}).validate().staged
     with pytest.raises(NotImplementedError):
         cfg(density_type="exp").validate()
     cfg().validate()
@@ -111,7 +114,8 @@ def test_encoder_selectors_follow_the_reference():
     """The non-default encoder selectors (core/raycasters.py:251-305) as the reference behaves on them
     (reference_flags.json, recorded by tests/golden/probe_reference_flags.py): kp_dist_type 'cat' and
     bone_type 'axisang' raise TypeError there and here; view_type 'world' runs there and renders here
-    (fixture vw1_viewworld_s32i16_d8w128); relpos / querypts / rayangle run there and stay refused."""
+    (fixture vw1_viewworld_s32i16_d8w128); relpos and rayangle run there and render here on the training
+    stages (staged encoders, fixtures sg*); querypts runs there and stays refused."""
     import json
     with open(os.path.join(os.path.dirname(__file__), "golden", "reference_flags.json")) as f:
         rec = json.load(f)
@@ -122,10 +126,12 @@ def test_encoder_selectors_follow_the_reference():
             cfg(extra={key: val}).validate()
     assert rec["view_type=world"]["raises"] is None
     assert cfg(extra={"view_type": "world"}).validate().extra["view_type"] == "world"
-    for key, val in (("kp_dist_type", "relpos"), ("kp_dist_type", "querypts"), ("view_type", "rayangle")):
+    for key, val in (("kp_dist_type", "relpos"), ("view_type", "rayangle")):
         assert rec[f"{key}={val}"]["raises"] is None
-        with pytest.raises(NotImplementedError):
-            cfg(extra={key: val}).validate()
+        assert cfg(extra={key: val}).validate().staged
+    assert rec["kp_dist_type=querypts"]["raises"] is None
+    with pytest.raises(NotImplementedError):
+        cfg(extra={"kp_dist_type": "querypts"}).validate()
 
 
 def test_config_lindisp_from_args():
@@ -249,8 +255,8 @@ def test_normalize_cutoff_is_a_noop_like_the_reference():
     cfg = config.RenderConfig.from_args(args, 24)
     assert cfg.normalize_cutoff and cfg.cut_to_dist and cfg.cutoff_shift
     assert config.RenderConfig.from_args(types.SimpleNamespace(cutoff_bones=True), 24).cutoff_bones
-    with pytest.raises(NotImplementedError):  # (bone frequencies stay refused)
-        config.RenderConfig.from_args(types.SimpleNamespace(cutoff_bones=True, multires_bones=4), 24)
+    # (bone frequencies: a staged encoder since round 5, include/anerf.h)
+    assert config.RenderConfig.from_args(types.SimpleNamespace(cutoff_bones=True, multires_bones=4), 24).staged
 
 
 def test_forward_dispatch_matches_the_reference():
@@ -259,6 +265,7 @@ def test_forward_dispatch_matches_the_reference():
     has no texture_linears), anything else renders rays."""
     rc_mod = importlib.import_module("a-nerf_amd.raycaster")
     rc = object.__new__(rc_mod.RayCaster)  # (dispatch only: no device model)
+    rc._staged = None
     rc.render_pts_density = lambda *a, **k: "density"
     rc.render_mesh_density = lambda *a, **k: "mesh"
     rc.render_rays = lambda *a, **k: "rays"
@@ -266,3 +273,49 @@ def test_forward_dispatch_matches_the_reference():
     assert rc() == "rays" and rc(fwd_type="something") == "rays"
     with pytest.raises(AssertionError, match="texture layer"):
         rc(fwd_type="density_color")
+
+
+def test_staged_encoder_configs_match_reference_checkpoints():
+    """Round 5: --multires_bones > 0, --kp_dist_type relpos and --view_type rayangle build (staged encoders,
+    include/anerf.h) with the reference's input widths: the fixtures' checkpoints, made by the reference's
+    create_raycaster with those flags (tests/golden/make_golden.py), have exactly these layer shapes."""
+    from _golden import STAGED, Golden
+    for name in STAGED + ["sgd1_relpos_mrb2_density"]:
+        g = Golden(name)
+        cfg = g.cfg
+        assert cfg.staged
+        sd = g.ckpt["network_fn_state_dict"]
+        dnet = cfg.input_ch + cfg.input_ch_bones
+        assert sd["pts_linears.0.weight"].shape == (cfg.netwidth, dnet), name
+        assert sd["views_linears.0.weight"].shape[1] == cfg.netwidth + cfg.input_ch_views + cfg.framecode_ch, name
+        if cfg.netdepth > 5:
+            assert sd[f"pts_linears.{cfg.skips[0] + 1}.weight"].shape == (cfg.netwidth, cfg.netwidth + dnet), name
+    g = Golden("sg3_all_fs_s32i16_d8w256")
+    assert (g.cfg.kp_relpos, g.cfg.view_angle, g.cfg.multires_bones) == (True, True, 3)
+    with pytest.raises(NotImplementedError):
+        dataclasses.replace(g.cfg, multires_bones=11).validate()
+    with pytest.raises(NotImplementedError):  # (the reference's other kp type stays refused)
+        dataclasses.replace(g.cfg, extra={"kp_dist_type": "querypts"}).validate()
+
+
+def test_feature_scales_follow_the_staged_layout():
+    """--freq_schedule weights per frequency block of each part: relpos 3 NJ columns per slot, windowed bone
+    frequencies 3 NJ (their own sched_alpha), ray angles NJ."""
+    from _golden import Golden
+    cfg = Golden("sg3_all_fs_s32i16_d8w256").cfg
+    nj = cfg.n_joints
+    s = config.feature_scales(cfg, 2.3, 1.6, 0.4)
+    assert s.shape == (cfg.feature_dim,)
+    wp, wv, wb = (config.schedule_weights(a, n) for a, n in ((2.3, cfg.multires), (1.6, cfg.multires_views),
+                                                              (0.4, cfg.multires_bones)))
+    assert np.all(s[:3 * nj] == 1.0)
+    for k in range(cfg.multires):
+        assert np.all(s[(1 + 2 * k) * 3 * nj:(3 + 2 * k) * 3 * nj] == wp[k])
+    ob = cfg.input_ch
+    assert np.all(s[ob:ob + 3 * nj] == 1.0)
+    for k in range(cfg.multires_bones):
+        assert np.all(s[ob + (1 + 2 * k) * 3 * nj:ob + (3 + 2 * k) * 3 * nj] == wb[k])
+    ov = cfg.input_ch + cfg.input_ch_bones
+    assert np.all(s[ov:ov + nj] == 1.0)
+    for k in range(cfg.multires_views):
+        assert np.all(s[ov + (1 + 2 * k) * nj:ov + (3 + 2 * k) * nj] == wv[k])
