@@ -307,17 +307,32 @@ def parity_leg(a, cfg, ck, sc, cyls, idx, c2w_np, H, W, out, n, dev, want_cpu):
     rb_h = oracle.gen_rays(c2w_np, H, W, sc["focal"], idx)
     near_f, far_f, _, _ = om.near_far(rb_h, cyls[0:1], chunk=4096)  # the whole frame's chunk NaN fill
     sel = np.linspace(0, n - 1, min(a.cpu_rays, n)).astype(np.int64)
-    t1 = time.perf_counter()
-    ref = om.render_rays(rb_h[sel], sc["skts"][0], cyls[0:1], chunk=4096, nthreads=cores, near=near_f[sel],
-                         far=far_f[sel])
-    dt = time.perf_counter() - t1
+    # (timed as two interleaved halves: the line reports both rates and their spread)
+    halves = [np.arange(0, len(sel), 2), np.arange(1, len(sel), 2)]
+    parts, dts = [], []
+    for h in halves:
+        t1 = time.perf_counter()
+        parts.append(om.render_rays(rb_h[sel[h]], sc["skts"][0], cyls[0:1], chunk=4096, nthreads=cores,
+                                    near=near_f[sel[h]], far=far_f[sel[h]]))
+        dts.append(time.perf_counter() - t1)
+    ref = {}
+    for k in ("rgb_map", "disp_map", "acc_map"):
+        v = np.empty((len(sel),) + parts[0][k].shape[1:], parts[0][k].dtype)
+        for h, pr in zip(halves, parts):
+            v[h] = pr[k]
+        ref[k] = v
+    dt = sum(dts)
     cpu = None
     if want_cpu:
+        rates = [len(h) / t for h, t in zip(halves, dts)]
         cpu = {"value": round(len(sel) / dt, 2), "unit": "rays/s", "cores": cores, "kind": "port",
                "cpu_model": cpu_model(), "cpus_in_affinity_mask": cores,
+               "samples_rays_per_s": [round(r, 2) for r in rates],
+               "spread": round((max(rates) - min(rates)) / (len(sel) / dt), 4),
                "sample": f"{len(sel)} rays evenly spaced over the frame's {n} bbox rays, C oracle "
                          f"(oracle/anerf_oracle.c, OpenMP, {cores} threads = every CPU of the process's affinity "
-                         f"mask), {dt:.1f} s wall"}
+                         f"mask), {dt:.1f} s wall, timed as two interleaved halves (samples_rays_per_s; the rate "
+                         f"moves ~30 % between boxes of the same model, profiles r04k vs BENCH_r04)"}
     sel_d = torch.from_numpy(sel).to(dev)
     diff = {k: np.abs(out[k].index_select(0, sel_d).cpu().numpy().astype(np.float64) - ref[k].astype(np.float64))
             for k in ("rgb_map", "disp_map", "acc_map")}
