@@ -60,13 +60,16 @@ DTYPE = {
               "W = W0+W1+W2, the six bf16 MFMA products with i + j <= 2 (each dropped term below 2^-23 of |x W|), fp32 "
               "accumulate; encoder, windowed layer-0 part, heads, compositing fp32",
     "fp16x3": "22-bit operands: split fp16 after exact power-of-two scaling (x = x0+x1 within 2^-23 |x|, W = W0+W1), "
-              "three fp16 MFMA products (x1 W1, ~2^-22 of |x W|, dropped), fp32 accumulate; bone-direction parts and "
-              "the windowed layer-0 / skip-layer parts bf16x6 at widths 128/256 (fp32 at 64); encoder, heads, "
+              "three fp16 MFMA products (x1 W1, ~2^-22 of |x W|, dropped), fp32 accumulate; the bone-direction and "
+              "windowed layer-0 / skip-layer parts the same way in fixed power-of-two units of their bounded features "
+              "at widths 128/256 when the windows bound them (bf16x6 otherwise, fp32 at 64); encoder, heads, "
               "compositing fp32",
     "fp16x4": "fp32-accurate split fp16: hidden and view layers after exact power-of-two scaling, x = x0+x1 and "
               "W = W0+W1 (remainders within 2^-23 of |x|, |W|), the four fp16 MFMA products x_i W_j (dropped: the "
-              "remainders' ~2^-22 of |x W|, the bound of bf16x6's dropped terms), fp32 accumulate; bone-direction and "
-              "windowed layer-0 / skip-layer parts bf16x6 at widths 128/256; encoder, heads, compositing fp32",
+              "remainders' ~2^-22 of |x W|, the bound of bf16x6's dropped terms), fp32 accumulate; the bone-direction "
+              "and windowed layer-0 / skip-layer parts the same way in fixed power-of-two units of their bounded "
+              "features at widths 128/256 (round 5; bf16x6 when the windows do not bound them); encoder, heads, "
+              "compositing fp32",
     "bf16x3": "16-bit operands: split bf16 (x = hi+lo, W = hi+lo, three bf16 MFMA products), fp32 accumulate; "
               "fp32 elsewhere",
 }
