@@ -136,7 +136,9 @@ __device__ __forceinline__ void render_item(const ModelDev& M, const RenderArgs&
         STAMP(st, 6);
         // ---- composite (+ importance sampling after the coarse pass); one wave per ray
         for (int r0 = 0; r0 < R; r0 += 4) {
-            const int r = r0 + wave;
+            // (the wave index as a scalar here: the ray index and the output pointers become wave-uniform SGPR
+            // values instead of 64-bit per-lane pointers the allocator kept live, spilled, across the MLP)
+            const int r = r0 + __builtin_amdgcn_readfirstlane(wave);
             const bool active = r < nr;
             const int64_t i = ray0 + r;
             const float* ray = lds + P.ray + 16 * min(r, R - 1);
