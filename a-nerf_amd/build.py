@@ -45,6 +45,8 @@ def build(force=False, verbose=True):
         return OUT
     digest = source_hash()
     tmp = OUT + ".tmp"
+    if os.path.exists(tmp):
+        os.remove(tmp)
     cmd = [HIPCC] + FLAGS + ["-o", tmp] + SRC
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
@@ -53,7 +55,8 @@ def build(force=False, verbose=True):
     # the device passes different struct layouts (a torn library).  Keep only a build whose sources did not
     # move, and replace the library in one rename (a copy of the tree never sees a half-written file).
     if source_hash() != digest:
-        os.remove(tmp)
+        if os.path.exists(tmp):
+            os.remove(tmp)
         raise RuntimeError("sources changed during the build: the library was discarded, build again")
     os.replace(tmp, OUT)
     with open(STAMP, "w") as f:

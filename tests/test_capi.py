@@ -8,7 +8,10 @@ import importlib
 import os
 import re
 
+import pytest
+
 HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
 HEADER = os.path.join(os.path.dirname(HERE), "include", "anerf.h")
 _lib = importlib.import_module("a-nerf_amd._lib")
 
@@ -72,3 +75,29 @@ def test_library_reads_no_experiment_switches_from_the_environment():
         blob = f.read()
     for name in (b"ANERF_H3_TARGET", b"ANERF_UX6", b"ANERF_FUSED_PASSES"):
         assert name not in blob, name
+
+
+def test_build_discards_a_library_whose_sources_moved(tmp_path, monkeypatch):
+    """build.py keeps only a build whose sources did not change while hipcc ran (a header edited between
+    the offload passes gives host and device different struct layouts) and renames it into place whole."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("anerf_build", os.path.join(REPO, "a-nerf_amd", "build.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    out = str(tmp_path / "libx.so")
+    monkeypatch.setattr(b, "OUT", out)
+    monkeypatch.setattr(b, "STAMP", out + ".stamp")
+    cc = tmp_path / "cc.sh"  # (a stand-in compiler: creates the file after -o)
+    cc.write_text('#!/bin/sh\nwhile [ $# -gt 0 ]; do [ "$1" = -o ] && touch "$2"; shift; done\n')
+    cc.chmod(0o755)
+    monkeypatch.setattr(b, "HIPCC", str(cc))
+    monkeypatch.setattr(b, "FLAGS", [])
+    monkeypatch.setattr(b, "SRC", [])
+    hashes = iter(["a", "b"])
+    monkeypatch.setattr(b, "source_hash", lambda: next(hashes))
+    with pytest.raises(RuntimeError, match="sources changed"):
+        b.build(force=True, verbose=False)
+    assert not os.path.exists(out) and not os.path.exists(out + ".tmp")
+    monkeypatch.setattr(b, "source_hash", lambda: "c")
+    assert b.build(force=True, verbose=False) == out and os.path.exists(out)
+    assert open(out + ".stamp").read().strip() == "c"
