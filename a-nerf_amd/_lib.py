@@ -33,6 +33,7 @@ PRECISIONS = {"fp32": ANERF_PREC_FP32, "bf16x3": ANERF_PREC_BF16X3, "bf16x6": AN
 ANERF_ENC_CUT_TO_DIST, ANERF_ENC_CUTOFF_SHIFT, ANERF_ENC_CUTOFF_BONES = 1, 2, 4  # anerf_model_desc.encoder_flags
 ANERF_ENC_VIEW_RAW = 8  # --view_type world
 ANERF_ENC_KP_RELPOS, ANERF_ENC_VIEW_ANGLE = 16, 32  # --kp_dist_type relpos, --view_type rayangle (staged, ABI 15)
+ANERF_ENC_KP_QUERYPTS = 64  # --kp_dist_type querypts (staged, ABI 15)
 ABI_VERSION = 15  # include/anerf.h ANERF_ABI_VERSION: the structs below
 
 

@@ -97,7 +97,12 @@ class RenderConfig:
         if self.extra.get("bone_type") == "axisang":
             raise TypeError("--bone_type axisang: IdentityExpandEncoder.forward() missing 1 required positional "
                             "argument: 'refs' (core/raycasters.py:521)")
-        for k, allowed in (("kp_dist_type", ("reldist", "relpos")), ("bone_type", ("reldir",)),
+        if self.kp_query and self.bone_window:
+            # (the reference's bone CutoffEmbedder gets querypts' cutoff_dim 3 for its 3 NJ inputs and fails in
+            # _embed's window broadcast, core/cutoff_embedder.py:139-141)
+            raise NotImplementedError("--kp_dist_type querypts with --cutoff_bones fails in the reference's bone "
+                                      "embedder (cutoff_dim 3 for 3 NJ inputs)")
+        for k, allowed in (("kp_dist_type", ("reldist", "relpos", "querypts")), ("bone_type", ("reldir",)),
                            ("view_type", ("relray", "world", "rayangle")), ("pts_tr_type", ("local",))):
             v = self.extra.get(k, allowed[0])
             if v not in allowed:
@@ -115,6 +120,11 @@ class RenderConfig:
         return self.extra.get("kp_dist_type", "reldist") == "relpos"
 
     @property
+    def kp_query(self):
+        """--kp_dist_type querypts (core/raycasters.py:263-265): the world point itself, 3 values."""
+        return self.extra.get("kp_dist_type", "reldist") == "querypts"
+
+    @property
     def view_angle(self):
         """--view_type rayangle (core/encoders.py:195-212): one ray angle per joint."""
         return self.extra.get("view_type", "relray") == "rayangle"
@@ -123,7 +133,7 @@ class RenderConfig:
     def staged(self):
         """An encoder the fused render kernel does not stream (bone frequencies, relpos, ray angles,
         include/anerf.h "staged encoders"): the training stages render it (train.TrainRayCaster)."""
-        return self.multires_bones > 0 or self.kp_relpos or self.view_angle
+        return self.multires_bones > 0 or self.kp_relpos or self.kp_query or self.view_angle
 
     @property
     def framecode_ch(self):
@@ -131,6 +141,8 @@ class RenderConfig:
 
     @property
     def input_ch(self):
+        if self.kp_query:
+            return 3 * (1 + 2 * self.multires)
         return self.n_joints * (3 if self.kp_relpos else 1) * (1 + 2 * self.multires)
 
     @property
@@ -184,7 +196,7 @@ def feature_scales(cfg, alpha_pts, alpha_views, alpha_bones=None):
     """Per-column factor of the MLP input [x (input_ch) | bones | views] under --freq_schedule: the
     schedule weight of the column's frequency for the windowed sin/cos features of the cutoff
     embedders (a part's frequency slot f = 1 + 2k / 2 + 2k, the sin / cos of frequency k, is the column
-    block [f B, (f + 1) B) of the part, B its columns per slot: pts NJ (relpos 3 NJ), bones 3 NJ (a
+    block [f B, (f + 1) B) of the part, B its columns per slot: pts NJ (relpos 3 NJ, querypts 3), bones 3 NJ (a
     CutoffEmbedder with --cutoff_bones, `alpha_bones`), views 3 NJ (rayangle NJ)), 1 elsewhere; None
     without a schedule."""
     import numpy as np
@@ -201,7 +213,7 @@ def feature_scales(cfg, alpha_pts, alpha_views, alpha_bones=None):
                 s[o + f * b:o + (f + 1) * b] = w[k]
 
     if cfg.use_cutoff:  # (the pts embedder is a CutoffEmbedder only then)
-        part(0, nj * (3 if cfg.kp_relpos else 1), cfg.multires, alpha_pts)
+        part(0, 3 if cfg.kp_query else nj * (3 if cfg.kp_relpos else 1), cfg.multires, alpha_pts)
     if cfg.bone_window and cfg.multires_bones > 0:
         if alpha_bones is None:
             raise ValueError("freq_schedule with a windowed bone embedder: its sched_alpha is needed")

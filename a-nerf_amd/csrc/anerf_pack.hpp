@@ -545,8 +545,15 @@ static int validate_desc(const anerf_model_desc* d) {
     if (d->density_scale == 0.0f) return fail(ANERF_EINVAL, "density_scale must be non-zero");
     if (d->multires_bones < 0 || d->multires_bones > 10) return fail(ANERF_EINVAL, "multires_bones outside [0, 10]");
     if (d->encoder_flags & ~(ANERF_ENC_CUT_TO_DIST | ANERF_ENC_CUTOFF_SHIFT | ANERF_ENC_CUTOFF_BONES | ANERF_ENC_VIEW_RAW |
-                             ANERF_ENC_KP_RELPOS | ANERF_ENC_VIEW_ANGLE))
+                             ANERF_ENC_KP_RELPOS | ANERF_ENC_VIEW_ANGLE | ANERF_ENC_KP_QUERYPTS))
         return fail(ANERF_EINVAL, "unknown encoder_flags bits");
+    if ((d->encoder_flags & ANERF_ENC_KP_RELPOS) && (d->encoder_flags & ANERF_ENC_KP_QUERYPTS))
+        return fail(ANERF_EINVAL, "ANERF_ENC_KP_RELPOS and ANERF_ENC_KP_QUERYPTS are two kp types");
+    if ((d->encoder_flags & ANERF_ENC_KP_QUERYPTS) && (d->encoder_flags & ANERF_ENC_CUTOFF_BONES) && d->use_cutoff)
+        return fail(ANERF_EINVAL, "ANERF_ENC_KP_QUERYPTS with ANERF_ENC_CUTOFF_BONES: the reference's bone embedder "
+                                  "fails on it (cutoff_dim 3 for 3 NJ inputs)");
+    if ((d->encoder_flags & ANERF_ENC_KP_QUERYPTS) && d->n_joints < 3)
+        return fail(ANERF_EINVAL, "ANERF_ENC_KP_QUERYPTS needs n_joints >= 3");
     if ((d->encoder_flags & ANERF_ENC_VIEW_RAW) && (d->encoder_flags & ANERF_ENC_VIEW_ANGLE))
         return fail(ANERF_EINVAL, "ANERF_ENC_VIEW_RAW and ANERF_ENC_VIEW_ANGLE are two view types");
     return ANERF_OK;
@@ -554,7 +561,7 @@ static int validate_desc(const anerf_model_desc* d) {
 
 // A staged encoder (anerf.h, ABI 15): the training stages serve the model, the fused kernels do not.
 static bool desc_staged(const anerf_model_desc* d) {
-    return d->multires_bones > 0 || (d->encoder_flags & (ANERF_ENC_KP_RELPOS | ANERF_ENC_VIEW_ANGLE));
+    return d->multires_bones > 0 || (d->encoder_flags & (ANERF_ENC_KP_RELPOS | ANERF_ENC_VIEW_ANGLE | ANERF_ENC_KP_QUERYPTS));
 }
 
 static int pack_net(const anerf_model_desc* d, int njh2, const anerf_net_weights* w, Packer& pk,

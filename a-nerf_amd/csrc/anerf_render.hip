@@ -155,7 +155,11 @@ int anerf_model_create(const anerf_model_desc* desc, const anerf_net_weights* co
             if (rc) return rc;
         }
     }
-    const size_t off_cut = pk.add(std::vector<float>(embed->cutoff_dist, embed->cutoff_dist + nj));
+    // (querypts: the kp embedder's cutoff_dim is 3, its cutoff_dist 3 values; padded to NJ)
+    const int nkc = (desc->encoder_flags & ANERF_ENC_KP_QUERYPTS) ? 3 : nj;
+    std::vector<float> kc(embed->cutoff_dist, embed->cutoff_dist + nkc);
+    kc.resize(nj, 0.0f);
+    const size_t off_cut = pk.add(kc);
     const size_t off_cutv = pk.add(std::vector<float>(embed->cutoff_dist_v, embed->cutoff_dist_v + nj));
     const size_t off_cutb = pk.add(bone_tab ? std::vector<float>(embed->cutoff_dist_b, embed->cutoff_dist_b + nj)
                                             : std::vector<float>(nj, 0.0f));
@@ -208,6 +212,7 @@ int anerf_model_create(const anerf_model_desc* desc, const anerf_net_weights* co
     md.mrb = desc->multires_bones;
     md.kp_relpos = (desc->encoder_flags & ANERF_ENC_KP_RELPOS) ? 1 : 0;
     md.view_angle = (desc->encoder_flags & ANERF_ENC_VIEW_ANGLE) ? 1 : 0;
+    md.kp_query = (desc->encoder_flags & ANERF_ENC_KP_QUERYPTS) ? 1 : 0;
     md.bone_win = bone_win ? 1 : 0;
     md.staged = staged ? 1 : 0;
     md.tau = embed->tau;
@@ -221,7 +226,7 @@ int anerf_model_create(const anerf_model_desc* desc, const anerf_net_weights* co
         if (desc->has_fine) bind_net(desc, dbuf, of, fine->alpha_b[0], md.net[1]);
         else md.net[1] = md.net[0];
     }
-    m->cut_host.assign(embed->cutoff_dist, embed->cutoff_dist + nj);
+    m->cut_host.assign(kc.begin(), kc.end());
     if (!staged) enc16_units(m);
     *out = m;
     return ANERF_OK;
@@ -247,8 +252,9 @@ int anerf_model_set_embed(anerf_model* m, const anerf_embed_params* embed) {
         HIP_TRY(hipGetDevice(&prev));
         HIP_TRY(hipSetDevice(m->device));
         hipError_t e = hipDeviceSynchronize();
-        if (e == hipSuccess && embed->cutoff_dist)
-            e = hipMemcpy(const_cast<float*>(m->md.cutoff), embed->cutoff_dist, nb, hipMemcpyHostToDevice);
+        if (e == hipSuccess && embed->cutoff_dist)  // (querypts: 3 kp cutoffs, the rest of the table stays 0)
+            e = hipMemcpy(const_cast<float*>(m->md.cutoff), embed->cutoff_dist,
+                          m->md.kp_query ? 3 * sizeof(float) : nb, hipMemcpyHostToDevice);
         if (e == hipSuccess && embed->cutoff_dist_v)
             e = hipMemcpy(const_cast<float*>(m->md.cutoff_v), embed->cutoff_dist_v, nb, hipMemcpyHostToDevice);
         if (e == hipSuccess && cb)
@@ -259,7 +265,7 @@ int anerf_model_set_embed(anerf_model* m, const anerf_embed_params* embed) {
     m->md.tau = embed->tau;
     m->md.tau_v = embed->tau_v;
     if (btab) m->md.tau_b = embed->tau_b;
-    if (embed->cutoff_dist) m->cut_host.assign(embed->cutoff_dist, embed->cutoff_dist + m->desc.n_joints);
+    if (embed->cutoff_dist && !m->md.kp_query) m->cut_host.assign(embed->cutoff_dist, embed->cutoff_dist + m->desc.n_joints);
     if (!m->md.staged) enc16_units(m);  // (the windowed features' bound moves with tau and the cutoffs)
     return ANERF_OK;
 }

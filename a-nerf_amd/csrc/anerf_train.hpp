@@ -39,7 +39,7 @@ __host__ __device__ inline FeatLayout feat_layout(const ModelDev& M) {
     FeatLayout L;
     L.nkp = M.kp_relpos ? 3 : 1;
     L.nvw = M.view_angle ? 1 : 3;
-    L.cb = M.nj * L.nkp * (1 + 2 * M.mr);
+    L.cb = (M.kp_query ? 3 : M.nj * L.nkp) * (1 + 2 * M.mr);  // (querypts: the point's 3 coordinates)
     L.cv = L.cb + 3 * M.nj * (1 + 2 * M.mrb);
     L.F = L.cv + M.nj * L.nvw * (1 + 2 * M.mrv);
     return L;
@@ -68,7 +68,21 @@ __device__ __forceinline__ void encode_joint(const ModelDev& M, const float* __r
     const float dist = norm3(qx, qy, qz);
     const float dn = fmaxf(dist, 1e-12f);
     const float w = M.use_cutoff ? cutoff_w(M.tau, dist, M.cutoff[j]) : 1.0f;
-    if (!M.kp_relpos) {
+    if (M.kp_query) {  // querypts: joint-threads 0..2 write world coordinate c = j, windowed by itself
+        if (j < 3) {
+            const float x = j == 0 ? px : (j == 1 ? py : pz);
+            const float wq = M.use_cutoff ? cutoff_w(M.tau, x, M.cutoff[j]) : 1.0f;
+            float u, uf;
+            kp_inputs(M.cut_to, M.shift_in, x, M.cutoff[j], u, uf);
+            f[j] = (M.use_cutoff && M.cutoff_inputs) ? u * wq : u;
+            for (int fi = 0; fi < M.mr; ++fi) {
+                float s, c;
+                sincos_rr(uf * (float)(1 << fi), s, c);
+                f[3 * (1 + 2 * fi) + j] = s * wq;
+                f[3 * (2 + 2 * fi) + j] = c * wq;
+            }
+        }
+    } else if (!M.kp_relpos) {
         float u, uf;
         kp_inputs(M.cut_to, M.shift_in, dist, M.cutoff[j], u, uf);
         f[j] = (M.use_cutoff && M.cutoff_inputs) ? u * w : u;
@@ -326,7 +340,7 @@ __device__ __noinline__ void encode_row_grad_joint_staged(const ModelDev& M, con
                                                           const float* __restrict__ g, float (&gS)[12]) {
     const int nj = M.nj;
     const FeatLayout L = feat_layout(M);
-    const bool dg = !M.kp_relpos;  // (the windows' distance carries a gradient)
+    const bool dg = !M.kp_relpos && !M.kp_query;  // (the windows' distance carries a gradient)
     float qx, qy, qz;
     joint_local(S, px, py, pz, qx, qy, qz);
     const float dist = norm3(qx, qy, qz);
@@ -337,7 +351,9 @@ __device__ __noinline__ void encode_row_grad_joint_staged(const ModelDev& M, con
     const bool cut = M.use_cutoff != 0, cut_in = M.use_cutoff && M.cutoff_inputs;
     const float w = cut ? cutoff_w(M.tau, dist, M.cutoff[j]) : 1.0f;
     float g_w = 0.0f;
-    if (!M.kp_relpos) {
+    if (M.kp_query) {
+        // querypts: the kp features depend on the world point only -- nothing for skts
+    } else if (!M.kp_relpos) {
         float u, uf;
         kp_inputs(M.cut_to, M.shift_in, dist, M.cutoff[j], u, uf);
         const float du = M.cut_to ? -1.0f : 1.0f;

@@ -58,7 +58,8 @@ class DeviceModel:
                            (_lib.ANERF_ENC_CUTOFF_BONES if cfg.bone_window else 0) |
                            (_lib.ANERF_ENC_VIEW_RAW if cfg.extra.get("view_type", "relray") == "world" else 0) |
                            (_lib.ANERF_ENC_KP_RELPOS if cfg.kp_relpos else 0) |
-                           (_lib.ANERF_ENC_VIEW_ANGLE if cfg.view_angle else 0))
+                           (_lib.ANERF_ENC_VIEW_ANGLE if cfg.view_angle else 0) |
+                           (_lib.ANERF_ENC_KP_QUERYPTS if cfg.kp_query else 0))
         d.multires_bones = cfg.multires_bones
         # (the C side windows the bare bone directions under the reference's condition, cutoff_inputs too:
         # anerf.h, ANERF_ENC_CUTOFF_BONES)

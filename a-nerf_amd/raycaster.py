@@ -5,7 +5,7 @@ dict of `_collect_outputs`, :711-724) and the model factory `create_raycaster`
 (:17-184).  `render_rays` keeps the reference signature; what the reference does in a
 dozen ATen ops per stage happens in one fused launch (`anerf_render_rays`).
 
-Staged encoders (`--multires_bones > 0`, `--kp_dist_type relpos`, `--view_type rayangle`; include/anerf.h)
+Staged encoders (`--multires_bones > 0`, `--kp_dist_type relpos | querypts`, `--view_type rayangle`; anerf.h)
 render on the training stages instead (`train.StagedCaster`, deterministic).
 
 Supported: eval-mode rendering (`perturb=0`, `raw_noise_std=0`, `ray_noise_std=0`; `lindisp`

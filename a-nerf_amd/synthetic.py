@@ -151,11 +151,11 @@ def _linear(rng, n_out, n_in):
     return w, b
 
 
-def nerf_input_dims(n_joints, multires=7, multires_views=4, multires_bones=0, kp_dims=1, view_dims=3):
+def nerf_input_dims(n_joints, multires=7, multires_views=4, multires_bones=0, kp_dims=1, view_dims=3, kp_query=False):
     """(input_ch, input_ch_bones, input_ch_views) as create_raycaster derives them
     (core/raycasters.py:24-79, core/cutoff_embedder.py:15-40); kp_dims 3 for --kp_dist_type relpos,
     view_dims 1 for --view_type rayangle."""
-    input_ch = n_joints * kp_dims * (1 + 2 * multires)
+    input_ch = (3 if kp_query else n_joints * kp_dims) * (1 + 2 * multires)  # (querypts: the world point)
     input_ch_bones = 3 * n_joints * (1 + 2 * multires_bones)
     input_ch_views = view_dims * n_joints * (1 + 2 * multires_views)
     return input_ch, input_ch_bones, input_ch_views
@@ -163,11 +163,12 @@ def nerf_input_dims(n_joints, multires=7, multires_views=4, multires_bones=0, kp
 
 def make_nerf_state(seed, n_joints=24, D=8, W=256, multires=7, multires_views=4,
                     skips=(4,), use_framecode=False, framecode_ch=16, n_framecodes=0,
-                    alpha_bias=2.0, alpha_gain=1.0, rgb_gain=1.0, multires_bones=0, kp_dims=1, view_dims=3):
+                    alpha_bias=2.0, alpha_gain=1.0, rgb_gain=1.0, multires_bones=0, kp_dims=1, view_dims=3,
+                    kp_query=False):
     """Seeded NeRF state dict with the key layout of core/networks/nerf.py:57-88."""
     rng = np.random.default_rng(seed)
     input_ch, input_ch_bones, input_ch_views = nerf_input_dims(n_joints, multires, multires_views, multires_bones,
-                                                               kp_dims, view_dims)
+                                                               kp_dims, view_dims, kp_query)
     dnet = input_ch + input_ch_bones
     sd = {}
     w, b = _linear(rng, W, dnet)
@@ -202,7 +203,7 @@ def make_embed_state(n_joints, cutoff=0.5, tau=20.0, jitter=0.0, seed=0):
 def make_checkpoint(seed, n_joints=24, D=8, W=256, fine=True, tau=20.0, tau_views=None,
                     cutoff_jitter=0.05, alpha_bias=0.5, alpha_gain=30.0, rgb_gain=8.0,
                     use_framecode=False, n_framecodes=0, multires=7, multires_views=4, sched_alpha=None,
-                    cutoff_bones=False, tau_bones=None, multires_bones=0, kp_dims=1, view_dims=3):
+                    cutoff_bones=False, tau_bones=None, multires_bones=0, kp_dims=1, view_dims=3, kp_query=False):
     """A full RayCaster checkpoint dict with the key layout of RayCaster.state_dict()
     (core/raycasters.py:752-766); sched_alpha: the --freq_schedule buffer of the cutoff embedders
     (core/cutoff_embedder.py:97-99), absent when None; cutoff_bones: the bone embedder is a
@@ -212,8 +213,9 @@ def make_checkpoint(seed, n_joints=24, D=8, W=256, fine=True, tau=20.0, tau_view
                                                  use_framecode=use_framecode,
                                                  n_framecodes=n_framecodes, alpha_bias=alpha_bias,
                                                  alpha_gain=alpha_gain, rgb_gain=rgb_gain, multires_bones=multires_bones,
-                                                 kp_dims=kp_dims, view_dims=view_dims),
-        "embed_state_dict": make_embed_state(n_joints, tau=tau, jitter=cutoff_jitter, seed=seed + 101),
+                                                 kp_dims=kp_dims, view_dims=view_dims, kp_query=kp_query),
+        # (querypts: the kp embedder's cutoff_dim is 3, core/raycasters.py:263-265)
+        "embed_state_dict": make_embed_state(3 if kp_query else n_joints, tau=tau, jitter=cutoff_jitter, seed=seed + 101),
         "embedbones_state_dict": {},
         "embeddirs_state_dict": make_embed_state(n_joints, tau=tau if tau_views is None else tau_views,
                                                  jitter=cutoff_jitter, seed=seed + 202),
@@ -230,7 +232,7 @@ def make_checkpoint(seed, n_joints=24, D=8, W=256, fine=True, tau=20.0, tau_view
                                                         n_framecodes=n_framecodes, alpha_bias=alpha_bias,
                                                         alpha_gain=alpha_gain, rgb_gain=rgb_gain,
                                                         multires_bones=multires_bones, kp_dims=kp_dims,
-                                                        view_dims=view_dims)
+                                                        view_dims=view_dims, kp_query=kp_query)
     return ck
 
 

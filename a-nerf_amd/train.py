@@ -411,7 +411,7 @@ class TrainRayCaster(nn.Module):
         # fresh models: cutoff_mm (default 500, run_nerf.py:416) x ext_scale (raycasters.py:33), tau 20
         cut = float(cfg.extra.get("cutoff_mm", 500.0)) * cfg.ext_scale
         alpha0 = cfg.init_freq if cfg.freq_schedule else None
-        self.embed_fn = _Embed(cfg.n_joints, cut, alpha0)
+        self.embed_fn = _Embed(3 if cfg.kp_query else cfg.n_joints, cut, alpha0)  # (querypts: cutoff_dim 3)
         self.embeddirs_fn = _Embed(cfg.n_joints, cut, alpha0)
         # --cutoff_bones: the bone embedder is a CutoffEmbedder too (raycasters.py:52-64), with its own
         # tau schedule (update_embed_fns, :745-747); otherwise it has no state
@@ -677,7 +677,7 @@ class TrainRayCaster(nn.Module):
 
 class StagedCaster:
     """Eval renders of a staged-encoder model (RenderConfig.staged: --multires_bones > 0, --kp_dist_type
-    relpos, --view_type rayangle; include/anerf.h) on the training stages: TrainRayCaster.render_rays with
+    relpos | querypts, --view_type rayangle; include/anerf.h) on the training stages: TrainRayCaster.render_rays with
     perturb 0 and no noise -- the reference's eval path (core/raycasters.py:361-474, deterministic
     sample_pdf) -- under no_grad, the MLP on the trainable networks' GEMMs (mlp.py; the default "mixed"
     forward is the fp32-accurate bf16x6).  Density queries (fwd_type 'density' / 'mesh',

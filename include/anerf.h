@@ -133,7 +133,7 @@ typedef struct {
                                 directions, the default); > 0 is a staged encoder (below) */
 } anerf_model_desc;
 
-/* Staged encoders (ABI 15): --multires_bones > 0, ANERF_ENC_KP_RELPOS and ANERF_ENC_VIEW_ANGLE change the
+/* Staged encoders (ABI 15): --multires_bones > 0, ANERF_ENC_KP_RELPOS / _KP_QUERYPTS and ANERF_ENC_VIEW_ANGLE change the
  * MLP's input layout beyond what the fused render kernel streams (its layer-0 parts and the per-ray view
  * factor G assume one distance per joint, bare bone directions and per-ray view directions).  A model with
  * any of them ("staged") is served by the training stages -- anerf_train_samples / _encode (+ _backward) /
@@ -143,7 +143,8 @@ typedef struct {
  * (the anerf_net_weights pointers may be NULL).  The feature row of a sample is
  *   [kp part | bone part | view part], with
  *   kp part   reldist: NJ (1 + 2 multires) columns, column f NJ + j (f = 0 the input, 2k + 1 / 2k + 2 the sin /
- *             cos of frequency 2^k);  relpos: 3 NJ (1 + 2 multires), column 3 f NJ + 3 j + c;
+ *             cos of frequency 2^k);  relpos: 3 NJ (1 + 2 multires), column 3 f NJ + 3 j + c;  querypts:
+ *             3 (1 + 2 multires), column 3 f + c;
  *   bone part 3 NJ (1 + 2 multires_bones), column 3 f NJ + 3 j + c;
  *   view part relray / world: 3 NJ (1 + 2 multires_views), column 3 f NJ + 3 j + c;
  *             rayangle: NJ (1 + 2 multires_views), column f NJ + j. */
@@ -176,6 +177,13 @@ typedef struct {
 /* --view_type rayangle (core/encoders.py:195-212, skeleton_utils.py:594-605; staged, ABI 15): the view input
  * of joint j is one angle, acos(clamp(q_j . R_j d / (|q_j| |R_j d|), -1 + 1e-6, 1 - 1e-6)) - pi / 2. */
 #define ANERF_ENC_VIEW_ANGLE 32
+/* --kp_dist_type querypts (core/raycasters.py:263-265, IdentityEncoder(1, 3); staged, ABI 15): the kp input is the
+ * world point p itself (3 values, not per joint); the kp CutoffEmbedder then has cutoff_dim 3 (embed->cutoff_dist
+ * holds 3 values, not NJ) and windows each coordinate by itself, w_c = 1 - sigmoid(tau (p_c - c_c))
+ * (cutoff_embedder.py:122-144: dists = inputs; --cut_to_dist / --cutoff_shift apply to the encoded values).  No
+ * gradient reaches skts through it.  Not with ANERF_ENC_CUTOFF_BONES (the reference's bone CutoffEmbedder then
+ * gets cutoff_dim 3 for 3 NJ inputs and fails). */
+#define ANERF_ENC_KP_QUERYPTS 64
 
 /* HOST pointers to one NeRF's weights, torch nn.Linear layout [out][in] (core/networks/nerf.py:57-88). */
 typedef struct {

@@ -37,7 +37,8 @@ NAMES = ["c1_64_s32_d4w128", "c2_256_s64_d8w256", "c3_512_s64i128_d8w256", "c4_5
          "vw1_viewworld_s32i16_d8w128"]
 # (round 5) staged encoders (include/anerf.h): rendered by train.StagedCaster on the training stages; GPU parity
 # in tests/test_gpu_staged.py
-STAGED = ["sg1_relpos_s32i16_d4w128", "sg2_rayangle_mrb2_cb_s32i16_d8w128", "sg3_all_fs_s32i16_d8w256"]
+STAGED = ["sg1_relpos_s32i16_d4w128", "sg2_rayangle_mrb2_cb_s32i16_d8w128", "sg3_all_fs_s32i16_d8w256",
+          "sg4_querypts_shift_s32i16_d8w128"]
 FRAMES = ["c1_64_s32_d4w128", "pw_64_white_d4w128", "pb_64_bgimg_d4w128"]
 
 
@@ -59,7 +60,7 @@ class Golden:
             kw["extra"] = extra
         # (round 5) the staged encoders' input shapes (tests/golden/make_golden.py staged_dims)
         dims = dict(multires_bones=int(val("--multires_bones", 0)), kp_dims=3 if val("--kp_dist_type") == "relpos" else 1,
-                    view_dims=1 if val("--view_type") == "rayangle" else 3)
+                    view_dims=1 if val("--view_type") == "rayangle" else 3, kp_query=val("--kp_dist_type") == "querypts")
         if "--softplus_shift" in flags:
             kw["softplus_shift"] = float(flags[flags.index("--softplus_shift") + 1])
         self.cfg = config.RenderConfig(n_joints=m["NJ"], netdepth=m["D"], netwidth=m["W"], N_samples=m["S"],

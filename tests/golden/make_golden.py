@@ -139,6 +139,9 @@ CONFIGS = {
     "sgd1_relpos_mrb2_density": dict(H=64, NJ=24, S=32, I=16, D=8, W=128, tau=20.0, kind="density", seed=54, res=10,
                                      radius=1.0, n_pts=300, cb=True, tau_b=35.0,
                                      flags=["--kp_dist_type", "relpos", "--multires_bones", "2", "--cutoff_bones"]),
+    # --kp_dist_type querypts (the world point as the kp input, windowed per coordinate) with --cutoff_shift
+    "sg4_querypts_shift_s32i16_d8w128": dict(H=128, NJ=24, S=32, I=16, D=8, W=128, tau=20.0, kind="rays", n_rays=128,
+                                             seed=55, flags=["--kp_dist_type", "querypts", "--cutoff_shift"]),
     "sg1_relpos_s32i16_d4w128": dict(H=128, NJ=24, S=32, I=16, D=4, W=128, tau=20.0, kind="rays", n_rays=128,
                                      seed=51, flags=["--kp_dist_type", "relpos"]),
     "sg2_rayangle_mrb2_cb_s32i16_d8w128": dict(H=128, NJ=24, S=32, I=16, D=8, W=128, tau=20.0, kind="rays",
@@ -182,7 +185,8 @@ def staged_dims(flags):
     def val(k, d):
         return flags[flags.index(k) + 1] if k in flags else d
     return dict(multires_bones=int(val("--multires_bones", 0)), kp_dims=3 if val("--kp_dist_type", "") == "relpos" else 1,
-                view_dims=1 if val("--view_type", "") == "rayangle" else 3)
+                view_dims=1 if val("--view_type", "") == "rayangle" else 3,
+                kp_query=val("--kp_dist_type", "") == "querypts")
 
 
 def build_reference(mods, cfg, tmp):

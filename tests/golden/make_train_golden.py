@@ -68,6 +68,9 @@ CONFIGS = {
                                             n_rays=64, n_poses=2, cb=True, tau_b=35.0,
                                             flags=["--kp_dist_type", "relpos", "--view_type", "rayangle",
                                                    "--multires_bones", "2", "--cutoff_bones"]),
+    # --kp_dist_type querypts (no gradient to the poses through the kp part) with --cutoff_shift
+    "t13_querypts_shift": dict(H=128, NJ=24, S=32, I=16, D=4, W=128, tau=20.0, kind="rays", seed=47, n_rays=64,
+                               n_poses=2, flags=["--kp_dist_type", "querypts", "--cutoff_shift"]),
 }
 FULL_LIMIT = 20000   # parameters with more entries are sampled
 SAMPLE = 4096

@@ -47,8 +47,11 @@ def test_config_rejects_unsupported_flags():
     assert cfg(multires_bones=2, cutoff_bones=True).validate().staged
     assert cfg(cutoff_bones=True).validate().bone_window
     assert not cfg(cutoff_bones=True, use_cutoff=False).validate().bone_window
+    with pytest.raises(NotImplementedError):  # (the reference's bone embedder fails on this pair)
+        cfg(extra={"kp_dist_type": "querypts"}, cutoff_bones=True).validate()
     with pytest.raises(NotImplementedError):
-        cfg(extra={"kp_dist_type": "querypts"}).validate()
+        cfg(extra={"kp_dist_type": "knn"}).validate()
+    assert cfg(extra={"kp_dist_type": "querypts"}).validate().staged
     assert cfg(extra={"kp_dist_type": "relpos"}).validate().staged
     assert cfg(extra={"view_type": "rayangle"}).validate().staged
     assert not cfg(extra={"view_type": "world"}).validate().staged
@@ -115,7 +118,7 @@ def test_encoder_selectors_follow_the_reference():
     (reference_flags.json, recorded by tests/golden/probe_reference_flags.py): kp_dist_type 'cat' and
     bone_type 'axisang' raise TypeError there and here; view_type 'world' runs there and renders here
     (fixture vw1_viewworld_s32i16_d8w128); relpos and rayangle run there and render here on the training
-    stages (staged encoders, fixtures sg*); querypts runs there and stays refused."""
+    stages (staged encoders, fixtures sg*), querypts too (not with --cutoff_bones, which fails there)."""
     import json
     with open(os.path.join(os.path.dirname(__file__), "golden", "reference_flags.json")) as f:
         rec = json.load(f)
@@ -126,12 +129,9 @@ def test_encoder_selectors_follow_the_reference():
             cfg(extra={key: val}).validate()
     assert rec["view_type=world"]["raises"] is None
     assert cfg(extra={"view_type": "world"}).validate().extra["view_type"] == "world"
-    for key, val in (("kp_dist_type", "relpos"), ("view_type", "rayangle")):
+    for key, val in (("kp_dist_type", "relpos"), ("kp_dist_type", "querypts"), ("view_type", "rayangle")):
         assert rec[f"{key}={val}"]["raises"] is None
         assert cfg(extra={key: val}).validate().staged
-    assert rec["kp_dist_type=querypts"]["raises"] is None
-    with pytest.raises(NotImplementedError):
-        cfg(extra={"kp_dist_type": "querypts"}).validate()
 
 
 def test_config_lindisp_from_args():
@@ -294,8 +294,10 @@ def test_staged_encoder_configs_match_reference_checkpoints():
     assert (g.cfg.kp_relpos, g.cfg.view_angle, g.cfg.multires_bones) == (True, True, 3)
     with pytest.raises(NotImplementedError):
         dataclasses.replace(g.cfg, multires_bones=11).validate()
-    with pytest.raises(NotImplementedError):  # (the reference's other kp type stays refused)
+    with pytest.raises(NotImplementedError):  # (querypts with --cutoff_bones fails in the reference)
         dataclasses.replace(g.cfg, extra={"kp_dist_type": "querypts"}).validate()
+    assert Golden("sg4_querypts_shift_s32i16_d8w128").cfg.input_ch == 3 * (1 + 2 * 7)
+    assert Golden("sg4_querypts_shift_s32i16_d8w128").ckpt["embed_state_dict"]["cutoff_dist"].shape == (3,)
 
 
 def test_feature_scales_follow_the_staged_layout():
