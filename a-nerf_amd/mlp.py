@@ -36,6 +36,21 @@ def _stream(dev):
     return _lib.stream_handle(dev)
 
 
+# The weight gradients of the backward run on a second stream, beside the input gradients on the
+# caller's: a hidden layer's two products read the same dY and the same saved activation, so running
+# them together lets the second read of each hit the caches (and the two kernels fill each other's
+# tails).  The caller's stream waits for the side stream before the backward returns.
+WGRAD_OVERLAP = True
+_SIDE = {}
+
+
+def _side_stream(dev):
+    key = torch.device(dev).index
+    if key not in _SIDE:
+        _SIDE[key] = torch.cuda.Stream(device=dev)
+    return _SIDE[key]
+
+
 def _seg(t, cols, off=0):
     """anerf_seg over columns [off, off + cols) of a row-major 2-D tensor."""
     return (t.data_ptr() + 4 * off, t.stride(0), cols)
@@ -206,20 +221,31 @@ class _MLP(torch.autograd.Function):
         ws = [torch.empty(0, device=dev, dtype=torch.uint8)]  # grown to the largest layer's need
         grads = [None] * len(params)
 
-        def wg(n, k, dy, x):
+        main = torch.cuda.current_stream(dev)
+        side = _side_stream(dev) if WGRAD_OVERLAP else None
+
+        def wg(n, k, dy, x, xt=()):
+            """dW, db of one layer (x: its input segments over the tensors xt), on the side stream."""
             need = lib.anerf_mlp_wgrad_workspace(M, n, k)
             if ws[0].numel() < need:
                 ws[0] = torch.empty(need, device=dev, dtype=torch.uint8)
             dw = torch.empty(n, k, **f32)
             db = torch.empty(n, **f32)
-            wgrad(M, n, k, dy, x, dw, db, ws[0], dev, prec)
+            if side is None:
+                wgrad(M, n, k, dy, x, dw, db, ws[0], dev, prec)
+                return dw, db
+            side.wait_stream(main)  # (dy and the allocations above are the caller stream's work)
+            with torch.cuda.stream(side):
+                wgrad(M, n, k, dy, x, dw, db, ws[0], dev, prec)
+            for t in (dy, dw, db, ws[0], *xt):  # (their memory is not reused before the side stream is done)
+                t.record_stream(side)
             return dw, db
 
         # rgb_linear: input gradient masked by relu(view layer) > 0
         gzv = torch.empty(M, W // 2, **f32)
         mm(M, W // 2, 3, [_seg(g_raw, 3)], st[D + 2], None, False,
              [(gzv, W // 2, W // 2, 0, g, False)], dev)
-        grads[2 * nl + 6], grads[2 * nl + 7] = wg(3, W // 2, g_raw, [_seg(g, W // 2)])
+        grads[2 * nl + 6], grads[2 * nl + 7] = wg(3, W // 2, g_raw, [_seg(g, W // 2)], (g,))
         # views_linears[0]: gradients of feature (into gha[:, :W]), view columns of feat, framecodes
         gha = torch.empty(M, W + 4, **f32)  # [g_feature | g_alpha] (ld padded to 16 B)
         gha[:, W].copy_(g_raw[:, 3])
@@ -233,12 +259,13 @@ class _MLP(torch.autograd.Function):
         mm(M, nvo, W // 2, [_seg(gzv, W // 2)], st[D + 1], None, False,
              outs if nvo > W else outs[:1], dev)
         av = [_seg(hf, W), _seg(feat, nv, dnet)] + ([_seg(codes, cfc)] if cfc else [])
-        grads[2 * nl + 4], grads[2 * nl + 5] = wg(W // 2, W + nv + cfc, gzv, av)
+        grads[2 * nl + 4], grads[2 * nl + 5] = wg(W // 2, W + nv + cfc, gzv, av,
+                                                  (hf, feat) + ((codes,) if cfc else ()))
         # feature_linear + alpha_linear: one input gradient, masked by relu(last hidden) > 0
         gz = torch.empty(M, W, **f32)
         mm(M, W, W + 1, [_seg(gha, W + 1)], st[D], None, False,
              [(gz, W, W, 0, H[-1], False)], dev)
-        dwh, dbh = wg(W + 1, W, gha, [_seg(H[-1], W)])
+        dwh, dbh = wg(W + 1, W, gha, [_seg(H[-1], W)], (H[-1],))
         grads[2 * nl + 2], grads[2 * nl + 3] = dwh[:W], dbh[:W]  # feature_linear
         grads[2 * nl + 0], grads[2 * nl + 1] = dwh[W:], dbh[W:]  # alpha_linear
         # the trunk, last layer first
@@ -251,7 +278,7 @@ class _MLP(torch.autograd.Function):
                 a, k = [segx, _seg(H[i - 1], W)], dnet + W
             else:
                 a, k = [_seg(H[i - 1], W)], W
-            grads[2 * i], grads[2 * i + 1] = wg(W, k, gz, a)
+            grads[2 * i], grads[2 * i + 1] = wg(W, k, gz, a, (feat,) + ((H[i - 1],) if i > 0 else ()))
             if i == 0:
                 if need_feat:
                     mm(M, dnet, W, [_seg(gz, W)], st[0], None, False,
@@ -267,6 +294,8 @@ class _MLP(torch.autograd.Function):
                 mm(M, W, W, [_seg(gz, W)], st[i], None, False,
                      [(gprev, W, W, 0, H[i - 1], False)], dev)
             gz = gprev
+        if side is not None:
+            main.wait_stream(side)
         return (None, gfeat, gcodes, *grads)
 
 

@@ -36,6 +36,8 @@ def parser():
     ap.add_argument("--importance", type=int, default=16)
     ap.add_argument("--mlp", default="mixed", choices=["mixed", "mixed16", "bf16x6", "bf16x3", "fp32"],
                     help="training MLP arithmetic (train.TrainRayCaster mlp=)")
+    ap.add_argument("--no-wgrad-overlap", action="store_true",
+                    help="ablation: the weight gradients on the caller's stream (mlp.WGRAD_OVERLAP off)")
     ap.add_argument("--split-single", action="store_true",
                     help="ablation: one split launch per weight instead of the batched split")
     return ap
@@ -57,6 +59,8 @@ def measure(a, dev=None):
     sc = syn.make_scene(n_joints=24, H=512, W=512, seed=13, n_frames=a.images, yaw_step=2 * np.pi / a.images)
     idx, cyls, _ = anerf.rays.valid_pixels(sc["c2ws"], 512, 512, sc["focal"], kps=sc["kps"], ext_scale=0.001)
     rng = np.random.default_rng(0)
+    if getattr(a, "no_wgrad_overlap", False):
+        importlib.import_module("a-nerf_amd.mlp").WGRAD_OVERLAP = False
     tr = train.TrainRayCaster(cfg, ck, device=dev, mlp=a.mlp).train()
     skts = torch.from_numpy(sc["skts"]).to(dev)
     delta = torch.zeros_like(skts, requires_grad=True)  # pose optimisation variable per image
