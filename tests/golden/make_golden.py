@@ -142,6 +142,9 @@ CONFIGS = {
     # --kp_dist_type querypts (the world point as the kp input, windowed per coordinate) with --cutoff_shift
     "sg4_querypts_shift_s32i16_d8w128": dict(H=128, NJ=24, S=32, I=16, D=8, W=128, tau=20.0, kind="rays", n_rays=128,
                                              seed=55, flags=["--kp_dist_type", "querypts", "--cutoff_shift"]),
+    # a render_path frame (64 x 64) of a staged model: relpos + rayangle, 32 + 16 samples
+    "sgf1_frame_relpos_rayangle_d4w128": dict(H=64, NJ=24, S=32, I=16, D=4, W=128, tau=20.0, kind="frame", seed=56,
+                                              flags=["--kp_dist_type", "relpos", "--view_type", "rayangle"]),
     "sg1_relpos_s32i16_d4w128": dict(H=128, NJ=24, S=32, I=16, D=4, W=128, tau=20.0, kind="rays", n_rays=128,
                                      seed=51, flags=["--kp_dist_type", "relpos"]),
     "sg2_rayangle_mrb2_cb_s32i16_d8w128": dict(H=128, NJ=24, S=32, I=16, D=8, W=128, tau=20.0, kind="rays",

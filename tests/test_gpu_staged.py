@@ -130,3 +130,22 @@ def test_staged_eval_caster_equals_training_path_without_noise():
         b = tr.render_rays(rb, g.cfg.N_samples, skts=skts, cyls=cyls, N_importance=g.cfg.N_importance)
     for k in ("rgb_map", "disp_map", "acc_map"):
         assert torch.equal(a[k], b[k]), k
+
+
+def test_staged_render_path_frame_matches_reference():
+    """render_path (the caller of render_rays, run_nerf.py:27-145) over a staged model: a 64 x 64 frame with
+    relpos kp inputs and ray angles, pixel set exact and images within 1e-4 of the reference's own frame."""
+    g = Golden("sgf1_frame_relpos_rayangle_d4w128")
+    rc = anerf.RayCaster(g.cfg, g.ckpt)
+    kw = {"ray_caster": rc, "N_samples": g.cfg.N_samples, "N_importance": g.cfg.N_importance, "perturb": False,
+          "raw_noise_std": 0., "ray_noise_std": 0., "use_viewdirs": True, "preproc_kwargs": {"density_scale": 1.0},
+          "lindisp": False}
+    H = g.meta["H"]
+    rgbs, disps, accs, vids, bbs = anerf.render_path(
+        torch.from_numpy(g["c2ws"]), (H, H, g.meta["focal"]), 4096, kw, kp=torch.from_numpy(g["kps"]),
+        skts=torch.from_numpy(g["skts"]), ret_acc=True, ext_scale=0.001)
+    np.testing.assert_array_equal(vids[0].numpy(), g["valid_idx"])
+    assert rgbs.shape == g["frame_rgb"].shape
+    assert _maxdiff(rgbs, g["frame_rgb"]) <= TOL
+    assert _maxdiff(disps, g["frame_disp"]) <= TOL
+    assert _maxdiff(accs, g["frame_acc"]) <= TOL
