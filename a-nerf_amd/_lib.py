@@ -34,7 +34,8 @@ ANERF_ENC_CUT_TO_DIST, ANERF_ENC_CUTOFF_SHIFT, ANERF_ENC_CUTOFF_BONES = 1, 2, 4 
 ANERF_ENC_VIEW_RAW = 8  # --view_type world
 ANERF_ENC_KP_RELPOS, ANERF_ENC_VIEW_ANGLE = 16, 32  # --kp_dist_type relpos, --view_type rayangle (staged, ABI 15)
 ANERF_ENC_KP_QUERYPTS = 64  # --kp_dist_type querypts (staged, ABI 15)
-ABI_VERSION = 15  # include/anerf.h ANERF_ABI_VERSION: the structs below
+ANERF_ENC_VIEW_WINDOWS = 128  # training layout: the view part as the NJ view windows (ABI 16)
+ABI_VERSION = 16  # include/anerf.h ANERF_ABI_VERSION: the structs below
 
 
 class ModelDesc(ctypes.Structure):
@@ -190,6 +191,25 @@ SIGNATURES = {
     "anerf_train_importance": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
                                               ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
                                               ctypes.c_void_p, ctypes.c_void_p]),
+    "anerf_train_view_factor": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64,
+                                               ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                               ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                               ctypes.c_void_p]),
+    "anerf_train_view_factor_workspace": (ctypes.c_size_t, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                                            ctypes.c_int32]),
+    "anerf_train_view_factor_backward": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32,
+                                                        ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32,
+                                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                                        ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                        ctypes.c_size_t, ctypes.c_void_p]),
+    "anerf_train_view_mix": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                            ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_void_p]),
+    "anerf_train_view_mix_backward": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                                     ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                                     ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                                                     ctypes.c_void_p]),
     "anerf_mlp_split_bytes": (ctypes.c_size_t, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
     "anerf_mlp_forward_pack_bytes": (ctypes.c_size_t, [ctypes.POINTER(MlpShape)]),
     "anerf_mlp_forward_pack": (ctypes.c_int, [ctypes.POINTER(MlpShape), ctypes.POINTER(MlpFwdWeights),

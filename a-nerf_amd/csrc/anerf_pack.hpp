@@ -545,7 +545,7 @@ static int validate_desc(const anerf_model_desc* d) {
     if (d->density_scale == 0.0f) return fail(ANERF_EINVAL, "density_scale must be non-zero");
     if (d->multires_bones < 0 || d->multires_bones > 10) return fail(ANERF_EINVAL, "multires_bones outside [0, 10]");
     if (d->encoder_flags & ~(ANERF_ENC_CUT_TO_DIST | ANERF_ENC_CUTOFF_SHIFT | ANERF_ENC_CUTOFF_BONES | ANERF_ENC_VIEW_RAW |
-                             ANERF_ENC_KP_RELPOS | ANERF_ENC_VIEW_ANGLE | ANERF_ENC_KP_QUERYPTS))
+                             ANERF_ENC_KP_RELPOS | ANERF_ENC_VIEW_ANGLE | ANERF_ENC_KP_QUERYPTS | ANERF_ENC_VIEW_WINDOWS))
         return fail(ANERF_EINVAL, "unknown encoder_flags bits");
     if ((d->encoder_flags & ANERF_ENC_KP_RELPOS) && (d->encoder_flags & ANERF_ENC_KP_QUERYPTS))
         return fail(ANERF_EINVAL, "ANERF_ENC_KP_RELPOS and ANERF_ENC_KP_QUERYPTS are two kp types");
@@ -556,6 +556,13 @@ static int validate_desc(const anerf_model_desc* d) {
         return fail(ANERF_EINVAL, "ANERF_ENC_KP_QUERYPTS needs n_joints >= 3");
     if ((d->encoder_flags & ANERF_ENC_VIEW_RAW) && (d->encoder_flags & ANERF_ENC_VIEW_ANGLE))
         return fail(ANERF_EINVAL, "ANERF_ENC_VIEW_RAW and ANERF_ENC_VIEW_ANGLE are two view types");
+    if (d->encoder_flags & ANERF_ENC_VIEW_WINDOWS) {
+        if (!d->cutoff_viewdir || !d->cutoff_inputs)
+            return fail(ANERF_EINVAL, "ANERF_ENC_VIEW_WINDOWS needs cutoff_viewdir and cutoff_inputs (every view feature "
+                                      "windowed)");
+        if (d->multires_bones > 0 || (d->encoder_flags & (ANERF_ENC_KP_RELPOS | ANERF_ENC_VIEW_ANGLE | ANERF_ENC_KP_QUERYPTS)))
+            return fail(ANERF_EINVAL, "ANERF_ENC_VIEW_WINDOWS is not for a staged encoder");
+    }
     return ANERF_OK;
 }
 

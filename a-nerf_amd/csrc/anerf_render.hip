@@ -213,6 +213,7 @@ int anerf_model_create(const anerf_model_desc* desc, const anerf_net_weights* co
     md.kp_relpos = (desc->encoder_flags & ANERF_ENC_KP_RELPOS) ? 1 : 0;
     md.view_angle = (desc->encoder_flags & ANERF_ENC_VIEW_ANGLE) ? 1 : 0;
     md.kp_query = (desc->encoder_flags & ANERF_ENC_KP_QUERYPTS) ? 1 : 0;
+    md.view_win = (desc->encoder_flags & ANERF_ENC_VIEW_WINDOWS) ? 1 : 0;
     md.bone_win = bone_win ? 1 : 0;
     md.staged = staged ? 1 : 0;
     md.tau = embed->tau;
@@ -620,6 +621,9 @@ int anerf_train_encode_backward(const anerf_model* m, const float* ray_batch, in
                            grad_feat, grad_skts, spb);
     };
     if (m->md.staged) launch(train_encode_backward_kernel<-1, -1>);  // (the staged encoders: run-time layout)
+    else if (m->md.view_win && mr == 7) launch(train_encode_backward_kernel<7, -2>);  // (ANERF_ENC_VIEW_WINDOWS)
+    else if (m->md.view_win && mr == 10) launch(train_encode_backward_kernel<10, -2>);
+    else if (m->md.view_win && mr >= 0 && mr <= 10) launch(train_encode_backward_kernel<-1, -2>);
     else if (mr == 7 && mrv == 4) launch(train_encode_backward_kernel<7, 4>);
     else if (mr == 7 && mrv == 0) launch(train_encode_backward_kernel<7, 0>);
     else if (mr == 10 && mrv == 4) launch(train_encode_backward_kernel<10, 4>);
@@ -681,6 +685,113 @@ int anerf_train_importance(const float* z, const float* weights, int64_t n_rays,
                                 (int)lds));
     hipLaunchKernelGGL(train_importance_kernel, dim3((unsigned)n_rays), dim3(64), lds, st, z, weights, n_rays,
                        n_samples, n_importance, u, single_net, z_all, sorted_idx);
+    HIP_TRY(hipGetLastError());
+    return ANERF_OK;
+}
+
+static int check_view_factor(const char* fn, const anerf_model* m, const float* ray_batch, int32_t ray_stride,
+                             int64_t n_rays, const float* skts, int32_t n_poses, const int32_t* ray_pose,
+                             const float* weight, int64_t ld_weight, int32_t width) {
+    if (!m || !ray_batch || ray_stride < 6 || n_rays < 0 || !skts || !weight || width < 4 || width > 128 || (width & 3))
+        return fail(ANERF_EINVAL, std::string(fn) + ": bad arguments (width 4-128, a multiple of 4)");
+    if (m->md.view_angle) return fail(ANERF_EINVAL, std::string(fn) + ": ray-angle views have no per-ray factor");
+    if (ld_weight < 3LL * m->desc.n_joints * (1 + 2 * m->desc.multires_views))
+        return fail(ANERF_EINVAL, std::string(fn) + ": ld_weight shorter than the view columns");
+    if (!ray_pose && n_poses != n_rays) return fail(ANERF_EINVAL, "per-ray skeletons need n_poses == n_rays");
+    if (ray_pose && n_poses < 1) return fail(ANERF_EINVAL, "n_poses < 1");
+    if ((n_rays + VF_RC - 1) / VF_RC > 0x7fffffff) return fail(ANERF_EINVAL, "too many rays for one launch");
+    return ANERF_OK;
+}
+
+int anerf_train_view_factor(const anerf_model* m, const float* ray_batch, int32_t ray_stride, int64_t n_rays,
+                            const float* skts, int32_t n_poses, const int32_t* ray_pose, const float* weight,
+                            int64_t ld_weight, int32_t width, const float* col_scale, float* G, void* stream) {
+    int rc = check_view_factor("anerf_train_view_factor", m, ray_batch, ray_stride, n_rays, skts, n_poses, ray_pose,
+                               weight, ld_weight, width);
+    if (rc) return rc;
+    if (!G || (reinterpret_cast<uintptr_t>(G) & 15)) return fail(ANERF_EINVAL, "anerf_train_view_factor: G NULL or unaligned");
+    if (n_rays == 0) return ANERF_OK;
+    const int nk = 3 * (1 + 2 * m->md.mrv);
+    hipLaunchKernelGGL(train_view_factor_kernel, dim3((unsigned)((n_rays + VF_RC - 1) / VF_RC), m->desc.n_joints),
+                       dim3(256), (size_t)(nk * width + VF_RC * 28) * 4, reinterpret_cast<hipStream_t>(stream), m->md, ray_batch,
+                       ray_stride, n_rays, skts, ray_pose, n_poses, weight, ld_weight, width, col_scale, G);
+    HIP_TRY(hipGetLastError());
+    return ANERF_OK;
+}
+
+size_t anerf_train_view_factor_workspace(int64_t n_rays, int32_t n_joints, int32_t multires_views, int32_t width) {
+    if (n_rays <= 0 || n_joints < 1 || multires_views < 0 || multires_views > 4 || width < 1) return 0;
+    return (size_t)((n_rays + VF_RAYS_B - 1) / VF_RAYS_B) * n_joints * 3 * (1 + 2 * multires_views) * width * 4;
+}
+
+int anerf_train_view_factor_backward(const anerf_model* m, const float* ray_batch, int32_t ray_stride, int64_t n_rays,
+                                     const float* skts, int32_t n_poses, const int32_t* ray_pose, const float* weight,
+                                     int64_t ld_weight, int32_t width, const float* col_scale, const float* grad_G,
+                                     float* grad_skts, float* grad_weight, void* workspace, size_t workspace_bytes,
+                                     void* stream) {
+    int rc = check_view_factor("anerf_train_view_factor_backward", m, ray_batch, ray_stride, n_rays, skts, n_poses,
+                               ray_pose, weight, ld_weight, width);
+    if (rc) return rc;
+    if (!grad_G || !grad_skts || !grad_weight || (reinterpret_cast<uintptr_t>(grad_G) & 15))
+        return fail(ANERF_EINVAL, "anerf_train_view_factor_backward: NULL or unaligned gradient");
+    if (n_rays == 0) return ANERF_OK;
+    const size_t need = anerf_train_view_factor_workspace(n_rays, m->desc.n_joints, m->desc.multires_views, width);
+    if (!workspace || workspace_bytes < need || (reinterpret_cast<uintptr_t>(workspace) & 15))
+        return fail(ANERF_EINVAL, "anerf_train_view_factor_backward: workspace NULL, unaligned or smaller than "
+                                  "anerf_train_view_factor_workspace()");
+    const int nk = 3 * (1 + 2 * m->md.mrv), nj = m->desc.n_joints;
+    const unsigned nb = (unsigned)((n_rays + VF_RAYS_B - 1) / VF_RAYS_B);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    float* part = static_cast<float*>(workspace);
+    hipLaunchKernelGGL(train_view_factor_backward_kernel, dim3(nb, nj), dim3(256),
+                       (size_t)(nk * width + VF_RC * (width + 4) + 2 * VF_RC * 28) * 4, st, m->md, ray_batch, ray_stride,
+                       n_rays, skts, ray_pose, n_poses, weight, ld_weight, width, col_scale, grad_G, grad_skts, part);
+    HIP_TRY(hipGetLastError());
+    const int64_t per = (int64_t)nj * nk * width;
+    hipLaunchKernelGGL(train_view_factor_reduce_kernel, dim3((unsigned)((per + 255) / 256)), dim3(256), 0, st, part,
+                       (int)nb, nj, nk, width, col_scale, grad_weight, ld_weight);
+    HIP_TRY(hipGetLastError());
+    return ANERF_OK;
+}
+
+static int check_view_mix(const char* fn, int64_t n_rays, int32_t n_samples, int32_t n_joints, int32_t width,
+                          const float* windows, int64_t ld, const float* G) {
+    if (!windows || !G || n_rays < 0 || n_samples < 1 || n_joints < 1 || width < 4 || (width & 3) ||
+        n_joints * width > 4096 || ld < n_joints || (reinterpret_cast<uintptr_t>(G) & 15))
+        return fail(ANERF_EINVAL, std::string(fn) + ": bad arguments (width % 4 == 0, n_joints * width <= 4096, "
+                                                     "ld >= n_joints, G 16-byte aligned)");
+    if (n_rays > 0x7fffffff) return fail(ANERF_EINVAL, "too many rays for one launch");
+    return ANERF_OK;
+}
+
+int anerf_train_view_mix(int64_t n_rays, int32_t n_samples, int32_t n_joints, int32_t width, const float* windows,
+                         int64_t ld_windows, const float* G, float* out, void* stream) {
+    int rc = check_view_mix("anerf_train_view_mix", n_rays, n_samples, n_joints, width, windows, ld_windows, G);
+    if (rc) return rc;
+    if (!out || (reinterpret_cast<uintptr_t>(out) & 15)) return fail(ANERF_EINVAL, "anerf_train_view_mix: out NULL or unaligned");
+    if (n_rays == 0) return ANERF_OK;
+    if ((size_t)(n_joints * width + VM_SC * n_joints) * 4 > 64 * 1024)
+        return fail(ANERF_EINVAL, "anerf_train_view_mix: n_joints too large for the LDS plan");
+    hipLaunchKernelGGL(train_view_mix_kernel, dim3((unsigned)n_rays), dim3(256),
+                       (size_t)(n_joints * width + VM_SC * n_joints) * 4, reinterpret_cast<hipStream_t>(stream),
+                       windows, ld_windows, n_samples, n_joints, G, width, out);
+    HIP_TRY(hipGetLastError());
+    return ANERF_OK;
+}
+
+int anerf_train_view_mix_backward(int64_t n_rays, int32_t n_samples, int32_t n_joints, int32_t width,
+                                  const float* windows, int64_t ld_windows, const float* G, const float* grad_out,
+                                  float* grad_windows, int64_t ld_grad_windows, float* grad_G, void* stream) {
+    int rc = check_view_mix("anerf_train_view_mix_backward", n_rays, n_samples, n_joints, width, windows, ld_windows, G);
+    if (rc) return rc;
+    if (!grad_out || !grad_windows || !grad_G || ld_grad_windows < n_joints || (reinterpret_cast<uintptr_t>(grad_out) & 15))
+        return fail(ANERF_EINVAL, "anerf_train_view_mix_backward: bad gradient arguments");
+    if (n_rays == 0) return ANERF_OK;
+    const size_t lds = (size_t)(4 * ((n_joints + 3) / 4) * (width + 4) + VM_SC * (width + 4) + VM_SC * n_joints) * 4;
+    if (lds > 64 * 1024) return fail(ANERF_EINVAL, "anerf_train_view_mix_backward: n_joints too large for the LDS plan");
+    hipLaunchKernelGGL(train_view_mix_backward_kernel, dim3((unsigned)n_rays), dim3(256), lds,
+                       reinterpret_cast<hipStream_t>(stream), windows, ld_windows, n_samples, n_joints, G, width,
+                       grad_out, grad_windows, ld_grad_windows, grad_G);
     HIP_TRY(hipGetLastError());
     return ANERF_OK;
 }

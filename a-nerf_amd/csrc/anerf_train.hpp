@@ -41,7 +41,7 @@ __host__ __device__ inline FeatLayout feat_layout(const ModelDev& M) {
     L.nvw = M.view_angle ? 1 : 3;
     L.cb = (M.kp_query ? 3 : M.nj * L.nkp) * (1 + 2 * M.mr);  // (querypts: the point's 3 coordinates)
     L.cv = L.cb + 3 * M.nj * (1 + 2 * M.mrb);
-    L.F = L.cv + M.nj * L.nvw * (1 + 2 * M.mrv);
+    L.F = L.cv + (M.view_win ? M.nj : M.nj * L.nvw * (1 + 2 * M.mrv));  // (ANERF_ENC_VIEW_WINDOWS: the windows)
     return L;
 }
 
@@ -124,9 +124,13 @@ __device__ __forceinline__ void encode_joint(const ModelDev& M, const float* __r
             }
         }
     }
+    const float wv = M.cutoff_viewdir ? cutoff_w(M.tau_v, dist, M.cutoff_v[j]) : 1.0f;
+    if (M.view_win) {  // (the caller contracts the direction terms per ray, anerf.h ANERF_ENC_VIEW_WINDOWS)
+        f[L.cv + j] = wv;
+        return;
+    }
     float ex, ey, ez;
     joint_rot(S, dx, dy, dz, ex, ey, ez);
-    const float wv = M.cutoff_viewdir ? cutoff_w(M.tau_v, dist, M.cutoff_v[j]) : 1.0f;
     if (M.view_angle) {
         float cs;
         const float a = ray_angle(qx, qy, qz, ex, ey, ez, cs);
@@ -189,18 +193,21 @@ __global__ void train_encode_kernel(ModelDev M, const float* __restrict__ rb, in
 // F.normalize x / max(|x|, 1e-12); torch.norm's gradient 0 at 0).
 // MR / MRV: the frequencies (compile-time, so every feature gradient of the joint is loaded up front
 // and the loads overlap instead of waiting one loop iteration each); -1: the model's counts at run time
-// (multires up to 10, multires_views up to 4: the other configurations' generic instance).
+// (multires up to 10, multires_views up to 4: the other configurations' generic instance).  MRV -2: the
+// ANERF_ENC_VIEW_WINDOWS layout (the view part is the NJ windows; their gradient reaches skts through dist).
 template <int MR, int MRV>
 __device__ __forceinline__ void encode_row_grad_joint(const ModelDev& M, const float* __restrict__ S, int j,
                                                       float px, float py, float pz, float dx, float dy, float dz,
                                                       const float* __restrict__ g, float (&gS)[12]) {
-    constexpr int MRX = MR >= 0 ? MR : 10, MVX = MRV >= 0 ? MRV : 4;  // (loop bounds; runtime counts below)
-    const int mr = MR >= 0 ? MR : M.mr, mrv = MRV >= 0 ? MRV : M.mrv;
+    constexpr bool VW = MRV == -2;
+    constexpr int MRX = MR >= 0 ? MR : 10, MVX = MRV >= 0 ? MRV : (VW ? 0 : 4);  // (loop bounds; runtime counts below)
+    const int mr = MR >= 0 ? MR : M.mr, mrv = MRV >= 0 ? MRV : (VW ? 0 : M.mrv);
     const int nj = M.nj, nv = 1 + 2 * mr;
     const int cx = nj * nv + 3 * nj;
     constexpr int MV = MVX > 0 ? MVX : 1;
     float gs_[MRX > 0 ? MRX : 1], gc_[MRX > 0 ? MRX : 1], gu_[3], gv0_[3], gvs_[3][MV], gvc_[3][MV];
     const float g0 = g[j];
+    const float g_win = VW ? g[cx + j] : 0.0f;
 #pragma unroll
     for (int fi = 0; fi < MRX; ++fi) {
         gs_[fi] = fi < mr ? g[(1 + 2 * fi) * nj + j] : 0.0f;
@@ -209,7 +216,7 @@ __device__ __forceinline__ void encode_row_grad_joint(const ModelDev& M, const f
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         gu_[c] = g[nj * nv + 3 * j + c];
-        gv0_[c] = g[cx + 3 * j + c];
+        gv0_[c] = VW ? 0.0f : g[cx + 3 * j + c];
 #pragma unroll
         for (int fi = 0; fi < MVX; ++fi) {
             gvs_[c][fi] = fi < mrv ? g[cx + (1 + 2 * fi) * 3 * nj + 3 * j + c] : 0.0f;
@@ -271,49 +278,54 @@ __device__ __forceinline__ void encode_row_grad_joint(const ModelDev& M, const f
         }
     }
     // ---- view direction e = R d / max(|R d|, eps), window on dist
-    float ex, ey, ez;
-    joint_rot(S, dx, dy, dz, ex, ey, ez);
-    const float enr = norm3(ex, ey, ez);
-    const float en = M.view_raw ? 1.0f : fmaxf(enr, 1e-12f);  // (--view_type world: no normalisation)
-    const float e[3] = {ex / en, ey / en, ez / en};
-    const bool cutv = M.cutoff_viewdir != 0;
-    const float wv = cutv ? cutoff_w(M.tau_v, dist, M.cutoff_v[j]) : 1.0f;
-    float ge[3] = {0.0f, 0.0f, 0.0f}, g_wv = 0.0f;
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        const float gv0 = gv0_[c];
-        if (cutv && M.cutoff_inputs) {
-            ge[c] += gv0 * wv;
-            g_wv += gv0 * e[c];
-        } else {
-            ge[c] += gv0;
-        }
-#pragma unroll
-        for (int fi = 0; fi < MVX; ++fi) {
-            if (fi >= mrv) break;
-            const float fr = (float)(1 << fi);
-            float s, co;
-            sincos_rr(e[c] * fr, s, co);
-            const float gs = gvs_[c][fi], gc = gvc_[c][fi];
-            g_wv += gs * s + gc * co;
-            ge[c] += (gs * co - gc * s) * wv * fr;
-        }
-    }
-    if (cutv) g_dist += g_wv * (-M.tau_v * wv * (1.0f - wv));
-    float gex, gey, gez;
-    if (M.view_raw) {  // e = R_j d itself
-        gex = ge[0];
-        gey = ge[1];
-        gez = ge[2];
-    } else if (enr > 1e-12f) {
-        const float dot = e[0] * ge[0] + e[1] * ge[1] + e[2] * ge[2];
-        gex = (ge[0] - e[0] * dot) / enr;
-        gey = (ge[1] - e[1] * dot) / enr;
-        gez = (ge[2] - e[2] * dot) / enr;
+    float gex = 0.0f, gey = 0.0f, gez = 0.0f;
+    if constexpr (VW) {
+        const float wv = cutoff_w(M.tau_v, dist, M.cutoff_v[j]);  // (the flag implies cutoff_viewdir)
+        g_dist += g_win * (-M.tau_v * wv * (1.0f - wv));
     } else {
-        gex = ge[0] / 1e-12f;
-        gey = ge[1] / 1e-12f;
-        gez = ge[2] / 1e-12f;
+        float ex, ey, ez;
+        joint_rot(S, dx, dy, dz, ex, ey, ez);
+        const float enr = norm3(ex, ey, ez);
+        const float en = M.view_raw ? 1.0f : fmaxf(enr, 1e-12f);  // (--view_type world: no normalisation)
+        const float e[3] = {ex / en, ey / en, ez / en};
+        const bool cutv = M.cutoff_viewdir != 0;
+        const float wv = cutv ? cutoff_w(M.tau_v, dist, M.cutoff_v[j]) : 1.0f;
+        float ge[3] = {0.0f, 0.0f, 0.0f}, g_wv = 0.0f;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const float gv0 = gv0_[c];
+            if (cutv && M.cutoff_inputs) {
+                ge[c] += gv0 * wv;
+                g_wv += gv0 * e[c];
+            } else {
+                ge[c] += gv0;
+            }
+#pragma unroll
+            for (int fi = 0; fi < MVX; ++fi) {
+                if (fi >= mrv) break;
+                const float fr = (float)(1 << fi);
+                float s, co;
+                sincos_rr(e[c] * fr, s, co);
+                const float gs = gvs_[c][fi], gc = gvc_[c][fi];
+                g_wv += gs * s + gc * co;
+                ge[c] += (gs * co - gc * s) * wv * fr;
+            }
+        }
+        if (cutv) g_dist += g_wv * (-M.tau_v * wv * (1.0f - wv));
+        if (M.view_raw) {  // e = R_j d itself
+            gex = ge[0];
+            gey = ge[1];
+            gez = ge[2];
+        } else if (enr > 1e-12f) {
+            const float dot = e[0] * ge[0] + e[1] * ge[1] + e[2] * ge[2];
+            gex = (ge[0] - e[0] * dot) / enr;
+            gey = (ge[1] - e[1] * dot) / enr;
+            gez = (ge[2] - e[2] * dot) / enr;
+        } else {
+            gex = ge[0] / 1e-12f;
+            gey = ge[1] / 1e-12f;
+            gez = ge[2] / 1e-12f;
+        }
     }
     // ---- dist = |q|
     if (dist > 0.0f) {
@@ -739,4 +751,333 @@ __global__ __launch_bounds__(64) void train_importance_kernel(const float* __res
         z_all[i * T + s] = zf[s];
         if (sorted_idx) sorted_idx[i * T + s] = src[s];
     }
+}
+
+// ---- view-window layout (anerf.h ANERF_ENC_VIEW_WINDOWS): the view layer's view part sum_j w_j G_j per sample.
+// One workgroup per ray; G[ray] [NJ][WH] (NJ WH <= 4096) and the windows of VM_SC samples at a time staged in LDS,
+// lanes over (sample, 4 columns).  HBM: the windows (NJ floats per sample), G once per ray, the [WH] output row
+// per sample.
+constexpr int VM_SC = 32, VM_K = 4;  // (samples per LDS chunk; float4 dL/dG accumulators per thread)
+__global__ __launch_bounds__(256) void train_view_mix_kernel(const float* __restrict__ win, int64_t ldw, int ns, int nj,
+                                                             const float* __restrict__ G, int wh,
+                                                             float* __restrict__ out) {
+    extern __shared__ float sh[];
+    float* sG = sh;            // [nj][wh]
+    float* sW = sG + nj * wh;  // [VM_SC][nj]
+    const int64_t r = blockIdx.x;
+    const int tid = threadIdx.x, h4n = wh / 4;
+    const f32x4* g4 = reinterpret_cast<const f32x4*>(G + r * nj * wh);
+    for (int q = tid; q < nj * h4n; q += blockDim.x) reinterpret_cast<f32x4*>(sG)[q] = g4[q];
+    for (int s0 = 0; s0 < ns; s0 += VM_SC) {
+        const int sc = min(VM_SC, ns - s0);
+        __syncthreads();  // (the previous chunk's readers are done)
+        for (int q = tid; q < sc * nj; q += blockDim.x) {
+            const int s = q / nj, j = q - s * nj;
+            sW[q] = win[(r * ns + s0 + s) * ldw + j];
+        }
+        __syncthreads();
+        for (int t = tid; t < sc * h4n; t += blockDim.x) {
+            const int s = t / h4n, h4 = t - s * h4n;
+            f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+            for (int j = 0; j < nj; ++j) {
+                const float wj = sW[s * nj + j];  // (the lanes of one sample read one address)
+                const f32x4 gv = reinterpret_cast<const f32x4*>(sG)[j * h4n + h4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) acc[e] = fmaf(wj, gv[e], acc[e]);
+            }
+            reinterpret_cast<f32x4*>(out + (r * ns + s0 + s) * wh)[h4] = acc;
+        }
+    }
+}
+
+// Its gradients: dL/dw_j(s) = sum_h gz[s][h] G[j][h] (into the window columns of g_feat) and dL/dG[j][h] =
+// sum_s w_j(s) gz[s][h], per ray; samples in chunks of VM_SC through LDS.  dL/dw: lanes over samples (gz rows
+// padded by 4 floats), 4 joints per lane (G rows zero-padded to a multiple of 4 joints); dL/dG: float4 column
+// groups per lane, in registers across the chunks.
+__global__ __launch_bounds__(256) void train_view_mix_backward_kernel(const float* __restrict__ win, int64_t ldw,
+                                                                      int ns, int nj, const float* __restrict__ G,
+                                                                      int wh, const float* __restrict__ gz,
+                                                                      float* __restrict__ gwin, int64_t ldg,
+                                                                      float* __restrict__ gG) {
+    extern __shared__ float sh[];
+    const int wp = wh + 4;  // (padded row)
+    const int nj4 = (nj + 3) / 4;
+    float* sG = sh;                   // [4 nj4][wp]
+    float* sZ = sG + 4 * nj4 * wp;    // [VM_SC][wp]
+    float* sW = sZ + VM_SC * wp;      // [VM_SC][nj]
+    const int64_t r = blockIdx.x;
+    const int tid = threadIdx.x, h4n = wh / 4;
+    for (int q = tid; q < 4 * nj4 * h4n; q += blockDim.x) {
+        const int j = q / h4n, h4 = q - j * h4n;
+        const f32x4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
+        *reinterpret_cast<f32x4*>(sG + j * wp + 4 * h4) =
+            j < nj ? reinterpret_cast<const f32x4*>(G + (r * nj + j) * wh)[h4] : z4;
+    }
+    f32x4 acc[VM_K];
+#pragma unroll
+    for (int k = 0; k < VM_K; ++k) acc[k] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    for (int s0 = 0; s0 < ns; s0 += VM_SC) {
+        const int sc = min(VM_SC, ns - s0);
+        __syncthreads();  // (the previous chunk's readers are done; G is in place on the first pass)
+        for (int q = tid; q < sc * h4n; q += blockDim.x) {
+            const int s = q / h4n, h4 = q - s * h4n;
+            *reinterpret_cast<f32x4*>(sZ + s * wp + 4 * h4) =
+                reinterpret_cast<const f32x4*>(gz + (r * ns + s0 + s) * wh)[h4];
+        }
+        for (int q = tid; q < sc * nj; q += blockDim.x) {
+            const int s = q / nj, j = q - s * nj;
+            sW[q] = win[(r * ns + s0 + s) * ldw + j];
+        }
+        __syncthreads();
+        for (int q = tid; q < VM_SC * nj4; q += blockDim.x) {
+            const int s = q % VM_SC, jg = q / VM_SC;
+            if (s >= sc) continue;
+            f32x4 d[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) d[u] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+            for (int h = 0; h < wh; h += 4) {
+                const f32x4 a = *reinterpret_cast<const f32x4*>(sZ + s * wp + h);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const f32x4 b = *reinterpret_cast<const f32x4*>(sG + (4 * jg + u) * wp + h);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) d[u][e] = fmaf(a[e], b[e], d[u][e]);
+                }
+            }
+            float* gw = gwin + (r * ns + s0 + s) * ldg + 4 * jg;
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (4 * jg + u < nj) gw[u] = (d[u][0] + d[u][1]) + (d[u][2] + d[u][3]);
+        }
+#pragma unroll
+        for (int k = 0; k < VM_K; ++k) {
+            const int q = tid + 256 * k;  // (float4 group: joint q / h4n, columns 4 (q % h4n) ..)
+            if (q >= nj * h4n) break;
+            const int j = q / h4n, h = 4 * (q - j * h4n);
+            f32x4 a = acc[k];
+            for (int s = 0; s < sc; ++s) {
+                const float wj = sW[s * nj + j];
+                const f32x4 z = *reinterpret_cast<const f32x4*>(sZ + s * wp + h);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) a[e] = fmaf(wj, z[e], a[e]);
+            }
+            acc[k] = a;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < VM_K; ++k) {
+        const int q = tid + 256 * k;
+        if (q >= nj * h4n) break;
+        reinterpret_cast<f32x4*>(gG + r * nj * wh)[q] = acc[k];
+    }
+}
+
+// ---- the per-ray view factors of the view-window layout: G[r][j][h] = sum_k T_k(e_rj) Wv'[j][k][h], e_rj = R_j d_r
+// normalised (raw under --view_type world), T = [e, sin 2^m e, cos 2^m e ...] (slot f component c at k = 3 f + c),
+// Wv' the view layer's view columns (column f 3 NJ + 3 j + c) times the --freq_schedule weights.  One joint per
+// workgroup (its Wv' slice staged in LDS).
+#ifndef ANERF_VF_RAYS_B
+#define ANERF_VF_RAYS_B 128
+#endif
+constexpr int VF_RC = 64, VF_RAYS_B = ANERF_VF_RAYS_B, VF_KG = 4;  // (rays per chunk / per backward workgroup; float4
+                                                                   // dL/dWv groups per thread)
+__device__ __forceinline__ bool view_terms(const ModelDev& M, const float* __restrict__ rb, int stride, int64_t r,
+                                           const float* __restrict__ skts, const int32_t* __restrict__ ray_pose,
+                                           int n_poses, int j, float (&T)[27], float (&e)[3], float& enr,
+                                           int64_t& pose) {
+    pose = ray_pose ? ray_pose[r] : r;
+    if (pose < 0 || pose >= n_poses) return false;
+    const float* S = skts + (pose * M.nj + j) * 16;
+    const float* ray = rb + r * stride;
+    float ex, ey, ez;
+    joint_rot(S, ray[3], ray[4], ray[5], ex, ey, ez);
+    enr = norm3(ex, ey, ez);
+    const float en = M.view_raw ? 1.0f : fmaxf(enr, 1e-12f);
+    e[0] = ex / en, e[1] = ey / en, e[2] = ez / en;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        T[c] = e[c];
+#pragma unroll
+        for (int fi = 0; fi < 4; ++fi) {
+            float s = 0.0f, co = 0.0f;
+            if (fi < M.mrv) sincos_rr(e[c] * (float)(1 << fi), s, co);
+            T[3 * (1 + 2 * fi) + c] = s;
+            T[3 * (2 + 2 * fi) + c] = co;
+        }
+    }
+    return true;
+}
+
+__device__ __forceinline__ void stage_view_cols(const ModelDev& M, int j, const float* __restrict__ wv, int64_t ldv,
+                                                int wh, const float* __restrict__ fs, float* __restrict__ sw) {
+    const int nk = 3 * (1 + 2 * M.mrv);
+    for (int q = threadIdx.x; q < nk * wh; q += blockDim.x) {
+        const int k = q / wh, h = q - k * wh;
+        const int col = (k / 3) * 3 * M.nj + 3 * j + k % 3;
+        sw[q] = wv[h * ldv + col] * (fs ? fs[col] : 1.0f);
+    }
+}
+
+// Rays in chunks of VF_RC: one thread per ray forms T (LDS, padded rows of 28), the workgroup then forms the
+// chunk's [VF_RC][WH] outputs with lanes over (ray, 4 columns).
+__global__ __launch_bounds__(256) void train_view_factor_kernel(ModelDev M, const float* __restrict__ rb, int stride,
+                                                                int64_t n, const float* __restrict__ skts,
+                                                                const int32_t* __restrict__ ray_pose, int n_poses,
+                                                                const float* __restrict__ wv, int64_t ldv, int wh,
+                                                                const float* __restrict__ fs, float* __restrict__ G) {
+    extern __shared__ float sh[];
+    const int j = blockIdx.y, nj = M.nj, nk = 3 * (1 + 2 * M.mrv);
+    float* sw = sh;            // [nk][wh]
+    float* sT = sw + nk * wh;  // [VF_RC][28] (column 27: 0, or NaN for a bad pose index)
+    stage_view_cols(M, j, wv, ldv, wh, fs, sw);
+    const int tid = threadIdx.x, h4n = wh / 4;
+    const int64_t r0 = (int64_t)blockIdx.x * VF_RC;
+    if (tid < VF_RC && r0 + tid < n) {
+        float T[27], e[3], enr;
+        int64_t pose;
+        const bool ok = view_terms(M, rb, stride, r0 + tid, skts, ray_pose, n_poses, j, T, e, enr, pose);
+#pragma unroll
+        for (int k = 0; k < 27; ++k) sT[tid * 28 + k] = ok ? T[k] : 0.0f;
+        sT[tid * 28 + 27] = ok ? 0.0f : __int_as_float(0x7fc00000);
+    }
+    __syncthreads();
+    for (int q = tid; q < VF_RC * h4n; q += blockDim.x) {
+        const int rr = q / h4n, h4 = q - rr * h4n;
+        const int64_t r = r0 + rr;
+        if (r >= n) break;
+        const float bad = sT[rr * 28 + 27];
+        f32x4 acc = {bad, bad, bad, bad};
+        for (int k = 0; k < nk; ++k) {
+            const float t = sT[rr * 28 + k];
+            const f32x4 w4 = reinterpret_cast<const f32x4*>(sw)[k * h4n + h4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[e] = fmaf(t, w4[e], acc[e]);
+        }
+        reinterpret_cast<f32x4*>(G + (r * nj + j) * wh)[h4] = acc;
+    }
+}
+
+// Its gradients: dL/dskts (the rotation block of joint j, atomically added: R_j d's gradient through the
+// normalisation and the sin / cos) and dL/dWv (the view columns, atomically added once per workgroup).  Per chunk
+// of VF_RC rays: dL/dG rows and T in LDS; dL/dT (lanes over rays, 28-float rows) and the dL/dWv partial sums (float4
+// column groups per lane, in registers across the chunks); then one thread per ray maps dL/dT to dL/dR_j.
+__global__ __launch_bounds__(256) void train_view_factor_backward_kernel(
+    ModelDev M, const float* __restrict__ rb, int stride, int64_t n, const float* __restrict__ skts,
+    const int32_t* __restrict__ ray_pose, int n_poses, const float* __restrict__ wv, int64_t ldv, int wh,
+    const float* __restrict__ fs, const float* __restrict__ gG, float* __restrict__ gskts, float* __restrict__ part) {
+    extern __shared__ float sh[];
+    const int j = blockIdx.y, nj = M.nj, nk = 3 * (1 + 2 * M.mrv);
+    const int wp = wh + 4, h4n = wh / 4, tid = threadIdx.x;
+    float* sw = sh;               // [nk][wh]: Wv' (scaled)
+    float* sZ = sw + nk * wh;     // [VF_RC][wp]: dL/dG rows of the chunk
+    float* sT = sZ + VF_RC * wp;  // [VF_RC][28]: T
+    float* sg = sT + VF_RC * 28;  // [VF_RC][28]: dL/dT
+    stage_view_cols(M, j, wv, ldv, wh, fs, sw);
+    f32x4 acc[VF_KG];
+#pragma unroll
+    for (int i = 0; i < VF_KG; ++i) acc[i] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    for (int c0 = 0; c0 < VF_RAYS_B; c0 += VF_RC) {
+        const int64_t r0 = (int64_t)blockIdx.x * VF_RAYS_B + c0;
+        if (r0 >= n) break;
+        const int rc = (int)min<int64_t>(VF_RC, n - r0);
+        __syncthreads();  // (the previous chunk's readers are done)
+        float T[27], e[3], enr = 0.0f;
+        int64_t pose = 0;
+        bool ok = false;
+        if (tid < rc) {
+            ok = view_terms(M, rb, stride, r0 + tid, skts, ray_pose, n_poses, j, T, e, enr, pose);
+#pragma unroll
+            for (int k = 0; k < 27; ++k) sT[tid * 28 + k] = ok ? T[k] : 0.0f;  // (no gradient for a bad pose)
+        }
+        for (int q = tid; q < rc * h4n; q += blockDim.x) {
+            const int rr = q / h4n, h4 = q - rr * h4n;
+            *reinterpret_cast<f32x4*>(sZ + rr * wp + 4 * h4) =
+                reinterpret_cast<const f32x4*>(gG + ((r0 + rr) * nj + j) * wh)[h4];
+        }
+        __syncthreads();
+        // dL/dT[rr][k] = sum_h gG[rr][h] Wv'[k][h]: lanes over the rays, Wv' rows broadcast
+        for (int q = tid; q < VF_RC * nk; q += blockDim.x) {
+            const int rr = q % VF_RC, k = q / VF_RC;
+            if (rr >= rc) continue;
+            f32x4 d = {0.0f, 0.0f, 0.0f, 0.0f};
+            for (int h = 0; h < wh; h += 4) {
+                const f32x4 a = *reinterpret_cast<const f32x4*>(sZ + rr * wp + h);
+                const f32x4 b = *reinterpret_cast<const f32x4*>(sw + k * wh + h);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) d[u] = fmaf(a[u], b[u], d[u]);
+            }
+            sg[rr * 28 + k] = (d[0] + d[1]) + (d[2] + d[3]);
+        }
+        // dL/dWv'[k][h] += sum_rr T[rr][k] gG[rr][h]
+#pragma unroll
+        for (int i = 0; i < VF_KG; ++i) {
+            const int g = tid + 256 * i;
+            if (g < nk * h4n) {
+                const int k = g / h4n, h4 = g - k * h4n;
+                f32x4 a = acc[i];
+                for (int rr = 0; rr < rc; ++rr) {
+                    const float t = sT[rr * 28 + k];
+                    const f32x4 z = *reinterpret_cast<const f32x4*>(sZ + rr * wp + 4 * h4);
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) a[u] = fmaf(t, z[u], a[u]);
+                }
+                acc[i] = a;
+            }
+        }
+        __syncthreads();
+        if (tid < rc && ok) {  // dT/de (f = 0 the identity, sin / cos of 2^m e), the normalisation, x = R_j d
+            float gT[27];
+#pragma unroll
+            for (int k = 0; k < 27; ++k) gT[k] = k < nk ? sg[tid * 28 + k] : 0.0f;
+            float ge[3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                ge[c] = gT[c];
+#pragma unroll
+                for (int fi = 0; fi < 4; ++fi) {
+                    const float fr = (float)(1 << fi);
+                    const float s = T[3 * (1 + 2 * fi) + c], co = T[3 * (2 + 2 * fi) + c];
+                    if (fi < M.mrv) ge[c] += (gT[3 * (1 + 2 * fi) + c] * co - gT[3 * (2 + 2 * fi) + c] * s) * fr;
+                }
+            }
+            float gx[3];
+            if (M.view_raw) {
+                gx[0] = ge[0], gx[1] = ge[1], gx[2] = ge[2];
+            } else if (enr > 1e-12f) {
+                const float dot = e[0] * ge[0] + e[1] * ge[1] + e[2] * ge[2];
+#pragma unroll
+                for (int c = 0; c < 3; ++c) gx[c] = (ge[c] - e[c] * dot) / enr;
+            } else {
+#pragma unroll
+                for (int c = 0; c < 3; ++c) gx[c] = ge[c] / 1e-12f;
+            }
+            const float* ray = rb + (r0 + tid) * stride;
+            float* gs = gskts + (pose * nj + j) * 16;
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+#pragma unroll
+                for (int b = 0; b < 3; ++b) atomicAdd(gs + 4 * c + b, gx[c] * ray[3 + b]);
+        }
+    }
+    // the workgroup's dL/dWv' partial sums, part[blockIdx.x][j][k][h] (summed by train_view_factor_reduce_kernel)
+    f32x4* pp = reinterpret_cast<f32x4*>(part + ((int64_t)blockIdx.x * nj + j) * nk * wh);
+#pragma unroll
+    for (int i = 0; i < VF_KG; ++i) {
+        const int g = tid + 256 * i;
+        if (g < nk * h4n) pp[g] = acc[i];
+    }
+}
+
+// dL/dWv[h][col(k, j)] += fs[col] sum_b part[b][j][k][h]: one thread per (j, k, h), the nb partial sums in order
+__global__ __launch_bounds__(256) void train_view_factor_reduce_kernel(const float* __restrict__ part, int nb, int nj,
+                                                                       int nk, int wh, const float* __restrict__ fs,
+                                                                       float* __restrict__ gwv, int64_t ldv) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t per = (int64_t)nj * nk * wh;
+    if (q >= per) return;
+    const int j = (int)(q / (nk * wh)), k = (int)(q / wh % nk), h = (int)(q % wh);
+    float v = 0.0f;
+    for (int b = 0; b < nb; ++b) v += part[b * per + q];
+    const int col = (k / 3) * 3 * nj + 3 * j + k % 3;
+    gwv[h * ldv + col] += v * (fs ? fs[col] : 1.0f);  // (one thread per element)
 }

@@ -93,6 +93,7 @@ struct ModelDev {
     // bone_win: the bone embedder is a CutoffEmbedder (--cutoff_bones + use_cutoff: windows its sin / cos)
     int mrb, kp_relpos, view_angle, bone_win, staged;
     int kp_query;  // --kp_dist_type querypts: the world point as the kp input (cutoff[0..2] its 3 cutoffs)
+    int view_win;  // ANERF_ENC_VIEW_WINDOWS: the training layout's view part is the NJ view windows (anerf.h)
     // fp16x4 / fp16x3: the encoder-fed parts (bone-direction and windowed x parts of layer 0 and the skip
     // layer) as fp16 splits too, when every windowed feature is bounded (sparse windows, tau > 0; host:
     // enc16_units in anerf_pack.hpp); bf16x6 parts otherwise

@@ -124,13 +124,27 @@ def wgrad(m, n, k, dy, x, dw, db, ws, dev, prec=6):
                "anerf_mlp_wgrad")
 
 
+def _view_mix(feat, dnet, nwin, G):
+    """sum_j w_j(sample) G_j(ray) [M, W/2]: the view part of the view layer's pre-activation in the view-window
+    layout (anerf.h ANERF_ENC_VIEW_WINDOWS; feat columns dnet.. are the NJ windows, G [rays, NJ, W/2] contiguous),
+    anerf_train_view_mix."""
+    n, _, wh = G.shape
+    M = feat.shape[0]
+    out = torch.empty(M, wh, device=feat.device, dtype=torch.float32)
+    _lib.check(_lib.load().anerf_train_view_mix(n, M // n, nwin, wh, feat.data_ptr() + 4 * dnet, feat.stride(0),
+                                                _lib.ptr(G), _lib.ptr(out), _stream(feat.device)),
+               "anerf_train_view_mix")
+    return out
+
+
 class _MLP(torch.autograd.Function):
     """raw [M, 4] = NeRF(feat [M, F] (, codes [M, C])); params = the module's tensors in the order of
-    `NeRF.mlp_params()`."""
+    `NeRF.mlp_params()`.  G [rays, NJ, W/2] (view-window layout, shape's nwin = NJ): the view layer's view
+    part is sum_j w_j G_j (_view_mix) instead of a product with view columns (nv = 0 then)."""
 
     @staticmethod
-    def forward(ctx, shape, feat, codes, *params):
-        W, D, skip, dnet, nv, prec, _ = shape
+    def forward(ctx, shape, feat, codes, G, *params):
+        W, D, skip, dnet, nv, prec, _, nwin = shape
         dev = feat.device
         M, F = feat.shape
         nl = D
@@ -142,12 +156,13 @@ class _MLP(torch.autograd.Function):
         whead = torch.cat([wf, wa]).contiguous()
         cfc = 0 if codes is None else codes.shape[1]
         f32 = dict(device=dev, dtype=torch.float32)
-        if _FUSED and prec == 6 and W in (128, 256) and dnet % 4 == 0 and nv % 4 == 0 and cfc % 4 == 0:
+        if _FUSED and prec == 6 and W in (128, 256) and dnet % 4 == 0 and nv % 4 == 0 and cfc % 4 == 0 and not nwin:
             H, hf, g, raw = _fused_forward(feat, codes, pw, pb, wa, ba, wf, bf, wv, bv, wr, br, W, D, skip, dnet, nv,
                                            cfc, dev)
             ctx.shape = shape
             ctx.has_codes = codes is not None
-            ctx.save_for_backward(feat, codes if codes is not None else torch.empty(0), hf, g, whead, *H, *params)
+            ctx.save_for_backward(feat, codes if codes is not None else torch.empty(0), torch.empty(0), hf, g, whead,
+                                  *H, *params)
             return raw
         # fp16x4 forward (prec 4): the GEMMs whose input is one hidden layer's output run as fp16x4
         # with that layer's row maxima (written by its GEMM's epilogue); layer 0, the skip layer's
@@ -181,27 +196,33 @@ class _MLP(torch.autograd.Function):
              [(hf, W, W, 0, None, False), (raw, 4, 1, 3, None, False)], dev, hp,
              rin=rm[D - 1] if hp == ANERF_MLP_FP16X4 else None)
         prec = op_  # (the view and rgb layers)
-        # views_linears[0] on cat([feature, views(, framecode)]), relu
-        av = [_seg(hf, W), _seg(feat, nv, dnet)] + ([_seg(codes, cfc)] if cfc else [])
-        g = torch.empty(M, W // 2, **f32)
-        mm(M, W // 2, W + nv + cfc, av, sp[D + 1], bv, True, [(g, W // 2, W // 2, 0, None, False)], dev)
+        # views_linears[0] on cat([feature, views(, framecode)]), relu; view windows: the GEMM (no relu)
+        # accumulated onto sum_j w_j G_j, then the relu
+        av = [_seg(hf, W)] + ([_seg(feat, nv, dnet)] if nv else []) + ([_seg(codes, cfc)] if cfc else [])
+        if nwin:
+            G = G.contiguous()
+        g = _view_mix(feat, dnet, nwin, G) if nwin else torch.empty(M, W // 2, **f32)
+        mm(M, W // 2, W + nv + cfc, av, sp[D + 1], bv, not nwin, [(g, W // 2, W // 2, 0, None, bool(nwin))], dev)
+        if nwin:
+            g.relu_()
         # rgb_linear into raw[:, :3]
         mm(M, 3, W // 2, [_seg(g, W // 2)], sp[D + 2], br, False, [(raw, 4, 3, 0, None, False)], dev)
         ctx.shape = shape
         ctx.has_codes = codes is not None
-        ctx.save_for_backward(feat, codes if codes is not None else torch.empty(0), hf, g, whead, *H, *params)
+        ctx.save_for_backward(feat, codes if codes is not None else torch.empty(0), G if nwin else torch.empty(0), hf,
+                              g, whead, *H, *params)
         return raw
 
     @staticmethod
     def backward(ctx, g_raw):
-        W, D, skip, dnet, nv, _, prec = ctx.shape  # (the backward's own arithmetic)
+        W, D, skip, dnet, nv, _, prec, nwin = ctx.shape  # (the backward's own arithmetic)
 
         def mm(*a):
             gemm(*a, prec=prec)
         saved = ctx.saved_tensors
-        feat, codes, hf, g, whead = saved[:5]
-        H = saved[5:5 + D]
-        params = saved[5 + D:]
+        feat, codes, G, hf, g, whead = saved[:6]
+        H = saved[6:6 + D]
+        params = saved[6 + D:]
         codes = codes if ctx.has_codes else None
         nl = D
         pw = params[0:2 * nl:2]
@@ -252,15 +273,26 @@ class _MLP(torch.autograd.Function):
         gha[:, W + 1:].zero_()  # (read as the ragged last 4-column group; the B planes are zero there)
         gfeat = torch.empty(M, F, **f32) if need_feat else None
         gcodes = torch.empty(M, cfc, **f32) if need_codes else None
-        outs = [(gha, W + 4, W, 0, None, False), (gfeat, F, nv, dnet, None, False)]
-        if cfc:
-            outs.append((gcodes, cfc, cfc, 0, None, False))
-        nvo = W + (nv + cfc if (need_feat or need_codes) else 0)
-        mm(M, nvo, W // 2, [_seg(gzv, W // 2)], st[D + 1], None, False,
-             outs if nvo > W else outs[:1], dev)
-        av = [_seg(hf, W), _seg(feat, nv, dnet)] + ([_seg(codes, cfc)] if cfc else [])
+        outs = [(gha, W + 4, W, 0, None, False)]
+        if need_feat or need_codes:  # (the output columns in order [feature | views | framecode])
+            if nv:
+                outs.append((gfeat, F, nv, dnet, None, False))
+            if cfc:
+                outs.append((gcodes, cfc, cfc, 0, None, False))
+        nvo = W + sum(o[2] for o in outs[1:])
+        mm(M, nvo, W // 2, [_seg(gzv, W // 2)], st[D + 1], None, False, outs, dev)
+        av = [_seg(hf, W)] + ([_seg(feat, nv, dnet)] if nv else []) + ([_seg(codes, cfc)] if cfc else [])
         grads[2 * nl + 4], grads[2 * nl + 5] = wg(W // 2, W + nv + cfc, gzv, av,
                                                   (hf, feat) + ((codes,) if cfc else ()))
+        gG = None
+        if nwin:  # the windows' gradient sum_h gzv G_j (into gfeat's window columns), and G's sum_s w_j gzv
+            n = G.shape[0]
+            gG = torch.empty_like(G)
+            gw, off = (gfeat, dnet) if need_feat else (torch.empty(M, nwin, **f32), 0)
+            _lib.check(lib.anerf_train_view_mix_backward(n, M // n, nwin, W // 2, feat.data_ptr() + 4 * dnet,
+                                                         feat.stride(0), _lib.ptr(G), _lib.ptr(gzv),
+                                                         gw.data_ptr() + 4 * off, gw.stride(0), _lib.ptr(gG),
+                                                         _stream(dev)), "anerf_train_view_mix_backward")
         # feature_linear + alpha_linear: one input gradient, masked by relu(last hidden) > 0
         gz = torch.empty(M, W, **f32)
         mm(M, W, W + 1, [_seg(gha, W + 1)], st[D], None, False,
@@ -296,7 +328,7 @@ class _MLP(torch.autograd.Function):
             gz = gprev
         if side is not None:
             main.wait_stream(side)
-        return (None, gfeat, gcodes, *grads)
+        return (None, gfeat, gcodes, gG if ctx.needs_input_grad[3] else None, *grads)
 
 
 def _fused_forward(feat, codes, pw, pb, wa, ba, wf, bf, wv, bv, wr, br, W, D, skip, dnet, nv, cfc, dev):
@@ -337,9 +369,9 @@ def _fused_forward(feat, codes, pw, pb, wa, ba, wf, bf, wv, bv, wr, br, W, D, sk
 MODES = {"bf16x6": (6, 6), "bf16x3": (3, 3), "mixed": (6, 3), "mixed16": (4, 3)}
 
 
-def nerf_forward(net, feat, codes=None):
+def nerf_forward(net, feat, codes=None, G=None):
     """raw [M, 4] of `train.NeRF` on the split-bf16 GEMMs (same parameters, autograd included;
-    precision net.mlp: "bf16x6" or "bf16x3")."""
+    precision net.mlp: "bf16x6" or "bf16x3").  G: the view-window layout's per-ray view factors (_MLP)."""
     cfg = net.cfg
     if feat.dtype != torch.float32 or not feat.is_contiguous():
         feat = feat.float().contiguous()
@@ -354,10 +386,18 @@ def nerf_forward(net, feat, codes=None):
         params += [lin.weight, lin.bias]
     params += [net.alpha_linear.weight, net.alpha_linear.bias, net.feature_linear.weight, net.feature_linear.bias,
                net.views_linears[0].weight, net.views_linears[0].bias, net.rgb_linear.weight, net.rgb_linear.bias]
-    if dnet % 4 or nv % 4 or feat.shape[1] % 4:
+    nwin = 0
+    if G is not None:  # (the view columns of views_linears.0 entered G: the GEMM's weight is [feature | framecode])
+        nwin = G.shape[1]
+        wv = params[2 * D + 4]
+        params[2 * D + 4] = torch.cat([wv[:, :W], wv[:, W + nv:]], 1)
+        nv = 0
+        if dnet % 4 or feat.shape[1] % 4:
+            raise ValueError("view-window layout: the kp + bone columns and the row width must be multiples of 4")
+    elif dnet % 4 or nv % 4 or feat.shape[1] % 4:
         feat, params, dnet, nv = _pad_to_segments(feat, params, W, D, skip, dnet, nv)
-    shape = (W, D, skip, dnet, nv, fwd, bwd)
-    return _MLP.apply(shape, feat, codes, *params)
+    shape = (W, D, skip, dnet, nv, fwd, bwd, nwin)
+    return _MLP.apply(shape, feat, codes, G, *params)
 
 
 def _ceil4(x):

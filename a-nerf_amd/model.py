@@ -25,7 +25,9 @@ def _np(x):
 class DeviceModel:
     """Owns one `anerf_model*` on one GPU."""
 
-    def __init__(self, cfg, ckpt, device=None):
+    def __init__(self, cfg, ckpt, device=None, view_windows=False):
+        """view_windows: the training stages' view-window layout (anerf.h ANERF_ENC_VIEW_WINDOWS; the trainable
+        TrainRayCaster's own model)."""
         cfg.validate()
         self.cfg = cfg
         lib = _lib.load()
@@ -59,7 +61,9 @@ class DeviceModel:
                            (_lib.ANERF_ENC_VIEW_RAW if cfg.extra.get("view_type", "relray") == "world" else 0) |
                            (_lib.ANERF_ENC_KP_RELPOS if cfg.kp_relpos else 0) |
                            (_lib.ANERF_ENC_VIEW_ANGLE if cfg.view_angle else 0) |
-                           (_lib.ANERF_ENC_KP_QUERYPTS if cfg.kp_query else 0))
+                           (_lib.ANERF_ENC_KP_QUERYPTS if cfg.kp_query else 0) |
+                           (_lib.ANERF_ENC_VIEW_WINDOWS if view_windows else 0))
+        self.view_windows = bool(view_windows)
         d.multires_bones = cfg.multires_bones
         # (the C side windows the bare bone directions under the reference's condition, cutoff_inputs too:
         # anerf.h, ANERF_ENC_CUTOFF_BONES)

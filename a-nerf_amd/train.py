@@ -39,7 +39,8 @@ class _Encode(torch.autograd.Function):
     def forward(ctx, skts, model, rb, z, ray_pose, pts_noise=None):
         n, ns = z.shape
         cfg = model.cfg
-        F_ = cfg.feature_dim
+        # (the view-window layout: the view part is the NJ windows, anerf.h ANERF_ENC_VIEW_WINDOWS)
+        F_ = cfg.input_ch + cfg.input_ch_bones + cfg.n_joints if model.view_windows else cfg.feature_dim
         feat = torch.empty(n * ns, F_, device=z.device, dtype=torch.float32)
         n_poses = skts.shape[0]
         _lib.check(_lib.load().anerf_train_encode(model.handle, _lib.ptr(rb), rb.shape[1], n, _lib.ptr(z), ns,
@@ -285,12 +286,14 @@ class NeRF(nn.Module):
     # torch GEMMs
     mlp = "mixed"
 
-    def forward(self, feat, cams=None):
-        """feat [M, F] = [v | r | views] -> raw [M, 4] (rgb, alpha): forward_density + forward_view."""
+    def forward(self, feat, cams=None, G=None):
+        """feat [M, F] = [v | r | views] -> raw [M, 4] (rgb, alpha): forward_density + forward_view.  G [rays, NJ,
+        W/2] (view_factor): feat is in the view-window layout [v | r | w] (the NJ view windows) and the view
+        layer's view part is sum_j w_j G_j."""
         if self.mlp in ("mixed", "mixed16", "bf16x6", "bf16x3"):
             from . import mlp as _mlp
             codes = self.framecodes(cams) if self.cfg.opt_framecode else None
-            return _mlp.nerf_forward(self, feat, codes)
+            return _mlp.nerf_forward(self, feat, codes, G)
         if self.mlp != "fp32":
             raise ValueError(f"mlp={self.mlp!r}: 'mixed', 'mixed16', 'bf16x6', 'bf16x3' or 'fp32'")
         x, x_skip, views = _SplitCols.apply(feat, self.dnet)
@@ -305,7 +308,13 @@ class NeRF(nn.Module):
         W = feature.shape[1]
         vl = self.views_linears[0]
         nv = self.cfg.input_ch_views
-        if self.cfg.opt_framecode:
+        if G is not None:
+            n = G.shape[0]
+            g = _lin(feature, vl.weight[:, :W], vl.bias) + torch.bmm(views.reshape(n, -1, G.shape[1]), G).reshape(-1, W // 2)
+            if self.cfg.opt_framecode:
+                g = g + _lin(self.framecodes(cams), vl.weight[:, W + nv:])
+            g = F.relu(g)
+        elif self.cfg.opt_framecode:
             g = _Linear2.apply(feature, vl.weight[:, :W], views, vl.weight[:, W:W + nv], vl.bias)
             g = F.relu(g + _lin(self.framecodes(cams), vl.weight[:, W + nv:]))
         else:
@@ -376,6 +385,54 @@ class _Embed(nn.Module):
         new = (self.init_tau * torch.ones((), dtype=self.tau.dtype) * rate ** (global_step / float(step * 1000))).clamp(
             max=2000.)
         self._set("tau", new)
+
+
+def view_windows_ok(cfg):
+    """The view-window layout (anerf.h ANERF_ENC_VIEW_WINDOWS) holds for this configuration: every view feature is
+    a window times a function of the ray (cutoff_viewdir and cutoff_inputs, relray / world directions), and the
+    GEMM segments stay 16-byte aligned without padding, and the per-ray factors G fit anerf_train_view_mix's LDS plan
+    (NJ W / 2 <= 4096)."""
+    dnet = cfg.input_ch + cfg.input_ch_bones
+    return (cfg.cutoff_viewdir and cfg.cutoff_inputs and not cfg.view_angle and not cfg.staged and dnet % 4 == 0
+            and (dnet + cfg.n_joints) % 4 == 0 and cfg.n_joints * (cfg.netwidth // 2) <= 4096)
+
+
+class _ViewFactor(torch.autograd.Function):
+    """G [rays, NJ, W/2]: the per-ray view factors of the view-window layout (anerf_train_view_factor; anerf.h
+    ANERF_ENC_VIEW_WINDOWS) -- joint j's view features without their window times the view layer's view columns
+    (times the --freq_schedule weights fs [input_ch_views] or None); backward -> dL/dskts, dL/d(views_linears.0.weight)."""
+
+    @staticmethod
+    def forward(ctx, skts, weight, model, rb, fs):
+        n = rb.shape[0]
+        cfg = model.cfg
+        W = cfg.netwidth
+        G = torch.empty(n, cfg.n_joints, W // 2, device=rb.device, dtype=torch.float32)
+        _lib.check(_lib.load().anerf_train_view_factor(model.handle, _lib.ptr(rb), rb.shape[1], n, _lib.ptr(skts),
+                                                       skts.shape[0], None, weight.data_ptr() + 4 * W,
+                                                       weight.stride(0), W // 2, _lib.ptr(fs), _lib.ptr(G),
+                                                       _stream(rb.device)), "anerf_train_view_factor")
+        ctx.model = model
+        ctx.save_for_backward(skts, weight, rb, fs if fs is not None else torch.empty(0))
+        ctx.has_fs = fs is not None
+        return G
+
+    @staticmethod
+    def backward(ctx, gG):
+        skts, weight, rb, fs = ctx.saved_tensors
+        W = ctx.model.cfg.netwidth
+        gs, gw = torch.zeros_like(skts), torch.zeros_like(weight)
+        cfg = ctx.model.cfg
+        lib = _lib.load()
+        need = lib.anerf_train_view_factor_workspace(rb.shape[0], cfg.n_joints, cfg.multires_views, W // 2)
+        ws = torch.empty(max(need, 16), device=rb.device, dtype=torch.uint8)
+        _lib.check(lib.anerf_train_view_factor_backward(
+            ctx.model.handle, _lib.ptr(rb), rb.shape[1], rb.shape[0], _lib.ptr(skts), skts.shape[0], None,
+            weight.data_ptr() + 4 * W, weight.stride(0), W // 2, _lib.ptr(fs if ctx.has_fs else None),
+            _lib.ptr(gG.contiguous()), _lib.ptr(gs), gw.data_ptr() + 4 * W, _lib.ptr(ws), ws.numel(),
+            _stream(rb.device)),
+            "anerf_train_view_factor_backward")
+        return (gs if ctx.needs_input_grad[0] else None), (gw if ctx.needs_input_grad[1] else None), None, None, None
 
 
 class TrainRayCaster(nn.Module):
@@ -518,9 +575,15 @@ class TrainRayCaster(nn.Module):
             model.set_embed(e, ev, cutoffs=v[1] != seen[1], embedbones_sd=eb)
         return v
 
+    # the training stages' view-window layout where the configuration allows it (view_windows_ok): the encoder
+    # writes NJ windows instead of 3 NJ (1 + 2 multires_views) view features, the view layer reads them through the
+    # per-ray factors G (view_factor); False: the full view columns
+    view_windows = True
+
     def _constants(self):
         if self._consts is None:
-            self._consts = DeviceModel(self.cfg, self.checkpoint(), device=self._dev.index)
+            self._consts = DeviceModel(self.cfg, self.checkpoint(), device=self._dev.index,
+                                       view_windows=self.view_windows and view_windows_ok(self.cfg))
             self._consts_embed = self._embed_version()
         else:
             self._consts_embed = self._sync_embed(self._consts, self._consts_embed)
@@ -626,13 +689,19 @@ class TrainRayCaster(nn.Module):
             return (g * ray_noise_std).contiguous()
 
         fscale = self._feature_scale()
+        fs_view = None
+        if model.view_windows and fscale is not None:  # (the view columns' schedule weights go into G)
+            dnet = cfg.input_ch + cfg.input_ch_bones
+            fs_view = fscale[dnet:].contiguous()
+            fscale = torch.cat([fscale[:dnet], fscale.new_ones(nj)])
 
         def raw_of(net, zz, pn=None):
             ns = zz.shape[1]
             feat = _Encode.apply(sk, model, rb, zz, None, pn)
             if fscale is not None:  # (embedded * get_schedule_w(), cutoff_embedder.py:150; autograd scales dL/dfeat)
                 feat = feat * fscale
-            return net(feat, None if cam_t is None else cam_t.repeat_interleave(ns)).reshape(n, ns, 4)
+            G = _ViewFactor.apply(sk, net.views_linears[0].weight, model, rb, fs_view) if model.view_windows else None
+            return net(feat, None if cam_t is None else cam_t.repeat_interleave(ns), G).reshape(n, ns, 4)
 
         def composite(raw, zz, noise):
             return _Composite.apply(raw, model, zz, rb, noise)

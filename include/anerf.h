@@ -37,6 +37,9 @@
  *   anerf_train_composite   NeRF.raw2outputs with raw_noise_std                core/networks/nerf.py:150-205
  *   anerf_train_composite_backward   its autograd
  *   anerf_train_importance  isample_from_lineseg + sample_pdf(det=False) + sort core/utils/ray_utils.py:157-201, 255-289
+ *   anerf_train_view_factor (+ _backward)   per-ray view factors of the view-window layout
+ *   anerf_train_view_mix (+ _backward)   the view layer's view part in the view-window layout
+ *                           (ANERF_ENC_VIEW_WINDOWS; views_linears.0 on the view columns, core/networks/nerf.py:141-148)
  * The training MLP's linears (NeRF.forward / autograd, core/networks/nerf.py:94-148; the reference runs
  * them as torch addmm over cat()-ed inputs, core/raycasters.py:557-577):
  *   anerf_mlp_split_weights a weight (or its transpose) as bf16 hi / lo planes, once per step
@@ -55,7 +58,7 @@
 extern "C" {
 #endif
 
-#define ANERF_ABI_VERSION 15
+#define ANERF_ABI_VERSION 16
 
 enum {
     ANERF_OK = 0,
@@ -184,6 +187,15 @@ typedef struct {
  * gradient reaches skts through it.  Not with ANERF_ENC_CUTOFF_BONES (the reference's bone CutoffEmbedder then
  * gets cutoff_dim 3 for 3 NJ inputs and fails). */
 #define ANERF_ENC_KP_QUERYPTS 64
+/* Training layout of the view part (ABI 16; anerf_train_encode / _encode_backward only, the other entry points
+ * ignore the flag): the view part of a feature row is the NJ view windows w_j = 1 - sigmoid(tau_v (dist_j - c_v,j))
+ * (column cv + j, cv = the view part's first column) instead of the 3 NJ (1 + 2 multires_views) windowed
+ * direction features.  Every one of those features is w_j times a function of the ray alone (R_j d), so the
+ * view layer's product with them is sum_j w_j G_j(ray) with G_j = Wv_j T_j(R_j d) per ray: the caller forms
+ * T, G and that sum (the view direction's gradient to skts included) and the encoder handles the windows
+ * (their gradient in _encode_backward's g_feat column cv + j).  Needs cutoff_viewdir and cutoff_inputs (every
+ * direction feature windowed); not with ANERF_ENC_VIEW_ANGLE or a staged encoder. */
+#define ANERF_ENC_VIEW_WINDOWS 128
 
 /* HOST pointers to one NeRF's weights, torch nn.Linear layout [out][in] (core/networks/nerf.py:57-88). */
 typedef struct {
@@ -428,6 +440,40 @@ int anerf_train_composite_backward(const anerf_model* m, const float* raw, const
 int anerf_train_importance(const float* z, const float* weights, int64_t n_rays, int32_t n_samples,
                            int32_t n_importance, const float* u, int32_t single_net, float* z_all,
                            int32_t* sorted_idx, void* stream);
+
+/* The view-window layout's per-ray view factors (ABI 16, ANERF_ENC_VIEW_WINDOWS): G [N][NJ][width] with
+ * G[r][j][h] = sum_{f, c} T_fc(e_rj) weight[h ld_weight + f 3 NJ + 3 j + c] col_scale[f 3 NJ + 3 j + c], e_rj = R_j d_r
+ * normalised (R_j d_r itself under ANERF_ENC_VIEW_RAW), T_0c = e_c, T_{2m+1,c} / T_{2m+2,c} = sin / cos (2^m e_c),
+ * m < multires_views: joint j's view features without their window (encode_inputs' view part,
+ * core/raycasters.py:476-555, core/encoders.py:172-193).  weight points at the view layer's first view column
+ * (views_linears.0.weight + W, row stride ld_weight); col_scale (the --freq_schedule weights of the view columns) may
+ * be NULL.  Skeletons as anerf_train_encode (ray_pose NULL: one per ray).  width <= 128; not for ray-angle views. */
+int anerf_train_view_factor(const anerf_model* m, const float* ray_batch, int32_t ray_stride, int64_t n_rays,
+                            const float* skts, int32_t n_poses, const int32_t* ray_pose, const float* weight,
+                            int64_t ld_weight, int32_t width, const float* col_scale, float* G, void* stream);
+/* Its gradients from grad_G: ADDED into grad_skts [n_poses][NJ][4][4] (the rotation blocks, atomically) and into
+ * grad_weight (the view columns, the same layout as weight; no other writer on the stream meanwhile).  workspace:
+ * device scratch of anerf_train_view_factor_workspace() bytes (16-byte aligned; the per-workgroup partial sums of the
+ * weight gradient, reduced in order by a second launch). */
+size_t anerf_train_view_factor_workspace(int64_t n_rays, int32_t n_joints, int32_t multires_views, int32_t width);
+int anerf_train_view_factor_backward(const anerf_model* m, const float* ray_batch, int32_t ray_stride, int64_t n_rays,
+                                     const float* skts, int32_t n_poses, const int32_t* ray_pose, const float* weight,
+                                     int64_t ld_weight, int32_t width, const float* col_scale, const float* grad_G,
+                                     float* grad_skts, float* grad_weight, void* workspace, size_t workspace_bytes,
+                                     void* stream);
+
+/* The view-window layout's view part (ABI 16, ANERF_ENC_VIEW_WINDOWS): out [N S][width] = sum_j w_j G_j, the NJ
+ * windows w of sample s of ray r at windows + (r S + s) ld_windows (the window columns of an anerf_train_encode
+ * row) and G [N][NJ][width] the ray's view factors (the view layer's view columns times the ray's direction
+ * terms, per joint).  width % 4 == 0, NJ width <= 4096, G and out 16-byte aligned.  In the reference this is
+ * part of views_linears.0's product with the view features (core/networks/nerf.py:141-148). */
+int anerf_train_view_mix(int64_t n_rays, int32_t n_samples, int32_t n_joints, int32_t width, const float* windows,
+                         int64_t ld_windows, const float* G, float* out, void* stream);
+/* Its gradients from grad_out [N S][width]: grad_windows (r S + s) ld_grad_windows + j = sum_h grad_out G_j (written),
+ * grad_G [N][NJ][width] = sum_s w_j grad_out (written). */
+int anerf_train_view_mix_backward(int64_t n_rays, int32_t n_samples, int32_t n_joints, int32_t width,
+                                  const float* windows, int64_t ld_windows, const float* G, const float* grad_out,
+                                  float* grad_windows, int64_t ld_grad_windows, float* grad_G, void* stream);
 
 /* ---- training MLP linears on the bf16 MFMA pipe, fp32 in / out with split-bf16 operands:
  *   ANERF_MLP_BF16X6  x = x0 + x1 + x2, w likewise, the six products with i + j <= 2 (fp32-accurate:

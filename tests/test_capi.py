@@ -31,7 +31,8 @@ def test_header_declares_expected_entry_points():
               "anerf_train_encode_backward", "anerf_train_composite", "anerf_train_composite_backward",
               "anerf_train_importance", "anerf_pose_kinematics_backward", "anerf_ray_batch", "anerf_gather_rows",
               "anerf_mlp_split_bytes", "anerf_mlp_split_weights", "anerf_mlp_split_weights_batch", "anerf_mlp_gemm", "anerf_mlp_wgrad_workspace",
-              "anerf_mlp_wgrad"):
+              "anerf_mlp_wgrad", "anerf_train_view_mix", "anerf_train_view_mix_backward",
+              "anerf_train_view_factor", "anerf_train_view_factor_backward", "anerf_train_view_factor_workspace"):
         assert f in fns
 
 
@@ -101,3 +102,13 @@ def test_build_discards_a_library_whose_sources_moved(tmp_path, monkeypatch):
     monkeypatch.setattr(b, "source_hash", lambda: "c")
     assert b.build(force=True, verbose=False) == out and os.path.exists(out)
     assert open(out + ".stamp").read().strip() == "c"
+
+
+def test_view_mix_rejects_bad_shapes():
+    """anerf_train_view_mix validates before any HIP call (anerf.h: width % 4 == 0, NJ width <= 4096, ld >= NJ)."""
+    lib = _lib.load()
+    assert lib.anerf_train_view_mix(1, 1, 24, 130, 1, 24, 16, 16, None) == -1
+    assert lib.anerf_train_view_mix(1, 1, 64, 128, 1, 64, 16, 16, None) == -1
+    assert lib.anerf_train_view_mix(1, 1, 24, 128, 1, 20, 16, 16, None) == -1
+    assert b"anerf_train_view_mix" in lib.anerf_last_error()
+    assert lib.anerf_train_view_mix_backward(1, 1, 24, 128, 1, 24, 16, 16, None, 24, 16, None) == -1

@@ -42,10 +42,11 @@ def _loss(out, tgt, bg):
             F.mse_loss(out["rgb0"] + (1 - out["acc0"])[:, None] * bg, tgt))
 
 
-def _run(name, mlp="mixed"):
+def _run(name, mlp="mixed", view_windows=True):
     g = Golden(name)
     m = g.meta
     tr = train.TrainRayCaster(g.cfg, g.ckpt, mlp=mlp).train()
+    tr.view_windows = view_windows  # (the view-window layout where the configuration allows it, anerf.h)
     dev = torch.device("cuda:0")
     if m.get("global_step") is not None:
         # Trainer.train_batch's call (core/trainer.py:263-265), through the DataParallel-style alias
@@ -65,13 +66,15 @@ def _run(name, mlp="mixed"):
     loss = _loss(out, c("target"), c("bg"))
     loss.backward()
     torch.cuda.synchronize()
+    assert tr.model.view_windows == (view_windows and train.view_windows_ok(g.cfg))
     return g, tr, sk, out, loss
 
 
 # the training MLP on the hand-written split-bf16 GEMMs (mixed — the default —, mixed16 and bf16x6) and on
-# torch's fp32 GEMMs
-@pytest.fixture(scope="module", params=[(n, mlp) for n in TRAIN for mlp in ("mixed", "mixed16", "bf16x6", "fp32")],
-                ids=lambda p: f"{p[0]}-{p[1]}")
+# torch's fp32 GEMMs; the view-window layout (the default where it applies) and the full view columns
+@pytest.fixture(scope="module", params=[(n, mlp, vw) for n in TRAIN for mlp in ("mixed", "mixed16", "bf16x6", "fp32")
+                                        for vw in (True, False) if vw or mlp in ("mixed", "fp32")],
+                ids=lambda p: f"{p[0]}-{p[1]}" + ("" if p[2] else "-fullview"))
 def run(request):
     return _run(*request.param)
 

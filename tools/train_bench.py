@@ -38,6 +38,8 @@ def parser():
                     help="training MLP arithmetic (train.TrainRayCaster mlp=)")
     ap.add_argument("--no-wgrad-overlap", action="store_true",
                     help="ablation: the weight gradients on the caller's stream (mlp.WGRAD_OVERLAP off)")
+    ap.add_argument("--full-view", action="store_true",
+                    help="ablation: the full view columns instead of the view-window layout (TrainRayCaster.view_windows)")
     ap.add_argument("--split-single", action="store_true",
                     help="ablation: one split launch per weight instead of the batched split")
     return ap
@@ -62,6 +64,7 @@ def measure(a, dev=None):
     if getattr(a, "no_wgrad_overlap", False):
         importlib.import_module("a-nerf_amd.mlp").WGRAD_OVERLAP = False
     tr = train.TrainRayCaster(cfg, ck, device=dev, mlp=a.mlp).train()
+    tr.view_windows = not getattr(a, "full_view", False)
     skts = torch.from_numpy(sc["skts"]).to(dev)
     delta = torch.zeros_like(skts, requires_grad=True)  # pose optimisation variable per image
     opt = torch.optim.Adam(list(tr.parameters()) + [delta], lr=5e-4)
