@@ -462,6 +462,7 @@ __global__ __launch_bounds__(NTHR, CB == 1 ? 256 / TBM : 1) void mlp_nt_kernel(N
         const float* const mp = tab->mask[si];
         const long long ldm = tab->ldm[si];
         const bool need_acc = tab->accum[si] != 0;
+        const bool pre = tab->accum[si] == 2;  // (the old value joins the pre-activation: before the relu)
         const int start = si == 2 ? cs2 : (si == 1 ? cs1 : 0);
         const int col = n - start;
         const int send = si == 2 ? Nd : (si == 1 ? cs2 : cs1);  // end of this segment
@@ -507,6 +508,7 @@ __global__ __launch_bounds__(NTHR, CB == 1 ? 256 / TBM : 1) void mlp_nt_kernel(N
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     v[e] += bv[e];
+                    if (pre) v[e] += ov[q][e];
                     if (relu) v[e] = fmaxf(v[e], 0.0f);
                 }
                 if (rout) {  // the row's largest |output| (for the next layer's fp16x4 scale): a max over
@@ -524,7 +526,7 @@ __global__ __launch_bounds__(NTHR, CB == 1 ? 256 / TBM : 1) void mlp_nt_kernel(N
 #pragma unroll
                         for (int e = 0; e < 4; ++e) v[e] = mk[q][e] > 0.0f ? v[e] : 0.0f;
                     }
-                    if (need_acc) {
+                    if (need_acc && !pre) {
 #pragma unroll
                         for (int e = 0; e < 4; ++e) v[e] += ov[q][e];
                     }
@@ -547,13 +549,14 @@ __global__ __launch_bounds__(NTHR, CB == 1 ? 256 / TBM : 1) void mlp_nt_kernel(N
                     float x = tile[row * TP + c4 + e];
                     if constexpr (F16) x = x * uw * pow2i(-rsh[row]);
                     x += bv[e];
+                    const int ce = ne - (se == 2 ? cs2 : (se == 1 ? cs1 : 0));
+                    float* de = ope + m * tab->old[se] + ce;
+                    if (tab->accum[se] == 2) x += *de;
                     if (relu) x = fmaxf(x, 0.0f);
                     if (rout) atomicMax(rout + m, __builtin_bit_cast(int, fabsf(x)));
-                    const int ce = ne - (se == 2 ? cs2 : (se == 1 ? cs1 : 0));
                     const float* const mpe = tab->mask[se];
                     if (mpe && !(mpe[m * tab->ldm[se] + ce] > 0.0f)) x = 0.0f;
-                    float* de = ope + m * tab->old[se] + ce;
-                    if (tab->accum[se]) x += *de;
+                    if (tab->accum[se] == 1) x += *de;
                     *de = x;
                 }
             }
@@ -1130,7 +1133,9 @@ int anerf_mlp_gemm_rows(int64_t m, int32_t n, int32_t k, const anerf_seg* a, int
     for (int i = 0; i < n_c; ++i) {
         if (c[i].cols < 1 || (c[i].p && c[i].ld < c[i].cols))
             return anerf_internal_fail(ANERF_EINVAL, "bad output segment");
-        g.c[i] = OSegD{c[i].p, c[i].ld, start, c[i].cols, c[i].mask, c[i].ldm, c[i].accumulate != 0};
+        if (c[i].accumulate < 0 || c[i].accumulate > 2)
+            return anerf_internal_fail(ANERF_EINVAL, "output segment accumulate must be 0, 1 or 2");
+        g.c[i] = OSegD{c[i].p, c[i].ld, start, c[i].cols, c[i].mask, c[i].ldm, c[i].accumulate};
         start += c[i].cols;
     }
     if (start != n) return anerf_internal_fail(ANERF_EINVAL, "output segments do not add up to n");

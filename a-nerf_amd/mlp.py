@@ -196,15 +196,13 @@ class _MLP(torch.autograd.Function):
              [(hf, W, W, 0, None, False), (raw, 4, 1, 3, None, False)], dev, hp,
              rin=rm[D - 1] if hp == ANERF_MLP_FP16X4 else None)
         prec = op_  # (the view and rgb layers)
-        # views_linears[0] on cat([feature, views(, framecode)]), relu; view windows: the GEMM (no relu)
-        # accumulated onto sum_j w_j G_j, then the relu
+        # views_linears[0] on cat([feature, views(, framecode)]), relu; view windows: sum_j w_j G_j joins the
+        # GEMM's pre-activation (accumulate mode 2: product + bias + sum, then the relu)
         av = [_seg(hf, W)] + ([_seg(feat, nv, dnet)] if nv else []) + ([_seg(codes, cfc)] if cfc else [])
         if nwin:
             G = G.contiguous()
         g = _view_mix(feat, dnet, nwin, G) if nwin else torch.empty(M, W // 2, **f32)
-        mm(M, W // 2, W + nv + cfc, av, sp[D + 1], bv, not nwin, [(g, W // 2, W // 2, 0, None, bool(nwin))], dev)
-        if nwin:
-            g.relu_()
+        mm(M, W // 2, W + nv + cfc, av, sp[D + 1], bv, True, [(g, W // 2, W // 2, 0, None, 2 if nwin else 0)], dev)
         # rgb_linear into raw[:, :3]
         mm(M, 3, W // 2, [_seg(g, W // 2)], sp[D + 2], br, False, [(raw, 4, 3, 0, None, False)], dev)
         ctx.shape = shape

@@ -495,7 +495,9 @@ typedef struct {
 } anerf_seg;
 
 /* An output column segment: out[row * ld + c] = v, v *= (mask[row * ldm + c] > 0) when mask is set
- * (relu backward by the saved activation), v += out[...] when accumulate; p NULL discards it. */
+ * (relu backward by the saved activation), v += out[...] when accumulate == 1 (after the relu and mask);
+ * accumulate == 2 (ABI 16) adds out[...] to the pre-activation instead (product + bias + out, then the relu: the
+ * view-window layout's view part, anerf_train_view_mix); p NULL discards it. */
 typedef struct {
     float* p;
     int64_t ld;

@@ -73,6 +73,23 @@ def test_gemm_forward_segments_bias_relu(m, n, ks, prec):
     assert torch.all(err <= _bound(a, w, prec)), float(err.max())
 
 
+@pytest.mark.parametrize("m,n,k", [(1000, 128, 256), (163857, 128, 256), (77, 130, 264), (33, 3, 12)])
+def test_gemm_preactivation_accumulate(m, n, k):
+    """accumulate == 2 (anerf.h anerf_oseg): the old output joins the pre-activation, relu(A W^T + b + old) -- the
+    view layer of the view-window layout (old = sum_j w_j G_j); ragged columns take the per-element path."""
+    torch.manual_seed(m + n)
+    a = torch.randn(m, k, device=DEV)
+    w = torch.randn(n, k, device=DEV) / k ** 0.5
+    b = torch.randn(n, device=DEV)
+    old = torch.randn(m, n, device=DEV)
+    out = old.clone()
+    mlp.gemm(m, n, k, [mlp._seg(a, k)], mlp.split_weight(w, False, 6), b, True, [(out, n, n, 0, None, 2)],
+             torch.device(DEV), 6)
+    ref = torch.relu(a.double() @ w.double().t() + b.double() + old.double())
+    err = (out.double() - ref).abs()
+    assert torch.all(err <= _bound(a, w, 6) + 1e-6 * old.double().abs()), float(err.max())
+
+
 def _rowmax_bits(t):
     """int32 [m]: the bit pattern of each row's largest |value| (what the GEMM epilogue's rout holds)."""
     return t.abs().amax(1).contiguous().view(torch.int32) if t.shape[1] else torch.zeros(t.shape[0], dtype=torch.int32)
