@@ -81,7 +81,7 @@ def test_view_factor_matches_torch(mrv, world, sched):
     torch.cuda.synchronize()
 
     def close(a, ref, tol):
-        d = float((a.double().cpu() - ref).abs().max())
+        d = float((a.detach().double().cpu() - ref.detach()).abs().max())
         assert d <= tol * float(ref.abs().max()) + 1e-12, d
     close(G, Gr.detach(), 1e-5)
     close(sk1.grad, sk2.grad, 1e-4)
