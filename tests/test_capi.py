@@ -112,3 +112,25 @@ def test_view_mix_rejects_bad_shapes():
     assert lib.anerf_train_view_mix(1, 1, 24, 128, 1, 20, 16, 16, None) == -1
     assert b"anerf_train_view_mix" in lib.anerf_last_error()
     assert lib.anerf_train_view_mix_backward(1, 1, 24, 128, 1, 24, 16, 16, None, 24, 16, None) == -1
+
+
+def test_view_windows_flag_validation():
+    """ANERF_ENC_VIEW_WINDOWS (ABI 16) needs cutoff_viewdir and cutoff_inputs and no staged encoder; anerf_model_create
+    rejects the rest before any HIP call."""
+    lib = _lib.load()
+
+    def create(**kw):
+        d = _lib.ModelDesc()
+        d.n_joints, d.net_depth, d.net_width, d.multires, d.multires_views = 24, 8, 256, 7, 4
+        d.skip, d.use_cutoff, d.cutoff_inputs, d.cutoff_viewdir, d.density_scale = 4, 1, 1, 1, 1.0
+        d.encoder_flags = _lib.ANERF_ENC_VIEW_WINDOWS
+        for k, v in kw.items():
+            setattr(d, k, v)
+        h = ctypes.c_void_p()
+        return lib.anerf_model_create(ctypes.byref(d), None, None, None, 0, ctypes.byref(h))
+    assert create(cutoff_viewdir=0) == -1 and b"VIEW_WINDOWS" in lib.anerf_last_error()
+    assert create(cutoff_inputs=0) == -1 and b"VIEW_WINDOWS" in lib.anerf_last_error()
+    assert create(encoder_flags=_lib.ANERF_ENC_VIEW_WINDOWS | _lib.ANERF_ENC_VIEW_ANGLE) == -1
+    assert b"staged" in lib.anerf_last_error()
+    assert create(multires_bones=2) == -1 and b"staged" in lib.anerf_last_error()
+    assert create(encoder_flags=256) == -1 and b"unknown" in lib.anerf_last_error()
