@@ -148,19 +148,19 @@ __device__ inline float np_pairwise_sum(const float* a, int64_t n) {
 
 // The same tree split for a workgroup: the leaves (<= 128 elements, left to right) are listed once,
 // summed by many threads, then combined in the tree's order.  np_pairwise_leaves returns the leaf
-// count, or -1 when there are more than `cap`.
-__device__ inline int np_pairwise_leaves(int64_t n, int* off, int* cnt, int cap) {
-    int64_t st_off[64], st_n[64];
+// count, or -1 when there are more than `cap`.  st_off / st_n: [64] walk stacks the caller provides (LDS: a
+// private array indexed at run time would live in scratch, ~1 us per access).
+__device__ inline int np_pairwise_leaves(int64_t n, int* off, int* cnt, int cap, int* st_off, int* st_n) {
     int ns = 1, nl = 0;
-    st_off[0] = 0; st_n[0] = n;
+    st_off[0] = 0; st_n[0] = (int)n;
     while (ns > 0) {
         --ns;
-        const int64_t o = st_off[ns], c = st_n[ns];
+        const int o = st_off[ns], c = st_n[ns];
         if (c <= 128) {
             if (nl == cap) return -1;
-            off[nl] = (int)o; cnt[nl] = (int)c; ++nl;
+            off[nl] = o; cnt[nl] = c; ++nl;
         } else {
-            int64_t n2 = c / 2;
+            int n2 = c / 2;
             n2 -= n2 % 8;
             st_off[ns] = o + n2; st_n[ns] = c - n2; ++ns;   // right half after the left one
             st_off[ns] = o; st_n[ns] = n2; ++ns;
@@ -169,20 +169,17 @@ __device__ inline int np_pairwise_leaves(int64_t n, int* off, int* cnt, int cap)
     return nl;
 }
 
-// np_pairwise_sum given the leaf sums in left-to-right order
-__device__ inline float np_pairwise_combine(const float* leaf, int64_t n) {
-    int64_t node_n[64];
-    int node_exp[64];
-    float vals[64];
+// np_pairwise_sum given the leaf sums in left-to-right order; node_n / node_exp / vals: [64] caller stacks (LDS)
+__device__ inline float np_pairwise_combine(const float* leaf, int64_t n, int* node_n, int* node_exp, float* vals) {
     int ns = 1, vs = 0, k = 0;
-    node_n[0] = n; node_exp[0] = 0;
+    node_n[0] = (int)n; node_exp[0] = 0;
     while (ns > 0) {
         --ns;
-        const int64_t cnt = node_n[ns];
+        const int cnt = node_n[ns];
         if (cnt <= 128) {
             vals[vs++] = leaf[k++];
         } else if (!node_exp[ns]) {
-            int64_t n2 = cnt / 2;
+            int n2 = cnt / 2;
             n2 -= n2 % 8;
             node_exp[ns] = 1; ++ns;
             node_n[ns] = cnt - n2; node_exp[ns] = 0; ++ns;

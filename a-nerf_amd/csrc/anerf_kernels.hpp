@@ -373,6 +373,7 @@ __global__ void near_far_kernel(const float* __restrict__ rb, int stride, int64_
 
 // one workgroup per chunk: NaN rows <- np.nanmean of the chunk (ray_utils.py:328-342)
 constexpr int NF_LEAVES = 1024;  // leaves of <= 128 rays: chunks up to ~65 k rays in parallel
+constexpr int NF_LDS = 8192;     // chunks up to this many rays sum from LDS
 
 __global__ void nan_fill_kernel(const float* __restrict__ rb, int stride, int64_t n, int chunk,
                                 float* __restrict__ near_io, float* __restrict__ far_io,
@@ -390,8 +391,13 @@ __global__ void nan_fill_kernel(const float* __restrict__ rb, int stride, int64_
         if (near_io[i] != near_io[i]) any = 1;
     __syncthreads();
     if (!any) return;
-    if (threadIdx.x == 0) n_leaves = np_pairwise_leaves(m, leaf_off, leaf_cnt, NF_LEAVES);
-    float* buf = scratch + c0;  // NaN -> 0 copies, one vector at a time
+    __shared__ int st_a[64], st_b[64];  // (the tree walks' stacks, thread 0)
+    __shared__ float st_v[64];
+    if (threadIdx.x == 0) n_leaves = np_pairwise_leaves(m, leaf_off, leaf_cnt, NF_LEAVES, st_a, st_b);
+    // NaN -> 0 copies, one vector at a time: in LDS for chunks up to NF_LDS rays (the leaf sums' loads then wait
+    // on LDS, not on L2: 55 -> a few us for a 2048-ray training batch), else in the scratch
+    __shared__ float lbuf[NF_LDS];
+    float* buf = m <= NF_LDS ? lbuf : scratch + c0;
     for (int v = 0; v < 2; ++v) {
         const float* src = v == 0 ? near_io : far_io;
         int mine = 0;
@@ -407,7 +413,7 @@ __global__ void nan_fill_kernel(const float* __restrict__ rb, int stride, int64_
             for (int k = threadIdx.x; k < n_leaves; k += blockDim.x) leaf_sum[k] = np_leaf_sum(buf + leaf_off[k], leaf_cnt[k]);
         __syncthreads();
         if (threadIdx.x == 0) {
-            const float sum = n_leaves >= 0 ? np_pairwise_combine(leaf_sum, m) : np_pairwise_sum(buf, m);
+            const float sum = n_leaves >= 0 ? np_pairwise_combine(leaf_sum, m, st_a, st_b, st_v) : np_pairwise_sum(buf, m);
             means[v] = valid[v] ? (float)((double)sum / (double)valid[v]) : __int_as_float(0x7fc00000);
         }
         __syncthreads();
