@@ -122,6 +122,8 @@ def measure(a, dev=None):
                                       "two-way fp16 split, the bf16x6 error bound)",
                            "bf16x6": "fp32-accurate forward and gradients", "bf16x3": "~16-bit operands",
                            "fp32": "torch fp32 GEMMs"}[a.mlp],
+        "view_layout": ("view windows (anerf.h ANERF_ENC_VIEW_WINDOWS: 24 windows per sample + per-ray factors)"
+                        if tr.model.view_windows else "full view columns (648 per sample)"),
         "data": "synthetic (seeded SMPL-24 poses, 128 cameras on a circle, seeded weights)"}
 
 
