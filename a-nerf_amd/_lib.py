@@ -249,15 +249,39 @@ def load():
     if not os.path.exists(LIB_PATH):
         raise AnerfError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
                          "(hipcc --offload-arch=gfx950); there is no CPU fallback")
-    lib = ctypes.CDLL(LIB_PATH)
+    cdll = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
-        fn = getattr(lib, name)
+        fn = getattr(cdll, name)
         fn.restype = res
         fn.argtypes = args
+    lib = _Checked(cdll)
     if lib.anerf_abi_version() != ABI_VERSION:  # (a stale build would read these structs with another layout)
         raise AnerfError(f"{LIB_PATH} has ABI {lib.anerf_abi_version()}, this binding {ABI_VERSION}: rebuild it")
     _lib = lib
     return lib
+
+
+class _Checked:
+    """The library with every entry point's argument count enforced: ctypes passes surplus arguments of a
+    function with argtypes through unchecked (a call with one argument too many shifts the stream handle into
+    another slot), so each call is checked against SIGNATURES first."""
+
+    def __init__(self, cdll):
+        self._cdll = cdll
+        for name, (_, args) in SIGNATURES.items():
+            setattr(self, name, self._wrap(getattr(cdll, name), name, len(args)))
+
+    @staticmethod
+    def _wrap(fn, name, n):
+        def call(*a):
+            if len(a) != n:
+                raise TypeError(f"{name} takes {n} arguments, got {len(a)}")
+            return fn(*a)
+        call.__name__ = name
+        return call
+
+    def __getattr__(self, name):  # (symbols outside SIGNATURES: the raw ctypes function)
+        return getattr(self._cdll, name)
 
 
 def check(rc, what):

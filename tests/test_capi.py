@@ -134,3 +134,11 @@ def test_view_windows_flag_validation():
     assert b"staged" in lib.anerf_last_error()
     assert create(multires_bones=2) == -1 and b"staged" in lib.anerf_last_error()
     assert create(encoder_flags=256) == -1 and b"unknown" in lib.anerf_last_error()
+
+
+def test_binding_rejects_a_wrong_argument_count():
+    """_lib.load()'s entry points check their argument count (ctypes alone lets a surplus argument through)."""
+    lib = _lib.load()
+    with pytest.raises(TypeError, match="anerf_train_view_mix takes 9 arguments, got 10"):
+        lib.anerf_train_view_mix(1, 1, 24, 130, 1, 24, 16, 16, None, None)
+    assert lib.anerf_train_view_mix(1, 1, 24, 130, 1, 24, 16, 16, None) == -1
