@@ -345,11 +345,10 @@ def create_raycaster(args, data_attrs, device=None, ckpt=None):
             start = 0 if getattr(args, "finetune", False) else int(ckpt.get("global_step", 0))
     caster = TrainRayCaster(cfg, ckpt, device=device)
     grad_vars = [p for p in caster.parameters() if p.requires_grad]
-    # (the reference's Adam; fused into one kernel per step on the GPU: +0.5 % training step,
-    # profiles/r05zm_adam_ab.txt, the same update up to rounding)
-    on_gpu = bool(grad_vars) and grad_vars[0].is_cuda
-    optimizer = torch.optim.Adam(params=grad_vars, lr=getattr(args, "lrate", 5e-4), betas=(0.9, 0.999),
-                                 **({"fused": True} if on_gpu else {}))
+    # (the reference's Adam.  The fused implementation measured +0.5 % per step, profiles/r05zm_adam_ab.txt, but
+    # with it the eval caster missed the update in test_create_raycaster_training_drop_in: its in-place step
+    # evidently leaves the parameters' version counters, by which the eval caster notices new weights, unchanged)
+    optimizer = torch.optim.Adam(params=grad_vars, lr=getattr(args, "lrate", 5e-4), betas=(0.9, 0.999))
     if ckpt is not None and "optimizer_state_dict" in ckpt and not getattr(args, "finetune", False):
         optimizer.load_state_dict(ckpt["optimizer_state_dict"])
     common = {"N_importance": cfg.N_importance, "N_samples": cfg.N_samples, "use_viewdirs": cfg.use_viewdirs,

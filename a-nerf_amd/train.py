@@ -594,6 +594,11 @@ class TrainRayCaster(nn.Module):
         """The DeviceModel holding the encoder / compositing constants (device index for `render`)."""
         return self._constants()
 
+    def weights_changed(self):
+        """Force the next eval render to repack the weights: for updates the version counters do not show (an
+        optimizer that writes the parameters in place without advancing them, e.g. torch's fused Adam)."""
+        self._eval_version = None
+
     def eval_caster(self):
         """The fused eval RayCaster over the current weights (repacked only after they changed; a new
         tau / cutoff reaches it without a repack); for a staged encoder (cfg.staged) the training stages

@@ -262,3 +262,20 @@ def test_checkpoint_round_trip_through_torch_save(tmp_path):
     b = tr2(rb, m["S"], skts=sk, cyls=cy, N_importance=m["I"])
     for k in ("rgb_map", "disp_map", "acc_map", "rgb0"):
         assert torch.equal(a[k], b[k]), k
+
+
+def test_weights_changed_forces_the_eval_repack():
+    """TrainRayCaster.weights_changed(): after an update the version counters may not show (torch's fused Adam),
+    the next eval render repacks and renders the new weights."""
+    g = Golden("t1_s32i16_d4w128")
+    m = g.meta
+    tr = train.TrainRayCaster(g.cfg, g.ckpt).eval()
+    dev = torch.device("cuda:0")
+    rays, sk, cy = (torch.from_numpy(g[k]).to(dev) for k in ("rays", "skts", "cyls"))
+    r0 = tr.render_rays(rays, m["S"], skts=sk, cyls=cy, N_importance=m["I"])["rgb_map"].clone()
+    with torch.no_grad():
+        for p in tr.network_fn.parameters():
+            p.data.mul_(1.01)  # (through .data: the version counter does not move)
+    tr.weights_changed()
+    r1 = tr.render_rays(rays, m["S"], skts=sk, cyls=cy, N_importance=m["I"])["rgb_map"]
+    assert not torch.equal(r0, r1)
