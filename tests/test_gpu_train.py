@@ -272,10 +272,10 @@ def test_weights_changed_forces_the_eval_repack():
     tr = train.TrainRayCaster(g.cfg, g.ckpt).eval()
     dev = torch.device("cuda:0")
     rays, sk, cy = (torch.from_numpy(g[k]).to(dev) for k in ("rays", "skts", "cyls"))
-    r0 = tr.render_rays(rays, m["S"], skts=sk, cyls=cy, N_importance=m["I"])["rgb_map"].clone()
+    r0 = tr.eval_caster().render_rays(rays, m["S"], skts=sk, cyls=cy, N_importance=m["I"])["rgb_map"].clone()
     with torch.no_grad():
         for p in tr.network_fn.parameters():
             p.data.mul_(1.01)  # (through .data: the version counter does not move)
     tr.weights_changed()
-    r1 = tr.render_rays(rays, m["S"], skts=sk, cyls=cy, N_importance=m["I"])["rgb_map"]
+    r1 = tr.eval_caster().render_rays(rays, m["S"], skts=sk, cyls=cy, N_importance=m["I"])["rgb_map"]
     assert not torch.equal(r0, r1)
