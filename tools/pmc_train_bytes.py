@@ -18,7 +18,7 @@ def load(d, counter):
         n = r["Kernel_Name"]
         if n.startswith("near_far_kernel"):
             steps += 1
-        fam = n.split("(")[0].replace("void ", "").replace("(anonymous namespace)::", "")
+        fam = n.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
         fam = fam if len(fam) < 70 else fam[:70]
         out[fam] += float(r["Counter_Value"]) * 1024.0
     return out, steps
