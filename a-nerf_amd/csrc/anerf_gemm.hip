@@ -1012,9 +1012,14 @@ int set_segs(const anerf_seg* in, int n, int total, SegD* out) {
     return ANERF_OK;
 }
 
+// weight-gradient workgroups per launch (experiment switch): ~512 = two per CU; fewer slabs write and re-read fewer
+// partial tiles
+#ifndef ANERF_WGRAD_WG
+#define ANERF_WGRAD_WG 512
+#endif
 int wgrad_plan(int64_t m, int32_t n, int32_t k, int* splits, long long* rows) {
     const int tiles = ((n + BN - 1) / BN) * ((k + BM - 1) / BM);
-    long long s = (512 + tiles - 1) / tiles;         // ~512 workgroups (two per CU)
+    long long s = (ANERF_WGRAD_WG + tiles - 1) / tiles;  // ~ANERF_WGRAD_WG workgroups
     const long long smax = (m + 255) / 256;         // >= 256 rows per slab
     if (s > smax) s = smax;
     if (s < 1) s = 1;
