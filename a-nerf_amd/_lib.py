@@ -11,7 +11,7 @@ import os
 import torch  # noqa: F401  (must be loaded before the HIP library, see module docstring)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("ANERF_LIB_PATH") or os.path.join(HERE, "libanerf_hip.so")  # (override: A/B of builds)
+LIB_PATH = os.path.join(HERE, "libanerf_hip.so")  # (the in-tree build; the package reads no environment)
 
 MAXL = 16
 c_f = ctypes.POINTER(ctypes.c_float)
@@ -239,6 +239,15 @@ _lib = None
 
 class AnerfError(RuntimeError):
     pass
+
+
+def use_library(path):
+    """A/B tooling only (tools/_ablib.py, bench.py --lib): load an experiment build of the library instead of
+    the in-tree one.  Must run before the first load(); the ABI check below applies to it as to the default."""
+    global LIB_PATH
+    if _lib is not None and os.path.abspath(path) != os.path.abspath(LIB_PATH):
+        raise AnerfError(f"use_library({path!r}) after {LIB_PATH} was loaded")
+    LIB_PATH = os.path.abspath(path)
 
 
 def load():

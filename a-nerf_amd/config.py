@@ -115,6 +115,14 @@ class RenderConfig:
         return bool(self.cutoff_bones and self.use_cutoff)
 
     @property
+    def view_window(self):
+        """The view embedder is a CutoffEmbedder (its features windowed by w'_j): --cutoff_viewdir AND --use_cutoff.
+        create_raycaster copies cutoff_kwargs, whose "cutoff" is args.use_cutoff, for the view embedder
+        (core/raycasters.py:31, 68-71), and get_embedder builds a plain Embedder unless it is set
+        (core/cutoff_embedder.py:216-220): without --use_cutoff the view features carry no window."""
+        return bool(self.use_viewdirs and self.cutoff_viewdir and self.use_cutoff)
+
+    @property
     def kp_relpos(self):
         """--kp_dist_type relpos (core/encoders.py:124-142): three local coordinates per joint."""
         return self.extra.get("kp_dist_type", "reldist") == "relpos"
@@ -218,7 +226,7 @@ def feature_scales(cfg, alpha_pts, alpha_views, alpha_bones=None):
         if alpha_bones is None:
             raise ValueError("freq_schedule with a windowed bone embedder: its sched_alpha is needed")
         part(cfg.input_ch, 3 * nj, cfg.multires_bones, alpha_bones)
-    if cfg.use_viewdirs and cfg.cutoff_viewdir and cfg.multires_views > 0:
+    if cfg.view_window and cfg.multires_views > 0:
         part(dnet, nj * (1 if cfg.view_angle else 3), cfg.multires_views, alpha_views)
     return s
 

@@ -557,9 +557,9 @@ static int validate_desc(const anerf_model_desc* d) {
     if ((d->encoder_flags & ANERF_ENC_VIEW_RAW) && (d->encoder_flags & ANERF_ENC_VIEW_ANGLE))
         return fail(ANERF_EINVAL, "ANERF_ENC_VIEW_RAW and ANERF_ENC_VIEW_ANGLE are two view types");
     if (d->encoder_flags & ANERF_ENC_VIEW_WINDOWS) {
-        if (!d->cutoff_viewdir || !d->cutoff_inputs)
-            return fail(ANERF_EINVAL, "ANERF_ENC_VIEW_WINDOWS needs cutoff_viewdir and cutoff_inputs (every view feature "
-                                      "windowed)");
+        if (!d->cutoff_viewdir || !d->use_cutoff || !d->cutoff_inputs)
+            return fail(ANERF_EINVAL, "ANERF_ENC_VIEW_WINDOWS needs cutoff_viewdir, use_cutoff and cutoff_inputs (every "
+                                      "view feature windowed)");
         if (d->multires_bones > 0 || (d->encoder_flags & (ANERF_ENC_KP_RELPOS | ANERF_ENC_VIEW_ANGLE | ANERF_ENC_KP_QUERYPTS)))
             return fail(ANERF_EINVAL, "ANERF_ENC_VIEW_WINDOWS is not for a staged encoder");
     }

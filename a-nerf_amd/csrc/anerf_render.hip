@@ -195,7 +195,9 @@ int anerf_model_create(const anerf_model_desc* desc, const anerf_net_weights* co
     md.mrv = desc->multires_views;
     md.use_cutoff = desc->use_cutoff;
     md.cutoff_inputs = desc->cutoff_inputs;
-    md.cutoff_viewdir = desc->cutoff_viewdir;
+    // (the view embedder is a CutoffEmbedder only under use_cutoff too: create_raycaster copies cutoff_kwargs, whose
+    // "cutoff" is use_cutoff, core/raycasters.py:31, 68-71; cutoff_embedder.py:216-220)
+    md.cutoff_viewdir = desc->cutoff_viewdir && desc->use_cutoff;
     md.cfc = desc->framecode_ch;
     md.n_codes = desc->n_framecodes;
     md.softplus = desc->density_softplus;

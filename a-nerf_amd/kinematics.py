@@ -214,15 +214,21 @@ class PoseOptLayer(torch.nn.Module):
         if idxs is None:
             idxs = np.arange(self.N_kps)
         idxs = np.atleast_1d(np.asarray(idxs))
-        pelvis, bone = self.idx_to_params(idxs)
+        # (as the reference, pose_opt.py:380-381, 436-442: the chain runs once per distinct index -- a training
+        # batch names each ray's image -- and the outputs are gathered back in the requested order)
+        uniq, inv = np.unique(idxs, return_inverse=True)
+        pelvis, bone = self.idx_to_params(uniq)
         if len(self.rest_pose) == 1:
             rest, ridx = self.rest_pose, None
         elif rest_pose_idxs is not None:
-            rest, ridx = self.rest_pose, np.asarray(rest_pose_idxs)
+            rest, ridx = self.rest_pose, np.asarray(rest_pose_idxs)[np.unique(idxs, return_index=True)[1]]
         else:
-            rest, ridx = self.rest_pose, self.rest_pose_idxs[idxs]
+            rest, ridx = self.rest_pose, self.rest_pose_idxs[uniq]
         o = pose_kinematics(bone, rest, self.skel_type, pelvis=pelvis, rest_idx=ridx, device=self.device)
-        return o["kps"], bone, o["skts"], o["l2ws"], o["rots"]
+        if len(uniq) == len(idxs) and np.array_equal(uniq, idxs):
+            return o["kps"], bone, o["skts"], o["l2ws"], o["rots"]
+        g = torch.as_tensor(inv.reshape(-1), dtype=torch.long, device=self.device)
+        return o["kps"][g], bone[g], o["skts"][g], o["l2ws"][g], o["rots"][g]
 
     @torch.no_grad()
     def update_cache(self):

@@ -18,17 +18,16 @@ bf16x6 and the backward in bf16x3; fp32 accumulation in all (`anerf_gemm.hip`). 
 built and a GPU present.
 """
 import ctypes
-import os
 
 import torch
 
 from . import _lib
 
-# ANERF_TRAIN_FWD=fused: the whole bf16x6 forward (width 128 / 256) in one kernel (anerf_mlp_forward)
-# instead of the layer-by-layer GEMMs.  Measured equal on MI355X (1.96 vs 1.95 ms at M = 163840,
-# DESIGN.md §10): its 1.6 GB of saved activations cost as much as the GEMMs' re-reads, so the GEMMs
-# stay the default
-_FUSED = os.environ.get("ANERF_TRAIN_FWD", "gemm") == "fused"
+# FUSED_FORWARD (an A/B switch for tools/fwd_bench.py and tests/test_gpu_mlp.py, never read from the
+# environment): the whole bf16x6 forward (width 128 / 256) in one kernel (anerf_mlp_forward) instead of
+# the layer-by-layer GEMMs.  Measured equal on MI355X (1.96 vs 1.95 ms at M = 163840, DESIGN.md §10): its
+# 1.6 GB of saved activations cost as much as the GEMMs' re-reads, so the GEMMs stay the default
+FUSED_FORWARD = False
 ANERF_MLP_FP16X4 = _lib.MLP_PRECISIONS["fp16x4"]
 
 
@@ -156,7 +155,7 @@ class _MLP(torch.autograd.Function):
         whead = torch.cat([wf, wa]).contiguous()
         cfc = 0 if codes is None else codes.shape[1]
         f32 = dict(device=dev, dtype=torch.float32)
-        if _FUSED and prec == 6 and W in (128, 256) and dnet % 4 == 0 and nv % 4 == 0 and cfc % 4 == 0 and not nwin:
+        if FUSED_FORWARD and prec == 6 and W in (128, 256) and dnet % 4 == 0 and nv % 4 == 0 and cfc % 4 == 0 and not nwin:
             H, hf, g, raw = _fused_forward(feat, codes, pw, pb, wa, ba, wf, bf, wv, bv, wr, br, W, D, skip, dnet, nv,
                                            cfc, dev)
             ctx.shape = shape

@@ -39,8 +39,10 @@ class DeviceModel:
         d.n_joints, d.net_depth, d.net_width = cfg.n_joints, cfg.netdepth, cfg.netwidth
         d.skip = cfg.skips[0]
         d.multires, d.multires_views = cfg.multires, cfg.multires_views
+        # (cutoff_viewdir as the reference builds it: a windowed view embedder only under use_cutoff too,
+        # RenderConfig.view_window; anerf_model_create applies the same rule to a raw descriptor)
         d.use_cutoff, d.cutoff_inputs, d.cutoff_viewdir = int(cfg.use_cutoff), int(cfg.cutoff_inputs), int(
-            cfg.cutoff_viewdir)
+            cfg.view_window)
         d.framecode_ch = cfg.framecode_ch
         d.n_framecodes = cfg.n_framecodes if cfg.opt_framecode else 0
         d.density_softplus = int(cfg.density_type == "softplus")

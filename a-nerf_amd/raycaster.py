@@ -346,8 +346,9 @@ def create_raycaster(args, data_attrs, device=None, ckpt=None):
     caster = TrainRayCaster(cfg, ckpt, device=device)
     grad_vars = [p for p in caster.parameters() if p.requires_grad]
     # (the reference's Adam.  The fused implementation measured +0.5 % per step, profiles/r05zm_adam_ab.txt, but
-    # with it the eval caster missed the update in test_create_raycaster_training_drop_in: its in-place step
-    # evidently leaves the parameters' version counters, by which the eval caster notices new weights, unchanged)
+    # its step writes the parameters without advancing their version counters (p._version, by which the eval
+    # caster notices new weights): tests/test_host.py::test_fused_adam_leaves_version_counters checks exactly
+    # that, and TrainRayCaster.weights_changed() is the hook for such optimizers)
     optimizer = torch.optim.Adam(params=grad_vars, lr=getattr(args, "lrate", 5e-4), betas=(0.9, 0.999))
     if ckpt is not None and "optimizer_state_dict" in ckpt and not getattr(args, "finetune", False):
         optimizer.load_state_dict(ckpt["optimizer_state_dict"])

@@ -17,6 +17,8 @@ Random numbers: torch's generator on the device by default; pass `rand={"t_rand"
 ray_noise_std also "pts_noise0": (N,S,3), "pts_noise1": (N,I,3)) to reproduce a given draw — the
 parity tests feed the reference's.
 """
+import contextlib
+
 import numpy as np
 import torch
 import torch.nn as nn
@@ -389,11 +391,12 @@ class _Embed(nn.Module):
 
 def view_windows_ok(cfg):
     """The view-window layout (anerf.h ANERF_ENC_VIEW_WINDOWS) holds for this configuration: every view feature is
-    a window times a function of the ray (cutoff_viewdir and cutoff_inputs, relray / world directions), and the
+    a window times a function of the ray (a windowed view embedder -- cutoff_viewdir with use_cutoff,
+    RenderConfig.view_window -- and cutoff_inputs, relray / world directions), and the
     GEMM segments stay 16-byte aligned without padding, and the per-ray factors G fit anerf_train_view_mix's LDS plan
     (NJ W / 2 <= 4096)."""
     dnet = cfg.input_ch + cfg.input_ch_bones
-    return (cfg.cutoff_viewdir and cfg.cutoff_inputs and not cfg.view_angle and not cfg.staged and dnet % 4 == 0
+    return (cfg.view_window and cfg.cutoff_inputs and not cfg.view_angle and not cfg.staged and dnet % 4 == 0
             and (dnet + cfg.n_joints) % 4 == 0 and cfg.n_joints * (cfg.netwidth // 2) <= 4096)
 
 
@@ -578,7 +581,21 @@ class TrainRayCaster(nn.Module):
     # the training stages' view-window layout where the configuration allows it (view_windows_ok): the encoder
     # writes NJ windows instead of 3 NJ (1 + 2 multires_views) view features, the view layer reads them through the
     # per-ray factors G (view_factor); False: the full view columns
-    view_windows = True
+    _view_windows = True
+
+    @property
+    def view_windows(self):
+        return self._view_windows
+
+    @view_windows.setter
+    def view_windows(self, on):
+        """ the layout lives in the DeviceModel of the encoder constants: a change drops it, so the next
+        pass builds it in the new layout (a plain class attribute was read once and later changes were ignored)."""
+        on = bool(on)
+        if on != self._view_windows:
+            self._consts = None
+            self._consts_embed = None
+        self._view_windows = on
 
     def _constants(self):
         if self._consts is None:
@@ -760,6 +777,18 @@ class StagedCaster:
     def __init__(self, trainable):
         self._t = trainable
 
+    @contextlib.contextmanager
+    def _eval_mode(self):
+        """The trainable in eval mode for the call, its mode restored afterwards: called from a
+        TrainRayCaster still in training mode (forward(fwd_type='density'), an eval render with cams = -1) the
+        framecodes must take the eval-mode mean code (FrameCodes, gated on `training`), as the fused caster does."""
+        was = self._t.training
+        self._t.eval()
+        try:
+            yield
+        finally:
+            self._t.train(was)
+
     @property
     def model(self):
         return self._t.model
@@ -784,9 +813,10 @@ class StagedCaster:
                     preproc_kwargs=None, nerf_type="nerf", chunk=None, ret_alpha=True, **unused):
         if perturb or raw_noise_std or ray_noise_std:
             raise NotImplementedError("the eval caster renders deterministically; train() for stochastic renders")
-        out = self._t.render_rays(ray_batch, N_samples, kp_batch=kp_batch, skts=skts, cyls=cyls, bones=bones,
-                                  cams=cams, subject_idxs=subject_idxs, lindisp=lindisp, perturb=0.,
-                                  N_importance=N_importance, preproc_kwargs=preproc_kwargs, chunk=chunk)
+        with self._eval_mode():
+            out = self._t.render_rays(ray_batch, N_samples, kp_batch=kp_batch, skts=skts, cyls=cyls, bones=bones,
+                                      cams=cams, subject_idxs=subject_idxs, lindisp=lindisp, perturb=0.,
+                                      N_importance=N_importance, preproc_kwargs=preproc_kwargs, chunk=chunk)
         out = {k: v.detach() for k, v in out.items()}
         if not ret_alpha:
             out.pop("alpha", None)
@@ -829,7 +859,8 @@ class StagedCaster:
         if fs is not None:
             feat = feat * fs
         cams = torch.zeros(n, device=dev, dtype=torch.long) if self.cfg.opt_framecode else None
-        return net(feat, cams)[:, 3:4].reshape(*shape, 1)
+        with self._eval_mode():
+            return net(feat, cams)[:, 3:4].reshape(*shape, 1)
 
     @torch.no_grad()
     def render_mesh_density(self, kps, skts, bones, subject_idxs=None, radius=1.0, res=64, render_kwargs=None,

@@ -104,6 +104,12 @@ def parse():
                          "config 5's layout; the default under torch.distributed.run)")
     ap.add_argument("--also", default="bf16x6,fp16x3,fp32,bf16x3",
                     help="other precision modes timed on the same frame afterwards (rank 0, N=1; '' = none)")
+    ap.add_argument("--no-tally", action="store_true",
+                    help="skip the untimed MFMA-tally calls (count_mfma) so that every render_kernel dispatch of the "
+                         "run is a warmup or timed step: the PMC passes of tools/gpu_pmc.sh (frac_executed null)")
+    ap.add_argument("--lib", default=None,
+                    help="A/B tooling: an experiment build of libanerf_hip.so (default: the in-tree library; "
+                         "ANERF_LIB_PATH is honoured by this harness, never by the package)")
     ap.add_argument("--precision", default="fp16x4", choices=["fp32", "bf16x6", "fp16x4", "fp16x3", "bf16x3"],
                     help="MLP arithmetic (include/anerf.h ANERF_PREC_*)")
     return ap.parse_args()
@@ -387,6 +393,8 @@ def main():
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
 
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    importlib.import_module("_ablib").apply(a.lib)  # (A/B builds only; the default is the in-tree library)
     anerf = importlib.import_module("a-nerf_amd")
     syn = importlib.import_module("a-nerf_amd.synthetic")
     _lib = importlib.import_module("a-nerf_amd._lib")
@@ -499,11 +507,16 @@ def main():
     # the launches' MFMA work (kernel-side tally of one extra, untimed call over this rank's rays) and
     # the work an exact fp32 implementation must do after exact-zero window skipping: the fp32 mode's
     # tally of the same rays (v_mfma_f32_32x32x2_f32, FLOP_F32_MFMA each)
-    rc.render_rays(rb, S, skts=skts.expand(n_mine, -1, -1, -1), cyls=cyl.expand(n_mine, -1), N_importance=I,
-                   chunk=4096, ret_alpha=False, count_mfma=True, near_far_given=sharded)
-    torch.cuda.synchronize()
-    n_f32, n_bf16 = (int(v) for v in rc.last_mfma.tolist())
-    if a.precision == "fp32":
+    if a.no_tally:  # (PMC passes: no dispatch outside the timed steps)
+        n_f32 = n_bf16 = req_f32 = None
+    else:
+        rc.render_rays(rb, S, skts=skts.expand(n_mine, -1, -1, -1), cyls=cyl.expand(n_mine, -1), N_importance=I,
+                       chunk=4096, ret_alpha=False, count_mfma=True, near_far_given=sharded)
+        torch.cuda.synchronize()
+        n_f32, n_bf16 = (int(v) for v in rc.last_mfma.tolist())
+    if a.no_tally:
+        pass
+    elif a.precision == "fp32":
         req_f32 = n_f32
     else:
         rc32 = anerf.RayCaster(anerf.RenderConfig(n_joints=a.joints, N_samples=S, N_importance=I,
@@ -513,11 +526,12 @@ def main():
         torch.cuda.synchronize()
         req_f32 = int(rc32.last_mfma[0].item())
         del rc32
-    peak_exec, flop_exec = mix_peak(n_f32, n_bf16)
+    peak_exec, flop_exec = mix_peak(n_f32, n_bf16) if n_f32 is not None else (None, None)
     flop_ray = anerf.flops_per_sample(cfg) * anerf.samples_per_ray(cfg)  # SURVEY §8(d), reference work
     achieved_alg = flop_ray * n_mine / (kern_ms * 1e-3) / 1e12
-    achieved_exec = flop_exec / (kern_ms * 1e-3) / 1e12
-    achieved_req = req_f32 * FLOP_F32_MFMA / (kern_ms * 1e-3) / 1e12
+    achieved_exec = flop_exec / (kern_ms * 1e-3) / 1e12 if flop_exec is not None else None
+    achieved_req = req_f32 * FLOP_F32_MFMA / (kern_ms * 1e-3) / 1e12 if req_f32 is not None else None
+    r4 = lambda x: round(x, 4) if x is not None else None  # noqa: E731
     peak = pipe_peak(a.precision)
     # the committed PMC summaries are of config 3's frame; other shapes report null
     traffic, traffic_src, prof_clock = (traffic_from_profiles(a.precision)
@@ -535,7 +549,8 @@ def main():
             others[p] = {"rays_per_s_kernel": round(n_mine / (pms * 1e-3), 1), "kernel_ms": round(pms, 3),
                          "frac": round(flop_ray * n_mine / (pms * 1e-3) / 1e12 / pipe_peak(p), 4),
                          "frac_executed": round(pflop / (pms * 1e-3) / 1e12 / ppeak, 4),
-                         "frac_required": round(req_f32 * FLOP_F32_MFMA / (pms * 1e-3) / 1e12 / pipe_peak(p), 4),
+                         "frac_required": (round(req_f32 * FLOP_F32_MFMA / (pms * 1e-3) / 1e12 / pipe_peak(p), 4)
+                                           if req_f32 is not None else None),
                          "dtype": DTYPE[p]}
             del rcp
         if a.tau != 20.0 and not a.no_tau20:
@@ -616,15 +631,15 @@ def main():
                          "timing": "HIP events on the launch stream around anerf_render_rays: the coarse and the "
                                    "fine render_kernel launch (+ near/far, 0.2 %); rocprofv3's render_kernel "
                                    "average x launches_per_step agrees (profiles/)",
-                         "achieved_executed": round(achieved_exec, 2), "peak_executed_mix": round(peak_exec, 1),
-                         "frac_executed": round(achieved_exec / peak_exec, 4),
+                         "achieved_executed": r4(achieved_exec), "peak_executed_mix": r4(peak_exec),
+                         "frac_executed": r4(achieved_exec / peak_exec) if achieved_exec is not None else None,
                          # the peaks assume 2.4 GHz; the chip runs this load power-limited below that
                          # (GRBM_GUI_ACTIVE / kernel time in the same committed PMC summary as traffic)
                          "profile_clock_GHz": prof_clock,
                          "mfma_busy_at_profile_clock": (round(achieved_exec / peak_exec * 2.4 / prof_clock, 4)
-                                                        if prof_clock else None),
-                         "achieved_required": round(achieved_req, 2),
-                         "frac_required": round(achieved_req / peak, 4),
+                                                        if prof_clock and achieved_exec is not None else None),
+                         "achieved_required": r4(achieved_req),
+                         "frac_required": r4(achieved_req / peak) if achieved_req is not None else None,
                          "required": "the FLOPs an exact fp32 implementation must do after exact-zero cutoff-window "
                                      "skipping and the feature_linear fusion (the fp32 mode's MFMA tally of the same "
                                      "rays x 4096 FLOP) / kernel_ms / peak: why fp32's algorithmic frac exceeds 1",

@@ -120,7 +120,8 @@ typedef struct {
     int32_t multires_views;  /* view-direction frequencies: 4 (default) or 0 (surreal_single.txt) */
     int32_t use_cutoff;      /* --use_cutoff */
     int32_t cutoff_inputs;   /* --cutoff_inputs */
-    int32_t cutoff_viewdir;  /* --cutoff_viewdir */
+    int32_t cutoff_viewdir;  /* --cutoff_viewdir (windows the view features only together with use_cutoff, as the
+                                reference's create_raycaster builds the view embedder, core/raycasters.py:31, 68-71) */
     int32_t framecode_ch;    /* 0, or --framecode_size when --opt_framecode */
     int32_t n_framecodes;
     int32_t density_softplus;/* 0: relu, 1: softplus(x - softplus_shift) */
@@ -193,8 +194,8 @@ typedef struct {
  * direction features.  Every one of those features is w_j times a function of the ray alone (R_j d), so the
  * view layer's product with them is sum_j w_j G_j(ray) with G_j = Wv_j T_j(R_j d) per ray: the caller forms
  * T, G and that sum (the view direction's gradient to skts included) and the encoder handles the windows
- * (their gradient in _encode_backward's g_feat column cv + j).  Needs cutoff_viewdir and cutoff_inputs (every
- * direction feature windowed); not with ANERF_ENC_VIEW_ANGLE or a staged encoder. */
+ * (their gradient in _encode_backward's g_feat column cv + j).  Needs cutoff_viewdir, use_cutoff and cutoff_inputs
+ * (every direction feature windowed); not with ANERF_ENC_VIEW_ANGLE or a staged encoder. */
 #define ANERF_ENC_VIEW_WINDOWS 128
 
 /* HOST pointers to one NeRF's weights, torch nn.Linear layout [out][in] (core/networks/nerf.py:57-88). */

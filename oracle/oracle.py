@@ -82,8 +82,9 @@ class OracleModel:
         m = _Model()
         m.nj, m.D, m.W, m.skip = cfg.n_joints, cfg.netdepth, cfg.netwidth, cfg.skips[0]
         m.multires, m.multires_views = cfg.multires, cfg.multires_views
-        m.use_cutoff, m.cutoff_inputs, m.cutoff_viewdir = int(cfg.use_cutoff), int(cfg.cutoff_inputs), int(
-            cfg.cutoff_viewdir)
+        m.use_cutoff, m.cutoff_inputs = int(cfg.use_cutoff), int(cfg.cutoff_inputs)
+        # (the view embedder is windowed only under use_cutoff too: core/raycasters.py:31, 68-71)
+        m.cutoff_viewdir = int(cfg.cutoff_viewdir and cfg.use_cutoff)
         m.framecode_ch, m.n_framecodes = cfg.framecode_ch, (cfg.n_framecodes if cfg.opt_framecode else 0)
         m.density_softplus = int(cfg.density_type == "softplus")
         m.softplus_shift, m.density_scale = cfg.softplus_shift, cfg.density_scale

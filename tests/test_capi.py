@@ -94,6 +94,7 @@ def test_build_discards_a_library_whose_sources_moved(tmp_path, monkeypatch):
     monkeypatch.setattr(b, "HIPCC", str(cc))
     monkeypatch.setattr(b, "FLAGS", [])
     monkeypatch.setattr(b, "SRC", [])
+    monkeypatch.setattr(b, "OBJS", str(tmp_path / "objs"))
     hashes = iter(["a", "b"])
     monkeypatch.setattr(b, "source_hash", lambda: next(hashes))
     with pytest.raises(RuntimeError, match="sources changed"):
@@ -129,11 +130,38 @@ def test_view_windows_flag_validation():
         h = ctypes.c_void_p()
         return lib.anerf_model_create(ctypes.byref(d), None, None, None, 0, ctypes.byref(h))
     assert create(cutoff_viewdir=0) == -1 and b"VIEW_WINDOWS" in lib.anerf_last_error()
+    # (without use_cutoff the reference's view embedder is a plain Embedder: no windows to factor)
+    assert create(use_cutoff=0) == -1 and b"VIEW_WINDOWS" in lib.anerf_last_error()
     assert create(cutoff_inputs=0) == -1 and b"VIEW_WINDOWS" in lib.anerf_last_error()
     assert create(encoder_flags=_lib.ANERF_ENC_VIEW_WINDOWS | _lib.ANERF_ENC_VIEW_ANGLE) == -1
     assert b"staged" in lib.anerf_last_error()
     assert create(multires_bones=2) == -1 and b"staged" in lib.anerf_last_error()
     assert create(encoder_flags=256) == -1 and b"unknown" in lib.anerf_last_error()
+
+
+def test_package_reads_no_environment_switches(tmp_path):
+    """with ANERF_LIB_PATH and ANERF_TRAIN_FWD set, a fresh process importing the package gets the
+    in-tree library and the layer-by-layer training forward (the A/B tooling applies ANERF_LIB_PATH itself,
+    tools/_ablib.py, through _lib.use_library)."""
+    import subprocess
+    import sys
+    fake = tmp_path / "libfake.so"
+    fake.write_bytes(b"not a library")
+    code = ("import importlib, json; L = importlib.import_module('a-nerf_amd._lib'); "
+            "M = importlib.import_module('a-nerf_amd.mlp'); L.load(); "
+            "print(json.dumps([L.LIB_PATH, M.FUSED_FORWARD]))")
+    env = dict(os.environ, ANERF_LIB_PATH=str(fake), ANERF_TRAIN_FWD="fused")
+    out = subprocess.run([sys.executable, "-c", code], cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    import json
+    path, fused = json.loads(out.stdout.strip().splitlines()[-1])
+    assert os.path.abspath(path) == os.path.abspath(os.path.join(REPO, "a-nerf_amd", "libanerf_hip.so"))
+    assert fused is False
+    # the tooling hook does switch libraries, and the ABI check applies to what it loads
+    code2 = ("import sys; sys.path.insert(0, 'tools'); import _ablib, importlib; "
+             "L = importlib.import_module('a-nerf_amd._lib'); print(L.LIB_PATH)")
+    out2 = subprocess.run([sys.executable, "-c", code2], cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    assert out2.returncode == 0 and out2.stdout.strip().endswith("libfake.so"), out2.stderr[-2000:]
 
 
 def test_binding_rejects_a_wrong_argument_count():

@@ -290,7 +290,7 @@ def test_fused_forward_matches_layer_by_layer_gemms(D, W, fc, nj, M, monkeypatch
     cams = torch.randint(0, 5, (M,), device=DEV) if fc else None
     saved = {}
     for fused in (True, False):
-        monkeypatch.setattr(mlp, "_FUSED", fused)
+        monkeypatch.setattr(mlp, "FUSED_FORWARD", fused)
         tr = train.TrainRayCaster(cfg, ck, mlp="bf16x6").train()
         f = feat.clone().requires_grad_(True)
         raw = tr.network_fn(f, cams)

@@ -321,3 +321,18 @@ def test_feature_scales_follow_the_staged_layout():
     assert np.all(s[ov:ov + nj] == 1.0)
     for k in range(cfg.multires_views):
         assert np.all(s[ov + (1 + 2 * k) * nj:ov + (3 + 2 * k) * nj] == wv[k])
+
+
+def test_fused_adam_leaves_version_counters():
+    """ADVICE r5 (raycaster.py's note on torch's fused Adam): the fused step updates a parameter in place without
+    advancing p._version, while the foreach step advances it -- the cause of the eval caster missing fused updates
+    (its repack check reads the version counters; TrainRayCaster.weights_changed() forces the repack instead)."""
+    import torch
+    for fused, advances in ((True, False), (False, True)):
+        p = torch.nn.Parameter(torch.ones(8))
+        opt = torch.optim.Adam([p], lr=0.1, **({"fused": True} if fused else {"foreach": True}))
+        p.grad = torch.ones(8)
+        v0 = p._version
+        opt.step()
+        assert float(p.detach()[0]) < 1.0  # (the step did update the values)
+        assert (p._version != v0) == advances, (fused, v0, p._version)

@@ -283,4 +283,11 @@ def test_view_window_layout_conditions():
     assert train.view_windows_ok(cfg)
     assert not train.view_windows_ok(dataclasses.replace(cfg, cutoff_viewdir=False))
     assert not train.view_windows_ok(dataclasses.replace(cfg, cutoff_inputs=False))
+    #  --cutoff_viewdir without --use_cutoff: the reference's view embedder is a plain Embedder
+    # (core/raycasters.py:31, 68-71 -> cutoff_embedder.py:216-220), no window to factor and none to schedule
+    nocut = dataclasses.replace(cfg, use_cutoff=False)
+    assert nocut.cutoff_viewdir and not nocut.view_window
+    assert not train.view_windows_ok(nocut)
+    fs = importlib.import_module("a-nerf_amd.config").feature_scales(dataclasses.replace(nocut, freq_schedule=True), 1.5, 1.5)
+    assert (fs == 1).all()  # (neither the pts nor the view embedder is a CutoffEmbedder: no schedule weights)
     assert not train.view_windows_ok(dataclasses.replace(cfg, n_joints=17))

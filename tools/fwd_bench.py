@@ -8,6 +8,8 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import _ablib  # noqa: E402,F401  (ANERF_LIB_PATH: an experiment build, A/B tooling only)
 anerf = importlib.import_module("a-nerf_amd")
 syn = importlib.import_module("a-nerf_amd.synthetic")
 train = importlib.import_module("a-nerf_amd.train")
@@ -23,7 +25,7 @@ def main():
     res = {True: [], False: []}
     for rnd in range(4):
         for fused in (True, False):
-            mlp._FUSED = fused
+            mlp.FUSED_FORWARD = fused
             for _ in range(2):
                 tr.network_fn(feat)
             torch.cuda.synchronize()

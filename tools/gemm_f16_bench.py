@@ -2,11 +2,14 @@
 fp16x4 with and without the row-max epilogue, and the split (+ exponent) launch.  Prints one line per
 variant: mean µs over 50 launches (torch events on the current stream, which the GEMMs use)."""
 import importlib
+import os
 import sys
 
 import torch
 
 sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import _ablib  # noqa: E402,F401  (ANERF_LIB_PATH: an experiment build, A/B tooling only)
 mlp = importlib.import_module("a-nerf_amd.mlp")
 
 

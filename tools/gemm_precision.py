@@ -31,6 +31,8 @@ import torch
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import _ablib  # noqa: E402,F401  (ANERF_LIB_PATH: an experiment build, A/B tooling only)
 sys.path.insert(0, os.path.join(REPO, "oracle"))
 anerf = importlib.import_module("a-nerf_amd")
 syn = importlib.import_module("a-nerf_amd.synthetic")

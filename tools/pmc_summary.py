@@ -22,13 +22,18 @@ def rows(path, kernel="render_kernel"):
 
 
 def per_call(d, launches):
-    """sum every counter over the render_kernel dispatches, per render_rays call (`launches` launches)"""
+    """every counter summed over the LAST render_rays call's `launches` render_kernel dispatches (by dispatch id):
+    the timed step's.  The passes run `bench.py --no-tally`, so the run's only dispatches of this instance are its
+    warmup and timed steps; round 5's summary averaged in the untimed count_mfma tally call as well (VERDICT r5,
+    What's weak 3: 596 MB instead of the timed call's 459 MB)."""
+    ids = sorted(d, key=int)
+    if len(ids) % launches:
+        raise SystemExit(f"{len(ids)} dispatches is not a whole number of {launches}-launch calls")
     tot = {}
-    for v in d.values():
-        for k, x in v.items():
+    for i in ids[-launches:]:
+        for k, x in d[i].items():
             tot[k] = tot.get(k, 0.0) + x
-    calls = len(d) / launches
-    return {k: x / calls for k, x in tot.items()}, int(calls)
+    return tot, len(ids) // launches
 
 
 def main():
@@ -44,13 +49,13 @@ def main():
     clock = s["GRBM_GUI_ACTIVE"] / 8 / (s["ns"] * 1e-9) / 1e9
     busy = s["SQ_INSTS_MFMA"] / 1024 * 64 / (s["ns"] * 1e-9 * clock * 1e9)
     res = {
-        "kernel": "render_kernel<256,7> " + label,
+        "kernel": kern + " " + label,
         "precision": prec,
         "source": "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE | SQ_INSTS_VALU SQ_INSTS_MFMA SQ_WAVES SQ_BUSY_CYCLES "
-                  "GRBM_GUI_ACTIVE (separate passes) --kernel-trace -- python3 bench.py --steps 1 --warmup 0 --no-cpu "
-                  "--precision <precision>",
-        "unit": f"per render_rays call of one config-3 frame = {launches} render_kernel launches (coarse, fine); "
-                f"{calls} calls profiled",
+                  "GRBM_GUI_ACTIVE (separate passes) --kernel-trace -- python3 bench.py --steps 1 --warmup 1 --no-cpu "
+                  "--no-tally --precision <precision> (tools/gpu_pmc.sh)",
+        "unit": f"per render_rays call of one config-3 frame = {launches} render_kernel launches (coarse, fine) of the "
+                f"timed step (the last of the {calls} calls each pass made: warmup + timed, no MFMA-tally call)",
         "FETCH_SIZE_KB_per_launch": f["FETCH_SIZE"],
         "WRITE_SIZE_KB_per_launch": w["WRITE_SIZE"],
         "render_kernel_hbm_bytes_per_launch": int(hbm),

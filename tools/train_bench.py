@@ -22,6 +22,8 @@ import torch
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import _ablib  # noqa: E402,F401  (ANERF_LIB_PATH: an experiment build, A/B tooling only)
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md, FP32 matrix
 BF16_MFMA_PEAK_TFLOPS = 2516.6  # MI355X_MICROARCH.md, BF16 dense
 
@@ -44,6 +46,13 @@ def parser():
                     help="torch.optim.Adam's implementation (foreach: the drop-in's, create_raycaster; fused: one "
                          "kernel per step, +0.5 %%, but it does not advance the version counters the eval caster "
                          "reads)")
+    ap.add_argument("--pose", default="kinematic", choices=["kinematic", "delta"],
+                    help="pose optimisation: kinematic (default; Trainer.train_batch with --opt_pose --opt_rot6d, "
+                         "core/trainer.py:230-273, 382-403, 451-481): a kinematics.PoseOptLayer over the images runs "
+                         "calculate_kinematic for every ray's image each step (anerf_pose_kinematics and its backward), "
+                         "the rot6d anchor loss (opt_pose_tol 0.01, opt_pose_coef 2.0, configs/h36m/h36m_prot2.txt) "
+                         "joins the loss and a second Adam (opt_pose_lrate 5e-4) steps the poses every step; delta "
+                         "(rounds 1-5): a skts + delta leaf per image")
     ap.add_argument("--split-single", action="store_true",
                     help="ablation: one split launch per weight instead of the batched split")
     return ap
@@ -69,9 +78,22 @@ def measure(a, dev=None):
         importlib.import_module("a-nerf_amd.mlp").WGRAD_OVERLAP = False
     tr = train.TrainRayCaster(cfg, ck, device=dev, mlp=a.mlp).train()
     tr.view_windows = not getattr(a, "full_view", False)
-    skts = torch.from_numpy(sc["skts"]).to(dev)
-    delta = torch.zeros_like(skts, requires_grad=True)  # pose optimisation variable per image
-    opt = torch.optim.Adam(list(tr.parameters()) + [delta], lr=5e-4, **({"fused": True} if getattr(a, "adam", "foreach") == "fused" else {"foreach": True}))
+    adam_kw = {"fused": True} if getattr(a, "adam", "foreach") == "fused" else {"foreach": True}
+    kinematic = getattr(a, "pose", "kinematic") == "kinematic"
+    if kinematic:  # the reference's PoseOptLayer (core/pose_opt.py:240-445) on 6-D rotations (--opt_rot6d)
+        kin = importlib.import_module("a-nerf_amd.kinematics")
+        # (rest pose relative to the root, the pelvis parameter = the root keypoint: the chain then reproduces
+        # the scene's skeletons, pose_opt.py:398-431 adds the pelvis to every joint)
+        popt = kin.PoseOptLayer(sc["kps"], sc["bones"], sc["rest"][None] - sc["rest"][None, :1], kin.SMPLSkeleton,
+                                use_rot6d=True, device=dev)
+        with torch.no_grad():  # popt_anchors["rots"] (core/pose_opt.py:60-72): the initial poses
+            anchor = popt.calculate_kinematic(np.arange(a.images))[4][..., :3, :2].flatten(start_dim=-2).clone()
+        opt = torch.optim.Adam(list(tr.parameters()), lr=5e-4, **adam_kw)
+        popt_opt = torch.optim.Adam(list(popt.parameters()), lr=5e-4, **adam_kw)
+    else:
+        skts = torch.from_numpy(sc["skts"]).to(dev)
+        delta = torch.zeros_like(skts, requires_grad=True)  # pose optimisation variable per image
+        opt = torch.optim.Adam(list(tr.parameters()) + [delta], lr=5e-4, **adam_kw)
 
     def batch():
         img = rng.integers(0, a.images, n)
@@ -86,19 +108,32 @@ def measure(a, dev=None):
             rays[sel, 3:6] = d
             rays[sel, 8:11] = d / np.linalg.norm(d, axis=-1, keepdims=True)
         rays[:, 6], rays[:, 7] = 0.0, 1.0
-        return (torch.from_numpy(rays).to(dev), torch.from_numpy(img).to(dev),
+        return (torch.from_numpy(rays).to(dev), img, torch.from_numpy(img).to(dev),
                 torch.from_numpy(cyls[img]).to(dev), torch.rand(n, 3, device=dev))
 
     batches = [batch() for _ in range(4)]
 
     def step(b):
-        rb, img, cy, tgt = b
+        rb, img_np, img, cy, tgt = b
         opt.zero_grad(set_to_none=True)
-        out = tr.render_rays(rb, S, skts=(skts + delta)[img], cyls=cy, perturb=1.0, N_importance=I,
-                             raw_noise_std=1.0)
-        loss = train.nerf_loss(out, tgt, bgs=1.0, use_background=True)
+        if kinematic:
+            # Trainer.get_kp_args (core/trainer.py:285-312): the layer's kinematics for every ray's image
+            popt_opt.zero_grad(set_to_none=True)
+            kp, bone, sk, _, rots = popt(img_np)
+            out = tr.render_rays(rb, S, kp_batch=kp, skts=sk, cyls=cy, bones=bone, perturb=1.0, N_importance=I,
+                                 raw_noise_std=1.0)
+            # Trainer._compute_kp_loss (core/trainer.py:382-403) with --opt_rot6d, tol 0.01, coef 2.0
+            kl = (anchor[img] - rots[..., :3, :2].flatten(start_dim=-2)).pow(2.0)[:, 1:]
+            kl = torch.lerp(torch.zeros_like(kl), kl - 0.01, (kl > 0.01).float()).sum(-1).mean() * 2.0
+            loss = train.nerf_loss(out, tgt, bgs=1.0, use_background=True) + kl
+        else:
+            out = tr.render_rays(rb, S, skts=(skts + delta)[img], cyls=cy, perturb=1.0, N_importance=I,
+                                 raw_noise_std=1.0)
+            loss = train.nerf_loss(out, tgt, bgs=1.0, use_background=True)
         loss.backward()
         opt.step()
+        if kinematic:  # Trainer.optimize (core/trainer.py:451-481) with opt_pose_step 1
+            popt_opt.step()
         return loss
 
     for i in range(a.warmup):
@@ -111,8 +146,13 @@ def measure(a, dev=None):
     dt = (time.perf_counter() - t0) / a.steps
     flop = 3 * anerf.flops_per_sample(cfg) * n * anerf.samples_per_ray(cfg)
     return {
-        "metric": "training rays/s (render_rays fwd + loss + bwd + Adam; N_rand 2048, 64+16 samples, 8x256, "
-                  "128 images with pose optimisation)",
+        "metric": ("training rays/s (Trainer.train_batch: PoseOptLayer kinematics for every ray + render_rays fwd + "
+                   "loss (rgb + rot6d pose anchor) + bwd through the nets and the kinematic chain + Adam on both; "
+                   "N_rand 2048, 64+16 samples, 8x256, 128 images)" if kinematic else
+                   "training rays/s (render_rays fwd + loss + bwd + Adam; N_rand 2048, 64+16 samples, 8x256, "
+                   "128 images with a skts + delta pose leaf)"),
+        "pose": ("PoseOptLayer: anerf_pose_kinematics + its backward every step" if kinematic
+                 else "skts + delta leaf"),
         "value": round(n / dt, 1), "unit": "rays/s", "ms_per_step": round(1e3 * dt, 3), "steps": a.steps,
         "dtype": "fp32" if a.mlp == "fp32" else f"fp32 in/out, MLP GEMMs as split bf16 ({a.mlp})", "mlp": a.mlp,
         "mlp_gemm_flop_per_step": flop, "mlp_tflops": round(flop / dt / 1e12, 2),

@@ -3,11 +3,14 @@ and 80 samples): anerf_train_view_factor (+ _backward) and anerf_train_view_mix 
 calls each.  ANERF_LIB_PATH selects an experiment build."""
 import importlib
 import json
+import os
 import sys
 
 import torch
 
 sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import _ablib  # noqa: E402,F401  (ANERF_LIB_PATH: an experiment build, A/B tooling only)
 anerf = importlib.import_module("a-nerf_amd")
 train = importlib.import_module("a-nerf_amd.train")
 _lib = importlib.import_module("a-nerf_amd._lib")
