@@ -967,6 +967,347 @@ __global__ __launch_bounds__(1024) void split_exponent_kernel(SplitBatch b) {
     }
 }
 
+// ---------------------------------------------------------------- hidden layer backward, fused (round 6)
+// One launch per 256 x 256 hidden layer produces both products of its backward from ONE read of dY (the
+// layer's pre-activation gradient) and X (its input, the previous layer's relu output):
+//   dX = (dY W) * (X > 0)        the input gradient, relu' masked (what mlp_nt_kernel's backward epilogue does)
+//   dW = dY^T X, db = sum_m dY    the weight and bias gradients (what mlp_tn_kernel does)
+// The two-kernel schedule read dY and X twice (336 MB per layer at M = 163,840 in fp32) and ran the products on
+// two streams; here a persistent workgroup per CU owns a contiguous range of rows and walks it in 32-row chunks:
+// each chunk's dY and X are staged once into LDS as bf16 hi / lo planes (bf16x3, the backward's arithmetic in
+// the "mixed" mode) and feed both products.
+// Eight waves, two per SIMD (256 registers each).  Every wave w keeps rows 32 w .. 32 w + 31 of the workgroup's
+// 256 x 256 dW partial (8 tiles of 32 x 32, 128 accumulator registers) over the whole row range; it leaves once,
+// into a per-workgroup workspace slab summed in slab order by mlp_reduce_kernel (deterministic, no atomics).
+// The other work is split by role, one wave of each role per SIMD:
+//   * stager waves (0-3) load the next chunks' dY and X rows from HBM and split them into the LDS planes, a
+//     unit (one row piece) every other slot of the current chunk's compute, a whole chunk ahead;
+//   * dX waves (4-7) compute dX's columns 64 (w - 4) .. + 63 of every chunk, their B operand (the split W^T)
+//     from L2 as MFMA fragments one k16 step ahead.
+// The split keeps HBM loads out of the waves that wait on L2 loads: vector-memory loads of a wave complete in
+// order (vmcnt), so a wave that issued a chunk's HBM loads could not wait for a later W^T fragment before them.
+// LDS per chunk: dY hi, dY lo, X hi, X lo ([32][256] bf16 each, 512 B rows whose 16 B chunks are XOR-swizzled
+// by ((r & 3) << 2) | ((r >> 2) & 3): conflict-free for the transposed dW fragment reads (4 rows x 64 B per
+// lane group), the row-wise dX fragment reads (16 rows of one chunk per group) and the staging writes) and the
+// relu' mask bytes; two stages, plus the db column sums.
+constexpr int DGW_W = 256;                           // layer width (inputs = outputs)
+constexpr int DGW_CH = 32;                           // rows per chunk
+constexpr int DGW_THR = 512;                         // eight waves
+constexpr int DGW_PLANE = DGW_CH * DGW_W * 2;        // 16 KB: one bf16 plane [32][256]
+constexpr int DGW_MASKB = DGW_CH * DGW_W;            // 8 KB: relu' mask bytes [32][256]
+constexpr int DGW_STAGE = 4 * DGW_PLANE + DGW_MASKB;
+constexpr int DGW_BSUM = 8 * DGW_W * 4;              // 8 KB: the db column sums [8 staging rows][256]
+constexpr int DGW_LDS = 2 * DGW_STAGE + DGW_BSUM;    // 152 KB
+#ifndef ANERF_DGW_BD
+#define ANERF_DGW_BD 4
+#endif
+constexpr int DGW_BD = ANERF_DGW_BD;                 // W^T fragment ring depth (k16 steps)
+static_assert((DGW_W / 16) % DGW_BD == 0, "the W^T ring runs on across chunks: its depth divides the k16 steps");
+// (ANERF_DGW_PROBE, timing diagnostics of experiment builds only, wrong results: 1 no dX MFMAs, 2 no dW MFMAs,
+// 3 no W^T loads, 4 no chunk staging after the first)
+#ifndef ANERF_DGW_PROBE
+#define ANERF_DGW_PROBE 0
+#endif
+
+struct DGWArgs {
+    long long M, rows_per_wg;
+    const float* dy;
+    long long lddy;
+    const float* x;
+    long long ldx;
+    const unsigned short* wt;  // split W^T, bf16x3 planes (anerf_mlp_split_weights, transpose = 1)
+    float* dx;
+    long long lddx;
+    float* ws;   // [workgroups][256][256] dW partials
+    float* wsb;  // [workgroups][256] db partials
+};
+
+__device__ __forceinline__ int dgw_off(int row, int chunk) {
+    return row * 512 + ((chunk ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 4);
+}
+
+// 8 values -> bf16 hi (RNE) and lo (RNE of the exact remainder) at the same swizzled chunk of two planes
+__device__ __forceinline__ void dgw_split_store(const float (&v)[8], unsigned char* hi, unsigned char* lo, int off) {
+    u32x4 wh, wl;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const bf16x2 h = __builtin_convertvector((f32x2){v[2 * q], v[2 * q + 1]}, bf16x2);
+        wh[q] = __builtin_bit_cast(unsigned, h);
+        const bf16x2 l = __builtin_convertvector((f32x2){v[2 * q] - (float)h[0], v[2 * q + 1] - (float)h[1]}, bf16x2);
+        wl[q] = __builtin_bit_cast(unsigned, l);
+    }
+    *reinterpret_cast<u32x4*>(hi + off) = wh;
+    *reinterpret_cast<u32x4*>(lo + off) = wl;
+}
+
+__global__ __launch_bounds__(DGW_THR, 1) void mlp_dgw_kernel(DGWArgs g) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds8[];
+    // (the wave index as a uniform value: a buffer descriptor built from a per-lane value compiles to a
+    // waterfall loop around every load, and the role branches must be uniform)
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool stager = wave < 4;
+    const long long M = g.M;
+    const long long mlo = (long long)blockIdx.x * g.rows_per_wg;
+    const long long mhi = mlo + g.rows_per_wg < M ? mlo + g.rows_per_wg : M;
+    const int nch = mhi > mlo ? (int)((mhi - mlo + DGW_CH - 1) / DGW_CH) : 0;
+
+    // dW fragments (8 rows of one column) through the transpose read, as mlp_tn_kernel's: lane 4 q + p4 of each
+    // 16-lane group addresses row q (+ 4) at columns 16 g1 + 4 p4 of the 32-column block.  `ln` is the lane index
+    // re-pinned in every slot, so that no slot's address arithmetic is hoisted and kept live across the loop
+    int ln = lane;
+    auto tfrag = [&](const unsigned char* plane, int kk, int cb) {
+        const int h = ln >> 5, q = (ln >> 2) & 3, p4 = ln & 3, g1 = (ln >> 4) & 1;
+        const int row = 16 * kk + 8 * h + q, chunk = (cb >> 3) + 2 * g1 + (p4 >> 1);
+        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+            (lds_bf16x4*)(plane + dgw_off(row, chunk) + 8 * (p4 & 1)));
+        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+            (lds_bf16x4*)(plane + dgw_off(row + 4, chunk) + 8 * (p4 & 1)));
+        return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    };
+    // dX A fragments: row (lane & 31) of the chunk, k = 16 kt + 8 (lane >> 5) .. + 7 (one ds_read_b128)
+    auto rfrag = [&](const unsigned char* plane, int kt) {
+        return *reinterpret_cast<const bf16x8*>(plane + dgw_off(ln & 31, 2 * kt + (ln >> 5)));
+    };
+    auto pin_lane = [&]() {
+        ln = lane;
+        asm volatile("" : "+v"(ln));
+    };
+
+    f32x16 aw[8];  // dW rows 32 w .., columns 32 ib ..
+#pragma unroll
+    for (int j = 0; j < 8; ++j) aw[j] = f32x16{0};
+    // the dW work of slot t (kk = t / 8, ib = t % 8), A fragments of the k16 step in `ad`
+    auto dw_slot = [&](const unsigned char* S, int t, bf16x8 (&ad)[2]) {
+        const int kk = t >> 3, ib = t & 7;
+        if (ib == 0) {
+#pragma unroll
+            for (int p = 0; p < 2; ++p) ad[p] = tfrag(S + p * DGW_PLANE, kk, 32 * wave);
+        }
+        const bf16x8 bx0 = tfrag(S + 2 * DGW_PLANE, kk, 32 * ib), bx1 = tfrag(S + 3 * DGW_PLANE, kk, 32 * ib);
+        if (ANERF_DGW_PROBE != 2) {
+            f32x16 c = mfma(ad[1], bx0, aw[ib]);
+            c = mfma(ad[0], bx1, c);
+            aw[ib] = mfma(ad[0], bx0, c);
+        }
+    };
+
+    if (stager) {
+        // ------------------------------------------------------------------ stager waves
+        // staging: thread t < 256 -> columns c8 .. c8 + 7 of rows sr + 8 u (u < 4) of dY and X: 8 units (u, operand)
+        // of two float4 loads each (a wave instruction reads two whole rows)
+        const int c8 = 8 * (tid & 31), sr = tid >> 5;
+        const long long lddy = g.lddy, ldx = g.ldx;
+        const float* const dyp = g.dy;
+        const float* const xp = g.x;
+        const unsigned voy = (unsigned)((sr * lddy + c8) * 4), vox = (unsigned)((sr * ldx + c8) * 4);
+        const int ystep = (int)(8 * lddy * 4), xstep = (int)(8 * ldx * 4);
+        f32x4 R[8][2];  // unit k = 2 u + operand (0: dY, 1: X)
+        // (chunk rows past the workgroup's range read zero: the descriptors end at its last row; one lane offset per
+        // operand, the row step and the 16 B piece in the uniform offset)
+        auto fetch_unit = [&](int s, int k) {
+            const long long r0 = mlo + (long long)s * DGW_CH;
+            long long rows = mhi - r0;
+            rows = rows < 0 ? 0 : (rows > DGW_CH ? DGW_CH : rows);
+            const int u = k >> 1;
+            const float* const base = (k & 1) ? xp + r0 * ldx : dyp + r0 * lddy;
+            const long long ld = (k & 1) ? ldx : lddy;
+            const __amdgpu_buffer_rsrc_t rs =
+                __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)(rows * ld * 4), 0x00020000);
+            const unsigned vo = (k & 1) ? vox : voy;
+            const int step = (k & 1) ? xstep : ystep;
+#pragma unroll
+            for (int f = 0; f < 2; ++f)
+                R[k][f] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo, u * step + 16 * f, 0));
+        };
+        // db: the thread's running column sums of its staging rows, in LDS (its own 32 B of [8][256])
+        float* const bsum = reinterpret_cast<float*>(lds8 + 2 * DGW_STAGE) + sr * DGW_W + c8;
+        *reinterpret_cast<f32x4*>(bsum) = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        *reinterpret_cast<f32x4*>(bsum + 4) = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        auto stage_unit = [&](int buf, int k) {
+            unsigned char* const S = lds8 + buf * DGW_STAGE;
+            const int r = sr + 8 * (k >> 1);
+            const int off = dgw_off(r, c8 >> 3);
+            float v[8];
+#pragma unroll
+            for (int f = 0; f < 2; ++f)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    // (through float rvalues: clang's bit_cast of a vector-element lvalue reads element 0)
+                    const float t = R[k][f][e];
+                    v[4 * f + e] = t;
+                }
+            if (k & 1) {
+                dgw_split_store(v, S + 2 * DGW_PLANE, S + 3 * DGW_PLANE, off);
+                unsigned mk[2] = {0u, 0u};
+#pragma unroll
+                for (int e = 0; e < 8; ++e)
+                    if (v[e] > 0.0f) mk[e >> 2] |= 1u << (8 * (e & 3));
+                typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+                *reinterpret_cast<u32x2*>(S + 4 * DGW_PLANE + r * DGW_W + c8) = u32x2{mk[0], mk[1]};
+            } else {
+                f32x4 b0 = *reinterpret_cast<const f32x4*>(bsum), b1 = *reinterpret_cast<const f32x4*>(bsum + 4);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    b0[e] += v[e];
+                    b1[e] += v[4 + e];
+                }
+                *reinterpret_cast<f32x4*>(bsum) = b0;
+                *reinterpret_cast<f32x4*>(bsum + 4) = b1;
+                dgw_split_store(v, S, S + DGW_PLANE, off);
+            }
+        };
+        if (nch > 0) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) fetch_unit(0, k);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) stage_unit(0, k);
+        }
+        if (nch > 1) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) fetch_unit(1, k);
+        }
+        __syncthreads();
+        for (int s = 0; s < nch; ++s) {
+            const unsigned char* const S = lds8 + (s & 1) * DGW_STAGE;
+            bf16x8 ad[2];
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+                __builtin_amdgcn_sched_barrier(0);
+                pin_lane();
+                // unit t / 2 of the next chunk into the other stage (free since the barrier that ended chunk s - 1),
+                // then its loads for the chunk after: a whole chunk of compute to land
+                if (ANERF_DGW_PROBE != 4 && (t & 1) == 0) {
+                    if (s + 1 < nch) stage_unit((s + 1) & 1, t >> 1);
+                    if (s + 2 < nch) fetch_unit(s + 2, t >> 1);
+                }
+                dw_slot(S, t, ad);
+            }
+            __syncthreads();
+        }
+    } else {
+        // ------------------------------------------------------------------ dX waves
+        const int xw = wave - 4;  // dX columns 64 xw .. 64 xw + 63: blocks 2 xw, 2 xw + 1
+        const long long lddx = g.lddx;
+        // the split W^T (fragment-major: 32-column block nb, k16 step ks, plane p = 1 KB in lane order) of the
+        // wave's two blocks (a buffer descriptor: the lane's 16 B in the lane offset, the step in the uniform one)
+        constexpr int WBS = (DGW_W / 16) * 2 * 512;  // elements per 32-column block
+        const __amdgpu_buffer_rsrc_t rwt =
+            __builtin_amdgcn_make_buffer_rsrc((void*)(g.wt + (long long)(2 * xw) * WBS), 0, 2 * WBS * 2, 0x00020000);
+        const unsigned vwl = (unsigned)lane * 16;
+        struct WF {
+            u32x4 v[2][2];  // [block][plane]
+        };
+        // (the fragments of k16 step kt are the same for every chunk: the ring runs on across the chunks, so the
+        // first steps of chunk s + 1 are in flight before chunk s's dX stores, which count in vmcnt with them)
+        auto fetch_w = [&](int kt, WF& f) {
+            kt &= DGW_W / 16 - 1;
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int p = 0; p < 2; ++p) {
+#if ANERF_DGW_PROBE == 3
+                    f.v[j][p] = u32x4{vwl, vwl, vwl, (unsigned)kt};
+#else
+                    f.v[j][p] = __builtin_bit_cast(
+                        u32x4, __builtin_amdgcn_raw_buffer_load_b128(rwt, vwl, j * WBS * 2 + (kt * 2 + p) * 1024, 0));
+#endif
+                }
+        };
+        WF wf[DGW_BD];
+#pragma unroll
+        for (int j = 0; j < DGW_BD - 1; ++j) fetch_w(j, wf[j]);
+        __syncthreads();
+        for (int s = 0; s < nch; ++s) {
+            const unsigned char* const S = lds8 + (s & 1) * DGW_STAGE;
+            f32x16 ax[2] = {f32x16{0}, f32x16{0}};
+            bf16x8 ad[2];
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+                __builtin_amdgcn_sched_barrier(0);
+                pin_lane();
+                fetch_w(t + DGW_BD - 1, wf[(t + DGW_BD - 1) % DGW_BD]);
+                const bf16x8 ay0 = rfrag(S, t), ay1 = rfrag(S + DGW_PLANE, t);
+                const WF& f = wf[t % DGW_BD];
+                if (ANERF_DGW_PROBE != 1) {
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {  // small terms first
+                        const bf16x8 b0 = __builtin_bit_cast(bf16x8, f.v[j][0]), b1 = __builtin_bit_cast(bf16x8, f.v[j][1]);
+                        f32x16 c = mfma(ay1, b0, ax[j]);
+                        c = mfma(ay0, b1, c);
+                        ax[j] = mfma(ay0, b0, c);
+                    }
+                }
+                dw_slot(S, t, ad);
+            }
+            // dX epilogue: relu' mask bytes from LDS, buffer stores straight from the accumulator layout (a wave
+            // instruction writes two whole 128 B row pieces; the descriptor ends at the chunk's last row, so the
+            // rows past the workgroup's range are dropped without a branch, and the row offsets ride in SGPRs)
+            const long long r0 = mlo + (long long)s * DGW_CH;
+            long long rows = mhi - r0;
+            rows = rows > DGW_CH ? DGW_CH : rows;
+            const __amdgpu_buffer_rsrc_t rd =
+                __builtin_amdgcn_make_buffer_rsrc((void*)(g.dx + r0 * lddx), 0, (int)(rows * lddx * 4), 0x00020000);
+            const unsigned char* const mk = S + 4 * DGW_PLANE;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int col = 64 * xw + 32 * j + (lane & 31);
+                const unsigned vo = (unsigned)((4 * (lane >> 5) * lddx + col) * 4);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int rr = (r & 3) + 8 * (r >> 2);
+                    const float v = mk[(rr + 4 * (lane >> 5)) * DGW_W + col] ? ax[j][r] : 0.0f;
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rd, vo, (int)(rr * lddx * 4),
+                                                          0);
+                }
+            }
+            __syncthreads();
+        }
+    }
+    // the dW partial: [256][256] floats of this workgroup, straight from the accumulators (buffer stores, the
+    // per-register row and block offsets in SGPRs)
+    {
+        const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(g.ws + (long long)blockIdx.x * DGW_W * DGW_W), 0, DGW_W * DGW_W * 4, 0x00020000);
+        const unsigned vo = (unsigned)(((32 * wave + 4 * (lane >> 5)) * DGW_W + (lane & 31)) * 4);
+#pragma unroll
+        for (int ib = 0; ib < 8; ++ib)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int rr = (r & 3) + 8 * (r >> 2);
+                const float v = aw[ib][r];
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rw, vo,
+                                                      (rr * DGW_W + 32 * ib) * 4, 0);
+            }
+    }
+    // db partial: the 8 staging rows' column sums, added in a fixed order
+    const float* const red = reinterpret_cast<const float*>(lds8 + 2 * DGW_STAGE);  // [8][256]
+    __syncthreads();
+    if (tid < DGW_W) {
+        float t = red[tid];
+#pragma unroll
+        for (int w = 1; w < 8; ++w) t += red[w * DGW_W + tid];
+        g.wsb[(long long)blockIdx.x * DGW_W + tid] = t;
+    }
+}
+
+// rows per workgroup: one persistent workgroup per CU over whole 32-row chunks
+int dgw_plan(int64_t m, long long* rows_per_wg) {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) ==
+                                                    hipSuccess && n > 0)
+            cus = n;
+        else
+            cus = 256;
+    }
+    long long chunks = (m + DGW_CH - 1) / DGW_CH;
+    if (chunks < 1) chunks = 1;
+    const long long per = (chunks + cus - 1) / cus;  // chunks per workgroup
+    *rows_per_wg = per * DGW_CH;
+    return (int)((chunks + per - 1) / per);
+}
+
 inline int rup(long long x, int a) { return (int)((x + a - 1) / a * a); }
 
 int planes_of(int precision) {
@@ -1190,6 +1531,56 @@ int anerf_mlp_gemm_rows(int64_t m, int32_t n, int32_t k, const anerf_seg* a, int
     ANERF_NT_LAUNCH(2, 2)
     ANERF_NT_LAUNCH(2, 3)
 #undef ANERF_NT_LAUNCH
+    e = hipGetLastError();
+    return e == hipSuccess ? ANERF_OK : anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));
+}
+
+size_t anerf_mlp_backward_hidden_workspace(int64_t m, int32_t width) {
+    if (width != DGW_W || m < 0) return 0;
+    long long rows;
+    const int nwg = dgw_plan(m, &rows);
+    return (size_t)4 * nwg * (DGW_W * DGW_W + DGW_W);
+}
+
+int anerf_mlp_backward_hidden(int64_t m, int32_t width, const float* dy, int64_t lddy, const float* x, int64_t ldx,
+                              const void* wt_split, int32_t precision, float* dx, int64_t lddx, float* dw, int64_t lddw,
+                              float* db, void* workspace, size_t workspace_bytes, void* stream) {
+    if (width != DGW_W || precision != ANERF_MLP_BF16X3)
+        return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_backward_hidden: width 256 and ANERF_MLP_BF16X3 only");
+    if (m < 0 || !dy || !x || !wt_split || !dx || !dw || !db || lddw < width)
+        return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_backward_hidden: bad arguments");
+    // (float4 loads of whole rows; a 32-row chunk's byte range fits a buffer descriptor)
+    if ((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(x)) & 15 || (lddy | ldx) & 3 || lddy < width ||
+        ldx < width || lddx < width || lddy >= (1 << 22) || ldx >= (1 << 22) || lddx >= (1 << 22))
+        return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_backward_hidden: dy / x need 16 B aligned rows, "
+                                                 "ld % 4 == 0, width <= ld < 2^22 (dx: width <= ld < 2^22)");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (m == 0) {
+        hipError_t e = hipMemset2DAsync(dw, lddw * 4, 0, (size_t)width * 4, width, st);
+        if (e == hipSuccess) e = hipMemsetAsync(db, 0, (size_t)width * 4, st);
+        return e == hipSuccess ? ANERF_OK : anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));
+    }
+    if (!workspace || workspace_bytes < anerf_mlp_backward_hidden_workspace(m, width))
+        return anerf_internal_fail(ANERF_EWORKSPACE, "anerf_mlp_backward_hidden: workspace too small");
+    DGWArgs g = {};
+    const int nwg = dgw_plan(m, &g.rows_per_wg);
+    g.M = m;
+    g.dy = dy;
+    g.lddy = lddy;
+    g.x = x;
+    g.ldx = ldx;
+    g.wt = static_cast<const unsigned short*>(wt_split);
+    g.dx = dx;
+    g.lddx = lddx;
+    g.ws = static_cast<float*>(workspace);
+    g.wsb = g.ws + (size_t)nwg * DGW_W * DGW_W;
+    hipError_t e = hipFuncSetAttribute((const void*)mlp_dgw_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, DGW_LDS);
+    if (e != hipSuccess) return anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));
+    hipLaunchKernelGGL(mlp_dgw_kernel, dim3((unsigned)nwg), dim3(DGW_THR), DGW_LDS, st, g);
+    // dW rows 0 .. 255 and the bias row 256, summed over the workgroups' slabs in order
+    hipLaunchKernelGGL(mlp_reduce_kernel, dim3(DGW_W / 128, DGW_W + 1), dim3(256), 0, st, g.ws, nwg,
+                       (long long)DGW_W * DGW_W, (long long)DGW_W, DGW_W, dw, (long long)lddw, 0, DGW_W, g.wsb,
+                       (long long)DGW_W, DGW_W, db);
     e = hipGetLastError();
     return e == hipSuccess ? ANERF_OK : anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));
 }

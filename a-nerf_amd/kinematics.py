@@ -92,6 +92,18 @@ class _Kinematics(torch.autograd.Function):
         return gb, gp, None, None, None, None, None, None, None
 
 
+def _dev_index(idx, device):
+    """Host indices -> a device int64 tensor without a host synchronisation: a pageable copy waits for the stream
+    to drain (the training step's per-ray image indices arrive every step, Trainer.get_kp_args), so the indices go
+    through pinned memory and a non-blocking copy.  A device tensor passes through."""
+    if isinstance(idx, torch.Tensor):
+        return idx.to(device=device, dtype=torch.long).view(-1)
+    a = torch.from_numpy(np.ascontiguousarray(np.asarray(idx), dtype=np.int64).reshape(-1))
+    if torch.device(device).type != "cuda":
+        return a.to(device)
+    return a.pin_memory().to(device, non_blocking=True)
+
+
 def _dev_f32_grad(x, device):
     """float32 contiguous device tensor that keeps the autograd graph of a tensor input."""
     if isinstance(x, torch.Tensor):
@@ -192,7 +204,7 @@ class PoseOptLayer(torch.nn.Module):
             self.update_cache()
 
     def idx_to_params(self, idx):
-        idx = torch.as_tensor(np.asarray(idx), dtype=torch.long, device=self.device).view(-1)
+        idx = _dev_index(idx, self.device)
         pelvis = self.pelvis[idx]
         if self.kp_map is None:
             return pelvis, self.bones[idx]
@@ -227,7 +239,7 @@ class PoseOptLayer(torch.nn.Module):
         o = pose_kinematics(bone, rest, self.skel_type, pelvis=pelvis, rest_idx=ridx, device=self.device)
         if len(uniq) == len(idxs) and np.array_equal(uniq, idxs):
             return o["kps"], bone, o["skts"], o["l2ws"], o["rots"]
-        g = torch.as_tensor(inv.reshape(-1), dtype=torch.long, device=self.device)
+        g = _dev_index(inv, self.device)
         return o["kps"][g], bone[g], o["skts"][g], o["l2ws"][g], o["rots"][g]
 
     @torch.no_grad()
@@ -238,7 +250,7 @@ class PoseOptLayer(torch.nn.Module):
     def forward(self, idxs, rest_pose_idxs=None):
         if not self.use_cache:
             return self.calculate_kinematic(idxs, rest_pose_idxs)
-        i = torch.as_tensor(np.asarray(idxs), dtype=torch.long, device=self.device)
+        i = _dev_index(idxs, self.device)
         return self.cache_kps[i], self.cache_bones[i], self.cache_skts[i], self.cache_l2ws[i], self.cache_rots[i]
 
     def get_bones(self, idx=None):

@@ -42,6 +42,13 @@ def _stream(dev):
 WGRAD_OVERLAP = True
 _SIDE = {}
 
+# (round 6) the backward of every 256 x 256 hidden layer (input not the skip layer's [x | h]) as ONE kernel,
+# anerf_mlp_backward_hidden: dY and the saved activation are read once for the input gradient (relu' masked)
+# and the weight + bias gradients, instead of the input-gradient GEMM on this stream and the weight-gradient
+# GEMM on the side stream each reading both.  bf16x3 backward arithmetic only (the "mixed" default); an A/B
+# switch for tools/train_bench.py, never read from the environment
+FUSED_BACKWARD = True
+
 
 def _side_stream(dev):
     key = torch.device(dev).index
@@ -300,7 +307,22 @@ class _MLP(torch.autograd.Function):
         # the trunk, last layer first
         segx = _seg(feat, dnet)
         wrote_x = False
+        fused = FUSED_BACKWARD and prec == 3 and W == 256
+        fws = None
         for i in range(D - 1, -1, -1):
+            if fused and i >= 1 and i - 1 != skip:  # one pass: gprev, dW, db (anerf_mlp_backward_hidden)
+                if fws is None:
+                    fws = torch.empty(lib.anerf_mlp_backward_hidden_workspace(M, W), device=dev, dtype=torch.uint8)
+                gprev = torch.empty(M, W, **f32)
+                dw, db = torch.empty(W, W, **f32), torch.empty(W, **f32)
+                _lib.check(lib.anerf_mlp_backward_hidden(M, W, _lib.ptr(gz), gz.stride(0), _lib.ptr(H[i - 1]),
+                                                         H[i - 1].stride(0), _lib.ptr(st[i]), prec, _lib.ptr(gprev),
+                                                         gprev.stride(0), _lib.ptr(dw), dw.stride(0), _lib.ptr(db),
+                                                         _lib.ptr(fws), fws.numel(), _stream(dev)),
+                           "anerf_mlp_backward_hidden")
+                grads[2 * i], grads[2 * i + 1] = dw, db
+                gz = gprev
+                continue
             if i == 0:
                 a, k = [segx], dnet
             elif i - 1 == skip:

@@ -46,6 +46,7 @@
  *   anerf_mlp_split_weights_batch   the same for up to 32 weights in one launch
  *   anerf_mlp_gemm          forward (bias, relu) and input-gradient (relu' mask, accumulate) products
  *   anerf_mlp_wgrad         weight + bias gradients
+ *   anerf_mlp_backward_hidden  both of a 256 x 256 hidden layer's backward products in one pass (round 6)
  *   anerf_mlp_forward(_pack)  the whole forward in one kernel (opt-in alternative to the GEMMs)
  */
 #ifndef ANERF_H
@@ -58,7 +59,7 @@
 extern "C" {
 #endif
 
-#define ANERF_ABI_VERSION 16
+#define ANERF_ABI_VERSION 17
 
 enum {
     ANERF_OK = 0,
@@ -589,6 +590,21 @@ size_t anerf_mlp_wgrad_workspace(int64_t m, int32_t n, int32_t k);
 int anerf_mlp_wgrad(int64_t m, int32_t n, int32_t k, const float* dy, int64_t lddy, const anerf_seg* x, int32_t n_x,
                     int32_t precision, float* dw, int64_t lddw, float* db, int32_t accumulate, void* workspace,
                     size_t workspace_bytes, void* stream);
+
+/* Workspace bytes of anerf_mlp_backward_hidden (0 for an unsupported width). */
+size_t anerf_mlp_backward_hidden_workspace(int64_t m, int32_t width);
+/* The backward of one hidden layer y = relu(x W^T + b) of width 256 (pts_linears[i], i not after the skip,
+ * core/networks/nerf.py:133-139; its autograd in the reference), from its pre-activation gradient dy [m][256]
+ * and its input x [m][256] (the previous layer's relu output), in ONE pass over both:
+ *   dx[m][i] = (sum_o dy[m][o] W[o][i]) if x[m][i] > 0 else 0    (the input gradient, relu' masked by x)
+ *   dw[o][i] = sum_m dy[m][o] x[m][i],  db[o] = sum_m dy[m][o]    (written, not accumulated)
+ * wt_split: W's transposed planes from anerf_mlp_split_weights(W, 256, 256, ld, transpose 1, precision).
+ * precision: ANERF_MLP_BF16X3 (the "mixed" mode's backward arithmetic, as anerf_mlp_gemm / _wgrad).  The
+ * same sums as anerf_mlp_gemm (input gradient with the relu' mask) + anerf_mlp_wgrad in another summation order;
+ * deterministic (per-workgroup slabs summed in order).  dy, x: 16 B aligned, ld % 4 == 0, 256 <= ld < 2^22. */
+int anerf_mlp_backward_hidden(int64_t m, int32_t width, const float* dy, int64_t lddy, const float* x, int64_t ldx,
+                              const void* wt_split, int32_t precision, float* dx, int64_t lddx, float* dw, int64_t lddw,
+                              float* db, void* workspace, size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

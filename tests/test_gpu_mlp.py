@@ -308,3 +308,90 @@ def test_fused_forward_matches_layer_by_layer_gemms(D, W, fc, nj, M, monkeypatch
     for i, (a, b) in enumerate(zip(sa, sb)):  # feat, codes, hf, g, whead, h_0 .. h_{D-1}, params
         assert a.shape == b.shape
         close(a, b, f"saved tensor {i}")
+
+
+def _backward_hidden(m, dy, x, w, lddx=None):
+    """anerf_mlp_backward_hidden on dy [m][256] and x [m][256] (strided views allowed) with W [256][256]."""
+    lib = mlp._lib.load()
+    dev = torch.device(DEV)
+    wt = mlp.split_weight(w, True, 3)
+    dx = torch.full((m, lddx or 256), float("nan"), device=DEV)
+    dw, db = torch.empty(256, 256, device=DEV), torch.empty(256, device=DEV)
+    ws = torch.empty(lib.anerf_mlp_backward_hidden_workspace(m, 256), device=DEV, dtype=torch.uint8)
+    mlp._lib.check(lib.anerf_mlp_backward_hidden(m, 256, mlp._lib.ptr(dy), dy.stride(0), mlp._lib.ptr(x), x.stride(0),
+                                                 mlp._lib.ptr(wt), 3, mlp._lib.ptr(dx), dx.stride(0), mlp._lib.ptr(dw),
+                                                 256, mlp._lib.ptr(db), mlp._lib.ptr(ws), ws.numel(),
+                                                 mlp._stream(dev)), "anerf_mlp_backward_hidden")
+    return dx, dw, db
+
+
+@pytest.mark.parametrize("m", [163840, 131072, 5000, 777, 33, 1, 300001])
+def test_backward_hidden_matches_fp64(m):
+    """Round 6: the fused hidden-layer backward (one pass over dY and X) against fp64 torch of the same sums, at
+    the bf16x3 bounds of the two GEMMs it replaces: dX = (dY W) masked by X > 0 (test_gemm_input_gradient_*),
+    dW = dY^T X and db = sum dY (test_wgrad_and_bias_gradient); ragged m (not a multiple of the 32-row chunk,
+    fewer rows than workgroups, more chunks per workgroup than the training step's) and strided rows."""
+    torch.manual_seed(m % 1000)
+    dy = torch.randn(m, 260, device=DEV)[:, :256]        # (ld 260)
+    x = torch.relu(torch.randn(m, 264, device=DEV))[:, :256]  # (ld 264; half the entries exactly 0)
+    w = torch.randn(256, 256, device=DEV) / 16
+    dx, dw, db = _backward_hidden(m, dy, x, w, lddx=257)
+    full = dy.double() @ w.double()
+    ref_dx = torch.where(x > 0, full, torch.zeros_like(full))
+    bound = _bound(dy, w.t(), 3)
+    assert not torch.isnan(dx[:, :256]).any()
+    assert torch.all((dx[:, :256].double() - ref_dx).abs() <= bound), float((dx[:, :256].double() - ref_dx).abs().max())
+    assert torch.isnan(dx[:, 256]).all()  # (the padding column of the output rows is never written)
+    ref_w = dy.double().t() @ x.double()
+    bw = 2 * REL[3] * (dy.double().abs().t() @ x.double().abs()) + 1e-5
+    assert torch.all((dw.double() - ref_w).abs() <= bw), float((dw.double() - ref_w).abs().max())
+    ref_b = dy.double().sum(0)
+    assert torch.all((db.double() - ref_b).abs() <= 1e-5 * dy.double().abs().sum(0) + 1e-5)
+
+
+def test_backward_hidden_matches_the_two_gemms():
+    """The fused pass and the two kernels it replaces (anerf_mlp_gemm with the relu' mask + anerf_mlp_wgrad, bf16x3)
+    compute the same bf16x3 products: dX agrees to fp32 summation-order noise and the relu' mask exactly; dW, db to
+    fp32 summation order over 163,840 rows.  Deterministic: a second call is bit-identical."""
+    torch.manual_seed(5)
+    m = 163840
+    dy = torch.randn(m, 256, device=DEV)
+    x = torch.relu(torch.randn(m, 256, device=DEV))
+    w = torch.randn(256, 256, device=DEV) / 16
+    dx, dw, db = _backward_hidden(m, dy, x, w)
+    dx2, dw2, db2 = _backward_hidden(m, dy, x, w)
+    assert torch.equal(dx, dx2) and torch.equal(dw, dw2) and torch.equal(db, db2)
+    lib = mlp._lib.load()
+    ref_dx = torch.empty(m, 256, device=DEV)
+    mlp.gemm(m, 256, 256, [mlp._seg(dy, 256)], mlp.split_weight(w, True, 3), None, False,
+             [(ref_dx, 256, 256, 0, x, False)], torch.device(DEV), 3)
+    ws = torch.empty(lib.anerf_mlp_wgrad_workspace(m, 256, 256), device=DEV, dtype=torch.uint8)
+    ref_dw, ref_db = torch.empty(256, 256, device=DEV), torch.empty(256, device=DEV)
+    mlp.wgrad(m, 256, 256, dy, [mlp._seg(x, 256)], ref_dw, ref_db, ws, torch.device(DEV), 3)
+    assert torch.equal(dx == 0, ref_dx == 0)
+    scale = float(ref_dx.abs().max())
+    assert float((dx - ref_dx).abs().max()) <= 1e-6 * scale
+    assert float((dw - ref_dw).abs().max()) <= 2e-6 * float(ref_dw.abs().max())
+    assert float((db - ref_db).abs().max()) <= 2e-6 * float(ref_db.abs().max())
+
+
+def test_backward_hidden_rejects_bad_arguments():
+    lib = mlp._lib.load()
+    m = 64
+    dy, x = torch.randn(m, 256, device=DEV), torch.randn(m, 256, device=DEV)
+    out = torch.empty(m, 256, device=DEV)
+    dw, db = torch.empty(256, 256, device=DEV), torch.empty(256, device=DEV)
+    ws = torch.empty(lib.anerf_mlp_backward_hidden_workspace(m, 256), device=DEV, dtype=torch.uint8)
+    wt = mlp.split_weight(torch.randn(256, 256, device=DEV), True, 3)
+    P = mlp._lib.ptr
+    st = mlp._stream(torch.device(DEV))
+    assert lib.anerf_mlp_backward_hidden_workspace(m, 128) == 0
+    assert lib.anerf_mlp_backward_hidden(m, 128, P(dy), 256, P(x), 256, P(wt), 3, P(out), 256, P(dw), 256, P(db),
+                                         P(ws), ws.numel(), st) == -1
+    assert lib.anerf_mlp_backward_hidden(m, 256, P(dy), 256, P(x), 256, P(wt), 6, P(out), 256, P(dw), 256, P(db),
+                                         P(ws), ws.numel(), st) == -1
+    bad = torch.randn(m * 256 + 1, device=DEV)[1:].view(m, 256)  # (rows not 16 B aligned)
+    assert lib.anerf_mlp_backward_hidden(m, 256, P(bad), 256, P(x), 256, P(wt), 3, P(out), 256, P(dw), 256, P(db),
+                                         P(ws), ws.numel(), st) == -1
+    assert lib.anerf_mlp_backward_hidden(m, 256, P(dy), 256, P(x), 256, P(wt), 3, P(out), 256, P(dw), 256, P(db),
+                                         P(ws), 16, st) == -3  # (ANERF_EWORKSPACE)

@@ -25,7 +25,7 @@ train = importlib.import_module("a-nerf_amd.train")
 
 TRAIN = ["t1_s32i16_d4w128", "t2_s64i16_d8w256", "t3_softplus_fc", "t4_tau200", "t5_single_mrv0",
          "t6_lindisp_raynoise", "t7_single_raynoise", "t8_freqsched", "t9_cutto_shift", "t10_cutoffbones",
-         "t11_mr5_mrv2_world", "t12_staged_relpos_rayangle_mrb2", "t13_querypts_shift"]
+         "t11_mr5_mrv2_world", "t12_staged_relpos_rayangle_mrb2", "t13_querypts_shift", "t14_nj65_d8w256"]
 TOL = 1e-4
 TOL_ALPHA = 2e-3
 GRAD_REL = 2e-3

@@ -40,6 +40,8 @@ def parser():
                     help="training MLP arithmetic (train.TrainRayCaster mlp=)")
     ap.add_argument("--no-wgrad-overlap", action="store_true",
                     help="ablation: the weight gradients on the caller's stream (mlp.WGRAD_OVERLAP off)")
+    ap.add_argument("--no-fused-backward", action="store_true",
+                    help="ablation: the hidden layers' backward as the two GEMMs (mlp.FUSED_BACKWARD off)")
     ap.add_argument("--full-view", action="store_true",
                     help="ablation: the full view columns instead of the view-window layout (TrainRayCaster.view_windows)")
     ap.add_argument("--adam", default="foreach", choices=["fused", "foreach"],
@@ -76,6 +78,7 @@ def measure(a, dev=None):
     rng = np.random.default_rng(0)
     if getattr(a, "no_wgrad_overlap", False):
         importlib.import_module("a-nerf_amd.mlp").WGRAD_OVERLAP = False
+    importlib.import_module("a-nerf_amd.mlp").FUSED_BACKWARD = not getattr(a, "no_fused_backward", False)
     tr = train.TrainRayCaster(cfg, ck, device=dev, mlp=a.mlp).train()
     tr.view_windows = not getattr(a, "full_view", False)
     adam_kw = {"fused": True} if getattr(a, "adam", "foreach") == "fused" else {"foreach": True}
@@ -167,6 +170,10 @@ def measure(a, dev=None):
                            "bf16x6": "fp32-accurate forward and gradients", "bf16x3": "~16-bit operands",
                            "fp32": "torch fp32 GEMMs"}[a.mlp],
         "adam": getattr(a, "adam", "foreach"),
+        "hidden_backward": ("fused (anerf_mlp_backward_hidden: input + weight gradients from one read of dY and H)"
+                            if importlib.import_module("a-nerf_amd.mlp").FUSED_BACKWARD and a.mlp in ("mixed", "bf16x3",
+                                                                                                    "mixed16")
+                            else "two GEMMs (anerf_mlp_gemm + anerf_mlp_wgrad)"),
         "view_layout": ("view windows (anerf.h ANERF_ENC_VIEW_WINDOWS: 24 windows per sample + per-ray factors)"
                         if tr.model.view_windows else "full view columns (648 per sample)"),
         "data": "synthetic (seeded SMPL-24 poses, 128 cameras on a circle, seeded weights)"}
