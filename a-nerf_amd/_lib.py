@@ -228,6 +228,9 @@ SIGNATURES = {
                                            ctypes.c_void_p, ctypes.c_void_p]),
     "anerf_mlp_wgrad_workspace": (ctypes.c_size_t, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]),
     "anerf_mlp_backward_hidden_workspace": (ctypes.c_size_t, [ctypes.c_int64, ctypes.c_int32]),
+    "anerf_mlp_backward_hidden_reduce": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p, ctypes.c_size_t,
+                                                        ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                                                        ctypes.c_void_p]),
     "anerf_mlp_backward_hidden": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64,
                                                  ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32,
                                                  ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,

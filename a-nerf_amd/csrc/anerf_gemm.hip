@@ -1547,7 +1547,7 @@ int anerf_mlp_backward_hidden(int64_t m, int32_t width, const float* dy, int64_t
                               float* db, void* workspace, size_t workspace_bytes, void* stream) {
     if (width != DGW_W || precision != ANERF_MLP_BF16X3)
         return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_backward_hidden: width 256 and ANERF_MLP_BF16X3 only");
-    if (m < 0 || !dy || !x || !wt_split || !dx || !dw || !db || lddw < width)
+    if (m < 0 || !dy || !x || !wt_split || !dx || (!dw != !db) || (dw && lddw < width))
         return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_backward_hidden: bad arguments");
     // (float4 loads of whole rows; a 32-row chunk's byte range fits a buffer descriptor)
     if ((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(x)) & 15 || (lddy | ldx) & 3 || lddy < width ||
@@ -1555,13 +1555,13 @@ int anerf_mlp_backward_hidden(int64_t m, int32_t width, const float* dy, int64_t
         return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_backward_hidden: dy / x need 16 B aligned rows, "
                                                  "ld % 4 == 0, width <= ld < 2^22 (dx: width <= ld < 2^22)");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    if (m == 0) {
-        hipError_t e = hipMemset2DAsync(dw, lddw * 4, 0, (size_t)width * 4, width, st);
-        if (e == hipSuccess) e = hipMemsetAsync(db, 0, (size_t)width * 4, st);
-        return e == hipSuccess ? ANERF_OK : anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));
-    }
     if (!workspace || workspace_bytes < anerf_mlp_backward_hidden_workspace(m, width))
         return anerf_internal_fail(ANERF_EWORKSPACE, "anerf_mlp_backward_hidden: workspace too small");
+    if (m == 0) {  // (the slabs of an empty sum: one zero slab, so that a deferred reduce writes zeros)
+        hipError_t e = hipMemsetAsync(workspace, 0, anerf_mlp_backward_hidden_workspace(m, width), st);
+        if (e != hipSuccess) return anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));
+        return dw ? anerf_mlp_backward_hidden_reduce(m, width, workspace, workspace_bytes, dw, lddw, db, stream) : ANERF_OK;
+    }
     DGWArgs g = {};
     const int nwg = dgw_plan(m, &g.rows_per_wg);
     g.M = m;
@@ -1577,11 +1577,26 @@ int anerf_mlp_backward_hidden(int64_t m, int32_t width, const float* dy, int64_t
     hipError_t e = hipFuncSetAttribute((const void*)mlp_dgw_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, DGW_LDS);
     if (e != hipSuccess) return anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));
     hipLaunchKernelGGL(mlp_dgw_kernel, dim3((unsigned)nwg), dim3(DGW_THR), DGW_LDS, st, g);
-    // dW rows 0 .. 255 and the bias row 256, summed over the workgroups' slabs in order
-    hipLaunchKernelGGL(mlp_reduce_kernel, dim3(DGW_W / 128, DGW_W + 1), dim3(256), 0, st, g.ws, nwg,
-                       (long long)DGW_W * DGW_W, (long long)DGW_W, DGW_W, dw, (long long)lddw, 0, DGW_W, g.wsb,
-                       (long long)DGW_W, DGW_W, db);
     e = hipGetLastError();
+    if (e != hipSuccess) return anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));
+    return dw ? anerf_mlp_backward_hidden_reduce(m, width, workspace, workspace_bytes, dw, lddw, db, stream) : ANERF_OK;
+}
+
+int anerf_mlp_backward_hidden_reduce(int64_t m, int32_t width, const void* workspace, size_t workspace_bytes, float* dw,
+                                     int64_t lddw, float* db, void* stream) {
+    if (width != DGW_W || m < 0 || !dw || !db || lddw < width)
+        return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_backward_hidden_reduce: bad arguments");
+    if (!workspace || workspace_bytes < anerf_mlp_backward_hidden_workspace(m, width))
+        return anerf_internal_fail(ANERF_EWORKSPACE, "anerf_mlp_backward_hidden_reduce: workspace too small");
+    long long rows;
+    const int nwg = dgw_plan(m, &rows);
+    const float* ws = static_cast<const float*>(workspace);
+    // dW rows 0 .. 255 and the bias row 256, summed over the workgroups' slabs in order
+    hipLaunchKernelGGL(mlp_reduce_kernel, dim3(DGW_W / 128, DGW_W + 1), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), ws, nwg, (long long)DGW_W * DGW_W, (long long)DGW_W,
+                       DGW_W, dw, (long long)lddw, 0, DGW_W, ws + (size_t)nwg * DGW_W * DGW_W, (long long)DGW_W, DGW_W,
+                       db);
+    hipError_t e = hipGetLastError();
     return e == hipSuccess ? ANERF_OK : anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));
 }
 

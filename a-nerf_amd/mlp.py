@@ -308,18 +308,37 @@ class _MLP(torch.autograd.Function):
         segx = _seg(feat, dnet)
         wrote_x = False
         fused = FUSED_BACKWARD and prec == 3 and W == 256
-        fws = None
+        fws, fev, nfused = [None, None], [None, None], 0
         for i in range(D - 1, -1, -1):
             if fused and i >= 1 and i - 1 != skip:  # one pass: gprev, dW, db (anerf_mlp_backward_hidden)
-                if fws is None:
-                    fws = torch.empty(lib.anerf_mlp_backward_hidden_workspace(M, W), device=dev, dtype=torch.uint8)
+                # two workspaces in turn: layer i's slabs are summed on the side stream (its reduce beside the next
+                # layer's pass) while layer i - 1 writes the other; a workspace is reused once its reduce is done
+                slot = nfused & 1
+                nfused += 1
+                if fws[slot] is None:
+                    fws[slot] = torch.empty(lib.anerf_mlp_backward_hidden_workspace(M, W), device=dev,
+                                            dtype=torch.uint8)
+                if fev[slot] is not None:
+                    main.wait_event(fev[slot])
+                ws_l = fws[slot]
                 gprev = torch.empty(M, W, **f32)
                 dw, db = torch.empty(W, W, **f32), torch.empty(W, **f32)
+                defer = side is not None
                 _lib.check(lib.anerf_mlp_backward_hidden(M, W, _lib.ptr(gz), gz.stride(0), _lib.ptr(H[i - 1]),
                                                          H[i - 1].stride(0), _lib.ptr(st[i]), prec, _lib.ptr(gprev),
-                                                         gprev.stride(0), _lib.ptr(dw), dw.stride(0), _lib.ptr(db),
-                                                         _lib.ptr(fws), fws.numel(), _stream(dev)),
-                           "anerf_mlp_backward_hidden")
+                                                         gprev.stride(0), None if defer else _lib.ptr(dw), dw.stride(0),
+                                                         None if defer else _lib.ptr(db), _lib.ptr(ws_l),
+                                                         ws_l.numel(), _stream(dev)), "anerf_mlp_backward_hidden")
+                if defer:
+                    side.wait_stream(main)
+                    with torch.cuda.stream(side):
+                        _lib.check(lib.anerf_mlp_backward_hidden_reduce(M, W, _lib.ptr(ws_l), ws_l.numel(),
+                                                                        _lib.ptr(dw), dw.stride(0), _lib.ptr(db),
+                                                                        _stream(dev)), "anerf_mlp_backward_hidden_reduce")
+                        fev[slot] = torch.cuda.Event()
+                        fev[slot].record(side)
+                    for t in (dw, db, ws_l):
+                        t.record_stream(side)
                 grads[2 * i], grads[2 * i + 1] = dw, db
                 gz = gprev
                 continue

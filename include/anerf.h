@@ -601,10 +601,15 @@ size_t anerf_mlp_backward_hidden_workspace(int64_t m, int32_t width);
  * wt_split: W's transposed planes from anerf_mlp_split_weights(W, 256, 256, ld, transpose 1, precision).
  * precision: ANERF_MLP_BF16X3 (the "mixed" mode's backward arithmetic, as anerf_mlp_gemm / _wgrad).  The
  * same sums as anerf_mlp_gemm (input gradient with the relu' mask) + anerf_mlp_wgrad in another summation order;
- * deterministic (per-workgroup slabs summed in order).  dy, x: 16 B aligned, ld % 4 == 0, 256 <= ld < 2^22. */
+ * deterministic (per-workgroup slabs summed in order).  dy, x: 16 B aligned, ld % 4 == 0, 256 <= ld < 2^22.
+ * dw = db = NULL: the weight and bias gradients stay as slabs in the workspace for a later
+ * anerf_mlp_backward_hidden_reduce (on another stream, beside the next layer's pass). */
 int anerf_mlp_backward_hidden(int64_t m, int32_t width, const float* dy, int64_t lddy, const float* x, int64_t ldx,
                               const void* wt_split, int32_t precision, float* dx, int64_t lddx, float* dw, int64_t lddw,
                               float* db, void* workspace, size_t workspace_bytes, void* stream);
+/* dw, db of an anerf_mlp_backward_hidden call made with dw = db = NULL, from its workspace (same m, width). */
+int anerf_mlp_backward_hidden_reduce(int64_t m, int32_t width, const void* workspace, size_t workspace_bytes, float* dw,
+                                     int64_t lddw, float* db, void* stream);
 
 #ifdef __cplusplus
 }

@@ -395,3 +395,33 @@ def test_backward_hidden_rejects_bad_arguments():
                                          P(ws), ws.numel(), st) == -1
     assert lib.anerf_mlp_backward_hidden(m, 256, P(dy), 256, P(x), 256, P(wt), 3, P(out), 256, P(dw), 256, P(db),
                                          P(ws), 16, st) == -3  # (ANERF_EWORKSPACE)
+
+
+def test_backward_hidden_deferred_reduce_is_identical():
+    """dw = db = NULL leaves the slabs in the workspace; anerf_mlp_backward_hidden_reduce (on another stream, as
+    mlp.py runs it beside the next layer) gives the same bits as the in-call reduce.  m = 0: zeros."""
+    lib = mlp._lib.load()
+    P = mlp._lib.ptr
+    dev = torch.device(DEV)
+    for m in (20000, 0):
+        torch.manual_seed(7)
+        dy = torch.randn(max(m, 1), 256, device=DEV)
+        x = torch.relu(torch.randn(max(m, 1), 256, device=DEV))
+        wt = mlp.split_weight(torch.randn(256, 256, device=DEV) / 16, True, 3)
+        dx = torch.empty(max(m, 1), 256, device=DEV)
+        ws = torch.empty(lib.anerf_mlp_backward_hidden_workspace(m, 256), device=DEV, dtype=torch.uint8)
+        dw0, db0 = torch.full((256, 256), 7.0, device=DEV), torch.full((256,), 7.0, device=DEV)
+        mlp._lib.check(lib.anerf_mlp_backward_hidden(m, 256, P(dy), 256, P(x), 256, P(wt), 3, P(dx), 256, P(dw0), 256,
+                                                     P(db0), P(ws), ws.numel(), mlp._stream(dev)), "direct")
+        mlp._lib.check(lib.anerf_mlp_backward_hidden(m, 256, P(dy), 256, P(x), 256, P(wt), 3, P(dx), 256, None, 256,
+                                                     None, P(ws), ws.numel(), mlp._stream(dev)), "deferred")
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        dw1, db1 = torch.full((256, 256), 3.0, device=DEV), torch.full((256,), 3.0, device=DEV)
+        with torch.cuda.stream(side):
+            mlp._lib.check(lib.anerf_mlp_backward_hidden_reduce(m, 256, P(ws), ws.numel(), P(dw1), 256, P(db1),
+                                                                mlp._stream(dev)), "reduce")
+        torch.cuda.synchronize()
+        assert torch.equal(dw0, dw1) and torch.equal(db0, db1)
+        if m == 0:
+            assert not dw1.any() and not db1.any()
