@@ -512,6 +512,13 @@ __device__ __forceinline__ void split2_pair(float a, float b, float t, H3T& T, i
 #ifndef ANERF_F8_X1W1
 #define ANERF_F8_X1W1 0
 #endif
+// (round 6, experiment switch, off) the hidden layers' per-sample fp16 scale from a bound formed by the previous
+// layer (mlp_layer_h3): measured -0.6 % (1.2048 vs 1.2118 M rays/s, three alternating runs on one box, outputs
+// unchanged to 1e-8, profiles/r06i_ab_h3_bound.txt): the converts' maxima and 40 B/lane more scratch cost what
+// the drain before the scale saved
+#ifndef ANERF_H3_BOUND
+#define ANERF_H3_BOUND 0
+#endif
 template <bool HI_WORD>
 __device__ __forceinline__ void split2_pair_f8(float a, float b, float t, H3T& T, int q, unsigned& x8) {
     typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
@@ -582,6 +589,19 @@ __device__ __forceinline__ f32x16 mfma_h3(const float (&w)[16], int half, const 
 // bit patterns, 0 for all-negative / zero inputs; NaN stays large) over this lane's and the partner
 // lane's values, scaled into [2^10, 2^11).  es: exponent of the units the input is in; on return the units of this layer's
 // output, es + shift + ew, kept within [-100, 60] so that bias * 2^es stays finite.
+// h3_scale_bits: the same from m, the bit pattern of a sample's largest relu'd input -- or of a bound on it (the
+// scaled maximum then lies at or below [2^10, 2^11): never above, the fp16 MFMA's range stays safe).
+__device__ __forceinline__ float h3_scale_bits(int m, int& es, int ew, int top, int cap = 60) {
+    int shift = m > 0 ? top - (m >> 23) : 0;  // (m >> 23: the biased exponent; top = 127 + 10)
+    // (cap: the skip layer's h part keeps its output units at most 2^cap, so that the fp16 x parts'
+    // features, scaled into those units, stay in range: enc16_units)
+    shift = max(shift, -100 - es - ew);
+    shift = min(shift, cap - es - ew);
+    shift = min(max(shift, -126), 126);
+    es += shift + ew;
+    return pow2f(shift);
+}
+
 template <int RBI>
 __device__ __forceinline__ float h3_scale(const f32x16 (&a)[RBI], int& es, int ew, int top, int cap = 60) {
     int m = 0;
@@ -595,25 +615,26 @@ __device__ __forceinline__ float h3_scale(const f32x16 (&a)[RBI], int& es, int e
             m = max(m, __builtin_bit_cast(int, v));
         }
     m = max(m, __shfl_xor(m, 32));
-    int shift = m > 0 ? top - (m >> 23) : 0;  // (m >> 23: the biased exponent; top = 127 + 10)
-    // (cap: the skip layer's h part keeps its output units at most 2^cap, so that the fp16 x parts'
-    // features, scaled into those units, stay in range: enc16_units)
-    shift = max(shift, -100 - es - ew);
-    shift = min(shift, cap - es - ew);
-    shift = min(max(shift, -126), 126);
-    es += shift + ew;
-    return pow2f(shift);
+    return h3_scale_bits(m, es, ew, top, cap);
 }
 
 // mlp_layer_x6's schedule with 8-float groups (3 MFMAs each), two groups per ring slot (slot
 // (g / 2) % 4, prefetched 3 slots = 6 groups ahead).  OUT_SAME layers alias out and ain; bias * 2^es
 // initialises the outputs.  ALPHA folds sig += w_alpha . h with h in the INPUT's units.
+// (round 6) Bound-based scale: with use_bnd the per-sample scale comes from *bnd, a bound on the sample's largest
+// relu'd input (bit pattern, in the input's units) that the PREVIOUS layer formed in the middle of its MFMAs,
+// instead of the maximum over all 128 inputs, which needed every MFMA of the previous layer to retire first
+// (h3_scale: the drain at each layer boundary).  A hidden layer (OUT_SAME, RBO == RBI) with rsum > 0 forms the
+// bound for the next: the true maximum M of its relu'd inputs (taken as its converts run, both lanes of the
+// sample) through |y_i| <= sum_k |W_ik| |x_k| + |b_i| <= rsum M + bmax (rsum, bmax: host constants of this
+// layer, real units), in the output's units and widened by 2^-10 for the fp32 rounding of its own arithmetic.
 template <int RBO, int RBI, bool OUT_SAME, bool ALPHA, int NP = 3>
 __device__ __forceinline__ void mlp_layer_h3(f32x16 (&out)[RBO], f32x16 (&ain)[RBI], f32x16 (&h)[RBI],
                                              const float* __restrict__ bias, const float* __restrict__ wp, int lane,
                                              Ring& ring, bool preloaded, const float* __restrict__ next,
                                              const float* __restrict__ wa, float& sig, int& es, int ew, int top,
-                                             int cap = 60, const float* __restrict__ w8 = nullptr) {
+                                             int cap = 60, const float* __restrict__ w8 = nullptr, bool use_bnd = false,
+                                             int* bnd = nullptr, float rsum = -1.0f, float bmax = 0.0f) {
     static_assert(RBO <= RBI, "h3 layer shape");
     // F8: fp16x4 with x1 w1 as one v_mfma_scale_f32_32x32x64_f8f6f4 (e4m3) per output block and pair of
     // input blocks (64 k) instead of four f16 MFMAs: w8 holds the e4m3 w1 groups (pack_layer_f8)
@@ -633,12 +654,21 @@ __device__ __forceinline__ void mlp_layer_h3(f32x16 (&out)[RBO], f32x16 (&ain)[R
 #if ANERF_X6_PROBE == 4  // (diagnostic builds of tools/probe only: no per-sample scale)
     const float t = 1.0f;
 #else
-    const float t = h3_scale<RBI>(ain, es, ew, top, cap);
+    const float t = use_bnd ? h3_scale_bits(*bnd, es, ew, top, cap) : h3_scale<RBI>(ain, es, ew, top, cap);
 #endif
     const float S = pow2f(es);
+    constexpr bool MKB = OUT_SAME && RBO == RBI;  // (hidden layers: the true input maximum for the next bound)
+    int mx = 0;
     auto convert_half = [&](int rb, int half) {  // relu of 8 inputs (+ their 8 scaled bias outputs)
 #pragma unroll
         for (int i = 8 * half; i < 8 * half + 8; ++i) h[rb][i] = relu_act(ain[rb][i]);
+        if constexpr (MKB) {  // (integer maxima of the bit patterns, three operands each)
+#pragma unroll
+            for (int i = 8 * half; i < 8 * half + 8; i += 2) {
+                const float a = h[rb][i], b = h[rb][i + 1];
+                mx = max(mx, max(__builtin_bit_cast(int, a), __builtin_bit_cast(int, b)));
+            }
+        }
         if (OUT_SAME && rb < RBO) {
             const f32x4* p = reinterpret_cast<const f32x4*>(bias + (rb * 2 + hh) * 16 + 8 * half);
             const f32x4 v0 = p[0], v1 = p[1];
@@ -726,6 +756,14 @@ __device__ __forceinline__ void mlp_layer_h3(f32x16 (&out)[RBO], f32x16 (&ain)[R
                     split_block_pair(1, p, Tn);
         }
         h3_group_schedule<NPG, ANERF_H3_LEAD_IL>();
+    }
+    if constexpr (MKB) {  // every input converted: the next layer's bound, under this layer's MFMAs
+        if (bnd) {
+            mx = max(mx, __shfl_xor(mx, 32));
+            const float M = __builtin_bit_cast(float, mx) * t * pow2f(ew);  // (output units; powers of two: exact)
+            const float B = fmaf(rsum, M, bmax * S) * (1.0f + 0x1p-10f);
+            *bnd = rsum > 0.0f ? __builtin_bit_cast(int, B) : -1;
+        }
     }
 #pragma clang loop unroll(full)
     for (int ib = 1; ib < RBI; ++ib) {
@@ -1684,7 +1722,7 @@ __device__ __forceinline__ bool mlp_trunk(const ModelDev& M, const NetDev& net, 
                                           const float* __restrict__ bias, float* __restrict__ uf,
                                           float* __restrict__ wvo, f32x16 (&acc)[W / 32], f32x16 (&h)[W / 32],
                                           Ring& ring, JointMask& mask, const float* __restrict__ after_last,
-                                          Stamps& st, int& es) {
+                                          Stamps& st, int& es, int* bnd = nullptr, bool* have_bnd = nullptr) {
     constexpr int RB = W / 32;
     const int hh = lane >> 5;
     float nosig = 0.0f;
@@ -1743,6 +1781,9 @@ __device__ __forceinline__ bool mlp_trunk(const ModelDev& M, const NetDev& net, 
     }
     STAMP(st, 9);
     bool pre6 = false;
+    // fp16 modes (ANERF_H3_BOUND): layer L >= 2 takes its scale from the bound layer L - 1 formed, unless L - 1 is the
+    // skip layer (its x parts join the output after the h part; their features have no bound here)
+    bool hb = false;
     for (int L = 1; L < M.D; ++L) {
         const float* after = L + 1 < M.D ? wl[L + 1] : after_last;
         const bool skl = (L == M.skip + 1);
@@ -1766,9 +1807,12 @@ __device__ __forceinline__ bool mlp_trunk(const ModelDev& M, const NetDev& net, 
             // skip layer's x parts, which load themselves and scale their B operands by 2^es (the
             // units the h part left in the accumulators)
             const float* nxth = skl ? nullptr : after;
+            const bool use = ANERF_H3_BOUND && bnd && hb;
             mlp_layer_h3<RB, RB, true, false, P == 4 ? 4 : 3>(acc, acc, h, bias + L * W, wl[L], lane, ring, pre6, nxth, nullptr,
                                               nosig, es, net.ewl[L], M.h3_top, (skl && enc16) ? net.enc_cap : 60,
-                                              net.wl8[L]);
+                                              net.wl8[L], use, ANERF_H3_BOUND ? bnd : nullptr,
+                                              skl ? -1.0f : net.hrsum[L], net.hbmax[L]);
+            hb = !skl;
             pre6 = nxth != nullptr;
             if (skl) {  // the f32 skip x parts take their first groups from the ring (the x6 one loads itself)
                 if (!ux6) ring_preload<2 * RB>(ring, net.wskipu, lane);
@@ -1818,6 +1862,7 @@ __device__ __forceinline__ bool mlp_trunk(const ModelDev& M, const NetDev& net, 
             STAMP(st, 12);
         }
     }
+    if (have_bnd) *have_bnd = ANERF_H3_BOUND && bnd && hb && M.D > 1;
     return pre6;  // (bf16x6 / fp16x3: after_last's first groups are in the ring)
 }
 
@@ -1844,8 +1889,11 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
     JointMask mask;
     Ring ring;
     int es = 0;
+    int bnd = -1;
+    bool have_bnd = false;
     const bool pre = mlp_trunk<W, MR, true, P>(M, net, sk, cut, px, py, pz, lane, bias, uf, wvp, acc, h, ring, mask,
-                                               P >= 3 ? net.wviewh : (P == 2 ? net.wview6 : net.wview), st, es);
+                                               P >= 3 ? net.wviewh : (P == 2 ? net.wview6 : net.wview), st, es,
+                                               P >= 3 ? &bnd : nullptr, &have_bnd);
     // views_linears.0 with feature_linear fused in (W' = Wv_f Wf, see pack_net) on relu(h_last),
     // alpha_linear folded into its groups (same relu'd B operands), + the factorised
     // direction / code / bias part from G, then relu
@@ -1854,7 +1902,8 @@ __device__ void mlp_block(const ModelDev& M, const NetDev& net, const float* __r
     if constexpr (P >= 3) {
         const int es_h = es;  // the alpha head sums the last hidden layer's activations, in its units
         mlp_layer_h3<RBV, RB, false, true, P == 4 ? 4 : 3>(av, acc, h, nullptr, net.wviewh, lane, ring, pre, nullptr,
-                                           bias + (M.D + 1) * W, sig, es, net.ew_view, M.h3_top, 60, net.wview8);
+                                           bias + (M.D + 1) * W, sig, es, net.ew_view, M.h3_top, 60, net.wview8,
+                                           have_bnd, &bnd);
         sig *= pow2f(-es_h);
     } else if constexpr (P == 2)
         mlp_layer_x6<RBV, RB, false, true>(av, acc, h, nullptr, net.wview6, lane, ring, pre, nullptr,

@@ -715,6 +715,27 @@ static int pack_net(const anerf_model_desc* d, int njh2, const anerf_net_weights
         offs.push_back((size_t)(int64_t)ewv);
         offs.push_back(has ? pk.add(pack_vpart_h(Wp, W, ld, nj, mr, mrl, ewv)) : (size_t)-1);
     }
+    // (round 6) the fp16 modes' scale bounds of each hidden layer's h part (mlp_layer_h3): max_i sum_k |W_ik| and
+    // max_i |b_i|, summed in double and rounded up to float (bit patterns, read back by bind_net)
+    for (int i = 1; i < d->net_depth; ++i) {
+        const bool sk = (i == d->skip + 1);
+        const int ld = sk ? cin + W : W, c0 = sk ? cin : 0;
+        double rs = 0.0, bm = 0.0;
+        for (int r = 0; r < W; ++r) {
+            double s = 0.0;
+            for (int c = 0; c < W; ++c) s += std::fabs((double)w->pts_w[i][(size_t)r * ld + c0 + c]);
+            rs = std::max(rs, s);
+            bm = std::max(bm, std::fabs((double)w->pts_b[i][r]));
+        }
+        float rf = (float)rs, bf = (float)bm;
+        if ((double)rf < rs) rf = std::nextafter(rf, INFINITY);
+        if ((double)bf < bm) bf = std::nextafter(bf, INFINITY);
+        uint32_t ur, ub;
+        std::memcpy(&ur, &rf, 4);
+        std::memcpy(&ub, &bf, 4);
+        offs.push_back((size_t)ur);
+        offs.push_back((size_t)ub);
+    }
     return ANERF_OK;
 }
 
@@ -765,6 +786,11 @@ static void bind_net(const anerf_model_desc* d, const float* base, const std::ve
         nd.ewh_v[part] = (int)(int64_t)o[k++];
         nd.wvh[part] = o[k] == (size_t)-1 ? nullptr : base + o[k];
         ++k;
+    }
+    for (int i = 1; i < D; ++i) {
+        const uint32_t ur = (uint32_t)o[k++], ub = (uint32_t)o[k++];
+        std::memcpy(&nd.hrsum[i], &ur, 4);
+        std::memcpy(&nd.hbmax[i], &ub, 4);
     }
     nd.balpha = balpha;
 }

@@ -68,6 +68,9 @@ struct NetDev {
     const float* wlh[MAXL];  // [i>0] activation parts as fp16x3 fragments (pack_layer_h3), scaled by 2^ewl[i]
     const float* wviewh;     // wview as fp16x3 fragments, scaled by 2^ew_view
     int ewl[MAXL], ew_view;
+    // (round 6) per hidden layer (h part only): max_i sum_k |W_ik| and max_i |b_i| (real units, rounded up), the
+    // next layer's scale bound (mlp_layer_h3)
+    float hrsum[MAXL], hbmax[MAXL];
     // fp16 encoder-fed parts (ModelDev::enc16): [0] layer 0, [1] the skip layer (null without one); the
     // bone-direction (u) and windowed (v) weights scaled by 2^ewh_u / 2^ewh_v (pack_upart_h, pack_vpart_h)
     const float* wuh[2];

@@ -585,6 +585,12 @@ def main():
         import train_bench
         training = train_bench.measure(train_bench.parser().parse_args(["--steps", "10", "--warmup", "2"]), dev=dev)
         training.pop("data", None)
+        # BASELINE config 4's 65-joint skeleton in the same step: the full view columns (the
+        # view-window layout needs NJ W / 2 <= 4096 and 16-byte feature segments, train.view_windows_ok)
+        t65 = train_bench.measure(train_bench.parser().parse_args(["--steps", "6", "--warmup", "2", "--joints", "65"]),
+                                  dev=dev)
+        training["joints65"] = {k: t65[k] for k in ("value", "ms_per_step", "joints", "view_layout")}
+        torch.cuda.empty_cache()
 
     # parity at every N (rank 0: the all-gathered frame in pixels mode, its own frame in frames mode); the
     # CPU baseline at N = 1 only

@@ -34,6 +34,9 @@ def parser():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--rays", type=int, default=2048)
     ap.add_argument("--images", type=int, default=128)
+    ap.add_argument("--joints", type=int, default=24,
+                    help="skeleton joints: 24 (SMPL) or more (synthetic skeleton, e.g. 65 = BASELINE config 4's "
+                         "LDS-pressure case)")
     ap.add_argument("--samples", type=int, default=64)
     ap.add_argument("--importance", type=int, default=16)
     ap.add_argument("--mlp", default="mixed", choices=["mixed", "mixed16", "bf16x6", "bf16x3", "fp32"],
@@ -71,9 +74,10 @@ def measure(a, dev=None):
         mlp.split_weights = lambda jobs, prec: [mlp.split_weight(j[0], j[1], j[2] if len(j) > 2 else prec)
                                                    for j in jobs]
     S, I, n = a.samples, a.importance, a.rays
-    cfg = anerf.RenderConfig(N_samples=S, N_importance=I).validate()
-    ck = syn.make_checkpoint(13, n_joints=24, D=8, W=256, fine=True, tau=20.0)
-    sc = syn.make_scene(n_joints=24, H=512, W=512, seed=13, n_frames=a.images, yaw_step=2 * np.pi / a.images)
+    nj = getattr(a, "joints", 24)
+    cfg = anerf.RenderConfig(n_joints=nj, N_samples=S, N_importance=I).validate()
+    ck = syn.make_checkpoint(13, n_joints=nj, D=8, W=256, fine=True, tau=20.0)
+    sc = syn.make_scene(n_joints=nj, H=512, W=512, seed=13, n_frames=a.images, yaw_step=2 * np.pi / a.images)
     idx, cyls, _ = anerf.rays.valid_pixels(sc["c2ws"], 512, 512, sc["focal"], kps=sc["kps"], ext_scale=0.001)
     rng = np.random.default_rng(0)
     if getattr(a, "no_wgrad_overlap", False):
@@ -87,7 +91,9 @@ def measure(a, dev=None):
         kin = importlib.import_module("a-nerf_amd.kinematics")
         # (rest pose relative to the root, the pelvis parameter = the root keypoint: the chain then reproduces
         # the scene's skeletons, pose_opt.py:398-431 adds the pelvis to every joint)
-        popt = kin.PoseOptLayer(sc["kps"], sc["bones"], sc["rest"][None] - sc["rest"][None, :1], kin.SMPLSkeleton,
+        skel = kin.SMPLSkeleton if nj == 24 else kin.Skeleton(
+            [f"j{i}" for i in range(nj)], np.asarray(sc["parents"]), 0, list(range(1, nj)), {}, None)
+        popt = kin.PoseOptLayer(sc["kps"], sc["bones"], sc["rest"][None] - sc["rest"][None, :1], skel,
                                 use_rot6d=True, device=dev)
         with torch.no_grad():  # popt_anchors["rots"] (core/pose_opt.py:60-72): the initial poses
             anchor = popt.calculate_kinematic(np.arange(a.images))[4][..., :3, :2].flatten(start_dim=-2).clone()
@@ -174,8 +180,9 @@ def measure(a, dev=None):
                             if importlib.import_module("a-nerf_amd.mlp").FUSED_BACKWARD and a.mlp in ("mixed", "bf16x3",
                                                                                                     "mixed16")
                             else "two GEMMs (anerf_mlp_gemm + anerf_mlp_wgrad)"),
-        "view_layout": ("view windows (anerf.h ANERF_ENC_VIEW_WINDOWS: 24 windows per sample + per-ray factors)"
-                        if tr.model.view_windows else "full view columns (648 per sample)"),
+        "joints": nj,
+        "view_layout": (f"view windows (anerf.h ANERF_ENC_VIEW_WINDOWS: {nj} windows per sample + per-ray factors)"
+                        if tr.model.view_windows else f"full view columns ({cfg.input_ch_views} per sample)"),
         "data": "synthetic (seeded SMPL-24 poses, 128 cameras on a circle, seeded weights)"}
 
 
