@@ -93,15 +93,17 @@ class _Kinematics(torch.autograd.Function):
 
 
 def _dev_index(idx, device):
-    """Host indices -> a device int64 tensor without a host synchronisation: a pageable copy waits for the stream
-    to drain (the training step's per-ray image indices arrive every step, Trainer.get_kp_args), so the indices go
-    through pinned memory and a non-blocking copy.  A device tensor passes through."""
+    """Indices (host array or tensor) -> a device int64 tensor; a device tensor passes through."""
     if isinstance(idx, torch.Tensor):
         return idx.to(device=device, dtype=torch.long).view(-1)
-    a = torch.from_numpy(np.ascontiguousarray(np.asarray(idx), dtype=np.int64).reshape(-1))
-    if torch.device(device).type != "cuda":
-        return a.to(device)
-    return a.pin_memory().to(device, non_blocking=True)
+    return torch.as_tensor(np.ascontiguousarray(np.asarray(idx), dtype=np.int64).reshape(-1), device=device)
+
+
+# PoseOptLayer.calculate_kinematic on DEVICE indices: with at most this many frames every frame's chain runs once
+# and the requested rows are gathered on the device -- the same values and, through the gather's backward, the
+# same gradients as the reference's np.unique + inverse (pose_opt.py:380-381, 436-442), without taking the indices
+# to the host (np.unique) and back (two copies that each wait for the stream to drain, every training step)
+ALL_FRAMES_MAX = 8192
 
 
 def _dev_f32_grad(x, device):
@@ -128,7 +130,10 @@ def pose_kinematics(bones, rest_pose, skel_type=SMPLSkeleton, pelvis=None, scale
     rest = _dev_f32(rest_pose, device).reshape(-1, nj, 3)
     ridx = None
     if rest_idx is not None:
-        ridx = torch.as_tensor(np.asarray(rest_idx), dtype=torch.int32).to(device).contiguous()
+        if isinstance(rest_idx, torch.Tensor):
+            ridx = rest_idx.to(device=device, dtype=torch.int32).reshape(-1).contiguous()
+        else:
+            ridx = torch.as_tensor(np.asarray(rest_idx), dtype=torch.int32).to(device).contiguous()
         if ridx.numel() != F:
             raise ValueError("rest_idx must have one entry per frame")
     elif rest.shape[0] != 1:
@@ -222,7 +227,28 @@ class PoseOptLayer(torch.nn.Module):
         return self.rest_pose[torch.as_tensor(self.rest_pose_idxs[np.asarray(kp_idxs)], device=self.device)]
 
     def calculate_kinematic(self, idxs, rest_pose_idxs=None):
-        """-> kp (N, NJ, 3), bone (N, NJ, 3|6), skts (N, NJ, 4, 4), l2ws (N, NJ, 4, 4), rots (N, NJ, 3, 3)."""
+        """-> kp (N, NJ, 3), bone (N, NJ, 3|6), skts (N, NJ, 4, 4), l2ws (N, NJ, 4, 4), rots (N, NJ, 3, 3).
+        idxs: a host array (the reference's kp_idx) or a device tensor (a batch already on the device)."""
+        if (isinstance(idxs, torch.Tensor) and idxs.device.type != "cpu" and rest_pose_idxs is None
+                and self.N_kps <= ALL_FRAMES_MAX):
+            g = idxs.to(device=self.device, dtype=torch.long).reshape(-1)
+            if self.kp_map is None:
+                pelvis, bone = self.pelvis, self.bones
+            else:
+                pelvis = self.pelvis
+                bone = torch.cat([self.root_bones[:, None, :], self.bones[self.kp_map]], dim=1)
+            if len(self.rest_pose) == 1 or self.rest_pose_idxs is None:
+                ridx = None
+            else:
+                if getattr(self, "_ridx_all", None) is None or self._ridx_all.device != self.device:
+                    self._ridx_all = torch.as_tensor(np.asarray(self.rest_pose_idxs), dtype=torch.int32,
+                                                     device=self.device)
+                ridx = self._ridx_all
+            o = pose_kinematics(bone, self.rest_pose, self.skel_type, pelvis=pelvis, rest_idx=ridx,
+                                device=self.device)
+            return o["kps"][g], bone[g], o["skts"][g], o["l2ws"][g], o["rots"][g]
+        if isinstance(idxs, torch.Tensor):
+            idxs = idxs.detach().cpu().numpy()
         if idxs is None:
             idxs = np.arange(self.N_kps)
         idxs = np.atleast_1d(np.asarray(idxs))

@@ -51,6 +51,8 @@ def parser():
                     help="torch.optim.Adam's implementation (foreach: the drop-in's, create_raycaster; fused: one "
                          "kernel per step, +0.5 %%, but it does not advance the version counters the eval caster "
                          "reads)")
+    ap.add_argument("--host-index", action="store_true",
+                    help="hand PoseOptLayer the host image indices (np.unique per step) instead of the device batch")
     ap.add_argument("--pose", default="kinematic", choices=["kinematic", "delta"],
                     help="pose optimisation: kinematic (default; Trainer.train_batch with --opt_pose --opt_rot6d, "
                          "core/trainer.py:230-273, 382-403, 451-481): a kinematics.PoseOptLayer over the images runs "
@@ -128,7 +130,7 @@ def measure(a, dev=None):
         if kinematic:
             # Trainer.get_kp_args (core/trainer.py:285-312): the layer's kinematics for every ray's image
             popt_opt.zero_grad(set_to_none=True)
-            kp, bone, sk, _, rots = popt(img_np)
+            kp, bone, sk, _, rots = popt(img_np if a.host_index else img)
             out = tr.render_rays(rb, S, kp_batch=kp, skts=sk, cyls=cy, bones=bone, perturb=1.0, N_importance=I,
                                  raw_noise_std=1.0)
             # Trainer._compute_kp_loss (core/trainer.py:382-403) with --opt_rot6d, tol 0.01, coef 2.0
@@ -160,7 +162,9 @@ def measure(a, dev=None):
                    "N_rand 2048, 64+16 samples, 8x256, 128 images)" if kinematic else
                    "training rays/s (render_rays fwd + loss + bwd + Adam; N_rand 2048, 64+16 samples, 8x256, "
                    "128 images with a skts + delta pose leaf)"),
-        "pose": ("PoseOptLayer: anerf_pose_kinematics + its backward every step" if kinematic
+        "pose": ("PoseOptLayer: anerf_pose_kinematics + its backward every step, "
+                 + ("host indices (np.unique)" if a.host_index else "device indices (all frames + gather)")
+                 if kinematic
                  else "skts + delta leaf"),
         "value": round(n / dt, 1), "unit": "rays/s", "ms_per_step": round(1e3 * dt, 3), "steps": a.steps,
         "dtype": "fp32" if a.mlp == "fp32" else f"fp32 in/out, MLP GEMMs as split bf16 ({a.mlp})", "mlp": a.mlp,
