@@ -758,10 +758,10 @@ int anerf_train_view_factor_backward(const anerf_model* m, const float* ray_batc
 
 static int check_view_mix(const char* fn, int64_t n_rays, int32_t n_samples, int32_t n_joints, int32_t width,
                           const float* windows, int64_t ld, const float* G) {
-    if (!windows || !G || n_rays < 0 || n_samples < 1 || n_joints < 1 || width < 4 || (width & 3) ||
-        n_joints * width > 4096 || ld < n_joints || (reinterpret_cast<uintptr_t>(G) & 15))
-        return fail(ANERF_EINVAL, std::string(fn) + ": bad arguments (width % 4 == 0, n_joints * width <= 4096, "
-                                                     "ld >= n_joints, G 16-byte aligned)");
+    if (!windows || !G || n_rays < 0 || n_samples < 1 || n_joints < 1 || width < 4 || (width & 3) || width > 4096 ||
+        ld < n_joints || (reinterpret_cast<uintptr_t>(G) & 15))
+        return fail(ANERF_EINVAL, std::string(fn) + ": bad arguments (width % 4 == 0, ld >= n_joints, G 16-byte "
+                                                     "aligned)");
     if (n_rays > 0x7fffffff) return fail(ANERF_EINVAL, "too many rays for one launch");
     return ANERF_OK;
 }
@@ -790,10 +790,16 @@ int anerf_train_view_mix_backward(int64_t n_rays, int32_t n_samples, int32_t n_j
         return fail(ANERF_EINVAL, "anerf_train_view_mix_backward: bad gradient arguments");
     if (n_rays == 0) return ANERF_OK;
     const size_t lds = (size_t)(4 * ((n_joints + 3) / 4) * (width + 4) + VM_SC * (width + 4) + VM_SC * n_joints) * 4;
-    if (lds > 64 * 1024) return fail(ANERF_EINVAL, "anerf_train_view_mix_backward: n_joints too large for the LDS plan");
-    hipLaunchKernelGGL(train_view_mix_backward_kernel, dim3((unsigned)n_rays), dim3(256), lds,
-                       reinterpret_cast<hipStream_t>(stream), windows, ld_windows, n_samples, n_joints, G, width,
-                       grad_out, grad_windows, ld_grad_windows, grad_G);
+    if (lds > 64 * 1024 || (int64_t)n_joints * width > 1024LL * VM_K_LARGE)
+        return fail(ANERF_EINVAL, "anerf_train_view_mix_backward: n_joints too large for the LDS / register plan");
+    if ((int64_t)n_joints * width <= 1024LL * VM_K_SMALL)
+        hipLaunchKernelGGL(train_view_mix_backward_kernel<VM_K_SMALL>, dim3((unsigned)n_rays), dim3(256), lds,
+                           reinterpret_cast<hipStream_t>(stream), windows, ld_windows, n_samples, n_joints, G, width,
+                           grad_out, grad_windows, ld_grad_windows, grad_G);
+    else
+        hipLaunchKernelGGL(train_view_mix_backward_kernel<VM_K_LARGE>, dim3((unsigned)n_rays), dim3(256), lds,
+                           reinterpret_cast<hipStream_t>(stream), windows, ld_windows, n_samples, n_joints, G, width,
+                           grad_out, grad_windows, ld_grad_windows, grad_G);
     HIP_TRY(hipGetLastError());
     return ANERF_OK;
 }

@@ -754,10 +754,13 @@ __global__ __launch_bounds__(64) void train_importance_kernel(const float* __res
 }
 
 // ---- view-window layout (anerf.h ANERF_ENC_VIEW_WINDOWS): the view layer's view part sum_j w_j G_j per sample.
-// One workgroup per ray; G[ray] [NJ][WH] (NJ WH <= 4096) and the windows of VM_SC samples at a time staged in LDS,
+// One workgroup per ray; G[ray] [NJ][WH] (4 (NJ WH + VM_SC NJ) bytes <= 64 KB) and VM_SC samples' windows in LDS,
 // lanes over (sample, 4 columns).  HBM: the windows (NJ floats per sample), G once per ray, the [WH] output row
 // per sample.
-constexpr int VM_SC = 32, VM_K = 4;  // (samples per LDS chunk; float4 dL/dG accumulators per thread)
+constexpr int VM_SC = 32;  // (samples per LDS chunk)
+// float4 dL/dG accumulators per thread of the backward: 4 for NJ W <= 4096 (24 joints at W 128), 9 up to 9216
+// (65-72 joints at W 128)
+constexpr int VM_K_SMALL = 4, VM_K_LARGE = 9;
 __global__ __launch_bounds__(256) void train_view_mix_kernel(const float* __restrict__ win, int64_t ldw, int ns, int nj,
                                                              const float* __restrict__ G, int wh,
                                                              float* __restrict__ out) {
@@ -792,8 +795,9 @@ __global__ __launch_bounds__(256) void train_view_mix_kernel(const float* __rest
 
 // Its gradients: dL/dw_j(s) = sum_h gz[s][h] G[j][h] (into the window columns of g_feat) and dL/dG[j][h] =
 // sum_s w_j(s) gz[s][h], per ray; samples in chunks of VM_SC through LDS.  dL/dw: lanes over samples (gz rows
-// padded by 4 floats), 4 joints per lane (G rows zero-padded to a multiple of 4 joints); dL/dG: float4 column
-// groups per lane, in registers across the chunks.
+// padded by 4 floats), 4 joints per lane (G rows zero-padded to a multiple of 4 joints); dL/dG: VM_K float4
+// column groups per lane (NJ W <= 1024 VM_K), in registers across the chunks.
+template <int VM_K>
 __global__ __launch_bounds__(256) void train_view_mix_backward_kernel(const float* __restrict__ win, int64_t ldw,
                                                                       int ns, int nj, const float* __restrict__ G,
                                                                       int wh, const float* __restrict__ gz,

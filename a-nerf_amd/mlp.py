@@ -430,8 +430,8 @@ def nerf_forward(net, feat, codes=None, G=None):
         wv = params[2 * D + 4]
         params[2 * D + 4] = torch.cat([wv[:, :W], wv[:, W + nv:]], 1)
         nv = 0
-        if dnet % 4 or feat.shape[1] % 4:
-            raise ValueError("view-window layout: the kp + bone columns and the row width must be multiples of 4")
+        if dnet % 4 or feat.shape[1] % 4:  # (the NJ windows play the view block's part: [x | pad | w | pad])
+            feat, params, dnet, _ = _pad_to_segments(feat, params, W, D, skip, dnet, nwin, pad_view_weight=False)
     elif dnet % 4 or nv % 4 or feat.shape[1] % 4:
         feat, params, dnet, nv = _pad_to_segments(feat, params, W, D, skip, dnet, nv)
     shape = (W, D, skip, dnet, nv, fwd, bwd, nwin)
@@ -442,7 +442,7 @@ def _ceil4(x):
     return (x + 3) // 4 * 4
 
 
-def _pad_to_segments(feat, params, W, D, skip, dnet, nv):
+def _pad_to_segments(feat, params, W, D, skip, dnet, nv, pad_view_weight=True):
     """The GEMMs read operand segments as 16-byte float4 groups (anerf_gemm.hip set_segs): every
     segment starts 16-byte aligned, rows have ld % 4 == 0 and a segment followed by another has
     cols % 4 == 0.  The encoder's rows [x (18 NJ) | views (27 NJ)] meet that only for NJ % 4 == 0, so
@@ -450,7 +450,8 @@ def _pad_to_segments(feat, params, W, D, skip, dnet, nv):
     multiples of 4 columns, with zero weight columns inserted where the padding enters (layer 0, the
     skip layer's x part, the view layer's view part).  The padded products are the same sums plus
     exact zeros; torch autograd carries the gradients back through the pads to feat and the
-    unpadded parameters."""
+    unpadded parameters.  The view-window layout's rows [x | w (NJ windows)] pad the same way, nv = NJ; their
+    view layer has no view columns (pad_view_weight False)."""
     d4, v4 = _ceil4(dnet), _ceil4(nv)
     M = feat.shape[0]
     z = lambda c: feat.new_zeros(M, c)  # noqa: E731
@@ -462,8 +463,9 @@ def _pad_to_segments(feat, params, W, D, skip, dnet, nv):
     params[0] = pad_cols(params[0], dnet, d4 - dnet)  # layer 0: [W][dnet]
     if skip >= 0:
         params[2 * (skip + 1)] = pad_cols(params[2 * (skip + 1)], dnet, d4 - dnet)  # [x | h]
-    iv = 2 * D + 4  # views_linears.0: [feature (W) | views (nv) | framecode]
-    params[iv] = pad_cols(params[iv], W + nv, v4 - nv)
+    if pad_view_weight:
+        iv = 2 * D + 4  # views_linears.0: [feature (W) | views (nv) | framecode]
+        params[iv] = pad_cols(params[iv], W + nv, v4 - nv)
     return featp, params, d4, v4
 
 

@@ -389,15 +389,23 @@ class _Embed(nn.Module):
         self._set("tau", new)
 
 
+def view_mix_lds_ok(n_joints, width):
+    """The per-ray factors G [NJ][width] and a chunk of 32 samples' windows fit anerf_train_view_mix's and its
+    backward's LDS plans (anerf.h: 64 KB) and the backward's dL/dG registers (NJ width <= 9216); width 128 -> NJ <= 72."""
+    nj4 = (n_joints + 3) // 4 * 4
+    fwd = 4 * (n_joints * width + 32 * n_joints)
+    bwd = 4 * (nj4 * (width + 4) + 32 * (width + 4) + 32 * n_joints)
+    return width % 4 == 0 and max(fwd, bwd) <= 64 * 1024 and n_joints * width <= 9216
+
+
 def view_windows_ok(cfg):
     """The view-window layout (anerf.h ANERF_ENC_VIEW_WINDOWS) holds for this configuration: every view feature is
     a window times a function of the ray (a windowed view embedder -- cutoff_viewdir with use_cutoff,
-    RenderConfig.view_window -- and cutoff_inputs, relray / world directions), and the
-    GEMM segments stay 16-byte aligned without padding, and the per-ray factors G fit anerf_train_view_mix's LDS plan
-    (NJ W / 2 <= 4096)."""
-    dnet = cfg.input_ch + cfg.input_ch_bones
-    return (cfg.view_window and cfg.cutoff_inputs and not cfg.view_angle and not cfg.staged and dnet % 4 == 0
-            and (dnet + cfg.n_joints) % 4 == 0 and cfg.n_joints * (cfg.netwidth // 2) <= 4096)
+    RenderConfig.view_window -- and cutoff_inputs, relray / world directions), and the per-ray factors G fit
+    anerf_train_view_mix's LDS plan (view_mix_lds_ok).  Rows whose kp + bone block or width are not multiples of 4
+    (NJ % 4 != 0) run on a zero-padded copy (mlp._pad_to_segments)."""
+    return (cfg.view_window and cfg.cutoff_inputs and not cfg.view_angle and not cfg.staged
+            and cfg.netwidth // 2 <= 128 and view_mix_lds_ok(cfg.n_joints, cfg.netwidth // 2))
 
 
 class _ViewFactor(torch.autograd.Function):

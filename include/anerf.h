@@ -467,7 +467,10 @@ int anerf_train_view_factor_backward(const anerf_model* m, const float* ray_batc
 /* The view-window layout's view part (ABI 16, ANERF_ENC_VIEW_WINDOWS): out [N S][width] = sum_j w_j G_j, the NJ
  * windows w of sample s of ray r at windows + (r S + s) ld_windows (the window columns of an anerf_train_encode
  * row) and G [N][NJ][width] the ray's view factors (the view layer's view columns times the ray's direction
- * terms, per joint).  width % 4 == 0, NJ width <= 4096, G and out 16-byte aligned.  In the reference this is
+ * terms, per joint).  width % 4 == 0, G and out 16-byte aligned; G and a chunk of windows are staged in LDS:
+ * 4 (NJ width + 32 NJ) bytes <= 64 KB here, 4 (4 ceil(NJ / 4) (width + 4) + 32 (width + 4) + 32 NJ) bytes in
+ * the backward, which also keeps dL/dG in registers: NJ width <= 9216 (width 128: NJ <= 72; ANERF_EINVAL
+ * beyond).  In the reference this is
  * part of views_linears.0's product with the view features (core/networks/nerf.py:141-148). */
 int anerf_train_view_mix(int64_t n_rays, int32_t n_samples, int32_t n_joints, int32_t width, const float* windows,
                          int64_t ld_windows, const float* G, float* out, void* stream);

@@ -71,9 +71,9 @@ CONFIGS = {
     # --kp_dist_type querypts (no gradient to the poses through the kp part) with --cutoff_shift
     "t13_querypts_shift": dict(H=128, NJ=24, S=32, I=16, D=4, W=128, tau=20.0, kind="rays", seed=47, n_rays=64,
                                n_poses=2, flags=["--kp_dist_type", "querypts", "--cutoff_shift"]),
-    # (round 6) BASELINE config 4's 65-joint skeleton at 8 x 256 (the LDS-pressure case): NJ W / 2 = 8,320 > 4,096,
-    # so the full view columns (the view-window layout's per-ray factors do not fit anerf_train_view_mix's LDS
-    # plan); the fused hidden-layer backward at W 256
+    # (round 6) BASELINE config 4's 65-joint skeleton at 8 x 256 (the LDS-pressure case): the view-window layout
+    # with zero-padded rows (1170 kp + bone columns -> 1172, then the 65 windows; G 65 x 128 in anerf_train_view_mix's
+    # LDS) and the full view columns both run against it; the fused hidden-layer backward at W 256
     "t14_nj65_d8w256": dict(H=256, NJ=65, S=32, I=16, D=8, W=256, tau=20.0, kind="rays", seed=48, n_rays=32,
                             n_poses=2),
 }

@@ -106,10 +106,10 @@ def test_build_discards_a_library_whose_sources_moved(tmp_path, monkeypatch):
 
 
 def test_view_mix_rejects_bad_shapes():
-    """anerf_train_view_mix validates before any HIP call (anerf.h: width % 4 == 0, NJ width <= 4096, ld >= NJ)."""
+    """anerf_train_view_mix validates before any HIP call (anerf.h: width % 4 == 0, ld >= NJ, the LDS plan)."""
     lib = _lib.load()
     assert lib.anerf_train_view_mix(1, 1, 24, 130, 1, 24, 16, 16, None) == -1
-    assert lib.anerf_train_view_mix(1, 1, 64, 128, 1, 64, 16, 16, None) == -1
+    assert lib.anerf_train_view_mix(1, 1, 103, 128, 1, 103, 16, 16, None) == -1  # (G + windows over 64 KB of LDS)
     assert lib.anerf_train_view_mix(1, 1, 24, 128, 1, 20, 16, 16, None) == -1
     assert b"anerf_train_view_mix" in lib.anerf_last_error()
     assert lib.anerf_train_view_mix_backward(1, 1, 24, 128, 1, 24, 16, 16, None, 24, 16, None) == -1

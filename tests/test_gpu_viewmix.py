@@ -1,6 +1,8 @@
 """GPU: anerf_train_view_mix (+ _backward), the view-window layout's view part (anerf.h ANERF_ENC_VIEW_WINDOWS),
 against fp64 torch on the same inputs: out = sum_j w_j G_j per sample, dL/dw and dL/dG.  Ragged sample counts
-(chunks of 32 in the backward), row strides wider than NJ, joint counts off the powers of two, widths 32-128.
+(chunks of 32 in the backward), row strides wider than NJ, joint counts off the powers of two up to the LDS plan's
+72 at width 128 (the 65-joint training rows: 1170 kp + bone columns padded to 1172, then the windows; dL/dG in 4 or
+9 float4 registers per lane), widths 4-128.
 Tolerance 1e-5 relative to the largest |value| (fp32 sums of at most 128 terms)."""
 import importlib
 
@@ -23,7 +25,8 @@ def _close(a, ref):
 
 
 @pytest.mark.parametrize("n,ns,nj,wh,ld", [(3, 64, 24, 128, 456), (5, 80, 24, 128, 24), (7, 33, 17, 64, 21),
-                                           (2, 1, 1, 4, 1), (4, 100, 32, 128, 40), (6, 16, 65, 32, 70)])
+                                           (2, 1, 1, 4, 1), (4, 100, 32, 128, 40), (6, 16, 65, 32, 70),
+                                           (5, 80, 65, 128, 1236), (3, 47, 72, 128, 72), (2, 40, 100, 64, 101)])
 def test_view_mix_matches_torch(n, ns, nj, wh, ld):
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(n * 1000 + ns)

@@ -277,7 +277,8 @@ def test_view_window_layout_matches_full_view_columns():
 
 def test_view_window_layout_conditions():
     """view_windows_ok: every view feature windowed (cutoff_viewdir and cutoff_inputs), no ray-angle views, no staged
-    encoder, 16-byte GEMM segments."""
+    encoder, the per-ray factors within anerf_train_view_mix's LDS plan (anerf.h: width 128 -> NJ <= 72; other NJ % 4
+    run on zero-padded rows)."""
     import dataclasses
     cfg = Golden("t2_s64i16_d8w256").cfg
     assert train.view_windows_ok(cfg)
@@ -290,4 +291,8 @@ def test_view_window_layout_conditions():
     assert not train.view_windows_ok(nocut)
     fs = importlib.import_module("a-nerf_amd.config").feature_scales(dataclasses.replace(nocut, freq_schedule=True), 1.5, 1.5)
     assert (fs == 1).all()  # (neither the pts nor the view embedder is a CutoffEmbedder: no schedule weights)
-    assert not train.view_windows_ok(dataclasses.replace(cfg, n_joints=17))
+    assert train.view_windows_ok(dataclasses.replace(cfg, n_joints=17))
+    assert train.view_windows_ok(dataclasses.replace(cfg, n_joints=65))
+    assert not train.view_windows_ok(dataclasses.replace(cfg, n_joints=80))
+    assert train.view_mix_lds_ok(72, 128) and not train.view_mix_lds_ok(73, 128)
+    assert train.view_mix_lds_ok(140, 64) and not train.view_mix_lds_ok(141, 64)
