@@ -48,6 +48,9 @@ _SIDE = {}
 # GEMM on the side stream each reading both.  bf16x3 backward arithmetic only (the "mixed" default); an A/B
 # switch for tools/train_bench.py, never read from the environment
 FUSED_BACKWARD = True
+# (round 6, with FUSED_BACKWARD) the skip layer's h part as one more fused pass and its x part merged into layer
+# 0's two products (the backward's comment below); an A/B switch for tools/train_bench.py
+FUSED_SKIP = True
 
 
 def _side_stream(dev):
@@ -236,8 +239,19 @@ class _MLP(torch.autograd.Function):
         cfc = 0 if codes is None else codes.shape[1]
         need_feat = ctx.needs_input_grad[1]
         need_codes = ctx.has_codes and ctx.needs_input_grad[2]
+        fused = FUSED_BACKWARD and prec == 3 and W == 256
+        # (round 6) with the fused kernel the skip layer's h part is one more 256 x 256 pass, and its x part joins
+        # layer 0's products: both multiply the encoder features x, so [dY_0 | dY_s] (one [M, 2W] buffer the two
+        # passes write) gives gfeat = [dY_0 | dY_s] [W_0 ; W_s,x] in one GEMM (K = 2W) and [dW_0 ; dW_s,x] =
+        # [dY_0 | dY_s]^T x in one weight gradient: x, and the feature gradient, are read and written once
+        s1 = skip + 1
+        merge = fused and FUSED_SKIP and skip >= 0 and s1 < D - 1
+        tw = list(pw)
+        if merge:
+            tw[s1] = pw[s1][:, dnet:]
+            tw[0] = torch.cat([pw[0], pw[s1][:, :dnet]]) if need_feat else None
         # every transposed plane in one launch: [trunk (layer 0 only for the feature gradient)..., head, views, rgb]
-        st = split_weights([(w, True) for w in pw[0 if need_feat else 1:]] + [(whead, True), (wv, True), (wr, True)],
+        st = split_weights([(w, True) for w in tw[0 if need_feat else 1:]] + [(whead, True), (wv, True), (wr, True)],
                            prec)
         st = ([None] if not need_feat else []) + st
         f32 = dict(device=dev, dtype=torch.float32)
@@ -307,10 +321,11 @@ class _MLP(torch.autograd.Function):
         # the trunk, last layer first
         segx = _seg(feat, dnet)
         wrote_x = False
-        fused = FUSED_BACKWARD and prec == 3 and W == 256
         fws, fev, nfused = [None, None], [None, None], 0
+        gzx = torch.empty(M, 2 * W, **f32) if merge else None  # [dY_0 | dY_s1]
+        dwx = None
         for i in range(D - 1, -1, -1):
-            if fused and i >= 1 and i - 1 != skip:  # one pass: gprev, dW, db (anerf_mlp_backward_hidden)
+            if fused and i >= 1 and (i - 1 != skip or merge):  # one pass: gprev, dW, db (anerf_mlp_backward_hidden)
                 # two workspaces in turn: layer i's slabs are summed on the side stream (its reduce beside the next
                 # layer's pass) while layer i - 1 writes the other; a workspace is reused once its reduce is done
                 slot = nfused & 1
@@ -321,8 +336,16 @@ class _MLP(torch.autograd.Function):
                 if fev[slot] is not None:
                     main.wait_event(fev[slot])
                 ws_l = fws[slot]
-                gprev = torch.empty(M, W, **f32)
-                dw, db = torch.empty(W, W, **f32), torch.empty(W, **f32)
+                if merge and i in (1, s1 + 1):  # (dY_0, dY_s1: halves of gzx)
+                    gprev = gzx[:, :W] if i == 1 else gzx[:, W:]
+                else:
+                    gprev = torch.empty(M, W, **f32)
+                if merge and i == s1:  # (the h columns of the skip layer's weight gradient; x columns below)
+                    dwf = torch.empty(W, dnet + W, **f32)
+                    dw = dwf[:, dnet:]
+                else:
+                    dwf = dw = torch.empty(W, W, **f32)
+                db = torch.empty(W, **f32)
                 defer = side is not None
                 _lib.check(lib.anerf_mlp_backward_hidden(M, W, _lib.ptr(gz), gz.stride(0), _lib.ptr(H[i - 1]),
                                                          H[i - 1].stride(0), _lib.ptr(st[i]), prec, _lib.ptr(gprev),
@@ -339,9 +362,15 @@ class _MLP(torch.autograd.Function):
                         fev[slot].record(side)
                     for t in (dw, db, ws_l):
                         t.record_stream(side)
-                grads[2 * i], grads[2 * i + 1] = dw, db
+                grads[2 * i], grads[2 * i + 1] = dwf, db
                 gz = gprev
                 continue
+            if i == 0 and merge:
+                dwx, dbx = wg(2 * W, dnet, gzx, [segx], (feat, gzx))
+                grads[0], grads[1] = dwx[:W], dbx[:W]
+                if need_feat:
+                    mm(M, dnet, 2 * W, [_seg(gzx, 2 * W)], st[0], None, False, [(gfeat, F, dnet, 0, None, False)], dev)
+                break
             if i == 0:
                 a, k = [segx], dnet
             elif i - 1 == skip:
@@ -366,6 +395,8 @@ class _MLP(torch.autograd.Function):
             gz = gprev
         if side is not None:
             main.wait_stream(side)
+        if dwx is not None:
+            grads[2 * s1][:, :dnet].copy_(dwx[W:])
         return (None, gfeat, gcodes, gG if ctx.needs_input_grad[3] else None, *grads)
 
 

@@ -275,6 +275,42 @@ def test_nerf_forward_backward_matches_fp32_module(D, W, fc, nj, impl):
         assert rel(gp_b[k], gp_f[k]) <= 5e-3, (k, rel(gp_b[k], gp_f[k]))
 
 
+@pytest.mark.parametrize("D,fc,nj,need_feat", [(8, False, 24, True), (8, True, 17, True), (8, False, 65, True),
+                                                (8, False, 24, False), (6, False, 24, True)])
+def test_fused_skip_layer_backward_matches_two_gemms(D, fc, nj, need_feat, monkeypatch):
+    """mlp.FUSED_SKIP (round 6): the skip layer's h part on anerf_mlp_backward_hidden and its x part merged into
+    layer 0's products ([dY_0 | dY_s] against [W_0 ; W_s,x]) == the skip layer as two GEMMs and layer 0 apart: the
+    same bf16x3 products summed in another order, so every gradient within 1e-5 (relative Frobenius).  17 / 65
+    joints: zero-padded kp + bone blocks; D 6: the skip layer is the last (no merge); no feature gradient."""
+    mlp = importlib.import_module("a-nerf_amd.mlp")
+    cfg = anerf.RenderConfig(n_joints=nj, netdepth=D, netwidth=256, opt_framecode=fc,
+                             n_framecodes=5 if fc else 0).validate()
+    ck = syn.make_checkpoint(7, n_joints=nj, D=D, W=256, fine=False, use_framecode=fc, n_framecodes=5)
+    torch.manual_seed(1)
+    M = 4000
+    feat = (torch.rand(M, cfg.feature_dim, device=DEV) * 2 - 1)
+    cams = torch.randint(0, 5, (M,), device=DEV) if fc else None
+    gout = torch.randn(M, 4, device=DEV)
+    res = {}
+    for on in (True, False):
+        monkeypatch.setattr(mlp, "FUSED_SKIP", on)
+        tr = train.TrainRayCaster(cfg, ck, mlp="mixed").train()
+        net = tr.network_fn
+        f = feat.clone().requires_grad_(need_feat)
+        (net(f, cams) * gout).sum().backward()
+        res[on] = (f.grad, {k: p.grad.clone() for k, p in net.named_parameters()})
+
+    def rel(a, b):
+        return float((a.double() - b.double()).norm() / max(b.double().norm(), 1e-30))
+    if need_feat:
+        assert rel(res[True][0], res[False][0]) <= 1e-5
+    else:
+        assert res[True][0] is None
+    for k in res[False][1]:
+        assert res[True][1][k].shape == res[False][1][k].shape
+        assert rel(res[True][1][k], res[False][1][k]) <= 1e-5, (k, rel(res[True][1][k], res[False][1][k]))
+
+
 @pytest.mark.parametrize("D,W,fc,nj,M", [(8, 256, False, 24, 5000), (4, 128, True, 24, 3001), (8, 256, True, 17, 77),
                                          (8, 128, False, 65, 1000), (2, 256, False, 24, 40)])
 def test_fused_forward_matches_layer_by_layer_gemms(D, W, fc, nj, M, monkeypatch):

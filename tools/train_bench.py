@@ -60,8 +60,13 @@ def parser():
                          "the rot6d anchor loss (opt_pose_tol 0.01, opt_pose_coef 2.0, configs/h36m/h36m_prot2.txt) "
                          "joins the loss and a second Adam (opt_pose_lrate 5e-4) steps the poses every step; delta "
                          "(rounds 1-5): a skts + delta leaf per image")
+    ap.add_argument("--no-fused-skip", action="store_true",
+                    help="ablation: the skip layer's backward as two GEMMs and its x part apart from layer 0's")
     ap.add_argument("--split-single", action="store_true",
                     help="ablation: one split launch per weight instead of the batched split")
+    ap.add_argument("--probe", default="", choices=["", "no-hidden-reduce", "no-wgrad", "no-wgrad-no-reduce"],
+                    help="TIMING ONLY (wrong gradients): skip the fused backward's slab reduce and/or the other "
+                         "layers' weight gradients, to bound what speeding them up could give")
     return ap
 
 
@@ -82,9 +87,17 @@ def measure(a, dev=None):
     sc = syn.make_scene(n_joints=nj, H=512, W=512, seed=13, n_frames=a.images, yaw_step=2 * np.pi / a.images)
     idx, cyls, _ = anerf.rays.valid_pixels(sc["c2ws"], 512, 512, sc["focal"], kps=sc["kps"], ext_scale=0.001)
     rng = np.random.default_rng(0)
+    probe = getattr(a, "probe", "")
+    if probe:
+        lib = importlib.import_module("a-nerf_amd._lib").load()
+        if "reduce" in probe:
+            lib.anerf_mlp_backward_hidden_reduce = lambda *args: 0
+        if "wgrad" in probe:
+            lib.anerf_mlp_wgrad = lambda *args: 0
     if getattr(a, "no_wgrad_overlap", False):
         importlib.import_module("a-nerf_amd.mlp").WGRAD_OVERLAP = False
     importlib.import_module("a-nerf_amd.mlp").FUSED_BACKWARD = not getattr(a, "no_fused_backward", False)
+    importlib.import_module("a-nerf_amd.mlp").FUSED_SKIP = not getattr(a, "no_fused_skip", False)
     tr = train.TrainRayCaster(cfg, ck, device=dev, mlp=a.mlp).train()
     tr.view_windows = not getattr(a, "full_view", False)
     adam_kw = {"fused": True} if getattr(a, "adam", "foreach") == "fused" else {"foreach": True}
@@ -153,6 +166,7 @@ def measure(a, dev=None):
     t0 = time.perf_counter()
     for i in range(a.steps):
         step(batches[i % 4])
+    t_issue = time.perf_counter() - t0  # (the host's issue time: ~dt when the host, not the GPU, bounds the step)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.steps
     flop = 3 * anerf.flops_per_sample(cfg) * n * anerf.samples_per_ray(cfg)
@@ -167,6 +181,8 @@ def measure(a, dev=None):
                  if kinematic
                  else "skts + delta leaf"),
         "value": round(n / dt, 1), "unit": "rays/s", "ms_per_step": round(1e3 * dt, 3), "steps": a.steps,
+        "host_issue_ms_per_step": round(1e3 * t_issue / a.steps, 3),
+        **({"probe": probe + " (timing only: wrong gradients)"} if probe else {}),
         "dtype": "fp32" if a.mlp == "fp32" else f"fp32 in/out, MLP GEMMs as split bf16 ({a.mlp})", "mlp": a.mlp,
         "mlp_gemm_flop_per_step": flop, "mlp_tflops": round(flop / dt / 1e12, 2),
         "peak_tflops": FP32_MFMA_PEAK_TFLOPS if a.mlp == "fp32" else BF16_MFMA_PEAK_TFLOPS,
@@ -181,6 +197,8 @@ def measure(a, dev=None):
                            "fp32": "torch fp32 GEMMs"}[a.mlp],
         "adam": getattr(a, "adam", "foreach"),
         "hidden_backward": ("fused (anerf_mlp_backward_hidden: input + weight gradients from one read of dY and H)"
+                            + ("; the skip layer's h part fused too, its x part merged with layer 0's products"
+                               if importlib.import_module("a-nerf_amd.mlp").FUSED_SKIP else "")
                             if importlib.import_module("a-nerf_amd.mlp").FUSED_BACKWARD and a.mlp in ("mixed", "bf16x3",
                                                                                                     "mixed16")
                             else "two GEMMs (anerf_mlp_gemm + anerf_mlp_wgrad)"),
