@@ -995,9 +995,10 @@ constexpr int DGW_CH = 32;                           // rows per chunk
 constexpr int DGW_THR = 512;                         // eight waves
 constexpr int DGW_PLANE = DGW_CH * DGW_W * 2;        // 16 KB: one bf16 plane [32][256]
 constexpr int DGW_MASKB = DGW_CH * DGW_W;            // 8 KB: relu' mask bytes [32][256]
-constexpr int DGW_STAGE = 4 * DGW_PLANE + DGW_MASKB;
+constexpr int DGW_GA = 4 * DGW_PLANE + DGW_MASKB;     // the head pass: the chunk's 32 alpha gradients (fp32)
+constexpr int DGW_STAGE = DGW_GA + DGW_CH * 4;
 constexpr int DGW_BSUM = 8 * DGW_W * 4;              // 8 KB: the db column sums [8 staging rows][256]
-constexpr int DGW_LDS = 2 * DGW_STAGE + DGW_BSUM;    // 152 KB
+constexpr int DGW_LDS = 2 * DGW_STAGE + DGW_BSUM;    // 152.25 KB
 #ifndef ANERF_DGW_BD
 #define ANERF_DGW_BD 4
 #endif
@@ -1018,8 +1019,9 @@ struct DGWArgs {
     const unsigned short* wt;  // split W^T, bf16x3 planes (anerf_mlp_split_weights, transpose = 1)
     float* dx;
     long long lddx;
-    float* ws;   // [workgroups][256][256] dW partials
-    float* wsb;  // [workgroups][256] db partials
+    float* ws;   // [workgroups][256 (+ 1)][256] dW partials
+    float* wsb;  // [workgroups][256 (+ 4)] db partials
+    const float* wa;  // the head pass: alpha_linear's weight row [256] (its gradient column is dy's column 256)
 };
 
 __device__ __forceinline__ int dgw_off(int row, int chunk) {
@@ -1040,7 +1042,13 @@ __device__ __forceinline__ void dgw_split_store(const float (&v)[8], unsigned ch
     *reinterpret_cast<u32x4*>(lo + off) = wl;
 }
 
+// HEAD (the feature_linear + alpha_linear pass, anerf_mlp_backward_head): dY has a 257th column g_a, the gradient
+// of alpha_linear's output.  dX gains its rank-1 term, (dY W + g_a w_a^T) * (X > 0), in the epilogue (g_a staged
+// per chunk in LDS, w_a in two registers per dX lane); dW gains the row g_a^T X and db the entry sum g_a, summed by
+// the stager waves in fp32 as they split X (slab row 256, db entry 256)
+template <bool HEAD>
 __global__ __launch_bounds__(DGW_THR, 1) void mlp_dgw_kernel(DGWArgs g) {
+    constexpr int SROWS = HEAD ? DGW_W + 1 : DGW_W, BST = HEAD ? DGW_W + 4 : DGW_W;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds8[];
     // (the wave index as a uniform value: a buffer descriptor built from a per-lane value compiles to a
     // waterfall loop around every load, and the role branches must be uniform)
@@ -1102,6 +1110,12 @@ __global__ __launch_bounds__(DGW_THR, 1) void mlp_dgw_kernel(DGWArgs g) {
         const unsigned voy = (unsigned)((sr * lddy + c8) * 4), vox = (unsigned)((sr * ldx + c8) * 4);
         const int ystep = (int)(8 * lddy * 4), xstep = (int)(8 * ldx * 4);
         f32x4 R[8][2];  // unit k = 2 u + operand (0: dY, 1: X)
+        // (HEAD) g_a of the X unit's rows, loaded with that unit (it is consumed when the unit is staged, before the
+        // next chunk's loads reuse the register); the thread's sums of g_a X over its rows and columns, and of g_a
+        float Ga[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        float xa[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+        float dba = 0.0f;
+        const unsigned voa = (unsigned)(sr * lddy * 4);
         // (chunk rows past the workgroup's range read zero: the descriptors end at its last row; one lane offset per
         // operand, the row step and the 16 B piece in the uniform offset)
         auto fetch_unit = [&](int s, int k) {
@@ -1118,6 +1132,12 @@ __global__ __launch_bounds__(DGW_THR, 1) void mlp_dgw_kernel(DGWArgs g) {
 #pragma unroll
             for (int f = 0; f < 2; ++f)
                 R[k][f] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo, u * step + 16 * f, 0));
+            if (HEAD && (k & 1)) {  // (the descriptor ends at the last row's column lddy - 1: rows past it read 0)
+                const long long nb = rows * lddy * 4 - DGW_W * 4;
+                const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+                    (void*)(dyp + r0 * lddy + DGW_W), 0, (int)(nb > 0 ? nb : 0), 0x00020000);
+                Ga[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ra, voa, u * ystep, 0));
+            }
         };
         // db: the thread's running column sums of its staging rows, in LDS (its own 32 B of [8][256])
         float* const bsum = reinterpret_cast<float*>(lds8 + 2 * DGW_STAGE) + sr * DGW_W + c8;
@@ -1137,6 +1157,15 @@ __global__ __launch_bounds__(DGW_THR, 1) void mlp_dgw_kernel(DGWArgs g) {
                     v[4 * f + e] = t;
                 }
             if (k & 1) {
+                if (HEAD) {
+                    const float ga = Ga[k >> 1];
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) xa[e] = fmaf(ga, v[e], xa[e]);
+                    if ((tid & 31) == 0) {
+                        reinterpret_cast<float*>(S + DGW_GA)[r] = ga;
+                        dba += ga;
+                    }
+                }
                 dgw_split_store(v, S + 2 * DGW_PLANE, S + 3 * DGW_PLANE, off);
                 unsigned mk[2] = {0u, 0u};
 #pragma unroll
@@ -1184,6 +1213,12 @@ __global__ __launch_bounds__(DGW_THR, 1) void mlp_dgw_kernel(DGWArgs g) {
             }
             __syncthreads();
         }
+        if (HEAD) {  // (every stage read is done: the last barrier above) the thread's alpha sums into stage 0
+            float* const sc = reinterpret_cast<float*>(lds8);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) sc[sr * DGW_W + c8 + e] = xa[e];
+            if ((tid & 31) == 0) sc[8 * DGW_W + sr] = dba;
+        }
     } else {
         // ------------------------------------------------------------------ dX waves
         const int xw = wave - 4;  // dX columns 64 xw .. 64 xw + 63: blocks 2 xw, 2 xw + 1
@@ -1216,6 +1251,11 @@ __global__ __launch_bounds__(DGW_THR, 1) void mlp_dgw_kernel(DGWArgs g) {
         WF wf[DGW_BD];
 #pragma unroll
         for (int j = 0; j < DGW_BD - 1; ++j) fetch_w(j, wf[j]);
+        float wa[2] = {0.0f, 0.0f};  // (HEAD) w_a at the lane's two dX columns
+        if (HEAD) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) wa[j] = g.wa[64 * xw + 32 * j + (lane & 31)];
+        }
         __syncthreads();
         for (int s = 0; s < nch; ++s) {
             const unsigned char* const S = lds8 + (s & 1) * DGW_STAGE;
@@ -1248,6 +1288,7 @@ __global__ __launch_bounds__(DGW_THR, 1) void mlp_dgw_kernel(DGWArgs g) {
             const __amdgpu_buffer_rsrc_t rd =
                 __builtin_amdgcn_make_buffer_rsrc((void*)(g.dx + r0 * lddx), 0, (int)(rows * lddx * 4), 0x00020000);
             const unsigned char* const mk = S + 4 * DGW_PLANE;
+            const float* const gal = reinterpret_cast<const float*>(S + DGW_GA);
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 const int col = 64 * xw + 32 * j + (lane & 31);
@@ -1255,7 +1296,8 @@ __global__ __launch_bounds__(DGW_THR, 1) void mlp_dgw_kernel(DGWArgs g) {
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int rr = (r & 3) + 8 * (r >> 2);
-                    const float v = mk[(rr + 4 * (lane >> 5)) * DGW_W + col] ? ax[j][r] : 0.0f;
+                    const float a = HEAD ? fmaf(gal[rr + 4 * (lane >> 5)], wa[j], ax[j][r]) : ax[j][r];
+                    const float v = mk[(rr + 4 * (lane >> 5)) * DGW_W + col] ? a : 0.0f;
                     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rd, vo, (int)(rr * lddx * 4),
                                                           0);
                 }
@@ -1267,7 +1309,7 @@ __global__ __launch_bounds__(DGW_THR, 1) void mlp_dgw_kernel(DGWArgs g) {
     // per-register row and block offsets in SGPRs)
     {
         const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(g.ws + (long long)blockIdx.x * DGW_W * DGW_W), 0, DGW_W * DGW_W * 4, 0x00020000);
+            (void*)(g.ws + (long long)blockIdx.x * SROWS * DGW_W), 0, DGW_W * DGW_W * 4, 0x00020000);
         const unsigned vo = (unsigned)(((32 * wave + 4 * (lane >> 5)) * DGW_W + (lane & 31)) * 4);
 #pragma unroll
         for (int ib = 0; ib < 8; ++ib)
@@ -1286,7 +1328,23 @@ __global__ __launch_bounds__(DGW_THR, 1) void mlp_dgw_kernel(DGWArgs g) {
         float t = red[tid];
 #pragma unroll
         for (int w = 1; w < 8; ++w) t += red[w * DGW_W + tid];
-        g.wsb[(long long)blockIdx.x * DGW_W + tid] = t;
+        g.wsb[(long long)blockIdx.x * BST + tid] = t;
+        if (HEAD) {  // alpha's dW row and db entry, the 8 staging rows' sums in a fixed order
+            const float* const sc = reinterpret_cast<const float*>(lds8);
+            float a = sc[tid];
+#pragma unroll
+            for (int w = 1; w < 8; ++w) a += sc[w * DGW_W + tid];
+            g.ws[(long long)blockIdx.x * SROWS * DGW_W + DGW_W * DGW_W + tid] = a;
+            if (tid < 4) {
+                float d = 0.0f;
+                if (tid == 0) {
+                    d = sc[8 * DGW_W];
+#pragma unroll
+                    for (int w = 1; w < 8; ++w) d += sc[8 * DGW_W + w];
+                }
+                g.wsb[(long long)blockIdx.x * BST + DGW_W + tid] = d;  // (entries 257-259: zero padding)
+            }
+        }
     }
 }
 
@@ -1535,32 +1593,57 @@ int anerf_mlp_gemm_rows(int64_t m, int32_t n, int32_t k, const anerf_seg* a, int
     return e == hipSuccess ? ANERF_OK : anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));
 }
 
-size_t anerf_mlp_backward_hidden_workspace(int64_t m, int32_t width) {
-    if (width != DGW_W || m < 0) return 0;
+}  // extern "C"
+
+namespace {
+// workspace of the hidden (head = false) or head pass: per workgroup a [256 (+ 1)][256] dW slab, then per
+// workgroup 256 (+ 4) db entries
+size_t dgw_workspace(int64_t m, bool head) {
     long long rows;
     const int nwg = dgw_plan(m, &rows);
-    return (size_t)4 * nwg * (DGW_W * DGW_W + DGW_W);
+    return (size_t)4 * nwg * ((head ? DGW_W + 1 : DGW_W) * DGW_W + (head ? DGW_W + 4 : DGW_W));
 }
 
-int anerf_mlp_backward_hidden(int64_t m, int32_t width, const float* dy, int64_t lddy, const float* x, int64_t ldx,
-                              const void* wt_split, int32_t precision, float* dx, int64_t lddx, float* dw, int64_t lddw,
-                              float* db, void* workspace, size_t workspace_bytes, void* stream) {
+int dgw_reduce(const char* fn, bool head, int64_t m, int32_t width, const void* workspace, size_t workspace_bytes,
+               float* dw, int64_t lddw, float* db, void* stream) {
+    if (width != DGW_W || m < 0 || !dw || !db || lddw < width)
+        return anerf_internal_fail(ANERF_EINVAL, (std::string(fn) + ": bad arguments").c_str());
+    if (!workspace || workspace_bytes < dgw_workspace(m, head))
+        return anerf_internal_fail(ANERF_EWORKSPACE, (std::string(fn) + ": workspace too small").c_str());
+    long long rows;
+    const int nwg = dgw_plan(m, &rows);
+    const float* ws = static_cast<const float*>(workspace);
+    const int sr = head ? DGW_W + 1 : DGW_W, bst = head ? DGW_W + 4 : DGW_W;
+    // dW rows 0 .. sr - 1 and the bias row sr (sr entries), summed over the workgroups' slabs in order
+    hipLaunchKernelGGL(mlp_reduce_kernel, dim3(head ? 3 : DGW_W / 128, sr + 1), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), ws, nwg, (long long)sr * DGW_W, (long long)DGW_W, DGW_W,
+                       dw, (long long)lddw, 0, sr, ws + (size_t)nwg * sr * DGW_W, (long long)bst, sr, db);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? ANERF_OK : anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));
+}
+
+int dgw_launch(const char* fn, bool head, int64_t m, int32_t width, const float* dy, int64_t lddy, const float* x,
+               int64_t ldx, const void* wt_split, const float* wa, int32_t precision, float* dx, int64_t lddx,
+               float* dw, int64_t lddw, float* db, void* workspace, size_t workspace_bytes, void* stream) {
+    const std::string f(fn);
     if (width != DGW_W || precision != ANERF_MLP_BF16X3)
-        return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_backward_hidden: width 256 and ANERF_MLP_BF16X3 only");
-    if (m < 0 || !dy || !x || !wt_split || !dx || (!dw != !db) || (dw && lddw < width))
-        return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_backward_hidden: bad arguments");
-    // (float4 loads of whole rows; a 32-row chunk's byte range fits a buffer descriptor)
-    if ((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(x)) & 15 || (lddy | ldx) & 3 || lddy < width ||
-        ldx < width || lddx < width || lddy >= (1 << 22) || ldx >= (1 << 22) || lddx >= (1 << 22))
-        return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_backward_hidden: dy / x need 16 B aligned rows, "
-                                                 "ld % 4 == 0, width <= ld < 2^22 (dx: width <= ld < 2^22)");
+        return anerf_internal_fail(ANERF_EINVAL, (f + ": width 256 and ANERF_MLP_BF16X3 only").c_str());
+    if (m < 0 || !dy || !x || !wt_split || !dx || (!dw != !db) || (dw && lddw < width) || (head && !wa))
+        return anerf_internal_fail(ANERF_EINVAL, (f + ": bad arguments").c_str());
+    // (float4 loads of whole rows; a 32-row chunk's byte range fits a buffer descriptor; the head's dy rows also
+    // hold alpha's gradient at column 256)
+    if ((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(x)) & 15 || (lddy | ldx) & 3 ||
+        lddy < width + (head ? 1 : 0) || ldx < width || lddx < width || lddy >= (1 << 22) || ldx >= (1 << 22) ||
+        lddx >= (1 << 22))
+        return anerf_internal_fail(ANERF_EINVAL, (f + ": dy / x need 16 B aligned rows, ld % 4 == 0, width <= ld "
+                                                      "< 2^22 (head: dy ld > width; dx: width <= ld < 2^22)").c_str());
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    if (!workspace || workspace_bytes < anerf_mlp_backward_hidden_workspace(m, width))
-        return anerf_internal_fail(ANERF_EWORKSPACE, "anerf_mlp_backward_hidden: workspace too small");
+    if (!workspace || workspace_bytes < dgw_workspace(m, head))
+        return anerf_internal_fail(ANERF_EWORKSPACE, (f + ": workspace too small").c_str());
     if (m == 0) {  // (the slabs of an empty sum: one zero slab, so that a deferred reduce writes zeros)
-        hipError_t e = hipMemsetAsync(workspace, 0, anerf_mlp_backward_hidden_workspace(m, width), st);
+        hipError_t e = hipMemsetAsync(workspace, 0, dgw_workspace(m, head), st);
         if (e != hipSuccess) return anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));
-        return dw ? anerf_mlp_backward_hidden_reduce(m, width, workspace, workspace_bytes, dw, lddw, db, stream) : ANERF_OK;
+        return dw ? dgw_reduce(fn, head, m, width, workspace, workspace_bytes, dw, lddw, db, stream) : ANERF_OK;
     }
     DGWArgs g = {};
     const int nwg = dgw_plan(m, &g.rows_per_wg);
@@ -1573,31 +1656,55 @@ int anerf_mlp_backward_hidden(int64_t m, int32_t width, const float* dy, int64_t
     g.dx = dx;
     g.lddx = lddx;
     g.ws = static_cast<float*>(workspace);
-    g.wsb = g.ws + (size_t)nwg * DGW_W * DGW_W;
-    hipError_t e = hipFuncSetAttribute((const void*)mlp_dgw_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, DGW_LDS);
+    g.wsb = g.ws + (size_t)nwg * (head ? DGW_W + 1 : DGW_W) * DGW_W;
+    g.wa = wa;
+    const void* kern = head ? (const void*)mlp_dgw_kernel<true> : (const void*)mlp_dgw_kernel<false>;
+    hipError_t e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, DGW_LDS);
     if (e != hipSuccess) return anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));
-    hipLaunchKernelGGL(mlp_dgw_kernel, dim3((unsigned)nwg), dim3(DGW_THR), DGW_LDS, st, g);
+    if (head)
+        hipLaunchKernelGGL(mlp_dgw_kernel<true>, dim3((unsigned)nwg), dim3(DGW_THR), DGW_LDS, st, g);
+    else
+        hipLaunchKernelGGL(mlp_dgw_kernel<false>, dim3((unsigned)nwg), dim3(DGW_THR), DGW_LDS, st, g);
     e = hipGetLastError();
     if (e != hipSuccess) return anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));
-    return dw ? anerf_mlp_backward_hidden_reduce(m, width, workspace, workspace_bytes, dw, lddw, db, stream) : ANERF_OK;
+    return dw ? dgw_reduce(fn, head, m, width, workspace, workspace_bytes, dw, lddw, db, stream) : ANERF_OK;
+}
+}  // namespace
+
+extern "C" {
+
+size_t anerf_mlp_backward_hidden_workspace(int64_t m, int32_t width) {
+    return width != DGW_W || m < 0 ? 0 : dgw_workspace(m, false);
+}
+
+int anerf_mlp_backward_hidden(int64_t m, int32_t width, const float* dy, int64_t lddy, const float* x, int64_t ldx,
+                              const void* wt_split, int32_t precision, float* dx, int64_t lddx, float* dw, int64_t lddw,
+                              float* db, void* workspace, size_t workspace_bytes, void* stream) {
+    return dgw_launch("anerf_mlp_backward_hidden", false, m, width, dy, lddy, x, ldx, wt_split, nullptr, precision, dx,
+                      lddx, dw, lddw, db, workspace, workspace_bytes, stream);
 }
 
 int anerf_mlp_backward_hidden_reduce(int64_t m, int32_t width, const void* workspace, size_t workspace_bytes, float* dw,
                                      int64_t lddw, float* db, void* stream) {
-    if (width != DGW_W || m < 0 || !dw || !db || lddw < width)
-        return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_backward_hidden_reduce: bad arguments");
-    if (!workspace || workspace_bytes < anerf_mlp_backward_hidden_workspace(m, width))
-        return anerf_internal_fail(ANERF_EWORKSPACE, "anerf_mlp_backward_hidden_reduce: workspace too small");
-    long long rows;
-    const int nwg = dgw_plan(m, &rows);
-    const float* ws = static_cast<const float*>(workspace);
-    // dW rows 0 .. 255 and the bias row 256, summed over the workgroups' slabs in order
-    hipLaunchKernelGGL(mlp_reduce_kernel, dim3(DGW_W / 128, DGW_W + 1), dim3(256), 0,
-                       reinterpret_cast<hipStream_t>(stream), ws, nwg, (long long)DGW_W * DGW_W, (long long)DGW_W,
-                       DGW_W, dw, (long long)lddw, 0, DGW_W, ws + (size_t)nwg * DGW_W * DGW_W, (long long)DGW_W, DGW_W,
-                       db);
-    hipError_t e = hipGetLastError();
-    return e == hipSuccess ? ANERF_OK : anerf_internal_fail(ANERF_EHIP, hipGetErrorString(e));
+    return dgw_reduce("anerf_mlp_backward_hidden_reduce", false, m, width, workspace, workspace_bytes, dw, lddw, db,
+                      stream);
+}
+
+size_t anerf_mlp_backward_head_workspace(int64_t m, int32_t width) {
+    return width != DGW_W || m < 0 ? 0 : dgw_workspace(m, true);
+}
+
+int anerf_mlp_backward_head(int64_t m, int32_t width, const float* dy, int64_t lddy, const float* x, int64_t ldx,
+                            const void* wt_split, const float* w_alpha, int32_t precision, float* dx, int64_t lddx,
+                            float* dw, int64_t lddw, float* db, void* workspace, size_t workspace_bytes, void* stream) {
+    return dgw_launch("anerf_mlp_backward_head", true, m, width, dy, lddy, x, ldx, wt_split, w_alpha, precision, dx,
+                      lddx, dw, lddw, db, workspace, workspace_bytes, stream);
+}
+
+int anerf_mlp_backward_head_reduce(int64_t m, int32_t width, const void* workspace, size_t workspace_bytes, float* dw,
+                                   int64_t lddw, float* db, void* stream) {
+    return dgw_reduce("anerf_mlp_backward_head_reduce", true, m, width, workspace, workspace_bytes, dw, lddw, db,
+                      stream);
 }
 
 size_t anerf_mlp_wgrad_workspace(int64_t m, int32_t n, int32_t k) {

@@ -51,6 +51,9 @@ FUSED_BACKWARD = True
 # (round 6, with FUSED_BACKWARD) the skip layer's h part as one more fused pass and its x part merged into layer
 # 0's two products (the backward's comment below); an A/B switch for tools/train_bench.py
 FUSED_SKIP = True
+# (round 6, ABI 18, with FUSED_BACKWARD) the heads' backward (feature_linear + alpha_linear's rank-1 term) as one
+# fused pass, anerf_mlp_backward_head; an A/B switch for tools/train_bench.py
+FUSED_HEAD = True
 
 
 def _side_stream(dev):
@@ -250,9 +253,12 @@ class _MLP(torch.autograd.Function):
         if merge:
             tw[s1] = pw[s1][:, dnet:]
             tw[0] = torch.cat([pw[0], pw[s1][:, :dnet]]) if need_feat else None
+        # (round 6, ABI 18) the heads' backward on the fused pass too: feature_linear is a 256 x 256 layer on the last
+        # hidden layer's output, alpha_linear's rank-1 term joins its input gradient (anerf_mlp_backward_head)
+        fused_head = fused and FUSED_HEAD
         # every transposed plane in one launch: [trunk (layer 0 only for the feature gradient)..., head, views, rgb]
-        st = split_weights([(w, True) for w in tw[0 if need_feat else 1:]] + [(whead, True), (wv, True), (wr, True)],
-                           prec)
+        st = split_weights([(w, True) for w in tw[0 if need_feat else 1:]]
+                           + [(whead[:W] if fused_head else whead, True), (wv, True), (wr, True)], prec)
         st = ([None] if not need_feat else []) + st
         f32 = dict(device=dev, dtype=torch.float32)
         g_raw = g_raw.contiguous()
@@ -313,9 +319,27 @@ class _MLP(torch.autograd.Function):
                                                          _stream(dev)), "anerf_train_view_mix_backward")
         # feature_linear + alpha_linear: one input gradient, masked by relu(last hidden) > 0
         gz = torch.empty(M, W, **f32)
-        mm(M, W, W + 1, [_seg(gha, W + 1)], st[D], None, False,
-             [(gz, W, W, 0, H[-1], False)], dev)
-        dwh, dbh = wg(W + 1, W, gha, [_seg(H[-1], W)], (H[-1],))
+        if fused_head:
+            hws = torch.empty(lib.anerf_mlp_backward_head_workspace(M, W), device=dev, dtype=torch.uint8)
+            dwh, dbh = torch.empty(W + 1, W, **f32), torch.empty(W + 1, **f32)
+            defer = side is not None
+            _lib.check(lib.anerf_mlp_backward_head(M, W, _lib.ptr(gha), gha.stride(0), _lib.ptr(H[-1]), H[-1].stride(0),
+                                                   _lib.ptr(st[D]), _lib.ptr(wa.contiguous()), prec, _lib.ptr(gz),
+                                                   gz.stride(0), None if defer else _lib.ptr(dwh), dwh.stride(0),
+                                                   None if defer else _lib.ptr(dbh), _lib.ptr(hws), hws.numel(),
+                                                   _stream(dev)), "anerf_mlp_backward_head")
+            if defer:  # (the slabs' reduce beside the trunk's first passes)
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    _lib.check(lib.anerf_mlp_backward_head_reduce(M, W, _lib.ptr(hws), hws.numel(), _lib.ptr(dwh),
+                                                                  dwh.stride(0), _lib.ptr(dbh), _stream(dev)),
+                               "anerf_mlp_backward_head_reduce")
+                for t in (dwh, dbh, hws):
+                    t.record_stream(side)
+        else:
+            mm(M, W, W + 1, [_seg(gha, W + 1)], st[D], None, False,
+                 [(gz, W, W, 0, H[-1], False)], dev)
+            dwh, dbh = wg(W + 1, W, gha, [_seg(H[-1], W)], (H[-1],))
         grads[2 * nl + 2], grads[2 * nl + 3] = dwh[:W], dbh[:W]  # feature_linear
         grads[2 * nl + 0], grads[2 * nl + 1] = dwh[W:], dbh[W:]  # alpha_linear
         # the trunk, last layer first

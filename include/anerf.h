@@ -47,6 +47,7 @@
  *   anerf_mlp_gemm          forward (bias, relu) and input-gradient (relu' mask, accumulate) products
  *   anerf_mlp_wgrad         weight + bias gradients
  *   anerf_mlp_backward_hidden  both of a 256 x 256 hidden layer's backward products in one pass (round 6)
+ *   anerf_mlp_backward_head    the same for feature_linear with alpha_linear's rank-1 term (round 6, ABI 18)
  *   anerf_mlp_forward(_pack)  the whole forward in one kernel (opt-in alternative to the GEMMs)
  */
 #ifndef ANERF_H
@@ -59,7 +60,7 @@
 extern "C" {
 #endif
 
-#define ANERF_ABI_VERSION 17
+#define ANERF_ABI_VERSION 18
 
 enum {
     ANERF_OK = 0,
@@ -613,6 +614,25 @@ int anerf_mlp_backward_hidden(int64_t m, int32_t width, const float* dy, int64_t
 /* dw, db of an anerf_mlp_backward_hidden call made with dw = db = NULL, from its workspace (same m, width). */
 int anerf_mlp_backward_hidden_reduce(int64_t m, int32_t width, const void* workspace, size_t workspace_bytes, float* dw,
                                      int64_t lddw, float* db, void* stream);
+
+/* Workspace bytes of anerf_mlp_backward_head (0 for an unsupported width). */
+size_t anerf_mlp_backward_head_workspace(int64_t m, int32_t width);
+/* ABI 18: the backward of the heads on the last hidden layer's output x [m][256] -- feature_linear (256 x 256) and
+ * alpha_linear (1 x 256), core/networks/nerf.py:141-145 (the reference runs them as two nn.Linear; here, as in the
+ * forward, one [257][256] weight, feature rows then alpha's) -- in ONE pass over dy and x, as
+ * anerf_mlp_backward_hidden:
+ *   dx[m][i] = (sum_o dy[m][o] Wf[o][i] + dy[m][256] w_alpha[i]) if x[m][i] > 0 else 0
+ *   dw[o][i] = sum_m dy[m][o] x[m][i] for o < 257 (row 256: alpha's), db[o] = sum_m dy[m][o] (257 entries)
+ * dy rows hold the 256 feature gradients then alpha's at column 256 (lddy >= 257, % 4 == 0); wt_split: Wf's
+ * transposed bf16x3 planes (anerf_mlp_split_weights(Wf, 256, 256, ld, 1, ANERF_MLP_BF16X3)); w_alpha [256] fp32.
+ * Feature part in bf16x3 (as anerf_mlp_backward_hidden), alpha's terms in fp32.  dw [257][lddw], db [257], or
+ * both NULL for a later anerf_mlp_backward_head_reduce. */
+int anerf_mlp_backward_head(int64_t m, int32_t width, const float* dy, int64_t lddy, const float* x, int64_t ldx,
+                            const void* wt_split, const float* w_alpha, int32_t precision, float* dx, int64_t lddx,
+                            float* dw, int64_t lddw, float* db, void* workspace, size_t workspace_bytes, void* stream);
+/* dw [257][lddw], db [257] of an anerf_mlp_backward_head call made with dw = db = NULL (same m, width). */
+int anerf_mlp_backward_head_reduce(int64_t m, int32_t width, const void* workspace, size_t workspace_bytes, float* dw,
+                                   int64_t lddw, float* db, void* stream);
 
 #ifdef __cplusplus
 }

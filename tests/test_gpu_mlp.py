@@ -275,13 +275,16 @@ def test_nerf_forward_backward_matches_fp32_module(D, W, fc, nj, impl):
         assert rel(gp_b[k], gp_f[k]) <= 5e-3, (k, rel(gp_b[k], gp_f[k]))
 
 
+@pytest.mark.parametrize("switch", ["FUSED_SKIP", "FUSED_HEAD"])
 @pytest.mark.parametrize("D,fc,nj,need_feat", [(8, False, 24, True), (8, True, 17, True), (8, False, 65, True),
                                                 (8, False, 24, False), (6, False, 24, True)])
-def test_fused_skip_layer_backward_matches_two_gemms(D, fc, nj, need_feat, monkeypatch):
+def test_fused_skip_and_head_backward_match_two_gemms(D, fc, nj, need_feat, switch, monkeypatch):
     """mlp.FUSED_SKIP (round 6): the skip layer's h part on anerf_mlp_backward_hidden and its x part merged into
-    layer 0's products ([dY_0 | dY_s] against [W_0 ; W_s,x]) == the skip layer as two GEMMs and layer 0 apart: the
-    same bf16x3 products summed in another order, so every gradient within 1e-5 (relative Frobenius).  17 / 65
-    joints: zero-padded kp + bone blocks; D 6: the skip layer is the last (no merge); no feature gradient."""
+    layer 0's products ([dY_0 | dY_s] against [W_0 ; W_s,x]); mlp.FUSED_HEAD (ABI 18): feature_linear +
+    alpha_linear on anerf_mlp_backward_head.  Each == the same layers as two GEMMs: FUSED_SKIP the same bf16x3
+    products summed in another order, every gradient within 1e-5 (relative Frobenius); FUSED_HEAD computes alpha's
+    terms in fp32 where the GEMMs take them as bf16x3 products (relative error ~4e-5 each, REL[3]), so within 1e-4.
+    17 / 65 joints: zero-padded kp + bone blocks; D 6: the skip layer is the last (no merge); no feature gradient."""
     mlp = importlib.import_module("a-nerf_amd.mlp")
     cfg = anerf.RenderConfig(n_joints=nj, netdepth=D, netwidth=256, opt_framecode=fc,
                              n_framecodes=5 if fc else 0).validate()
@@ -293,7 +296,7 @@ def test_fused_skip_layer_backward_matches_two_gemms(D, fc, nj, need_feat, monke
     gout = torch.randn(M, 4, device=DEV)
     res = {}
     for on in (True, False):
-        monkeypatch.setattr(mlp, "FUSED_SKIP", on)
+        monkeypatch.setattr(mlp, switch, on)
         tr = train.TrainRayCaster(cfg, ck, mlp="mixed").train()
         net = tr.network_fn
         f = feat.clone().requires_grad_(need_feat)
@@ -302,13 +305,14 @@ def test_fused_skip_layer_backward_matches_two_gemms(D, fc, nj, need_feat, monke
 
     def rel(a, b):
         return float((a.double() - b.double()).norm() / max(b.double().norm(), 1e-30))
+    tol = 1e-5 if switch == "FUSED_SKIP" else 1e-4
     if need_feat:
-        assert rel(res[True][0], res[False][0]) <= 1e-5
+        assert rel(res[True][0], res[False][0]) <= tol
     else:
         assert res[True][0] is None
     for k in res[False][1]:
         assert res[True][1][k].shape == res[False][1][k].shape
-        assert rel(res[True][1][k], res[False][1][k]) <= 1e-5, (k, rel(res[True][1][k], res[False][1][k]))
+        assert rel(res[True][1][k], res[False][1][k]) <= tol, (k, rel(res[True][1][k], res[False][1][k]))
 
 
 @pytest.mark.parametrize("D,W,fc,nj,M", [(8, 256, False, 24, 5000), (4, 128, True, 24, 3001), (8, 256, True, 17, 77),
@@ -461,3 +465,101 @@ def test_backward_hidden_deferred_reduce_is_identical():
         assert torch.equal(dw0, dw1) and torch.equal(db0, db1)
         if m == 0:
             assert not dw1.any() and not db1.any()
+
+
+def _backward_head(m, dy, x, wf, wa, lddx=None, defer=False):
+    """anerf_mlp_backward_head on dy [m][>= 257] (feature gradients, then alpha's at column 256) and x [m][256]."""
+    lib = mlp._lib.load()
+    dev = torch.device(DEV)
+    P = mlp._lib.ptr
+    wt = mlp.split_weight(wf, True, 3)
+    dx = torch.full((m, lddx or 256), float("nan"), device=DEV)
+    dw, db = torch.full((257, 256), 7.0, device=DEV), torch.full((257,), 7.0, device=DEV)
+    ws = torch.empty(lib.anerf_mlp_backward_head_workspace(m, 256), device=DEV, dtype=torch.uint8)
+    mlp._lib.check(lib.anerf_mlp_backward_head(m, 256, P(dy), dy.stride(0), P(x), x.stride(0), P(wt), P(wa), 3, P(dx),
+                                               dx.stride(0), None if defer else P(dw), 256, None if defer else P(db),
+                                               P(ws), ws.numel(), mlp._stream(dev)), "anerf_mlp_backward_head")
+    if defer:
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            mlp._lib.check(lib.anerf_mlp_backward_head_reduce(m, 256, P(ws), ws.numel(), P(dw), 256, P(db),
+                                                              mlp._stream(dev)), "anerf_mlp_backward_head_reduce")
+        torch.cuda.synchronize()
+    return dx, dw, db
+
+
+@pytest.mark.parametrize("m", [163840, 5000, 777, 33, 1, 300001])
+def test_backward_head_matches_fp64(m):
+    """Round 6 (ABI 18): feature_linear + alpha_linear's backward in one pass, against fp64 torch: dX = (dY_f Wf +
+    g_a w_a^T) masked by X > 0 at the bf16x3 bound of the feature part (alpha's rank-1 term in fp32), dW [257][256]
+    (row 256 = g_a^T X, fp32 sums), db [257]; ragged m, strided rows (dy ld 260 as the training backward's [g_feature
+    | g_alpha | pad] buffer, the pad columns holding garbage that must not reach any output)."""
+    torch.manual_seed(m % 997)
+    dy = torch.randn(m, 260, device=DEV)
+    dy[:, 257:] = float("nan")  # (never read)
+    x = torch.relu(torch.randn(m, 264, device=DEV))[:, :256]
+    wf = torch.randn(256, 256, device=DEV) / 16
+    wa = torch.randn(1, 256, device=DEV) / 16
+    dx, dw, db = _backward_head(m, dy, x, wf, wa, lddx=257)
+    dyf, ga = dy[:, :256].double(), dy[:, 256].double()
+    full = dyf @ wf.double() + ga[:, None] * wa.double()
+    ref_dx = torch.where(x > 0, full, torch.zeros_like(full))
+    bound = _bound(dy[:, :256], wf.t(), 3) + 1e-6 * (ga.abs()[:, None] * wa.double().abs())
+    assert not torch.isnan(dx[:, :256]).any()
+    assert torch.all((dx[:, :256].double() - ref_dx).abs() <= bound), float((dx[:, :256].double() - ref_dx).abs().max())
+    assert torch.isnan(dx[:, 256]).all()
+    ref_w = dy[:, :257].double().t() @ x.double()
+    bw = 2 * REL[3] * (dy[:, :257].double().abs().t() @ x.double().abs()) + 1e-5
+    bw[256] = 1e-5 * (ga.abs() @ x.double().abs()) + 1e-5  # (alpha's row: fp32 sums)
+    assert torch.all((dw.double() - ref_w).abs() <= bw), float((dw.double() - ref_w).abs().max())
+    ref_b = dy[:, :257].double().sum(0)
+    assert torch.all((db.double() - ref_b).abs() <= 1e-5 * dy[:, :257].double().abs().sum(0) + 1e-5)
+
+
+def test_backward_head_deferred_and_deterministic():
+    """The deferred reduce (another stream) gives the in-call reduce's bits, a second call is bit-identical, and the
+    feature part equals anerf_mlp_backward_hidden's on the same dY columns when alpha's gradient is zero."""
+    torch.manual_seed(11)
+    m = 20000
+    dy = torch.randn(m, 260, device=DEV)
+    x = torch.relu(torch.randn(m, 256, device=DEV))
+    wf, wa = torch.randn(256, 256, device=DEV) / 16, torch.randn(1, 256, device=DEV) / 16
+    a = _backward_head(m, dy, x, wf, wa)
+    b = _backward_head(m, dy, x, wf, wa, defer=True)
+    c = _backward_head(m, dy, x, wf, wa)
+    for u, v, w in zip(a, b, c):
+        assert torch.equal(u, v) and torch.equal(u, w)
+    dy0 = dy.clone()
+    dy0[:, 256] = 0.0
+    dxh, dwh, dbh = _backward_head(m, dy0, x, wf, wa)
+    dx1, dw1, db1 = _backward_hidden(m, dy0[:, :256], x, wf)
+    assert torch.equal(dxh, dx1) and torch.equal(dwh[:256], dw1) and torch.equal(dbh[:256], db1)
+    assert not dwh[256].any() and float(dbh[256]) == 0.0
+
+
+def test_backward_head_rejects_bad_arguments():
+    lib = mlp._lib.load()
+    m = 64
+    P = mlp._lib.ptr
+    st = mlp._stream(torch.device(DEV))
+    dy, x = torch.randn(m, 260, device=DEV), torch.randn(m, 256, device=DEV)
+    out = torch.empty(m, 256, device=DEV)
+    dw, db = torch.empty(257, 256, device=DEV), torch.empty(257, device=DEV)
+    wa = torch.randn(256, device=DEV)
+    ws = torch.empty(lib.anerf_mlp_backward_head_workspace(m, 256), device=DEV, dtype=torch.uint8)
+    wt = mlp.split_weight(torch.randn(256, 256, device=DEV), True, 3)
+    assert lib.anerf_mlp_backward_head_workspace(m, 128) == 0
+    assert lib.anerf_mlp_backward_head_workspace(m, 256) > lib.anerf_mlp_backward_hidden_workspace(m, 256)
+    ok = (m, 256, P(dy), 260, P(x), 256, P(wt), P(wa), 3, P(out), 256, P(dw), 256, P(db), P(ws), ws.numel(), st)
+    assert lib.anerf_mlp_backward_head(*ok) == 0
+    bad_ld = list(ok)
+    bad_ld[3] = 256  # (no room for alpha's column)
+    assert lib.anerf_mlp_backward_head(*bad_ld) == -1
+    no_wa = list(ok)
+    no_wa[7] = None
+    assert lib.anerf_mlp_backward_head(*no_wa) == -1
+    small = list(ok)
+    small[15] = lib.anerf_mlp_backward_hidden_workspace(m, 256)  # (the hidden pass's size is too small here)
+    assert lib.anerf_mlp_backward_head(*small) == -3
+    torch.cuda.synchronize()

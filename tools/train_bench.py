@@ -62,6 +62,8 @@ def parser():
                          "(rounds 1-5): a skts + delta leaf per image")
     ap.add_argument("--no-fused-skip", action="store_true",
                     help="ablation: the skip layer's backward as two GEMMs and its x part apart from layer 0's")
+    ap.add_argument("--no-fused-head", action="store_true",
+                    help="ablation: the heads' backward as two GEMMs")
     ap.add_argument("--split-single", action="store_true",
                     help="ablation: one split launch per weight instead of the batched split")
     ap.add_argument("--probe", default="", choices=["", "no-hidden-reduce", "no-wgrad", "no-wgrad-no-reduce"],
@@ -98,6 +100,7 @@ def measure(a, dev=None):
         importlib.import_module("a-nerf_amd.mlp").WGRAD_OVERLAP = False
     importlib.import_module("a-nerf_amd.mlp").FUSED_BACKWARD = not getattr(a, "no_fused_backward", False)
     importlib.import_module("a-nerf_amd.mlp").FUSED_SKIP = not getattr(a, "no_fused_skip", False)
+    importlib.import_module("a-nerf_amd.mlp").FUSED_HEAD = not getattr(a, "no_fused_head", False)
     tr = train.TrainRayCaster(cfg, ck, device=dev, mlp=a.mlp).train()
     tr.view_windows = not getattr(a, "full_view", False)
     adam_kw = {"fused": True} if getattr(a, "adam", "foreach") == "fused" else {"foreach": True}
@@ -199,6 +202,8 @@ def measure(a, dev=None):
         "hidden_backward": ("fused (anerf_mlp_backward_hidden: input + weight gradients from one read of dY and H)"
                             + ("; the skip layer's h part fused too, its x part merged with layer 0's products"
                                if importlib.import_module("a-nerf_amd.mlp").FUSED_SKIP else "")
+                            + ("; the heads (feature_linear + alpha_linear's rank-1 term) fused"
+                               if importlib.import_module("a-nerf_amd.mlp").FUSED_HEAD else "")
                             if importlib.import_module("a-nerf_amd.mlp").FUSED_BACKWARD and a.mlp in ("mixed", "bf16x3",
                                                                                                     "mixed16")
                             else "two GEMMs (anerf_mlp_gemm + anerf_mlp_wgrad)"),
