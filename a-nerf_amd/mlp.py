@@ -57,7 +57,10 @@ FUSED_HEAD = True
 
 
 def _side_stream(dev):
-    key = torch.device(dev).index
+    """The side stream of the caller's current stream (one per (device, stream): the training step runs the fine
+    pass on a stream of its own, train.FINE_STREAM, and the two passes' weight gradients must not queue behind
+    each other's)."""
+    key = (torch.device(dev).index, torch.cuda.current_stream(dev).stream_id)
     if key not in _SIDE:
         _SIDE[key] = torch.cuda.Stream(device=dev)
     return _SIDE[key]

@@ -33,6 +33,25 @@ def _stream(dev):
     return _lib.stream_handle(dev)
 
 
+# (round 6) the fine pass of a training step on a stream of its own: the coarse and fine networks' backward passes
+# are independent (the fine samples come from the detached coarse weights, raycasters.py:456-466), and autograd runs
+# each node on the stream its forward ran on, so the two backward passes overlap on the GPU -- each pass's GEMMs
+# are latency-bound (≈40 % of the MFMA rate) and could fill each other's gaps.  Measured 1.5 %
+# SLOWER (profiles/r06s_train_fine_stream_ab.txt: the fused backward passes hold a CU each with 152 KB of LDS, so
+# the other pass's kernels cannot share it, and the two passes' activations compete for the caches), so off: an
+# A/B switch for tools/train_bench.py (bit-identical results either way, tests/test_gpu_train.py), never read from
+# the environment.
+FINE_STREAM = False
+_FINE = {}
+
+
+def _fine_stream(dev):
+    key = torch.device(dev).index
+    if key not in _FINE:
+        _FINE[key] = torch.cuda.Stream(device=dev)
+    return _FINE[key]
+
+
 # ----------------------------------------------------------------------------- autograd stages
 class _Encode(torch.autograd.Function):
     """encode_inputs of every sample (raycasters.py:476-555): features [N*S, F]; backward -> dL/dskts."""
@@ -767,8 +786,25 @@ class TrainRayCaster(nn.Module):
                 if pn0 is not None:
                     pn1 = torch.gather(torch.cat([pn0, pn_is], 1), 1,
                                        sidx.long()[..., None].expand(-1, -1, 3)).contiguous()
-                raw1 = raw_of(self.network_fine, z_all, pn1)
-            rgb1, disp1, acc1, w1, a1 = composite(raw1, z_all, noise_for("noise1", S + I))
+                noise1 = noise_for("noise1", S + I)
+                if FINE_STREAM and torch.is_grad_enabled():
+                    main = torch.cuda.current_stream(dev)
+                    fine = _fine_stream(dev)
+                    fine.wait_stream(main)
+                    for t in (rb, sk, z_all, pn1, noise1, cam_t, fscale, fs_view):  # (made on main, read on fine)
+                        if t is not None:
+                            t.record_stream(fine)
+                    with torch.cuda.stream(fine):
+                        raw1 = raw_of(self.network_fine, z_all, pn1)
+                        rgb1, disp1, acc1, w1, a1 = composite(raw1, z_all, noise1)
+                    main.wait_stream(fine)
+                    for t in (rgb1, disp1, acc1, w1, a1):  # (made on fine, read on main)
+                        t.record_stream(main)
+                else:
+                    raw1 = raw_of(self.network_fine, z_all, pn1)
+                    rgb1, disp1, acc1, w1, a1 = composite(raw1, z_all, noise1)
+            if cfg.single_net:
+                rgb1, disp1, acc1, w1, a1 = composite(raw1, z_all, noise_for("noise1", S + I))
             out = {"rgb_map": rgb1, "disp_map": disp1, "acc_map": acc1, "alpha": a1,
                    "rgb0": rgb, "disp0": disp, "acc0": acc, "alpha0": a}
         return out

@@ -122,6 +122,47 @@ def test_train_parameter_gradients_match_reference(run):
     assert n_checked >= 10
 
 
+@pytest.mark.parametrize("name", ["t2_s64i16_d8w256", "t14_nj65_d8w256"])
+def test_fine_stream_is_bit_identical(name, monkeypatch):
+    """train.FINE_STREAM (round 6, measured slower and off by default): the fine pass on its own stream, so that the
+    coarse and fine backward passes overlap, gives the single-stream step's outputs, pose gradient and parameter
+    gradients bit for bit (the same kernels on the same inputs; the streams only reorder independent work), over a
+    step of Adam and a second forward."""
+    if name not in TRAIN:
+        pytest.skip(f"{name}: no golden")
+    res = {}
+    for on in (True, False):
+        monkeypatch.setattr(train, "FINE_STREAM", on)
+        g, tr, sk, out, loss = _run(name)
+        opt = torch.optim.Adam(tr.parameters(), lr=1e-3)
+        opt.step()
+        out2 = _run_again(g, tr)
+        torch.cuda.synchronize()
+        res[on] = ({k: v.detach().clone() for k, v in out.items()}, sk.grad.clone(),
+                   {k: p.detach().clone() for k, p in tr.named_parameters()}, out2)
+    (o1, s1, p1, q1), (o0, s0, p0, q0) = res[True], res[False]
+    for k in o0:
+        assert torch.equal(o1[k], o0[k]), k
+    assert torch.equal(s1, s0)
+    for k in p0:
+        assert torch.equal(p1[k], p0[k]), k
+    for k in q0:
+        assert torch.equal(q1[k], q0[k]), k
+
+
+def _run_again(g, tr):
+    """A second forward of the stepped model on the golden's rays (its outputs, detached)."""
+    m = g.meta
+    dev = torch.device("cuda:0")
+    c = lambda k: torch.from_numpy(g[k]).to(dev)  # noqa: E731
+    rand = {k: c("rand_" + k) for k in ("t_rand", "noise0", "u", "noise1", "pts_noise0", "pts_noise1")
+            if g.has("rand_" + k)}
+    out = tr.render_rays(c("rays"), m["S"], skts=c("skts"), cyls=c("cyls"), cams=c("cams") if g.has("cams") else None,
+                         perturb=1.0, N_importance=m["I"], raw_noise_std=m["raw_noise_std"], rand=rand,
+                         lindisp=m.get("lindisp", False), ray_noise_std=m.get("ray_noise_std", 0.0))
+    return {k: v.detach().clone() for k, v in out.items()}
+
+
 def test_eval_mode_delegates_to_fused_kernel():
     g = Golden("t1_s32i16_d4w128")
     m = g.meta

@@ -62,6 +62,8 @@ def parser():
                          "(rounds 1-5): a skts + delta leaf per image")
     ap.add_argument("--no-fused-skip", action="store_true",
                     help="ablation: the skip layer's backward as two GEMMs and its x part apart from layer 0's")
+    ap.add_argument("--no-fine-stream", action="store_true",
+                    help="ablation: the fine pass on the caller's stream (its backward then follows the coarse one's)")
     ap.add_argument("--no-fused-head", action="store_true",
                     help="ablation: the heads' backward as two GEMMs")
     ap.add_argument("--split-single", action="store_true",
@@ -101,6 +103,7 @@ def measure(a, dev=None):
     importlib.import_module("a-nerf_amd.mlp").FUSED_BACKWARD = not getattr(a, "no_fused_backward", False)
     importlib.import_module("a-nerf_amd.mlp").FUSED_SKIP = not getattr(a, "no_fused_skip", False)
     importlib.import_module("a-nerf_amd.mlp").FUSED_HEAD = not getattr(a, "no_fused_head", False)
+    train.FINE_STREAM = not getattr(a, "no_fine_stream", False)
     tr = train.TrainRayCaster(cfg, ck, device=dev, mlp=a.mlp).train()
     tr.view_windows = not getattr(a, "full_view", False)
     adam_kw = {"fused": True} if getattr(a, "adam", "foreach") == "fused" else {"foreach": True}
@@ -207,6 +210,7 @@ def measure(a, dev=None):
                             if importlib.import_module("a-nerf_amd.mlp").FUSED_BACKWARD and a.mlp in ("mixed", "bf16x3",
                                                                                                     "mixed16")
                             else "two GEMMs (anerf_mlp_gemm + anerf_mlp_wgrad)"),
+        "fine_stream": bool(train.FINE_STREAM),
         "joints": nj,
         "view_layout": (f"view windows (anerf.h ANERF_ENC_VIEW_WINDOWS: {nj} windows per sample + per-ray factors)"
                         if tr.model.view_windows else f"full view columns ({cfg.input_ch_views} per sample)"),
