@@ -35,7 +35,7 @@ ANERF_ENC_VIEW_RAW = 8  # --view_type world
 ANERF_ENC_KP_RELPOS, ANERF_ENC_VIEW_ANGLE = 16, 32  # --kp_dist_type relpos, --view_type rayangle (staged, ABI 15)
 ANERF_ENC_KP_QUERYPTS = 64  # --kp_dist_type querypts (staged, ABI 15)
 ANERF_ENC_VIEW_WINDOWS = 128  # training layout: the view part as the NJ view windows (ABI 16)
-ABI_VERSION = 18  # include/anerf.h ANERF_ABI_VERSION: the structs below
+ABI_VERSION = 19  # include/anerf.h ANERF_ABI_VERSION: the structs below
 
 
 class ModelDesc(ctypes.Structure):
@@ -235,6 +235,9 @@ SIGNATURES = {
                                                  ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32,
                                                  ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,
                                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "anerf_mlp_forward_hidden": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64,
+                                                ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                                ctypes.c_int64, ctypes.c_void_p]),
     "anerf_mlp_backward_head_workspace": (ctypes.c_size_t, [ctypes.c_int64, ctypes.c_int32]),
     "anerf_mlp_backward_head_reduce": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p, ctypes.c_size_t,
                                                       ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,

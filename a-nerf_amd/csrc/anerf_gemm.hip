@@ -1366,6 +1366,246 @@ int dgw_plan(int64_t m, long long* rows_per_wg) {
     return (int)((chunks + per - 1) / per);
 }
 
+// ---------------------------------------------------------------- hidden layer forward, persistent (round 6)
+// y = relu(x W^T + b) of one 256 x 256 hidden layer (pts_linears[i], core/networks/nerf.py:133-139) with the
+// arithmetic of mlp_nt_kernel<NPL, 1> (x and W split into NPL bf16 planes, the same products in the same order
+// per k16 step, k16 steps ascending from a zero accumulator, + bias, relu): the outputs are bit-identical to
+// anerf_mlp_gemm's.  What changes is the schedule.  mlp_nt_kernel runs 128 x 128 tiles, two per CU, each staging its
+// A rows, looping eight k32 steps and storing through its epilogue in turn: in the training step a layer ran at
+// 2.3-2.5 TB/s of its 336 MB (M = 163,840) with every byte moved once, i.e. bound by the tiles' serial
+// prologue / k-loop / epilogue latency, not by bandwidth.  Here one persistent workgroup per CU walks a contiguous
+// row range in 64-row chunks, each as two units of 128 k columns, with the work split by role (as mlp_dgw_kernel):
+//   * stager waves (0-3): load a unit's x rows from HBM one unit ahead, split them into the LDS planes of the other
+//     stage, and copy the previous chunk's output tile from LDS to HBM in whole-row 16 B stores;
+//   * compute waves (4-7): output columns 64 (w - 4) .. + 63 of every chunk (2 x 2 blocks of 32 x 32), the split W
+//     fragments from L2 in a 4-deep ring that runs on across units and chunks, the A fragments from LDS; after a
+//     chunk's second unit, bias + relu into the LDS output tile.
+// So the compute waves issue no HBM access at all (their in-order vmcnt holds only L2 weight loads) and the HBM
+// reads, the splits and the stores overlap the MFMAs of the current unit.
+// LDS: two stages of NPL planes [64][128] bf16 (256 B rows, the 16 B chunks XOR-swizzled by row & 15: the staging
+// writes, 16 lanes x one row, and the fragment reads, 16 rows x one chunk, are conflict-free) + the fp32 output
+// tile [64][256] (64 KB): 160 KB at bf16x6, 128 KB at bf16x3.
+constexpr int FW_W = 256;     // layer width (inputs = outputs)
+constexpr int FW_CH = 64;     // rows per chunk
+constexpr int FW_KH = 128;    // k columns per unit (a chunk is two units)
+constexpr int FW_THR = 512;   // eight waves
+constexpr int FW_BD = 4;      // W fragment ring depth (k16 steps; divides a unit's 8)
+template <int NPL>
+struct FWGeo {
+    static constexpr int PLANE = FW_CH * FW_KH * 2;  // 16 KB
+    static constexpr int STAGE = NPL * PLANE;
+    static constexpr int OUT = FW_CH * FW_W * 4;     // 64 KB
+    static constexpr int LDS = 2 * STAGE + OUT;
+};
+
+struct FWArgs {
+    long long M, rows_per_wg;
+    const float* x;
+    long long ldx;
+    const unsigned short* w;  // split W, NPL bf16 planes (anerf_mlp_split_weights, transpose = 0)
+    const float* bias;
+    float* y;
+    long long ldy;
+};
+
+__device__ __forceinline__ int fw_off(int row, int chunk) { return row * 256 + ((chunk ^ (row & 15)) << 4); }
+
+template <int NPL>
+__global__ __launch_bounds__(FW_THR, 1) void mlp_fwd_kernel(FWArgs g) {
+    using G = FWGeo<NPL>;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds8[];
+    float* const otile = reinterpret_cast<float*>(lds8 + 2 * G::STAGE);  // [64][256]
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const long long M = g.M;
+    const long long mlo = (long long)blockIdx.x * g.rows_per_wg;
+    const long long mhi = mlo + g.rows_per_wg < M ? mlo + g.rows_per_wg : M;
+    const int nch = mhi > mlo ? (int)((mhi - mlo + FW_CH - 1) / FW_CH) : 0;
+    const int nun = 2 * nch;  // units
+    auto chunk_rows = [&](int s) {
+        long long rows = mhi - (mlo + (long long)s * FW_CH);
+        return (int)(rows < 0 ? 0 : (rows > FW_CH ? FW_CH : rows));
+    };
+
+    if (wave < 4) {
+        // ------------------------------------------------------------------ stager waves
+        // thread t < 256: columns c8 .. c8 + 7 of the unit (two float4 loads) in rows r16 + 16 p (p < 4)
+        const int c8 = 8 * (tid & 15), r16 = tid >> 4;
+        const long long ldx = g.ldx, ldy = g.ldy;
+        const unsigned vox = (unsigned)((r16 * ldx + c8) * 4);
+        const int xstep = (int)(16 * ldx * 4);
+        f32x4 R[4][2];
+        auto fetch = [&](int u) {
+            const int s = u >> 1, kh = u & 1;
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(g.x + (mlo + (long long)s * FW_CH) * ldx), 0, (int)(chunk_rows(s) * ldx * 4), 0x00020000);
+#pragma unroll
+            for (int p = 0; p < 4; ++p)
+#pragma unroll
+                for (int f = 0; f < 2; ++f)
+                    R[p][f] = __builtin_bit_cast(
+                        f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vox, p * xstep + 4 * FW_KH * kh + 16 * f, 0));
+        };
+        auto stage = [&](int buf) {
+            unsigned char* const S = lds8 + buf * G::STAGE;
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+                float v[8];
+#pragma unroll
+                for (int f = 0; f < 2; ++f)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        // (through float rvalues: clang's bit_cast of a vector-element lvalue reads element 0)
+                        const float t = R[p][f][e];
+                        v[4 * f + e] = t;
+                    }
+                const int off = fw_off(r16 + 16 * p, c8 >> 3);
+                // (mlp_nt_kernel's split: round to nearest even, the exact remainder split again)
+#pragma unroll
+                for (int pl = 0; pl < NPL; ++pl) {
+                    u32x4 w;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const bf16x2 h = __builtin_convertvector((f32x2){v[2 * q], v[2 * q + 1]}, bf16x2);
+                        w[q] = __builtin_bit_cast(unsigned, h);
+                        if (pl + 1 < NPL) {
+                            v[2 * q] -= (float)h[0];
+                            v[2 * q + 1] -= (float)h[1];
+                        }
+                    }
+                    *reinterpret_cast<u32x4*>(S + pl * G::PLANE + off) = w;
+                }
+            }
+        };
+        // the output tile of chunk s: thread t, rows 4 q + (t >> 6), columns 4 (t & 63) .. + 3 (a wave
+        // instruction stores one whole 1 KB row); the descriptor ends at the chunk's last row
+        auto copy_out = [&](int s) {
+            const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(g.y + (mlo + (long long)s * FW_CH) * ldy), 0, (int)(chunk_rows(s) * ldy * 4), 0x00020000);
+            const int c4 = 4 * (tid & 63), rq = tid >> 6;
+            const unsigned vo = (unsigned)((rq * ldy + c4) * 4);
+#pragma unroll
+            for (int q = 0; q < FW_CH / 4; ++q) {
+                const f32x4 v = *reinterpret_cast<const f32x4*>(otile + (4 * q + rq) * FW_W + c4);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rd, vo, (int)(4 * q * ldy * 4), 0);
+            }
+        };
+        if (nun > 0) {
+            fetch(0);
+            stage(0);
+            fetch(1);
+        }
+        __syncthreads();
+        for (int u = 0; u < nun; ++u) {
+            if (u >= 2 && !(u & 1)) copy_out((u >> 1) - 1);  // (written before the barrier that ended unit u - 1)
+            if (u + 1 < nun) stage((u + 1) & 1);              // (free since the barrier that ended unit u - 1)
+            if (u + 2 < nun) fetch(u + 2);
+            __syncthreads();
+        }
+        if (nch > 0) copy_out(nch - 1);
+    } else {
+        // ------------------------------------------------------------------ compute waves
+        const int xw = wave - 4;  // output columns 64 xw .. 64 xw + 63: blocks 2 xw, 2 xw + 1
+        constexpr int WBS = (FW_W / 16) * NPL * 512;  // elements per 32-column block of the split W
+        const __amdgpu_buffer_rsrc_t rw =
+            __builtin_amdgcn_make_buffer_rsrc((void*)(g.w + (long long)(2 * xw) * WBS), 0, 2 * WBS * 2, 0x00020000);
+        const unsigned vwl = (unsigned)lane * 16;
+        struct WF {
+            u32x4 v[2][NPL];  // [block][plane]
+        };
+        auto fetch_w = [&](int kt, WF& f) {
+            kt &= FW_W / 16 - 1;
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int p = 0; p < NPL; ++p)
+                    f.v[j][p] = __builtin_bit_cast(
+                        u32x4, __builtin_amdgcn_raw_buffer_load_b128(rw, vwl, (j * WBS + (kt * NPL + p) * 512) * 2, 0));
+        };
+        const float b0 = g.bias[64 * xw + (lane & 31)], b1 = g.bias[64 * xw + 32 + (lane & 31)];
+        WF wf[FW_BD];
+#pragma unroll
+        for (int j = 0; j < FW_BD - 1; ++j) fetch_w(j, wf[j]);
+        f32x16 acc[2][2];
+        __syncthreads();
+        for (int u = 0; u < nun; ++u) {
+            const unsigned char* const S = lds8 + (u & 1) * G::STAGE;
+            const int kh = u & 1;
+            if (!kh) {
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{0};
+            }
+#pragma unroll
+            for (int t = 0; t < FW_KH / 16; ++t) {
+                __builtin_amdgcn_sched_barrier(0);
+                fetch_w(8 * kh + t + FW_BD - 1, wf[(t + FW_BD - 1) % FW_BD]);  // ((8 kh + t) % FW_BD = t % FW_BD)
+                __builtin_amdgcn_sched_barrier(0);
+                bf16x8 a[NPL][2];
+#pragma unroll
+                for (int p = 0; p < NPL; ++p)
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+                        a[p][i] = *reinterpret_cast<const bf16x8*>(S + p * G::PLANE +
+                                                                   fw_off(32 * i + (lane & 31), 2 * t + (lane >> 5)));
+                const WF& f = wf[t % FW_BD];
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    bf16x8 b[NPL];
+#pragma unroll
+                    for (int p = 0; p < NPL; ++p) b[p] = __builtin_bit_cast(bf16x8, f.v[j][p]);
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {  // (mlp_nt_kernel's product order: small terms first)
+                        f32x16 c = acc[i][j];
+                        if constexpr (NPL == 3) {
+                            c = mfma(a[2][i], b[0], c);
+                            c = mfma(a[1][i], b[1], c);
+                            c = mfma(a[0][i], b[2], c);
+                        }
+                        c = mfma(a[1][i], b[0], c);
+                        c = mfma(a[0][i], b[1], c);
+                        acc[i][j] = mfma(a[0][i], b[0], c);
+                    }
+                }
+            }
+            if (kh) {  // the chunk's output: + bias, relu, into the tile (its previous copy left before the barrier
+                       // that ended unit u - 1)
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) {
+                            const int row = 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                            float v = acc[i][j][r];
+                            v += j ? b1 : b0;
+                            v = fmaxf(v, 0.0f);
+                            otile[row * FW_W + 64 * xw + 32 * j + (lane & 31)] = v;
+                        }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// rows per workgroup: one persistent workgroup per CU over whole 64-row chunks
+int fw_plan(int64_t m, long long* rows_per_wg) {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) ==
+                                                    hipSuccess && n > 0)
+            cus = n;
+        else
+            cus = 256;
+    }
+    long long chunks = (m + FW_CH - 1) / FW_CH;
+    if (chunks < 1) chunks = 1;
+    const long long per = (chunks + cus - 1) / cus;
+    *rows_per_wg = per * FW_CH;
+    return (int)((chunks + per - 1) / per);
+}
+
 inline int rup(long long x, int a) { return (int)((x + a - 1) / a * a); }
 
 int planes_of(int precision) {
@@ -1688,6 +1928,47 @@ int anerf_mlp_backward_hidden_reduce(int64_t m, int32_t width, const void* works
                                      int64_t lddw, float* db, void* stream) {
     return dgw_reduce("anerf_mlp_backward_hidden_reduce", false, m, width, workspace, workspace_bytes, dw, lddw, db,
                       stream);
+}
+
+int anerf_mlp_forward_hidden(int64_t m, int32_t width, const float* x, int64_t ldx, const void* w_split,
+                             int32_t precision, const float* bias, float* y, int64_t ldy, void* stream) {
+    const char* fn = "anerf_mlp_forward_hidden";
+    const int npl = precision == ANERF_MLP_BF16X6 ? 3 : (precision == ANERF_MLP_BF16X3 ? 2 : 0);
+    if (width != FW_W || !npl)
+        return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_forward_hidden: width 256, ANERF_MLP_BF16X6 or _BF16X3");
+    if (m < 0 || !x || !w_split || !bias || !y) return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_forward_hidden: bad arguments");
+    // (float4 loads and stores of whole rows; a 64-row chunk's byte range fits a buffer descriptor; the stagers read
+    // a unit ahead of the stores, so y must not overlap x)
+    if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15 || (ldx | ldy) & 3 || ldx < width ||
+        ldy < width || ldx >= (1 << 22) || ldy >= (1 << 22))
+        return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_forward_hidden: x / y need 16 B aligned rows, ld % 4 == 0, "
+                                                 "256 <= ld < 2^22");
+    if (m > 0) {
+        const uintptr_t xb = reinterpret_cast<uintptr_t>(x), xe = xb + 4 * ((m - 1) * ldx + width);
+        const uintptr_t yb = reinterpret_cast<uintptr_t>(y), ye = yb + 4 * ((m - 1) * ldy + width);
+        if (xb < ye && yb < xe) return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_forward_hidden: y overlaps x");
+    }
+    if (m == 0) return ANERF_OK;
+    FWArgs g = {};
+    const int nwg = fw_plan(m, &g.rows_per_wg);
+    g.M = m;
+    g.x = x;
+    g.ldx = ldx;
+    g.w = static_cast<const unsigned short*>(w_split);
+    g.bias = bias;
+    g.y = y;
+    g.ldy = ldy;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const void* kern = npl == 3 ? (const void*)mlp_fwd_kernel<3> : (const void*)mlp_fwd_kernel<2>;
+    const int lb = npl == 3 ? FWGeo<3>::LDS : FWGeo<2>::LDS;
+    hipError_t e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, lb);
+    if (e != hipSuccess) return anerf_internal_fail(ANERF_EHIP, (std::string(fn) + ": " + hipGetErrorString(e)).c_str());
+    if (npl == 3)
+        hipLaunchKernelGGL(mlp_fwd_kernel<3>, dim3((unsigned)nwg), dim3(FW_THR), lb, st, g);
+    else
+        hipLaunchKernelGGL(mlp_fwd_kernel<2>, dim3((unsigned)nwg), dim3(FW_THR), lb, st, g);
+    e = hipGetLastError();
+    return e == hipSuccess ? ANERF_OK : anerf_internal_fail(ANERF_EHIP, (std::string(fn) + ": " + hipGetErrorString(e)).c_str());
 }
 
 size_t anerf_mlp_backward_head_workspace(int64_t m, int32_t width) {

@@ -54,6 +54,11 @@ FUSED_SKIP = True
 # (round 6, ABI 18, with FUSED_BACKWARD) the heads' backward (feature_linear + alpha_linear's rank-1 term) as one
 # fused pass, anerf_mlp_backward_head; an A/B switch for tools/train_bench.py
 FUSED_HEAD = True
+# (round 6, ABI 19) the forward of every 256 x 256 hidden layer (input one hidden layer's output) on the persistent
+# kernel anerf_mlp_forward_hidden instead of anerf_mlp_gemm: bit-identical outputs, another schedule (stager waves
+# stream the rows from HBM and the outputs back while the compute waves run the MFMAs); bf16x6 / bf16x3 only; an A/B
+# switch for tools/train_bench.py, never read from the environment
+FORWARD_PERSISTENT = True
 
 
 def _side_stream(dev):
@@ -132,6 +137,13 @@ def gemm(m, n, k, a, b_split, bias, relu, outs, dev, prec=6, rin=None, rout=None
                                                so, no, _lib.ptr(rin), _lib.ptr(rout), _stream(dev)), "anerf_mlp_gemm")
 
 
+def forward_hidden(m, x, w_split, prec, bias, y, dev):
+    """y = relu(x W^T + b) of a 256 x 256 hidden layer (anerf_mlp_forward_hidden); w_split from split_weight(W)."""
+    _lib.check(_lib.load().anerf_mlp_forward_hidden(m, 256, _lib.ptr(x), x.stride(0), _lib.ptr(w_split), prec,
+                                                    _lib.ptr(bias), _lib.ptr(y), y.stride(0), _stream(dev)),
+               "anerf_mlp_forward_hidden")
+
+
 def wgrad(m, n, k, dy, x, dw, db, ws, dev, prec=6):
     sx, nx = _segs(x)
     _lib.check(_lib.load().anerf_mlp_wgrad(m, n, k, _lib.ptr(dy), dy.stride(0), sx, nx, prec, _lib.ptr(dw),
@@ -200,8 +212,11 @@ class _MLP(torch.autograd.Function):
             else:
                 a, k = [_seg(H[-1], W)], W
             h = torch.empty(M, W, **f32)
-            gemm(M, W, k, a, sp[i], pb[i], True, [(h, W, W, 0, None, False)], dev, lp[i],
-                 rin=rm[i - 1] if lp[i] == ANERF_MLP_FP16X4 else None, rout=rm[i] if f16 else None)
+            if FORWARD_PERSISTENT and W == 256 and i >= 1 and i - 1 != skip and lp[i] in (3, 6):
+                forward_hidden(M, H[-1], sp[i], lp[i], pb[i], h, dev)
+            else:
+                gemm(M, W, k, a, sp[i], pb[i], True, [(h, W, W, 0, None, False)], dev, lp[i],
+                     rin=rm[i - 1] if lp[i] == ANERF_MLP_FP16X4 else None, rout=rm[i] if f16 else None)
             H.append(h)
         # feature_linear + alpha_linear as one GEMM (alpha in raw[:, 3]); no activation
         raw = torch.empty(M, 4, **f32)

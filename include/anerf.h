@@ -48,6 +48,7 @@
  *   anerf_mlp_wgrad         weight + bias gradients
  *   anerf_mlp_backward_hidden  both of a 256 x 256 hidden layer's backward products in one pass (round 6)
  *   anerf_mlp_backward_head    the same for feature_linear with alpha_linear's rank-1 term (round 6, ABI 18)
+ *   anerf_mlp_forward_hidden   a 256 x 256 hidden layer's forward, persistent (round 6, ABI 19)
  *   anerf_mlp_forward(_pack)  the whole forward in one kernel (opt-in alternative to the GEMMs)
  */
 #ifndef ANERF_H
@@ -60,7 +61,7 @@
 extern "C" {
 #endif
 
-#define ANERF_ABI_VERSION 18
+#define ANERF_ABI_VERSION 19
 
 enum {
     ANERF_OK = 0,
@@ -633,6 +634,16 @@ int anerf_mlp_backward_head(int64_t m, int32_t width, const float* dy, int64_t l
 /* dw [257][lddw], db [257] of an anerf_mlp_backward_head call made with dw = db = NULL (same m, width). */
 int anerf_mlp_backward_head_reduce(int64_t m, int32_t width, const void* workspace, size_t workspace_bytes, float* dw,
                                    int64_t lddw, float* db, void* stream);
+
+/* ABI 19: the forward of one hidden layer of width 256 (pts_linears[i], core/networks/nerf.py:133-139),
+ *   y[m][o] = relu(sum_i x[m][i] W[o][i] + b[o]),
+ * bit-identical to anerf_mlp_gemm(m, 256, 256, {x}, w_split, precision, b, relu 1, {y}) -- the same split, the same
+ * products in the same order -- on one persistent workgroup per CU whose stager waves stream x from HBM and the
+ * output tile back while its compute waves run the MFMAs (anerf_gemm.hip, mlp_fwd_kernel).  w_split:
+ * anerf_mlp_split_weights(W, 256, 256, ld, transpose 0, precision); precision ANERF_MLP_BF16X6 or _BF16X3.
+ * x, y: 16 B aligned rows, ld % 4 == 0, 256 <= ld < 2^22; y must not overlap x. */
+int anerf_mlp_forward_hidden(int64_t m, int32_t width, const float* x, int64_t ldx, const void* w_split,
+                             int32_t precision, const float* bias, float* y, int64_t ldy, void* stream);
 
 #ifdef __cplusplus
 }

@@ -350,6 +350,84 @@ def test_fused_forward_matches_layer_by_layer_gemms(D, W, fc, nj, M, monkeypatch
         close(a, b, f"saved tensor {i}")
 
 
+def _forward_hidden(m, x, w_split, prec, b, ldy=256):
+    y = torch.full((m, ldy), float("nan"), device=DEV)
+    mlp.forward_hidden(m, x, w_split, prec, b, y, torch.device(DEV))
+    return y
+
+
+@pytest.mark.parametrize("prec", [6, 3])
+@pytest.mark.parametrize("m", [163840, 131072, 5000, 777, 65, 64, 63, 1, 300001])
+def test_forward_hidden_is_bit_identical_to_the_gemm(m, prec):
+    """Round 6, ABI 19: the persistent hidden-layer forward (anerf_mlp_forward_hidden) computes relu(x W^T + b) with
+    anerf_mlp_gemm's split, products and order, so every output bit matches the GEMM's: ragged m (not a multiple of
+    the 64-row chunk, fewer rows than workgroups, more chunks per workgroup than the training step's), strided
+    input and output rows (the output's padding column is never written), inputs spanning 2^-60 .. 2^60 with zeros,
+    and the fp64 bound of the arithmetic as a second check."""
+    torch.manual_seed(m % 997 + prec)
+    x = torch.relu(torch.randn(m, 260, device=DEV))[:, :256]  # (ld 260; half the entries exactly 0)
+    if m > 10:
+        x[::7] *= 2.0 ** 60
+        x[3::11] *= 2.0 ** -60
+    w = torch.randn(256, 256, device=DEV) / 16
+    b = torch.randn(256, device=DEV)
+    ws = mlp.split_weight(w, False, prec)
+    y = _forward_hidden(m, x, ws, prec, b, ldy=260)
+    ref = torch.full((m, 260), float("nan"), device=DEV)
+    mlp.gemm(m, 256, 256, [mlp._seg(x, 256)], ws, b, True, [(ref, 260, 256, 0, None, False)], torch.device(DEV), prec)
+    assert torch.isnan(y[:, 256:]).all()
+    assert torch.equal(y[:, :256], ref[:, :256]), float((y[:, :256] - ref[:, :256]).abs().max())
+    full = torch.relu(x.double() @ w.double().t() + b.double())
+    bound = _bound(x, w, prec) + 1e-6 * b.double().abs()
+    assert torch.all((y[:, :256].double() - full).abs() <= bound)
+
+
+def test_forward_hidden_edge_cases_and_bad_arguments():
+    lib = mlp._lib.load()
+    dev = torch.device(DEV)
+    w = torch.randn(256, 256, device=DEV)
+    ws = mlp.split_weight(w, False, 6)
+    b = torch.zeros(256, device=DEV)
+    x = torch.randn(64, 256, device=DEV)
+    y = torch.empty(64, 256, device=DEV)
+    st = mlp._stream(dev)
+    P = mlp._lib.ptr
+    assert lib.anerf_mlp_forward_hidden(0, 256, P(x), 256, P(ws), 6, P(b), P(y), 256, st) == 0  # (empty: nothing)
+    bad = [dict(width=128), dict(prec=4), dict(ldx=255), dict(ldy=258), dict(xoff=1), dict(ldx=1 << 22),
+           dict(overlap=True), dict(bias=False)]
+    for case in bad:
+        xp = x.data_ptr() + 4 * case.get("xoff", 0)
+        yp = x.data_ptr() + 4 * 128 if case.get("overlap") else y.data_ptr()
+        rc = lib.anerf_mlp_forward_hidden(64, case.get("width", 256), xp, case.get("ldx", 256), P(ws),
+                                          case.get("prec", 6), P(b) if case.get("bias", True) else None, yp,
+                                          case.get("ldy", 256), st)
+        assert rc != 0, case
+
+
+@pytest.mark.parametrize("prec", ["bf16x6", "mixed", "bf16x3"])
+def test_network_forward_identical_with_the_persistent_hidden_layers(prec, monkeypatch):
+    """The training network's forward (raw and every saved activation) is bit-identical with the hidden layers on
+    anerf_mlp_forward_hidden and on anerf_mlp_gemm; so are the gradients (the backward reads the same tensors)."""
+    cfg = anerf.RenderConfig(n_joints=24, netdepth=8, netwidth=256).validate()
+    ck = syn.make_checkpoint(3, n_joints=24, D=8, W=256, fine=False)
+    torch.manual_seed(2)
+    feat = torch.rand(20000, cfg.feature_dim, device=DEV) * 2 - 1
+    out = {}
+    for pers in (True, False):
+        monkeypatch.setattr(mlp, "FORWARD_PERSISTENT", pers)
+        tr = train.TrainRayCaster(cfg, ck, mlp=prec).train()
+        f = feat.clone().requires_grad_(True)
+        raw = tr.network_fn(f, None)
+        saved = [t.detach().clone() for t in raw.grad_fn.saved_tensors]
+        raw.square().sum().backward()
+        grads = [f.grad.clone()] + [p.grad.clone() for p in tr.parameters() if p.grad is not None]
+        out[pers] = (raw.detach(), saved, grads)
+    (ra, sa, ga), (rb, sb, gb) = out[True], out[False]
+    assert torch.equal(ra, rb)
+    assert len(sa) == len(sb) and all(torch.equal(a, b) for a, b in zip(sa, sb))
+    assert len(ga) == len(gb) and all(torch.equal(a, b) for a, b in zip(ga, gb))
+
+
 def _backward_hidden(m, dy, x, w, lddx=None):
     """anerf_mlp_backward_hidden on dy [m][256] and x [m][256] (strided views allowed) with W [256][256]."""
     lib = mlp._lib.load()

@@ -54,6 +54,9 @@ def main():
     cases = {
         "forward": (lambda: mlp.gemm(M, W, K, [mlp._seg(xk, K)], wk_f, b, True, [(out, W, W, 0, None, False)], dev,
                                      a.prec), M * (K + W) * 4),
+        "forward_persistent": (lambda: mlp.forward_hidden(M, x, ws_f, a.prec, b, out, dev), 2 * M * W * 4),
+        "forward_256": (lambda: mlp.gemm(M, W, W, [mlp._seg(x, W)], ws_f, b, True, [(out, W, W, 0, None, False)], dev,
+                                         a.prec), 2 * M * W * 4),
         "input_grad": (lambda: mlp.gemm(M, W, W, [mlp._seg(x, W)], ws_t, None, False, [(out, W, W, 0, h, False)], dev,
                                         a.prec), 3 * M * W * 4),
         "weight_grad": (lambda: mlp.wgrad(M, W, W, x, [mlp._seg(h, W)], dw, db, wsp, dev, a.prec), 2 * M * W * 4),
@@ -63,7 +66,7 @@ def main():
     for name in a.cases.split(","):
         fn, by = cases[name]
         us = timeit(fn, a.reps)
-        k = K if name == "forward" else W
+        k = K if name == "forward" else W  # (forward_persistent, forward_256: K = 256)
         print(json.dumps({"case": name, "M": M, "N": W, "K": k, "prec": a.prec, "us": round(us, 1),
                           "GBps": round(by / us / 1e3, 1),
                           "TFLOPs_ref": round(2 * M * W * k / us / 1e6, 1)}), flush=True)

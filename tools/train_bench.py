@@ -66,6 +66,8 @@ def parser():
                     help="ablation: the fine pass on the caller's stream (its backward then follows the coarse one's)")
     ap.add_argument("--no-fused-head", action="store_true",
                     help="ablation: the heads' backward as two GEMMs")
+    ap.add_argument("--no-forward-persistent", action="store_true",
+                    help="ablation: the hidden layers' forward on anerf_mlp_gemm instead of anerf_mlp_forward_hidden")
     ap.add_argument("--split-single", action="store_true",
                     help="ablation: one split launch per weight instead of the batched split")
     ap.add_argument("--probe", default="", choices=["", "no-hidden-reduce", "no-wgrad", "no-wgrad-no-reduce"],
@@ -103,6 +105,7 @@ def measure(a, dev=None):
     importlib.import_module("a-nerf_amd.mlp").FUSED_BACKWARD = not getattr(a, "no_fused_backward", False)
     importlib.import_module("a-nerf_amd.mlp").FUSED_SKIP = not getattr(a, "no_fused_skip", False)
     importlib.import_module("a-nerf_amd.mlp").FUSED_HEAD = not getattr(a, "no_fused_head", False)
+    importlib.import_module("a-nerf_amd.mlp").FORWARD_PERSISTENT = not getattr(a, "no_forward_persistent", False)
     train.FINE_STREAM = not getattr(a, "no_fine_stream", False)
     tr = train.TrainRayCaster(cfg, ck, device=dev, mlp=a.mlp).train()
     tr.view_windows = not getattr(a, "full_view", False)
@@ -210,6 +213,8 @@ def measure(a, dev=None):
                             if importlib.import_module("a-nerf_amd.mlp").FUSED_BACKWARD and a.mlp in ("mixed", "bf16x3",
                                                                                                     "mixed16")
                             else "two GEMMs (anerf_mlp_gemm + anerf_mlp_wgrad)"),
+        "hidden_forward": ("persistent (anerf_mlp_forward_hidden)" if importlib.import_module("a-nerf_amd.mlp")
+                           .FORWARD_PERSISTENT and a.mlp in ("mixed", "bf16x6", "bf16x3") else "anerf_mlp_gemm"),
         "fine_stream": bool(train.FINE_STREAM),
         "joints": nj,
         "view_layout": (f"view windows (anerf.h ANERF_ENC_VIEW_WINDOWS: {nj} windows per sample + per-ray factors)"
