@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 #include <cstdlib>
 #include <string>
 
@@ -1366,30 +1367,38 @@ int dgw_plan(int64_t m, long long* rows_per_wg) {
     return (int)((chunks + per - 1) / per);
 }
 
-// ---------------------------------------------------------------- hidden layer forward, persistent (round 6)
-// y = relu(x W^T + b) of one 256 x 256 hidden layer (pts_linears[i], core/networks/nerf.py:133-139) with the
-// arithmetic of mlp_nt_kernel<NPL, 1> (x and W split into NPL bf16 planes, the same products in the same order
-// per k16 step, k16 steps ascending from a zero accumulator, + bias, relu): the outputs are bit-identical to
-// anerf_mlp_gemm's.  What changes is the schedule.  mlp_nt_kernel runs 128 x 128 tiles, two per CU, each staging its
-// A rows, looping eight k32 steps and storing through its epilogue in turn: in the training step a layer ran at
-// 2.3-2.5 TB/s of its 336 MB (M = 163,840) with every byte moved once, i.e. bound by the tiles' serial
-// prologue / k-loop / epilogue latency, not by bandwidth.  Here one persistent workgroup per CU walks a contiguous
-// row range in 64-row chunks, each as two units of 128 k columns, with the work split by role (as mlp_dgw_kernel):
-//   * stager waves (0-3): load a unit's x rows from HBM one unit ahead, split them into the LDS planes of the other
-//     stage, and copy the previous chunk's output tile from LDS to HBM in whole-row 16 B stores;
+// ---------------------------------------------------------------- layer forward, persistent (round 6)
+// y = act(x W^T + b) of one layer with 256 outputs -- the hidden layers (pts_linears[i], core/networks/nerf.py:133-139),
+// layer 0 and the skip layer on [x | h] (the concatenation as two operand segments, never built) and feature_linear
+// (no activation) with alpha_linear beside it (:141-145) -- with the arithmetic of mlp_nt_kernel<NPL, *> (x and W split
+// into NPL bf16 planes, the same products in the same order per k16 step, k16 steps ascending from a zero
+// accumulator, + bias, relu): the 256 outputs are bit-identical to anerf_mlp_gemm's.  What changes is the schedule.
+// mlp_nt_kernel runs 128 x 128 tiles, two per CU, each staging its A rows, looping its k steps and storing through
+// its epilogue in turn: in the training step a 256 x 256 layer ran at 2.3-2.5 TB/s of its 336 MB (M = 163,840) with
+// every byte moved once, i.e. bound by the tiles' serial prologue / k-loop / epilogue latency, not by bandwidth.
+// Here one persistent workgroup per CU walks a contiguous row range in 64-row chunks, each as ceil(K / 128) units of
+// 128 k columns, with the work split by role (as mlp_dgw_kernel):
+//   * stager waves (0-3): load a unit's x rows from HBM two units ahead, split them into the LDS planes of the other
+//     stage, and copy the previous chunk's output tile from LDS to HBM in whole-row 16 B stores (head: also
+//     alpha = x . w_alpha + b_alpha in fp32 from the rows they stage, written to its own column);
 //   * compute waves (4-7): output columns 64 (w - 4) .. + 63 of every chunk (2 x 2 blocks of 32 x 32), the split W
-//     fragments from L2 in a 4-deep ring that runs on across units and chunks, the A fragments from LDS; after a
-//     chunk's second unit, bias + relu into the LDS output tile.
+//     fragments from L2 in a 4-deep ring that runs on across units and chunks, the A fragments from LDS a k16 step
+//     ahead; after a chunk's last unit, bias (+ relu) into the LDS output tile.
 // So the compute waves issue no HBM access at all (their in-order vmcnt holds only L2 weight loads) and the HBM
 // reads, the splits and the stores overlap the MFMAs of the current unit.
 // LDS: two stages of NPL planes [64][128] bf16 (256 B rows, the 16 B chunks XOR-swizzled by row & 15: the staging
 // writes, 16 lanes x one row, and the fragment reads, 16 rows x one chunk, are conflict-free) + the fp32 output
 // tile [64][256] (64 KB): 160 KB at bf16x6, 128 KB at bf16x3.
-constexpr int FW_W = 256;     // layer width (inputs = outputs)
+constexpr int FW_W = 256;     // outputs
 constexpr int FW_CH = 64;     // rows per chunk
-constexpr int FW_KH = 128;    // k columns per unit (a chunk is two units)
+constexpr int FW_KH = 128;    // k columns per unit
 constexpr int FW_THR = 512;   // eight waves
 constexpr int FW_BD = 4;      // W fragment ring depth (k16 steps; divides a unit's 8)
+// (ANERF_FW_PROBE, timing diagnostics of experiment builds only, wrong results: 1 no MFMAs, 2 no W loads after the
+// ring's first, 3 no x loads after the first units, 4 no output stores)
+#ifndef ANERF_FW_PROBE
+#define ANERF_FW_PROBE 0
+#endif
 template <int NPL>
 struct FWGeo {
     static constexpr int PLANE = FW_CH * FW_KH * 2;  // 16 KB
@@ -1400,12 +1409,19 @@ struct FWGeo {
 
 struct FWArgs {
     long long M, rows_per_wg;
-    const float* x;
-    long long ldx;
+    const float* x0;  // operand segments: columns [0, c0) of x0 rows, then [c0, K) of x1 rows (or none)
+    const float* x1;
+    long long ld0, ld1;
+    int c0, K, nk, nu;        // k16 steps of W (ceil(K / 16)), units per chunk (ceil(K / 128) >= 2)
     const unsigned short* w;  // split W, NPL bf16 planes (anerf_mlp_split_weights, transpose = 0)
     const float* bias;
+    int relu;
     float* y;
     long long ldy;
+    const float* wa;  // head: alpha_linear's weight [K] and bias [1], alpha out (column 0 of rows with ld lda), or null
+    const float* ba;
+    float* alpha;
+    long long lda;
 };
 
 __device__ __forceinline__ int fw_off(int row, int chunk) { return row * 256 + ((chunk ^ (row & 15)) << 4); }
@@ -1420,7 +1436,16 @@ __global__ __launch_bounds__(FW_THR, 1) void mlp_fwd_kernel(FWArgs g) {
     const long long mlo = (long long)blockIdx.x * g.rows_per_wg;
     const long long mhi = mlo + g.rows_per_wg < M ? mlo + g.rows_per_wg : M;
     const int nch = mhi > mlo ? (int)((mhi - mlo + FW_CH - 1) / FW_CH) : 0;
-    const int nun = 2 * nch;  // units
+    const int nu = g.nu;
+    const int nun = nu * nch;  // units
+    // (kernel-argument fields as locals: a lambda referencing `g` makes clang copy the whole argument struct to
+    // scratch and reload the fields from there)
+    const float* const x0p = g.x0;
+    const float* const x1p = g.x1;
+    float* const yp = g.y;
+    const float* const wap = g.wa;
+    float* const alp = g.alpha;
+    const long long lda = g.lda;
     auto chunk_rows = [&](int s) {
         long long rows = mhi - (mlo + (long long)s * FW_CH);
         return (int)(rows < 0 ? 0 : (rows > FW_CH ? FW_CH : rows));
@@ -1430,23 +1455,72 @@ __global__ __launch_bounds__(FW_THR, 1) void mlp_fwd_kernel(FWArgs g) {
         // ------------------------------------------------------------------ stager waves
         // thread t < 256: columns c8 .. c8 + 7 of the unit (two float4 loads) in rows r16 + 16 p (p < 4)
         const int c8 = 8 * (tid & 15), r16 = tid >> 4;
-        const long long ldx = g.ldx, ldy = g.ldy;
-        const unsigned vox = (unsigned)((r16 * ldx + c8) * 4);
-        const int xstep = (int)(16 * ldx * 4);
-        f32x4 R[4][2];
-        auto fetch = [&](int u) {
-            const int s = u >> 1, kh = u & 1;
-            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                (void*)(g.x + (mlo + (long long)s * FW_CH) * ldx), 0, (int)(chunk_rows(s) * ldx * 4), 0x00020000);
+        const long long ld0 = g.ld0, ld1 = g.ld1, ldy = g.ldy;
+        const int c0 = g.c0, K = g.K;
+        const bool two = x1p != nullptr;
+        const unsigned vo0 = (unsigned)(r16 * ld0 * 4), vo1 = (unsigned)(r16 * ld1 * 4);
+        const int st0 = (int)(16 * ld0 * 4), st1 = (int)(16 * ld1 * 4);
+        // two register sets: unit v in set v & 1, loaded two units before it is staged (HBM latency under the
+        // whole chip's load exceeds a unit's MFMA time)
+        f32x4 RR[2][4][2];
+        auto fetch = [&](int u, f32x4 (&R)[4][2]) __attribute__((always_inline)) {
+            if (ANERF_FW_PROBE == 3 && u >= 2) return;
+            const int s = u / nu, kh = u - s * nu;
+            const long long r0 = mlo + (long long)s * FW_CH;
+            const int rows = chunk_rows(s);
+            const __amdgpu_buffer_rsrc_t rs0 =
+                __builtin_amdgcn_make_buffer_rsrc((void*)(x0p + r0 * ld0), 0, (int)(rows * ld0 * 4), 0x00020000);
+            // (columns outside a segment read zero through an offset past its range; a float4 never straddles
+            // segments: c0 % 4 == 0.  Row steps ride in the lane offset, which the range check covers, so the rows
+            // past the chunk read zero)
+            unsigned o0[2], o1[2];
+#pragma unroll
+            for (int f = 0; f < 2; ++f) {
+                const int c = FW_KH * kh + c8 + 4 * f;
+                o0[f] = c < c0 ? vo0 + (unsigned)c * 4u : NOOB;
+                o1[f] = c >= c0 && c < K ? vo1 + (unsigned)(c - c0) * 4u : NOOB;
+            }
 #pragma unroll
             for (int p = 0; p < 4; ++p)
 #pragma unroll
                 for (int f = 0; f < 2; ++f)
-                    R[p][f] = __builtin_bit_cast(
-                        f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vox, p * xstep + 4 * FW_KH * kh + 16 * f, 0));
+                    R[p][f] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs0, o0[f] + p * st0, 0, 0));
+            if (two) {
+                const __amdgpu_buffer_rsrc_t rs1 =
+                    __builtin_amdgcn_make_buffer_rsrc((void*)(x1p + r0 * ld1), 0, (int)(rows * ld1 * 4), 0x00020000);
+#pragma unroll
+                for (int p = 0; p < 4; ++p)
+#pragma unroll
+                    for (int f = 0; f < 2; ++f) {
+                        const f32x4 v = __builtin_bit_cast(
+                            f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs1, o1[f] + p * st1, 0, 0));
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {  // (one segment is live per lane, the other reads 0)
+                            const float a = R[p][f][e], b = v[e];
+                            R[p][f][e] = __builtin_bit_cast(float, __builtin_bit_cast(unsigned, a) |
+                                                                       __builtin_bit_cast(unsigned, b));
+                        }
+                    }
+            }
         };
-        auto stage = [&](int buf) {
+        // head: the thread's partial alpha sums of its four rows over the chunk's units
+        float asum[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        const bool head = alp != nullptr;
+        const float ba = head ? g.ba[0] : 0.0f;
+        auto stage = [&](int u, int buf, const f32x4 (&R)[4][2]) __attribute__((always_inline)) {
             unsigned char* const S = lds8 + buf * G::STAGE;
+            const int s = u / nu, kh = u - s * nu;
+            float wa[8];
+            if (head) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const int c = FW_KH * kh + c8 + e;
+                    wa[e] = c < K ? wap[c] : 0.0f;
+                }
+                if (kh == 0)
+#pragma unroll
+                    for (int p = 0; p < 4; ++p) asum[p] = 0.0f;
+            }
 #pragma unroll
             for (int p = 0; p < 4; ++p) {
                 float v[8];
@@ -1458,6 +1532,9 @@ __global__ __launch_bounds__(FW_THR, 1) void mlp_fwd_kernel(FWArgs g) {
                         const float t = R[p][f][e];
                         v[4 * f + e] = t;
                     }
+                if (head)
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) asum[p] = fmaf(wa[e], v[e], asum[p]);
                 const int off = fw_off(r16 + 16 * p, c8 >> 3);
                 // (mlp_nt_kernel's split: round to nearest even, the exact remainder split again)
 #pragma unroll
@@ -1475,45 +1552,76 @@ __global__ __launch_bounds__(FW_THR, 1) void mlp_fwd_kernel(FWArgs g) {
                     *reinterpret_cast<u32x4*>(S + pl * G::PLANE + off) = w;
                 }
             }
+            if (head && kh == nu - 1) {  // the chunk's alpha: the 16 lanes of a row, then one store per row
+                const long long r0 = mlo + (long long)s * FW_CH;
+                const int rows = chunk_rows(s);
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+                    float a = asum[p];
+                    a += __shfl_xor(a, 8, 16);
+                    a += __shfl_xor(a, 4, 16);
+                    a += __shfl_xor(a, 2, 16);
+                    a += __shfl_xor(a, 1, 16);
+                    const int row = r16 + 16 * p;
+                    if ((tid & 15) == 0 && row < rows) alp[(r0 + row) * lda] = a + ba;
+                }
+            }
         };
         // the output tile of chunk s: thread t, rows 4 q + (t >> 6), columns 4 (t & 63) .. + 3 (a wave
         // instruction stores one whole 1 KB row); the descriptor ends at the chunk's last row
-        auto copy_out = [&](int s) {
+        auto copy_out = [&](int s) __attribute__((always_inline)) {
+            if (ANERF_FW_PROBE == 4) return;
             const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
-                (void*)(g.y + (mlo + (long long)s * FW_CH) * ldy), 0, (int)(chunk_rows(s) * ldy * 4), 0x00020000);
+                (void*)(yp + (mlo + (long long)s * FW_CH) * ldy), 0, (int)(chunk_rows(s) * ldy * 4), 0x00020000);
             const int c4 = 4 * (tid & 63), rq = tid >> 6;
             const unsigned vo = (unsigned)((rq * ldy + c4) * 4);
 #pragma unroll
             for (int q = 0; q < FW_CH / 4; ++q) {
                 const f32x4 v = *reinterpret_cast<const f32x4*>(otile + (4 * q + rq) * FW_W + c4);
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rd, vo, (int)(4 * q * ldy * 4), 0);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rd, vo + (unsigned)(4 * q * ldy * 4), 0, 0);
             }
         };
-        if (nun > 0) {
-            fetch(0);
-            stage(0);
-            fetch(1);
+        if (nun > 0) {  // (nun >= 2)
+            fetch(0, RR[0]);
+            fetch(1, RR[1]);
+            stage(0, 0, RR[0]);
+            if (nun > 2) fetch(2, RR[0]);
         }
         __syncthreads();
-        for (int u = 0; u < nun; ++u) {
-            if (u >= 2 && !(u & 1)) copy_out((u >> 1) - 1);  // (written before the barrier that ended unit u - 1)
-            if (u + 1 < nun) stage((u + 1) & 1);              // (free since the barrier that ended unit u - 1)
-            if (u + 2 < nun) fetch(u + 2);
+        // unit u (parity P = u & 1, static): stage unit u + 1 from set 1 - P into the other LDS stage (free since the
+        // barrier that ended unit u - 1), then load unit u + 3 into that set.  The output tile of chunk s is written
+        // before the barrier ending its last unit and copied during the next chunk's first unit (nu >= 2: before the
+        // compute waves write it again)
+        auto body = [&](int u, auto P) __attribute__((always_inline)) {
+            constexpr int Q = 1 - decltype(P)::value;
+            if (u >= nu && u % nu == 0) copy_out(u / nu - 1);
+            if (u + 1 < nun) stage(u + 1, Q, RR[Q]);
+            if (u + 3 < nun) fetch(u + 3, RR[Q]);
             __syncthreads();
+        };
+        for (int u = 0; u < nun; u += 2) {
+            body(u, std::integral_constant<int, 0>{});
+            if (u + 1 < nun) body(u + 1, std::integral_constant<int, 1>{});
         }
         if (nch > 0) copy_out(nch - 1);
     } else {
         // ------------------------------------------------------------------ compute waves
         const int xw = wave - 4;  // output columns 64 xw .. 64 xw + 63: blocks 2 xw, 2 xw + 1
-        constexpr int WBS = (FW_W / 16) * NPL * 512;  // elements per 32-column block of the split W
+        const unsigned short* const wp = g.w;
+        const int nk = g.nk, ku = 8 * nu;   // W's k16 steps; k16 steps of a chunk's units
+        const int WBS = ((g.K + 15) / 16) * NPL * 512;  // elements per 32-column block of the split W
         const __amdgpu_buffer_rsrc_t rw =
-            __builtin_amdgcn_make_buffer_rsrc((void*)(g.w + (long long)(2 * xw) * WBS), 0, 2 * WBS * 2, 0x00020000);
+            __builtin_amdgcn_make_buffer_rsrc((void*)(wp + (long long)(2 * xw) * WBS), 0, 2 * WBS * 2, 0x00020000);
         const unsigned vwl = (unsigned)lane * 16;
         struct WF {
             u32x4 v[2][NPL];  // [block][plane]
         };
-        auto fetch_w = [&](int kt, WF& f) {
-            kt &= FW_W / 16 - 1;
+        // global k16 index q = 8 u + t: the chunk's step q % ku; steps past W's (the last unit's padding, whose
+        // A columns are zero) are neither loaded nor multiplied
+        auto fetch_w = [&](int q, WF& f) {
+            if (ANERF_FW_PROBE == 2 && q >= FW_BD) return;
+            int kt = q % ku;
+            kt = kt < nk ? kt : nk - 1;  // (a straight-line instruction stream: the padding steps reload the last)
 #pragma unroll
             for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -1522,6 +1630,7 @@ __global__ __launch_bounds__(FW_THR, 1) void mlp_fwd_kernel(FWArgs g) {
                         u32x4, __builtin_amdgcn_raw_buffer_load_b128(rw, vwl, (j * WBS + (kt * NPL + p) * 512) * 2, 0));
         };
         const float b0 = g.bias[64 * xw + (lane & 31)], b1 = g.bias[64 * xw + 32 + (lane & 31)];
+        const bool relu = g.relu != 0;
         WF wf[FW_BD];
 #pragma unroll
         for (int j = 0; j < FW_BD - 1; ++j) fetch_w(j, wf[j]);
@@ -1529,25 +1638,32 @@ __global__ __launch_bounds__(FW_THR, 1) void mlp_fwd_kernel(FWArgs g) {
         __syncthreads();
         for (int u = 0; u < nun; ++u) {
             const unsigned char* const S = lds8 + (u & 1) * G::STAGE;
-            const int kh = u & 1;
+            const int kh = u % nu;
             if (!kh) {
 #pragma unroll
                 for (int i = 0; i < 2; ++i)
 #pragma unroll
                     for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{0};
             }
-#pragma unroll
-            for (int t = 0; t < FW_KH / 16; ++t) {
-                __builtin_amdgcn_sched_barrier(0);
-                fetch_w(8 * kh + t + FW_BD - 1, wf[(t + FW_BD - 1) % FW_BD]);  // ((8 kh + t) % FW_BD = t % FW_BD)
-                __builtin_amdgcn_sched_barrier(0);
-                bf16x8 a[NPL][2];
+            // A fragments of k16 step t (rows 32 i + (lane & 31), k chunk 2 t + (lane >> 5)), read a step ahead
+            bf16x8 A[2][NPL][2];
+            auto read_a = [&](int t, bf16x8 (&a)[NPL][2]) {
 #pragma unroll
                 for (int p = 0; p < NPL; ++p)
 #pragma unroll
                     for (int i = 0; i < 2; ++i)
                         a[p][i] = *reinterpret_cast<const bf16x8*>(S + p * G::PLANE +
                                                                    fw_off(32 * i + (lane & 31), 2 * t + (lane >> 5)));
+            };
+            read_a(0, A[0]);
+#pragma unroll
+            for (int t = 0; t < FW_KH / 16; ++t) {
+                __builtin_amdgcn_sched_barrier(0);
+                fetch_w(8 * u + t + FW_BD - 1, wf[(t + FW_BD - 1) % FW_BD]);  // ((8 u + t) % FW_BD = t % FW_BD)
+                if (t + 1 < FW_KH / 16) read_a(t + 1, A[(t + 1) & 1]);
+                __builtin_amdgcn_sched_barrier(0);
+                if (8 * kh + t >= nk || ANERF_FW_PROBE == 1) continue;
+                const bf16x8 (&a)[NPL][2] = A[t & 1];
                 const WF& f = wf[t % FW_BD];
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
@@ -1568,8 +1684,8 @@ __global__ __launch_bounds__(FW_THR, 1) void mlp_fwd_kernel(FWArgs g) {
                     }
                 }
             }
-            if (kh) {  // the chunk's output: + bias, relu, into the tile (its previous copy left before the barrier
-                       // that ended unit u - 1)
+            if (kh == nu - 1) {  // the chunk's output: + bias (, relu), into the tile (its previous copy left before
+                                 // the barrier that ended unit u - 1)
 #pragma unroll
                 for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -1579,7 +1695,7 @@ __global__ __launch_bounds__(FW_THR, 1) void mlp_fwd_kernel(FWArgs g) {
                             const int row = 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
                             float v = acc[i][j][r];
                             v += j ? b1 : b0;
-                            v = fmaxf(v, 0.0f);
+                            if (relu) v = fmaxf(v, 0.0f);
                             otile[row * FW_W + 64 * xw + 32 * j + (lane & 31)] = v;
                         }
             }
@@ -1930,34 +2046,57 @@ int anerf_mlp_backward_hidden_reduce(int64_t m, int32_t width, const void* works
                       stream);
 }
 
-int anerf_mlp_forward_hidden(int64_t m, int32_t width, const float* x, int64_t ldx, const void* w_split,
-                             int32_t precision, const float* bias, float* y, int64_t ldy, void* stream) {
-    const char* fn = "anerf_mlp_forward_hidden";
+int anerf_mlp_forward_layer(int64_t m, int32_t k, const anerf_seg* a, int32_t n_a, const void* w_split,
+                            int32_t precision, const float* bias, int32_t relu, float* y, int64_t ldy,
+                            const float* w_alpha, const float* b_alpha, float* alpha, int64_t ld_alpha, void* stream) {
+    const char* fn = "anerf_mlp_forward_layer";
     const int npl = precision == ANERF_MLP_BF16X6 ? 3 : (precision == ANERF_MLP_BF16X3 ? 2 : 0);
-    if (width != FW_W || !npl)
-        return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_forward_hidden: width 256, ANERF_MLP_BF16X6 or _BF16X3");
-    if (m < 0 || !x || !w_split || !bias || !y) return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_forward_hidden: bad arguments");
+    if (!npl) return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_forward_layer: ANERF_MLP_BF16X6 or _BF16X3");
+    if (m < 0 || !a || n_a < 1 || n_a > 2 || !w_split || !bias || !y || k <= FW_KH || k % 4)
+        return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_forward_layer: bad arguments (1 or 2 segments, "
+                                                 "128 < k, k % 4 == 0)");
+    if (!w_alpha != !alpha || !w_alpha != !b_alpha || (alpha && ld_alpha < 1))
+        return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_forward_layer: w_alpha, b_alpha, alpha all or none");
     // (float4 loads and stores of whole rows; a 64-row chunk's byte range fits a buffer descriptor; the stagers read
-    // a unit ahead of the stores, so y must not overlap x)
-    if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15 || (ldx | ldy) & 3 || ldx < width ||
-        ldy < width || ldx >= (1 << 22) || ldy >= (1 << 22))
-        return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_forward_hidden: x / y need 16 B aligned rows, ld % 4 == 0, "
-                                                 "256 <= ld < 2^22");
-    if (m > 0) {
-        const uintptr_t xb = reinterpret_cast<uintptr_t>(x), xe = xb + 4 * ((m - 1) * ldx + width);
-        const uintptr_t yb = reinterpret_cast<uintptr_t>(y), ye = yb + 4 * ((m - 1) * ldy + width);
-        if (xb < ye && yb < xe) return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_forward_hidden: y overlaps x");
+    // units ahead of the stores, so y must not overlap an operand)
+    int cols = 0;
+    for (int i = 0; i < n_a; ++i) {
+        if (!a[i].p || a[i].cols < 4 || a[i].cols % 4 || a[i].ld < a[i].cols || a[i].ld % 4 || a[i].ld >= (1 << 22) ||
+            (reinterpret_cast<uintptr_t>(a[i].p) & 15))
+            return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_forward_layer: segments need 16 B aligned rows, "
+                                                     "cols % 4 == 0, cols <= ld < 2^22, ld % 4 == 0");
+        cols += a[i].cols;
     }
+    if (cols != k) return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_forward_layer: segments do not add up to k");
+    if ((reinterpret_cast<uintptr_t>(y) & 15) || (ldy & 3) || ldy < FW_W || ldy >= (1 << 22))
+        return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_forward_layer: y needs 16 B aligned rows, ld % 4 == 0, "
+                                                 "256 <= ld < 2^22");
     if (m == 0) return ANERF_OK;
+    const uintptr_t yb = reinterpret_cast<uintptr_t>(y), ye = yb + 4 * ((m - 1) * ldy + FW_W);
+    for (int i = 0; i < n_a; ++i) {
+        const uintptr_t xb = reinterpret_cast<uintptr_t>(a[i].p), xe = xb + 4 * ((m - 1) * a[i].ld + a[i].cols);
+        if (xb < ye && yb < xe) return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_forward_layer: y overlaps an operand");
+    }
     FWArgs g = {};
     const int nwg = fw_plan(m, &g.rows_per_wg);
     g.M = m;
-    g.x = x;
-    g.ldx = ldx;
+    g.x0 = a[0].p;
+    g.ld0 = a[0].ld;
+    g.c0 = a[0].cols;
+    g.x1 = n_a > 1 ? a[1].p : nullptr;
+    g.ld1 = n_a > 1 ? a[1].ld : 0;
+    g.K = k;
+    g.nk = (k + 15) / 16;
+    g.nu = (k + FW_KH - 1) / FW_KH;
     g.w = static_cast<const unsigned short*>(w_split);
     g.bias = bias;
+    g.relu = relu != 0;
     g.y = y;
     g.ldy = ldy;
+    g.wa = w_alpha;
+    g.ba = b_alpha;
+    g.alpha = alpha;
+    g.lda = ld_alpha;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const void* kern = npl == 3 ? (const void*)mlp_fwd_kernel<3> : (const void*)mlp_fwd_kernel<2>;
     const int lb = npl == 3 ? FWGeo<3>::LDS : FWGeo<2>::LDS;
@@ -1969,6 +2108,14 @@ int anerf_mlp_forward_hidden(int64_t m, int32_t width, const float* x, int64_t l
         hipLaunchKernelGGL(mlp_fwd_kernel<2>, dim3((unsigned)nwg), dim3(FW_THR), lb, st, g);
     e = hipGetLastError();
     return e == hipSuccess ? ANERF_OK : anerf_internal_fail(ANERF_EHIP, (std::string(fn) + ": " + hipGetErrorString(e)).c_str());
+}
+
+int anerf_mlp_forward_hidden(int64_t m, int32_t width, const float* x, int64_t ldx, const void* w_split,
+                             int32_t precision, const float* bias, float* y, int64_t ldy, void* stream) {
+    if (width != FW_W) return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_forward_hidden: width 256");
+    const anerf_seg seg = {x, ldx, FW_W};
+    return anerf_mlp_forward_layer(m, FW_W, &seg, 1, w_split, precision, bias, 1, y, ldy, nullptr, nullptr, nullptr, 0,
+                                   stream);
 }
 
 size_t anerf_mlp_backward_head_workspace(int64_t m, int32_t width) {

@@ -54,10 +54,12 @@ FUSED_SKIP = True
 # (round 6, ABI 18, with FUSED_BACKWARD) the heads' backward (feature_linear + alpha_linear's rank-1 term) as one
 # fused pass, anerf_mlp_backward_head; an A/B switch for tools/train_bench.py
 FUSED_HEAD = True
-# (round 6, ABI 19) the forward of every 256 x 256 hidden layer (input one hidden layer's output) on the persistent
-# kernel anerf_mlp_forward_hidden instead of anerf_mlp_gemm: bit-identical outputs, another schedule (stager waves
-# stream the rows from HBM and the outputs back while the compute waves run the MFMAs); bf16x6 / bf16x3 only; an A/B
-# switch for tools/train_bench.py, never read from the environment
+# (round 6, ABI 19) the forward of every trunk layer (layer 0 on the encoder features, the hidden layers, the skip
+# layer on [x | h]) and of feature_linear on the persistent kernel anerf_mlp_forward_layer instead of anerf_mlp_gemm:
+# bit-identical outputs (another schedule: stager waves stream the rows from HBM and the outputs back while the compute
+# waves run the MFMAs), alpha_linear beside feature_linear in fp32 (the GEMM computed it as a 257th output in the split
+# arithmetic: equal to fp32 rounding); bf16x6 / bf16x3 only; an A/B switch for tools/train_bench.py, never read from
+# the environment
 FORWARD_PERSISTENT = True
 
 
@@ -137,6 +139,18 @@ def gemm(m, n, k, a, b_split, bias, relu, outs, dev, prec=6, rin=None, rout=None
                                                so, no, _lib.ptr(rin), _lib.ptr(rout), _stream(dev)), "anerf_mlp_gemm")
 
 
+def forward_layer(m, k, a, w_split, prec, bias, relu, y, dev, alpha=None):
+    """y [m, 256] = act(a W^T + b) on the persistent kernel (anerf_mlp_forward_layer): a = 1 or 2 operand segments
+    adding up to k > 128 columns; alpha = (w_alpha [k], b_alpha [1], out tensor column view [m]) or None."""
+    sa, na = _segs(a)
+    wa, ba, out = alpha if alpha is not None else (None, None, None)
+    _lib.check(_lib.load().anerf_mlp_forward_layer(m, k, sa, na, _lib.ptr(w_split), prec, _lib.ptr(bias), int(relu),
+                                                   _lib.ptr(y), y.stride(0), _lib.ptr(wa), _lib.ptr(ba),
+                                                   None if out is None else ctypes.c_void_p(out.data_ptr()),
+                                                   0 if out is None else out.stride(0), _stream(dev)),
+               "anerf_mlp_forward_layer")
+
+
 def forward_hidden(m, x, w_split, prec, bias, y, dev):
     """y = relu(x W^T + b) of a 256 x 256 hidden layer (anerf_mlp_forward_hidden); w_split from split_weight(W)."""
     _lib.check(_lib.load().anerf_mlp_forward_hidden(m, 256, _lib.ptr(x), x.stride(0), _lib.ptr(w_split), prec,
@@ -212,8 +226,8 @@ class _MLP(torch.autograd.Function):
             else:
                 a, k = [_seg(H[-1], W)], W
             h = torch.empty(M, W, **f32)
-            if FORWARD_PERSISTENT and W == 256 and i >= 1 and i - 1 != skip and lp[i] in (3, 6):
-                forward_hidden(M, H[-1], sp[i], lp[i], pb[i], h, dev)
+            if FORWARD_PERSISTENT and W == 256 and k > 128 and lp[i] in (3, 6) and not f16:
+                forward_layer(M, k, a, sp[i], lp[i], pb[i], True, h, dev)
             else:
                 gemm(M, W, k, a, sp[i], pb[i], True, [(h, W, W, 0, None, False)], dev, lp[i],
                      rin=rm[i - 1] if lp[i] == ANERF_MLP_FP16X4 else None, rout=rm[i] if f16 else None)
@@ -221,10 +235,13 @@ class _MLP(torch.autograd.Function):
         # feature_linear + alpha_linear as one GEMM (alpha in raw[:, 3]); no activation
         raw = torch.empty(M, 4, **f32)
         hf = torch.empty(M, W, **f32)
-        bhead = torch.cat([bf, ba]).contiguous()
-        gemm(M, W + 1, W, [_seg(H[-1], W)], sp[D], bhead, False,
-             [(hf, W, W, 0, None, False), (raw, 4, 1, 3, None, False)], dev, hp,
-             rin=rm[D - 1] if hp == ANERF_MLP_FP16X4 else None)
+        if FORWARD_PERSISTENT and W == 256 and hp in (3, 6) and not f16:  # (the split rows of whead's first 256 = wf's)
+            forward_layer(M, W, [_seg(H[-1], W)], sp[D], hp, bf, False, hf, dev, alpha=(wa, ba, raw[:, 3]))
+        else:
+            bhead = torch.cat([bf, ba]).contiguous()
+            gemm(M, W + 1, W, [_seg(H[-1], W)], sp[D], bhead, False,
+                 [(hf, W, W, 0, None, False), (raw, 4, 1, 3, None, False)], dev, hp,
+                 rin=rm[D - 1] if hp == ANERF_MLP_FP16X4 else None)
         prec = op_  # (the view and rgb layers)
         # views_linears[0] on cat([feature, views(, framecode)]), relu; view windows: sum_j w_j G_j joins the
         # GEMM's pre-activation (accumulate mode 2: product + bias + sum, then the relu)

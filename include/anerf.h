@@ -49,6 +49,7 @@
  *   anerf_mlp_backward_hidden  both of a 256 x 256 hidden layer's backward products in one pass (round 6)
  *   anerf_mlp_backward_head    the same for feature_linear with alpha_linear's rank-1 term (round 6, ABI 18)
  *   anerf_mlp_forward_hidden   a 256 x 256 hidden layer's forward, persistent (round 6, ABI 19)
+ *   anerf_mlp_forward_layer    the same for any 256-output layer: layer 0, the skip layer, the heads (ABI 19)
  *   anerf_mlp_forward(_pack)  the whole forward in one kernel (opt-in alternative to the GEMMs)
  */
 #ifndef ANERF_H
@@ -644,6 +645,17 @@ int anerf_mlp_backward_head_reduce(int64_t m, int32_t width, const void* workspa
  * x, y: 16 B aligned rows, ld % 4 == 0, 256 <= ld < 2^22; y must not overlap x. */
 int anerf_mlp_forward_hidden(int64_t m, int32_t width, const float* x, int64_t ldx, const void* w_split,
                              int32_t precision, const float* bias, float* y, int64_t ldy, void* stream);
+/* ABI 19: the same persistent kernel for any layer with 256 outputs on k > 128 input columns (k % 4 == 0) given as
+ * one or two operand segments (layer 0 on the encoder features, the skip layer on [x | h]; each segment 16 B aligned,
+ * cols % 4 == 0, cols <= ld < 2^22, ld % 4 == 0):  y[m][o] = act(sum_i a[m][i] W[o][i] + b[o]), act = relu if
+ * relu != 0 -- bit-identical to anerf_mlp_gemm on the same segments.  With w_alpha [k], b_alpha [1] and alpha (all or
+ * none) the kernel also writes alpha[m * ld_alpha] = sum_i a[m][i] w_alpha[i] + b_alpha in fp32 from the rows it
+ * stages: feature_linear with alpha_linear beside it (core/networks/nerf.py:141-145; anerf_mlp_gemm computes the alpha
+ * column as a 257th output in the layer's split arithmetic instead, so alpha agrees to fp32 rounding, not bit for
+ * bit).  w_split: anerf_mlp_split_weights(W, 256, k, ld, 0, precision). */
+int anerf_mlp_forward_layer(int64_t m, int32_t k, const anerf_seg* a, int32_t n_a, const void* w_split,
+                            int32_t precision, const float* bias, int32_t relu, float* y, int64_t ldy,
+                            const float* w_alpha, const float* b_alpha, float* alpha, int64_t ld_alpha, void* stream);
 
 #ifdef __cplusplus
 }

@@ -404,10 +404,87 @@ def test_forward_hidden_edge_cases_and_bad_arguments():
         assert rc != 0, case
 
 
+@pytest.mark.parametrize("prec", [6, 3])
+@pytest.mark.parametrize("m", [163840, 4097, 65, 1])
+@pytest.mark.parametrize("shape", ["layer0", "skip", "k132"])
+def test_forward_layer_segments_are_bit_identical_to_the_gemm(m, prec, shape):
+    """anerf_mlp_forward_layer on the trunk's other inputs: layer 0 on the encoder rows' first 432 columns (ld 456),
+    the skip layer on [x (432 of ld 456) | h (256)] as two segments (a 128-column unit straddles them), and k = 132
+    (the last unit 4 columns wide): every output bit as anerf_mlp_gemm's on the same segments."""
+    torch.manual_seed(m % 991 + prec)
+    feat = torch.rand(m, 456, device=DEV) * 2 - 1
+    h = torch.relu(torch.randn(m, 256, device=DEV))
+    if shape == "layer0":
+        segs, k = [mlp._seg(feat, 432)], 432
+    elif shape == "skip":
+        segs, k = [mlp._seg(feat, 432), mlp._seg(h, 256)], 688
+    else:
+        segs, k = [mlp._seg(feat, 132)], 132
+    w = torch.randn(256, k, device=DEV) / 16
+    b = torch.randn(256, device=DEV)
+    ws = mlp.split_weight(w, False, prec)
+    y = torch.full((m, 260), float("nan"), device=DEV)
+    mlp.forward_layer(m, k, segs, ws, prec, b, True, y, torch.device(DEV))
+    ref = torch.full((m, 260), float("nan"), device=DEV)
+    mlp.gemm(m, 256, k, segs, ws, b, True, [(ref, 260, 256, 0, None, False)], torch.device(DEV), prec)
+    assert torch.isnan(y[:, 256:]).all()
+    assert torch.equal(y[:, :256], ref[:, :256]), float((y[:, :256] - ref[:, :256]).abs().max())
+
+
+@pytest.mark.parametrize("m", [163840, 777, 1])
+def test_forward_layer_head_with_alpha(m):
+    """feature_linear (no relu) with alpha_linear beside it: the 256 outputs bit-identical to the GEMM's, alpha (fp32
+    dot products of the staged rows) within fp32 accumulation error of fp64, written to its strided column only."""
+    torch.manual_seed(m % 101)
+    x = torch.relu(torch.randn(m, 256, device=DEV))
+    wf = torch.randn(256, 256, device=DEV) / 16
+    bf = torch.randn(256, device=DEV)
+    wa = torch.randn(1, 256, device=DEV) / 16
+    ba = torch.randn(1, device=DEV)
+    ws = mlp.split_weight(wf, False, 6)
+    hf = torch.empty(m, 256, device=DEV)
+    raw = torch.full((m, 4), float("nan"), device=DEV)
+    mlp.forward_layer(m, 256, [mlp._seg(x, 256)], ws, 6, bf, False, hf, torch.device(DEV), alpha=(wa, ba, raw[:, 3]))
+    ref = torch.empty(m, 256, device=DEV)
+    mlp.gemm(m, 256, 256, [mlp._seg(x, 256)], ws, bf, False, [(ref, 256, 256, 0, None, False)], torch.device(DEV), 6)
+    assert torch.equal(hf, ref)
+    assert (hf < 0).any()  # (no relu)
+    assert torch.isnan(raw[:, :3]).all()
+    full = x.double() @ wa.double().t()[:, 0] + ba.double()
+    bound = 4e-6 * (x.double().abs() @ wa.double().abs().t()[:, 0] + ba.double().abs()) + 1e-7
+    assert torch.all((raw[:, 3].double() - full).abs() <= bound), float((raw[:, 3].double() - full).abs().max())
+
+
+def test_forward_layer_rejects_bad_arguments():
+    lib = mlp._lib.load()
+    dev = torch.device(DEV)
+    x = torch.randn(64, 512, device=DEV)
+    y = torch.empty(64, 256, device=DEV)
+    b = torch.zeros(256, device=DEV)
+    ws = mlp.split_weight(torch.randn(256, 512, device=DEV), False, 6)
+    P = mlp._lib.ptr
+
+    def call(segs, k, prec=6, bias=b, alpha=None):
+        sa, na = mlp._segs(segs)
+        wa, ba, out = alpha if alpha else (None, None, None)
+        return lib.anerf_mlp_forward_layer(64, k, sa, na, P(ws), prec, P(bias), 1, P(y), 256, P(wa), P(ba), P(out), 4,
+                                           mlp._stream(dev))
+    assert call([mlp._seg(x, 256)], 256) == 0
+    assert call([mlp._seg(x, 128)], 128) != 0                        # (k <= 128)
+    assert call([mlp._seg(x, 130)], 130) != 0                        # (cols % 4)
+    assert call([mlp._seg(x, 128), mlp._seg(x, 128, 128), mlp._seg(x, 128, 256)], 384) != 0  # (3 segments)
+    assert call([mlp._seg(x, 256)], 260) != 0                        # (segments do not add up to k)
+    assert call([mlp._seg(x, 256)], 256, prec=4) != 0
+    assert call([mlp._seg(x, 256)], 256, bias=None) != 0
+    assert call([mlp._seg(x, 256)], 256, alpha=(b, None, y)) != 0    # (alpha: all or none)
+
+
 @pytest.mark.parametrize("prec", ["bf16x6", "mixed", "bf16x3"])
-def test_network_forward_identical_with_the_persistent_hidden_layers(prec, monkeypatch):
-    """The training network's forward (raw and every saved activation) is bit-identical with the hidden layers on
-    anerf_mlp_forward_hidden and on anerf_mlp_gemm; so are the gradients (the backward reads the same tensors)."""
+def test_network_forward_with_the_persistent_layers(prec, monkeypatch):
+    """The training network with every trunk layer and feature_linear on anerf_mlp_forward_layer against the same
+    network on anerf_mlp_gemm: the saved activations (h_i, feature, view hidden) and rgb bit-identical, alpha (fp32
+    beside the head instead of a 257th split-arithmetic output) to fp32 rounding, the gradients to what that
+    difference propagates."""
     cfg = anerf.RenderConfig(n_joints=24, netdepth=8, netwidth=256).validate()
     ck = syn.make_checkpoint(3, n_joints=24, D=8, W=256, fine=False)
     torch.manual_seed(2)
@@ -423,9 +500,13 @@ def test_network_forward_identical_with_the_persistent_hidden_layers(prec, monke
         grads = [f.grad.clone()] + [p.grad.clone() for p in tr.parameters() if p.grad is not None]
         out[pers] = (raw.detach(), saved, grads)
     (ra, sa, ga), (rb, sb, gb) = out[True], out[False]
-    assert torch.equal(ra, rb)
+    assert torch.equal(ra[:, :3], rb[:, :3])
+    tol = 4e-5 if prec == "bf16x3" else 2e-6  # (the GEMM's alpha column carries its mode's split error)
+    assert float((ra[:, 3] - rb[:, 3]).abs().max()) <= tol * float(rb[:, 3].abs().max()) + 1e-7
     assert len(sa) == len(sb) and all(torch.equal(a, b) for a, b in zip(sa, sb))
-    assert len(ga) == len(gb) and all(torch.equal(a, b) for a, b in zip(ga, gb))
+    assert len(ga) == len(gb)
+    for a, b in zip(ga, gb):
+        assert float((a - b).abs().max()) <= 10 * tol * float(b.abs().max()) + 1e-9
 
 
 def _backward_hidden(m, dy, x, w, lddx=None):
