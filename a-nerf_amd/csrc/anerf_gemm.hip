@@ -1395,9 +1395,22 @@ constexpr int FW_KH = 128;    // k columns per unit
 constexpr int FW_THR = 512;   // eight waves
 constexpr int FW_BD = 4;      // W fragment ring depth (k16 steps; divides a unit's 8)
 // (ANERF_FW_PROBE, timing diagnostics of experiment builds only, wrong results: 1 no MFMAs, 2 no W loads after the
-// ring's first, 3 no x loads after the first units, 4 no output stores)
+// ring's first, 3 no x loads after the first units, 4 no output stores, 5 = 3 + 4, 6 = 2 + 3 + 4)
 #ifndef ANERF_FW_PROBE
 #define ANERF_FW_PROBE 0
+#endif
+// (experiment switch) 1: the compute waves store their outputs straight from the accumulators (no LDS tile, the
+// storer waves idle)
+// (experiment switch) 1: the MFMAs of a k16 step interleaved over the four accumulators
+#ifndef ANERF_FW_IL
+#define ANERF_FW_IL 0
+#endif
+// (experiment switch) s_setprio of the compute waves (0: none)
+#ifndef ANERF_FW_PRIO
+#define ANERF_FW_PRIO 0
+#endif
+#ifndef ANERF_FW_DIRECT
+#define ANERF_FW_DIRECT 0
 #endif
 template <int NPL>
 struct FWGeo {
@@ -1426,7 +1439,7 @@ struct FWArgs {
 
 __device__ __forceinline__ int fw_off(int row, int chunk) { return row * 256 + ((chunk ^ (row & 15)) << 4); }
 
-template <int NPL>
+template <int NPL, int NSEG, bool HEAD>
 __global__ __launch_bounds__(FW_THR, 1) void mlp_fwd_kernel(FWArgs g) {
     using G = FWGeo<NPL>;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds8[];
@@ -1446,25 +1459,28 @@ __global__ __launch_bounds__(FW_THR, 1) void mlp_fwd_kernel(FWArgs g) {
     const float* const wap = g.wa;
     float* const alp = g.alpha;
     const long long lda = g.lda;
-    auto chunk_rows = [&](int s) {
+    auto chunk_rows = [&](int s) {  // (0 past the last chunk)
         long long rows = mhi - (mlo + (long long)s * FW_CH);
         return (int)(rows < 0 ? 0 : (rows > FW_CH ? FW_CH : rows));
     };
 
-    if (wave < 4) {
-        // ------------------------------------------------------------------ stager waves
-        // thread t < 256: columns c8 .. c8 + 7 of the unit (two float4 loads) in rows r16 + 16 p (p < 4)
-        const int c8 = 8 * (tid & 15), r16 = tid >> 4;
-        const long long ld0 = g.ld0, ld1 = g.ld1, ldy = g.ldy;
+    if (wave < 2) {
+        // ------------------------------------------------------------------ loader waves
+        // thread t < 128: columns c8 .. c8 + 7 of the unit (two float4 loads) in rows r8 + 8 p (p < 8).  Their vmcnt
+        // holds only these loads, issued unconditionally (past the last unit through a zero-range descriptor, which
+        // reads 0 and moves nothing), so every wait the compiler places is exact: a unit's loads land while two units
+        // of MFMAs run
+        const int c8 = 8 * (tid & 15), r8 = tid >> 4;
+        const long long ld0 = g.ld0, ld1 = g.ld1;
         const int c0 = g.c0, K = g.K;
-        const bool two = x1p != nullptr;
-        const unsigned vo0 = (unsigned)(r16 * ld0 * 4), vo1 = (unsigned)(r16 * ld1 * 4);
-        const int st0 = (int)(16 * ld0 * 4), st1 = (int)(16 * ld1 * 4);
-        // two register sets: unit v in set v & 1, loaded two units before it is staged (HBM latency under the
-        // whole chip's load exceeds a unit's MFMA time)
-        f32x4 RR[2][4][2];
-        auto fetch = [&](int u, f32x4 (&R)[4][2]) __attribute__((always_inline)) {
-            if (ANERF_FW_PROBE == 3 && u >= 2) return;
+        const unsigned vo0 = (unsigned)(r8 * ld0 * 4), vo1 = (unsigned)(r8 * ld1 * 4);
+        const unsigned st0 = (unsigned)(8 * ld0 * 4), st1 = (unsigned)(8 * ld1 * 4);
+        // two register sets (unit v in set v & 1, loaded two units before it is staged); one with two segments (the
+        // second segment's loads need their own registers until merged: one unit ahead)
+        constexpr int NS = NSEG == 2 ? 1 : 2;
+        f32x4 RR[NS][8][2];
+        auto fetch = [&](int u, f32x4 (&R)[8][2]) __attribute__((always_inline)) {
+            if ((ANERF_FW_PROBE == 3 || ANERF_FW_PROBE >= 5) && u >= 2) return;
             const int s = u / nu, kh = u - s * nu;
             const long long r0 = mlo + (long long)s * FW_CH;
             const int rows = chunk_rows(s);
@@ -1481,15 +1497,15 @@ __global__ __launch_bounds__(FW_THR, 1) void mlp_fwd_kernel(FWArgs g) {
                 o1[f] = c >= c0 && c < K ? vo1 + (unsigned)(c - c0) * 4u : NOOB;
             }
 #pragma unroll
-            for (int p = 0; p < 4; ++p)
+            for (int p = 0; p < 8; ++p)
 #pragma unroll
                 for (int f = 0; f < 2; ++f)
                     R[p][f] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs0, o0[f] + p * st0, 0, 0));
-            if (two) {
+            if constexpr (NSEG == 2) {
                 const __amdgpu_buffer_rsrc_t rs1 =
                     __builtin_amdgcn_make_buffer_rsrc((void*)(x1p + r0 * ld1), 0, (int)(rows * ld1 * 4), 0x00020000);
 #pragma unroll
-                for (int p = 0; p < 4; ++p)
+                for (int p = 0; p < 8; ++p)
 #pragma unroll
                     for (int f = 0; f < 2; ++f) {
                         const f32x4 v = __builtin_bit_cast(
@@ -1503,26 +1519,24 @@ __global__ __launch_bounds__(FW_THR, 1) void mlp_fwd_kernel(FWArgs g) {
                     }
             }
         };
-        // head: the thread's partial alpha sums of its four rows over the chunk's units
-        float asum[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-        const bool head = alp != nullptr;
-        const float ba = head ? g.ba[0] : 0.0f;
-        auto stage = [&](int u, int buf, const f32x4 (&R)[4][2]) __attribute__((always_inline)) {
+        // HEAD (k = 256: two units): alpha_linear's weights at the thread's columns of either unit, loaded once; the
+        // partial sums of its eight rows over the chunk's units
+        float wa0[8], wa1[8], asum[8];
+        float ba = 0.0f;
+        if constexpr (HEAD) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                wa0[e] = wap[c8 + e];
+                wa1[e] = wap[FW_KH + c8 + e];
+                asum[e] = 0.0f;
+            }
+            ba = g.ba[0];
+        }
+        auto stage = [&](int u, int buf, const f32x4 (&R)[8][2]) __attribute__((always_inline)) {
             unsigned char* const S = lds8 + buf * G::STAGE;
             const int s = u / nu, kh = u - s * nu;
-            float wa[8];
-            if (head) {
 #pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const int c = FW_KH * kh + c8 + e;
-                    wa[e] = c < K ? wap[c] : 0.0f;
-                }
-                if (kh == 0)
-#pragma unroll
-                    for (int p = 0; p < 4; ++p) asum[p] = 0.0f;
-            }
-#pragma unroll
-            for (int p = 0; p < 4; ++p) {
+            for (int p = 0; p < 8; ++p) {
                 float v[8];
 #pragma unroll
                 for (int f = 0; f < 2; ++f)
@@ -1532,10 +1546,13 @@ __global__ __launch_bounds__(FW_THR, 1) void mlp_fwd_kernel(FWArgs g) {
                         const float t = R[p][f][e];
                         v[4 * f + e] = t;
                     }
-                if (head)
+                if constexpr (HEAD) {
+                    float a = kh ? asum[p] : 0.0f;
 #pragma unroll
-                    for (int e = 0; e < 8; ++e) asum[p] = fmaf(wa[e], v[e], asum[p]);
-                const int off = fw_off(r16 + 16 * p, c8 >> 3);
+                    for (int e = 0; e < 8; ++e) a = fmaf(kh ? wa1[e] : wa0[e], v[e], a);
+                    asum[p] = a;
+                }
+                const int off = fw_off(r8 + 8 * p, c8 >> 3);
                 // (mlp_nt_kernel's split: round to nearest even, the exact remainder split again)
 #pragma unroll
                 for (int pl = 0; pl < NPL; ++pl) {
@@ -1552,62 +1569,80 @@ __global__ __launch_bounds__(FW_THR, 1) void mlp_fwd_kernel(FWArgs g) {
                     *reinterpret_cast<u32x4*>(S + pl * G::PLANE + off) = w;
                 }
             }
-            if (head && kh == nu - 1) {  // the chunk's alpha: the 16 lanes of a row, then one store per row
-                const long long r0 = mlo + (long long)s * FW_CH;
-                const int rows = chunk_rows(s);
+            if constexpr (HEAD) {
+                if (kh == nu - 1) {  // the chunk's alpha: the 16 lanes of a row, then one store per row
+                    const long long r0 = mlo + (long long)s * FW_CH;
+                    const int rows = chunk_rows(s);
 #pragma unroll
-                for (int p = 0; p < 4; ++p) {
-                    float a = asum[p];
-                    a += __shfl_xor(a, 8, 16);
-                    a += __shfl_xor(a, 4, 16);
-                    a += __shfl_xor(a, 2, 16);
-                    a += __shfl_xor(a, 1, 16);
-                    const int row = r16 + 16 * p;
-                    if ((tid & 15) == 0 && row < rows) alp[(r0 + row) * lda] = a + ba;
+                    for (int p = 0; p < 8; ++p) {
+                        float a = asum[p];
+                        a += __shfl_xor(a, 8, 16);
+                        a += __shfl_xor(a, 4, 16);
+                        a += __shfl_xor(a, 2, 16);
+                        a += __shfl_xor(a, 1, 16);
+                        const int row = r8 + 8 * p;
+                        if ((tid & 15) == 0 && row < rows) alp[(r0 + row) * lda] = a + ba;
+                    }
                 }
             }
         };
-        // the output tile of chunk s: thread t, rows 4 q + (t >> 6), columns 4 (t & 63) .. + 3 (a wave
-        // instruction stores one whole 1 KB row); the descriptor ends at the chunk's last row
-        auto copy_out = [&](int s) __attribute__((always_inline)) {
-            if (ANERF_FW_PROBE == 4) return;
-            const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
-                (void*)(yp + (mlo + (long long)s * FW_CH) * ldy), 0, (int)(chunk_rows(s) * ldy * 4), 0x00020000);
-            const int c4 = 4 * (tid & 63), rq = tid >> 6;
-            const unsigned vo = (unsigned)((rq * ldy + c4) * 4);
-#pragma unroll
-            for (int q = 0; q < FW_CH / 4; ++q) {
-                const f32x4 v = *reinterpret_cast<const f32x4*>(otile + (4 * q + rq) * FW_W + c4);
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rd, vo + (unsigned)(4 * q * ldy * 4), 0, 0);
-            }
-        };
-        if (nun > 0) {  // (nun >= 2)
-            fetch(0, RR[0]);
-            fetch(1, RR[1]);
-            stage(0, 0, RR[0]);
-            if (nun > 2) fetch(2, RR[0]);
-        }
+        fetch(0, RR[0]);
+        if constexpr (NS == 2) fetch(1, RR[NS - 1]);
+        if (nun > 0) stage(0, 0, RR[0]);
+        fetch(NS, RR[0]);
         __syncthreads();
-        // unit u (parity P = u & 1, static): stage unit u + 1 from set 1 - P into the other LDS stage (free since the
-        // barrier that ended unit u - 1), then load unit u + 3 into that set.  The output tile of chunk s is written
-        // before the barrier ending its last unit and copied during the next chunk's first unit (nu >= 2: before the
-        // compute waves write it again)
+        // unit u (parity P = u & 1, static): stage unit u + 1 from its set into the other LDS stage (free since the
+        // barrier that ended unit u - 1), then load unit u + 1 + NS into that set
         auto body = [&](int u, auto P) __attribute__((always_inline)) {
             constexpr int Q = 1 - decltype(P)::value;
-            if (u >= nu && u % nu == 0) copy_out(u / nu - 1);
-            if (u + 1 < nun) stage(u + 1, Q, RR[Q]);
-            if (u + 3 < nun) fetch(u + 3, RR[Q]);
+            constexpr int SET = NS == 2 ? Q : 0;
+            if (u + 1 < nun) stage(u + 1, Q, RR[SET]);
+            fetch(u + 1 + NS, RR[SET]);
             __syncthreads();
         };
         for (int u = 0; u < nun; u += 2) {
             body(u, std::integral_constant<int, 0>{});
             if (u + 1 < nun) body(u + 1, std::integral_constant<int, 1>{});
         }
+    } else if (wave < 4) {
+        // ------------------------------------------------------------------ storer waves
+        // the output tile of chunk s (written by the compute waves before the barrier ending its last unit) during
+        // the next chunk's first unit (nu >= 2: before they write it again): thread t < 128 of the role, rows 2 q +
+        // (t >> 6), columns 4 (t & 63) .. + 3 (a wave instruction stores one whole 1 KB row).  Stores only, never
+        // waited on
+        const int t = tid - 128;
+        const long long ldy = g.ldy;
+        auto copy_out = [&](int s) __attribute__((always_inline)) {
+            if (ANERF_FW_PROBE == 4 || ANERF_FW_PROBE >= 5 || ANERF_FW_DIRECT) return;
+            const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(yp + (mlo + (long long)s * FW_CH) * ldy), 0, (int)(chunk_rows(s) * ldy * 4), 0x00020000);
+            const int c4 = 4 * (t & 63), rq = t >> 6;
+            const unsigned vo = (unsigned)((rq * ldy + c4) * 4);
+#pragma unroll
+            for (int q = 0; q < FW_CH / 2; ++q) {
+                const f32x4 v = *reinterpret_cast<const f32x4*>(otile + (2 * q + rq) * FW_W + c4);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rd, vo + (unsigned)(2 * q * ldy * 4),
+                                                       0, 0);
+            }
+        };
+        __syncthreads();
+        for (int u = 0; u < nun; ++u) {
+            if (u >= nu && u % nu == 0) copy_out(u / nu - 1);
+            __syncthreads();
+        }
         if (nch > 0) copy_out(nch - 1);
     } else {
         // ------------------------------------------------------------------ compute waves
         const int xw = wave - 4;  // output columns 64 xw .. 64 xw + 63: blocks 2 xw, 2 xw + 1
+#if ANERF_FW_PRIO
+        // (experiment) the compute waves' instruction issue ahead of the loader / storer waves' on the same SIMD
+        __builtin_amdgcn_s_setprio(ANERF_FW_PRIO);
+#endif
         const unsigned short* const wp = g.w;
+#if ANERF_FW_DIRECT
+        float* const ypc = yp;
+        const long long ldyc = g.ldy;
+#endif
         const int nk = g.nk, ku = 8 * nu;   // W's k16 steps; k16 steps of a chunk's units
         const int WBS = ((g.K + 15) / 16) * NPL * 512;  // elements per 32-column block of the split W
         const __amdgpu_buffer_rsrc_t rw =
@@ -1619,7 +1654,7 @@ __global__ __launch_bounds__(FW_THR, 1) void mlp_fwd_kernel(FWArgs g) {
         // global k16 index q = 8 u + t: the chunk's step q % ku; steps past W's (the last unit's padding, whose
         // A columns are zero) are neither loaded nor multiplied
         auto fetch_w = [&](int q, WF& f) {
-            if (ANERF_FW_PROBE == 2 && q >= FW_BD) return;
+            if ((ANERF_FW_PROBE == 2 || ANERF_FW_PROBE == 6) && q >= FW_BD) return;
             int kt = q % ku;
             kt = kt < nk ? kt : nk - 1;  // (a straight-line instruction stream: the padding steps reload the last)
 #pragma unroll
@@ -1665,6 +1700,20 @@ __global__ __launch_bounds__(FW_THR, 1) void mlp_fwd_kernel(FWArgs g) {
                 if (8 * kh + t >= nk || ANERF_FW_PROBE == 1) continue;
                 const bf16x8 (&a)[NPL][2] = A[t & 1];
                 const WF& f = wf[t % FW_BD];
+#if ANERF_FW_IL
+                // (experiment) the four accumulators' chains interleaved product by product (each accumulator's own
+                // product order unchanged: the same bits)
+                constexpr int NPR = NPL == 3 ? 6 : 3;
+                constexpr int PA[6] = {NPL == 3 ? 2 : 1, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};
+                constexpr int O = NPL == 3 ? 0 : 3;
+#pragma unroll
+                for (int q = 0; q < NPR; ++q)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+#pragma unroll
+                        for (int i = 0; i < 2; ++i)
+                            acc[i][j] = mfma(a[PA[O + q]][i], __builtin_bit_cast(bf16x8, f.v[j][PB[O + q]]), acc[i][j]);
+#else
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
                     bf16x8 b[NPL];
@@ -1683,9 +1732,17 @@ __global__ __launch_bounds__(FW_THR, 1) void mlp_fwd_kernel(FWArgs g) {
                         acc[i][j] = mfma(a[0][i], b[0], c);
                     }
                 }
+#endif
             }
             if (kh == nu - 1) {  // the chunk's output: + bias (, relu), into the tile (its previous copy left before
                                  // the barrier that ended unit u - 1)
+#if ANERF_FW_DIRECT
+                // (experiment) straight from the accumulators to HBM: a wave instruction writes two 128 B row pieces;
+                // the descriptor ends at the chunk's last row
+                const int s = u / nu;
+                const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+                    (void*)(ypc + (mlo + (long long)s * FW_CH) * ldyc), 0, (int)(chunk_rows(s) * ldyc * 4), 0x00020000);
+#endif
 #pragma unroll
                 for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -1696,7 +1753,13 @@ __global__ __launch_bounds__(FW_THR, 1) void mlp_fwd_kernel(FWArgs g) {
                             float v = acc[i][j][r];
                             v += j ? b1 : b0;
                             if (relu) v = fmaxf(v, 0.0f);
+#if ANERF_FW_DIRECT
+                            __builtin_amdgcn_raw_buffer_store_b32(
+                                __builtin_bit_cast(unsigned, v), rd,
+                                (unsigned)((row * ldyc + 64 * xw + 32 * j + (lane & 31)) * 4), 0, 0);
+#else
                             otile[row * FW_W + 64 * xw + 32 * j + (lane & 31)] = v;
+#endif
                         }
             }
             __syncthreads();
@@ -2098,14 +2161,25 @@ int anerf_mlp_forward_layer(int64_t m, int32_t k, const anerf_seg* a, int32_t n_
     g.alpha = alpha;
     g.lda = ld_alpha;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    const void* kern = npl == 3 ? (const void*)mlp_fwd_kernel<3> : (const void*)mlp_fwd_kernel<2>;
+    const bool head = alpha != nullptr;
+    if (head && (n_a != 1 || k != FW_W))
+        return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_forward_layer: alpha with one segment of k = 256 only");
     const int lb = npl == 3 ? FWGeo<3>::LDS : FWGeo<2>::LDS;
-    hipError_t e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, lb);
-    if (e != hipSuccess) return anerf_internal_fail(ANERF_EHIP, (std::string(fn) + ": " + hipGetErrorString(e)).c_str());
-    if (npl == 3)
-        hipLaunchKernelGGL(mlp_fwd_kernel<3>, dim3((unsigned)nwg), dim3(FW_THR), lb, st, g);
-    else
-        hipLaunchKernelGGL(mlp_fwd_kernel<2>, dim3((unsigned)nwg), dim3(FW_THR), lb, st, g);
+    hipError_t e = hipSuccess;
+#define ANERF_FW_LAUNCH(P, S, H)                                                                                   \
+    if (npl == P && n_a == S && head == H) {                                                                       \
+        e = hipFuncSetAttribute((const void*)mlp_fwd_kernel<P, S, H>, hipFuncAttributeMaxDynamicSharedMemorySize, lb); \
+        if (e != hipSuccess)                                                                                       \
+            return anerf_internal_fail(ANERF_EHIP, (std::string(fn) + ": " + hipGetErrorString(e)).c_str());      \
+        hipLaunchKernelGGL((mlp_fwd_kernel<P, S, H>), dim3((unsigned)nwg), dim3(FW_THR), lb, st, g);             \
+    }
+    ANERF_FW_LAUNCH(3, 1, false)
+    ANERF_FW_LAUNCH(3, 2, false)
+    ANERF_FW_LAUNCH(3, 1, true)
+    ANERF_FW_LAUNCH(2, 1, false)
+    ANERF_FW_LAUNCH(2, 2, false)
+    ANERF_FW_LAUNCH(2, 1, true)
+#undef ANERF_FW_LAUNCH
     e = hipGetLastError();
     return e == hipSuccess ? ANERF_OK : anerf_internal_fail(ANERF_EHIP, (std::string(fn) + ": " + hipGetErrorString(e)).c_str());
 }
