@@ -1395,12 +1395,17 @@ constexpr int FW_KH = 128;    // k columns per unit
 constexpr int FW_THR = 512;   // eight waves
 constexpr int FW_BD = 4;      // W fragment ring depth (k16 steps; divides a unit's 8)
 // (ANERF_FW_PROBE, timing diagnostics of experiment builds only, wrong results: 1 no MFMAs, 2 no W loads after the
-// ring's first, 3 no x loads after the first units, 4 no output stores, 5 = 3 + 4, 6 = 2 + 3 + 4)
+// ring's first, 3 no x loads after the first units, 4 no output stores, 5 = 3 + 4, 6 = 2 + 3 + 4, 7 = 6 + no staging
+// after the first units, 8 = 6 + no A fragment reads after the first units, 9 = 6 + no epilogue, 10 = 6 + no barriers
+// in the unit loop)
 #ifndef ANERF_FW_PROBE
 #define ANERF_FW_PROBE 0
 #endif
 // (experiment switch) 1: the compute waves store their outputs straight from the accumulators (no LDS tile, the
 // storer waves idle)
+#ifndef ANERF_FW_MAP
+#define ANERF_FW_MAP 0
+#endif
 // (experiment switch) 1: the MFMAs of a k16 step interleaved over the four accumulators
 #ifndef ANERF_FW_IL
 #define ANERF_FW_IL 0
@@ -1444,7 +1449,10 @@ __global__ __launch_bounds__(FW_THR, 1) void mlp_fwd_kernel(FWArgs g) {
     using G = FWGeo<NPL>;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds8[];
     float* const otile = reinterpret_cast<float*>(lds8 + 2 * G::STAGE);  // [64][256]
-    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // (ANERF_FW_MAP 1, experiment: the roles on the odd (compute) and even hardware waves instead of 4-7 / 0-3)
+    const int hw = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    const int wave = ANERF_FW_MAP ? ((hw & 1) ? 4 + (hw >> 1) : (hw >> 1)) : hw;
+    const int lane = (int)threadIdx.x & 63, tid = wave * 64 + lane;
     const long long M = g.M;
     const long long mlo = (long long)blockIdx.x * g.rows_per_wg;
     const long long mhi = mlo + g.rows_per_wg < M ? mlo + g.rows_per_wg : M;
@@ -1533,6 +1541,7 @@ __global__ __launch_bounds__(FW_THR, 1) void mlp_fwd_kernel(FWArgs g) {
             ba = g.ba[0];
         }
         auto stage = [&](int u, int buf, const f32x4 (&R)[8][2]) __attribute__((always_inline)) {
+            if (ANERF_FW_PROBE == 7 && u >= 2) return;
             unsigned char* const S = lds8 + buf * G::STAGE;
             const int s = u / nu, kh = u - s * nu;
 #pragma unroll
@@ -1598,7 +1607,7 @@ __global__ __launch_bounds__(FW_THR, 1) void mlp_fwd_kernel(FWArgs g) {
             constexpr int SET = NS == 2 ? Q : 0;
             if (u + 1 < nun) stage(u + 1, Q, RR[SET]);
             fetch(u + 1 + NS, RR[SET]);
-            __syncthreads();
+            if (ANERF_FW_PROBE != 10) __syncthreads();
         };
         for (int u = 0; u < nun; u += 2) {
             body(u, std::integral_constant<int, 0>{});
@@ -1628,7 +1637,7 @@ __global__ __launch_bounds__(FW_THR, 1) void mlp_fwd_kernel(FWArgs g) {
         __syncthreads();
         for (int u = 0; u < nun; ++u) {
             if (u >= nu && u % nu == 0) copy_out(u / nu - 1);
-            __syncthreads();
+            if (ANERF_FW_PROBE != 10) __syncthreads();
         }
         if (nch > 0) copy_out(nch - 1);
     } else {
@@ -1654,7 +1663,7 @@ __global__ __launch_bounds__(FW_THR, 1) void mlp_fwd_kernel(FWArgs g) {
         // global k16 index q = 8 u + t: the chunk's step q % ku; steps past W's (the last unit's padding, whose
         // A columns are zero) are neither loaded nor multiplied
         auto fetch_w = [&](int q, WF& f) {
-            if ((ANERF_FW_PROBE == 2 || ANERF_FW_PROBE == 6) && q >= FW_BD) return;
+            if ((ANERF_FW_PROBE == 2 || ANERF_FW_PROBE >= 6) && q >= FW_BD) return;
             int kt = q % ku;
             kt = kt < nk ? kt : nk - 1;  // (a straight-line instruction stream: the padding steps reload the last)
 #pragma unroll
@@ -1695,7 +1704,7 @@ __global__ __launch_bounds__(FW_THR, 1) void mlp_fwd_kernel(FWArgs g) {
             for (int t = 0; t < FW_KH / 16; ++t) {
                 __builtin_amdgcn_sched_barrier(0);
                 fetch_w(8 * u + t + FW_BD - 1, wf[(t + FW_BD - 1) % FW_BD]);  // ((8 u + t) % FW_BD = t % FW_BD)
-                if (t + 1 < FW_KH / 16) read_a(t + 1, A[(t + 1) & 1]);
+                if (t + 1 < FW_KH / 16 && (ANERF_FW_PROBE != 8 || u < 2)) read_a(t + 1, A[(t + 1) & 1]);
                 __builtin_amdgcn_sched_barrier(0);
                 if (8 * kh + t >= nk || ANERF_FW_PROBE == 1) continue;
                 const bf16x8 (&a)[NPL][2] = A[t & 1];
@@ -1749,6 +1758,7 @@ __global__ __launch_bounds__(FW_THR, 1) void mlp_fwd_kernel(FWArgs g) {
                     for (int j = 0; j < 2; ++j)
 #pragma unroll
                         for (int r = 0; r < 16; ++r) {
+                            if (ANERF_FW_PROBE == 9) continue;
                             const int row = 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
                             float v = acc[i][j][r];
                             v += j ? b1 : b0;
@@ -1762,7 +1772,7 @@ __global__ __launch_bounds__(FW_THR, 1) void mlp_fwd_kernel(FWArgs g) {
 #endif
                         }
             }
-            __syncthreads();
+            if (ANERF_FW_PROBE != 10) __syncthreads();
         }
     }
 }
