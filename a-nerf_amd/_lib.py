@@ -235,6 +235,9 @@ SIGNATURES = {
                                                  ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32,
                                                  ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,
                                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "anerf_mlp_gemm_persistent": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(Seg),
+                                                 ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+                                                 ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
     "anerf_mlp_forward_layer": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(Seg), ctypes.c_int32,
                                                ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32,
                                                ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,

@@ -1432,8 +1432,9 @@ struct FWArgs {
     long long ld0, ld1;
     int c0, K, nk, nu;        // k16 steps of W (ceil(K / 16)), units per chunk (ceil(K / 128) >= 2)
     const unsigned short* w;  // split W, NPL bf16 planes (anerf_mlp_split_weights, transpose = 0)
-    const float* bias;
+    const float* bias;  // or null
     int relu;
+    int nval;  // output columns of this launch's 256-column tile that exist (% 4 == 0)
     float* y;
     long long ldy;
     const float* wa;  // head: alpha_linear's weight [K] and bias [1], alpha out (column 0 of rows with ld lda), or null
@@ -1621,12 +1622,13 @@ __global__ __launch_bounds__(FW_THR, 1) void mlp_fwd_kernel(FWArgs g) {
         // waited on
         const int t = tid - 128;
         const long long ldy = g.ldy;
+        const int nval = g.nval;
         auto copy_out = [&](int s) __attribute__((always_inline)) {
             if (ANERF_FW_PROBE == 4 || ANERF_FW_PROBE >= 5 || ANERF_FW_DIRECT) return;
             const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
                 (void*)(yp + (mlo + (long long)s * FW_CH) * ldy), 0, (int)(chunk_rows(s) * ldy * 4), 0x00020000);
             const int c4 = 4 * (t & 63), rq = t >> 6;
-            const unsigned vo = (unsigned)((rq * ldy + c4) * 4);
+            const unsigned vo = c4 < nval ? (unsigned)((rq * ldy + c4) * 4) : NOOB;  // (columns past the tile's n)
 #pragma unroll
             for (int q = 0; q < FW_CH / 2; ++q) {
                 const f32x4 v = *reinterpret_cast<const f32x4*>(otile + (2 * q + rq) * FW_W + c4);
@@ -1673,7 +1675,9 @@ __global__ __launch_bounds__(FW_THR, 1) void mlp_fwd_kernel(FWArgs g) {
                     f.v[j][p] = __builtin_bit_cast(
                         u32x4, __builtin_amdgcn_raw_buffer_load_b128(rw, vwl, (j * WBS + (kt * NPL + p) * 512) * 2, 0));
         };
-        const float b0 = g.bias[64 * xw + (lane & 31)], b1 = g.bias[64 * xw + 32 + (lane & 31)];
+        const float* const bp = g.bias;
+        const int n0c = 64 * xw + (lane & 31);
+        const float b0 = bp && n0c < g.nval ? bp[n0c] : 0.0f, b1 = bp && n0c + 32 < g.nval ? bp[n0c + 32] : 0.0f;
         const bool relu = g.relu != 0;
         WF wf[FW_BD];
 #pragma unroll
@@ -2119,36 +2123,42 @@ int anerf_mlp_backward_hidden_reduce(int64_t m, int32_t width, const void* works
                       stream);
 }
 
-int anerf_mlp_forward_layer(int64_t m, int32_t k, const anerf_seg* a, int32_t n_a, const void* w_split,
-                            int32_t precision, const float* bias, int32_t relu, float* y, int64_t ldy,
-                            const float* w_alpha, const float* b_alpha, float* alpha, int64_t ld_alpha, void* stream) {
-    const char* fn = "anerf_mlp_forward_layer";
+}  // extern "C"
+
+namespace {
+// y[m][0, n) = act(sum_k a[m][k] W[o][k] + b[o]) on the persistent kernel, one launch per 256 output columns
+int fw_launch(const char* fn, int64_t m, int32_t n, int32_t k, const anerf_seg* a, int32_t n_a, const void* w_split,
+              int32_t precision, const float* bias, int32_t relu, float* y, int64_t ldy, const float* w_alpha,
+              const float* b_alpha, float* alpha, int64_t ld_alpha, void* stream) {
+    const std::string f(fn);
     const int npl = precision == ANERF_MLP_BF16X6 ? 3 : (precision == ANERF_MLP_BF16X3 ? 2 : 0);
-    if (!npl) return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_forward_layer: ANERF_MLP_BF16X6 or _BF16X3");
-    if (m < 0 || !a || n_a < 1 || n_a > 2 || !w_split || !bias || !y || k <= FW_KH || k % 4)
-        return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_forward_layer: bad arguments (1 or 2 segments, "
-                                                 "128 < k, k % 4 == 0)");
+    if (!npl) return anerf_internal_fail(ANERF_EINVAL, (f + ": ANERF_MLP_BF16X6 or _BF16X3").c_str());
+    if (m < 0 || n < 4 || n % 4 || !a || n_a < 1 || n_a > 2 || !w_split || !y || k <= FW_KH || k % 4)
+        return anerf_internal_fail(ANERF_EINVAL, (f + ": bad arguments (n % 4 == 0, 1 or 2 segments, 128 < k, "
+                                                      "k % 4 == 0)").c_str());
     if (!w_alpha != !alpha || !w_alpha != !b_alpha || (alpha && ld_alpha < 1))
-        return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_forward_layer: w_alpha, b_alpha, alpha all or none");
-    // (float4 loads and stores of whole rows; a 64-row chunk's byte range fits a buffer descriptor; the stagers read
+        return anerf_internal_fail(ANERF_EINVAL, (f + ": w_alpha, b_alpha, alpha all or none").c_str());
+    const bool head = alpha != nullptr;
+    if (head && (n_a != 1 || k != FW_W || n != FW_W))
+        return anerf_internal_fail(ANERF_EINVAL, (f + ": alpha with one segment, k = n = 256 only").c_str());
+    // (float4 loads and stores of whole rows; a 64-row chunk's byte range fits a buffer descriptor; the loaders read
     // units ahead of the stores, so y must not overlap an operand)
     int cols = 0;
     for (int i = 0; i < n_a; ++i) {
         if (!a[i].p || a[i].cols < 4 || a[i].cols % 4 || a[i].ld < a[i].cols || a[i].ld % 4 || a[i].ld >= (1 << 22) ||
             (reinterpret_cast<uintptr_t>(a[i].p) & 15))
-            return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_forward_layer: segments need 16 B aligned rows, "
-                                                     "cols % 4 == 0, cols <= ld < 2^22, ld % 4 == 0");
+            return anerf_internal_fail(ANERF_EINVAL, (f + ": segments need 16 B aligned rows, cols % 4 == 0, cols <= "
+                                                          "ld < 2^22, ld % 4 == 0").c_str());
         cols += a[i].cols;
     }
-    if (cols != k) return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_forward_layer: segments do not add up to k");
-    if ((reinterpret_cast<uintptr_t>(y) & 15) || (ldy & 3) || ldy < FW_W || ldy >= (1 << 22))
-        return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_forward_layer: y needs 16 B aligned rows, ld % 4 == 0, "
-                                                 "256 <= ld < 2^22");
+    if (cols != k) return anerf_internal_fail(ANERF_EINVAL, (f + ": segments do not add up to k").c_str());
+    if ((reinterpret_cast<uintptr_t>(y) & 15) || (ldy & 3) || ldy < n || ldy >= (1 << 22))
+        return anerf_internal_fail(ANERF_EINVAL, (f + ": y needs 16 B aligned rows, ld % 4 == 0, n <= ld < 2^22").c_str());
     if (m == 0) return ANERF_OK;
-    const uintptr_t yb = reinterpret_cast<uintptr_t>(y), ye = yb + 4 * ((m - 1) * ldy + FW_W);
+    const uintptr_t yb = reinterpret_cast<uintptr_t>(y), ye = yb + 4 * ((m - 1) * ldy + n);
     for (int i = 0; i < n_a; ++i) {
         const uintptr_t xb = reinterpret_cast<uintptr_t>(a[i].p), xe = xb + 4 * ((m - 1) * a[i].ld + a[i].cols);
-        if (xb < ye && yb < xe) return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_forward_layer: y overlaps an operand");
+        if (xb < ye && yb < xe) return anerf_internal_fail(ANERF_EINVAL, (f + ": y overlaps an operand").c_str());
     }
     FWArgs g = {};
     const int nwg = fw_plan(m, &g.rows_per_wg);
@@ -2161,37 +2171,55 @@ int anerf_mlp_forward_layer(int64_t m, int32_t k, const anerf_seg* a, int32_t n_
     g.K = k;
     g.nk = (k + 15) / 16;
     g.nu = (k + FW_KH - 1) / FW_KH;
-    g.w = static_cast<const unsigned short*>(w_split);
-    g.bias = bias;
     g.relu = relu != 0;
-    g.y = y;
     g.ldy = ldy;
     g.wa = w_alpha;
     g.ba = b_alpha;
     g.alpha = alpha;
     g.lda = ld_alpha;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    const bool head = alpha != nullptr;
-    if (head && (n_a != 1 || k != FW_W))
-        return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_forward_layer: alpha with one segment of k = 256 only");
     const int lb = npl == 3 ? FWGeo<3>::LDS : FWGeo<2>::LDS;
+    const long long wtile = (long long)(FW_W / 32) * g.nk * npl * 512;  // split-W elements of 256 output rows
     hipError_t e = hipSuccess;
+    for (int n0 = 0; n0 < n; n0 += FW_W) {  // (the split W's rows are zero-padded to whole 256s)
+        g.w = static_cast<const unsigned short*>(w_split) + (n0 / FW_W) * wtile;
+        g.bias = bias ? bias + n0 : nullptr;
+        g.nval = n - n0 < FW_W ? n - n0 : FW_W;
+        g.y = y + n0;
 #define ANERF_FW_LAUNCH(P, S, H)                                                                                   \
-    if (npl == P && n_a == S && head == H) {                                                                       \
-        e = hipFuncSetAttribute((const void*)mlp_fwd_kernel<P, S, H>, hipFuncAttributeMaxDynamicSharedMemorySize, lb); \
-        if (e != hipSuccess)                                                                                       \
-            return anerf_internal_fail(ANERF_EHIP, (std::string(fn) + ": " + hipGetErrorString(e)).c_str());      \
-        hipLaunchKernelGGL((mlp_fwd_kernel<P, S, H>), dim3((unsigned)nwg), dim3(FW_THR), lb, st, g);             \
-    }
-    ANERF_FW_LAUNCH(3, 1, false)
-    ANERF_FW_LAUNCH(3, 2, false)
-    ANERF_FW_LAUNCH(3, 1, true)
-    ANERF_FW_LAUNCH(2, 1, false)
-    ANERF_FW_LAUNCH(2, 2, false)
-    ANERF_FW_LAUNCH(2, 1, true)
+        if (npl == P && n_a == S && head == H) {                                                                   \
+            e = hipFuncSetAttribute((const void*)mlp_fwd_kernel<P, S, H>, hipFuncAttributeMaxDynamicSharedMemorySize, lb); \
+            if (e != hipSuccess) return anerf_internal_fail(ANERF_EHIP, (f + ": " + hipGetErrorString(e)).c_str()); \
+            hipLaunchKernelGGL((mlp_fwd_kernel<P, S, H>), dim3((unsigned)nwg), dim3(FW_THR), lb, st, g);         \
+        }
+        ANERF_FW_LAUNCH(3, 1, false)
+        ANERF_FW_LAUNCH(3, 2, false)
+        ANERF_FW_LAUNCH(3, 1, true)
+        ANERF_FW_LAUNCH(2, 1, false)
+        ANERF_FW_LAUNCH(2, 2, false)
+        ANERF_FW_LAUNCH(2, 1, true)
 #undef ANERF_FW_LAUNCH
-    e = hipGetLastError();
-    return e == hipSuccess ? ANERF_OK : anerf_internal_fail(ANERF_EHIP, (std::string(fn) + ": " + hipGetErrorString(e)).c_str());
+        e = hipGetLastError();
+        if (e != hipSuccess) return anerf_internal_fail(ANERF_EHIP, (f + ": " + hipGetErrorString(e)).c_str());
+    }
+    return ANERF_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int anerf_mlp_forward_layer(int64_t m, int32_t k, const anerf_seg* a, int32_t n_a, const void* w_split,
+                            int32_t precision, const float* bias, int32_t relu, float* y, int64_t ldy,
+                            const float* w_alpha, const float* b_alpha, float* alpha, int64_t ld_alpha, void* stream) {
+    if (!bias) return anerf_internal_fail(ANERF_EINVAL, "anerf_mlp_forward_layer: bias required");
+    return fw_launch("anerf_mlp_forward_layer", m, FW_W, k, a, n_a, w_split, precision, bias, relu, y, ldy, w_alpha,
+                     b_alpha, alpha, ld_alpha, stream);
+}
+
+int anerf_mlp_gemm_persistent(int64_t m, int32_t n, int32_t k, const anerf_seg* a, int32_t n_a, const void* b_split,
+                              int32_t precision, const float* bias, int32_t relu, float* c, int64_t ldc, void* stream) {
+    return fw_launch("anerf_mlp_gemm_persistent", m, n, k, a, n_a, b_split, precision, bias, relu, c, ldc, nullptr,
+                     nullptr, nullptr, 0, stream);
 }
 
 int anerf_mlp_forward_hidden(int64_t m, int32_t width, const float* x, int64_t ldx, const void* w_split,

@@ -54,11 +54,17 @@ FUSED_SKIP = True
 # (round 6, ABI 18, with FUSED_BACKWARD) the heads' backward (feature_linear + alpha_linear's rank-1 term) as one
 # fused pass, anerf_mlp_backward_head; an A/B switch for tools/train_bench.py
 FUSED_HEAD = True
+# (round 6) the caller's stream waits for the weight-gradient side stream at the end of the whole backward (an
+# autograd engine callback) instead of at the end of the MLP's backward, when no parameter already holds a .grad to
+# accumulate into: layer 0's weight gradient then overlaps the encoder's and the poses' backward; an A/B switch for
+# tools/train_bench.py, never read from the environment
+DEFER_WGRAD_SYNC = True
 # (round 6, ABI 19) the forward of every trunk layer (layer 0 on the encoder features, the hidden layers, the skip
 # layer on [x | h]) and of feature_linear on the persistent kernel anerf_mlp_forward_layer instead of anerf_mlp_gemm:
 # bit-identical outputs (another schedule: stager waves stream the rows from HBM and the outputs back while the compute
 # waves run the MFMAs), alpha_linear beside feature_linear in fp32 (the GEMM computed it as a 257th output in the split
-# arithmetic: equal to fp32 rounding); bf16x6 / bf16x3 only; an A/B switch for tools/train_bench.py, never read from
+# arithmetic: equal to fp32 rounding), and the backward's feature gradient [dY_0 | dY_s] [W_0 ; W_s,x] on the same
+# kernel (anerf_mlp_gemm_persistent); bf16x6 / bf16x3 only; an A/B switch for tools/train_bench.py, never read from
 # the environment
 FORWARD_PERSISTENT = True
 
@@ -149,6 +155,15 @@ def forward_layer(m, k, a, w_split, prec, bias, relu, y, dev, alpha=None):
                                                    None if out is None else ctypes.c_void_p(out.data_ptr()),
                                                    0 if out is None else out.stride(0), _stream(dev)),
                "anerf_mlp_forward_layer")
+
+
+def gemm_persistent(m, n, k, a, b_split, prec, bias, relu, c, dev):
+    """c[:, :n] = act(a B^T (+ b)) on the persistent kernel (anerf_mlp_gemm_persistent): one output segment, no mask,
+    no accumulation; a = 1 or 2 operand segments adding up to k > 128 columns."""
+    sa, na = _segs(a)
+    _lib.check(_lib.load().anerf_mlp_gemm_persistent(m, n, k, sa, na, _lib.ptr(b_split), prec, _lib.ptr(bias),
+                                                     int(relu), _lib.ptr(c), c.stride(0), _stream(dev)),
+               "anerf_mlp_gemm_persistent")
 
 
 def forward_hidden(m, x, w_split, prec, bias, y, dev):
@@ -425,10 +440,19 @@ class _MLP(torch.autograd.Function):
                 gz = gprev
                 continue
             if i == 0 and merge:
+                # (the feature gradient first: it is on the path to the encoder's and the poses' backward, and the
+                # weight gradient's side-stream launch then waits for it instead of taking CUs from it)
+                if need_feat:
+                    if FORWARD_PERSISTENT and prec in (3, 6) and dnet % 4 == 0 and F % 4 == 0:
+                        gemm_persistent(M, dnet, 2 * W, [_seg(gzx, 2 * W)], st[0], prec, None, False, gfeat, dev)
+                    else:
+                        mm(M, dnet, 2 * W, [_seg(gzx, 2 * W)], st[0], None, False, [(gfeat, F, dnet, 0, None, False)],
+                           dev)
+                if side is not None:  # (every side-stream gradient before layer 0's: what the end of the MLP's
+                    ev_pre = torch.cuda.Event()  # backward waits for when layer 0's own is deferred)
+                    ev_pre.record(side)
                 dwx, dbx = wg(2 * W, dnet, gzx, [segx], (feat, gzx))
                 grads[0], grads[1] = dwx[:W], dbx[:W]
-                if need_feat:
-                    mm(M, dnet, 2 * W, [_seg(gzx, 2 * W)], st[0], None, False, [(gfeat, F, dnet, 0, None, False)], dev)
                 break
             if i == 0:
                 a, k = [segx], dnet
@@ -453,8 +477,25 @@ class _MLP(torch.autograd.Function):
                      [(gprev, W, W, 0, H[i - 1], False)], dev)
             gz = gprev
         if side is not None:
-            main.wait_stream(side)
-        if dwx is not None:
+            if dwx is not None:  # (the skip layer's x columns, after its side-stream weight gradient)
+                with torch.cuda.stream(side):
+                    grads[2 * s1][:, :dnet].copy_(dwx[W:])
+                for t in (dwx, grads[2 * s1]):
+                    t.record_stream(side)
+            late = (params[0], params[1], params[2 * s1]) if dwx is not None else ()
+            if DEFER_WGRAD_SYNC and late and all(p.is_leaf and p.grad is None for p in late):
+                # layer 0's weight gradient (and the skip layer's x columns after it) are the last side-stream work:
+                # the caller's stream waits for everything before them now, and for them once the whole backward has
+                # been queued (the encoder's and the poses' backward run on meanwhile).  Their parameters are leaves
+                # without a .grad, so the engine hands the tensors over uncopied and no kernel reads them before that
+                # wait
+                main.wait_event(ev_pre)
+                ev = torch.cuda.Event()
+                ev.record(side)
+                torch.autograd.Variable._execution_engine.queue_callback(lambda: main.wait_event(ev))
+            else:
+                main.wait_stream(side)
+        elif dwx is not None:
             grads[2 * s1][:, :dnet].copy_(dwx[W:])
         return (None, gfeat, gcodes, gG if ctx.needs_input_grad[3] else None, *grads)
 

@@ -50,6 +50,7 @@
  *   anerf_mlp_backward_head    the same for feature_linear with alpha_linear's rank-1 term (round 6, ABI 18)
  *   anerf_mlp_forward_hidden   a 256 x 256 hidden layer's forward, persistent (round 6, ABI 19)
  *   anerf_mlp_forward_layer    the same for any 256-output layer: layer 0, the skip layer, the heads (ABI 19)
+ *   anerf_mlp_gemm_persistent  the same kernel as a product of any width (the feature gradient, ABI 19)
  *   anerf_mlp_forward(_pack)  the whole forward in one kernel (opt-in alternative to the GEMMs)
  */
 #ifndef ANERF_H
@@ -656,6 +657,14 @@ int anerf_mlp_forward_hidden(int64_t m, int32_t width, const float* x, int64_t l
 int anerf_mlp_forward_layer(int64_t m, int32_t k, const anerf_seg* a, int32_t n_a, const void* w_split,
                             int32_t precision, const float* bias, int32_t relu, float* y, int64_t ldy,
                             const float* w_alpha, const float* b_alpha, float* alpha, int64_t ld_alpha, void* stream);
+/* ABI 19: the persistent kernel as a plain product of any width, one launch per 256 output columns:
+ *   c[m][o] = act(sum_i a[m][i] B[o][i] (+ bias[o])), o < n (n % 4 == 0; bias may be NULL),
+ * bit-identical to anerf_mlp_gemm with one output segment {c, ldc, n} (no mask, no accumulation).  b_split:
+ * anerf_mlp_split_weights(B, n, k, ld, transpose, precision) -- e.g. an input gradient dX = dY W with b_split the
+ * transposed split of W, as the training backward's feature gradient [dY_0 | dY_skip] [W_0 ; W_skip,x] (k 512,
+ * n = the encoder columns). */
+int anerf_mlp_gemm_persistent(int64_t m, int32_t n, int32_t k, const anerf_seg* a, int32_t n_a, const void* b_split,
+                              int32_t precision, const float* bias, int32_t relu, float* c, int64_t ldc, void* stream);
 
 #ifdef __cplusplus
 }

@@ -431,6 +431,27 @@ def test_forward_layer_segments_are_bit_identical_to_the_gemm(m, prec, shape):
     assert torch.equal(y[:, :256], ref[:, :256]), float((y[:, :256] - ref[:, :256]).abs().max())
 
 
+@pytest.mark.parametrize("prec", [3, 6])
+@pytest.mark.parametrize("m", [163840, 777, 1])
+@pytest.mark.parametrize("n", [432, 176, 256, 4])
+def test_gemm_persistent_is_bit_identical_to_the_gemm(m, n, prec):
+    """anerf_mlp_gemm_persistent (one launch per 256 output columns) as the training backward's feature gradient:
+    dX = [dY_0 | dY_s] W^T with W [512][n] split transposed, no bias, no relu, written into the first n columns of
+    rows with ld 460 (the rest of each row untouched), every bit as anerf_mlp_gemm's; with a bias and relu too."""
+    torch.manual_seed(m % 89 + n + prec)
+    dy = torch.randn(m, 512, device=DEV)
+    w = torch.randn(512, n, device=DEV) / 16
+    wt = mlp.split_weight(w, True, prec)
+    for bias, relu in ((None, False), (torch.randn(n, device=DEV), True)):
+        y = torch.full((m, 460), float("nan"), device=DEV)
+        mlp.gemm_persistent(m, n, 512, [mlp._seg(dy, 512)], wt, prec, bias, relu, y, torch.device(DEV))
+        ref = torch.full((m, 460), float("nan"), device=DEV)
+        mlp.gemm(m, n, 512, [mlp._seg(dy, 512)], wt, bias, relu, [(ref, 460, n, 0, None, False)], torch.device(DEV),
+                 prec)
+        assert torch.isnan(y[:, n:]).all()
+        assert torch.equal(y[:, :n], ref[:, :n]), float((y[:, :n] - ref[:, :n]).abs().max())
+
+
 @pytest.mark.parametrize("m", [163840, 777, 1])
 def test_forward_layer_head_with_alpha(m):
     """feature_linear (no relu) with alpha_linear beside it: the 256 outputs bit-identical to the GEMM's, alpha (fp32
@@ -477,6 +498,9 @@ def test_forward_layer_rejects_bad_arguments():
     assert call([mlp._seg(x, 256)], 256, prec=4) != 0
     assert call([mlp._seg(x, 256)], 256, bias=None) != 0
     assert call([mlp._seg(x, 256)], 256, alpha=(b, None, y)) != 0    # (alpha: all or none)
+    sa, na = mlp._segs([mlp._seg(x, 256)])
+    assert lib.anerf_mlp_gemm_persistent(64, 254, 256, sa, na, P(ws), 6, None, 0, P(y), 256, mlp._stream(dev)) != 0
+    assert lib.anerf_mlp_gemm_persistent(64, 260, 256, sa, na, P(ws), 6, None, 0, P(y), 256, mlp._stream(dev)) != 0
 
 
 @pytest.mark.parametrize("prec", ["bf16x6", "mixed", "bf16x3"])

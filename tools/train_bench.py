@@ -66,6 +66,9 @@ def parser():
                     help="ablation: the fine pass on the caller's stream (its backward then follows the coarse one's)")
     ap.add_argument("--no-fused-head", action="store_true",
                     help="ablation: the heads' backward as two GEMMs")
+    ap.add_argument("--no-defer-sync", action="store_true",
+                    help="ablation: the caller's stream waits for the weight-gradient side stream at the end of the "
+                         "MLP's backward (not at the end of the whole backward)")
     ap.add_argument("--no-forward-persistent", action="store_true",
                     help="ablation: the hidden layers' forward on anerf_mlp_gemm instead of anerf_mlp_forward_hidden")
     ap.add_argument("--split-single", action="store_true",
@@ -106,6 +109,7 @@ def measure(a, dev=None):
     importlib.import_module("a-nerf_amd.mlp").FUSED_SKIP = not getattr(a, "no_fused_skip", False)
     importlib.import_module("a-nerf_amd.mlp").FUSED_HEAD = not getattr(a, "no_fused_head", False)
     importlib.import_module("a-nerf_amd.mlp").FORWARD_PERSISTENT = not getattr(a, "no_forward_persistent", False)
+    importlib.import_module("a-nerf_amd.mlp").DEFER_WGRAD_SYNC = not getattr(a, "no_defer_sync", False)
     train.FINE_STREAM = not getattr(a, "no_fine_stream", False)
     tr = train.TrainRayCaster(cfg, ck, device=dev, mlp=a.mlp).train()
     tr.view_windows = not getattr(a, "full_view", False)
