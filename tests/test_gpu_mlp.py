@@ -533,6 +533,30 @@ def test_network_forward_with_the_persistent_layers(prec, monkeypatch):
         assert float((a - b).abs().max()) <= 10 * tol * float(b.abs().max()) + 1e-9
 
 
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_deferred_side_stream_sync_gives_the_same_gradients(accumulate, monkeypatch):
+    """mlp.DEFER_WGRAD_SYNC: layer 0's side-stream weight gradient is waited for at the end of the whole backward
+    (an engine callback) instead of inside the MLP's.  The gradients read right after backward() -- including a
+    second backward accumulating into existing .grad tensors, where the MLP waits at once -- are bit-identical to
+    the immediate wait's, and so are the feature gradient and the encoder rows behind it."""
+    cfg = anerf.RenderConfig(n_joints=24, netdepth=8, netwidth=256).validate()
+    ck = syn.make_checkpoint(5, n_joints=24, D=8, W=256, fine=False)
+    torch.manual_seed(4)
+    feat = torch.rand(30000, cfg.feature_dim, device=DEV) * 2 - 1
+    out = {}
+    for defer in (True, False):
+        monkeypatch.setattr(mlp, "DEFER_WGRAD_SYNC", defer)
+        tr = train.TrainRayCaster(cfg, ck, mlp="mixed").train()
+        f = feat.clone().requires_grad_(True)
+        (tr.network_fn(f, None).square().sum() * 1e3).backward()
+        if accumulate:
+            (tr.network_fn(f, None).sum()).backward()
+        out[defer] = [f.grad.clone()] + [p.grad.clone() for p in tr.parameters() if p.grad is not None]
+    assert len(out[True]) == len(out[False]) > 10
+    for a, b in zip(out[True], out[False]):
+        assert torch.equal(a, b)
+
+
 def _backward_hidden(m, dy, x, w, lddx=None):
     """anerf_mlp_backward_hidden on dy [m][256] and x [m][256] (strided views allowed) with W [256][256]."""
     lib = mlp._lib.load()
