@@ -443,7 +443,8 @@ class _MLP(torch.autograd.Function):
                 # (the feature gradient first: it is on the path to the encoder's and the poses' backward, and the
                 # weight gradient's side-stream launch then waits for it instead of taking CUs from it)
                 if need_feat:
-                    if FORWARD_PERSISTENT and prec in (3, 6) and dnet % 4 == 0 and F % 4 == 0:
+                    # (one launch per 256 output columns, each reading all of [dY_0 | dY_s]: kept to <= 2 launches)
+                    if FORWARD_PERSISTENT and prec in (3, 6) and dnet % 4 == 0 and F % 4 == 0 and dnet <= 2 * W:
                         gemm_persistent(M, dnet, 2 * W, [_seg(gzx, 2 * W)], st[0], prec, None, False, gfeat, dev)
                     else:
                         mm(M, dnet, 2 * W, [_seg(gzx, 2 * W)], st[0], None, False, [(gfeat, F, dnet, 0, None, False)],
