@@ -62,8 +62,10 @@ def parser():
                          "(rounds 1-5): a skts + delta leaf per image")
     ap.add_argument("--no-fused-skip", action="store_true",
                     help="ablation: the skip layer's backward as two GEMMs and its x part apart from layer 0's")
-    ap.add_argument("--no-fine-stream", action="store_true",
-                    help="ablation: the fine pass on the caller's stream (its backward then follows the coarse one's)")
+    ap.add_argument("--fine-stream", action="store_true",
+                    help="experiment: the fine pass on a stream of its own (train.FINE_STREAM; off in the product: "
+                         "-1.5 to -2 %, profiles/r06st/ab.txt)")
+    ap.add_argument("--no-fine-stream", action="store_true", help="(the default; kept for older scripts)")
     ap.add_argument("--no-fused-head", action="store_true",
                     help="ablation: the heads' backward as two GEMMs")
     ap.add_argument("--no-defer-sync", action="store_true",
@@ -110,7 +112,7 @@ def measure(a, dev=None):
     importlib.import_module("a-nerf_amd.mlp").FUSED_HEAD = not getattr(a, "no_fused_head", False)
     importlib.import_module("a-nerf_amd.mlp").FORWARD_PERSISTENT = not getattr(a, "no_forward_persistent", False)
     importlib.import_module("a-nerf_amd.mlp").DEFER_WGRAD_SYNC = not getattr(a, "no_defer_sync", False)
-    train.FINE_STREAM = not getattr(a, "no_fine_stream", False)
+    train.FINE_STREAM = bool(getattr(a, "fine_stream", False))  # (the product default: off)
     tr = train.TrainRayCaster(cfg, ck, device=dev, mlp=a.mlp).train()
     tr.view_windows = not getattr(a, "full_view", False)
     adam_kw = {"fused": True} if getattr(a, "adam", "foreach") == "fused" else {"foreach": True}
@@ -217,7 +219,9 @@ def measure(a, dev=None):
                             if importlib.import_module("a-nerf_amd.mlp").FUSED_BACKWARD and a.mlp in ("mixed", "bf16x3",
                                                                                                     "mixed16")
                             else "two GEMMs (anerf_mlp_gemm + anerf_mlp_wgrad)"),
-        "hidden_forward": ("persistent (anerf_mlp_forward_hidden)" if importlib.import_module("a-nerf_amd.mlp")
+        "hidden_forward": (("persistent (anerf_mlp_forward_layer: every trunk layer and feature_linear + alpha; the feature gradient "
+                            "on anerf_mlp_gemm_persistent; layer 0's weight-gradient wait deferred to the end of the "
+                            "backward)") if importlib.import_module("a-nerf_amd.mlp")
                            .FORWARD_PERSISTENT and a.mlp in ("mixed", "bf16x6", "bf16x3") else "anerf_mlp_gemm"),
         "fine_stream": bool(train.FINE_STREAM),
         "joints": nj,
